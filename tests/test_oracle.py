@@ -1,0 +1,203 @@
+"""Pins the CPU restatement (oracle/) against the reference's own fixtures.
+
+Reference test strategy: test/index.html (ten browser cases) + test/perf.html
+(size table). The reference cannot be executed here, so these
+known answers are the pin for every later GPU parity test.
+"""
+import random
+import struct
+import zlib
+
+import pytest
+
+import oracle as O
+from conftest import golden
+
+# test/perf.html:63-69 (L1-L6, L9 published; L7/L8 observed pre-denial)
+SIZES = {1: 226188, 2: 216830, 3: 207545, 4: 203828, 5: 197239, 6: 193730, 7: 193295,
+         8: 193162, 9: 193162}
+
+
+def s32(x):
+    return struct.unpack("<i", struct.pack("<I", x & 0xFFFFFFFF))[0]
+
+
+def test_deflate_l6_is_reference_fixture(paradise):
+    assert O.deflate(paradise, level=6) == golden("paradiselost.deflate")
+
+
+@pytest.mark.parametrize("level", range(1, 10))
+def test_deflate_size_table(paradise, level):
+    out = O.deflate(paradise, level=level)
+    assert len(out) == SIZES[level]
+    assert zlib.decompress(out) == paradise
+
+
+@pytest.mark.parametrize("name", ["simple", "paradiselost"])
+def test_inflate_text(name):                      # index.html:55-74
+    r = O.inflate(golden(name + ".deflate"))
+    assert r["error"] == 0 and r["success"] and r["checksum"] == "match"
+    assert r["data"] == golden(name + ".txt")
+
+
+@pytest.mark.parametrize("name", ["simple", "paradiselost"])
+def test_inflate_gzip(name):                      # index.html:97-118
+    r = O.inflater_run([golden(name + ".gz")])
+    assert r["success"] and r["checksum"] == "match" and r["fileSize"] == "match"
+    assert r["fileName"] == name + ".txt"
+    assert r["data"] == golden(name + ".txt")
+
+
+def test_inflate_raw_autodetect():                 # index.html:76-95
+    r = O.inflate(golden("simple.raw"))
+    assert r["error"] == 0 and r["checksum"] == "unchecked"
+    assert r["data"] == golden("simple.txt")
+
+
+def test_inflate_parts(paradise):                  # index.html:29-53
+    r = O.inflater_run([golden("paradiselost.part1.deflate"), golden("paradiselost.part2.deflate")])
+    assert r["success"] and r["data"] == paradise
+
+
+def test_inflate_binary():                         # index.html:120-137
+    r = O.inflate(golden("vertices.deflate"))
+    assert r["success"] and r["checksum"] == "match" and len(r["data"]) == 43440
+
+
+@pytest.mark.parametrize("name", ["simple", "paradiselost"])
+def test_roundtrip_gzip_filename(name):            # index.html:141-171
+    src = golden(name + ".txt")
+    comp = O.deflate(src, level=6, format="gzip", file_name=name + ".orig", mtime=1234567)
+    assert comp[:4] == b"\x1f\x8b\x08\x08" and comp[8:10] == b"\x00\xff"   # sd-deflate.ts:133-143
+    assert struct.unpack("<I", comp[4:8])[0] == 1234567
+    r = O.inflater_run([comp])
+    assert r["success"] and r["data"] == src and r["fileName"] == name + ".orig"
+    assert zlib.decompress(comp, 31) == src
+
+
+def test_roundtrip_dictionary(paradise):           # index.html:173-208
+    terms = (b"andthetoofinhiswithorthatallfromnottheirbutiasaheonbyforsothouthisthywhattheythee"
+             b"himbehernowthusheavenwhichwhoshallouratmemymoreisgodthenwhenyetthemthoughwhomwas"
+             b"norwenohadearthuswillwhereiffirstsuchthesehowhavethanmanthroughithighonecanwhile"
+             b"mayfargreattillhathotherintodeatheachherebothwhoseliketherethosedaystoodmightup"
+             b"shethingswerehellsomeeveadamgoodlovelightsoonletyefairstilldownworldosononlyknow"
+             b"nightplaceunderlessforthlongairnewpowermuchoutmustownbeforefindwithout")
+    comp = O.deflate(paradise, format="deflate", dictionary=terms)
+    assert comp[:2] == b"\x78\x20"
+    assert s32(struct.unpack(">I", comp[2:6])[0]) == O.adler32(terms)
+    r = O.inflater_run([comp], dictionary=terms)
+    assert r["success"] and r["data"] == paradise
+    assert O.inflater_run([comp])["message"] == "Custom dictionary required for this data"
+    d = zlib.decompressobj(zdict=terms)
+    assert d.decompress(comp) == paradise
+
+
+def test_checksum_kats(paradise):                  # SURVEY §4 fixture table
+    simple = golden("simple.txt")
+    assert O.adler32(simple) == -1612443532
+    assert O.crc32(simple) == 1488305224
+    assert O.adler32(paradise) == -1949153550
+    assert O.crc32(paradise) == -499006831
+
+
+def test_checksums_vs_zlib():
+    rng = random.Random(7)
+    for n in [0, 1, 15, 16, 17, 5551, 5553, 11105, 70000]:
+        data = bytes(rng.getrandbits(8) for _ in range(n))
+        assert O.crc32(data) == s32(zlib.crc32(data))
+        assert O.adler32(data) == s32(zlib.adler32(data))
+        seed = rng.getrandbits(32)
+        assert O.crc32(data, s32(seed)) == s32(zlib.crc32(data, seed))
+
+
+def test_adler32_nmax_quirk():
+    """adler32.ts:67 adds BASE instead of reducing sum2; with no remainder the
+    final reduction never happens (multiples of NMAX=5552)."""
+    for n in [5552, 11104]:
+        data = bytes([255]) * n
+        got = O.adler32(data) & 0xFFFFFFFF
+        s1, s2 = 1, 0
+        for i in range(0, n, 5552):
+            for b in data[i:i + 5552]:
+                s1 += b
+                s2 += s1
+            s1 %= 65521
+            s2 += 65521
+        assert got == (s1 | ((s2 & 0xFFFF) << 16))
+        assert got != zlib.adler32(data)
+
+
+def test_fixed_tables_spot_check():
+    # inftree.ts:20 first entries of fixed_tl and inftree.ts:60 of fixed_td
+    tl = [96, 7, 256, 0, 8, 80, 0, 8, 16, 84, 8, 115, 82, 7, 31, 0, 8, 112, 0, 8, 48, 0, 9, 192]
+    td = [80, 5, 1, 87, 5, 257, 83, 5, 17, 91, 5, 4097, 81, 5, 5, 89, 5, 1025]
+    L = O.lib()
+    assert [L.oracle_fixed_table_entry(0, i) for i in range(len(tl))] == tl
+    assert [L.oracle_fixed_table_entry(1, i) for i in range(len(td))] == td
+    # deftree.ts:319 / 336 static trees, 25 dist code, 269 length code, 277/279 bases
+    assert [L.oracle_tree_table(0, i) for i in range(6)] == [12, 8, 140, 8, 76, 8]
+    assert [L.oracle_tree_table(0, 280 * 2 + i) for i in range(2)] == [3, 8]
+    assert [L.oracle_tree_table(1, i) for i in range(6)] == [0, 5, 16, 5, 8, 5]
+    assert [L.oracle_tree_table(2, i) for i in range(12)] == [0, 1, 2, 3, 4, 4, 5, 5, 6, 6, 6, 6]
+    assert [L.oracle_tree_table(2, 256 + i) for i in range(6)] == [0, 0, 16, 17, 18, 18]
+    assert [L.oracle_tree_table(3, i) for i in (0, 8, 9, 255)] == [0, 8, 8, 28]
+    assert [L.oracle_tree_table(4, i) for i in (27, 28)] == [224, 0]
+    assert [L.oracle_tree_table(5, i) for i in (29,)] == [24576]
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_inflate_vs_system_zlib(seed):
+    """Independent implementation cross-check on valid streams (zlib 1.2.11)."""
+    rng = random.Random(seed)
+    words = [bytes(rng.choice(b"abcdefghij ") for _ in range(rng.randint(1, 9))) for _ in range(300)]
+    data = b" ".join(rng.choice(words) for _ in range(rng.randint(1000, 40000)))
+    level = rng.randint(1, 9)   # level 0 = stored blocks: see test_stored_block_defect_a9
+    for wbits in (15, -15, 31):
+        c = zlib.compressobj(level, zlib.DEFLATED, wbits, rng.randint(1, 9), rng.choice([0, 1, 2, 3]))
+        comp = c.compress(data) + c.flush()
+        r = O.inflater_run([comp], raw=(wbits < 0))
+        assert r["data"] == data
+        if wbits > 0:
+            assert r["success"]
+
+
+def test_deflate_empty_throws():
+    with pytest.raises(RuntimeError, match="Cannot call finish"):
+        O.deflate(b"")
+
+
+def test_inflate_errors():
+    assert O.inflate(b"x")["message"] == "data buffer is too small"
+    bad = bytearray(golden("simple.deflate"))
+    bad[-1] ^= 1
+    assert O.inflate(bytes(bad))["message"] == "Data integrity check failed"
+    trunc = golden("paradiselost.deflate")[:5000]
+    assert O.inflate(trunc)["message"] == "Unexpected EOF during decompression"
+    # invalid block type 3 as a raw stream
+    r = O.inflate(b"\x07\x00\x00")
+    assert r["message"] == "inflate error: invalid block type"
+
+
+def test_multi_append_deflate_matches_single(paradise):
+    # chunked appends do not change output when the chunks keep the window full
+    one = O.deflate(paradise)
+    two = O.deflater_run([paradise[:200000], paradise[200000:]])
+    assert zlib.decompress(two) == paradise
+    assert len(two) == len(one) or abs(len(two) - len(one)) < 64
+
+
+def test_stored_block_defect_a9():
+    """SURVEY A9 (infblocks.ts:134,303-311): `left` is a proc-local, so a stored
+    block interrupted by a full 16 KiB output chunk loses its remaining length.
+    The faithful restatement reproduces the reference's failure; the GPU path
+    decodes such streams correctly (documented divergence)."""
+    data = bytes(random.Random(1).getrandbits(8) for _ in range(70000))
+    c = zlib.compressobj(0, zlib.DEFLATED, 15)
+    comp = c.compress(data) + c.flush()
+    r = O.inflater_run([comp])
+    assert not r["success"] and len(r["data"]) < len(data)
+    small = data[:9000]
+    c = zlib.compressobj(0, zlib.DEFLATED, 15)
+    comp = c.compress(small) + c.flush()
+    r = O.inflater_run([comp])
+    assert r["success"] and r["data"] == small
