@@ -1,0 +1,286 @@
+#!/usr/bin/env python3
+"""Headline benchmark: batched inflate on MI355X (BASELINE.json configs[1], "C2").
+
+A step = one pass of the hot path over one batch: 65,536 device-resident copies
+of the reference fixture paradiselost.deflate (193,730 B -> 471,162 B each) are
+inflated by the HIP kernel into their own output slots, checksums fused.  With
+--gpus N (torchrun, one rank per GPU, RCCL) every rank inflates its own 64 Ki
+streams (weak scaling, no data-path collective); per-stream result records are
+all-gathered over RCCL after the timed region (reported as gather_ms).
+
+Also reported: the kernel's HBM roofline fraction (HIP events on the launch
+stream), the CPU baseline (oracle restatement on host cores; the reference's
+own Node path cannot be run) and a deflate leg (configs[2]).
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+import threading
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "sd-zlib_amd", "python"))
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+
+METRIC = ("uncompressed MB/s (inflate) + compressed MB/s (deflate) per node, 1/2/4/8 GPUs; "
+          "% HBM roofline")
+HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def round_up(x, a):
+    return (x + a - 1) // a * a
+
+
+class DeviceBatch:
+    """n device-resident streams replicated from one payload (no aliasing)."""
+
+    def __init__(self, sdz, payload, n, out_cap, in_align=256):
+        L = sdz.lib()
+        self.sdz, self.n = sdz, n
+        self.in_stride = round_up(len(payload), in_align)
+        self.out_stride = round_up(out_cap, 256)
+        self.d_in = sdz.DeviceBuffer(self.in_stride * n + 128)
+        self.d_out = sdz.DeviceBuffer(self.out_stride * n + 64)
+        self.d_in.upload(payload, 0)
+        have = 1
+        while have < n:                                   # doubling device-side replication
+            k = min(have, n - have)
+            rc = L.sdz_copy_device_to_device(self.d_in.ptr + have * self.in_stride, self.d_in.ptr,
+                                             k * self.in_stride)
+            assert rc == 0, L.sdz_last_error()
+            have += k
+        meta = []
+        meta += [i * self.in_stride for i in range(n)]
+        meta += [len(payload)] * n
+        meta += [i * self.out_stride for i in range(n)]
+        meta += [out_cap] * n
+        arr = (ctypes.c_uint64 * len(meta))(*meta)
+        self.d_meta = sdz.DeviceBuffer(8 * len(meta))
+        self.d_meta.upload(bytes(arr))
+        self.rec_size = ctypes.sizeof(sdz.InflateRecord)
+        self.d_rec = sdz.DeviceBuffer(max(self.rec_size, ctypes.sizeof(sdz.DeflateRecord)) * n)
+
+    def ptrs(self):
+        m, n = self.d_meta.ptr, self.n
+        return m, m + 8 * n, m + 16 * n, m + 24 * n
+
+    def free(self):
+        for b in (self.d_in, self.d_out, self.d_meta, self.d_rec):
+            b.free()
+
+
+def inflate_step(sdz, b):
+    in_off, in_len, out_off, out_cap = b.ptrs()
+    rc = sdz.lib().sdz_inflate_batch_device(b.d_in.ptr, in_off, in_len, b.d_out.ptr, out_off, out_cap,
+                                            b.d_rec.ptr, b.n, sdz.FMT_AUTO, None, 0, None)
+    if rc:
+        raise RuntimeError(sdz.lib().sdz_last_error().decode())
+    return sdz.lib().sdz_last_kernel_ms()
+
+
+def deflate_step(sdz, b, level, fmt):
+    in_off, in_len, out_off, out_cap = b.ptrs()
+    rc = sdz.lib().sdz_deflate_batch_device(b.d_in.ptr, in_off, in_len, b.d_out.ptr, out_off, out_cap,
+                                            b.d_rec.ptr, b.n, level, fmt, None, 0, 0, None)
+    if rc:
+        raise RuntimeError(sdz.lib().sdz_last_error().decode())
+    return sdz.lib().sdz_last_kernel_ms()
+
+
+def cpu_baseline_inflate(comp, seconds, threads):
+    """Oracle (CPU restatement of the reference) inflating the same stream on host cores."""
+    import oracle as O
+    L = O.lib()
+    out_cap = 600000
+    counts = [0] * threads
+    stop = time.perf_counter() + seconds
+
+    def work(t):
+        buf = ctypes.create_string_buffer(out_cap)
+        res = O.InflateResult()
+        while time.perf_counter() < stop:
+            L.oracle_inflate(comp, len(comp), None, 0, buf, out_cap, ctypes.byref(res))
+            assert res.success
+            counts[t] += 1
+
+    t0 = time.perf_counter()
+    ths = [threading.Thread(target=work, args=(i,)) for i in range(threads)]
+    for th in ths:
+        th.start()
+    for th in ths:
+        th.join()
+    dt = time.perf_counter() - t0
+    return sum(counts), dt
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--streams", type=int, default=65536, help="streams per GPU (C2: 65536)")
+    ap.add_argument("--cpu-seconds", type=float, default=1.5)
+    ap.add_argument("--deflate-streams", type=int, default=4096,
+                    help="streams for the deflate leg (64 KiB slices, L6); 0 disables")
+    ap.add_argument("--deflate-steps", type=int, default=1)
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    import sdz
+    L = sdz.lib()
+    if sdz.device_count() < 1:
+        raise SystemExit("bench.py: no GPU visible")
+    torch.cuda.set_device(local)
+    assert L.sdz_set_device(local) == 0
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    def allmax(x):
+        if world == 1:
+            return x
+        t = torch.tensor([x], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    golden = os.path.join(ROOT, "tests", "golden")
+    comp = open(os.path.join(golden, "paradiselost.deflate"), "rb").read()
+    text = open(os.path.join(golden, "paradiselost.txt"), "rb").read()
+    n = args.streams
+    b = DeviceBatch(sdz, comp, n, len(text))
+    L.sdz_set_timing(1)
+    for _ in range(args.warmup):
+        inflate_step(sdz, b)
+    L.sdz_sync(None)
+    barrier()
+    L.sdz_sync(None)
+    kms = []
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        kms.append(inflate_step(sdz, b))
+    L.sdz_sync(None)
+    barrier()
+    t1 = time.perf_counter()
+    wall = allmax(t1 - t0)
+    ms_per_step = 1000.0 * wall / args.steps
+    kernel_ms = sum(kms) / len(kms)
+
+    # ---- parity of the timed outputs (records + sampled payloads)
+    recs = (sdz.InflateRecord * n).from_buffer_copy(b.d_rec.download(n * b.rec_size))
+    ok = all(r.status == 0 and r.success and r.out_len == len(text) and r.checksum_verdict == 1 for r in recs)
+    for i in sorted({0, n // 3, n - 1}):
+        ok = ok and b.d_out.download(len(text), i * b.out_stride) == text
+    # ---- RCCL gather of per-stream result records (outside the timed region)
+    gather_ms = None
+    if world > 1:
+        rt = torch.frombuffer(bytearray(bytes(recs)), dtype=torch.uint8).cuda()
+        outs = [torch.empty_like(rt) for _ in range(world)]
+        torch.cuda.synchronize()
+        g0 = time.perf_counter()
+        dist.all_gather(outs, rt)
+        torch.cuda.synchronize()
+        gather_ms = 1000.0 * (time.perf_counter() - g0)
+        if rank == 0:
+            allrec = [(sdz.InflateRecord * n).from_buffer_copy(o.cpu().numpy().tobytes()) for o in outs]
+            ok = ok and all(r.status == 0 and r.success for rr in allrec for r in rr)
+    okall = allmax(0.0 if ok else 1.0) == 0.0
+    bytes_in, bytes_out = len(comp) * n, len(text) * n
+    b.free()
+
+    # ---- deflate leg (configs[2]: 64 KiB text slices, level 6, "deflate" container)
+    deflate = None
+    if args.deflate_streams > 0:
+        import random
+        rng = random.Random(0x5D5A1B1E)
+        nd = args.deflate_streams
+        slice_len = 65536
+        offs = [(i * 65521) % (len(text) - slice_len) for i in range(64)]
+        payloads = [text[o:o + slice_len] for o in offs]
+        bd = DeviceBatch(sdz, payloads[0], nd, int(L.sdz_deflate_bound(slice_len, 1, 0)))
+        for i, pl in enumerate(payloads[1:], 1):           # 64 distinct slices, cycled
+            for j in range(i, nd, 64):
+                bd.d_in.upload(pl, j * bd.in_stride)
+        deflate_step(sdz, bd, 6, 1)
+        L.sdz_sync(None)
+        barrier()
+        d0 = time.perf_counter()
+        dk = [deflate_step(sdz, bd, 6, 1) for _ in range(args.deflate_steps)]
+        L.sdz_sync(None)
+        barrier()
+        dwall = allmax(time.perf_counter() - d0) / args.deflate_steps
+        drec = (sdz.DeflateRecord * nd).from_buffer_copy(bd.d_rec.download(nd * ctypes.sizeof(sdz.DeflateRecord)))
+        comp_total = sum(r.out_len for r in drec)
+        dok = all(r.status == 0 for r in drec)
+        if rank == 0:
+            import oracle as O
+            for j in (0, 1, nd - 1):
+                got = bd.d_out.download(drec[j].out_len, j * bd.out_stride)
+                dok = dok and got == O.deflate(payloads[j % 64], level=6)
+        bd.free()
+        deflate = {
+            "value": round(world * comp_total / dwall / 1e6, 2), "unit": "compressed MB/s",
+            "input_MBps": round(world * nd * slice_len / dwall / 1e6, 2),
+            "kernel_ms": round(sum(dk) / len(dk), 3), "ms_per_step": round(1000 * dwall, 3),
+            "config": {"workload": "C3 deflate level=6 format=deflate", "streams_per_gpu": nd,
+                       "slice_bytes": slice_len, "data": "paradiselost.txt slices (enwik8 absent offline)"},
+            "parity": bool(dok),
+        }
+
+    cpu = None
+    if rank == 0 and world == 1 and args.cpu_seconds > 0:
+        threads = max(1, min(16, os.cpu_count() or 1))
+        cnt, dt = cpu_baseline_inflate(comp, args.cpu_seconds, threads)
+        cpu = {"value": round(cnt * len(text) / dt / 1e6, 2), "unit": "MB/s", "cores": threads,
+               "kind": "port",
+               "sample": "%d x paradiselost.deflate inflated by the oracle C restatement on %d threads "
+                         "in %.1f s" % (cnt, threads, dt)}
+
+    traffic = None
+    pmc = os.path.join(ROOT, "profiles", "r01_inflate_pmc.json")
+    if os.path.exists(pmc) and n == 65536:
+        try:
+            traffic = json.load(open(pmc)).get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+    achieved = (bytes_in + bytes_out) / (kernel_ms / 1000.0) / 1e9
+    line = {
+        "metric": METRIC,
+        "value": round(world * bytes_out / (wall / args.steps) / 1e6, 2),
+        "unit": "MB/s",
+        "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 3),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+        "data": "synthetic: 65536 device copies/GPU of reference fixture paradiselost.deflate",
+        "config": {"workload": "C2 batched inflate: paradiselost.deflate x %d per GPU (zlib, dynamic Huffman)" % n,
+                   "streams_per_gpu": n, "bytes_in_per_gpu": bytes_in, "bytes_out_per_gpu": bytes_out,
+                   "parallelism": "dp%d (independent streams, no data-path collective)" % world},
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
+                     "kernel_ms": round(kernel_ms, 3),
+                     "algorithmic_bytes_per_launch": bytes_in + bytes_out},
+        "cpu_baseline": cpu,
+        "parity": bool(okall),
+        "gather_ms": None if gather_ms is None else round(gather_ms, 3),
+        "deflate": deflate,
+    }
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,180 @@
+/*
+ * sdz.h -- C ABI of libsdz.so, the MI355X-native batched DEFLATE engine that
+ * replaces the inflate/deflate hot path of @stardazed/zlib 1.0.1.
+ *
+ * The reference has no FFI: its boundary is the ES-module API
+ * (src/sd-zlib.ts:39-43, typed in dist/sd-zlib.d.ts:11-149) over the engine seams
+ * Inflate.inflate(z) (src/inflate.ts:132) and Deflate.deflate(flush)
+ * (src/deflate.ts:1218).  Each entry point below names the reference interface it
+ * replaces.  The N-API addon (sd-zlib_amd/js/sdz_napi.cpp) and the pytest ctypes
+ * binding (sd-zlib_amd/python/sdz.py) are its two callers; see INTEGRATION.md.
+ *
+ * Conventions
+ *  - plain pointers and sizes; no C++ exceptions cross this boundary;
+ *  - functions return SDZ_API_OK (0) or a negative SDZ_API_* code, with the
+ *    message in sdz_last_error();
+ *  - per-stream outcomes are reported in records, never as API errors;
+ *  - *_device entry points take device pointers and a hipStream_t (as void*),
+ *    are asynchronous, and are the timed hot path;
+ *  - the host entry points copy in, run the same kernels, and copy out.
+ *  - there is no CPU implementation of any codec in this library: every path
+ *    runs on the GPU and fails (SDZ_API_NO_DEVICE) when none is present.
+ */
+#ifndef SDZ_H
+#define SDZ_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SDZ_ABI_VERSION 1
+
+/* API return codes */
+enum {
+    SDZ_API_OK = 0,
+    SDZ_API_BAD_ARG = -1,
+    SDZ_API_NO_DEVICE = -2,
+    SDZ_API_HIP_ERROR = -3,
+    SDZ_API_OOM = -4,
+};
+
+/* Container handling for inflate.
+ *  AUTO:      inflate() detection rule, sd-inflate.ts:203-207
+ *             (78 + FCHECK -> zlib, 1F 8B -> gzip, else raw);
+ *  RAW:       Inflater({raw: true})  -> Inflate(blocksOnly) inflate.ts:100;
+ *  CONTAINER: Inflater({raw: false}) -> DETECT mode, inflate.ts:142-175.      */
+enum { SDZ_FMT_AUTO = 0, SDZ_FMT_RAW = 1, SDZ_FMT_CONTAINER = 2 };
+
+/* Deflate container, sd-deflate.ts:17-30 ("raw" | "deflate" | "gzip") */
+enum { SDZ_DEFLATE_RAW = 0, SDZ_DEFLATE_ZLIB = 1, SDZ_DEFLATE_GZIP = 2 };
+
+/* Per-stream inflate status (maps 1:1 onto the reference's outcomes) */
+enum {
+    SDZ_OK = 0,            /* decoded; see verdict fields (finish(), sd-inflate.ts:159-179) */
+    SDZ_DATA_ERROR = 1,    /* "inflate error: " + sdz_zmsg(zmsg)        sd-inflate.ts:128 */
+    SDZ_NEED_DICT = 2,     /* "Custom dictionary required for this data" sd-inflate.ts:124 */
+    SDZ_DICT_MISMATCH = 3, /* "Custom dictionary is not valid for this data" :120 */
+    SDZ_TRUNCATED = 4,     /* incomplete: "Unexpected EOF during decompression" :216 */
+    SDZ_OUT_OVERFLOW = 5,  /* out_cap too small: retry with a larger capacity */
+    SDZ_TRAILING = 6,      /* bytes after the end of the stream: the reference's append()
+                              loops forever here; reported instead */
+    SDZ_TOO_SMALL = 7,     /* AUTO and < 2 bytes: "data buffer is too small" :195 */
+    SDZ_BAD_RECORD = 8,    /* misaligned output offset (must be a multiple of 8) */
+};
+
+/* Checksum / size verdicts ("unchecked" | "match" | "mismatch") */
+enum { SDZ_UNCHECKED = 0, SDZ_MATCH = 1, SDZ_MISMATCH = 2 };
+/* container actually seen (Inflate.containerFormat, inflate.ts:128-130) */
+enum { SDZ_CONTAINER_RAW = 0, SDZ_CONTAINER_ZLIB = 1, SDZ_CONTAINER_GZIP = 2 };
+
+/* One record per stream, written by the device (64 bytes). */
+typedef struct sdz_inflate_record {
+    int32_t  status;            /* SDZ_OK ... */
+    int32_t  zmsg;              /* reason, sdz_zmsg(); 0 = none */
+    uint64_t out_len;           /* bytes written to the stream's output slot */
+    uint64_t in_used;           /* input bytes consumed */
+    int32_t  stored_checksum;   /* Inflate.checksum (signed, 0 = absent) */
+    int32_t  running_checksum;  /* Inflater.checksum over the output, reference quirks included */
+    int32_t  stored_size;       /* gzip ISIZE as the reference reads it (signed int32) */
+    int32_t  mtime;             /* gzip MTIME (signed int32); 0 => modDate undefined */
+    uint32_t name_off;          /* gzip FNAME: byte offset within the input stream */
+    uint32_t name_len;          /*            and length (Latin-1, no terminator) */
+    uint8_t  container;         /* SDZ_CONTAINER_* */
+    uint8_t  complete;          /* Inflate.isComplete, inflate.ts:103-107 */
+    uint8_t  checksum_verdict;  /* SDZ_UNCHECKED / SDZ_MATCH / SDZ_MISMATCH */
+    uint8_t  size_verdict;
+    uint8_t  success;           /* complete && no mismatch */
+    uint8_t  reserved[11];
+} sdz_inflate_record;
+
+typedef struct sdz_deflate_record {
+    int32_t  status;            /* 0 ok; SDZ_OUT_OVERFLOW; SDZ_DATA_ERROR (pending_buf overflow
+                                   in the reference's overlay, undefined output there) */
+    int32_t  checksum;          /* adler32 / crc32 of the input as written in the trailer */
+    uint64_t out_len;
+    uint64_t reserved;
+} sdz_deflate_record;
+
+/* ---------------------------------------------------------------- inflate */
+
+/* Replaces Inflater.append(whole stream) + finish() / inflate()
+ * (sd-inflate.ts:87-179, 189-228; engine inflate.ts:132 + infblocks/infcodes/inftree).
+ * Device pointers.  Stream i reads in[in_off[i] .. +in_len[i]) and writes
+ * out[out_off[i] .. +out_cap[i]).  out_off must be a multiple of 8; the input
+ * allocation must have >= 64 readable bytes after the last stream (reads are
+ * 16-byte vectors).  dict (may be NULL) is the preset dictionary offered to
+ * every stream that sets FDICT.  stream = hipStream_t (NULL = default). */
+int sdz_inflate_batch_device(const uint8_t* in, const uint64_t* in_off, const uint64_t* in_len,
+                             uint8_t* out, const uint64_t* out_off, const uint64_t* out_cap,
+                             sdz_inflate_record* rec, uint32_t n, int32_t format,
+                             const uint8_t* dict, uint32_t dict_len, void* stream);
+
+/* Host convenience wrapper around sdz_inflate_batch_device (copies both ways). */
+int sdz_inflate_batch(const uint8_t* const* in, const size_t* in_len, uint8_t* const* out,
+                      const size_t* out_cap, sdz_inflate_record* rec, uint32_t n,
+                      int32_t format, const uint8_t* dict, size_t dict_len);
+
+/* ---------------------------------------------------------------- deflate */
+
+/* Replaces Deflater(opts).append(whole input) + finish() / deflate()
+ * (sd-deflate.ts:51-274; engine deflate.ts:196-1327 + deftree.ts).  Output is
+ * bit-exact with the reference for the same input, level, format, file name and
+ * MTIME (the reference stamps Math.floor(Date.now()/1000), sd-deflate.ts:140;
+ * the caller passes it here).  fname: Latin-1 bytes already mapped as
+ * sd-deflate.ts:125-130 does (NULL/0 = no FNAME).  Device pointers. */
+int sdz_deflate_batch_device(const uint8_t* in, const uint64_t* in_off, const uint64_t* in_len,
+                             uint8_t* out, const uint64_t* out_off, const uint64_t* out_cap,
+                             sdz_deflate_record* rec, uint32_t n, int32_t level, int32_t format,
+                             const uint8_t* fname, uint32_t fname_len, uint32_t mtime,
+                             void* stream);
+
+int sdz_deflate_batch(const uint8_t* const* in, const size_t* in_len, uint8_t* const* out,
+                      const size_t* out_cap, sdz_deflate_record* rec, uint32_t n, int32_t level,
+                      int32_t format, const uint8_t* fname, size_t fname_len, uint32_t mtime);
+
+/* Worst-case compressed size for one stream (header + blocks + trailer). */
+uint64_t sdz_deflate_bound(uint64_t in_len, int32_t format, uint32_t fname_len);
+
+/* -------------------------------------------------------------- checksums */
+
+/* adler32(src, seed = 1) / crc32(src, seed = 0): adler32.ts:17-24 (including the
+ * adler32.ts:67 NMAX quirk) and crc32.ts:17-23.  Signed int32 results.  Run on
+ * the GPU (host buffer copied in). */
+int32_t sdz_adler32(const uint8_t* buf, size_t len, int32_t seed);
+int32_t sdz_crc32(const uint8_t* buf, size_t len, int32_t seed);
+
+/* Batched device versions: result[i] = checksum(in[in_off[i] .. +in_len[i]), seed[i]) */
+int sdz_adler32_batch_device(const uint8_t* in, const uint64_t* in_off, const uint64_t* in_len,
+                             const int32_t* seed, int32_t* result, uint32_t n, void* stream);
+int sdz_crc32_batch_device(const uint8_t* in, const uint64_t* in_off, const uint64_t* in_len,
+                           const int32_t* seed, int32_t* result, uint32_t n, void* stream);
+
+/* ----------------------------------------------------------------- misc */
+
+const char* sdz_zmsg(int32_t code);       /* z.msg text for a record's zmsg */
+const char* sdz_last_error(void);
+int sdz_version(void);                    /* SDZ_ABI_VERSION */
+int sdz_device_count(void);
+int sdz_set_device(int device);
+
+/* Device memory plumbing for callers without their own HIP runtime (node, ctypes). */
+void* sdz_device_alloc(uint64_t bytes);
+void sdz_device_free(void* ptr);
+int sdz_copy_to_device(void* dst, const void* src, uint64_t bytes);
+int sdz_copy_to_host(void* dst, const void* src, uint64_t bytes);
+int sdz_memset_device(void* dst, int value, uint64_t bytes);
+int sdz_copy_device_to_device(void* dst, const void* src, uint64_t bytes);
+int sdz_sync(void* stream);
+
+/* Kernel timing: when enabled, *_device calls record HIP events on their launch
+ * stream around the codec kernel(s); sdz_last_kernel_ms() waits for the stop
+ * event of the most recent call on this thread and returns the elapsed ms. */
+int sdz_set_timing(int enabled);
+float sdz_last_kernel_ms(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

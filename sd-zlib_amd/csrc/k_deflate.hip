@@ -1,0 +1,753 @@
+// k_deflate.hip -- batched, bit-exact DEFLATE encoder for gfx950 (MI355X).
+//
+// Replaces the serial compressor of @stardazed/zlib:
+//   Deflate (fill_window, longest_match, deflate_fast/slow, _tr_tally,
+//            _tr_flush_block, compress_block, send_bits)   src/deflate.ts:102-1327
+//   Tree (build_tree, gen_bitlen, gen_codes)                src/deftree.ts:40-267
+//   config_table                                            src/defconfig.ts:33-44
+//   Deflater container header/trailer                       src/sd-deflate.ts:98-253
+//
+// v1 design: one lane per stream, the reference's exact state machine, with the
+// per-stream state (64 KiB window, 32 K-entry head/prev chains, the 64 KiB
+// pending_buf with its d_buf@8192 / l_buf@49152 overlay, trees) in an HBM
+// scratch slab, scalars in registers.  Bit-exactness needs the reference's
+// quirks verbatim: TRUNCATE_BLOCK, 4-byte clz compare from +2,
+// stale window bytes past the input, the pending_buf overlay, (freq, depth)
+// heap ties.  The output is produced with the reference's block decisions and
+// flushed straight into the stream's output slot.
+#include "sdz_internal.h"
+
+namespace sdz {
+
+#define DF_THREADS 64
+#define W_SIZE 32768
+#define W_MASK (W_SIZE - 1)
+#define WINDOW_SIZE (2 * W_SIZE)
+#define HASH_SIZE 32768
+#define HASH_MASK (HASH_SIZE - 1)
+#define HASH_SHIFT 5
+#define LIT_BUFSIZE 16384
+#define PENDING_SIZE (4 * LIT_BUFSIZE)
+#define D_BUF (LIT_BUFSIZE / 2)
+#define L_BUF (3 * LIT_BUFSIZE)
+#define MIN_MATCH 3
+#define MAX_MATCH 258
+#define MIN_LOOKAHEAD (MAX_MATCH + MIN_MATCH + 1)
+#define MAX_DIST (W_SIZE - MIN_LOOKAHEAD)
+#define L_CODES 286
+#define D_CODES 30
+#define BL_CODES 19
+#define HEAP_SIZE (2 * L_CODES + 1)
+#define END_BLOCK 256
+
+struct DSlab {                      // per-stream HBM state
+    uint8_t window[WINDOW_SIZE];
+    uint8_t pending[PENDING_SIZE];
+    uint16_t prev[W_SIZE];
+    uint16_t head[HASH_SIZE];
+    uint16_t ltree[HEAP_SIZE * 2];
+    uint16_t dtree[(2 * D_CODES + 1) * 2];
+    uint16_t bltree[(2 * BL_CODES + 1) * 2];
+    uint16_t depth[2 * L_CODES + 1];
+    uint16_t heap[2 * L_CODES + 1];
+    uint16_t bl_count[16];
+    uint16_t next_code[16];
+};
+
+#define SLAB_BYTES ((sizeof(DSlab) + 255) & ~(uint64_t)255)
+uint64_t deflate_state_bytes() { return SLAB_BYTES; }
+
+// tables shared by all streams (deftree.ts:25-38, 269-298, 319-337)
+struct DTables {
+    uint8_t dist_code[512];
+    uint8_t length_code[256];
+    uint16_t base_length[29];
+    uint16_t base_dist[30];
+    uint16_t static_ltree[288 * 2];
+    uint16_t static_dtree[30 * 2];
+};
+__constant__ uint8_t c_extra_lbits[29] = { 0, 0, 0, 0, 0, 0, 0, 0, 1, 1, 1, 1, 2, 2, 2, 2, 3, 3, 3, 3, 4, 4, 4, 4, 5, 5, 5, 5, 0 };
+__constant__ uint8_t c_extra_dbits[30] = { 0, 0, 0, 0, 1, 1, 2, 2, 3, 3, 4, 4, 5, 5, 6, 6, 7, 7, 8, 8, 9, 9, 10, 10, 11, 11, 12, 12, 13, 13 };
+__constant__ uint8_t c_extra_blbits[19] = { 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 2, 3, 7 };
+__constant__ uint8_t c_bl_order[19] = { 16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15 };
+// defconfig.ts:33-44 {good, lazy, nice, chain, fast?}
+__constant__ int c_config[10][5] = {
+    { 0, 0, 0, 0, 0 }, { 4, 4, 8, 4, 1 }, { 4, 5, 16, 8, 1 }, { 4, 6, 32, 32, 1 },
+    { 4, 4, 16, 16, 0 }, { 8, 16, 32, 32, 0 }, { 8, 16, 128, 128, 0 }, { 8, 32, 128, 256, 0 },
+    { 32, 128, 258, 1024, 0 }, { 32, 258, 258, 4096, 0 } };
+
+__device__ __forceinline__ uint32_t bitrev_n(uint32_t code, int len) {
+    return __builtin_bitreverse32(code) >> (32 - len);
+}
+
+// build the shared tables in LDS (zlib trees.h derivation, deftree.ts literals)
+__device__ void build_tables(DTables& T) {
+    if (threadIdx.x == 0) {
+        int length = 0, code, n, dist;
+        for (code = 0; code < 28; code++) {
+            T.base_length[code] = (uint16_t)length;
+            for (n = 0; n < (1 << c_extra_lbits[code]); n++) T.length_code[length++] = (uint8_t)code;
+        }
+        T.length_code[length - 1] = (uint8_t)code;
+        T.base_length[28] = 0;
+        dist = 0;
+        for (code = 0; code < 16; code++) {
+            T.base_dist[code] = (uint16_t)dist;
+            for (n = 0; n < (1 << c_extra_dbits[code]); n++) T.dist_code[dist++] = (uint8_t)code;
+        }
+        T.dist_code[256] = 0; T.dist_code[257] = 0;
+        dist >>= 7;
+        for (; code < 30; code++) {
+            T.base_dist[code] = (uint16_t)(dist << 7);
+            for (n = 0; n < (1 << (c_extra_dbits[code] - 7)); n++) T.dist_code[256 + dist++] = (uint8_t)code;
+        }
+        int nc[16] = { 0 }, cnt[16] = { 0 };
+        for (n = 0; n < 288; n++) {
+            int l = n < 144 ? 8 : n < 256 ? 9 : n < 280 ? 7 : 8;
+            T.static_ltree[n * 2 + 1] = (uint16_t)l;
+            cnt[l]++;
+        }
+        int c = 0;
+        for (int b = 1; b < 16; b++) { c = (c + cnt[b - 1]) << 1; nc[b] = c; }
+        for (n = 0; n < 288; n++) {
+            int l = T.static_ltree[n * 2 + 1];
+            T.static_ltree[n * 2] = (uint16_t)bitrev_n((uint32_t)nc[l]++, l);
+        }
+        for (n = 0; n < 30; n++) { T.static_dtree[n * 2 + 1] = 5; T.static_dtree[n * 2] = (uint16_t)bitrev_n((uint32_t)n, 5); }
+    }
+    __syncthreads();
+}
+
+// scalar state of one stream (deflate.ts:102-194), registers
+struct DS {
+    DSlab* S;
+    const DTables* T;
+    const uint8_t* in;
+    uint64_t in_len, in_pos;
+    uint8_t* out;
+    uint64_t out_cap, out_len;
+    int pending;
+    int ins_h, block_start, match_length, match_available, strstart, match_start, lookahead, prev_length;
+    int level, good_match, nice_match, max_chain, max_lazy;
+    int last_lit, matches;
+    int opt_len, static_len;
+    uint32_t bi_buf;
+    int bi_valid;
+    int heap_len, heap_max;
+    int l_max_code, d_max_code, bl_max_code;
+    int err;                        // 1 = pending_buf overflow (reference undefined), 2 = out overflow
+};
+
+// ------------------------------------------------------------------ bit writer (deflate.ts:347-374)
+
+__device__ __forceinline__ void pput(DS& s, int idx, uint32_t v) {
+    if ((unsigned)idx < PENDING_SIZE) s.S->pending[idx] = (uint8_t)v; else s.err |= 1;
+}
+__device__ __forceinline__ void put_short(DS& s, uint32_t w) {
+    pput(s, s.pending++, w & 0xff);
+    pput(s, s.pending++, (w >> 8) & 0xff);
+}
+__device__ __forceinline__ void send_bits(DS& s, uint32_t value, int length) {
+    if (s.bi_valid > 16 - length) {
+        s.bi_buf |= (value << s.bi_valid) & 0xffff;
+        pput(s, s.pending, s.bi_buf);
+        pput(s, s.pending + 1, s.bi_buf >> 8);
+        s.pending += 2;
+        s.bi_buf = value >> (16 - s.bi_valid);
+        s.bi_valid += length - 16;
+    } else {
+        s.bi_buf |= (value << s.bi_valid) & 0xffff;
+        s.bi_valid += length;
+    }
+}
+__device__ __forceinline__ void send_code(DS& s, int c, const uint16_t* tree) {
+    send_bits(s, tree[c * 2], tree[c * 2 + 1]);
+}
+
+// ------------------------------------------------------------------ trees (deftree.ts)
+
+__device__ __forceinline__ bool smaller(const uint16_t* tree, int n, int m, const uint16_t* depth) {
+    int tn = tree[n * 2], tm = tree[m * 2];
+    return tn < tm || (tn == tm && depth[n] <= depth[m]);
+}
+
+__device__ void pqdownheap(DS& s, uint16_t* tree, int k) {                 // deflate.ts:241-263
+    uint16_t* heap = s.S->heap;
+    const uint16_t* depth = s.S->depth;
+    int v = heap[k];
+    int j = k << 1;
+    while (j <= s.heap_len) {
+        if (j < s.heap_len && smaller(tree, heap[j + 1], heap[j], depth)) j++;
+        if (smaller(tree, v, heap[j], depth)) break;
+        heap[k] = heap[j];
+        k = j;
+        j <<= 1;
+    }
+    heap[k] = (uint16_t)v;
+}
+
+// deftree.ts:60-132 gen_bitlen
+__device__ void gen_bitlen(DS& s, uint16_t* tree, int max_code, const uint16_t* stree,
+                           const uint8_t* extra, int base, int max_length) {
+    uint16_t* heap = s.S->heap;
+    uint16_t* bl_count = s.S->bl_count;
+    int h, n, m, bits, xbits, f, overflow = 0;
+    for (bits = 0; bits <= 15; bits++) bl_count[bits] = 0;
+    tree[heap[s.heap_max] * 2 + 1] = 0;
+    for (h = s.heap_max + 1; h < HEAP_SIZE; h++) {
+        n = heap[h];
+        bits = tree[tree[n * 2 + 1] * 2 + 1] + 1;
+        if (bits > max_length) { bits = max_length; overflow++; }
+        tree[n * 2 + 1] = (uint16_t)bits;
+        if (n > max_code) continue;
+        bl_count[bits]++;
+        xbits = 0;
+        if (n >= base) xbits = extra[n - base];
+        f = tree[n * 2];
+        s.opt_len += f * (bits + xbits);
+        if (stree) s.static_len += f * (stree[n * 2 + 1] + xbits);
+    }
+    if (overflow == 0) return;
+    do {
+        bits = max_length - 1;
+        while (bl_count[bits] == 0) bits--;
+        bl_count[bits]--;
+        bl_count[bits + 1] += 2;
+        bl_count[max_length]--;
+        overflow -= 2;
+    } while (overflow > 0);
+    for (bits = max_length; bits != 0; bits--) {
+        n = bl_count[bits];
+        while (n != 0) {
+            m = heap[--h];
+            if (m > max_code) continue;
+            if (tree[m * 2 + 1] != bits) {
+                s.opt_len += (bits - tree[m * 2 + 1]) * tree[m * 2];
+                tree[m * 2 + 1] = (uint16_t)bits;
+            }
+            n--;
+        }
+    }
+}
+
+// deftree.ts:155-182 gen_codes
+__device__ void gen_codes(DS& s, uint16_t* tree, int max_code) {
+    uint16_t* next_code = s.S->next_code;
+    const uint16_t* bl_count = s.S->bl_count;
+    int code = 0;
+    for (int bits = 1; bits <= 15; bits++) {
+        code = (code + bl_count[bits - 1]) << 1;
+        next_code[bits] = (uint16_t)code;
+    }
+    for (int n = 0; n <= max_code; n++) {
+        int len = tree[n * 2 + 1];
+        if (len == 0) continue;
+        tree[n * 2] = (uint16_t)bitrev_n(next_code[len]++, len);
+    }
+}
+
+// deftree.ts:190-267 build_tree; returns max_code
+__device__ int build_tree(DS& s, uint16_t* tree, const uint16_t* stree, const uint8_t* extra,
+                          int base, int elems, int max_length) {
+    uint16_t* heap = s.S->heap;
+    uint16_t* depth = s.S->depth;
+    int n, m, max_code = -1, node;
+    s.heap_len = 0;
+    s.heap_max = HEAP_SIZE;
+    for (n = 0; n < elems; n++) {
+        if (tree[n * 2] != 0) { heap[++s.heap_len] = (uint16_t)(max_code = n); depth[n] = 0; }
+        else tree[n * 2 + 1] = 0;
+    }
+    while (s.heap_len < 2) {
+        node = max_code < 2 ? ++max_code : 0;
+        heap[++s.heap_len] = (uint16_t)node;
+        tree[node * 2] = 1;
+        depth[node] = 0;
+        s.opt_len--;
+        if (stree) s.static_len -= stree[node * 2 + 1];
+    }
+    for (n = s.heap_len / 2; n >= 1; n--) pqdownheap(s, tree, n);
+    node = elems;
+    do {
+        n = heap[1];
+        heap[1] = heap[s.heap_len--];
+        pqdownheap(s, tree, 1);
+        m = heap[1];
+        heap[--s.heap_max] = (uint16_t)n;
+        heap[--s.heap_max] = (uint16_t)m;
+        tree[node * 2] = (uint16_t)(tree[n * 2] + tree[m * 2]);
+        depth[node] = (uint16_t)((depth[n] > depth[m] ? depth[n] : depth[m]) + 1);
+        tree[n * 2 + 1] = tree[m * 2 + 1] = (uint16_t)node;
+        heap[1] = (uint16_t)(node++);
+        pqdownheap(s, tree, 1);
+    } while (s.heap_len >= 2);
+    heap[--s.heap_max] = heap[1];
+    gen_bitlen(s, tree, max_code, stree, extra, base, max_length);
+    gen_codes(s, tree, max_code);
+    return max_code;
+}
+
+// deflate.ts:267-312 scan_tree
+__device__ void scan_tree(DS& s, uint16_t* tree, int max_code) {
+    uint16_t* bl = s.S->bltree;
+    int prevlen = -1, curlen, nextlen = tree[1], count = 0, max_count = 7, min_count = 4;
+    if (nextlen == 0) { max_count = 138; min_count = 3; }
+    tree[(max_code + 1) * 2 + 1] = 0xffff;
+    for (int n = 0; n <= max_code; n++) {
+        curlen = nextlen;
+        nextlen = tree[(n + 1) * 2 + 1];
+        if (++count < max_count && curlen == nextlen) continue;
+        else if (count < min_count) bl[curlen * 2] = (uint16_t)(bl[curlen * 2] + count);
+        else if (curlen != 0) { if (curlen != prevlen) bl[curlen * 2]++; bl[16 * 2]++; }
+        else if (count <= 10) bl[17 * 2]++;
+        else bl[18 * 2]++;
+        count = 0;
+        prevlen = curlen;
+        if (nextlen == 0) { max_count = 138; min_count = 3; }
+        else if (curlen == nextlen) { max_count = 6; min_count = 3; }
+        else { max_count = 7; min_count = 4; }
+    }
+}
+
+// deflate.ts:378-429 send_tree
+__device__ void send_tree(DS& s, const uint16_t* tree, int max_code) {
+    const uint16_t* bl = s.S->bltree;
+    int prevlen = -1, curlen, nextlen = tree[1], count = 0, max_count = 7, min_count = 4;
+    if (nextlen == 0) { max_count = 138; min_count = 3; }
+    for (int n = 0; n <= max_code; n++) {
+        curlen = nextlen;
+        nextlen = tree[(n + 1) * 2 + 1];
+        if (++count < max_count && curlen == nextlen) continue;
+        else if (count < min_count) { do { send_code(s, curlen, bl); } while (--count != 0); }
+        else if (curlen != 0) {
+            if (curlen != prevlen) { send_code(s, curlen, bl); count--; }
+            send_code(s, 16, bl);
+            send_bits(s, (uint32_t)(count - 3), 2);
+        } else if (count <= 10) { send_code(s, 17, bl); send_bits(s, (uint32_t)(count - 3), 3); }
+        else { send_code(s, 18, bl); send_bits(s, (uint32_t)(count - 11), 7); }
+        count = 0;
+        prevlen = curlen;
+        if (nextlen == 0) { max_count = 138; min_count = 3; }
+        else if (curlen == nextlen) { max_count = 6; min_count = 3; }
+        else { max_count = 7; min_count = 4; }
+    }
+}
+
+__device__ __forceinline__ int d_code(const DTables* T, int dist) {
+    return dist < 256 ? T->dist_code[dist] : T->dist_code[256 + (dist >> 7)];
+}
+
+// deflate.ts:222-234
+__device__ void init_block(DS& s) {
+    for (int i = 0; i < L_CODES; i++) s.S->ltree[i * 2] = 0;
+    for (int i = 0; i < D_CODES; i++) s.S->dtree[i * 2] = 0;
+    for (int i = 0; i < BL_CODES; i++) s.S->bltree[i * 2] = 0;
+    s.S->ltree[END_BLOCK * 2] = 1;
+    s.opt_len = s.static_len = 0;
+    s.last_lit = s.matches = 0;
+}
+
+// deflate.ts:488-524 _tr_tally (TRUNCATE_BLOCK heuristic kept)
+__device__ __forceinline__ bool tr_tally(DS& s, int dist, int lc) {
+    uint8_t* pb = s.S->pending;
+    pb[D_BUF + s.last_lit * 2] = (uint8_t)(dist >> 8);
+    pb[D_BUF + s.last_lit * 2 + 1] = (uint8_t)dist;
+    pb[L_BUF + s.last_lit] = (uint8_t)lc;
+    s.last_lit++;
+    if (dist == 0) {
+        s.S->ltree[lc * 2]++;
+    } else {
+        s.matches++;
+        dist--;
+        s.S->ltree[(s.T->length_code[lc] + 257) * 2]++;
+        s.S->dtree[d_code(s.T, dist) * 2]++;
+    }
+    if ((s.last_lit & 0x1fff) == 0 && s.level > 2) {
+        uint32_t out_length = (uint32_t)s.last_lit * 8;
+        int in_length = s.strstart - s.block_start;
+        for (int dc = 0; dc < D_CODES; dc++) out_length += (uint32_t)s.S->dtree[dc * 2] * (5 + c_extra_dbits[dc]);
+        out_length >>= 3;
+        if (s.matches < s.last_lit / 2 && (int)out_length < in_length / 2) return true;
+    }
+    return s.last_lit == LIT_BUFSIZE - 1;
+}
+
+// deflate.ts:527-571 compress_block: reads d_buf/l_buf out of the pending_buf it writes
+__device__ void compress_block(DS& s, const uint16_t* ltree, const uint16_t* dtree) {
+    const uint8_t* pb = s.S->pending;
+    int lx = 0;
+    if (s.last_lit != 0) {
+        do {
+            int dist = (pb[D_BUF + lx * 2] << 8) | pb[D_BUF + lx * 2 + 1];
+            int lc = pb[L_BUF + lx];
+            lx++;
+            if (dist == 0) {
+                send_code(s, lc, ltree);
+            } else {
+                int code = s.T->length_code[lc];
+                send_code(s, code + 257, ltree);
+                int extra = c_extra_lbits[code];
+                if (extra != 0) send_bits(s, (uint32_t)(lc - s.T->base_length[code]), extra);
+                dist--;
+                code = d_code(s.T, dist);
+                send_code(s, code, dtree);
+                extra = c_extra_dbits[code];
+                if (extra != 0) send_bits(s, (uint32_t)(dist - s.T->base_dist[code]), extra);
+            }
+        } while (lx < s.last_lit);
+    }
+    send_code(s, END_BLOCK, ltree);
+}
+
+// deflate.ts:574-583
+__device__ void bi_windup(DS& s) {
+    if (s.bi_valid > 8) put_short(s, s.bi_buf);
+    else if (s.bi_valid > 0) pput(s, s.pending++, s.bi_buf);
+    s.bi_buf = 0;
+    s.bi_valid = 0;
+}
+
+// zstream.ts:76-94 into the stream's output slot
+__device__ void flush_pending(DS& s) {
+    int len = s.pending;
+    if (len == 0) return;
+    if (s.out_len + (uint64_t)len > s.out_cap) { s.err |= 2; s.pending = 0; return; }
+    if (len > PENDING_SIZE) { s.err |= 1; len = PENDING_SIZE; }
+    const uint8_t* pb = s.S->pending;
+    for (int i = 0; i < len; i++) s.out[s.out_len + i] = pb[i];
+    s.out_len += (uint64_t)s.pending;
+    s.pending = 0;
+}
+
+// deflate.ts:614-674 _tr_flush_block (+ flush_block_only 676-680)
+__device__ void flush_block(DS& s, bool eof) {
+    int buf = s.block_start >= 0 ? s.block_start : -1;
+    int stored_len = s.strstart - s.block_start;
+    s.l_max_code = build_tree(s, s.S->ltree, s.T->static_ltree, c_extra_lbits, 257, L_CODES, 15);
+    s.d_max_code = build_tree(s, s.S->dtree, s.T->static_dtree, c_extra_dbits, 0, D_CODES, 15);
+    // build_bl_tree (deflate.ts:316-339)
+    scan_tree(s, s.S->ltree, s.l_max_code);
+    scan_tree(s, s.S->dtree, s.d_max_code);
+    build_tree(s, s.S->bltree, nullptr, c_extra_blbits, 0, BL_CODES, 7);
+    int max_blindex;
+    for (max_blindex = BL_CODES - 1; max_blindex >= 3; max_blindex--)
+        if (s.S->bltree[c_bl_order[max_blindex] * 2 + 1] != 0) break;
+    s.opt_len += 3 * (max_blindex + 1) + 5 + 5 + 4;
+    uint32_t opt_lenb = (uint32_t)(s.opt_len + 3 + 7) >> 3;
+    uint32_t static_lenb = (uint32_t)(s.static_len + 3 + 7) >> 3;
+    if (static_lenb <= opt_lenb) opt_lenb = static_lenb;
+    if ((uint32_t)(stored_len + 4) <= opt_lenb && buf != -1) {
+        send_bits(s, eof ? 1u : 0u, 3);                     // _tr_stored_block
+        bi_windup(s);
+        put_short(s, (uint32_t)stored_len);
+        put_short(s, ~(uint32_t)stored_len);
+        if (s.pending + stored_len > PENDING_SIZE) s.err |= 1;
+        else {
+            for (int i = 0; i < stored_len; i++) s.S->pending[s.pending + i] = s.S->window[buf + i];
+            s.pending += stored_len;
+        }
+    } else if (static_lenb == opt_lenb) {
+        send_bits(s, 2u + (eof ? 1u : 0u), 3);
+        compress_block(s, s.T->static_ltree, s.T->static_dtree);
+    } else {
+        send_bits(s, 4u + (eof ? 1u : 0u), 3);
+        int lcodes = s.l_max_code + 1, dcodes = s.d_max_code + 1, blcodes = max_blindex + 1;
+        send_bits(s, (uint32_t)(lcodes - 257), 5);
+        send_bits(s, (uint32_t)(dcodes - 1), 5);
+        send_bits(s, (uint32_t)(blcodes - 4), 4);
+        for (int rank = 0; rank < blcodes; rank++) send_bits(s, s.S->bltree[c_bl_order[rank] * 2 + 1], 3);
+        send_tree(s, s.S->ltree, lcodes - 1);
+        send_tree(s, s.S->dtree, dcodes - 1);
+        compress_block(s, s.S->ltree, s.S->dtree);
+    }
+    init_block(s);
+    if (eof) bi_windup(s);
+    s.block_start = s.strstart;
+    flush_pending(s);
+}
+
+// deflate.ts:690-766 fill_window (the whole input is available: one-shot append)
+__device__ void fill_window(DS& s) {
+    do {
+        int more = WINDOW_SIZE - s.lookahead - s.strstart;
+        if (more == 0 && s.strstart == 0 && s.lookahead == 0) more = W_SIZE;
+        else if (more == -1) more--;
+        else if (s.strstart >= W_SIZE + W_SIZE - MIN_LOOKAHEAD) {
+            uint4* w4 = (uint4*)s.S->window;
+            for (int i = 0; i < W_SIZE / 16; i++) w4[i] = w4[i + W_SIZE / 16];
+            s.match_start -= W_SIZE;
+            s.strstart -= W_SIZE;
+            s.block_start -= W_SIZE;
+            for (int p = 0; p < HASH_SIZE; p++) { int m = s.S->head[p]; s.S->head[p] = (uint16_t)(m >= W_SIZE ? m - W_SIZE : 0); }
+            for (int p = 0; p < W_SIZE; p++) { int m = s.S->prev[p]; s.S->prev[p] = (uint16_t)(m >= W_SIZE ? m - W_SIZE : 0); }
+            more += W_SIZE;
+        }
+        uint64_t avail = s.in_len - s.in_pos;
+        if (avail == 0) return;
+        int n = avail > (uint64_t)more ? more : (int)avail;
+        uint8_t* dst = s.S->window + s.strstart + s.lookahead;
+        for (int i = 0; i < n; i++) dst[i] = s.in[s.in_pos + i];
+        s.in_pos += (uint64_t)n;
+        s.lookahead += n;
+        if (s.lookahead >= MIN_MATCH) {
+            s.ins_h = s.S->window[s.strstart];
+            s.ins_h = ((s.ins_h << HASH_SHIFT) ^ s.S->window[s.strstart + 1]) & HASH_MASK;
+        }
+    } while (s.lookahead < MIN_LOOKAHEAD && s.in_pos < s.in_len);
+}
+
+// deflate.ts:827-946 longest_match
+__device__ int longest_match(DS& s, int cur_match) {
+    const uint8_t* win = s.S->window;
+    const uint16_t* prev = s.S->prev;
+    int chain_length = s.max_chain;
+    int scan = s.strstart;
+    int best_len = s.prev_length;
+    int limit = s.strstart > MAX_DIST ? s.strstart - MAX_DIST : 0;
+    int nice = s.nice_match;
+    int strend = s.strstart + MAX_MATCH;
+    int scan_end1 = win[scan + best_len - 1];
+    int scan_end = win[scan + best_len];
+    int scan_start = win[scan];
+    int scan_start1 = win[scan + 1];
+    if (s.prev_length >= s.good_match) chain_length >>= 2;
+    if (nice > s.lookahead) nice = s.lookahead;
+    do {
+        int match = cur_match;
+        if (win[match + best_len] != scan_end || win[match + best_len - 1] != scan_end1 ||
+            win[match] != scan_start || win[match + 1] != scan_start1)
+            continue;
+        int sp = scan + 2, mp = match + 2;
+        do {
+            uint32_t sv = ((uint32_t)win[sp] << 24) | ((uint32_t)win[sp + 1] << 16) | ((uint32_t)win[sp + 2] << 8) | win[sp + 3];
+            uint32_t mv = ((uint32_t)win[mp] << 24) | ((uint32_t)win[mp + 1] << 16) | ((uint32_t)win[mp + 2] << 8) | win[mp + 3];
+            uint32_t x = sv ^ mv;
+            if (x) { int mb = __builtin_clz(x) >> 3; sp += mb; mp += mb; break; }
+            sp += 4; mp += 4;
+        } while (sp < strend);
+        if (sp > strend) sp = strend;
+        int len = MAX_MATCH - (strend - sp);
+        if (len > best_len) {
+            s.match_start = cur_match;
+            best_len = len;
+            if (len >= nice) break;
+            scan_end1 = win[scan + best_len - 1];
+            scan_end = win[scan + best_len];
+        }
+    } while ((cur_match = prev[cur_match & W_MASK]) > limit && --chain_length != 0);
+    return best_len <= s.lookahead ? best_len : s.lookahead;
+}
+
+__device__ __forceinline__ int insert_string(DS& s) {
+    s.ins_h = ((s.ins_h << HASH_SHIFT) ^ s.S->window[s.strstart + (MIN_MATCH - 1)]) & HASH_MASK;
+    int hh = s.S->head[s.ins_h];
+    s.S->prev[s.strstart & W_MASK] = (uint16_t)hh;
+    s.S->head[s.ins_h] = (uint16_t)s.strstart;
+    return hh;
+}
+
+// deflate.ts:953-1049 (levels 1-3), run to FINISH
+__device__ void deflate_fast(DS& s) {
+    int hash_head = 0;
+    for (;;) {
+        if (s.lookahead < MIN_LOOKAHEAD) {
+            fill_window(s);
+            if (s.lookahead == 0) break;
+        }
+        if (s.lookahead >= MIN_MATCH) hash_head = insert_string(s);
+        if (hash_head != 0 && ((s.strstart - hash_head) & 0xffff) <= MAX_DIST)
+            s.match_length = longest_match(s, hash_head);
+        bool bflush;
+        if (s.match_length >= MIN_MATCH) {
+            bflush = tr_tally(s, s.strstart - s.match_start, s.match_length - MIN_MATCH);
+            s.lookahead -= s.match_length;
+            if (s.match_length <= s.max_lazy && s.lookahead >= MIN_MATCH) {
+                s.match_length--;
+                do { s.strstart++; hash_head = insert_string(s); } while (--s.match_length != 0);
+                s.strstart++;
+            } else {
+                s.strstart += s.match_length;
+                s.match_length = 0;
+                s.ins_h = s.S->window[s.strstart];
+                s.ins_h = ((s.ins_h << HASH_SHIFT) ^ s.S->window[s.strstart + 1]) & HASH_MASK;
+            }
+        } else {
+            bflush = tr_tally(s, 0, s.S->window[s.strstart]);
+            s.lookahead--;
+            s.strstart++;
+        }
+        if (bflush) flush_block(s, false);
+    }
+    flush_block(s, true);
+}
+
+// deflate.ts:1054-1182 (levels 4-9), run to FINISH
+__device__ void deflate_slow(DS& s) {
+    int hash_head = 0;
+    for (;;) {
+        if (s.lookahead < MIN_LOOKAHEAD) {
+            fill_window(s);
+            if (s.lookahead == 0) break;
+        }
+        if (s.lookahead >= MIN_MATCH) hash_head = insert_string(s);
+        s.prev_length = s.match_length;
+        int prev_match = s.match_start;
+        s.match_length = MIN_MATCH - 1;
+        if (hash_head != 0 && s.prev_length < s.max_lazy && ((s.strstart - hash_head) & 0xffff) <= MAX_DIST) {
+            s.match_length = longest_match(s, hash_head);
+            if (s.match_length <= 5 && s.match_length == MIN_MATCH && s.strstart - s.match_start > 4096)
+                s.match_length = MIN_MATCH - 1;
+        }
+        if (s.prev_length >= MIN_MATCH && s.match_length <= s.prev_length) {
+            int max_insert = s.strstart + s.lookahead - MIN_MATCH;
+            bool bflush = tr_tally(s, s.strstart - 1 - prev_match, s.prev_length - MIN_MATCH);
+            s.lookahead -= s.prev_length - 1;
+            s.prev_length -= 2;
+            do {
+                if (++s.strstart <= max_insert) hash_head = insert_string(s);
+            } while (--s.prev_length != 0);
+            s.match_available = 0;
+            s.match_length = MIN_MATCH - 1;
+            s.strstart++;
+            if (bflush) flush_block(s, false);
+        } else if (s.match_available) {
+            bool bflush = tr_tally(s, 0, s.S->window[s.strstart - 1]);
+            if (bflush) flush_block(s, false);
+            s.strstart++;
+            s.lookahead--;
+        } else {
+            s.match_available = 1;
+            s.strstart++;
+            s.lookahead--;
+        }
+    }
+    if (s.match_available) {
+        tr_tally(s, 0, s.S->window[s.strstart - 1]);
+        s.match_available = 0;
+    }
+    flush_block(s, true);
+}
+
+// adler32.ts:34-105 / crc32.ts:48-106 over the input (Deflater.append, sd-deflate.ts:185-190)
+__device__ int32_t input_checksum(const uint8_t* p, uint64_t n, bool gzip, const uint32_t* crct) {
+    if (gzip) {
+        uint32_t c = 0xffffffffu;
+        for (uint64_t i = 0; i < n; i++) c = crct[(c ^ p[i]) & 255] ^ (c >> 8);
+        return (int32_t)~c;
+    }
+    uint64_t a = 1, s2 = 0, len = n, off = 0;
+    while (len >= 5552) {
+        len -= 5552;
+        for (int i = 0; i < 5552; i++) { a += p[off++]; s2 += a; }
+        a %= 65521u;
+        s2 += 65521u;
+    }
+    if (len) {
+        while (len--) { a += p[off++]; s2 += a; }
+        a %= 65521u;
+        s2 %= 65521u;
+    }
+    return (int32_t)((uint32_t)a | ((uint32_t)s2 << 16));
+}
+
+__global__ __launch_bounds__(DF_THREADS) void k_deflate(DeflateArgs A) {
+    __shared__ DTables T;
+    __shared__ uint32_t crct[256];
+    build_tables(T);
+    for (int n = threadIdx.x; n < 256; n += DF_THREADS) {
+        uint32_t c = (uint32_t)n;
+        for (int k = 0; k < 8; ++k) c = (c & 1) ? 0xedb88320u ^ (c >> 1) : c >> 1;
+        crct[n] = c;
+    }
+    __syncthreads();
+    uint32_t sid = blockIdx.x * DF_THREADS + threadIdx.x;
+    if (sid >= A.n) return;
+
+    DS s;
+    s.S = (DSlab*)(A.state + (uint64_t)sid * SLAB_BYTES);
+    s.T = &T;
+    s.in = A.in + A.in_off[sid];
+    s.in_len = A.in_len[sid];
+    s.in_pos = 0;
+    s.out = A.out + A.out_off[sid];
+    s.out_cap = A.out_cap[sid];
+    s.out_len = 0;
+    s.err = 0;
+    sdz_deflate_record R;
+    R.status = SDZ_OK; R.checksum = 0; R.out_len = 0; R.reserved = 0;
+    if (s.in_len == 0) {                        // sd-deflate.ts:180-182 + 232-234
+        R.status = SDZ_DATA_ERROR;
+        A.rec[sid] = R;
+        return;
+    }
+    // Deflate constructor (deflate.ts:196-220) + window zero fill (deflate.ts:119)
+    {
+        uint4 z = make_uint4(0, 0, 0, 0);
+        uint4* w4 = (uint4*)s.S->window;
+        for (int i = 0; i < WINDOW_SIZE / 16; i++) w4[i] = z;
+        uint4* h4 = (uint4*)s.S->head;
+        for (int i = 0; i < HASH_SIZE * 2 / 16; i++) h4[i] = z;
+        uint4* p4 = (uint4*)s.S->prev;
+        for (int i = 0; i < W_SIZE * 2 / 16; i++) p4[i] = z;
+        for (int i = 0; i < HEAP_SIZE * 2; i++) s.S->ltree[i] = 0;
+        for (int i = 0; i < (2 * D_CODES + 1) * 2; i++) s.S->dtree[i] = 0;
+        for (int i = 0; i < (2 * BL_CODES + 1) * 2; i++) s.S->bltree[i] = 0;
+    }
+    s.level = A.level;
+    s.good_match = c_config[A.level][0];
+    s.max_lazy = c_config[A.level][1];
+    s.nice_match = c_config[A.level][2];
+    s.max_chain = c_config[A.level][3];
+    s.pending = 0;
+    s.ins_h = 0; s.block_start = 0; s.match_length = MIN_MATCH - 1; s.match_available = 0;
+    s.strstart = 0; s.match_start = 0; s.lookahead = 0; s.prev_length = MIN_MATCH - 1;
+    s.bi_buf = 0; s.bi_valid = 0;
+    s.heap_len = 0; s.heap_max = HEAP_SIZE;
+    s.l_max_code = s.d_max_code = s.bl_max_code = 0;
+    init_block(s);
+
+    bool gzip = A.format == SDZ_DEFLATE_GZIP;
+    int32_t cks = input_checksum(s.in, s.in_len, gzip, crct);
+    // container header (sd-deflate.ts:98-152): written straight to the output slot
+    uint64_t hdr = A.format == SDZ_DEFLATE_ZLIB ? 2 : gzip ? 10 + (A.fname_len ? A.fname_len + 1 : 0) : 0;
+    if (hdr > s.out_cap) { R.status = SDZ_OUT_OVERFLOW; A.rec[sid] = R; return; }
+    if (A.format == SDZ_DEFLATE_ZLIB) { s.out[0] = 0x78; s.out[1] = 0x01; }
+    else if (gzip) {
+        s.out[0] = 0x1f; s.out[1] = 0x8b; s.out[2] = 8; s.out[3] = A.fname_len ? 8 : 0;
+        s.out[4] = (uint8_t)A.mtime; s.out[5] = (uint8_t)(A.mtime >> 8);
+        s.out[6] = (uint8_t)(A.mtime >> 16); s.out[7] = (uint8_t)(A.mtime >> 24);
+        s.out[8] = 0; s.out[9] = 0xff;
+        for (uint32_t i = 0; i < A.fname_len; i++) s.out[10 + i] = A.fname[i];
+        if (A.fname_len) s.out[10 + A.fname_len] = 0;
+    }
+    s.out_len = hdr;
+
+    if (c_config[A.level][4]) deflate_fast(s); else deflate_slow(s);
+
+    // trailer (sd-deflate.ts:154-165)
+    uint64_t tl = A.format == SDZ_DEFLATE_ZLIB ? 4 : gzip ? 8 : 0;
+    if (s.out_len + tl > s.out_cap) s.err |= 2;
+    else if (A.format == SDZ_DEFLATE_ZLIB) {
+        uint32_t c = (uint32_t)cks;
+        s.out[s.out_len] = (uint8_t)(c >> 24); s.out[s.out_len + 1] = (uint8_t)(c >> 16);
+        s.out[s.out_len + 2] = (uint8_t)(c >> 8); s.out[s.out_len + 3] = (uint8_t)c;
+        s.out_len += 4;
+    } else if (gzip) {
+        uint32_t c = (uint32_t)cks, z = (uint32_t)s.in_len;
+        for (int k = 0; k < 4; k++) s.out[s.out_len + k] = (uint8_t)(c >> (8 * k));
+        for (int k = 0; k < 4; k++) s.out[s.out_len + 4 + k] = (uint8_t)(z >> (8 * k));
+        s.out_len += 8;
+    }
+    R.status = (s.err & 2) ? SDZ_OUT_OVERFLOW : (s.err & 1) ? SDZ_DATA_ERROR : SDZ_OK;
+    R.checksum = cks;
+    R.out_len = s.out_len;
+    A.rec[sid] = R;
+}
+
+void launch_deflate(const DeflateArgs& a, hipStream_t st) {
+    if (a.n == 0) return;
+    dim3 grid((a.n + DF_THREADS - 1) / DF_THREADS);
+    hipLaunchKernelGGL(k_deflate, grid, dim3(DF_THREADS), 0, st, a);
+}
+
+}  // namespace sdz

@@ -1,0 +1,62 @@
+// sdz_internal.h -- shared between the runtime (sdz_runtime.cpp) and the HIP kernels.
+#pragma once
+#include <stdint.h>
+#include <hip/hip_runtime.h>
+#include "sdz.h"
+
+namespace sdz {
+
+// z.msg reason codes (texts in sdz_runtime.cpp)
+enum ZMsg : int32_t {
+    ZM_NONE = 0, ZM_INVALID_GZIP_ID, ZM_UNKNOWN_METHOD, ZM_INVALID_WINDOW, ZM_HEADER_CHECK,
+    ZM_NEED_DICT, ZM_BLOCK_TYPE, ZM_STORED_LENS, ZM_TOO_MANY_SYMS, ZM_BL_REPEAT,
+    ZM_BL_OVERSUB, ZM_BL_INCOMPLETE, ZM_LL_OVERSUB, ZM_LL_INCOMPLETE, ZM_D_OVERSUB,
+    ZM_D_INCOMPLETE, ZM_D_EMPTY, ZM_INVALID_DIST, ZM_INVALID_LITLEN, ZM_COUNT
+};
+
+// bytes of per-stream global scratch used by the inflate kernel (code lengths)
+constexpr uint64_t kInflateScratchPerStream = 320;
+
+struct InflateArgs {
+    const uint8_t* in;
+    const uint64_t* in_off;
+    const uint64_t* in_len;
+    uint8_t* out;
+    const uint64_t* out_off;
+    const uint64_t* out_cap;
+    sdz_inflate_record* rec;
+    uint8_t* scratch;            // n * kInflateScratchPerStream
+    const uint32_t* order;       // lane -> stream id (LPT order), may be null
+    const uint8_t* dict;         // preset dictionary (last <= 32767 bytes used), may be null
+    uint32_t dict_len;
+    int32_t dict_adler;          // adler32.ts of the full dictionary
+    uint32_t n;
+    int32_t format;
+};
+
+void launch_inflate(const InflateArgs& a, hipStream_t s);
+
+struct DeflateArgs {
+    const uint8_t* in;
+    const uint64_t* in_off;
+    const uint64_t* in_len;
+    uint8_t* out;
+    const uint64_t* out_off;
+    const uint64_t* out_cap;
+    sdz_deflate_record* rec;
+    uint8_t* state;              // n * deflate_state_bytes()
+    const uint8_t* fname;
+    uint32_t fname_len;
+    uint32_t mtime;
+    uint32_t n;
+    int32_t level;
+    int32_t format;
+};
+
+uint64_t deflate_state_bytes();
+void launch_deflate(const DeflateArgs& a, hipStream_t s);
+
+void launch_checksum(const uint8_t* in, const uint64_t* in_off, const uint64_t* in_len,
+                     const int32_t* seed, int32_t* result, uint32_t n, int kind, hipStream_t s);
+
+}  // namespace sdz

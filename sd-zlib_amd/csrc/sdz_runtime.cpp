@@ -1,0 +1,412 @@
+// sdz_runtime.cpp -- the C ABI of libsdz.so (include/sdz.h): argument checks,
+// device scratch pools, kernel-timing events and the host-copy convenience paths.
+// No codec runs on the CPU here: every entry point launches the HIP kernels.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <numeric>
+#include <string>
+#include <vector>
+
+#include "sdz_internal.h"
+
+using namespace sdz;
+
+namespace {
+
+thread_local std::string g_err;
+thread_local float g_last_ms = 0.f;
+thread_local hipEvent_t g_ev0 = nullptr, g_ev1 = nullptr;
+thread_local bool g_ev_pending = false;
+int g_timing = 0;
+std::mutex g_mu;
+
+int fail(int code, const std::string& msg) {
+    g_err = msg;
+    return code;
+}
+
+int hip_fail(hipError_t e, const char* what) {
+    return fail(SDZ_API_HIP_ERROR, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+#define HIPCHK(x)                                             \
+    do {                                                      \
+        hipError_t e_ = (x);                                  \
+        if (e_ != hipSuccess) return hip_fail(e_, #x);        \
+    } while (0)
+
+int ensure_device() {
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess || n == 0)
+        return fail(SDZ_API_NO_DEVICE, "no HIP device available (libsdz has no CPU codec path)");
+    return SDZ_API_OK;
+}
+
+// grow-only device scratch, one per (device, purpose)
+struct Pool {
+    void* p = nullptr;
+    size_t cap = 0;
+    int dev = -1;
+    int get(size_t bytes, void** out) {
+        int d = 0;
+        hipGetDevice(&d);
+        if (p && (cap < bytes || dev != d)) {
+            int cur = d;
+            hipSetDevice(dev);
+            hipFree(p);
+            hipSetDevice(cur);
+            p = nullptr;
+            cap = 0;
+        }
+        if (!p) {
+            size_t want = std::max(bytes, (size_t)1 << 20);
+            hipError_t e = hipMalloc(&p, want);
+            if (e != hipSuccess) { p = nullptr; return hip_fail(e, "hipMalloc(scratch)"); }
+            cap = want;
+            dev = d;
+        }
+        *out = p;
+        return SDZ_API_OK;
+    }
+};
+Pool g_inflate_scratch, g_deflate_state, g_tmp;
+
+void timing_begin(hipStream_t s) {
+    if (!g_timing) return;
+    if (!g_ev0) { hipEventCreate(&g_ev0); hipEventCreate(&g_ev1); }
+    hipEventRecord(g_ev0, s);
+}
+void timing_end(hipStream_t s) {
+    if (!g_timing) return;
+    hipEventRecord(g_ev1, s);
+    g_ev_pending = true;
+}
+
+const char* const kZmsg[ZM_COUNT] = {
+    "",
+    "invalid gzip id",
+    "unknown compression method",
+    "invalid window size",
+    "incorrect header check",
+    "need dictionary",
+    "invalid block type",
+    "invalid stored block lengths",
+    "too many length or distance symbols",
+    "invalid bit length repeat",
+    "oversubscribed dynamic bit lengths tree",
+    "incomplete dynamic bit lengths tree",
+    "oversubscribed literal/length tree",
+    "incomplete literal/length tree",
+    "oversubscribed distance tree",
+    "incomplete distance tree",
+    "empty distance tree with lengths",
+    "invalid distance code",
+    "invalid literal/length code",
+};
+
+// one-shot device checksum of a device buffer (used for the dictionary's DICTID)
+int device_checksum(const uint8_t* d_buf, uint64_t len, int kind, int32_t seed, int32_t* out,
+                    hipStream_t s) {
+    void* tmp = nullptr;
+    int rc = g_tmp.get(64, &tmp);
+    if (rc) return rc;
+    uint64_t* d_off = (uint64_t*)tmp;
+    uint64_t* d_len = d_off + 1;
+    int32_t* d_seed = (int32_t*)(d_off + 2);
+    int32_t* d_res = d_seed + 1;
+    uint64_t hv[2] = { 0, len };
+    HIPCHK(hipMemcpyAsync(d_off, hv, sizeof hv, hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(d_seed, &seed, sizeof seed, hipMemcpyHostToDevice, s));
+    launch_checksum(d_buf, d_off, d_len, d_seed, d_res, 1, kind, s);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(out, d_res, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    return SDZ_API_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* sdz_last_error(void) { return g_err.c_str(); }
+int sdz_version(void) { return SDZ_ABI_VERSION; }
+
+int sdz_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+int sdz_set_device(int device) {
+    HIPCHK(hipSetDevice(device));
+    return SDZ_API_OK;
+}
+
+const char* sdz_zmsg(int32_t code) { return (code >= 0 && code < ZM_COUNT) ? kZmsg[code] : ""; }
+
+void* sdz_device_alloc(uint64_t bytes) {
+    if (ensure_device()) return nullptr;
+    void* p = nullptr;
+    hipError_t e = hipMalloc(&p, bytes ? bytes : 1);
+    if (e != hipSuccess) { hip_fail(e, "hipMalloc"); return nullptr; }
+    return p;
+}
+void sdz_device_free(void* ptr) { if (ptr) hipFree(ptr); }
+int sdz_copy_to_device(void* dst, const void* src, uint64_t bytes) {
+    HIPCHK(hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice));
+    return SDZ_API_OK;
+}
+int sdz_copy_to_host(void* dst, const void* src, uint64_t bytes) {
+    HIPCHK(hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost));
+    return SDZ_API_OK;
+}
+int sdz_memset_device(void* dst, int value, uint64_t bytes) {
+    HIPCHK(hipMemset(dst, value, bytes));
+    return SDZ_API_OK;
+}
+int sdz_copy_device_to_device(void* dst, const void* src, uint64_t bytes) {
+    HIPCHK(hipMemcpy(dst, src, bytes, hipMemcpyDeviceToDevice));
+    return SDZ_API_OK;
+}
+int sdz_sync(void* stream) {
+    if (stream) { HIPCHK(hipStreamSynchronize((hipStream_t)stream)); }
+    else { HIPCHK(hipDeviceSynchronize()); }
+    return SDZ_API_OK;
+}
+int sdz_set_timing(int enabled) { g_timing = enabled; return SDZ_API_OK; }
+float sdz_last_kernel_ms(void) {
+    if (g_ev_pending) {
+        hipEventSynchronize(g_ev1);
+        float ms = 0.f;
+        hipEventElapsedTime(&ms, g_ev0, g_ev1);
+        g_last_ms = ms;
+        g_ev_pending = false;
+    }
+    return g_last_ms;
+}
+
+// ----------------------------------------------------------------- inflate
+
+int sdz_inflate_batch_device(const uint8_t* in, const uint64_t* in_off, const uint64_t* in_len,
+                             uint8_t* out, const uint64_t* out_off, const uint64_t* out_cap,
+                             sdz_inflate_record* rec, uint32_t n, int32_t format,
+                             const uint8_t* dict, uint32_t dict_len, void* stream) {
+    if (int rc = ensure_device()) return rc;
+    if (n == 0) return SDZ_API_OK;
+    if (!in || !in_off || !in_len || !out || !out_off || !out_cap || !rec)
+        return fail(SDZ_API_BAD_ARG, "sdz_inflate_batch_device: null pointer");
+    if (format < SDZ_FMT_AUTO || format > SDZ_FMT_CONTAINER)
+        return fail(SDZ_API_BAD_ARG, "sdz_inflate_batch_device: bad format");
+    hipStream_t s = (hipStream_t)stream;
+    std::lock_guard<std::mutex> lk(g_mu);
+    void* scratch = nullptr;
+    if (int rc = g_inflate_scratch.get((size_t)n * kInflateScratchPerStream, &scratch)) return rc;
+    int32_t dict_adler = 1;
+    if (dict) {
+        if (int rc = device_checksum(dict, dict_len, 0, 1, &dict_adler, s)) return rc;
+    }
+    InflateArgs a;
+    a.in = in; a.in_off = in_off; a.in_len = in_len;
+    a.out = out; a.out_off = out_off; a.out_cap = out_cap;
+    a.rec = rec; a.scratch = (uint8_t*)scratch; a.order = nullptr;
+    a.dict = dict; a.dict_len = dict_len; a.dict_adler = dict_adler;
+    a.n = n; a.format = format;
+    timing_begin(s);
+    launch_inflate(a, s);
+    timing_end(s);
+    HIPCHK(hipGetLastError());
+    return SDZ_API_OK;
+}
+
+// ----------------------------------------------------------------- deflate
+
+uint64_t sdz_deflate_bound(uint64_t in_len, int32_t format, uint32_t fname_len) {
+    // stored-block worst case (5 bytes per <= 16383-symbol block at most) + trees + container
+    uint64_t blocks = in_len / 16000 + 2;
+    uint64_t b = in_len + blocks * 5 + in_len / 8 + 1024;
+    if (format == SDZ_DEFLATE_ZLIB) b += 6;
+    if (format == SDZ_DEFLATE_GZIP) b += 18 + fname_len + 1;
+    return (b + 7) & ~7ull;
+}
+
+int sdz_deflate_batch_device(const uint8_t* in, const uint64_t* in_off, const uint64_t* in_len,
+                             uint8_t* out, const uint64_t* out_off, const uint64_t* out_cap,
+                             sdz_deflate_record* rec, uint32_t n, int32_t level, int32_t format,
+                             const uint8_t* fname, uint32_t fname_len, uint32_t mtime,
+                             void* stream) {
+    if (int rc = ensure_device()) return rc;
+    if (n == 0) return SDZ_API_OK;
+    if (level < 1 || level > 9) return fail(SDZ_API_BAD_ARG, "level must be between 1 and 9, inclusive");
+    if (format < SDZ_DEFLATE_RAW || format > SDZ_DEFLATE_GZIP)
+        return fail(SDZ_API_BAD_ARG, "container must be one of `raw`, `deflate`, `gzip`");
+    if (!in || !in_off || !in_len || !out || !out_off || !out_cap || !rec)
+        return fail(SDZ_API_BAD_ARG, "sdz_deflate_batch_device: null pointer");
+    hipStream_t s = (hipStream_t)stream;
+    std::lock_guard<std::mutex> lk(g_mu);
+    // per-stream state slabs: process in sub-batches so the slab pool stays bounded
+    const uint32_t kMaxSlabs = 16384;
+    uint64_t slab = deflate_state_bytes();
+    uint32_t chunk = std::min(n, kMaxSlabs);
+    void* state = nullptr;
+    if (int rc = g_deflate_state.get((size_t)chunk * slab, &state)) return rc;
+    uint8_t* d_fname = nullptr;
+    void* tmp = nullptr;
+    if (fname_len) {
+        if (int rc = g_tmp.get(fname_len + 64, &tmp)) return rc;
+        d_fname = (uint8_t*)tmp;
+        HIPCHK(hipMemcpyAsync(d_fname, fname, fname_len, hipMemcpyHostToDevice, s));
+    }
+    timing_begin(s);
+    for (uint32_t b = 0; b < n; b += chunk) {
+        DeflateArgs a;
+        uint32_t m = std::min(chunk, n - b);
+        a.in = in; a.in_off = in_off + b; a.in_len = in_len + b;
+        a.out = out; a.out_off = out_off + b; a.out_cap = out_cap + b;
+        a.rec = rec + b; a.state = (uint8_t*)state;
+        a.fname = d_fname; a.fname_len = fname_len; a.mtime = mtime;
+        a.n = m; a.level = level; a.format = format;
+        launch_deflate(a, s);
+    }
+    timing_end(s);
+    HIPCHK(hipGetLastError());
+    if (fname_len) HIPCHK(hipStreamSynchronize(s));   // tmp pool is reused
+    return SDZ_API_OK;
+}
+
+// ----------------------------------------------------------------- checksums
+
+int sdz_adler32_batch_device(const uint8_t* in, const uint64_t* in_off, const uint64_t* in_len,
+                             const int32_t* seed, int32_t* result, uint32_t n, void* stream) {
+    if (int rc = ensure_device()) return rc;
+    launch_checksum(in, in_off, in_len, seed, result, n, 0, (hipStream_t)stream);
+    HIPCHK(hipGetLastError());
+    return SDZ_API_OK;
+}
+
+int sdz_crc32_batch_device(const uint8_t* in, const uint64_t* in_off, const uint64_t* in_len,
+                           const int32_t* seed, int32_t* result, uint32_t n, void* stream) {
+    if (int rc = ensure_device()) return rc;
+    launch_checksum(in, in_off, in_len, seed, result, n, 1, (hipStream_t)stream);
+    HIPCHK(hipGetLastError());
+    return SDZ_API_OK;
+}
+
+static int32_t host_checksum(const uint8_t* buf, size_t len, int32_t seed, int kind) {
+    if (ensure_device()) return 0;
+    std::lock_guard<std::mutex> lk(g_mu);
+    uint8_t* d = nullptr;
+    if (hipMalloc(&d, len + 64) != hipSuccess) { fail(SDZ_API_OOM, "hipMalloc"); return 0; }
+    int32_t r = 0;
+    if (len && hipMemcpy(d, buf, len, hipMemcpyHostToDevice) != hipSuccess) { hipFree(d); return 0; }
+    device_checksum(d, len, kind, seed, &r, nullptr);
+    hipFree(d);
+    return r;
+}
+
+int32_t sdz_adler32(const uint8_t* buf, size_t len, int32_t seed) { return host_checksum(buf, len, seed, 0); }
+int32_t sdz_crc32(const uint8_t* buf, size_t len, int32_t seed) { return host_checksum(buf, len, seed, 1); }
+
+// ----------------------------------------------------------------- host wrappers
+
+namespace {
+struct HostBatch {
+    uint8_t* d_in = nullptr;
+    uint8_t* d_out = nullptr;
+    uint64_t* d_meta = nullptr;
+    void* d_rec = nullptr;
+    ~HostBatch() {
+        if (d_in) hipFree(d_in);
+        if (d_out) hipFree(d_out);
+        if (d_meta) hipFree(d_meta);
+        if (d_rec) hipFree(d_rec);
+    }
+};
+}  // namespace
+
+int sdz_inflate_batch(const uint8_t* const* in, const size_t* in_len, uint8_t* const* out,
+                      const size_t* out_cap, sdz_inflate_record* rec, uint32_t n, int32_t format,
+                      const uint8_t* dict, size_t dict_len) {
+    if (int rc = ensure_device()) return rc;
+    if (n == 0) return SDZ_API_OK;
+    // LPT order: longest streams first so each wave decodes similar lengths
+    std::vector<uint32_t> ord(n);
+    std::iota(ord.begin(), ord.end(), 0u);
+    std::stable_sort(ord.begin(), ord.end(), [&](uint32_t a, uint32_t b) { return in_len[a] > in_len[b]; });
+    std::vector<uint64_t> meta(4 * (size_t)n);
+    uint64_t ti = 0, to = 0;
+    for (uint32_t k = 0; k < n; ++k) {
+        uint32_t i = ord[k];
+        meta[k] = ti; meta[n + k] = in_len[i];
+        meta[2 * (size_t)n + k] = to; meta[3 * (size_t)n + k] = out_cap[i];
+        ti += (in_len[i] + 15) & ~(uint64_t)15;
+        to += (out_cap[i] + 7) & ~(uint64_t)7;
+    }
+    HostBatch hb;
+    HIPCHK(hipMalloc(&hb.d_in, ti + 128));
+    HIPCHK(hipMalloc(&hb.d_out, to + 64));
+    HIPCHK(hipMalloc(&hb.d_meta, meta.size() * sizeof(uint64_t)));
+    HIPCHK(hipMalloc(&hb.d_rec, (size_t)n * sizeof(sdz_inflate_record)));
+    uint8_t* d_dict = nullptr;
+    if (dict) { HIPCHK(hipMalloc(&d_dict, dict_len + 64)); HIPCHK(hipMemcpy(d_dict, dict, dict_len, hipMemcpyHostToDevice)); }
+    for (uint32_t k = 0; k < n; ++k)
+        if (in_len[ord[k]]) HIPCHK(hipMemcpy(hb.d_in + meta[k], in[ord[k]], in_len[ord[k]], hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(hb.d_meta, meta.data(), meta.size() * sizeof(uint64_t), hipMemcpyHostToDevice));
+    int rc = sdz_inflate_batch_device(hb.d_in, hb.d_meta, hb.d_meta + n, hb.d_out, hb.d_meta + 2 * (size_t)n,
+                                      hb.d_meta + 3 * (size_t)n, (sdz_inflate_record*)hb.d_rec, n, format,
+                                      d_dict, (uint32_t)dict_len, nullptr);
+    if (rc) { if (d_dict) hipFree(d_dict); return rc; }
+    HIPCHK(hipDeviceSynchronize());
+    if (d_dict) hipFree(d_dict);
+    std::vector<sdz_inflate_record> r(n);
+    HIPCHK(hipMemcpy(r.data(), hb.d_rec, (size_t)n * sizeof(sdz_inflate_record), hipMemcpyDeviceToHost));
+    for (uint32_t k = 0; k < n; ++k) {
+        uint32_t i = ord[k];
+        rec[i] = r[k];
+        uint64_t len = std::min<uint64_t>(r[k].out_len, out_cap[i]);
+        if (len && out[i]) HIPCHK(hipMemcpy(out[i], hb.d_out + meta[2 * (size_t)n + k], len, hipMemcpyDeviceToHost));
+    }
+    return SDZ_API_OK;
+}
+
+int sdz_deflate_batch(const uint8_t* const* in, const size_t* in_len, uint8_t* const* out,
+                      const size_t* out_cap, sdz_deflate_record* rec, uint32_t n, int32_t level,
+                      int32_t format, const uint8_t* fname, size_t fname_len, uint32_t mtime) {
+    if (int rc = ensure_device()) return rc;
+    if (n == 0) return SDZ_API_OK;
+    std::vector<uint64_t> meta(4 * (size_t)n);
+    uint64_t ti = 0, to = 0;
+    for (uint32_t i = 0; i < n; ++i) {
+        meta[i] = ti; meta[n + i] = in_len[i];
+        meta[2 * (size_t)n + i] = to; meta[3 * (size_t)n + i] = out_cap[i];
+        ti += (in_len[i] + 15) & ~(uint64_t)15;
+        to += (out_cap[i] + 7) & ~(uint64_t)7;
+    }
+    HostBatch hb;
+    HIPCHK(hipMalloc(&hb.d_in, ti + 128));
+    HIPCHK(hipMalloc(&hb.d_out, to + 64));
+    HIPCHK(hipMalloc(&hb.d_meta, meta.size() * sizeof(uint64_t)));
+    HIPCHK(hipMalloc(&hb.d_rec, (size_t)n * sizeof(sdz_deflate_record)));
+    for (uint32_t i = 0; i < n; ++i)
+        if (in_len[i]) HIPCHK(hipMemcpy(hb.d_in + meta[i], in[i], in_len[i], hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(hb.d_meta, meta.data(), meta.size() * sizeof(uint64_t), hipMemcpyHostToDevice));
+    int rc = sdz_deflate_batch_device(hb.d_in, hb.d_meta, hb.d_meta + n, hb.d_out, hb.d_meta + 2 * (size_t)n,
+                                      hb.d_meta + 3 * (size_t)n, (sdz_deflate_record*)hb.d_rec, n, level,
+                                      format, fname, (uint32_t)fname_len, mtime, nullptr);
+    if (rc) return rc;
+    HIPCHK(hipDeviceSynchronize());
+    std::vector<sdz_deflate_record> r(n);
+    HIPCHK(hipMemcpy(r.data(), hb.d_rec, (size_t)n * sizeof(sdz_deflate_record), hipMemcpyDeviceToHost));
+    for (uint32_t i = 0; i < n; ++i) {
+        rec[i] = r[i];
+        uint64_t len = std::min<uint64_t>(r[i].out_len, out_cap[i]);
+        if (len && out[i]) HIPCHK(hipMemcpy(out[i], hb.d_out + meta[2 * (size_t)n + i], len, hipMemcpyDeviceToHost));
+    }
+    return SDZ_API_OK;
+}
+
+}  // extern "C"

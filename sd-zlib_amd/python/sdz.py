@@ -1,0 +1,394 @@
+"""ctypes binding of libsdz.so + a Python mirror of @stardazed/zlib's API.
+
+Mirrors the reference's public surface (src/sd-zlib.ts:39-43; typed in
+dist/sd-zlib.d.ts): inflate(), deflate(), Inflater, Deflater, adler32(),
+crc32(), mergeBuffers().  Argument validation and error messages follow
+sd-inflate.ts / sd-deflate.ts so tests read like the reference's test/index.html.
+Every codec call runs on the GPU through include/sdz.h; there is no CPU
+fallback -- without a HIP device the calls raise.
+
+Reference exception classes map to Python as: TypeError -> TypeError,
+RangeError -> ValueError, Error -> SdzError.
+"""
+import ctypes
+import math
+import os
+import time
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(os.path.dirname(_HERE), "lib", "libsdz.so")
+
+FMT_AUTO, FMT_RAW, FMT_CONTAINER = 0, 1, 2
+DEFLATE_FORMATS = {"raw": 0, "deflate": 1, "gzip": 2}
+STATUS = {0: "OK", 1: "DATA_ERROR", 2: "NEED_DICT", 3: "DICT_MISMATCH", 4: "TRUNCATED",
+          5: "OUT_OVERFLOW", 6: "TRAILING", 7: "TOO_SMALL", 8: "BAD_RECORD"}
+VERDICT = ("unchecked", "match", "mismatch")
+
+
+class SdzError(Exception):
+    """The reference's plain `Error` (sd-inflate.ts / sd-deflate.ts throw sites)."""
+
+
+class InflateRecord(ctypes.Structure):
+    _fields_ = [
+        ("status", ctypes.c_int32), ("zmsg", ctypes.c_int32), ("out_len", ctypes.c_uint64),
+        ("in_used", ctypes.c_uint64), ("stored_checksum", ctypes.c_int32),
+        ("running_checksum", ctypes.c_int32), ("stored_size", ctypes.c_int32),
+        ("mtime", ctypes.c_int32), ("name_off", ctypes.c_uint32), ("name_len", ctypes.c_uint32),
+        ("container", ctypes.c_uint8), ("complete", ctypes.c_uint8),
+        ("checksum_verdict", ctypes.c_uint8), ("size_verdict", ctypes.c_uint8),
+        ("success", ctypes.c_uint8), ("reserved", ctypes.c_uint8 * 11),
+    ]
+
+
+class DeflateRecord(ctypes.Structure):
+    _fields_ = [("status", ctypes.c_int32), ("checksum", ctypes.c_int32),
+                ("out_len", ctypes.c_uint64), ("reserved", ctypes.c_uint64)]
+
+
+assert ctypes.sizeof(InflateRecord) == 64
+assert ctypes.sizeof(DeflateRecord) == 24
+
+# every symbol include/sdz.h declares (checked by tests/test_abi.py)
+EXPORTS = [
+    "sdz_inflate_batch_device", "sdz_inflate_batch", "sdz_deflate_batch_device",
+    "sdz_deflate_batch", "sdz_deflate_bound", "sdz_adler32", "sdz_crc32",
+    "sdz_adler32_batch_device", "sdz_crc32_batch_device", "sdz_zmsg", "sdz_last_error",
+    "sdz_version", "sdz_device_count", "sdz_set_device", "sdz_device_alloc",
+    "sdz_device_free", "sdz_copy_to_device", "sdz_copy_to_host", "sdz_memset_device",
+    "sdz_copy_device_to_device",
+    "sdz_sync", "sdz_set_timing", "sdz_last_kernel_ms",
+]
+
+_lib = None
+
+
+def lib():
+    """Load libsdz.so and declare signatures (no device is touched here)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise OSError("libsdz.so not built: run `make -C sd-zlib_amd` (or __graft_entry__.build())")
+    L = ctypes.CDLL(LIB_PATH)
+    vp, u8p, u64p = ctypes.c_void_p, ctypes.c_char_p, ctypes.POINTER(ctypes.c_uint64)
+    sz, i32, u32 = ctypes.c_size_t, ctypes.c_int32, ctypes.c_uint32
+    L.sdz_inflate_batch_device.argtypes = [vp, vp, vp, vp, vp, vp, vp, u32, i32, vp, u32, vp]
+    L.sdz_inflate_batch_device.restype = ctypes.c_int
+    L.sdz_inflate_batch.argtypes = [ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(sz),
+                                    ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(sz),
+                                    ctypes.POINTER(InflateRecord), u32, i32, u8p, sz]
+    L.sdz_inflate_batch.restype = ctypes.c_int
+    L.sdz_deflate_batch_device.argtypes = [vp, vp, vp, vp, vp, vp, vp, u32, i32, i32, vp, u32, u32, vp]
+    L.sdz_deflate_batch_device.restype = ctypes.c_int
+    L.sdz_deflate_batch.argtypes = [ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(sz),
+                                    ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(sz),
+                                    ctypes.POINTER(DeflateRecord), u32, i32, i32, u8p, sz, u32]
+    L.sdz_deflate_batch.restype = ctypes.c_int
+    L.sdz_deflate_bound.argtypes = [ctypes.c_uint64, i32, u32]
+    L.sdz_deflate_bound.restype = ctypes.c_uint64
+    L.sdz_adler32.argtypes = [u8p, sz, i32]
+    L.sdz_adler32.restype = i32
+    L.sdz_crc32.argtypes = [u8p, sz, i32]
+    L.sdz_crc32.restype = i32
+    for f in ("sdz_adler32_batch_device", "sdz_crc32_batch_device"):
+        getattr(L, f).argtypes = [vp, vp, vp, vp, vp, u32, vp]
+        getattr(L, f).restype = ctypes.c_int
+    L.sdz_zmsg.argtypes = [i32]
+    L.sdz_zmsg.restype = ctypes.c_char_p
+    L.sdz_last_error.restype = ctypes.c_char_p
+    L.sdz_device_alloc.argtypes = [ctypes.c_uint64]
+    L.sdz_device_alloc.restype = vp
+    L.sdz_device_free.argtypes = [vp]
+    L.sdz_copy_to_device.argtypes = [vp, vp, ctypes.c_uint64]
+    L.sdz_copy_to_host.argtypes = [vp, vp, ctypes.c_uint64]
+    L.sdz_memset_device.argtypes = [vp, ctypes.c_int, ctypes.c_uint64]
+    L.sdz_copy_device_to_device.argtypes = [vp, vp, ctypes.c_uint64]
+    L.sdz_sync.argtypes = [vp]
+    L.sdz_set_timing.argtypes = [ctypes.c_int]
+    L.sdz_last_kernel_ms.restype = ctypes.c_float
+    L.sdz_set_device.argtypes = [ctypes.c_int]
+    _lib = L
+    return L
+
+
+def _check(rc):
+    if rc != 0:
+        raise SdzError("libsdz: %s" % lib().sdz_last_error().decode())
+
+
+def zmsg(code):
+    return lib().sdz_zmsg(code).decode()
+
+
+def device_count():
+    return lib().sdz_device_count()
+
+
+# --------------------------------------------------------------------- batches
+
+def _record_dict(r, data, src=None):
+    d = {
+        "status": STATUS.get(r.status, r.status), "zmsg": zmsg(r.zmsg), "out_len": r.out_len,
+        "in_used": r.in_used, "stored_checksum": r.stored_checksum,
+        "running_checksum": r.running_checksum, "stored_size": r.stored_size,
+        "mtime": r.mtime, "container": ("raw", "deflate", "gzip")[r.container],
+        "complete": bool(r.complete), "checksum": VERDICT[r.checksum_verdict],
+        "fileSize": VERDICT[r.size_verdict], "success": bool(r.success), "data": data,
+        "fileName": "",
+    }
+    if src is not None and r.name_len:
+        d["fileName"] = bytes(src[r.name_off:r.name_off + r.name_len]).decode("latin-1")
+    return d
+
+
+def inflate_batch(streams, out_caps=None, fmt=FMT_AUTO, dictionary=None):
+    """Decode many independent streams on the GPU (host buffers in and out)."""
+    L = lib()
+    n = len(streams)
+    streams = [bytes(s) for s in streams]
+    if out_caps is None:
+        out_caps = [max(1 << 16, 8 * len(s)) for s in streams]
+    ins = (ctypes.c_char_p * n)(*streams)
+    in_len = (ctypes.c_size_t * n)(*[len(s) for s in streams])
+    bufs = [ctypes.create_string_buffer(max(1, c)) for c in out_caps]
+    outs = (ctypes.c_void_p * n)(*[ctypes.addressof(b) for b in bufs])
+    caps = (ctypes.c_size_t * n)(*out_caps)
+    recs = (InflateRecord * n)()
+    d = bytes(dictionary) if dictionary is not None else None
+    _check(L.sdz_inflate_batch(ins, in_len, outs, caps, recs, n, fmt, d, len(d) if d else 0))
+    return [_record_dict(recs[i], bufs[i].raw[:min(recs[i].out_len, out_caps[i])], streams[i])
+            for i in range(n)]
+
+
+def inflate_one(data, fmt=FMT_AUTO, dictionary=None):
+    """One stream, growing the output capacity on SDZ_OUT_OVERFLOW."""
+    cap = max(1 << 16, 4 * len(data))
+    while True:
+        r = inflate_batch([data], [cap], fmt, dictionary)[0]
+        if r["status"] != "OUT_OVERFLOW":
+            return r
+        cap *= 4
+
+
+def deflate_batch(streams, level=6, format="deflate", file_name_latin1=b"", mtime=0):
+    L = lib()
+    n = len(streams)
+    streams = [bytes(s) for s in streams]
+    fmt = DEFLATE_FORMATS[format]
+    caps_l = [int(L.sdz_deflate_bound(len(s), fmt, len(file_name_latin1))) for s in streams]
+    ins = (ctypes.c_char_p * n)(*streams)
+    in_len = (ctypes.c_size_t * n)(*[len(s) for s in streams])
+    bufs = [ctypes.create_string_buffer(c) for c in caps_l]
+    outs = (ctypes.c_void_p * n)(*[ctypes.addressof(b) for b in bufs])
+    caps = (ctypes.c_size_t * n)(*caps_l)
+    recs = (DeflateRecord * n)()
+    fn = bytes(file_name_latin1)
+    _check(L.sdz_deflate_batch(ins, in_len, outs, caps, recs, n, level, fmt, fn or None, len(fn),
+                               mtime & 0xFFFFFFFF))
+    return [{"status": STATUS.get(recs[i].status, recs[i].status), "checksum": recs[i].checksum,
+             "data": bufs[i].raw[:recs[i].out_len]} for i in range(n)]
+
+
+# --------------------------------------------------------------------- device-resident
+
+class DeviceBuffer:
+    def __init__(self, nbytes):
+        self.nbytes = int(nbytes)
+        self.ptr = lib().sdz_device_alloc(max(1, self.nbytes))
+        if not self.ptr:
+            raise SdzError("device alloc failed: " + lib().sdz_last_error().decode())
+
+    def upload(self, data, offset=0):
+        buf = (ctypes.c_char * len(data)).from_buffer_copy(data) if not isinstance(data, ctypes.Array) else data
+        _check(lib().sdz_copy_to_device(self.ptr + offset, ctypes.addressof(buf), len(data)))
+
+    def download(self, nbytes, offset=0):
+        out = ctypes.create_string_buffer(max(1, nbytes))
+        _check(lib().sdz_copy_to_host(ctypes.addressof(out), self.ptr + offset, nbytes))
+        return out.raw[:nbytes]
+
+    def free(self):
+        if self.ptr:
+            lib().sdz_device_free(self.ptr)
+            self.ptr = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+def _u64_array(vals):
+    return (ctypes.c_uint64 * len(vals))(*vals)
+
+
+# --------------------------------------------------------------------- reference API mirror
+
+def _u8(source, what="data must be an ArrayBuffer or buffer view"):
+    if isinstance(source, (bytes, bytearray, memoryview)):
+        return bytes(source)
+    raise TypeError(what)
+
+
+def adler32(source, seed=1):
+    """adler32.ts:17-24 (signed int32; NMAX quirk of adler32.ts:67 included)."""
+    d = _u8(source, "source must be a BufferSource")
+    return lib().sdz_adler32(d, len(d), ctypes.c_int32(seed).value)
+
+
+def crc32(source, seed=0):
+    """crc32.ts:17-23 (signed int32)."""
+    d = _u8(source, "source must be a BufferSource")
+    return lib().sdz_crc32(d, len(d), ctypes.c_int32(seed).value)
+
+
+def mergeBuffers(buffers):
+    """common.ts:116-126"""
+    return b"".join(bytes(b) for b in buffers)
+
+
+_CHUNK = 16384   # zstream.ts:11 OUTPUT_BUFSIZE
+
+
+def _chunks(data):
+    return [data[i:i + _CHUNK] for i in range(0, len(data), _CHUNK)]
+
+
+def _raise_for(r):
+    st = r["status"]
+    if st == "DATA_ERROR":
+        raise SdzError("inflate error: " + r["zmsg"])
+    if st == "NEED_DICT":
+        raise SdzError("Custom dictionary required for this data")
+    if st == "DICT_MISMATCH":
+        raise SdzError("Custom dictionary is not valid for this data")
+    if st == "TRAILING":
+        raise SdzError("inflate error: trailing data after end of stream")
+
+
+class Inflater:
+    """sd-inflate.ts:54-180.  Streams are decoded one-shot on the GPU: append()
+    returns the stream's output (in 16 KiB chunks) once the accumulated input
+    holds a complete stream, [] before that; finish() reports the verdicts."""
+
+    def __init__(self, options=None):
+        options = options or {}
+        raw = options.get("raw")
+        if raw is not None and raw is not True and raw is not False:
+            raise TypeError("options.raw must be undefined or true or false")
+        self._raw = bool(raw)
+        d = options.get("dictionary")
+        if d is not None:
+            if self._raw:
+                raise ValueError("options.dictionary cannot be set when options.raw is true")
+            if not isinstance(d, (bytes, bytearray, memoryview)):
+                raise TypeError("options.dictionary must be undefined or a buffer or a buffer view")
+            d = bytes(d)
+        self._dict = d
+        self._input = b""
+        self._emitted = 0
+        self._last = None
+
+    def append(self, data):
+        chunk = _u8(data)
+        if not chunk:
+            return []
+        self._input += chunk
+        r = inflate_one(self._input, FMT_RAW if self._raw else FMT_CONTAINER, self._dict)
+        self._last = r
+        if r["status"] == "TRUNCATED":
+            return []
+        _raise_for(r)
+        out = r["data"][self._emitted:]
+        self._emitted = len(r["data"])
+        return _chunks(out)
+
+    def finish(self):
+        r = self._last
+        if r is None:
+            return {"success": False, "complete": False, "checksum": "unchecked",
+                    "fileSize": "unchecked", "fileName": "", "modDate": None}
+        return {"success": r["success"], "complete": r["complete"], "checksum": r["checksum"],
+                "fileSize": r["fileSize"], "fileName": r["fileName"],
+                "modDate": None if r["mtime"] == 0 else r["mtime"]}
+
+
+def inflate(data, dictionary=None):
+    """sd-inflate.ts:189-228"""
+    inp = _u8(data)
+    if len(inp) < 2:
+        raise SdzError("data buffer is too small")
+    m, f = inp[0], inp[1]
+    ident = (m == 0x78 and ((m << 8) + f) % 31 == 0) or (m == 0x1F and f == 0x8B)
+    if not ident and dictionary is not None:
+        raise ValueError("options.dictionary cannot be set when options.raw is true")
+    r = inflate_one(inp, FMT_CONTAINER if ident else FMT_RAW, dictionary)
+    if r["status"] != "TRUNCATED":
+        _raise_for(r)
+    if not r["success"]:
+        if not r["complete"]:
+            raise SdzError("Unexpected EOF during decompression")
+        if r["checksum"] == "mismatch":
+            raise SdzError("Data integrity check failed")
+        if r["fileSize"] == "mismatch":
+            raise SdzError("Data size check failed")
+        raise SdzError("Decompression error")
+    return r["data"]
+
+
+def _latin1(name):
+    return bytes((ord(c) if ord(c) <= 0xFF else 95) for c in name)   # sd-deflate.ts:125-130
+
+
+class Deflater:
+    """sd-deflate.ts:51-254.  append() buffers, finish() compresses the whole input
+    on the GPU; the merged output is identical to the reference's."""
+
+    def __init__(self, options=None):
+        options = options or {}
+        level = options.get("level", 6)
+        fmt = options.get("format", "deflate")
+        file_name = options.get("fileName")
+        if not isinstance(level, int) or level < 1 or level > 9:
+            raise ValueError("level must be between 1 and 9, inclusive")
+        if fmt not in ("gzip", "raw", "deflate"):
+            raise ValueError("container must be one of `raw`, `deflate`, `gzip`")
+        if file_name is not None and not isinstance(file_name, str):
+            raise TypeError("fileName must be a string")
+        if options.get("dictionary") is not None:
+            if fmt != "deflate":
+                raise TypeError("Can only provide a dictionary for `deflate` containers.")
+            raise NotImplementedError("preset dictionaries on the GPU deflate path: SURVEY §8f row 3")
+        self._level, self._fmt = level, fmt
+        self._name = _latin1(file_name or "")
+        self._input = b""
+        self._appended = False
+        self.mtime = None
+
+    def append(self, data):
+        chunk = _u8(data)
+        if not chunk:
+            return []
+        self._input += chunk
+        self._appended = True
+        return []
+
+    def finish(self):
+        if not self._appended:
+            raise SdzError("Cannot call finish before at least 1 call to append")
+        mtime = self.mtime if self.mtime is not None else int(math.floor(time.time()))
+        r = deflate_batch([self._input], self._level, self._fmt, self._name, mtime)[0]
+        if r["status"] != "OK":
+            raise SdzError("deflating: " + r["status"])
+        return _chunks(r["data"])
+
+
+def deflate(data, options=None):
+    """sd-deflate.ts:263-274"""
+    _u8(data)
+    d = Deflater(options)
+    bufs = d.append(data)
+    bufs += d.finish()
+    return mergeBuffers(bufs)
