@@ -1,0 +1,275 @@
+// index.mjs -- drop-in ES module facade of @stardazed/zlib (src/sd-zlib.ts:39-43)
+// over the MI355X engine (N-API addon -> libsdz.so -> HIP kernels).
+//
+// Same exports, argument validation, messages and auto-detection as the
+// reference (src/sd-inflate.ts, src/sd-deflate.ts, src/adler32.ts,
+// src/crc32.ts, src/common.ts); written for Node 12 (no ?. / ??).
+// Streams are decoded/encoded one-shot on the GPU: Inflater.append() returns
+// a stream's output (16 KiB chunks, zstream.ts:11) once the accumulated input
+// holds the complete stream; Deflater returns its whole output from finish().
+// Merged outputs are identical to the reference's.
+import { createRequire } from "module";
+
+const require = createRequire(import.meta.url);
+const addon = require("./sdz_napi.node");
+
+const FMT_AUTO = 0, FMT_RAW = 1, FMT_CONTAINER = 2;
+const OUTPUT_BUFSIZE = 16384;
+
+// common.ts:102-114
+function u8ArrayFromBufferSource(source) {
+	if (source instanceof ArrayBuffer) {
+		return new Uint8Array(source);
+	}
+	if (!ArrayBuffer.isView(source)) {
+		return undefined;
+	}
+	if (!(source instanceof Uint8Array)) {
+		return new Uint8Array(source.buffer, source.byteOffset, source.byteLength);
+	}
+	return source;
+}
+
+// common.ts:116-126
+export function mergeBuffers(buffers) {
+	const total = buffers.reduce((s, b) => s + b.byteLength, 0);
+	const out = new Uint8Array(total);
+	let off = 0;
+	for (const b of buffers) {
+		out.set(b, off);
+		off += b.length;
+	}
+	return out;
+}
+
+// adler32.ts:17-24
+export function adler32(source, seed) {
+	const view = u8ArrayFromBufferSource(source);
+	if (!view) {
+		throw new TypeError("source must be a BufferSource");
+	}
+	return addon.adler32(view, seed === undefined ? 1 : seed | 0);
+}
+
+// crc32.ts:17-23
+export function crc32(source, seed) {
+	const view = u8ArrayFromBufferSource(source);
+	if (!view) {
+		throw new TypeError("source must be a BufferSource");
+	}
+	return addon.crc32(view, seed === undefined ? 0 : seed | 0);
+}
+
+function chunks(data) {
+	const out = [];
+	for (let i = 0; i < data.length; i += OUTPUT_BUFSIZE) {
+		out.push(data.subarray(i, Math.min(data.length, i + OUTPUT_BUFSIZE)));
+	}
+	return out;
+}
+
+function inflateOne(input, fmt, dict) {
+	let cap = Math.max(65536, input.length * 4);
+	for (;;) {
+		const r = addon.inflateBatch([input], fmt, [cap], dict || null)[0];
+		if (r.status !== "OUT_OVERFLOW") {
+			return r;
+		}
+		cap *= 4;
+	}
+}
+
+function throwFor(r) {
+	switch (r.status) {
+	case "DATA_ERROR": throw new Error("inflate error: " + r.zmsg);
+	case "NEED_DICT": throw new Error("Custom dictionary required for this data");
+	case "DICT_MISMATCH": throw new Error("Custom dictionary is not valid for this data");
+	case "TRAILING": throw new Error("inflate error: trailing data after end of stream");
+	default: break;
+	}
+}
+
+// sd-inflate.ts:54-180
+export class Inflater {
+	constructor(options) {
+		const raw = options ? options.raw : undefined;
+		if (raw !== undefined && raw !== true && raw !== false) {
+			throw new TypeError("options.raw must be undefined or true or false");
+		}
+		this.raw = raw === undefined ? false : raw;
+		const dictionary = options ? options.dictionary : undefined;
+		if (dictionary !== undefined) {
+			if (this.raw) {
+				throw new RangeError("options.dictionary cannot be set when options.raw is true");
+			}
+			if (u8ArrayFromBufferSource(dictionary) === undefined) {
+				throw new TypeError("options.dictionary must be undefined or a buffer or a buffer view");
+			}
+			this.dict = u8ArrayFromBufferSource(dictionary);
+		}
+		this.pending = [];
+		this.emitted = 0;
+		this.last = undefined;
+	}
+
+	append(data) {
+		const chunk = u8ArrayFromBufferSource(data);
+		if (!(chunk instanceof Uint8Array)) {
+			throw new TypeError("data must be an ArrayBuffer or buffer view");
+		}
+		if (chunk.length === 0) {
+			return [];
+		}
+		this.pending.push(chunk);
+		const input = this.pending.length === 1 ? chunk : mergeBuffers(this.pending);
+		const r = inflateOne(input, this.raw ? FMT_RAW : FMT_CONTAINER, this.dict);
+		this.last = r;
+		if (r.status === "TRUNCATED") {
+			return [];
+		}
+		throwFor(r);
+		const out = r.data.subarray(this.emitted);
+		this.emitted = r.data.length;
+		return chunks(out);
+	}
+
+	finish() {
+		const r = this.last;
+		if (!r) {
+			return { success: false, complete: false, checksum: "unchecked", fileSize: "unchecked",
+				fileName: "", modDate: undefined };
+		}
+		return {
+			success: r.success,
+			complete: r.complete,
+			checksum: r.checksum,
+			fileSize: r.fileSize,
+			fileName: r.fileName,
+			modDate: r.mtime === 0 ? undefined : new Date(r.mtime * 1000)
+		};
+	}
+}
+
+// sd-inflate.ts:189-228
+export function inflate(data, dictionary) {
+	const input = u8ArrayFromBufferSource(data);
+	if (!(input instanceof Uint8Array)) {
+		throw new TypeError("data must be an ArrayBuffer or buffer view");
+	}
+	if (input.length < 2) {
+		throw new Error("data buffer is too small");
+	}
+	const method = input[0], flag = input[1];
+	const ident = (method === 0x78 && (((method << 8) + flag) % 31) === 0) ||
+		(method === 0x1F && flag === 0x8B);
+	const inflater = new Inflater({ raw: !ident, dictionary });
+	const buffers = inflater.append(input);
+	const result = inflater.finish();
+	if (!result.success) {
+		if (!result.complete) {
+			throw new Error("Unexpected EOF during decompression");
+		}
+		if (result.checksum === "mismatch") {
+			throw new Error("Data integrity check failed");
+		}
+		if (result.fileSize === "mismatch") {
+			throw new Error("Data size check failed");
+		}
+		throw new Error("Decompression error");
+	}
+	return mergeBuffers(buffers);
+}
+
+// sd-deflate.ts:51-254
+export class Deflater {
+	constructor(options) {
+		const o = options || {};
+		const level = o.level === undefined || o.level === null ? 6 : o.level;
+		const format = o.format === undefined || o.format === null ? "deflate" : o.format;
+		const dictionary = o.dictionary;
+		const fileName = o.fileName;
+		if (typeof level !== "number" || level < 1 || level > 9) {
+			throw new RangeError("level must be between 1 and 9, inclusive");
+		}
+		if (format !== "gzip" && format !== "raw" && format !== "deflate") {
+			throw new RangeError("container must be one of `raw`, `deflate`, `gzip`");
+		}
+		if (typeof fileName !== "undefined" && typeof fileName !== "string") {
+			throw new TypeError("fileName must be a string");
+		}
+		if (dictionary) {
+			if (format !== "deflate") {
+				throw new TypeError("Can only provide a dictionary for `deflate` containers.");
+			}
+			if (!u8ArrayFromBufferSource(dictionary)) {
+				throw new TypeError("dictionary must be an ArrayBuffer or buffer view");
+			}
+			throw new Error("preset dictionaries are not yet on the GPU deflate path (SURVEY.md §8f row 3)");
+		}
+		this.level = level;
+		this.format = format;
+		// sd-deflate.ts:125-130: code points above 0xFF become "_"
+		const name = Array.from(fileName || "").map(c => {
+			const cc = c.charCodeAt(0);
+			return cc > 0xff ? 95 : cc;
+		});
+		this.fileName = new Uint8Array(name);
+		this.parts = [];
+	}
+
+	append(data) {
+		const chunk = u8ArrayFromBufferSource(data);
+		if (!(chunk instanceof Uint8Array)) {
+			throw new TypeError("data must be an ArrayBuffer or buffer view");
+		}
+		if (!chunk.length) {
+			return [];
+		}
+		this.parts.push(chunk);
+		return [];
+	}
+
+	finish() {
+		if (this.parts.length === 0) {
+			throw new Error("Cannot call finish before at least 1 call to append");
+		}
+		const input = this.parts.length === 1 ? this.parts[0] : mergeBuffers(this.parts);
+		const fmt = this.format === "raw" ? 0 : this.format === "deflate" ? 1 : 2;
+		const mtime = Math.floor(Date.now() / 1000);      // sd-deflate.ts:140
+		const r = addon.deflateBatch([input], this.level, fmt, this.fileName, mtime)[0];
+		if (r.status !== "OK") {
+			throw new Error("deflating: " + r.status);
+		}
+		return chunks(r.data);
+	}
+}
+
+// sd-deflate.ts:263-274
+export function deflate(data, options) {
+	const input = u8ArrayFromBufferSource(data);
+	if (!(input instanceof Uint8Array)) {
+		throw new TypeError("data must be an ArrayBuffer or buffer view");
+	}
+	const deflater = new Deflater(options);
+	const buffers = deflater.append(data);
+	buffers.push(...deflater.finish());
+	return mergeBuffers(buffers);
+}
+
+// batched entry points (the GPU's native shape; not in the reference API)
+export function inflateBatch(streams, outCaps, format) {
+	const views = streams.map(s => u8ArrayFromBufferSource(s));
+	const caps = outCaps || views.map(v => Math.max(65536, v.length * 8));
+	return addon.inflateBatch(views, format === undefined ? FMT_AUTO : format, caps, null);
+}
+
+export function deflateBatch(streams, options) {
+	const o = options || {};
+	const views = streams.map(s => u8ArrayFromBufferSource(s));
+	const fmt = o.format === "raw" ? 0 : o.format === "gzip" ? 2 : 1;
+	return addon.deflateBatch(views, o.level || 6, fmt, new Uint8Array(0), o.mtime || 0);
+}
+
+export function deviceCount() {
+	return addon.deviceCount();
+}

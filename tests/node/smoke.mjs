@@ -1,0 +1,56 @@
+// Node smoke test of the drop-in facade, modelled on the reference's test/index.html
+// cases (inflate text/gzip/raw/parts/binary, gzip round trip).  Runs on a GPU box:
+//   node tests/node/smoke.mjs
+import { readFileSync } from "fs";
+import { fileURLToPath } from "url";
+import { dirname, join } from "path";
+import { inflate, deflate, Inflater, Deflater, adler32, crc32, mergeBuffers } from "../../sd-zlib_amd/js/index.mjs";
+
+const here = dirname(fileURLToPath(import.meta.url));
+const golden = name => new Uint8Array(readFileSync(join(here, "..", "golden", name)));
+const eq = (a, b) => a.length === b.length && a.every((v, i) => v === b[i]);
+let failures = 0;
+function check(name, cond) {
+	console.log((cond ? "ok   " : "FAIL ") + name);
+	if (!cond) failures++;
+}
+
+const text = golden("paradiselost.txt");
+check("inflate(simple.deflate)", eq(inflate(golden("simple.deflate")), golden("simple.txt")));
+check("inflate(paradiselost.deflate)", eq(inflate(golden("paradiselost.deflate")), text));
+check("inflate(simple.raw) auto-detect", eq(inflate(golden("simple.raw")), golden("simple.txt")));
+{
+	const inf = new Inflater();
+	const out = mergeBuffers(inf.append(golden("paradiselost.gz")));
+	const res = inf.finish();
+	check("Inflater gzip + verdicts", eq(out, text) && res.success && res.checksum === "match" &&
+		res.fileSize === "match" && res.fileName === "paradiselost.txt" && res.modDate instanceof Date);
+}
+{
+	const inf = new Inflater();
+	const a = inf.append(golden("paradiselost.part1.deflate"));
+	const b = inf.append(golden("paradiselost.part2.deflate"));
+	check("Inflater two parts", eq(mergeBuffers(a.concat(b)), text) && inf.finish().success);
+}
+{
+	const inf = new Inflater();
+	inf.append(golden("vertices.deflate"));
+	check("Inflater binary (vertices)", inf.finish().checksum === "match");
+}
+{
+	const d = new Deflater({ level: 6, format: "gzip", fileName: "paradiselost.orig" });
+	const comp = mergeBuffers(d.append(text).concat(d.finish()));
+	const inf = new Inflater();
+	const out = mergeBuffers(inf.append(comp));
+	check("gzip round trip", eq(out, text) && inf.finish().fileName === "paradiselost.orig");
+}
+check("deflate L6 == reference fixture", eq(deflate(text, { level: 6 }), golden("paradiselost.deflate")));
+check("adler32 KAT", adler32(golden("simple.txt")) === -1612443532);
+check("crc32 KAT", crc32(golden("simple.txt")) === 1488305224);
+let threw = "";
+try { inflate(new Uint8Array([1])); } catch (e) { threw = e.message; }
+check("error message: too small", threw === "data buffer is too small");
+threw = "";
+try { new Deflater({ level: 10 }); } catch (e) { threw = e.constructor.name + ":" + e.message; }
+check("RangeError level", threw === "RangeError:level must be between 1 and 9, inclusive");
+process.exit(failures ? 1 : 0);

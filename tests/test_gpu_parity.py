@@ -116,7 +116,7 @@ def test_c2_mini_batch_copies_of_paradiselost(paradise):
 @pytest.mark.parametrize("seed", range(3))
 def test_inflate_zlib_generated(seed):
     rng = random.Random(100 + seed)
-    streams, expect_raw = [], []
+    streams, expect_raw, originals = [], [], []
     for i in range(96):
         n = rng.choice([0, 1, 2, 3, 17, 300, 5000, 20000, 70000, 140000])
         data = text_corpus(rng, n) if i % 3 else binary_corpus(rng, n)
@@ -125,11 +125,26 @@ def test_inflate_zlib_generated(seed):
         c = zlib.compressobj(level, zlib.DEFLATED, wbits, rng.randint(1, 9), rng.choice([0, 1, 2, 3]))
         streams.append(c.compress(data) + c.flush())
         expect_raw.append(wbits < 0)
+        originals.append(data)
+    a9 = 0
     for raw in (False, True):
-        sel = [s for s, r in zip(streams, expect_raw) if r == raw]
-        gpu = run_container(sel, raw=raw)
-        for g, s in zip(gpu, sel):
-            assert_same(g, O.inflater_run([s], raw=raw), s)
+        sel = [(s, d) for s, r, d in zip(streams, expect_raw, originals) if r == raw]
+        gpu = run_container([s for s, _ in sel], raw=raw)
+        for g, (s, d) in zip(gpu, sel):
+            o = O.inflater_run([s], raw=raw)
+            if is_a9_divergence(o, g, d):
+                a9 += 1
+                continue
+            assert_same(g, o, s)
+    assert a9 < 20
+
+
+def is_a9_divergence(ora, gpu, original):
+    """SURVEY A9 (infblocks.ts:134,303-311): the reference loses a stored block's
+    remaining length when a 16 KiB output chunk fills mid-block, so it fails
+    after a whole number of chunks; the GPU decodes the ground truth."""
+    return (gpu["status"] == "OK" and gpu["data"] == original and not ora["success"]
+            and len(ora["data"]) % 16384 == 0 and original.startswith(ora["data"]))
 
 
 @pytest.mark.parametrize("fmt", ["deflate", "gzip", "raw"])
