@@ -1,0 +1,47 @@
+#!/usr/bin/env python3
+"""Lightweight driver for profiling (no torch): runs the C2 inflate batch or the
+C3 deflate batch K times through the C ABI and prints kernel times.
+  rocprofv3 --kernel-trace --stats -- python3 tools/run_c2.py --mode inflate --steps 2
+"""
+import argparse
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "sd-zlib_amd", "python"))
+sys.path.insert(0, ROOT)
+
+import sdz  # noqa: E402
+from bench import DeviceBatch, inflate_step, deflate_step  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--mode", default="inflate", choices=["inflate", "deflate"])
+    ap.add_argument("--steps", type=int, default=2)
+    ap.add_argument("--streams", type=int, default=65536)
+    ap.add_argument("--level", type=int, default=6)
+    args = ap.parse_args()
+    L = sdz.lib()
+    L.sdz_set_timing(1)
+    golden = os.path.join(ROOT, "tests", "golden")
+    text = open(os.path.join(golden, "paradiselost.txt"), "rb").read()
+    if args.mode == "inflate":
+        comp = open(os.path.join(golden, "paradiselost.deflate"), "rb").read()
+        b = DeviceBatch(sdz, comp, args.streams, len(text))
+        for i in range(args.steps):
+            ms = inflate_step(sdz, b)
+            print("inflate step %d: kernel %.3f ms, %.1f GB/s out" % (i, ms, len(text) * args.streams / ms / 1e6),
+                  flush=True)
+    else:
+        sl = text[:65536]
+        b = DeviceBatch(sdz, sl, args.streams, int(L.sdz_deflate_bound(65536, 1, 0)))
+        for i in range(args.steps):
+            ms = deflate_step(sdz, b, args.level, 1)
+            print("deflate step %d: kernel %.3f ms, %.2f GB/s in" % (i, ms, 65536 * args.streams / ms / 1e6),
+                  flush=True)
+    b.free()
+
+
+if __name__ == "__main__":
+    main()
