@@ -7,21 +7,23 @@
 //   huft_build + tree builders      src/inftree.ts:95-392
 //   Inflater.append/finish verdicts src/sd-inflate.ts:87-179
 //
-// Design: one LANE per stream.  A batch of independent streams is
-// the only parallelism DEFLATE offers without changing the format, and a wave
-// that decodes 64 streams in lock-step spends one wave-instruction per 64 symbols,
-// where a wave-per-stream decoder spends tens of wave-instructions per symbol.
-//  * Huffman decode is table-free in registers: canonical left-justified limits
-//    (15 per tree) are compared against the 15 bit-reversed peek bits; only the
-//    symbol-by-rank array lives in LDS (612 B per stream -> 256 streams per CU).
-//  * Output goes straight to its final HBM slot through an 8-byte aligned
-//    accumulator; the slot IS the LZ77 window, matches copy aligned 64-bit words
-//    (funnel shift) so stores are whole words.
-//  * adler32 / crc32 are fused into the word store (dot4 weighted sums /
-//    slicing-by-4 LDS tables): the output is never re-read for checksums.
-//  * Block headers are processed in "phases": lanes that hit end-of-block wait
-//    until 1/8 of the wave is waiting, then all waiting lanes build their tables
-//    together, so the wave does not serialise on one lane's header at a time.
+// Two phases per round:
+//  PHASE 1  k_inflate_decode -- one LANE per stream.  Huffman decoding is serial
+//    per stream, so a wave decodes 64 streams in lock-step (one wave-instruction
+//    per 64 symbols).  Decoding is table-free in registers: canonical left-
+//    justified limits (15 per tree) against 15 bit-reversed peek bits; only the
+//    rank->symbol array lives in LDS (612 B/stream, 256 streams/CU).  The lane
+//    emits 32-bit tokens (up to 3 literals, or a length/distance pair) into a
+//    per-stream ring, 16 bytes per store.  No window reads, no output writes.
+//  PHASE 2  k_inflate_resolve -- one WAVE per stream.  64 tokens at a time:
+//    wave prefix-sum of token lengths, literals and back-references whose
+//    source precedes the batch copied in parallel (the window is the stream's
+//    own output slot, recently written by this wave -> L2), in-batch
+//    references resolved in token order from an LDS stage, then the batch is
+//    written with coalesced dword stores and folded into adler32/crc32.
+// The host runs rounds (phase 1 fills up to T tokens per stream, phase 2
+// drains them) until every stream is finished.
+//
 // Reference quirks mirrored: root-bits "need" at end of
 // input (infcodes.ts:368-387), huft_build's MANY=1400 table budget, incomplete
 // single-code trees, distances before the output start reading zeros/dictionary
@@ -34,18 +36,15 @@ namespace sdz {
 #define IL_THREADS 256
 #define IL_REGION 612                 // bytes of LDS per stream (153 dwords: odd stride)
 #define IL_DSYM 576                   // distance symbols follow 288 u16 lit/len symbols
-#define IL_CRC_OFF (IL_THREADS * IL_REGION)
-#define IL_LDS (IL_CRC_OFF + 4096)
 
 __constant__ uint8_t c_border[19] = { 16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15 };
 
-enum : int { LM_TYPE = 0, LM_CODES = 1, LM_TRAILER = 2, LM_DONE = 3 };
-enum : int { CK_NONE = 0, CK_ADLER = 1, CK_CRC = 2 };
+enum : int { LM_INIT = 0, LM_TYPE = 1, LM_CODES = 2, LM_STORED = 3, LM_TRAILER = 4, LM_DONE = 5 };
 
 struct Dec {                          // canonical decoder for one tree
     uint32_t lim[16];                 // left-justified (15-bit) limit per length
     int32_t off[16];                  // rank offset per length
-    uint32_t c[5];                    // code counts per length, 3 x 10 bits per word (+dummies)
+    uint32_t c[5];                    // code counts per length, 3 x 10 bits per word
     int l, g;                         // huft_build root bits and max length
 };
 
@@ -57,19 +56,21 @@ struct Lane {
     uint64_t buf;
     int cnt;
     uint64_t loaded, total;
-    // output
-    uint64_t* ob;
-    uint64_t pos, cap, acc;
-    // checksums
-    int ck;
-    uint32_t s1, s2, crc, snap1, snap2;
+    // output accounting (bytes the tokens expand to)
+    uint64_t pos, cap;
     // state
     int mode, last, container, status, zmsg, fixed, nl, nd;
     int32_t stored_ck, stored_size, mtime;
-    uint32_t name_off, name_len;
+    uint32_t name_off, name_len, stored_left;
+    int dict_used;
     uint8_t* lens;                    // global scratch for code lengths
-    const uint8_t* dict;
-    uint32_t dict_len;
+    // token output
+    uint32_t* tb;
+    uint32_t ntok, tcap;
+    uint32_t t0, t1, t2, t3;
+    uint32_t litw;
+    int nlit;
+    bool full;
 };
 
 // ------------------------------------------------------------------ bit reader
@@ -99,90 +100,23 @@ __device__ __forceinline__ bool br_get(Lane& L, int n, uint32_t& v) {
     br_drop(L, n);
     return true;
 }
-
-// ------------------------------------------------------------------ checksums
-
-__device__ __forceinline__ void ck_word(Lane& L, uint64_t w, const uint32_t* crct) {
-    uint32_t lo = (uint32_t)w, hi = (uint32_t)(w >> 32);
-    if (L.ck == CK_ADLER) {
-        uint32_t sum = __builtin_amdgcn_udot4(lo, 0x01010101u, __builtin_amdgcn_udot4(hi, 0x01010101u, 0u, false), false);
-        uint32_t wsum = __builtin_amdgcn_udot4(lo, 0x05060708u, __builtin_amdgcn_udot4(hi, 0x01020304u, 0u, false), false);
-        uint32_t s2 = L.s2 + 8u * L.s1 + wsum;
-        uint32_t s1 = L.s1 + sum;
-        L.s1 = s1 >= 65521u ? s1 - 65521u : s1;
-        L.s2 = s2 % 65521u;
-    } else if (L.ck == CK_CRC) {
-        uint32_t c = L.crc ^ lo;
-        c = crct[768 + (c & 255)] ^ crct[512 + ((c >> 8) & 255)] ^ crct[256 + ((c >> 16) & 255)] ^ crct[c >> 24];
-        c ^= hi;
-        c = crct[768 + (c & 255)] ^ crct[512 + ((c >> 8) & 255)] ^ crct[256 + ((c >> 16) & 255)] ^ crct[c >> 24];
-        L.crc = c;
-    }
-}
-
-__device__ __forceinline__ void ck_byte(Lane& L, uint32_t b, const uint32_t* crct) {
-    if (L.ck == CK_ADLER) {
-        L.s1 += b; if (L.s1 >= 65521u) L.s1 -= 65521u;
-        L.s2 += L.s1; if (L.s2 >= 65521u) L.s2 -= 65521u;
-    } else if (L.ck == CK_CRC) {
-        L.crc = crct[(L.crc ^ b) & 255] ^ (L.crc >> 8);
-    }
-}
-
-// ------------------------------------------------------------------ output
-
-__device__ __forceinline__ void word_done(Lane& L, uint64_t widx, uint64_t w, const uint32_t* crct) {
-    L.ob[widx] = w;
-    ck_word(L, w, crct);
-    if (((widx + 1) & 2047u) == 0) { L.snap1 = L.s1; L.snap2 = L.s2; }   // 16 KiB chunk boundary
-}
-
-__device__ __forceinline__ void put_byte(Lane& L, uint32_t b, const uint32_t* crct) {
-    L.acc |= (uint64_t)b << ((L.pos & 7) * 8);
-    L.pos++;
-    if ((L.pos & 7) == 0) { word_done(L, (L.pos >> 3) - 1, L.acc, crct); L.acc = 0; }
-}
-
-// byte at output offset s (s < pos); s < 0 reads the preset dictionary / zeros (A12)
-__device__ __forceinline__ uint32_t get_byte(const Lane& L, int64_t s) {
-    if (s < 0) {
-        int64_t d = (int64_t)L.dict_len + s;
-        return d >= 0 ? (uint32_t)L.dict[d] : 0u;
-    }
-    if ((uint64_t)s >= (L.pos & ~7ull)) return (uint32_t)(L.acc >> ((s & 7) * 8)) & 255u;
-    return ((const uint8_t*)L.ob)[s];
-}
-
-__device__ __forceinline__ void copy_slow(Lane& L, uint32_t len, uint32_t dist, const uint32_t* crct) {
-    for (uint32_t k = 0; k < len; ++k) {
-        uint32_t b = get_byte(L, (int64_t)L.pos - (int64_t)dist);
-        put_byte(L, b, crct);
-    }
-}
-
-// LZ77 copy; the output slot is the window (src = already-written output)
-__device__ __forceinline__ void copy_match(Lane& L, uint32_t len, uint32_t dist, const uint32_t* crct) {
-    if (dist < 8 || (uint64_t)dist > L.pos) { copy_slow(L, len, dist, crct); return; }
-    uint64_t end = L.pos + len;
-    uint64_t W = L.pos & ~7ull;
-    uint64_t acc = L.acc;
-    while (W < end) {
-        int64_t sw = (int64_t)W - (int64_t)dist;          // source of output byte W (>= -7)
-        int64_t a = sw >> 3;
-        uint32_t sh = (uint32_t)(sw & 7) * 8;
-        uint64_t lo = a >= 0 ? L.ob[a] : 0ull;
-        uint64_t val = lo;
-        if (sh) { uint64_t hi = L.ob[a + 1]; val = (lo >> sh) | (hi << (64 - sh)); }
-        uint32_t o0 = W < L.pos ? (uint32_t)(L.pos - W) : 0u;
-        uint64_t rem = end - W;
-        uint64_t m = rem >= 8 ? ~0ull : ((1ull << (rem * 8)) - 1ull);
-        m &= ~((1ull << (o0 * 8)) - 1ull);
-        acc |= val & m;
-        if (rem >= 8) { word_done(L, W >> 3, acc, crct); acc = 0; }
-        W += 8;
-    }
-    L.acc = acc;
-    L.pos = end;
+// position the reader at bit `bitpos` of the stream starting at p
+__device__ __forceinline__ void br_init(Lane& L, const uint8_t* p, uint64_t bitpos, uint64_t total_bits) {
+    uintptr_t addr = (uintptr_t)(p + (bitpos >> 3));
+    int skip = (int)(addr & 15);
+    L.vp = (const uint4*)(addr & ~(uintptr_t)15);
+    L.cur = *L.vp++;
+    L.nxt = *L.vp++;
+    L.ncur = 4;
+    for (int k = 0; k < (skip >> 2); ++k) { L.cur.x = L.cur.y; L.cur.y = L.cur.z; L.cur.z = L.cur.w; L.ncur--; }
+    L.buf = 0;
+    L.cnt = 0;
+    br_refill(L);
+    int dropb = 8 * (skip & 3) + (int)(bitpos & 7);
+    L.buf >>= dropb;
+    L.cnt -= dropb;
+    L.loaded = bitpos + (uint64_t)L.cnt;
+    L.total = total_bits;
 }
 
 // ------------------------------------------------------------------ canonical decoders
@@ -511,7 +445,38 @@ __device__ __forceinline__ bool setup_dynamic(Lane& L, Dec& LL, Dec& DD, BuildIn
     return true;
 }
 
-// ------------------------------------------------------------------ kernel
+// ------------------------------------------------------------------ phase 1: tokens
+
+// token: bit31=0 -> literals: bits 24-25 = count-1 (1..3 bytes in bits 0-23)
+//        bit31=1 -> match: bits 16-23 = length-3, bits 0-14 = distance-1
+__device__ __forceinline__ void tok_push(Lane& L, uint32_t t) {
+    L.t0 = L.t1; L.t1 = L.t2; L.t2 = L.t3; L.t3 = t;
+    L.ntok++;
+    if ((L.ntok & 3) == 0) *(uint4*)(L.tb + L.ntok - 4) = make_uint4(L.t0, L.t1, L.t2, L.t3);
+    if (L.ntok + 3 > L.tcap) L.full = true;
+}
+__device__ __forceinline__ void tok_flush_lits(Lane& L) {
+    if (L.nlit) {
+        tok_push(L, ((uint32_t)(L.nlit - 1) << 24) | L.litw);
+        L.nlit = 0;
+        L.litw = 0;
+    }
+}
+__device__ __forceinline__ void tok_lit(Lane& L, uint32_t b) {
+    L.litw |= b << (8 * L.nlit);
+    if (++L.nlit == 3) tok_flush_lits(L);
+}
+__device__ __forceinline__ void tok_match(Lane& L, uint32_t len, uint32_t dist) {
+    tok_flush_lits(L);
+    tok_push(L, 0x80000000u | ((len - 3u) << 16) | (dist - 1u));
+}
+__device__ __forceinline__ void tok_finish(Lane& L) {
+    tok_flush_lits(L);
+    uint32_t k = L.ntok & 3u, b = L.ntok - k;
+    if (k >= 1) L.tb[b + k - 1] = L.t3;
+    if (k >= 2) L.tb[b + k - 2] = L.t2;
+    if (k >= 3) L.tb[b + k - 3] = L.t1;
+}
 
 __device__ __forceinline__ void lane_fail(Lane& L, int status, int zmsg) {
     L.status = status;
@@ -520,26 +485,21 @@ __device__ __forceinline__ void lane_fail(Lane& L, int status, int zmsg) {
 }
 
 // one block-level step for a lane that is not decoding symbols
-__device__ __forceinline__ void block_step(Lane& L, Dec& LL, Dec& DD, BuildInfo& bll, BuildInfo& bdd, uint8_t* region,
-                           const uint32_t* crct) {
+__device__ __forceinline__ void block_step(Lane& L, Dec& LL, Dec& DD, BuildInfo& bll, BuildInfo& bdd,
+                                           uint8_t* region) {
     if (L.mode == LM_TYPE) {
         uint32_t t;
         if (!br_get(L, 3, t)) { lane_fail(L, SDZ_TRUNCATED, 0); return; }
         L.last = (int)(t & 1);
         uint32_t bt = t >> 1;
-        if (bt == 0) {                                   // stored (infblocks.ts:184-196, 243-333)
+        if (bt == 0) {                                   // stored (infblocks.ts:184-196, 243-277)
             uint64_t cons = br_consumed(L);
             br_drop(L, (int)((8 - (cons & 7)) & 7));
             uint32_t lo, hi;
             if (!br_get(L, 16, lo) || !br_get(L, 16, hi)) { lane_fail(L, SDZ_TRUNCATED, 0); return; }
             if ((~hi & 0xffffu) != lo) { lane_fail(L, SDZ_DATA_ERROR, ZM_STORED_LENS); return; }
-            for (uint32_t k = 0; k < lo; ++k) {
-                uint32_t b;
-                if (!br_get(L, 8, b)) { lane_fail(L, SDZ_TRUNCATED, 0); return; }
-                if (L.pos >= L.cap) { lane_fail(L, SDZ_OUT_OVERFLOW, 0); return; }
-                put_byte(L, b, crct);
-            }
-            L.mode = L.last ? LM_TRAILER : LM_TYPE;
+            L.stored_left = lo;
+            L.mode = lo ? LM_STORED : (L.last ? LM_TRAILER : LM_TYPE);
         } else if (bt == 1) {
             setup_fixed(L, LL, DD, bll, bdd, region);
             L.mode = LM_CODES;
@@ -549,6 +509,18 @@ __device__ __forceinline__ void block_step(Lane& L, Dec& LL, Dec& DD, BuildInfo&
         } else {
             lane_fail(L, SDZ_DATA_ERROR, ZM_BLOCK_TYPE);
         }
+        return;
+    }
+    if (L.mode == LM_STORED) {                            // infblocks.ts:278-333, resumable
+        while (L.stored_left && !L.full) {
+            uint32_t b;
+            if (!br_get(L, 8, b)) { lane_fail(L, SDZ_TRUNCATED, 0); return; }
+            if (L.pos >= L.cap) { lane_fail(L, SDZ_OUT_OVERFLOW, 0); return; }
+            tok_lit(L, b);
+            L.pos++;
+            L.stored_left--;
+        }
+        if (!L.stored_left) L.mode = L.last ? LM_TRAILER : LM_TYPE;
         return;
     }
     if (L.mode == LM_TRAILER) {                          // inflate.ts:403-463
@@ -583,10 +555,9 @@ __device__ __forceinline__ void block_step(Lane& L, Dec& LL, Dec& DD, BuildInfo&
     }
 }
 
-// decode one literal/length symbol (+ its match) -- the hot loop body
+// decode one literal/length symbol (+ its distance) into a token -- the hot loop body
 __device__ __forceinline__ void decode_step(Lane& L, const Dec& LL, const Dec& DD, const BuildInfo& bll,
-                                            const BuildInfo& bdd, const uint8_t* region,
-                                            const uint32_t* crct) {
+                                            const BuildInfo& bdd, const uint8_t* region) {
     br_refill(L);
     bool careful = br_avail(L) < 64;
     uint32_t rc = __builtin_bitreverse32((uint32_t)L.buf) >> 17;
@@ -598,7 +569,8 @@ __device__ __forceinline__ void decode_step(Lane& L, const Dec& LL, const Dec& D
     br_drop(L, len);
     if (sym < 256) {
         if (L.pos >= L.cap) { lane_fail(L, SDZ_OUT_OVERFLOW, 0); return; }
-        put_byte(L, sym, crct);
+        tok_lit(L, sym);
+        L.pos++;
         return;
     }
     if (sym == 256) { L.mode = L.last ? LM_TRAILER : LM_TYPE; return; }
@@ -626,11 +598,204 @@ __device__ __forceinline__ void decode_step(Lane& L, const Dec& LL, const Dec& D
     uint32_t dist = dbase + br_peek(L, e);
     br_drop(L, e);
     if (L.pos + mlen > L.cap) { lane_fail(L, SDZ_OUT_OVERFLOW, 0); return; }
-    copy_match(L, mlen, dist, crct);
+    tok_match(L, mlen, dist);
+    L.pos += mlen;
 }
 
-// adler32.ts:34-105 over the final chunk of r bytes, seeded with the chunk-start
-// state; reproduces the unreduced sum2 when r is a multiple of NMAX
+// per-stream decode state kept in HBM between rounds
+struct DSave {
+    uint8_t region[640];
+    uint64_t bitpos, pos;
+    int32_t mode, last, container, status, zmsg, fixed, nl, nd;
+    int32_t stored_ck, stored_size, mtime;
+    uint32_t name_off, name_len, stored_left;
+    int32_t dict_used, pad;
+    Dec LL, DD;
+    BuildInfo bll, bdd;
+};
+
+// per-stream resolve state (phase 2)
+struct RSave {
+    uint64_t pos;
+    uint32_t s1, s2, crc, snap1, snap2;
+    int32_t ck;
+};
+
+// container header (inflate.ts:142-401; sd-inflate.ts:194-207 for AUTO)
+__device__ __forceinline__ void parse_container(Lane& L, const InflateArgs& A, uint64_t ilen) {
+    bool raw = A.format == SDZ_FMT_RAW;
+    if (A.format == SDZ_FMT_AUTO) {
+        if (ilen < 2) { lane_fail(L, SDZ_TOO_SMALL, 0); return; }
+        br_refill(L);
+        uint32_t b0 = br_peek(L, 8), b1 = (uint32_t)(L.buf >> 8) & 255u;
+        bool ident = (b0 == 0x78 && ((b0 << 8) + b1) % 31 == 0) || (b0 == 0x1f && b1 == 0x8b);
+        raw = !ident;
+    }
+    if (raw) return;
+    uint32_t b = 0, method = 0, flg = 0, v = 0;
+    bool gz = false;
+    if (!br_get(L, 8, b)) { lane_fail(L, SDZ_TRUNCATED, 0); return; }
+    if (b == 0x1f) {
+        if (!br_get(L, 8, b)) { lane_fail(L, SDZ_TRUNCATED, 0); return; }
+        if (b != 0x8b) { lane_fail(L, SDZ_DATA_ERROR, ZM_INVALID_GZIP_ID); return; }
+        gz = true;
+        if (!br_get(L, 8, method)) { lane_fail(L, SDZ_TRUNCATED, 0); return; }
+    } else {
+        method = b;
+    }
+    if ((method & 0xf) != 8) { lane_fail(L, SDZ_DATA_ERROR, ZM_UNKNOWN_METHOD); return; }
+    if ((method >> 4) + 8 > 15) { lane_fail(L, SDZ_DATA_ERROR, ZM_INVALID_WINDOW); return; }
+    if (!br_get(L, 8, flg)) { lane_fail(L, SDZ_TRUNCATED, 0); return; }
+    if (gz) {
+        L.container = SDZ_CONTAINER_GZIP;
+        uint32_t mt = 0;
+        for (int k = 0; k < 4; ++k) {
+            if (!br_get(L, 8, v)) { lane_fail(L, SDZ_TRUNCATED, 0); return; }
+            mt = (mt >> 8) | (v << 24);
+        }
+        L.mtime = (int32_t)mt;
+        for (int k = 0; k < 2; ++k)
+            if (!br_get(L, 8, v)) { lane_fail(L, SDZ_TRUNCATED, 0); return; }
+        if (flg & 4) { lane_fail(L, SDZ_TRUNCATED, 0); return; }   // inflate.ts:333-346 (EXTRA0 never advances)
+        if (flg & 8) {
+            L.name_off = (uint32_t)(br_consumed(L) >> 3);
+            for (;;) {
+                if (!br_get(L, 8, v)) { lane_fail(L, SDZ_TRUNCATED, 0); return; }
+                if (v == 0) break;
+                L.name_len++;
+            }
+        }
+        if (flg & 16) {
+            for (;;) {
+                if (!br_get(L, 8, v)) { lane_fail(L, SDZ_TRUNCATED, 0); return; }
+                if (v == 0) break;
+            }
+        }
+        if (flg & 2)
+            for (int k = 0; k < 2; ++k)
+                if (!br_get(L, 8, v)) { lane_fail(L, SDZ_TRUNCATED, 0); return; }
+    } else {
+        L.container = SDZ_CONTAINER_ZLIB;
+        if (((method << 8) + flg) % 31 != 0) { lane_fail(L, SDZ_DATA_ERROR, ZM_HEADER_CHECK); return; }
+        if (flg & 0x20) {
+            uint32_t id = 0;
+            for (int k = 0; k < 4; ++k) {
+                if (!br_get(L, 8, v)) { lane_fail(L, SDZ_TRUNCATED, 0); return; }
+                id = (id << 8) | v;
+            }
+            if (!A.dict) { lane_fail(L, SDZ_NEED_DICT, ZM_NEED_DICT); return; }
+            if ((int32_t)id != A.dict_adler) { lane_fail(L, SDZ_DICT_MISMATCH, 0); return; }
+            L.dict_used = 1;
+        }
+    }
+}
+
+__global__ __launch_bounds__(IL_THREADS, 1) void k_inflate_decode(InflateArgs A, uint32_t round) {
+    __shared__ __attribute__((aligned(16))) uint8_t lds[IL_THREADS * IL_REGION];
+    uint8_t* region = lds + threadIdx.x * IL_REGION;
+    uint32_t gid = blockIdx.x * IL_THREADS + threadIdx.x;
+    bool valid = gid < A.n;
+    uint32_t sid = valid ? gid : 0u;
+    DSave* S = (DSave*)A.dsave + sid;
+
+    Lane L;
+    Dec LL, DD;
+    BuildInfo bll, bdd;
+    L.mode = LM_DONE; L.status = SDZ_OK; L.zmsg = 0; L.container = SDZ_CONTAINER_RAW;
+    L.pos = 0; L.last = 0; L.fixed = 0; L.nl = L.nd = 0; L.stored_left = 0; L.dict_used = 0;
+    L.stored_ck = 0; L.stored_size = 0; L.mtime = 0; L.name_off = 0; L.name_len = 0;
+    L.cnt = 0; L.buf = 0; L.loaded = 0; L.total = 0; L.ncur = 1;
+    L.ntok = 0; L.tcap = A.round_tokens; L.t0 = L.t1 = L.t2 = L.t3 = 0; L.litw = 0; L.nlit = 0;
+    L.full = false;
+    L.cap = 0;
+    L.tb = A.tokens + (uint64_t)sid * A.round_tokens;
+    LL.l = DD.l = 0; LL.g = DD.g = 0;
+    bll.kmin = bdd.kmin = 1; bll.g = bdd.g = 0; bll.left = bdd.left = 0; bll.allzero = bdd.allzero = true;
+    bll.nlong = bdd.nlong = 0;
+    uint32_t flag = 2;                                   // 2: finished in an earlier round
+    if (valid) {
+        const uint8_t* inp = A.in + A.in_off[sid];
+        uint64_t ilen = A.in_len[sid];
+        L.cap = A.out_cap[sid];
+        L.lens = A.scratch + (uint64_t)sid * kInflateScratchPerStream;
+        if (round == 0) {
+            br_init(L, inp, 0, ilen * 8);
+            L.mode = LM_TYPE;
+            if (A.out_off[sid] & 7) lane_fail(L, SDZ_BAD_RECORD, 0);
+            else parse_container(L, A, ilen);
+            flag = 0;
+        } else if (S->mode != LM_DONE) {
+            for (int k = 0; k < IL_REGION / 4; ++k) ((uint32_t*)region)[k] = ((const uint32_t*)S->region)[k];
+            L.pos = S->pos; L.mode = S->mode; L.last = S->last; L.container = S->container;
+            L.status = S->status; L.zmsg = S->zmsg; L.fixed = S->fixed; L.nl = S->nl; L.nd = S->nd;
+            L.stored_ck = S->stored_ck; L.stored_size = S->stored_size; L.mtime = S->mtime;
+            L.name_off = S->name_off; L.name_len = S->name_len; L.stored_left = S->stored_left;
+            L.dict_used = S->dict_used;
+            LL = S->LL; DD = S->DD; bll = S->bll; bdd = S->bdd;
+            br_init(L, inp, S->bitpos, ilen * 8);
+            flag = 0;
+        }
+    }
+
+    // phases: lanes at a block boundary advance together, then decode together
+    for (;;) {
+        while (!L.full && L.mode != LM_CODES && L.mode != LM_DONE) block_step(L, LL, DD, bll, bdd, region);
+        int ncodes = __popcll(__ballot(L.mode == LM_CODES && !L.full));
+        if (ncodes == 0) break;
+        int k = ncodes >> 3;
+        int stop = ncodes - (k > 0 ? k : 1);
+        do {
+            if (L.mode == LM_CODES && !L.full) decode_step(L, LL, DD, bll, bdd, region);
+        } while (__popcll(__ballot(L.mode == LM_CODES && !L.full)) > stop);
+    }
+
+    bool more = valid && flag == 0 && L.mode != LM_DONE;
+    uint64_t mm = __ballot(more);                        // one counter update per wave
+    if (mm && (threadIdx.x & 63u) == (uint32_t)__builtin_ctzll(mm)) atomicAdd(A.active, (uint32_t)__popcll(mm));
+    if (!valid || flag == 2) {
+        if (valid) { A.ntok[sid] = 0; A.flags[sid] = 2; }
+        return;
+    }
+    tok_finish(L);
+    A.ntok[sid] = L.ntok;
+    bool done = L.mode == LM_DONE;
+    A.flags[sid] = done ? 1u : 0u;
+    for (int k = 0; k < IL_REGION / 4; ++k) ((uint32_t*)S->region)[k] = ((const uint32_t*)region)[k];
+    S->bitpos = br_consumed(L); S->pos = L.pos; S->mode = L.mode; S->last = L.last;
+    S->container = L.container; S->status = L.status; S->zmsg = L.zmsg; S->fixed = L.fixed;
+    S->nl = L.nl; S->nd = L.nd; S->stored_ck = L.stored_ck; S->stored_size = L.stored_size;
+    S->mtime = L.mtime; S->name_off = L.name_off; S->name_len = L.name_len;
+    S->stored_left = L.stored_left; S->dict_used = L.dict_used;
+    S->LL = LL; S->DD = DD; S->bll = bll; S->bdd = bdd;
+}
+
+// ------------------------------------------------------------------ phase 2: LZ77 resolve
+
+#define RS_WAVES 4
+#define RS_STAGE 4096                 // batch output budget (bytes) per wave
+
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v, uint32_t lane) {
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        uint32_t u = __shfl_up(v, o);
+        if (lane >= (uint32_t)o) v += u;
+    }
+    return v;
+}
+__device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+}
+
+// byte at output offset s of this stream (s may be negative: preset dictionary / zeros, A12)
+__device__ __forceinline__ uint32_t src_byte(const uint8_t* out, int64_t s, const uint8_t* dict, int64_t dl) {
+    if (s >= 0) return out[s];
+    int64_t d = dl + s;
+    return d >= 0 ? (uint32_t)dict[d] : 0u;
+}
+
+// adler32.ts:34-105 over r bytes seeded with the chunk-start state (NMAX quirk)
 __device__ int32_t adler_quirk_tail(const uint8_t* p, uint32_t r, uint32_t s1, uint32_t s2in) {
     uint64_t a = s1, s2 = s2in;
     uint32_t off = 0, len = r;
@@ -648,206 +813,195 @@ __device__ int32_t adler_quirk_tail(const uint8_t* p, uint32_t r, uint32_t s1, u
     return (int32_t)((uint32_t)a | ((uint32_t)s2 << 16));
 }
 
-__global__ __launch_bounds__(IL_THREADS, 1) void k_inflate(InflateArgs A) {
-    __shared__ __attribute__((aligned(16))) uint8_t lds[IL_LDS];
-    uint32_t* crct = (uint32_t*)(lds + IL_CRC_OFF);
-    // slicing-by-4 CRC tables (crc32.ts:179-214)
-    for (int n = threadIdx.x; n < 256; n += IL_THREADS) {
-        uint32_t c = (uint32_t)n;
+__global__ __launch_bounds__(RS_WAVES * 64) void k_inflate_resolve(InflateArgs A, uint32_t round) {
+    __shared__ __attribute__((aligned(16))) uint8_t stage_all[RS_WAVES][RS_STAGE + 64];
+    __shared__ uint32_t crct[256];
+    for (int v = threadIdx.x; v < 256; v += RS_WAVES * 64) {
+        uint32_t c = (uint32_t)v;
         for (int k = 0; k < 8; ++k) c = (c & 1) ? 0xedb88320u ^ (c >> 1) : c >> 1;
-        crct[n] = c;
+        crct[v] = c;
     }
     __syncthreads();
-    for (int n = threadIdx.x; n < 256; n += IL_THREADS) {
-        uint32_t c = crct[n];
-        for (int k = 1; k < 4; ++k) { c = crct[c & 255] ^ (c >> 8); crct[256 * k + n] = c; }
-    }
-    __syncthreads();
+    uint32_t lane = threadIdx.x & 63u;
+    uint32_t w = threadIdx.x >> 6;
+    uint32_t sid = blockIdx.x * RS_WAVES + w;
+    if (sid >= A.n) return;
+    uint32_t flag = A.flags[sid];
+    if (flag == 2) return;
+    uint8_t* stage = stage_all[w];
+    RSave* R = (RSave*)A.rsave + sid;
+    const DSave* S = (const DSave*)A.dsave + sid;
+    uint64_t pos;
+    uint32_t s1, s2, crc, snap1, snap2;
+    bool gz = S->container == SDZ_CONTAINER_GZIP;
+    if (round == 0) { pos = 0; s1 = 1; s2 = 0; crc = 0xffffffffu; snap1 = 1; snap2 = 0; }
+    else { pos = R->pos; s1 = R->s1; s2 = R->s2; crc = R->crc; snap1 = R->snap1; snap2 = R->snap2; }
+    uint8_t* out = A.out + A.out_off[sid];
+    const uint32_t* tk = A.tokens + (uint64_t)sid * A.round_tokens;
+    uint32_t ntok = A.ntok[sid];
+    int64_t dl = S->dict_used && A.dict ? (A.dict_len > 32767 ? 32767 : A.dict_len) : 0;
+    const uint8_t* dict = dl ? A.dict + (A.dict_len - dl) : nullptr;
 
-    uint8_t* region = lds + threadIdx.x * IL_REGION;
-    uint32_t gid = blockIdx.x * IL_THREADS + threadIdx.x;
-    bool valid = gid < A.n;
-    uint32_t sid = valid ? (A.order ? A.order[gid] : gid) : 0u;
-
-    Lane L;
-    Dec LL, DD;
-    BuildInfo bll, bdd;
-    L.mode = LM_DONE; L.status = SDZ_OK; L.zmsg = 0; L.container = SDZ_CONTAINER_RAW;
-    L.pos = 0; L.acc = 0; L.last = 0; L.fixed = 0; L.nl = L.nd = 0;
-    L.stored_ck = 0; L.stored_size = 0; L.mtime = 0; L.name_off = 0; L.name_len = 0;
-    L.s1 = 1; L.s2 = 0; L.crc = 0xffffffffu; L.snap1 = 1; L.snap2 = 0; L.ck = CK_NONE;
-    L.cnt = 0; L.buf = 0; L.loaded = 0; L.total = 0; L.ncur = 1;
-    L.dict = A.dict; L.dict_len = A.dict ? A.dict_len : 0;
-    LL.l = DD.l = 0; LL.g = DD.g = 0;
-    bll.kmin = bdd.kmin = 1; bll.g = bdd.g = 0; bll.left = bdd.left = 0; bll.allzero = bdd.allzero = true;
-    bll.nlong = bdd.nlong = 0;
-    bool dict_used = false;
-
-    if (valid) {
-        uint64_t ioff = A.in_off[sid], ilen = A.in_len[sid];
-        uint64_t ooff = A.out_off[sid];
-        L.cap = A.out_cap[sid];
-        L.ob = (uint64_t*)(A.out + ooff);
-        L.lens = A.scratch + (uint64_t)gid * kInflateScratchPerStream;
-        uintptr_t addr = (uintptr_t)(A.in + ioff);
-        int skip = (int)(addr & 15);
-        L.vp = (const uint4*)(addr & ~(uintptr_t)15);
-        L.cur = *L.vp++;
-        L.nxt = *L.vp++;
-        L.ncur = 4;
-        for (int k = 0; k < (skip >> 2); ++k) { L.cur.x = L.cur.y; L.cur.y = L.cur.z; L.cur.z = L.cur.w; L.ncur--; }
-        br_refill(L);
-        L.buf >>= 8 * (skip & 3);
-        L.cnt -= 8 * (skip & 3);
-        L.loaded = (uint64_t)L.cnt;
-        L.total = ilen * 8;
-        L.mode = LM_TYPE;
-        if (ooff & 7) lane_fail(L, SDZ_BAD_RECORD, 0);
-
-        // ---- container (inflate.ts:142-401; sd-inflate.ts:194-207 for AUTO)
-        bool raw = A.format == SDZ_FMT_RAW;
-        if (L.mode != LM_DONE && A.format == SDZ_FMT_AUTO) {
-            if (ilen < 2) lane_fail(L, SDZ_TOO_SMALL, 0);
-            else {
-                br_refill(L);
-                uint32_t b0 = br_peek(L, 8), b1 = (uint32_t)(L.buf >> 8) & 255u;
-                bool ident = (b0 == 0x78 && ((b0 << 8) + b1) % 31 == 0) || (b0 == 0x1f && b1 == 0x8b);
-                raw = !ident;
-            }
-        }
-        if (L.mode != LM_DONE && !raw) {
-            uint32_t b = 0, method = 0, flg = 0;
-            bool ok = br_get(L, 8, b);
-            bool gz = false;
-            if (ok && b == 0x1f) {
-                ok = br_get(L, 8, b);
-                if (ok && b != 0x8b) { lane_fail(L, SDZ_DATA_ERROR, ZM_INVALID_GZIP_ID); }
-                gz = true;
-                if (ok && L.mode != LM_DONE) ok = br_get(L, 8, method);
+    for (uint32_t base = 0; base < ntok;) {
+        bool inr = base + lane < ntok;
+        uint32_t t = inr ? tk[base + lane] : 0u;
+        bool ism = (t >> 31) != 0;
+        uint32_t len = !inr ? 0u : ism ? ((t >> 16) & 255u) + 3u : ((t >> 24) & 3u) + 1u;
+        uint32_t dist = (t & 0x7fffu) + 1u;
+        uint32_t head = (uint32_t)(pos & 3);
+        uint32_t incl = wave_incl_scan(len, lane);
+        uint32_t off = incl - len;
+        bool take = inr && (incl + head <= RS_STAGE || lane == 0);
+        uint64_t tm = __ballot(take);
+        uint32_t nv = (uint32_t)__popcll(tm);
+        uint32_t B = __shfl(incl, nv - 1);
+        uint32_t TB = head + B;
+        if (lane == 0 && head) *(uint32_t*)stage = *(const uint32_t*)(out + (pos & ~3ull));
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        // generation 0: literals and references to bytes before this batch
+        bool gen0 = take && (!ism || dist >= off + len);
+        if (gen0) {
+            uint8_t* dst = stage + head + off;
+            if (!ism) {
+                for (uint32_t k = 0; k < len; ++k) dst[k] = (uint8_t)(t >> (8 * k));
             } else {
-                method = b;
-            }
-            if (L.mode != LM_DONE) {
-                if (!ok) lane_fail(L, SDZ_TRUNCATED, 0);
-                else if ((method & 0xf) != 8) lane_fail(L, SDZ_DATA_ERROR, ZM_UNKNOWN_METHOD);
-                else if ((method >> 4) + 8 > 15) lane_fail(L, SDZ_DATA_ERROR, ZM_INVALID_WINDOW);
-                else if (!br_get(L, 8, flg)) lane_fail(L, SDZ_TRUNCATED, 0);
-            }
-            if (L.mode != LM_DONE && gz) {
-                L.container = SDZ_CONTAINER_GZIP;
-                uint32_t mt = 0, v;
-                for (int k = 0; k < 4 && L.mode != LM_DONE; ++k) {
-                    if (!br_get(L, 8, v)) lane_fail(L, SDZ_TRUNCATED, 0);
-                    else mt = (mt >> 8) | (v << 24);
-                }
-                L.mtime = (int32_t)mt;
-                for (int k = 0; k < 2 && L.mode != LM_DONE; ++k)
-                    if (!br_get(L, 8, v)) lane_fail(L, SDZ_TRUNCATED, 0);
-                if (L.mode != LM_DONE && (flg & 4)) {
-                    // inflate.ts:333-346: EXTRA0 never advances; all input is swallowed
-                    lane_fail(L, SDZ_TRUNCATED, 0);
-                }
-                if (L.mode != LM_DONE && (flg & 8)) {
-                    L.name_off = (uint32_t)(br_consumed(L) >> 3);
-                    while (L.mode != LM_DONE) {
-                        if (!br_get(L, 8, v)) { lane_fail(L, SDZ_TRUNCATED, 0); break; }
-                        if (v == 0) break;
-                        L.name_len++;
+                int64_t s = (int64_t)(pos + off) - (int64_t)dist;
+                if (s >= 0) {
+                    const uint8_t* sp = out + s;
+                    uint32_t a = (uint32_t)((uintptr_t)sp & 3u);
+                    const uint32_t* wp = (const uint32_t*)(sp - a);
+                    uint32_t nw = (len + a + 3) >> 2;
+                    uint32_t k = 0;
+                    for (uint32_t q = 0; q < nw; ++q) {
+                        uint32_t wv = wp[q];
+                        for (uint32_t bb = (q == 0 ? a : 0); bb < 4 && k < len; ++bb, ++k) dst[k] = (uint8_t)(wv >> (8 * bb));
                     }
-                }
-                if (L.mode != LM_DONE && (flg & 16)) {
-                    while (L.mode != LM_DONE) {
-                        if (!br_get(L, 8, v)) { lane_fail(L, SDZ_TRUNCATED, 0); break; }
-                        if (v == 0) break;
-                    }
-                }
-                if (L.mode != LM_DONE && (flg & 2)) {
-                    for (int k = 0; k < 2 && L.mode != LM_DONE; ++k)
-                        if (!br_get(L, 8, v)) lane_fail(L, SDZ_TRUNCATED, 0);
-                }
-            } else if (L.mode != LM_DONE) {
-                L.container = SDZ_CONTAINER_ZLIB;
-                if (((method << 8) + flg) % 31 != 0) lane_fail(L, SDZ_DATA_ERROR, ZM_HEADER_CHECK);
-                else if (flg & 0x20) {
-                    uint32_t id = 0, v;
-                    for (int k = 0; k < 4 && L.mode != LM_DONE; ++k) {
-                        if (!br_get(L, 8, v)) lane_fail(L, SDZ_TRUNCATED, 0);
-                        else id = (id << 8) | v;
-                    }
-                    if (L.mode != LM_DONE) {
-                        if (!A.dict) lane_fail(L, SDZ_NEED_DICT, ZM_NEED_DICT);
-                        else if ((int32_t)id != A.dict_adler) lane_fail(L, SDZ_DICT_MISMATCH, 0);
-                        else dict_used = true;
-                    }
+                } else {
+                    for (uint32_t k = 0; k < len; ++k) dst[k] = (uint8_t)src_byte(out, s + k, dict, dl);
                 }
             }
         }
-        if (!dict_used) L.dict_len = 0;
-        if (L.dict_len > 32767) { L.dict += L.dict_len - 32767; L.dict_len = 32767; }   // inflate.ts:488-491
-        L.ck = L.container == SDZ_CONTAINER_GZIP ? CK_CRC : CK_ADLER;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        // generation 1: in-batch references, in token order, one match per step
+        uint64_t rem = __ballot(take && ism && !gen0);
+        while (rem) {
+            uint32_t i = (uint32_t)__builtin_ctzll(rem);
+            rem &= rem - 1;
+            uint32_t o_i = __shfl(off, i), l_i = __shfl(len, i), d_i = __shfl(dist, i);
+            for (uint32_t k = lane; k < l_i; k += 64) {
+                uint32_t kk = d_i < l_i ? k % d_i : k;
+                int64_t sidx = (int64_t)o_i - (int64_t)d_i + (int64_t)kk;   // batch index, < o_i
+                uint32_t b;
+                if (sidx + (int64_t)head >= 0) b = stage[head + sidx];
+                else b = src_byte(out, (int64_t)pos + sidx, dict, dl);
+                stage[head + o_i + k] = (uint8_t)b;
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        }
+        // write back: coalesced dwords from the dword-aligned start
+        uint32_t nd = (TB + 3) >> 2;
+        uint32_t* dstw = (uint32_t*)(out + (pos & ~3ull));
+        const uint32_t* sw = (const uint32_t*)stage;
+        for (uint32_t q = lane; q < nd; q += 64) dstw[q] = sw[q];
+        // checksums over batch bytes stage[head .. TB)
+        if (!gz) {
+            uint32_t S1 = 0, W = 0;
+            uint64_t cut = ((pos + B) >> 14) << 14;
+            bool cross = (pos >> 14) != ((pos + B) >> 14);
+            uint32_t c = cross ? (uint32_t)(cut - pos) : 0u;
+            uint32_t Sc = 0, Wc = 0;
+            for (uint32_t q = lane; q < nd; q += 64) {
+                uint32_t wv = sw[q];
+#pragma unroll
+                for (uint32_t bb = 0; bb < 4; ++bb) {
+                    uint32_t j = 4 * q + bb;
+                    if (j >= head && j < TB) {
+                        uint32_t tix = j - head, b = (wv >> (8 * bb)) & 255u;
+                        S1 += b;
+                        W += (B - tix) * b;
+                        if (tix < c) { Sc += b; Wc += (c - tix) * b; }
+                    }
+                }
+                W %= 65521u;
+                Wc %= 65521u;
+            }
+            S1 = wave_sum(S1);
+            W = wave_sum(W);
+            if (cross) {
+                Sc = wave_sum(Sc);
+                Wc = wave_sum(Wc);
+                snap1 = (uint32_t)(((uint64_t)s1 + Sc) % 65521u);
+                snap2 = (uint32_t)(((uint64_t)s2 + (uint64_t)c * s1 + Wc) % 65521u);
+            }
+            s2 = (uint32_t)(((uint64_t)s2 + (uint64_t)B * s1 + W) % 65521u);
+            s1 = (uint32_t)(((uint64_t)s1 + S1) % 65521u);
+        } else if (lane == 0) {
+            for (uint32_t j = head; j < TB; ++j) crc = crct[(crc ^ stage[j]) & 255u] ^ (crc >> 8);
+        }
+        pos += B;
+        base += nv;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     }
-
-    // ---- phase loop: lanes at a block boundary advance together, then decode together
-    for (;;) {
-        while (L.mode != LM_CODES && L.mode != LM_DONE) block_step(L, LL, DD, bll, bdd, region, crct);
-        int ncodes = __popcll(__ballot(L.mode == LM_CODES));
-        if (ncodes == 0) break;
-        int k = ncodes >> 3;
-        int stop = ncodes - (k > 0 ? k : 1);
-        do {
-            if (L.mode == LM_CODES) decode_step(L, LL, DD, bll, bdd, region, crct);
-        } while (__popcll(__ballot(L.mode == LM_CODES)) > stop);
+    crc = __shfl(crc, 0);
+    if (lane == 0) {
+        R->pos = pos; R->s1 = s1; R->s2 = s2; R->crc = crc; R->snap1 = snap1; R->snap2 = snap2;
     }
-
-    if (!valid) return;
-    // ---- final partial word + checksums + verdicts (sd-inflate.ts:134-179)
-    uint32_t rem = (uint32_t)(L.pos & 7);
-    if (rem && L.status != SDZ_BAD_RECORD) {
-        L.ob[L.pos >> 3] = L.acc;
-        for (uint32_t k = 0; k < rem; ++k) ck_byte(L, (uint32_t)(L.acc >> (8 * k)) & 255u, crct);
-    }
-    sdz_inflate_record R;
-    R.status = L.status;
-    R.zmsg = L.zmsg;
-    R.out_len = L.pos;
-    uint64_t cons = br_consumed(L);
-    R.in_used = (cons + 7) >> 3;
-    if (R.in_used > (L.total >> 3)) R.in_used = L.total >> 3;
-    R.stored_checksum = L.stored_ck;
-    int32_t running;
-    bool have = L.pos > 0;                               // Inflater.checksum stays undefined otherwise
-    if (L.ck == CK_CRC) {
-        running = (int32_t)~L.crc;
-    } else {
-        uint32_t r = (uint32_t)(L.pos & 16383u);
-        if (r == 5552u || r == 11104u) {
-            running = adler_quirk_tail((const uint8_t*)L.ob + (L.pos - r), r, L.snap1, L.snap2);
+    if (flag != 1) return;
+    // final: record + verdicts (sd-inflate.ts:134-179)
+    if (lane == 0) {
+        sdz_inflate_record Rc;
+        Rc.status = S->status;
+        Rc.zmsg = S->zmsg;
+        Rc.out_len = pos;
+        uint64_t ib = S->bitpos;
+        uint64_t ilen = A.in_len[sid];
+        Rc.in_used = (ib + 7) >> 3;
+        if (Rc.in_used > ilen) Rc.in_used = ilen;
+        Rc.stored_checksum = S->stored_ck;
+        bool have = pos > 0;                              // Inflater.checksum stays undefined otherwise
+        int32_t running;
+        if (gz) {
+            running = (int32_t)~crc;
         } else {
-            running = (int32_t)(L.s1 | (L.s2 << 16));
+            uint32_t r = (uint32_t)(pos & 16383u);
+            if (r == 5552u || r == 11104u) running = adler_quirk_tail(out + (pos - r), r, snap1, snap2);
+            else running = (int32_t)(s1 | (s2 << 16));
         }
+        Rc.running_checksum = have ? running : 0;
+        Rc.stored_size = S->stored_size;
+        Rc.mtime = S->mtime;
+        Rc.name_off = S->name_off;
+        Rc.name_len = S->name_len;
+        Rc.container = (uint8_t)S->container;
+        bool complete = S->mode == LM_DONE && (S->status == SDZ_OK || S->status == SDZ_TRAILING);
+        Rc.complete = complete ? 1 : 0;
+        uint8_t cv = S->stored_ck == 0 ? SDZ_UNCHECKED : ((have && S->stored_ck == running) ? SDZ_MATCH : SDZ_MISMATCH);
+        uint8_t sv = S->stored_size == 0 ? SDZ_UNCHECKED
+                   : ((int64_t)S->stored_size == (int64_t)pos ? SDZ_MATCH : SDZ_MISMATCH);
+        Rc.checksum_verdict = cv;
+        Rc.size_verdict = sv;
+        Rc.success = (complete && cv != SDZ_MISMATCH && sv != SDZ_MISMATCH) ? 1 : 0;
+        for (int k = 0; k < 11; ++k) Rc.reserved[k] = 0;
+        A.rec[sid] = Rc;
     }
-    R.running_checksum = have ? running : 0;
-    R.stored_size = L.stored_size;
-    R.mtime = L.mtime;
-    R.name_off = L.name_off;
-    R.name_len = L.name_len;
-    R.container = (uint8_t)L.container;
-    bool complete = L.mode == LM_DONE && (L.status == SDZ_OK || L.status == SDZ_TRAILING);
-    R.complete = complete ? 1 : 0;
-    uint8_t cv = L.stored_ck == 0 ? SDZ_UNCHECKED : ((have && L.stored_ck == running) ? SDZ_MATCH : SDZ_MISMATCH);
-    uint8_t sv = L.stored_size == 0 ? SDZ_UNCHECKED
-               : ((int64_t)L.stored_size == (int64_t)L.pos ? SDZ_MATCH : SDZ_MISMATCH);
-    R.checksum_verdict = cv;
-    R.size_verdict = sv;
-    R.success = (complete && cv != SDZ_MISMATCH && sv != SDZ_MISMATCH) ? 1 : 0;
-    for (int k = 0; k < 11; ++k) R.reserved[k] = 0;
-    A.rec[sid] = R;
 }
 
-void launch_inflate(const InflateArgs& a, hipStream_t s) {
-    if (a.n == 0) return;
-    dim3 grid((a.n + IL_THREADS - 1) / IL_THREADS);
-    hipLaunchKernelGGL(k_inflate, grid, dim3(IL_THREADS), 0, s, a);
+uint64_t inflate_dsave_bytes() { return (sizeof(DSave) + 15) & ~(uint64_t)15; }
+uint64_t inflate_rsave_bytes() { return (sizeof(RSave) + 15) & ~(uint64_t)15; }
+
+// host driver: rounds of (decode, resolve) until no stream needs another round
+int run_inflate_rounds(const InflateArgs& a, hipStream_t s, uint32_t* host_active) {
+    if (a.n == 0) return 0;
+    dim3 g1((a.n + IL_THREADS - 1) / IL_THREADS), g2((a.n + RS_WAVES - 1) / RS_WAVES);
+    for (uint32_t round = 0;; ++round) {
+        if (hipMemsetAsync(a.active, 0, sizeof(uint32_t), s) != hipSuccess) return -1;
+        hipLaunchKernelGGL(k_inflate_decode, g1, dim3(IL_THREADS), 0, s, a, round);
+        hipLaunchKernelGGL(k_inflate_resolve, g2, dim3(RS_WAVES * 64), 0, s, a, round);
+        if (hipMemcpyAsync(host_active, a.active, sizeof(uint32_t), hipMemcpyDeviceToHost, s) != hipSuccess) return -1;
+        if (hipStreamSynchronize(s) != hipSuccess) return -1;
+        if (*host_active == 0) break;
+    }
+    return 0;
 }
 
 }  // namespace sdz

@@ -26,15 +26,24 @@ struct InflateArgs {
     const uint64_t* out_cap;
     sdz_inflate_record* rec;
     uint8_t* scratch;            // n * kInflateScratchPerStream
-    const uint32_t* order;       // lane -> stream id (LPT order), may be null
     const uint8_t* dict;         // preset dictionary (last <= 32767 bytes used), may be null
     uint32_t dict_len;
     int32_t dict_adler;          // adler32.ts of the full dictionary
     uint32_t n;
     int32_t format;
+    // round machinery (phase 1 -> tokens -> phase 2)
+    void* dsave;                 // n * decode state
+    void* rsave;                 // n * resolve state (inside the same slab, after dsave)
+    uint32_t* tokens;            // n * round_tokens
+    uint32_t round_tokens;
+    uint32_t* ntok;              // n
+    uint32_t* flags;             // n: 0 more rounds, 1 finished this round, 2 finished earlier
+    uint32_t* active;            // 1 counter
 };
 
-void launch_inflate(const InflateArgs& a, hipStream_t s);
+uint64_t inflate_dsave_bytes();  // per stream decode state
+uint64_t inflate_rsave_bytes();  // per stream resolve state
+int run_inflate_rounds(const InflateArgs& a, hipStream_t s, uint32_t* host_active);
 
 struct DeflateArgs {
     const uint8_t* in;

@@ -204,8 +204,19 @@ int sdz_inflate_batch_device(const uint8_t* in, const uint64_t* in_off, const ui
         return fail(SDZ_API_BAD_ARG, "sdz_inflate_batch_device: bad format");
     hipStream_t s = (hipStream_t)stream;
     std::lock_guard<std::mutex> lk(g_mu);
+    // per-stream slabs: code lengths | decode state | resolve state, then the token
+    // ring (round_tokens per stream, bounded to ~4 GiB in total), flags, counter
+    const uint64_t dsb = inflate_dsave_bytes(), rsb = inflate_rsave_bytes();
+    uint32_t T = (uint32_t)std::min<uint64_t>(16384, std::max<uint64_t>(1024, (4ull << 30) / (4ull * n)));
+    T &= ~3u;
+    const size_t off_ds = (size_t)n * kInflateScratchPerStream;
+    const size_t off_rs = off_ds + (size_t)n * dsb;
+    const size_t off_tk = (off_rs + (size_t)n * rsb + 255) & ~(size_t)255;
+    const size_t off_nt = off_tk + (size_t)n * T * 4;
+    size_t bytes = off_nt + (size_t)n * 8 + 256;
     void* scratch = nullptr;
-    if (int rc = g_inflate_scratch.get((size_t)n * kInflateScratchPerStream, &scratch)) return rc;
+    if (int rc = g_inflate_scratch.get(bytes, &scratch)) return rc;
+    uint8_t* base = (uint8_t*)scratch;
     int32_t dict_adler = 1;
     if (dict) {
         if (int rc = device_checksum(dict, dict_len, 0, 1, &dict_adler, s)) return rc;
@@ -213,11 +224,20 @@ int sdz_inflate_batch_device(const uint8_t* in, const uint64_t* in_off, const ui
     InflateArgs a;
     a.in = in; a.in_off = in_off; a.in_len = in_len;
     a.out = out; a.out_off = out_off; a.out_cap = out_cap;
-    a.rec = rec; a.scratch = (uint8_t*)scratch; a.order = nullptr;
+    a.rec = rec;
+    a.scratch = base;
     a.dict = dict; a.dict_len = dict_len; a.dict_adler = dict_adler;
     a.n = n; a.format = format;
+    a.dsave = base + off_ds;
+    a.rsave = base + off_rs;
+    a.tokens = (uint32_t*)(base + off_tk);
+    a.round_tokens = T;
+    a.ntok = (uint32_t*)(base + off_nt);
+    a.flags = a.ntok + n;
+    a.active = a.flags + n;
+    static thread_local uint32_t host_active = 0;
     timing_begin(s);
-    launch_inflate(a, s);
+    if (run_inflate_rounds(a, s, &host_active)) return hip_fail(hipGetLastError(), "inflate rounds");
     timing_end(s);
     HIPCHK(hipGetLastError());
     return SDZ_API_OK;
