@@ -5,7 +5,7 @@ import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 GOLDEN = os.path.join(ROOT, "tests", "golden")
-for sub in ("oracle", os.path.join("sd-zlib_amd", "python")):
+for sub in ("oracle", "tools", os.path.join("sd-zlib_amd", "python")):
     p = os.path.join(ROOT, sub)
     if p not in sys.path:
         sys.path.insert(0, p)

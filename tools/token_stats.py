@@ -60,15 +60,20 @@ def tokens(data, raw=False):
         if last: break
     return out, blocks
 
-data = open(sys.argv[1], "rb").read()
-toks, blocks = tokens(data)
-lits = sum(1 for t in toks if t[0] == "L"); ms = [t for t in toks if t[0] == "M"]
-print("blocks", blocks, "tokens", len(toks), "literals", lits, "matches", len(ms))
-print("avg match len %.2f" % (sum(m[1] for m in ms) / len(ms)), "bytes from matches", sum(m[1] for m in ms))
-dists = sorted(m[2] for m in ms)
-for q in (0.1, 0.25, 0.5, 0.75, 0.9):
-    print("dist q%.2f = %d" % (q, dists[int(q * len(dists))]))
-print("frac dist<8: %.3f" % (sum(1 for d in dists if d < 8) / len(dists)))
-lens = sorted(m[1] for m in ms)
-for q in (0.5, 0.9, 0.99):
-    print("len q%.2f = %d" % (q, lens[int(q * len(lens))]))
+def main():
+    data = open(sys.argv[1], "rb").read()
+    toks, blocks = tokens(data)
+    lits = sum(1 for t in toks if t[0] == "L"); ms = [t for t in toks if t[0] == "M"]
+    print("blocks", blocks, "tokens", len(toks), "literals", lits, "matches", len(ms))
+    print("avg match len %.2f" % (sum(m[1] for m in ms) / len(ms)), "bytes from matches", sum(m[1] for m in ms))
+    dists = sorted(m[2] for m in ms)
+    for q in (0.1, 0.25, 0.5, 0.75, 0.9):
+        print("dist q%.2f = %d" % (q, dists[int(q * len(dists))]))
+    print("frac dist<8: %.3f" % (sum(1 for d in dists if d < 8) / len(dists)))
+    lens = sorted(m[1] for m in ms)
+    for q in (0.5, 0.9, 0.99):
+        print("len q%.2f = %d" % (q, lens[int(q * len(lens))]))
+
+
+if __name__ == "__main__":
+    main()
