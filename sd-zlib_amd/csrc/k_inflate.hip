@@ -1,125 +1,192 @@
-// k_inflate.hip -- batched DEFLATE decoder for gfx950 (MI355X).
+// k_inflate.hip -- batched DEFLATE decoder for gfx950 (MI355X), phase 1 + round driver.
 //
 // Replaces the serial hot path of @stardazed/zlib's inflate:
 //   Inflate.inflate container FSM   src/inflate.ts:132-473
 //   InfBlocks.proc block FSM        src/infblocks.ts:123-628
 //   InfCodes inflate_fast / proc    src/infcodes.ts:62-676
 //   huft_build + tree builders      src/inftree.ts:95-392
-//   Inflater.append/finish verdicts src/sd-inflate.ts:87-179
+//   Inflater.append/finish verdicts src/sd-inflate.ts:87-179 (finished in k_resolve.hip)
 //
 // Two phases per round:
-//  PHASE 1  k_inflate_decode -- one LANE per stream.  Huffman decoding is serial
-//    per stream, so a wave decodes 64 streams in lock-step (one wave-instruction
-//    per 64 symbols).  Decoding is table-free in registers: canonical left-
-//    justified limits (15 per tree) against 15 bit-reversed peek bits; only the
-//    rank->symbol array lives in LDS (612 B/stream, 256 streams/CU).  The lane
-//    emits 32-bit tokens (up to 3 literals, or a length/distance pair) into a
-//    per-stream ring, 16 bytes per store.  No window reads, no output writes.
-//  PHASE 2  k_inflate_resolve -- one WAVE per stream.  64 tokens at a time:
-//    wave prefix-sum of token lengths, literals and back-references whose
-//    source precedes the batch copied in parallel (the window is the stream's
-//    own output slot, recently written by this wave -> L2), in-batch
-//    references resolved in token order from an LDS stage, then the batch is
-//    written with coalesced dword stores and folded into adler32/crc32.
-// The host runs rounds (phase 1 fills up to T tokens per stream, phase 2
-// drains them) until every stream is finished.
+//  PHASE 1  k_inflate_decode (this file) -- one LANE per stream.  Huffman decoding is
+//    serial per stream, so a wave decodes 64 streams in lock-step.  Decoding is
+//    table-free in registers: the 15 left-justified limits of a tree are compared
+//    with the 15 bit-reversed peek bits and a depth-4 select tree picks a packed
+//    per-length word (rank offset, literal threshold, shift).  Only the rank->symbol
+//    bytes live in LDS (324 B/stream).  The lane emits 32-bit tokens (up to 3
+//    literals, or a length/distance pair), staged in LDS and flushed to HBM as
+//    128-byte lines.  No window reads, no output writes.
+//  PHASE 2  k_inflate_resolve (k_resolve.hip) -- turns the tokens into bytes.
+// The host runs rounds (phase 1 fills up to T tokens per stream, phase 2 drains
+// them) until every stream is finished.
 //
 // Reference quirks mirrored: root-bits "need" at end of
 // input (infcodes.ts:368-387), huft_build's MANY=1400 table budget, incomplete
-// single-code trees, distances before the output start reading zeros/dictionary
-// (A12), the gzip FEXTRA mode that never advances (inflate.ts:343-345), the
-// Inflater's chunk-wise adler32 with the NMAX quirk (adler32.ts:67).
-#include "sdz_internal.h"
+// single-code trees, the gzip FEXTRA mode that never advances (inflate.ts:343-345).
+#include "inflate_state.h"
 
 namespace sdz {
 
 #define IL_THREADS 256
-#define IL_REGION 612                 // bytes of LDS per stream (153 dwords: odd stride)
-#define IL_DSYM 576                   // distance symbols follow 288 u16 lit/len symbols
+#define IL_TSTAGE 32                  // tokens staged in LDS per stream (one 128 B line)
+#define IL_TSTRIDE 136                // LDS bytes per stream for the token stage (8-aligned)
+#define IL_BAD_IDX 300                // rank selected by codes past lim[15]
+
+// LDS: per-stream symbol tables, then per-stream token stages (file scope, so the
+// non-inlined hot and cold functions address it as LDS, not through flat pointers)
+__shared__ __attribute__((aligned(16))) uint8_t g_region[IL_THREADS * IL_REGION];
+__shared__ __attribute__((aligned(16))) uint32_t g_stage[IL_THREADS * (IL_TSTRIDE / 4)];
+__device__ __forceinline__ uint8_t* lane_region() { return g_region + threadIdx.x * IL_REGION; }
+__shared__ __attribute__((aligned(16))) uint32_t g_ring[IL_THREADS * 18];   // 64 B + 8 B pad per lane
+__device__ __forceinline__ uint32_t* lane_stage() { return g_stage + threadIdx.x * (IL_TSTRIDE / 4); }
+__device__ __forceinline__ uint32_t* lane_ring() { return g_ring + threadIdx.x * 18; }
 
 __constant__ uint8_t c_border[19] = { 16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15 };
 
-enum : int { LM_INIT = 0, LM_TYPE = 1, LM_CODES = 2, LM_STORED = 3, LM_TRAILER = 4, LM_DONE = 5 };
+#if defined(__HIP_DEVICE_COMPILE__)
+typedef __attribute__((address_space(1))) const uint4 g_uint4;   // global_load, not flat_load
+#else
+typedef const uint4 g_uint4;
+#endif
 
-struct Dec {                          // canonical decoder for one tree
-    uint32_t lim[16];                 // left-justified (15-bit) limit per length
-    int32_t off[16];                  // rank offset per length
-    uint32_t c[5];                    // code counts per length, 3 x 10 bits per word
-    int l, g;                         // huft_build root bits and max length
+// decoder state shared by the hot symbol loop and the cold block-level code
+struct Core {
+    // 64-bit window w1:w0 of which bo bits are consumed (bo < 32 after a refill)
+    uint32_t w0, w1, bo;
+    int32_t avail;                    // input bits from bit 0 of w0 (saturated at 2^30)
+    int32_t avail0;                   // avail when the reader was positioned
+    uint64_t base_bit;                // stream bit index of w0's bit 0 at that time
+    uint32_t room, room0;             // output bytes still allowed (saturated), at positioning
+    uint64_t pos0;                    // output position at positioning
+    int mode, last, status, zmsg;
+    // token output
+    uint32_t* tb;                     // this stream's token ring in HBM
+    uint32_t* ts;                     // LDS stage
+    uint32_t ntok, tcap;
+    uint32_t litw, nlit;
+    bool full;
 };
-
-struct Lane {
-    // bit reader
-    const uint4* vp;
-    uint4 cur, nxt;
-    int ncur;
-    uint64_t buf;
-    int cnt;
-    uint64_t loaded, total;
-    // output accounting (bytes the tokens expand to)
-    uint64_t pos, cap;
-    // state
-    int mode, last, container, status, zmsg, fixed, nl, nd;
+// The symbol loop's input: w2 (next dword) is fed from a per-lane 64-byte LDS ring.
+// Once per 4 loop iterations -- a wave-uniform point -- each lane commits the 16-32
+// bytes it loaded one group earlier and issues the next loads.  Per-lane register
+// prefetch would not do: some lane's load would always be in flight into the
+// registers every lane reads, and the wave would wait on it at each refill.
+struct Hot : Core {
+    uint32_t w2, nx;                  // next dword, and the ring dword after it (read ahead)
+    uint32_t rpos, wpos;              // ring bytes consumed / committed (mod 2^32)
+    uint4 s0, s1;                     // loads in flight, committed at the next group
+    uint32_t ns;
+    g_uint4* vp;                      // next 16 input bytes to load
+    g_uint4* vend;                    // first 16-byte chunk past the input
+    uint32_t* ring;
+};
+// ... and the cold code: a plain reader plus the block-level state
+struct Lane : Core {
+    const uint32_t* dp;               // next input dword
+    int container, fixed, nl, nd;
     int32_t stored_ck, stored_size, mtime;
     uint32_t name_off, name_len, stored_left;
     int dict_used;
     uint8_t* lens;                    // global scratch for code lengths
-    // token output
-    uint32_t* tb;
-    uint32_t ntok, tcap;
-    uint32_t t0, t1, t2, t3;
-    uint32_t litw;
-    int nlit;
-    bool full;
 };
 
 // ------------------------------------------------------------------ bit reader
 
+__device__ __forceinline__ uint32_t br_peek32(const Core& L) { return __builtin_amdgcn_alignbit(L.w1, L.w0, L.bo); }
+__device__ __forceinline__ int32_t br_avail(const Core& L) { return L.avail - (int32_t)L.bo; }
+__device__ __forceinline__ uint64_t br_consumed(const Core& L) {
+    return L.base_bit + (uint64_t)(int64_t)(L.avail0 - L.avail) + L.bo;
+}
+__device__ __forceinline__ void br_drop(Core& L, uint32_t n) { L.bo += n; }
+__device__ __forceinline__ void br_setavail(Core& L, uint64_t bitpos, uint64_t total_bits) {
+    L.base_bit = bitpos - L.bo;
+    uint64_t av = total_bits - L.base_bit;
+    L.avail = (int32_t)(av > (1ull << 30) ? (1ull << 30) : av);
+    L.avail0 = L.avail;
+}
+
 __device__ __forceinline__ void br_refill(Lane& L) {
-    if (L.cnt <= 32) {
-        L.buf |= (uint64_t)L.cur.x << L.cnt;
-        L.cnt += 32;
-        L.loaded += 32;
-        L.cur.x = L.cur.y; L.cur.y = L.cur.z; L.cur.z = L.cur.w;
-        if (--L.ncur == 0) { L.cur = L.nxt; L.nxt = *L.vp++; L.ncur = 4; }
-    }
+    if (L.bo >= 32) { L.w0 = L.w1; L.w1 = *L.dp++; L.bo -= 32; L.avail -= 32; }
 }
-__device__ __forceinline__ int64_t br_avail(const Lane& L) {
-    return (int64_t)L.total - (int64_t)(L.loaded - (uint64_t)L.cnt);
-}
-__device__ __forceinline__ uint64_t br_consumed(const Lane& L) { return L.loaded - (uint64_t)L.cnt; }
-__device__ __forceinline__ uint32_t br_peek(const Lane& L, int n) {
-    return (uint32_t)L.buf & ((1u << n) - 1u);
-}
-__device__ __forceinline__ void br_drop(Lane& L, int n) { L.buf >>= n; L.cnt -= n; }
 // read n <= 24 bits; returns false (stall) if the input does not hold them
 __device__ __forceinline__ bool br_get(Lane& L, int n, uint32_t& v) {
     br_refill(L);
     if (br_avail(L) < n) return false;
-    v = br_peek(L, n);
-    br_drop(L, n);
+    v = br_peek32(L) & ((1u << n) - 1u);
+    L.bo += (uint32_t)n;
     return true;
 }
 // position the reader at bit `bitpos` of the stream starting at p
 __device__ __forceinline__ void br_init(Lane& L, const uint8_t* p, uint64_t bitpos, uint64_t total_bits) {
     uintptr_t addr = (uintptr_t)(p + (bitpos >> 3));
-    int skip = (int)(addr & 15);
-    L.vp = (const uint4*)(addr & ~(uintptr_t)15);
-    L.cur = *L.vp++;
-    L.nxt = *L.vp++;
-    L.ncur = 4;
-    for (int k = 0; k < (skip >> 2); ++k) { L.cur.x = L.cur.y; L.cur.y = L.cur.z; L.cur.z = L.cur.w; L.ncur--; }
-    L.buf = 0;
-    L.cnt = 0;
-    br_refill(L);
-    int dropb = 8 * (skip & 3) + (int)(bitpos & 7);
-    L.buf >>= dropb;
-    L.cnt -= dropb;
-    L.loaded = bitpos + (uint64_t)L.cnt;
-    L.total = total_bits;
+    L.dp = (const uint32_t*)(addr & ~(uintptr_t)3);
+    L.w0 = L.dp[0];
+    L.w1 = L.dp[1];
+    L.dp += 2;
+    L.bo = (uint32_t)(8 * (addr & 3) + (bitpos & 7));
+    br_setavail(L, bitpos, total_bits);
 }
 
-// ------------------------------------------------------------------ canonical decoders
+// branch-free: the ring dword that becomes w2 was read one refill earlier (nx), and
+// the next one is read unconditionally, so no refill waits on an LDS read
+__device__ __forceinline__ void br_refill(Hot& L) {
+    bool c = L.bo >= 32;
+    L.w0 = c ? L.w1 : L.w0;
+    L.w1 = c ? L.w2 : L.w1;
+    L.w2 = c ? L.nx : L.w2;
+    L.rpos += c ? 4u : 0u;
+    L.avail -= c ? 32 : 0;
+    L.bo &= 31u;
+    L.nx = L.ring[(L.rpos >> 2) & 15u];
+}
+// the wave-uniform ring step (see struct Hot); keeps >= 24 bytes in the ring,
+// enough for the 4 iterations of up to 48 bits each that follow
+__device__ __forceinline__ void ring_step(Hot& L) {
+    if (L.ns) {
+        uint32_t k = (L.wpos >> 2) & 15u;
+        *(uint2*)(L.ring + k) = make_uint2(L.s0.x, L.s0.y);
+        *(uint2*)(L.ring + k + 2) = make_uint2(L.s0.z, L.s0.w);
+        L.wpos += 16;
+        if (L.ns == 2) {
+            k = (L.wpos >> 2) & 15u;
+            *(uint2*)(L.ring + k) = make_uint2(L.s1.x, L.s1.y);
+            *(uint2*)(L.ring + k + 2) = make_uint2(L.s1.z, L.s1.w);
+            L.wpos += 16;
+        }
+        L.ns = 0;
+    }
+    uint32_t lvl = L.wpos - L.rpos;
+    if (lvl <= 48 && L.vp < L.vend) {
+        L.s0 = *L.vp++;
+        L.ns = 1;
+        if (lvl <= 32 && L.vp < L.vend) { L.s1 = *L.vp++; L.ns = 2; }
+    }
+}
+__device__ __forceinline__ void br_init(Hot& L, const uint8_t* p, uint64_t bitpos, uint64_t total_bits,
+                                        uint32_t* ring) {
+    uintptr_t addr = (uintptr_t)(p + (bitpos >> 3));
+    g_uint4* vp = (g_uint4*)(addr & ~(uintptr_t)15);
+    uint4 c0 = vp[0], c1 = vp[1], c2 = vp[2], c3 = vp[3];
+    L.ring = ring;
+    // ring rows are 8-byte aligned (72-byte stride): written as pairs of uint2
+    *(uint2*)(ring + 0) = make_uint2(c0.x, c0.y); *(uint2*)(ring + 2) = make_uint2(c0.z, c0.w);
+    *(uint2*)(ring + 4) = make_uint2(c1.x, c1.y); *(uint2*)(ring + 6) = make_uint2(c1.z, c1.w);
+    *(uint2*)(ring + 8) = make_uint2(c2.x, c2.y); *(uint2*)(ring + 10) = make_uint2(c2.z, c2.w);
+    *(uint2*)(ring + 12) = make_uint2(c3.x, c3.y); *(uint2*)(ring + 14) = make_uint2(c3.z, c3.w);
+    L.vp = vp + 4;
+    L.wpos = 64;
+    uint32_t k = (uint32_t)((addr >> 2) & 3);
+    L.w0 = ring[k];
+    L.w1 = ring[k + 1];
+    L.w2 = ring[k + 2];
+    L.nx = ring[k + 3];
+    L.rpos = 4 * (k + 3);
+    L.ns = 0;
+    L.bo = (uint32_t)(8 * (addr & 3) + (bitpos & 7));
+    br_setavail(L, bitpos, total_bits);
+}
+
+// ------------------------------------------------------------------ canonical trees
 
 __device__ __forceinline__ uint32_t cnt_get(const uint32_t (&c)[5], int len) {
     int i = (len - 1) / 3;
@@ -133,18 +200,23 @@ __device__ __forceinline__ void cnt_add(uint32_t (&c)[5], int len, uint32_t v) {
     c[3] += i == 3 ? d : 0u; c[4] += i == 4 ? d : 0u;
 }
 
-// rank of the code whose bit-reversed 15-bit prefix is rc; sets len (16 = invalid)
-__device__ __forceinline__ int32_t hdecode(uint32_t rc, const Dec& D, int& len) {
-    int l = 1;
-    int32_t off = D.off[1];
-#pragma unroll
-    for (int k = 1; k < 15; ++k) {
-        bool ge = rc >= D.lim[k];
-        l = ge ? k + 1 : l;
-        off = ge ? D.off[k + 1] : off;
-    }
-    len = l;
-    return off + (int32_t)(rc >> (15 - l));
+// packed word for the code (rank offset / threshold / shift) whose 15-bit bit-reversed
+// prefix is rc: pk[1 + #{k : rc >= lim[k]}], as a depth-4 select tree (limits ascend)
+__device__ __forceinline__ uint32_t tsel(const HTree& T, uint32_t rc) {
+    bool g1 = rc >= T.lim[1], g2 = rc >= T.lim[2], g3 = rc >= T.lim[3], g4 = rc >= T.lim[4];
+    bool g5 = rc >= T.lim[5], g6 = rc >= T.lim[6], g7 = rc >= T.lim[7], g8 = rc >= T.lim[8];
+    bool g9 = rc >= T.lim[9], g10 = rc >= T.lim[10], g11 = rc >= T.lim[11], g12 = rc >= T.lim[12];
+    bool g13 = rc >= T.lim[13], g14 = rc >= T.lim[14], g15 = rc >= T.lim[15];
+    uint32_t a1 = g1 ? T.pk[2] : T.pk[1], a3 = g3 ? T.pk[4] : T.pk[3];
+    uint32_t a5 = g5 ? T.pk[6] : T.pk[5], a7 = g7 ? T.pk[8] : T.pk[7];
+    uint32_t a9 = g9 ? T.pk[10] : T.pk[9], a11 = g11 ? T.pk[12] : T.pk[11];
+    uint32_t a13 = g13 ? T.pk[14] : T.pk[13], a15 = g15 ? T.pk[16] : T.pk[15];
+    uint32_t b1 = g2 ? a3 : a1, b5 = g6 ? a7 : a5, b9 = g10 ? a11 : a9, b13 = g14 ? a15 : a13;
+    uint32_t c1 = g4 ? b5 : b1, c9 = g12 ? b13 : b9;
+    return g8 ? c9 : c1;
+}
+__device__ __forceinline__ int32_t pk_rank(uint32_t v, uint32_t rc) {
+    return (int32_t)(v >> 16) + (int32_t)(rc >> (v & 15u)) - 32768;
 }
 
 // inftree.ts:212-296 table allocation replayed over counts only (c[g] already holds
@@ -197,78 +269,6 @@ __device__ __noinline__ int huft_replay(uint32_t c0, uint32_t c1, uint32_t c2, u
     return entries;
 }
 
-// code-length statistics of lens[0..n) -> D (counts, Kraft), returns kraft remainder at 15
-struct BuildInfo { int kmin, g, left, nlong; bool allzero; };
-
-__device__ __forceinline__ void finish_dec(Dec& D, const BuildInfo& bi) {
-    uint32_t code = 0;
-    int32_t idx = 0;
-#pragma unroll
-    for (int L = 1; L <= 15; ++L) {
-        uint32_t cl = cnt_get(D.c, L);
-        D.lim[L] = (code + cl) << (15 - L);
-        D.off[L] = idx - (int32_t)code;
-        idx += (int32_t)cl;
-        code = (code + cl) << 1;
-    }
-    D.lim[0] = 0; D.off[0] = 0;
-}
-
-// counts + Kraft for n lengths read from global memory
-__device__ __forceinline__ BuildInfo count_lens(Dec& D, const uint8_t* lens, int n, int root) {
-    D.c[0] = D.c[1] = D.c[2] = D.c[3] = D.c[4] = 0;
-    for (int s = 0; s < n; ++s) {
-        int len = lens[s];
-        if (len) cnt_add(D.c, len, 1u);
-    }
-    BuildInfo bi;
-    int left = 1, kmin = 16, g = 0;
-#pragma unroll
-    for (int L = 1; L <= 15; ++L) {
-        int cl = (int)cnt_get(D.c, L);
-        left = 2 * left - cl;
-        if (cl) { kmin = kmin > L ? L : kmin; g = L; }
-    }
-    bi.allzero = g == 0;
-    bi.kmin = kmin;
-    bi.g = g;
-    bi.left = left;
-    int l = root;
-    if (!bi.allzero) { if (l < kmin) l = kmin; if (l > g) l = g; }
-    D.l = l;
-    D.g = g;
-    int nlong = 0;
-#pragma unroll
-    for (int L = 1; L <= 15; ++L) nlong += L > l ? (int)cnt_get(D.c, L) : 0;
-    bi.nlong = nlong;
-    return bi;
-}
-
-// place symbols 0..n-1 into the LDS rank array (canonical order)
-template <typename T>
-__device__ __forceinline__ void place_syms(const Dec& D, const uint8_t* lens, int n, T* out) {
-    uint32_t nx[5] = { 0, 0, 0, 0, 0 };
-    uint32_t idx = 0;
-#pragma unroll
-    for (int L = 1; L <= 15; ++L) { cnt_add(nx, L, idx); idx += cnt_get(D.c, L); }
-    for (int s = 0; s < n; ++s) {
-        int len = lens[s];
-        if (len) {
-            uint32_t k = cnt_get(nx, len);
-            out[k] = (T)s;
-            cnt_add(nx, len, 1u);
-        }
-    }
-}
-
-// add huft_build's dummy codes (c[g] += y) so the replay sees its counts
-__device__ __forceinline__ void add_dummies(Dec& D, const BuildInfo& bi) {
-    if (!bi.allzero && bi.left > 0) cnt_add(D.c, bi.g, (uint32_t)(bi.left >> (15 - bi.g)));
-}
-__device__ __forceinline__ void remove_dummies(Dec& D, const BuildInfo& bi) {
-    if (!bi.allzero && bi.left > 0) cnt_add(D.c, bi.g, (uint32_t)(-(int)(bi.left >> (15 - bi.g))));
-}
-
 // bits the reference's slow path needs before it can resolve this code (infcodes.ts:367-387)
 __device__ __noinline__ int dec_need(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t c4,
                                      int l, int kmin, int g, int left, int len, int rank) {
@@ -279,8 +279,71 @@ __device__ __noinline__ int dec_need(uint32_t c0, uint32_t c1, uint32_t c2, uint
     huft_replay(c[0], c[1], c[2], c[3], c[4], kmin, g, l, rank, &need);
     return need;
 }
-#define DEC_NEED(D, B, len, rank) \
-    dec_need((D).c[0], (D).c[1], (D).c[2], (D).c[3], (D).c[4], (D).l, (B).kmin, (B).g, (B).left, (len), (rank))
+#define TREE_NEED(T, len, rank) \
+    dec_need((T).c[0], (T).c[1], (T).c[2], (T).c[3], (T).c[4], (T).l, (T).kmin, (T).g, (T).left, (len), (rank))
+
+// limits and packed words from the counts; hs = per-length literal threshold
+// (packed like the counts) or null for the distance tree
+template <bool LIT>
+__device__ __forceinline__ void finish_tree(Tree& T, const uint32_t (&hs)[5]) {
+    uint32_t code = 0;
+    int32_t idx = 0;
+#pragma unroll
+    for (int L = 1; L <= 15; ++L) {
+        uint32_t cl = cnt_get(T.c, L);
+        T.lim[L] = (code + cl) << (15 - L);
+        int32_t off = idx - (int32_t)code;
+        uint32_t h = LIT ? cnt_get(hs, L) : 511u;
+        T.pk[L] = ((uint32_t)(off + 32768) << 16) | (h << 4) | (uint32_t)(15 - L);
+        idx += (int32_t)cl;
+        code = (code + cl) << 1;
+    }
+    T.lim[0] = 0;
+    T.pk[0] = 0;
+    T.pk[16] = ((uint32_t)(IL_BAD_IDX + 32768) << 16) | 15u;   // threshold 0: never a literal
+}
+
+// counts + Kraft remainder for n lengths read from global memory
+__device__ __forceinline__ void count_lens(Tree& T, const uint8_t* lens, int n, int root) {
+    T.c[0] = T.c[1] = T.c[2] = T.c[3] = T.c[4] = 0;
+    for (int s = 0; s < n; ++s) {
+        int len = lens[s];
+        if (len) cnt_add(T.c, len, 1u);
+    }
+    int left = 1, kmin = 16, g = 0;
+#pragma unroll
+    for (int L = 1; L <= 15; ++L) {
+        int cl = (int)cnt_get(T.c, L);
+        left = 2 * left - cl;
+        if (cl) { kmin = kmin > L ? L : kmin; g = L; }
+    }
+    T.kmin = kmin;
+    T.g = g;
+    T.left = left;
+    int l = root;
+    if (g != 0) { if (l < kmin) l = kmin; if (l > g) l = g; }
+    T.l = l;
+}
+
+// rank -> symbol bytes in canonical order; returns the per-length literal thresholds
+// (lit/len: symbols >= 256 are stored as sym - 256 after the literals of their length)
+__device__ __forceinline__ void place_syms(const Tree& T, const uint8_t* lens, int n, uint8_t* out,
+                                           uint32_t (&hs)[5]) {
+    uint32_t nx[5] = { 0, 0, 0, 0, 0 };
+    uint32_t idx = 0;
+#pragma unroll
+    for (int L = 1; L <= 15; ++L) { cnt_add(nx, L, idx); idx += cnt_get(T.c, L); }
+    int nlit = n < 256 ? n : 256;
+    for (int s = 0; s < nlit; ++s) {
+        int len = lens[s];
+        if (len) { out[cnt_get(nx, len)] = (uint8_t)s; cnt_add(nx, len, 1u); }
+    }
+    hs[0] = nx[0]; hs[1] = nx[1]; hs[2] = nx[2]; hs[3] = nx[3]; hs[4] = nx[4];
+    for (int s = nlit; s < n; ++s) {
+        int len = lens[s];
+        if (len) { out[cnt_get(nx, len)] = (uint8_t)(s - 256); cnt_add(nx, len, 1u); }
+    }
+}
 
 // upper bound on the entries huft_build allocates for these counts (dummies included)
 __device__ __forceinline__ int table_bound(const uint32_t (&c)[5], int l, int g) {
@@ -299,34 +362,83 @@ __device__ __forceinline__ int table_bound(const uint32_t (&c)[5], int l, int g)
     if (g > 2 * l) { int s2 = g - 2 * l < l ? g - 2 * l : l; b += nlong2 * (1 << s2); }
     return b;
 }
+__device__ __forceinline__ void with_dummies(const Tree& T, uint32_t (&c)[5]) {
+    c[0] = T.c[0]; c[1] = T.c[1]; c[2] = T.c[2]; c[3] = T.c[3]; c[4] = T.c[4];
+    if (T.g != 0 && T.left > 0) cnt_add(c, T.g, (uint32_t)(T.left >> (15 - T.g)));
+}
+
+// ------------------------------------------------------------------ tokens
+
+// token: bit31=0 -> literals: bits 24-25 = count-1 (1..3 bytes in bits 0-23)
+//        bit31=1 -> match: bits 16-23 = length-3, bits 0-14 = distance-1
+__device__ __forceinline__ void tok_flush_stage(Core& L) {       // 32 staged tokens -> HBM
+    const uint2* s = (const uint2*)L.ts;
+    uint4* d = (uint4*)(L.tb + (L.ntok - IL_TSTAGE));
+#pragma unroll
+    for (int k = 0; k < IL_TSTAGE / 4; ++k) {
+        uint2 a = s[2 * k], b = s[2 * k + 1];
+        d[k] = make_uint4(a.x, a.y, b.x, b.y);
+    }
+}
+__device__ __forceinline__ void tok_push(Core& L, uint32_t t) {
+    uint32_t k = L.ntok & (IL_TSTAGE - 1);
+    L.ts[k] = t;
+    L.ntok++;
+    if (k == IL_TSTAGE - 1) tok_flush_stage(L);
+}
+__device__ __forceinline__ void tok_flush_lits(Core& L) {
+    if (L.nlit) {
+        tok_push(L, ((L.nlit - 1u) << 24) | L.litw);
+        L.nlit = 0;
+        L.litw = 0;
+    }
+}
+__device__ __forceinline__ void tok_lit(Core& L, uint32_t b) {
+    L.litw |= b << (8 * L.nlit);
+    if (++L.nlit == 3) tok_flush_lits(L);
+}
+__device__ __forceinline__ void tok_match(Core& L, uint32_t len, uint32_t dist) {
+    tok_flush_lits(L);
+    tok_push(L, 0x80000000u | ((len - 3u) << 16) | (dist - 1u));
+}
+__device__ __forceinline__ void tok_finish(Core& L) {
+    tok_flush_lits(L);
+    uint32_t k = L.ntok & (IL_TSTAGE - 1), b = L.ntok - k;
+    for (uint32_t j = 0; j < k; ++j) L.tb[b + j] = L.ts[j];
+}
+
+__device__ __forceinline__ void lane_fail(Core& L, int status, int zmsg) {
+    L.status = status;
+    L.zmsg = zmsg;
+    L.mode = LM_DONE;
+}
 
 // ------------------------------------------------------------------ block setup
 
-__device__ __forceinline__ void setup_fixed(Lane& L, Dec& LL, Dec& DD, BuildInfo& bll, BuildInfo& bdd, uint8_t* region) {
-    uint16_t* ll = (uint16_t*)region;
-    uint8_t* dd = region + IL_DSYM;
+__device__ __forceinline__ void setup_fixed(Lane& L, Tree& LL, Tree& DD, uint8_t* region) {
+    // ranks: 256..279 (7 bits) | 0..143, 280..287 (8 bits) | 144..255 (9 bits)
     int k = 0;
-    for (int s = 256; s < 280; ++s) ll[k++] = (uint16_t)s;
-    for (int s = 0; s < 144; ++s) ll[k++] = (uint16_t)s;
-    for (int s = 280; s < 288; ++s) ll[k++] = (uint16_t)s;
-    for (int s = 144; s < 256; ++s) ll[k++] = (uint16_t)s;
-    for (int s = 0; s < 30; ++s) dd[s] = (uint8_t)s;
-    LL.c[0] = 0; LL.c[1] = 0; LL.c[2] = 0; LL.c[3] = 0; LL.c[4] = 0;
+    for (int s = 0; s < 24; ++s) region[k++] = (uint8_t)s;
+    for (int s = 0; s < 144; ++s) region[k++] = (uint8_t)s;
+    for (int s = 24; s < 32; ++s) region[k++] = (uint8_t)s;
+    for (int s = 144; s < 256; ++s) region[k++] = (uint8_t)s;
+    for (int s = 0; s < 30; ++s) region[IL_DSYM + s] = (uint8_t)s;
+    LL.c[0] = LL.c[1] = LL.c[2] = LL.c[3] = LL.c[4] = 0;
     cnt_add(LL.c, 7, 24); cnt_add(LL.c, 8, 152); cnt_add(LL.c, 9, 112);
-    LL.l = 9; LL.g = 9;
-    DD.c[0] = 0; DD.c[1] = 0; DD.c[2] = 0; DD.c[3] = 0; DD.c[4] = 0;
+    LL.l = 9; LL.kmin = 7; LL.g = 9; LL.left = 0;
+    DD.c[0] = DD.c[1] = DD.c[2] = DD.c[3] = DD.c[4] = 0;
     cnt_add(DD.c, 5, 30);
-    DD.l = 5; DD.g = 5;
-    bll.kmin = 7; bll.g = 9; bll.left = 0; bll.allzero = false; bll.nlong = 0;
-    bdd.kmin = 5; bdd.g = 5; bdd.left = 2 << 10; bdd.allzero = false; bdd.nlong = 0;
-    finish_dec(LL, bll);
-    finish_dec(DD, bdd);
+    DD.l = 5; DD.kmin = 5; DD.g = 5; DD.left = 2 << 10;
+    uint32_t hs[5] = { 0, 0, 0, 0, 0 };                  // literal thresholds: 0 | 168 | 288
+    cnt_add(hs, 8, 168); cnt_add(hs, 9, 288);
+    finish_tree<true>(LL, hs);
+    finish_tree<false>(DD, hs);
     L.fixed = 1;
 }
 
 // infblocks.ts:334-551 + inftree.ts:313-379.  Returns false when the lane stopped
 // (error or stall); L.status/zmsg say which.
-__device__ __forceinline__ bool setup_dynamic(Lane& L, Dec& LL, Dec& DD, BuildInfo& bll, BuildInfo& bdd, uint8_t* region) {
+__device__ __forceinline__ bool setup_dynamic(Lane& L, Tree& LL, Tree& DD, uint8_t* region) {
     uint32_t t;
     if (!br_get(L, 14, t)) { L.status = SDZ_TRUNCATED; return false; }
     if ((t & 0x1f) > 29 || ((t >> 5) & 0x1f) > 29) { L.status = SDZ_DATA_ERROR; L.zmsg = ZM_TOO_MANY_SYMS; return false; }
@@ -383,7 +495,7 @@ __device__ __forceinline__ bool setup_dynamic(Lane& L, Dec& LL, Dec& DD, BuildIn
     while (idx < total) {
         br_refill(L);
         if (br_avail(L) < g7) { L.status = SDZ_TRUNCATED; return false; }
-        uint32_t rc = __builtin_bitreverse32((uint32_t)L.buf) >> 25;
+        uint32_t rc = __builtin_bitreverse32(br_peek32(L)) >> 25;
         int len = 1;
         int32_t off = off7[1];
 #pragma unroll
@@ -391,7 +503,7 @@ __device__ __forceinline__ bool setup_dynamic(Lane& L, Dec& LL, Dec& DD, BuildIn
         // g7 == 1 with one code: both patterns read the last entry written (inftree.ts:265-267)
         uint32_t c = cls[(g7 == 1 && left > 0) ? 0 : (off + (int32_t)(rc >> (7 - len)))];
         if (g7 == 1 && left > 0) len = 1;
-        br_drop(L, len);
+        br_drop(L, (uint32_t)len);
         if (c < 16) {
             L.lens[idx++] = (uint8_t)c;
             prev = (int)c;
@@ -409,84 +521,45 @@ __device__ __forceinline__ bool setup_dynamic(Lane& L, Dec& LL, Dec& DD, BuildIn
     }
     // literal/length tree (inftree.ts:344-357); the MANY=1400 budget of huft_build
     // (inftree.ts:242) is checked exactly only when a cheap bound cannot rule it out
-    bll = count_lens(LL, L.lens, nl, 9);
-    if (bll.left < 0) { L.status = SDZ_DATA_ERROR; L.zmsg = ZM_LL_OVERSUB; return false; }
-    bdd = count_lens(DD, L.lens + nl, nd, 6);
+    count_lens(LL, L.lens, nl, 9);
+    if (LL.left < 0) { L.status = SDZ_DATA_ERROR; L.zmsg = ZM_LL_OVERSUB; return false; }
+    count_lens(DD, L.lens + nl, nd, 6);
+    bool llzero = LL.g == 0, ddzero = DD.g == 0;
     int ent_ll = 0, ent_d = 0;
-    Dec tl = LL, td = DD;
-    add_dummies(tl, bll);
-    add_dummies(td, bdd);
+    uint32_t tl[5], td[5];
+    with_dummies(LL, tl);
+    with_dummies(DD, td);
     bool exact = false;
-    if (!bll.allzero) ent_ll = table_bound(tl.c, LL.l, bll.g);
-    if (!bdd.allzero && bdd.left >= 0) ent_d = table_bound(td.c, DD.l, bdd.g);
+    if (!llzero) ent_ll = table_bound(tl, LL.l, LL.g);
+    if (!ddzero && DD.left >= 0) ent_d = table_bound(td, DD.l, DD.g);
     if (ent_ll + ent_d > 1400) {
         exact = true;
         int dummy;
-        if (!bll.allzero)
-            ent_ll = huft_replay(tl.c[0], tl.c[1], tl.c[2], tl.c[3], tl.c[4], bll.kmin, bll.g, LL.l, -1, &dummy);
+        if (!llzero) ent_ll = huft_replay(tl[0], tl[1], tl[2], tl[3], tl[4], LL.kmin, LL.g, LL.l, -1, &dummy);
     }
-    if (!bll.allzero && ent_ll > 1400) { L.status = SDZ_DATA_ERROR; L.zmsg = ZM_LL_OVERSUB; return false; }
-    if (bll.allzero || (bll.left > 0 && bll.g != 1)) { L.status = SDZ_DATA_ERROR; L.zmsg = ZM_LL_INCOMPLETE; return false; }
+    if (!llzero && ent_ll > 1400) { L.status = SDZ_DATA_ERROR; L.zmsg = ZM_LL_OVERSUB; return false; }
+    if (llzero || (LL.left > 0 && LL.g != 1)) { L.status = SDZ_DATA_ERROR; L.zmsg = ZM_LL_INCOMPLETE; return false; }
     // distance tree (inftree.ts:359-376)
-    if (bdd.left < 0) { L.status = SDZ_DATA_ERROR; L.zmsg = ZM_D_OVERSUB; return false; }
-    if (exact && !bdd.allzero) {
+    if (DD.left < 0) { L.status = SDZ_DATA_ERROR; L.zmsg = ZM_D_OVERSUB; return false; }
+    if (exact && !ddzero) {
         int dummy;
-        ent_d = huft_replay(td.c[0], td.c[1], td.c[2], td.c[3], td.c[4], bdd.kmin, bdd.g, DD.l, -1, &dummy);
+        ent_d = huft_replay(td[0], td[1], td[2], td[3], td[4], DD.kmin, DD.g, DD.l, -1, &dummy);
     }
-    if (!bdd.allzero && ent_ll + ent_d > 1400) { L.status = SDZ_DATA_ERROR; L.zmsg = ZM_D_OVERSUB; return false; }
-    if (!bdd.allzero && bdd.left > 0 && bdd.g != 1) { L.status = SDZ_DATA_ERROR; L.zmsg = ZM_D_INCOMPLETE; return false; }
-    if (bdd.allzero && nl > 257) { L.status = SDZ_DATA_ERROR; L.zmsg = ZM_D_EMPTY; return false; }
-    finish_dec(LL, bll);
-    finish_dec(DD, bdd);
-    place_syms<uint16_t>(LL, L.lens, nl, (uint16_t*)region);
-    place_syms<uint8_t>(DD, L.lens + nl, nd, region + IL_DSYM);
+    if (!ddzero && ent_ll + ent_d > 1400) { L.status = SDZ_DATA_ERROR; L.zmsg = ZM_D_OVERSUB; return false; }
+    if (!ddzero && DD.left > 0 && DD.g != 1) { L.status = SDZ_DATA_ERROR; L.zmsg = ZM_D_INCOMPLETE; return false; }
+    if (ddzero && nl > 257) { L.status = SDZ_DATA_ERROR; L.zmsg = ZM_D_EMPTY; return false; }
+    uint32_t hs[5], hd[5];
+    place_syms(LL, L.lens, nl, region, hs);
+    place_syms(DD, L.lens + nl, nd, region + IL_DSYM, hd);
+    finish_tree<true>(LL, hs);
+    finish_tree<false>(DD, hd);
     L.nl = nl; L.nd = nd;
     L.fixed = 0;
     return true;
 }
 
-// ------------------------------------------------------------------ phase 1: tokens
-
-// token: bit31=0 -> literals: bits 24-25 = count-1 (1..3 bytes in bits 0-23)
-//        bit31=1 -> match: bits 16-23 = length-3, bits 0-14 = distance-1
-__device__ __forceinline__ void tok_push(Lane& L, uint32_t t) {
-    L.t0 = L.t1; L.t1 = L.t2; L.t2 = L.t3; L.t3 = t;
-    L.ntok++;
-    if ((L.ntok & 3) == 0) *(uint4*)(L.tb + L.ntok - 4) = make_uint4(L.t0, L.t1, L.t2, L.t3);
-    if (L.ntok + 3 > L.tcap) L.full = true;
-}
-__device__ __forceinline__ void tok_flush_lits(Lane& L) {
-    if (L.nlit) {
-        tok_push(L, ((uint32_t)(L.nlit - 1) << 24) | L.litw);
-        L.nlit = 0;
-        L.litw = 0;
-    }
-}
-__device__ __forceinline__ void tok_lit(Lane& L, uint32_t b) {
-    L.litw |= b << (8 * L.nlit);
-    if (++L.nlit == 3) tok_flush_lits(L);
-}
-__device__ __forceinline__ void tok_match(Lane& L, uint32_t len, uint32_t dist) {
-    tok_flush_lits(L);
-    tok_push(L, 0x80000000u | ((len - 3u) << 16) | (dist - 1u));
-}
-__device__ __forceinline__ void tok_finish(Lane& L) {
-    tok_flush_lits(L);
-    uint32_t k = L.ntok & 3u, b = L.ntok - k;
-    if (k >= 1) L.tb[b + k - 1] = L.t3;
-    if (k >= 2) L.tb[b + k - 2] = L.t2;
-    if (k >= 3) L.tb[b + k - 3] = L.t1;
-}
-
-__device__ __forceinline__ void lane_fail(Lane& L, int status, int zmsg) {
-    L.status = status;
-    L.zmsg = zmsg;
-    L.mode = LM_DONE;
-}
-
 // one block-level step for a lane that is not decoding symbols
-__device__ __forceinline__ void block_step(Lane& L, Dec& LL, Dec& DD, BuildInfo& bll, BuildInfo& bdd,
-                                           uint8_t* region) {
+__device__ __forceinline__ void block_step(Lane& L, Tree& LL, Tree& DD, uint8_t* region) {
     if (L.mode == LM_TYPE) {
         uint32_t t;
         if (!br_get(L, 3, t)) { lane_fail(L, SDZ_TRUNCATED, 0); return; }
@@ -494,17 +567,17 @@ __device__ __forceinline__ void block_step(Lane& L, Dec& LL, Dec& DD, BuildInfo&
         uint32_t bt = t >> 1;
         if (bt == 0) {                                   // stored (infblocks.ts:184-196, 243-277)
             uint64_t cons = br_consumed(L);
-            br_drop(L, (int)((8 - (cons & 7)) & 7));
+            br_drop(L, (uint32_t)((8 - (cons & 7)) & 7));
             uint32_t lo, hi;
             if (!br_get(L, 16, lo) || !br_get(L, 16, hi)) { lane_fail(L, SDZ_TRUNCATED, 0); return; }
             if ((~hi & 0xffffu) != lo) { lane_fail(L, SDZ_DATA_ERROR, ZM_STORED_LENS); return; }
             L.stored_left = lo;
             L.mode = lo ? LM_STORED : (L.last ? LM_TRAILER : LM_TYPE);
         } else if (bt == 1) {
-            setup_fixed(L, LL, DD, bll, bdd, region);
+            setup_fixed(L, LL, DD, region);
             L.mode = LM_CODES;
         } else if (bt == 2) {
-            if (!setup_dynamic(L, LL, DD, bll, bdd, region)) { L.mode = LM_DONE; return; }
+            if (!setup_dynamic(L, LL, DD, region)) { L.mode = LM_DONE; return; }
             L.mode = LM_CODES;
         } else {
             lane_fail(L, SDZ_DATA_ERROR, ZM_BLOCK_TYPE);
@@ -515,17 +588,19 @@ __device__ __forceinline__ void block_step(Lane& L, Dec& LL, Dec& DD, BuildInfo&
         while (L.stored_left && !L.full) {
             uint32_t b;
             if (!br_get(L, 8, b)) { lane_fail(L, SDZ_TRUNCATED, 0); return; }
-            if (L.pos >= L.cap) { lane_fail(L, SDZ_OUT_OVERFLOW, 0); return; }
+            if (L.room == 0) { lane_fail(L, SDZ_OUT_OVERFLOW, 0); return; }
             tok_lit(L, b);
-            L.pos++;
+            L.room--;
             L.stored_left--;
+            if (L.ntok + 3 > L.tcap) L.full = true;
         }
         if (!L.stored_left) L.mode = L.last ? LM_TRAILER : LM_TYPE;
         return;
     }
     if (L.mode == LM_TRAILER) {                          // inflate.ts:403-463
         uint64_t cons = br_consumed(L);
-        br_drop(L, (int)((8 - (cons & 7)) & 7));          // WASH + blocks.reset()
+        br_refill(L);
+        br_drop(L, (uint32_t)((8 - (cons & 7)) & 7));   // WASH + blocks.reset()
         if (L.container == SDZ_CONTAINER_ZLIB) {
             uint32_t v = 0;
             for (int k = 0; k < 4; ++k) {
@@ -555,79 +630,117 @@ __device__ __forceinline__ void block_step(Lane& L, Dec& LL, Dec& DD, BuildInfo&
     }
 }
 
-// decode one literal/length symbol (+ its distance) into a token -- the hot loop body
-__device__ __forceinline__ void decode_step(Lane& L, const Dec& LL, const Dec& DD, const BuildInfo& bll,
-                                            const BuildInfo& bdd, const uint8_t* region) {
-    br_refill(L);
-    bool careful = br_avail(L) < 64;
-    uint32_t rc = __builtin_bitreverse32((uint32_t)L.buf) >> 17;
-    int len;
-    int32_t idx = hdecode(rc, LL, len);
-    if (careful && br_avail(L) < DEC_NEED(LL, bll, len, idx)) { lane_fail(L, SDZ_TRUNCATED, 0); return; }
-    if (rc >= LL.lim[15]) { lane_fail(L, SDZ_DATA_ERROR, ZM_INVALID_LITLEN); return; }
-    uint32_t sym = ((const uint16_t*)region)[idx];
-    br_drop(L, len);
-    if (sym < 256) {
-        if (L.pos >= L.cap) { lane_fail(L, SDZ_OUT_OVERFLOW, 0); return; }
-        tok_lit(L, sym);
-        L.pos++;
-        return;
-    }
-    if (sym == 256) { L.mode = L.last ? LM_TRAILER : LM_TYPE; return; }
-    if (sym > 285) { lane_fail(L, SDZ_DATA_ERROR, ZM_INVALID_LITLEN); return; }
-    uint32_t li = sym - 257;
-    int e;
-    uint32_t base;
-    if (li < 8) { e = 0; base = li + 3; }
-    else if (li == 28) { e = 0; base = 258; }
-    else { e = (int)((li - 4) >> 2); base = ((4u + (li & 3u)) << e) + 3u; }
-    if (careful && br_avail(L) < e) { lane_fail(L, SDZ_TRUNCATED, 0); return; }
-    uint32_t mlen = base + br_peek(L, e);
-    br_drop(L, e);
-    br_refill(L);
-    rc = __builtin_bitreverse32((uint32_t)L.buf) >> 17;
-    idx = hdecode(rc, DD, len);
-    if (careful && br_avail(L) < DEC_NEED(DD, bdd, len, idx)) { lane_fail(L, SDZ_TRUNCATED, 0); return; }
-    if (rc >= DD.lim[15]) { lane_fail(L, SDZ_DATA_ERROR, ZM_INVALID_DIST); return; }
-    uint32_t ds = region[IL_DSYM + idx];
-    br_drop(L, len);
-    uint32_t dbase;
-    if (ds < 4) { e = 0; dbase = ds + 1; }
-    else { e = (int)((ds - 2) >> 1); dbase = ((2u + (ds & 1u)) << e) + 1u; }
-    if (careful && br_avail(L) < e) { lane_fail(L, SDZ_TRUNCATED, 0); return; }
-    uint32_t dist = dbase + br_peek(L, e);
-    br_drop(L, e);
-    if (L.pos + mlen > L.cap) { lane_fail(L, SDZ_OUT_OVERFLOW, 0); return; }
-    tok_match(L, mlen, dist);
-    L.pos += mlen;
+// length symbol (1..29 = sym - 256) -> base length and extra bits (infcodes.ts:27-35)
+__device__ __forceinline__ uint32_t len_base(uint32_t li, uint32_t& e) {
+    uint32_t k = li - 1u;                                 // 0..28
+    e = (k < 8u || k == 28u) ? 0u : (k - 4u) >> 2;
+    return k < 8u ? k + 3u : k == 28u ? 258u : ((4u + (k & 3u)) << e) + 3u;
+}
+// distance symbol 0..29 -> base distance and extra bits (infcodes.ts:37-46)
+__device__ __forceinline__ uint32_t dist_base(uint32_t ds, uint32_t& e) {
+    e = ds < 4u ? 0u : (ds - 2u) >> 1;
+    return ds < 4u ? ds + 1u : ((2u + (ds & 1u)) << e) + 1u;
 }
 
-// per-stream decode state kept in HBM between rounds
-struct DSave {
-    uint8_t region[640];
-    uint64_t bitpos, pos;
-    int32_t mode, last, container, status, zmsg, fixed, nl, nd;
-    int32_t stored_ck, stored_size, mtime;
-    uint32_t name_off, name_len, stored_left;
-    int32_t dict_used, pad;
-    Dec LL, DD;
-    BuildInfo bll, bdd;
-};
+// decode one literal/length symbol (+ its distance): the fast path, taken while at
+// least 64 input bits remain (one step reads at most 48)
+__device__ __forceinline__ void fast_step(Hot& L, const HTree& LL, const HTree& DD, const uint8_t* region) {
+    br_refill(L);
+    uint32_t pw = br_peek32(L);
+    uint32_t rc = __builtin_bitreverse32(pw) >> 17;
+    uint32_t v = tsel(LL, rc);
+    int32_t idx = pk_rank(v, rc);
+    uint32_t len = 15u - (v & 15u);
+    uint32_t b = region[idx];
+    L.bo += len;
+    if (idx < (int32_t)((v >> 4) & 511u)) {               // literal
+        if (L.room == 0) { lane_fail(L, SDZ_OUT_OVERFLOW, 0); return; }
+        L.room--;
+        tok_lit(L, b);
+        return;
+    }
+    if (b - 1u >= 29u || idx >= 288) {                    // end of block, or invalid code
+        if (b == 0 && idx < 288) L.mode = L.last ? LM_TRAILER : LM_TYPE;
+        else lane_fail(L, SDZ_DATA_ERROR, ZM_INVALID_LITLEN);
+        return;
+    }
+    uint32_t e;
+    uint32_t mlen = len_base(b, e);
+    mlen += (pw >> len) & ((1u << e) - 1u);
+    L.bo += e;
+    br_refill(L);
+    pw = br_peek32(L);
+    rc = __builtin_bitreverse32(pw) >> 17;
+    v = tsel(DD, rc);
+    idx = pk_rank(v, rc);
+    len = 15u - (v & 15u);
+    uint32_t ds = region[IL_DSYM + idx];
+    if (idx >= (int32_t)((v >> 4) & 511u)) { lane_fail(L, SDZ_DATA_ERROR, ZM_INVALID_DIST); return; }
+    uint32_t dist = dist_base(ds, e);
+    dist += (pw >> len) & ((1u << e) - 1u);
+    L.bo += len + e;
+    if (L.room < mlen) { lane_fail(L, SDZ_OUT_OVERFLOW, 0); return; }
+    L.room -= mlen;
+    tok_match(L, mlen, dist);
+}
 
-// per-stream resolve state (phase 2)
-struct RSave {
-    uint64_t pos;
-    uint32_t s1, s2, crc, snap1, snap2;
-    int32_t ck;
-};
+// the same with the reference's end-of-input behaviour: every read checks the
+// bits available, and a code is only resolved once the reference's table walk
+// would have had the bits it asks for (infcodes.ts:367-387)
+__device__ __forceinline__ void slow_step(Lane& L, const Tree& LL, const Tree& DD, const uint8_t* region) {
+    br_refill(L);
+    uint32_t pw = br_peek32(L);
+    uint32_t rc = __builtin_bitreverse32(pw) >> 17;
+    uint32_t v = tsel(LL, rc);
+    bool bad = rc >= LL.lim[15];
+    int32_t idx = bad ? (int32_t)(LL.pk[15] >> 16) - 32768 + (int32_t)rc : pk_rank(v, rc);
+    int len = bad ? 15 : 15 - (int)(v & 15u);
+    if (br_avail(L) < TREE_NEED(LL, len, idx)) { lane_fail(L, SDZ_TRUNCATED, 0); return; }
+    if (bad) { lane_fail(L, SDZ_DATA_ERROR, ZM_INVALID_LITLEN); return; }
+    uint32_t b = region[idx];
+    L.bo += (uint32_t)len;
+    if (idx < (int32_t)((v >> 4) & 511u)) {
+        if (L.room == 0) { lane_fail(L, SDZ_OUT_OVERFLOW, 0); return; }
+        L.room--;
+        tok_lit(L, b);
+        return;
+    }
+    if (b == 0) { L.mode = L.last ? LM_TRAILER : LM_TYPE; return; }
+    if (b > 29) { lane_fail(L, SDZ_DATA_ERROR, ZM_INVALID_LITLEN); return; }
+    uint32_t e;
+    uint32_t mlen = len_base(b, e);
+    if (br_avail(L) < (int)e) { lane_fail(L, SDZ_TRUNCATED, 0); return; }
+    mlen += (pw >> len) & ((1u << e) - 1u);
+    L.bo += e;
+    br_refill(L);
+    pw = br_peek32(L);
+    rc = __builtin_bitreverse32(pw) >> 17;
+    v = tsel(DD, rc);
+    bad = rc >= DD.lim[15];
+    idx = bad ? (int32_t)(DD.pk[15] >> 16) - 32768 + (int32_t)rc : pk_rank(v, rc);
+    len = bad ? 15 : 15 - (int)(v & 15u);
+    if (br_avail(L) < TREE_NEED(DD, len, idx)) { lane_fail(L, SDZ_TRUNCATED, 0); return; }
+    if (bad) { lane_fail(L, SDZ_DATA_ERROR, ZM_INVALID_DIST); return; }
+    uint32_t ds = region[IL_DSYM + idx];
+    L.bo += (uint32_t)len;
+    uint32_t dist = dist_base(ds, e);
+    if (br_avail(L) < (int)e) { lane_fail(L, SDZ_TRUNCATED, 0); return; }
+    dist += (pw >> len) & ((1u << e) - 1u);
+    L.bo += e;
+    if (L.room < mlen) { lane_fail(L, SDZ_OUT_OVERFLOW, 0); return; }
+    L.room -= mlen;
+    tok_match(L, mlen, dist);
+}
 
 // container header (inflate.ts:142-401; sd-inflate.ts:194-207 for AUTO)
-__device__ __forceinline__ void parse_container(Lane& L, const InflateArgs& A, uint64_t ilen) {
-    bool raw = A.format == SDZ_FMT_RAW;
-    if (A.format == SDZ_FMT_AUTO) {
+__device__ __forceinline__ void parse_container(Lane& L, int32_t format, int32_t has_dict,
+                                                int32_t dict_adler, uint64_t ilen) {
+    bool raw = format == SDZ_FMT_RAW;
+    if (format == SDZ_FMT_AUTO) {
         if (ilen < 2) { lane_fail(L, SDZ_TOO_SMALL, 0); return; }
         br_refill(L);
-        uint32_t b0 = br_peek(L, 8), b1 = (uint32_t)(L.buf >> 8) & 255u;
+        uint32_t pw = br_peek32(L);
+        uint32_t b0 = pw & 255u, b1 = (pw >> 8) & 255u;
         bool ident = (b0 == 0x78 && ((b0 << 8) + b1) % 31 == 0) || (b0 == 0x1f && b1 == 0x8b);
         raw = !ident;
     }
@@ -683,308 +796,191 @@ __device__ __forceinline__ void parse_container(Lane& L, const InflateArgs& A, u
                 if (!br_get(L, 8, v)) { lane_fail(L, SDZ_TRUNCATED, 0); return; }
                 id = (id << 8) | v;
             }
-            if (!A.dict) { lane_fail(L, SDZ_NEED_DICT, ZM_NEED_DICT); return; }
-            if ((int32_t)id != A.dict_adler) { lane_fail(L, SDZ_DICT_MISMATCH, 0); return; }
+            if (!has_dict) { lane_fail(L, SDZ_NEED_DICT, ZM_NEED_DICT); return; }
+            if ((int32_t)id != dict_adler) { lane_fail(L, SDZ_DICT_MISMATCH, 0); return; }
             L.dict_used = 1;
         }
     }
 }
 
+// ------------------------------------------------------------------ cold path
+
+// Everything but the symbol loop -- container header, block headers and tree
+// building, stored blocks, the careful end-of-input symbol path -- on the state
+// parked in the stream's DSave.  Returns when the lane can use the fast path
+// again, has finished, or has filled its token ring.  Not inlined: its registers
+// are its own, so the symbol loop keeps a small register footprint.
+__device__ __noinline__ void cold_run(DSave* S, const uint8_t* inp, uint64_t ilen, uint64_t cap,
+                                      uint32_t* tb, uint32_t tcap, uint8_t* lens, int32_t format, int32_t has_dict,
+                                      int32_t dict_adler, uint32_t init) {
+    Lane L;
+    Tree LL, DD;
+    uint8_t* region = lane_region();
+    L.tb = tb; L.ts = lane_stage(); L.tcap = tcap; L.lens = lens;
+    if (init) {
+        L.mode = LM_TYPE; L.last = 0; L.status = SDZ_OK; L.zmsg = 0; L.container = SDZ_CONTAINER_RAW;
+        L.fixed = 0; L.nl = L.nd = 0; L.stored_ck = 0; L.stored_size = 0; L.mtime = 0;
+        L.name_off = 0; L.name_len = 0; L.stored_left = 0; L.dict_used = 0;
+        L.ntok = 0; L.litw = 0; L.nlit = 0; L.full = false;
+        br_init(L, inp, 0, ilen * 8);
+        L.pos0 = 0;
+        LL.l = DD.l = 0; LL.g = DD.g = 0; LL.kmin = DD.kmin = 1; LL.left = DD.left = 0;
+        parse_container(L, format, has_dict, dict_adler, ilen);
+    } else {
+        L.mode = S->mode; L.last = S->last; L.status = S->status; L.zmsg = S->zmsg;
+        L.container = S->container; L.fixed = S->fixed; L.nl = S->nl; L.nd = S->nd;
+        L.stored_ck = S->stored_ck; L.stored_size = S->stored_size; L.mtime = S->mtime;
+        L.name_off = S->name_off; L.name_len = S->name_len; L.stored_left = S->stored_left;
+        L.dict_used = S->dict_used;
+        L.ntok = S->ntok; L.litw = S->litw; L.nlit = S->nlit; L.full = S->full != 0;
+        br_init(L, inp, S->bitpos, ilen * 8);
+        L.pos0 = S->pos;
+        LL = S->LL; DD = S->DD;
+    }
+    uint64_t r = cap - L.pos0;
+    L.room = L.room0 = (uint32_t)(r > 0x7fffffffull ? 0x7fffffffull : r);
+    for (;;) {
+        if (L.full || L.mode == LM_DONE) break;
+        if (L.mode == LM_CODES) {
+            if (br_avail(L) >= 64) break;
+            slow_step(L, LL, DD, region);
+            if (L.ntok + 3 > L.tcap) L.full = true;
+        } else {
+            block_step(L, LL, DD, region);
+            if (L.avail0 - L.avail > (1 << 28)) L.full = true;   // keeps the saturated counter exact
+        }
+    }
+    S->bitpos = br_consumed(L); S->pos = L.pos0 + (L.room0 - L.room);
+    S->mode = L.mode; S->last = L.last; S->status = L.status; S->zmsg = L.zmsg;
+    S->container = L.container; S->fixed = L.fixed; S->nl = L.nl; S->nd = L.nd;
+    S->stored_ck = L.stored_ck; S->stored_size = L.stored_size; S->mtime = L.mtime;
+    S->name_off = L.name_off; S->name_len = L.name_len; S->stored_left = L.stored_left;
+    S->dict_used = L.dict_used;
+    S->ntok = L.ntok; S->litw = L.litw; S->nlit = L.nlit; S->full = L.full ? 1 : 0;
+    S->LL = LL; S->DD = DD;
+}
+
+// ------------------------------------------------------------------ hot path
+
+__device__ __forceinline__ void hot_load(Hot& H, HTree& LL, HTree& DD, const DSave* S,
+                                         const uint8_t* inp, uint64_t ilen, uint64_t cap) {
+    br_init(H, inp, S->bitpos, ilen * 8, lane_ring());
+    H.vend = (g_uint4*)(((uintptr_t)(inp + ilen) + 15) & ~(uintptr_t)15);
+    H.pos0 = S->pos;
+    uint64_t r = cap - H.pos0;
+    H.room = H.room0 = (uint32_t)(r > 0x7fffffffull ? 0x7fffffffull : r);
+    H.mode = S->mode; H.last = S->last; H.status = S->status; H.zmsg = S->zmsg;
+    H.ntok = S->ntok; H.litw = S->litw; H.nlit = S->nlit; H.full = S->full != 0;
+    LL = (const HTree&)S->LL;
+    DD = (const HTree&)S->DD;
+}
+__device__ __forceinline__ void hot_save(const Hot& H, DSave* S) {
+    S->bitpos = br_consumed(H); S->pos = H.pos0 + (H.room0 - H.room);
+    S->mode = H.mode; S->last = H.last; S->status = H.status; S->zmsg = H.zmsg;
+    S->ntok = H.ntok; S->litw = H.litw; S->nlit = H.nlit; S->full = H.full ? 1 : 0;
+}
+__device__ __forceinline__ bool hot_ready(const Hot& H) {
+    return H.mode == LM_CODES && !H.full && br_avail(H) >= 64;
+}
+
+// one epoch of the symbol loop: every lane with `hot` set decodes until no more
+// than `stop` lanes of the wave can continue.  Not inlined, so that its register
+// allocation is not shaped by the cold call in the caller's loop.
+__device__ __noinline__ void hot_epoch(DSave* S, const uint8_t* inp, uint64_t ilen, uint64_t cap,
+                                       uint32_t* tb, uint32_t tcap, bool hot, int stop) {
+    Hot H;
+    HTree LL, DD;
+    const uint8_t* region = lane_region();
+    H.mode = LM_DONE; H.full = true; H.ntok = 0; H.tcap = tcap; H.tb = tb; H.ts = lane_stage();
+    H.avail = 0; H.bo = 0;
+    if (hot) hot_load(H, LL, DD, S, inp, ilen, cap);
+    do {
+        if (hot) ring_step(H);
+#pragma unroll 1
+        for (int rep = 0; rep < 4; ++rep) {
+            if (hot_ready(H)) {
+                fast_step(H, LL, DD, region);
+                if (H.ntok + 3 > H.tcap) H.full = true;
+            }
+        }
+    } while (__popcll(__ballot(hot_ready(H))) > stop);
+    if (hot) hot_save(H, S);
+}
+
 __global__ __launch_bounds__(IL_THREADS, 1) void k_inflate_decode(InflateArgs A, uint32_t round) {
-    __shared__ __attribute__((aligned(16))) uint8_t lds[IL_THREADS * IL_REGION];
-    uint8_t* region = lds + threadIdx.x * IL_REGION;
+    uint8_t* region = lane_region();
+    uint32_t* ts = lane_stage();
     uint32_t gid = blockIdx.x * IL_THREADS + threadIdx.x;
     bool valid = gid < A.n;
     uint32_t sid = valid ? gid : 0u;
     DSave* S = (DSave*)A.dsave + sid;
-
-    Lane L;
-    Dec LL, DD;
-    BuildInfo bll, bdd;
-    L.mode = LM_DONE; L.status = SDZ_OK; L.zmsg = 0; L.container = SDZ_CONTAINER_RAW;
-    L.pos = 0; L.last = 0; L.fixed = 0; L.nl = L.nd = 0; L.stored_left = 0; L.dict_used = 0;
-    L.stored_ck = 0; L.stored_size = 0; L.mtime = 0; L.name_off = 0; L.name_len = 0;
-    L.cnt = 0; L.buf = 0; L.loaded = 0; L.total = 0; L.ncur = 1;
-    L.ntok = 0; L.tcap = A.round_tokens; L.t0 = L.t1 = L.t2 = L.t3 = 0; L.litw = 0; L.nlit = 0;
-    L.full = false;
-    L.cap = 0;
-    L.tb = A.tokens + (uint64_t)sid * A.round_tokens;
-    LL.l = DD.l = 0; LL.g = DD.g = 0;
-    bll.kmin = bdd.kmin = 1; bll.g = bdd.g = 0; bll.left = bdd.left = 0; bll.allzero = bdd.allzero = true;
-    bll.nlong = bdd.nlong = 0;
-    uint32_t flag = 2;                                   // 2: finished in an earlier round
+    uint32_t* tb = A.tokens + (uint64_t)sid * A.round_tokens;
+    uint8_t* lens = A.scratch + (uint64_t)sid * kInflateScratchPerStream;
+    const uint8_t* inp = A.in;
+    uint64_t ilen = 0, cap = 0;
+    bool live = false;
     if (valid) {
-        const uint8_t* inp = A.in + A.in_off[sid];
-        uint64_t ilen = A.in_len[sid];
-        L.cap = A.out_cap[sid];
-        L.lens = A.scratch + (uint64_t)sid * kInflateScratchPerStream;
+        inp = A.in + A.in_off[sid];
+        ilen = A.in_len[sid];
+        cap = A.out_cap[sid];
         if (round == 0) {
-            br_init(L, inp, 0, ilen * 8);
-            L.mode = LM_TYPE;
-            if (A.out_off[sid] & 7) lane_fail(L, SDZ_BAD_RECORD, 0);
-            else parse_container(L, A, ilen);
-            flag = 0;
+            live = true;
+            if (A.out_off[sid] & 7) {
+                S->mode = LM_DONE; S->status = SDZ_BAD_RECORD; S->zmsg = 0; S->bitpos = 0; S->pos = 0;
+                S->container = SDZ_CONTAINER_RAW; S->stored_ck = 0; S->stored_size = 0; S->mtime = 0;
+                S->name_off = 0; S->name_len = 0; S->dict_used = 0; S->ntok = 0; S->litw = 0;
+                S->nlit = 0; S->full = 0;
+            } else {
+                cold_run(S, inp, ilen, cap, tb, A.round_tokens, lens, A.format,
+                         A.dict != nullptr, A.dict_adler, 1u);
+            }
         } else if (S->mode != LM_DONE) {
+            live = true;
             for (int k = 0; k < IL_REGION / 4; ++k) ((uint32_t*)region)[k] = ((const uint32_t*)S->region)[k];
-            L.pos = S->pos; L.mode = S->mode; L.last = S->last; L.container = S->container;
-            L.status = S->status; L.zmsg = S->zmsg; L.fixed = S->fixed; L.nl = S->nl; L.nd = S->nd;
-            L.stored_ck = S->stored_ck; L.stored_size = S->stored_size; L.mtime = S->mtime;
-            L.name_off = S->name_off; L.name_len = S->name_len; L.stored_left = S->stored_left;
-            L.dict_used = S->dict_used;
-            LL = S->LL; DD = S->DD; bll = S->bll; bdd = S->bdd;
-            br_init(L, inp, S->bitpos, ilen * 8);
-            flag = 0;
+            S->ntok = 0; S->full = 0;
         }
     }
-
-    // phases: lanes at a block boundary advance together, then decode together
+    // epochs: lanes that need block-level work do it together (cold_run), then
+    // every lane that can decodes symbols with register-resident state until an
+    // eighth of them has left the fast path; state is parked in DSave in between
+    uint64_t tbits = ilen * 8;
     for (;;) {
-        while (!L.full && L.mode != LM_CODES && L.mode != LM_DONE) block_step(L, LL, DD, bll, bdd, region);
-        int ncodes = __popcll(__ballot(L.mode == LM_CODES && !L.full));
-        if (ncodes == 0) break;
-        int k = ncodes >> 3;
-        int stop = ncodes - (k > 0 ? k : 1);
-        do {
-            if (L.mode == LM_CODES && !L.full) decode_step(L, LL, DD, bll, bdd, region);
-        } while (__popcll(__ballot(L.mode == LM_CODES && !L.full)) > stop);
+        bool hot = live && S->mode == LM_CODES && !S->full && tbits - S->bitpos >= 64;
+        bool cold = live && !S->full && S->mode != LM_DONE && !hot;
+        if (__ballot(cold)) {
+            if (cold)
+                cold_run(S, inp, ilen, cap, tb, A.round_tokens, lens, A.format,
+                         A.dict != nullptr, A.dict_adler, 0u);
+            hot = live && S->mode == LM_CODES && !S->full && tbits - S->bitpos >= 64;
+        }
+        uint64_t hm = __ballot(hot);
+        if (hm == 0) break;
+        int nhot = __popcll(hm);
+        hot_epoch(S, inp, ilen, cap, tb, A.round_tokens, hot, nhot - (nhot >= 16 ? nhot >> 3 : 1));
     }
 
-    bool more = valid && flag == 0 && L.mode != LM_DONE;
+    bool more = live && S->mode != LM_DONE;
     uint64_t mm = __ballot(more);                        // one counter update per wave
     if (mm && (threadIdx.x & 63u) == (uint32_t)__builtin_ctzll(mm)) atomicAdd(A.active, (uint32_t)__popcll(mm));
-    if (!valid || flag == 2) {
+    if (!live) {
         if (valid) { A.ntok[sid] = 0; A.flags[sid] = 2; }
         return;
     }
-    tok_finish(L);
-    A.ntok[sid] = L.ntok;
-    bool done = L.mode == LM_DONE;
-    A.flags[sid] = done ? 1u : 0u;
-    for (int k = 0; k < IL_REGION / 4; ++k) ((uint32_t*)S->region)[k] = ((const uint32_t*)region)[k];
-    S->bitpos = br_consumed(L); S->pos = L.pos; S->mode = L.mode; S->last = L.last;
-    S->container = L.container; S->status = L.status; S->zmsg = L.zmsg; S->fixed = L.fixed;
-    S->nl = L.nl; S->nd = L.nd; S->stored_ck = L.stored_ck; S->stored_size = L.stored_size;
-    S->mtime = L.mtime; S->name_off = L.name_off; S->name_len = L.name_len;
-    S->stored_left = L.stored_left; S->dict_used = L.dict_used;
-    S->LL = LL; S->DD = DD; S->bll = bll; S->bdd = bdd;
+    {
+        Core H;                                          // flush the token stage
+        H.tb = tb; H.ts = ts; H.ntok = S->ntok; H.litw = S->litw; H.nlit = S->nlit;
+        tok_finish(H);
+        S->ntok = H.ntok; S->litw = 0; S->nlit = 0;
+        A.ntok[sid] = H.ntok;
+    }
+    A.flags[sid] = S->mode == LM_DONE ? 1u : 0u;
+    if (S->mode != LM_DONE)
+        for (int k = 0; k < IL_REGION / 4; ++k) ((uint32_t*)S->region)[k] = ((const uint32_t*)region)[k];
 }
 
-// ------------------------------------------------------------------ phase 2: LZ77 resolve
-
-#define RS_WAVES 4
-#define RS_STAGE 4096                 // batch output budget (bytes) per wave
-
-__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v, uint32_t lane) {
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        uint32_t u = __shfl_up(v, o);
-        if (lane >= (uint32_t)o) v += u;
-    }
-    return v;
-}
-__device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-    return v;
-}
-
-// byte at output offset s of this stream (s may be negative: preset dictionary / zeros, A12)
-__device__ __forceinline__ uint32_t src_byte(const uint8_t* out, int64_t s, const uint8_t* dict, int64_t dl) {
-    if (s >= 0) return out[s];
-    int64_t d = dl + s;
-    return d >= 0 ? (uint32_t)dict[d] : 0u;
-}
-
-// adler32.ts:34-105 over r bytes seeded with the chunk-start state (NMAX quirk)
-__device__ int32_t adler_quirk_tail(const uint8_t* p, uint32_t r, uint32_t s1, uint32_t s2in) {
-    uint64_t a = s1, s2 = s2in;
-    uint32_t off = 0, len = r;
-    while (len >= 5552) {
-        len -= 5552;
-        for (int i = 0; i < 5552; ++i) { a += p[off++]; s2 += a; }
-        a %= 65521u;
-        s2 += 65521u;
-    }
-    if (len) {
-        while (len--) { a += p[off++]; s2 += a; }
-        a %= 65521u;
-        s2 %= 65521u;
-    }
-    return (int32_t)((uint32_t)a | ((uint32_t)s2 << 16));
-}
-
-__global__ __launch_bounds__(RS_WAVES * 64) void k_inflate_resolve(InflateArgs A, uint32_t round) {
-    __shared__ __attribute__((aligned(16))) uint8_t stage_all[RS_WAVES][RS_STAGE + 64];
-    __shared__ uint32_t crct[256];
-    for (int v = threadIdx.x; v < 256; v += RS_WAVES * 64) {
-        uint32_t c = (uint32_t)v;
-        for (int k = 0; k < 8; ++k) c = (c & 1) ? 0xedb88320u ^ (c >> 1) : c >> 1;
-        crct[v] = c;
-    }
-    __syncthreads();
-    uint32_t lane = threadIdx.x & 63u;
-    uint32_t w = threadIdx.x >> 6;
-    uint32_t sid = blockIdx.x * RS_WAVES + w;
-    if (sid >= A.n) return;
-    uint32_t flag = A.flags[sid];
-    if (flag == 2) return;
-    uint8_t* stage = stage_all[w];
-    RSave* R = (RSave*)A.rsave + sid;
-    const DSave* S = (const DSave*)A.dsave + sid;
-    uint64_t pos;
-    uint32_t s1, s2, crc, snap1, snap2;
-    bool gz = S->container == SDZ_CONTAINER_GZIP;
-    if (round == 0) { pos = 0; s1 = 1; s2 = 0; crc = 0xffffffffu; snap1 = 1; snap2 = 0; }
-    else { pos = R->pos; s1 = R->s1; s2 = R->s2; crc = R->crc; snap1 = R->snap1; snap2 = R->snap2; }
-    uint8_t* out = A.out + A.out_off[sid];
-    const uint32_t* tk = A.tokens + (uint64_t)sid * A.round_tokens;
-    uint32_t ntok = A.ntok[sid];
-    int64_t dl = S->dict_used && A.dict ? (A.dict_len > 32767 ? 32767 : A.dict_len) : 0;
-    const uint8_t* dict = dl ? A.dict + (A.dict_len - dl) : nullptr;
-
-    for (uint32_t base = 0; base < ntok;) {
-        bool inr = base + lane < ntok;
-        uint32_t t = inr ? tk[base + lane] : 0u;
-        bool ism = (t >> 31) != 0;
-        uint32_t len = !inr ? 0u : ism ? ((t >> 16) & 255u) + 3u : ((t >> 24) & 3u) + 1u;
-        uint32_t dist = (t & 0x7fffu) + 1u;
-        uint32_t head = (uint32_t)(pos & 3);
-        uint32_t incl = wave_incl_scan(len, lane);
-        uint32_t off = incl - len;
-        bool take = inr && (incl + head <= RS_STAGE || lane == 0);
-        uint64_t tm = __ballot(take);
-        uint32_t nv = (uint32_t)__popcll(tm);
-        uint32_t B = __shfl(incl, nv - 1);
-        uint32_t TB = head + B;
-        if (lane == 0 && head) *(uint32_t*)stage = *(const uint32_t*)(out + (pos & ~3ull));
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        // generation 0: literals and references to bytes before this batch
-        bool gen0 = take && (!ism || dist >= off + len);
-        if (gen0) {
-            uint8_t* dst = stage + head + off;
-            if (!ism) {
-                for (uint32_t k = 0; k < len; ++k) dst[k] = (uint8_t)(t >> (8 * k));
-            } else {
-                int64_t s = (int64_t)(pos + off) - (int64_t)dist;
-                if (s >= 0) {
-                    const uint8_t* sp = out + s;
-                    uint32_t a = (uint32_t)((uintptr_t)sp & 3u);
-                    const uint32_t* wp = (const uint32_t*)(sp - a);
-                    uint32_t nw = (len + a + 3) >> 2;
-                    uint32_t k = 0;
-                    for (uint32_t q = 0; q < nw; ++q) {
-                        uint32_t wv = wp[q];
-                        for (uint32_t bb = (q == 0 ? a : 0); bb < 4 && k < len; ++bb, ++k) dst[k] = (uint8_t)(wv >> (8 * bb));
-                    }
-                } else {
-                    for (uint32_t k = 0; k < len; ++k) dst[k] = (uint8_t)src_byte(out, s + k, dict, dl);
-                }
-            }
-        }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        // generation 1: in-batch references, in token order, one match per step
-        uint64_t rem = __ballot(take && ism && !gen0);
-        while (rem) {
-            uint32_t i = (uint32_t)__builtin_ctzll(rem);
-            rem &= rem - 1;
-            uint32_t o_i = __shfl(off, i), l_i = __shfl(len, i), d_i = __shfl(dist, i);
-            for (uint32_t k = lane; k < l_i; k += 64) {
-                uint32_t kk = d_i < l_i ? k % d_i : k;
-                int64_t sidx = (int64_t)o_i - (int64_t)d_i + (int64_t)kk;   // batch index, < o_i
-                uint32_t b;
-                if (sidx + (int64_t)head >= 0) b = stage[head + sidx];
-                else b = src_byte(out, (int64_t)pos + sidx, dict, dl);
-                stage[head + o_i + k] = (uint8_t)b;
-            }
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        }
-        // write back: coalesced dwords from the dword-aligned start
-        uint32_t nd = (TB + 3) >> 2;
-        uint32_t* dstw = (uint32_t*)(out + (pos & ~3ull));
-        const uint32_t* sw = (const uint32_t*)stage;
-        for (uint32_t q = lane; q < nd; q += 64) dstw[q] = sw[q];
-        // checksums over batch bytes stage[head .. TB)
-        if (!gz) {
-            uint32_t S1 = 0, W = 0;
-            uint64_t cut = ((pos + B) >> 14) << 14;
-            bool cross = (pos >> 14) != ((pos + B) >> 14);
-            uint32_t c = cross ? (uint32_t)(cut - pos) : 0u;
-            uint32_t Sc = 0, Wc = 0;
-            for (uint32_t q = lane; q < nd; q += 64) {
-                uint32_t wv = sw[q];
-#pragma unroll
-                for (uint32_t bb = 0; bb < 4; ++bb) {
-                    uint32_t j = 4 * q + bb;
-                    if (j >= head && j < TB) {
-                        uint32_t tix = j - head, b = (wv >> (8 * bb)) & 255u;
-                        S1 += b;
-                        W += (B - tix) * b;
-                        if (tix < c) { Sc += b; Wc += (c - tix) * b; }
-                    }
-                }
-                W %= 65521u;
-                Wc %= 65521u;
-            }
-            S1 = wave_sum(S1);
-            W = wave_sum(W);
-            if (cross) {
-                Sc = wave_sum(Sc);
-                Wc = wave_sum(Wc);
-                snap1 = (uint32_t)(((uint64_t)s1 + Sc) % 65521u);
-                snap2 = (uint32_t)(((uint64_t)s2 + (uint64_t)c * s1 + Wc) % 65521u);
-            }
-            s2 = (uint32_t)(((uint64_t)s2 + (uint64_t)B * s1 + W) % 65521u);
-            s1 = (uint32_t)(((uint64_t)s1 + S1) % 65521u);
-        } else if (lane == 0) {
-            for (uint32_t j = head; j < TB; ++j) crc = crct[(crc ^ stage[j]) & 255u] ^ (crc >> 8);
-        }
-        pos += B;
-        base += nv;
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    }
-    crc = __shfl(crc, 0);
-    if (lane == 0) {
-        R->pos = pos; R->s1 = s1; R->s2 = s2; R->crc = crc; R->snap1 = snap1; R->snap2 = snap2;
-    }
-    if (flag != 1) return;
-    // final: record + verdicts (sd-inflate.ts:134-179)
-    if (lane == 0) {
-        sdz_inflate_record Rc;
-        Rc.status = S->status;
-        Rc.zmsg = S->zmsg;
-        Rc.out_len = pos;
-        uint64_t ib = S->bitpos;
-        uint64_t ilen = A.in_len[sid];
-        Rc.in_used = (ib + 7) >> 3;
-        if (Rc.in_used > ilen) Rc.in_used = ilen;
-        Rc.stored_checksum = S->stored_ck;
-        bool have = pos > 0;                              // Inflater.checksum stays undefined otherwise
-        int32_t running;
-        if (gz) {
-            running = (int32_t)~crc;
-        } else {
-            uint32_t r = (uint32_t)(pos & 16383u);
-            if (r == 5552u || r == 11104u) running = adler_quirk_tail(out + (pos - r), r, snap1, snap2);
-            else running = (int32_t)(s1 | (s2 << 16));
-        }
-        Rc.running_checksum = have ? running : 0;
-        Rc.stored_size = S->stored_size;
-        Rc.mtime = S->mtime;
-        Rc.name_off = S->name_off;
-        Rc.name_len = S->name_len;
-        Rc.container = (uint8_t)S->container;
-        bool complete = S->mode == LM_DONE && (S->status == SDZ_OK || S->status == SDZ_TRAILING);
-        Rc.complete = complete ? 1 : 0;
-        uint8_t cv = S->stored_ck == 0 ? SDZ_UNCHECKED : ((have && S->stored_ck == running) ? SDZ_MATCH : SDZ_MISMATCH);
-        uint8_t sv = S->stored_size == 0 ? SDZ_UNCHECKED
-                   : ((int64_t)S->stored_size == (int64_t)pos ? SDZ_MATCH : SDZ_MISMATCH);
-        Rc.checksum_verdict = cv;
-        Rc.size_verdict = sv;
-        Rc.success = (complete && cv != SDZ_MISMATCH && sv != SDZ_MISMATCH) ? 1 : 0;
-        for (int k = 0; k < 11; ++k) Rc.reserved[k] = 0;
-        A.rec[sid] = Rc;
-    }
-}
+__global__ void k_inflate_resolve(InflateArgs A, uint32_t round);
+uint32_t resolve_block_threads();
+uint32_t resolve_streams_per_block();
 
 uint64_t inflate_dsave_bytes() { return (sizeof(DSave) + 15) & ~(uint64_t)15; }
 uint64_t inflate_rsave_bytes() { return (sizeof(RSave) + 15) & ~(uint64_t)15; }
@@ -992,11 +988,12 @@ uint64_t inflate_rsave_bytes() { return (sizeof(RSave) + 15) & ~(uint64_t)15; }
 // host driver: rounds of (decode, resolve) until no stream needs another round
 int run_inflate_rounds(const InflateArgs& a, hipStream_t s, uint32_t* host_active) {
     if (a.n == 0) return 0;
-    dim3 g1((a.n + IL_THREADS - 1) / IL_THREADS), g2((a.n + RS_WAVES - 1) / RS_WAVES);
+    uint32_t spb = resolve_streams_per_block();
+    dim3 g1((a.n + IL_THREADS - 1) / IL_THREADS), g2((a.n + spb - 1) / spb);
     for (uint32_t round = 0;; ++round) {
         if (hipMemsetAsync(a.active, 0, sizeof(uint32_t), s) != hipSuccess) return -1;
         hipLaunchKernelGGL(k_inflate_decode, g1, dim3(IL_THREADS), 0, s, a, round);
-        hipLaunchKernelGGL(k_inflate_resolve, g2, dim3(RS_WAVES * 64), 0, s, a, round);
+        hipLaunchKernelGGL(k_inflate_resolve, g2, dim3(resolve_block_threads()), 0, s, a, round);
         if (hipMemcpyAsync(host_active, a.active, sizeof(uint32_t), hipMemcpyDeviceToHost, s) != hipSuccess) return -1;
         if (hipStreamSynchronize(s) != hipSuccess) return -1;
         if (*host_active == 0) break;
