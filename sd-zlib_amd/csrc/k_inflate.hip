@@ -981,6 +981,7 @@ __global__ __launch_bounds__(IL_THREADS, 1) void k_inflate_decode(InflateArgs A,
 __global__ void k_inflate_resolve(InflateArgs A, uint32_t round);
 uint32_t resolve_block_threads();
 uint32_t resolve_streams_per_block();
+void launch_inflate_finalize(const InflateArgs& a, hipStream_t s);
 
 uint64_t inflate_dsave_bytes() { return (sizeof(DSave) + 15) & ~(uint64_t)15; }
 uint64_t inflate_rsave_bytes() { return (sizeof(RSave) + 15) & ~(uint64_t)15; }
@@ -998,7 +999,8 @@ int run_inflate_rounds(const InflateArgs& a, hipStream_t s, uint32_t* host_activ
         if (hipStreamSynchronize(s) != hipSuccess) return -1;
         if (*host_active == 0) break;
     }
-    return 0;
+    launch_inflate_finalize(a, s);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
 }  // namespace sdz

@@ -5,6 +5,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <numeric>
@@ -207,8 +208,15 @@ int sdz_inflate_batch_device(const uint8_t* in, const uint64_t* in_off, const ui
     // per-stream slabs: code lengths | decode state | resolve state, then the token
     // ring (round_tokens per stream, bounded to ~4 GiB in total), flags, counter
     const uint64_t dsb = inflate_dsave_bytes(), rsb = inflate_rsave_bytes();
-    uint32_t T = (uint32_t)std::min<uint64_t>(16384, std::max<uint64_t>(1024, (4ull << 30) / (4ull * n)));
-    T &= ~3u;
+    // tokens per stream per round: as many as a quarter of free HBM (at most 32 GiB) allows,
+    // up to 128 Ki (C2's streams then finish in one round); SDZ_ROUND_TOKENS overrides
+    size_t mem_free = 0, mem_total = 0;
+    if (hipMemGetInfo(&mem_free, &mem_total) != hipSuccess) mem_free = 16ull << 30;
+    uint64_t budget = std::min<uint64_t>(32ull << 30, mem_free / 4);
+    uint64_t want = 1u << 17;
+    if (const char* e = getenv("SDZ_ROUND_TOKENS")) want = strtoull(e, nullptr, 10);
+    uint32_t T = (uint32_t)std::min<uint64_t>(want, std::max<uint64_t>(1024, budget / (4ull * n)));
+    T = std::max<uint32_t>(64, T & ~31u);
     const size_t off_ds = (size_t)n * kInflateScratchPerStream;
     const size_t off_rs = off_ds + (size_t)n * dsb;
     const size_t off_tk = (off_rs + (size_t)n * rsb + 255) & ~(size_t)255;

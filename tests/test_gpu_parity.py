@@ -347,3 +347,45 @@ def test_api_mirror_roundtrip(paradise):
     a = parts.append(golden("paradiselost.part1.deflate"))
     b = parts.append(golden("paradiselost.part2.deflate"))
     assert sdz.mergeBuffers(a + b) == paradise and parts.finish()["success"]
+
+
+# ------------------------------------------------------------------ resolve edge paths
+
+def _periodic(rng, n):
+    out = bytearray()
+    while len(out) < n:
+        p = rng.choice([1, 2, 3, 4, 5, 7, 31, 258, 1000])
+        unit = bytes(rng.getrandbits(8) for _ in range(p))
+        out += unit * rng.randint(1, 4000 // p + 2)
+    return bytes(out[:n])
+
+
+@pytest.mark.parametrize("level", [1, 6, 9])
+def test_repetitive_data_long_match_chains(level):
+    """Distances 1-3 (repeating words), 258-byte chains inside one batch, ring wrap."""
+    rng = random.Random(7 + level)
+    originals = [b"a" * 100000, b"ab" * 50000, b"abc" * 40000, bytes(70000)]
+    originals += [_periodic(rng, rng.randint(1, 200000)) for _ in range(12)]
+    streams = [zlib.compress(d, level) for d in originals]
+    gpu = sdz.inflate_batch(streams, [len(d) + 64 for d in originals], sdz.FMT_CONTAINER)
+    for g, d, s in zip(gpu, originals, streams):
+        assert g["status"] == "OK" and g["data"] == d
+        if not has_stored_block(s, False):
+            assert_same(g, O.inflater_run([s]), s)
+
+
+def test_small_rounds_rebuild_the_window(monkeypatch, paradise):
+    """Force many rounds: the resolve window is rebuilt from HBM at every round start."""
+    monkeypatch.setenv("SDZ_ROUND_TOKENS", "96")
+    rng = random.Random(3)
+    originals = [paradise, paradise[:70001], text_corpus(rng, 150000), _periodic(rng, 90000)]
+    streams = [zlib.compress(d, 6) for d in originals]
+    streams.append(golden("paradiselost.gz"))
+    originals.append(paradise)
+    gpu = sdz.inflate_batch(streams, [len(d) + 64 for d in originals], sdz.FMT_CONTAINER)
+    for g, d, s in zip(gpu, originals, streams):
+        assert g["status"] == "OK" and g["data"] == d and g["success"]
+        assert_same(g, O.inflater_run([s]), s)
+    dgpu = sdz.inflate_batch([golden("simple.deflate")], [4096], sdz.FMT_CONTAINER,
+                             None)[0]
+    assert dgpu["data"] == golden("simple.txt")
