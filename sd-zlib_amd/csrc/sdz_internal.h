@@ -39,6 +39,7 @@ struct InflateArgs {
     uint32_t* ntok;              // n
     uint32_t* flags;             // n: 0 more rounds, 1 finished this round, 2 finished earlier
     uint32_t* active;            // 1 counter
+    unsigned long long* dbg;     // phase cycle counters (SDZ_PHASE_TIMING), normally null
 };
 
 uint64_t inflate_dsave_bytes();  // per stream decode state

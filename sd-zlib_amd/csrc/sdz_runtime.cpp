@@ -244,9 +244,24 @@ int sdz_inflate_batch_device(const uint8_t* in, const uint64_t* in_off, const ui
     a.flags = a.ntok + n;
     a.active = a.flags + n;
     static thread_local uint32_t host_active = 0;
+    a.dbg = nullptr;
+    const bool phases = getenv("SDZ_PHASE_TIMING") != nullptr;   // development aid
+    if (phases) {
+        HIPCHK(hipMalloc(&a.dbg, 64 * sizeof(unsigned long long)));
+        HIPCHK(hipMemsetAsync(a.dbg, 0, 64 * sizeof(unsigned long long), s));
+    }
     timing_begin(s);
     if (run_inflate_rounds(a, s, &host_active)) return hip_fail(hipGetLastError(), "inflate rounds");
     timing_end(s);
+    if (phases) {
+        unsigned long long h[64];
+        HIPCHK(hipMemcpyAsync(h, a.dbg, sizeof h, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        fprintf(stderr, "sdz phases:");
+        for (int k = 0; k < 16; ++k) fprintf(stderr, " %llu", h[k]);
+        fprintf(stderr, "\n");
+        hipFree(a.dbg);
+    }
     HIPCHK(hipGetLastError());
     return SDZ_API_OK;
 }
