@@ -75,13 +75,18 @@ class DeviceBatch:
             b.free()
 
 
-def inflate_step(sdz, b):
+def inflate_step(sdz, b, split=None):
     in_off, in_len, out_off, out_cap = b.ptrs()
     rc = sdz.lib().sdz_inflate_batch_device(b.d_in.ptr, in_off, in_len, b.d_out.ptr, out_off, out_cap,
                                             b.d_rec.ptr, b.n, sdz.FMT_AUTO, None, 0, None)
     if rc:
         raise RuntimeError(sdz.lib().sdz_last_error().decode())
-    return sdz.lib().sdz_last_kernel_ms()
+    ms = sdz.lib().sdz_last_kernel_ms()
+    if split is not None:                                  # decode / resolve / finalize (HIP events)
+        f3 = (ctypes.c_float * 3)()
+        sdz.lib().sdz_last_kernel_breakdown(f3)
+        split.append(list(f3))
+    return ms
 
 
 def deflate_step(sdz, b, level, fmt):
@@ -126,7 +131,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--streams", type=int, default=65536, help="streams per GPU (C2: 65536)")
     ap.add_argument("--cpu-seconds", type=float, default=1.5)
-    ap.add_argument("--deflate-streams", type=int, default=4096,
+    ap.add_argument("--deflate-streams", type=int, default=512,
                     help="streams for the deflate leg (64 KiB slices, L6); 0 disables")
     ap.add_argument("--deflate-steps", type=int, default=1)
     args = ap.parse_args()
@@ -167,10 +172,10 @@ def main():
     L.sdz_sync(None)
     barrier()
     L.sdz_sync(None)
-    kms = []
+    kms, split = [], []
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        kms.append(inflate_step(sdz, b))
+        kms.append(inflate_step(sdz, b, split))
     L.sdz_sync(None)
     barrier()
     t1 = time.perf_counter()
@@ -256,6 +261,7 @@ def main():
         except Exception:
             traffic = None
     achieved = (bytes_in + bytes_out) / (kernel_ms / 1000.0) / 1e9
+    kparts = [sum(x[k] for x in split) / len(split) for k in range(3)]
     line = {
         "metric": METRIC,
         "value": round(world * bytes_out / (wall / args.steps) / 1e6, 2),
@@ -270,6 +276,10 @@ def main():
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
                      "kernel_ms": round(kernel_ms, 3),
+                     "kernels_ms": {"k_inflate_decode": round(kparts[0], 3),
+                                    "k_inflate_resolve": round(kparts[1], 3),
+                                    "k_inflate_finalize": round(kparts[2], 3)},
+                     "launch": "one sdz_inflate_batch_device call = decode + resolve + finalize kernels",
                      "algorithmic_bytes_per_launch": bytes_in + bytes_out},
         "cpu_baseline": cpu,
         "parity": bool(okall),

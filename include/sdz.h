@@ -173,6 +173,9 @@ int sdz_sync(void* stream);
  * event of the most recent call on this thread and returns the elapsed ms. */
 int sdz_set_timing(int enabled);
 float sdz_last_kernel_ms(void);
+/* per-kernel split of the last inflate call with timing on: [0] k_inflate_decode,
+ * [1] k_inflate_resolve (both summed over rounds), [2] k_inflate_finalize, in ms */
+int sdz_last_kernel_breakdown(float* ms3);
 
 #ifdef __cplusplus
 }

@@ -986,21 +986,50 @@ void launch_inflate_finalize(const InflateArgs& a, hipStream_t s);
 uint64_t inflate_dsave_bytes() { return (sizeof(DSave) + 15) & ~(uint64_t)15; }
 uint64_t inflate_rsave_bytes() { return (sizeof(RSave) + 15) & ~(uint64_t)15; }
 
-// host driver: rounds of (decode, resolve) until no stream needs another round
-int run_inflate_rounds(const InflateArgs& a, hipStream_t s, uint32_t* host_active) {
+// host driver: rounds of (decode, resolve) until no stream needs another round.
+// kernel_ms (optional, 3 entries) accumulates decode / resolve / finalize times.
+int run_inflate_rounds(const InflateArgs& a, hipStream_t s, uint32_t* host_active, float* kernel_ms) {
     if (a.n == 0) return 0;
     uint32_t spb = resolve_streams_per_block();
     dim3 g1((a.n + IL_THREADS - 1) / IL_THREADS), g2((a.n + spb - 1) / spb);
+    hipEvent_t ev[4] = { nullptr, nullptr, nullptr, nullptr };
+    if (kernel_ms) {
+        for (auto& e : ev) (void)hipEventCreate(&e);
+        kernel_ms[0] = kernel_ms[1] = kernel_ms[2] = 0.f;
+    }
+    int rc = 0;
     for (uint32_t round = 0;; ++round) {
-        if (hipMemsetAsync(a.active, 0, sizeof(uint32_t), s) != hipSuccess) return -1;
+        if (hipMemsetAsync(a.active, 0, sizeof(uint32_t), s) != hipSuccess) { rc = -1; break; }
+        if (kernel_ms) (void)hipEventRecord(ev[0], s);
         hipLaunchKernelGGL(k_inflate_decode, g1, dim3(IL_THREADS), 0, s, a, round);
+        if (kernel_ms) (void)hipEventRecord(ev[1], s);
         hipLaunchKernelGGL(k_inflate_resolve, g2, dim3(resolve_block_threads()), 0, s, a, round);
-        if (hipMemcpyAsync(host_active, a.active, sizeof(uint32_t), hipMemcpyDeviceToHost, s) != hipSuccess) return -1;
-        if (hipStreamSynchronize(s) != hipSuccess) return -1;
+        if (kernel_ms) (void)hipEventRecord(ev[2], s);
+        if (hipMemcpyAsync(host_active, a.active, sizeof(uint32_t), hipMemcpyDeviceToHost, s) != hipSuccess) { rc = -1; break; }
+        if (hipStreamSynchronize(s) != hipSuccess) { rc = -1; break; }
+        if (kernel_ms) {
+            float t0 = 0.f, t1 = 0.f;
+            (void)hipEventElapsedTime(&t0, ev[0], ev[1]);
+            (void)hipEventElapsedTime(&t1, ev[1], ev[2]);
+            kernel_ms[0] += t0;
+            kernel_ms[1] += t1;
+        }
         if (*host_active == 0) break;
     }
-    launch_inflate_finalize(a, s);
-    return hipGetLastError() == hipSuccess ? 0 : -1;
+    if (rc == 0) {
+        if (kernel_ms) (void)hipEventRecord(ev[2], s);
+        launch_inflate_finalize(a, s);
+        if (kernel_ms) {
+            (void)hipEventRecord(ev[3], s);
+            (void)hipEventSynchronize(ev[3]);
+            float t2 = 0.f;
+            (void)hipEventElapsedTime(&t2, ev[2], ev[3]);
+            kernel_ms[2] = t2;
+        }
+        if (hipGetLastError() != hipSuccess) rc = -1;
+    }
+    if (kernel_ms) for (auto& e : ev) (void)hipEventDestroy(e);
+    return rc;
 }
 
 }  // namespace sdz

@@ -44,7 +44,7 @@ struct InflateArgs {
 
 uint64_t inflate_dsave_bytes();  // per stream decode state
 uint64_t inflate_rsave_bytes();  // per stream resolve state
-int run_inflate_rounds(const InflateArgs& a, hipStream_t s, uint32_t* host_active);
+int run_inflate_rounds(const InflateArgs& a, hipStream_t s, uint32_t* host_active, float* kernel_ms);
 
 struct DeflateArgs {
     const uint8_t* in;

@@ -23,6 +23,7 @@ thread_local float g_last_ms = 0.f;
 thread_local hipEvent_t g_ev0 = nullptr, g_ev1 = nullptr;
 thread_local bool g_ev_pending = false;
 int g_timing = 0;
+float g_breakdown[3] = { 0.f, 0.f, 0.f };   // decode / resolve / finalize of the last inflate
 std::mutex g_mu;
 
 int fail(int code, const std::string& msg) {
@@ -180,6 +181,11 @@ int sdz_sync(void* stream) {
     return SDZ_API_OK;
 }
 int sdz_set_timing(int enabled) { g_timing = enabled; return SDZ_API_OK; }
+int sdz_last_kernel_breakdown(float* ms3) {
+    if (!ms3) return fail(SDZ_API_BAD_ARG, "sdz_last_kernel_breakdown: null pointer");
+    ms3[0] = g_breakdown[0]; ms3[1] = g_breakdown[1]; ms3[2] = g_breakdown[2];
+    return SDZ_API_OK;
+}
 float sdz_last_kernel_ms(void) {
     if (g_ev_pending) {
         hipEventSynchronize(g_ev1);
@@ -251,7 +257,8 @@ int sdz_inflate_batch_device(const uint8_t* in, const uint64_t* in_off, const ui
         HIPCHK(hipMemsetAsync(a.dbg, 0, 64 * sizeof(unsigned long long), s));
     }
     timing_begin(s);
-    if (run_inflate_rounds(a, s, &host_active)) return hip_fail(hipGetLastError(), "inflate rounds");
+    if (run_inflate_rounds(a, s, &host_active, g_timing ? g_breakdown : nullptr))
+        return hip_fail(hipGetLastError(), "inflate rounds");
     timing_end(s);
     if (phases) {
         unsigned long long h[64];

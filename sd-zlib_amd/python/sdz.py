@@ -57,7 +57,7 @@ EXPORTS = [
     "sdz_version", "sdz_device_count", "sdz_set_device", "sdz_device_alloc",
     "sdz_device_free", "sdz_copy_to_device", "sdz_copy_to_host", "sdz_memset_device",
     "sdz_copy_device_to_device",
-    "sdz_sync", "sdz_set_timing", "sdz_last_kernel_ms",
+    "sdz_sync", "sdz_set_timing", "sdz_last_kernel_ms", "sdz_last_kernel_breakdown",
 ]
 
 _lib = None
@@ -107,6 +107,8 @@ def lib():
     L.sdz_sync.argtypes = [vp]
     L.sdz_set_timing.argtypes = [ctypes.c_int]
     L.sdz_last_kernel_ms.restype = ctypes.c_float
+    L.sdz_last_kernel_breakdown.argtypes = [ctypes.POINTER(ctypes.c_float)]
+    L.sdz_last_kernel_breakdown.restype = ctypes.c_int
     L.sdz_set_device.argtypes = [ctypes.c_int]
     _lib = L
     return L
