@@ -62,6 +62,7 @@ enum {
                               loops forever here; reported instead */
     SDZ_TOO_SMALL = 7,     /* AUTO and < 2 bytes: "data buffer is too small" :195 */
     SDZ_BAD_RECORD = 8,    /* misaligned output offset (must be a multiple of 8) */
+    SDZ_INTERNAL = 9,      /* engine watchdog: a resolve wait did not complete (never expected) */
 };
 
 /* Checksum / size verdicts ("unchecked" | "match" | "mismatch") */

@@ -1,30 +1,38 @@
 // k_resolve.hip -- batched DEFLATE decoder, phase 2: tokens -> bytes, adler32, and the
 // Inflater verdicts (src/sd-inflate.ts:134-179); k_inflate_finalize adds crc32 for gzip.
 //
-// One WORKGROUP (4 waves) per stream, four streams per CU.  The stream's LZ77 window
-// lives in LDS: a 36 KiB ring holds the last 32 KiB of output plus the batch being
-// built, so back-references never leave the CU (a global-memory window re-reads the
-// source lines of every match from beyond L2: median distance is ~7 KiB on text).
-// Per batch of up to 256 tokens (<= 4 KiB of output):
-//   1. block-wide prefix sum of token lengths (DPP within waves, LDS across them);
-//   2. literals, and matches whose source lies before the batch, are written in
-//      parallel (4-byte unaligned LDS copies; distances 1-3 as repeating words);
-//   3. matches reading bytes of this batch resolve in barrier-separated rounds:
-//      a match goes once every token it reads from is final (256-bit LDS mask);
-//      the earliest pending match is always ready, so rounds terminate;
-//   4. the batch is written to HBM as coalesced dwords and folded into adler32
-//      (S = sum b, W = sum (B - t) b, wave then block reduction), with the 16 KiB
-//      snapshot the Inflater's chunk-wise checksum needs (adler32.ts:67 quirk).
+// One WORKGROUP of RS_WAVES waves per stream, four streams per CU.  The stream's LZ77
+// window lives in LDS: a ~39 KiB ring holds the last 32 KiB of output plus the bytes in
+// flight, so back-references never leave the CU.
+//
+// The waves form a pipeline without block barriers.  The round's tokens are cut into
+// GROUPS of 64 (one per lane); wave w takes groups w, w + RS_WAVES, ...  Per group:
+//   1. lengths and a DPP wave scan give the group's byte count T; the group's start S
+//      comes from its predecessor through a one-word LDS chain (tag, end), and S + T
+//      is passed on at once, so starts run ahead of the copying;
+//   2. rounds: every token whose source bytes are final is written (4-byte unaligned
+//      LDS copies; distances 1-3 as repeating words).  "Final" means below the
+//      stream-wide frontier Wf, or inside this group's own finished prefix;
+//   3. the group's bytes go to HBM as coalesced dwords, folded into adler32
+//      (S = sum b, T = sum i b as whole-output sums);
+//   4. the group publishes Wf = S + T once Wf reached S (in order), then Wwb (bytes
+//      written back, which frees their ring slots) the same way.
+// A head group (Wf == S) publishes its finished prefix as it goes, so a large group
+// never waits on its own ring space.  Ring-space rule: writing byte p needs
+// p < Wf + (R - 32 KiB) (no reader needs byte p - R any more) and p < Wwb + R (byte
+// p - R is in HBM).  Every wait is bounded (SDZ_INTERNAL if a bound trips).
 // Positions before the output start read the preset dictionary or zeros.
 #include "inflate_state.h"
 
 namespace sdz {
 
-#define RS_THREADS 256
-#define RS_WAVES (RS_THREADS / 64)
-#define RS_R 35840                    // ring bytes: 32 KiB window + one batch
-#define RS_STAGE 3072                 // batch output budget
+#define RS_WAVES 8
+#define RS_THREADS (64 * RS_WAVES)
 #define RS_WIN 32768
+#define RS_R 36352                    // ring bytes: 32 KiB window + bytes in flight
+#define RS_SLACK (RS_R - RS_WIN)
+#define RS_BM 4096                    // finality map bytes (>= RS_SLACK; lap = position >> 12)
+#define RS_SPIN_LIMIT (1u << 22)      // watchdog: polls per wait (~0.2 s)
 
 __device__ __forceinline__ uint32_t ridx(int32_t x) {            // x in (-R, 2R)
     x += x < 0 ? RS_R : 0;
@@ -32,7 +40,7 @@ __device__ __forceinline__ uint32_t ridx(int32_t x) {            // x in (-R, 2R
     return (uint32_t)x;
 }
 
-// inclusive wave scan / reduction with DPP row shifts and row broadcasts (gfx9)
+// inclusive wave scan with DPP row shifts and row broadcasts (gfx9)
 template <int CTRL, int ROWS>
 __device__ __forceinline__ uint32_t dpp_add(uint32_t x) {
     return x + (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, ROWS, 0xf, false);
@@ -46,8 +54,9 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) {
     x = dpp_add<0x143, 0xc>(x);                           // row_bcast:31 -> rows 2, 3
     return x;
 }
-__device__ __forceinline__ uint32_t wave_sum(uint32_t x) {
-    return (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_scan(x), 63);
+__device__ __forceinline__ uint32_t uni(uint32_t x) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)x); }
+__device__ __forceinline__ uint32_t lane_at(uint32_t x, uint32_t l) {
+    return (uint32_t)__builtin_amdgcn_readlane((int)x, (int)l);
 }
 
 __device__ __forceinline__ uint32_t ld32(const uint8_t* ring, uint32_t i) {   // unaligned ds_read_b32
@@ -61,78 +70,17 @@ __device__ __forceinline__ void st16(uint8_t* ring, uint32_t i, uint32_t v) {
     __builtin_memcpy(ring + i, &h, 2);
 }
 
-// write the low n <= 4 bytes of v at ring index d (no wrap: d + n <= R)
-__device__ __forceinline__ void put_tail(uint8_t* ring, uint32_t d, uint32_t v, uint32_t n) {
-    if (n == 4) { st32(ring, d, v); return; }
-    if (n & 2) { st16(ring, d, v); d += 2; v >>= 16; }
-    if (n & 1) ring[d] = (uint8_t)v;
+// LDS-only ordering for the frontier words (no wait on outstanding HBM stores)
+__device__ __forceinline__ void lds_release() { __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local"); }
+__device__ __forceinline__ void lds_acquire() { __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local"); }
+__device__ __forceinline__ uint32_t lds_get(uint32_t* p) {
+    return uni(__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
 }
-// the same across the ring's end
-__device__ __forceinline__ void put_wrap(uint8_t* ring, uint32_t d, uint32_t v, uint32_t n) {
-    for (uint32_t b = 0; b < n; ++b) ring[ridx((int32_t)(d + b))] = (uint8_t)(v >> (8 * b));
+__device__ __forceinline__ uint64_t lds_get64(uint64_t* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
-
-// LZ77 copy of len bytes from ring index s to ring index d (s = d - dist mod R)
-__device__ __forceinline__ void copy_match(uint8_t* ring, uint32_t d, uint32_t s, uint32_t len, uint32_t dist) {
-    const bool nowrap = d + len <= RS_R && s + len + 3 <= RS_R;
-    if (dist >= 4) {
-        // 4-byte units in order: a unit reads bytes at least 4 behind its own
-        if (nowrap) {
-            uint32_t k = 0;
-            for (; k + 4 <= len; k += 4) st32(ring, d + k, ld32(ring, s + k));
-            if (k < len) put_tail(ring, d + k, ld32(ring, s + k), len - k);
-            return;
-        }
-        for (uint32_t k = 0; k < len; k += 4) {
-            uint32_t v = 0;
-            for (uint32_t b = 0; b < 4; ++b) v |= (uint32_t)ring[ridx((int32_t)(s + k + b))] << (8 * b);
-            put_wrap(ring, d + k, v, len - k < 4 ? len - k : 4);
-        }
-        return;
-    }
-    // period 1..3: the source bytes repeat; emit them as 4-byte words
-    uint32_t p0 = ring[s], p1 = ring[ridx((int32_t)s + 1)], p2 = ring[ridx((int32_t)s + 2)];
-    uint32_t w0, w1, w2;
-    if (dist == 1) { w0 = w1 = w2 = p0 * 0x01010101u; }
-    else if (dist == 2) { w0 = w1 = w2 = (p0 | (p1 << 8)) * 0x00010001u; }
-    else {
-        w0 = p0 | (p1 << 8) | (p2 << 16) | (p0 << 24);
-        w1 = p1 | (p2 << 8) | (p0 << 16) | (p1 << 24);
-        w2 = p2 | (p0 << 8) | (p1 << 16) | (p2 << 24);
-    }
-    if (d + len <= RS_R) {
-        uint32_t k = 0;
-        for (; k + 4 <= len; k += 4) {
-            st32(ring, d + k, w0);
-            uint32_t t = w0; w0 = w1; w1 = w2; w2 = t;       // the next unit starts 4 bytes on
-        }
-        if (k < len) put_tail(ring, d + k, w0, len - k);
-        return;
-    }
-    for (uint32_t k = 0; k < len; k += 4) {
-        put_wrap(ring, d + k, w0, len - k < 4 ? len - k : 4);
-        uint32_t t = w0; w0 = w1; w1 = w2; w2 = t;
-    }
-}
-
-// are tokens j0..j1 all final?  (mask of 256 bits; empty range -> true)
-__device__ __forceinline__ bool range_final(const uint64_t* fin, int j0, int j1) {
-    for (int q = j0 >> 6; q <= (j1 >> 6); ++q) {
-        int lo = j0 > 64 * q ? j0 : 64 * q, hi = j1 < 64 * q + 63 ? j1 : 64 * q + 63;
-        uint64_t m = (~0ull >> (63 - (hi - lo))) << (lo - 64 * q);
-        if ((fin[q] & m) != m) return false;
-    }
-    return true;
-}
-
-// index of the token whose output covers batch byte x (ei = inclusive ends, ascending)
-__device__ __forceinline__ int tok_of(const uint32_t* ei, int ntk, uint32_t x) {
-    int lo = 0, hi = ntk - 1;                             // first j with ei[j] > x
-    while (lo < hi) {
-        int mid = (lo + hi) >> 1;
-        if (ei[mid] > x) hi = mid; else lo = mid + 1;
-    }
-    return lo;
+__device__ __forceinline__ void lds_put(uint32_t* p, uint32_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
 // adler32.ts:34-105 over r bytes seeded with the chunk-start state (NMAX quirk)
@@ -153,104 +101,174 @@ __device__ int32_t adler_quirk_tail(const uint8_t* p, uint32_t r, uint32_t s1, u
     return (int32_t)((uint32_t)a | ((uint32_t)s2 << 16));
 }
 
-// Emit tokens' bytes into the ring -- called by a whole wave; lanes with act set
-// write their token.  Loops run to the wave's longest job; writes past a token's
-// end go to the lane's dummy slot, so output is exact without divergent branches.
-// UNROLL: four 4-byte units per step, all reads before the writes (only for copies
-// whose source cannot overlap what the step writes: no in-batch self-overlap).
-// Tokens whose destination or source crosses the ring's end go byte-serial.
-// redirected writes go to a per-thread slot past the ring (distinct banks: a shared
-// dummy address would serialize every inactive lane's store)
-#define RS_DUMMY (RS_R + 4u * threadIdx.x)
-template <bool UNROLL>
-__device__ __forceinline__ void emit_tokens(uint8_t* ring, bool act, uint32_t t, uint32_t d, uint32_t s,
-                                            uint32_t len, uint32_t dist) {
+// Write the bytes of the lanes' tokens into the ring and mark them in the finality map
+// -- called by a whole wave; lanes with `act` set write their token (d, s: ring indices
+// of destination and source; mp: map index of the destination, lb: its lap byte).
+// Every LDS access is aligned (an unaligned ds_read_b32/ds_write_b32 costs ~10x an
+// aligned one on gfx950: measured, tools/ubench/lds_cost.hip).  A token is written as
+// head bytes up to a dword boundary, whole aligned dwords, tail bytes; a copy's source
+// dwords are assembled from aligned reads with v_alignbyte.  Copies whose source cannot
+// reach what a step writes (dist >= 8 or no self-overlap) move two dwords per step,
+// all reads before the writes; the others go dword by dword.  Loops run to the wave's
+// longest job; writes past a token's end go to the lane's dummy slot, so output is
+// exact without divergent branches.  Tokens that cross the ring's (or the map's) end
+// go byte-serial.  Ring bytes are stored before their map bytes (LDS operations of a
+// wave complete in order), so a reader that sees the map byte sees the data.
+#define RS_DUMMY (RS_R + 4u * (threadIdx.x & 63u))
+#define RS_CBAR() asm volatile("" ::: "memory")
+__device__ __forceinline__ uint32_t lap_next(uint32_t lb) { return (lb & 127u) + 1u; }
+// the 4 bytes of a period-`dist` (1..3) pattern P starting at phase ph: byte j = P[(ph + j) mod dist]
+__device__ __forceinline__ uint32_t rep4(uint32_t P, uint32_t dist, uint32_t ph) {
+    const uint32_t sel = dist == 1 ? 0x00000000u
+                       : dist == 2 ? (ph ? 0x00010001u : 0x01000100u)
+                       : (ph == 0 ? 0x00020100u : ph == 1 ? 0x01000201u : 0x02010002u);
+    return __builtin_amdgcn_perm(P, P, sel);
+}
+// 4 bytes of source starting at ring index x, from two aligned reads
+__device__ __forceinline__ uint32_t src_word(const uint32_t* ring32, uint32_t x) {
+    return __builtin_amdgcn_alignbyte(ring32[(x >> 2) + 1], ring32[x >> 2], x & 3u);
+}
+__device__ __forceinline__ void emit_tokens(uint8_t* ring, uint8_t* fmap, bool act, uint32_t t, uint32_t d,
+                                            uint32_t s, uint32_t len, uint32_t dist, uint32_t mp, uint32_t lb) {
+    uint32_t* ring32 = (uint32_t*)ring;
+    uint32_t* fmap32 = (uint32_t*)fmap;
+    uint8_t* dum8 = ring + RS_DUMMY;
+    uint16_t* dum16 = (uint16_t*)(ring + RS_DUMMY);
+    uint32_t* dum32 = ring32 + RS_DUMMY / 4;
     const bool lit = (t >> 31) == 0;
-    const bool slow = act && (d + len > RS_R || (!lit && s + len + 3 > RS_R));
+    const bool slow = act && (d + len > RS_R || (!lit && (s + len > RS_R || s < 4u)) || mp + len > RS_BM);
     const bool fast = act && !slow;
     const bool per = fast && !lit && dist < 4;
     const bool cp = fast && !lit && dist >= 4;
-    const uint32_t nfull = fast && !lit ? len >> 2 : 0u;
-    const uint32_t ncp = cp ? nfull : 0u;
-    if (UNROLL) {
-        for (uint32_t u = 0; __ballot(u < ncp); u += 4) {
-            uint32_t v[4];
+    const uint32_t kd = d & 3u;
+    const uint32_t h0 = (4u - kd) & 3u;
+    const uint32_t h = fast ? (len < h0 ? len : h0) : 0u;
+    const uint32_t nf = fast ? (len - h) >> 2 : 0u;
+    const uint32_t r = fast ? len - h - 4 * nf : 0u;
+    const uint32_t e = d + h + 4 * nf;                   // tail start (aligned)
+    const uint32_t lw = lb * 0x01010101u;
+    // the first source word: head bytes of a copy, or a period's pattern
+    uint32_t H = 0;
+    if (__ballot(fast && !lit)) H = src_word(ring32, fast && !lit ? s : 0u);
+    const uint32_t Vh = lit ? t : per ? rep4(H, dist, 0) : H;
+    // head: bytes [d, d + h) -- b8 at d (odd d or one byte), b16 at the even position, and
+    // the second byte of a 2-byte head at d = 1 mod 4
+    {
+        const bool w8 = h > 0 && ((kd & 1u) || h == 1);
+        const bool w16 = h >= 2 && !(kd == 1 && h == 2);
+        const uint32_t p16 = kd == 1 ? d + 1 : d;
+        const uint32_t v16 = kd == 1 ? Vh >> 8 : Vh;
+        *(w8 ? ring + d : dum8) = (uint8_t)Vh;
+        *(w16 ? (uint16_t*)(ring + p16) : dum16) = (uint16_t)v16;
+        RS_CBAR();
+        *(w8 ? fmap + mp : dum8) = (uint8_t)lb;
+        *(w16 ? (uint16_t*)(fmap + (mp + (p16 - d))) : dum16) = (uint16_t)lw;
+        const bool w8b = kd == 1 && h == 2;
+        if (__ballot(w8b)) {
+            *(w8b ? ring + d + 1 : dum8) = (uint8_t)(Vh >> 8);
+            RS_CBAR();
+            *(w8b ? fmap + mp + 1 : dum8) = (uint8_t)lb;
+        }
+    }
+    // body: whole aligned dwords
+    const uint32_t db = (d + h) >> 2, mb = (mp + h) >> 2;   // dword indices of the first body dword
+    const uint32_t ss = s + h, sa = ss >> 2, k = ss & 3u;    // source: aligned base, byte shift
+    const bool wide = per || (cp && (dist >= 8 || dist >= len));
+    const uint32_t na = wide ? nf : 0u, nb = cp && !wide ? nf : 0u;
+    uint32_t ph = per ? (dist == 3 ? h % 3u : h & (dist - 1u)) : 0u;   // phase of body dword 0
+    for (uint32_t q = 0; __ballot(q < na); q += 2) {
+        uint32_t a[3];
 #pragma unroll
-            for (int k = 0; k < 4; ++k) v[k] = ld32(ring, u + k < ncp ? s + 4 * (u + k) : 0u);
+        for (int j = 0; j < 3; ++j) a[j] = ring32[cp && q + j <= na ? sa + q + j : 0u];
 #pragma unroll
-            for (int k = 0; k < 4; ++k) st32(ring, u + k < ncp ? d + 4 * (u + k) : RS_DUMMY, v[k]);
+        for (int j = 0; j < 2; ++j) {
+            const uint32_t v = per ? rep4(H, dist, ph) : __builtin_amdgcn_alignbyte(a[j + 1], a[j], k);
+            ph = dist == 3 ? (ph == 2 ? 0u : ph + 1u) : ph;  // +4 mod 3 = +1; mod 2 and 1: unchanged
+            *(q + j < na ? ring32 + db + q + j : dum32) = v;
         }
-    } else {
-        for (uint32_t u = 0; __ballot(u < ncp); ++u)
-            st32(ring, u < ncp ? d + 4 * u : RS_DUMMY, ld32(ring, u < ncp ? s + 4 * u : 0u));
+        RS_CBAR();
+#pragma unroll
+        for (int j = 0; j < 2; ++j) *(q + j < na ? fmap32 + mb + q + j : dum32) = lw;
     }
-    uint32_t w0 = 0, w1 = 0, w2 = 0;
-    if (__ballot(per)) {                                  // period 1..3: repeating words
-        const uint32_t p0 = ring[s], p1 = ring[ridx((int32_t)s + 1)], p2 = ring[ridx((int32_t)s + 2)];
-        const uint32_t a1 = p0 * 0x01010101u, a2 = (p0 | (p1 << 8)) * 0x00010001u;
-        w0 = dist == 1 ? a1 : dist == 2 ? a2 : p0 | (p1 << 8) | (p2 << 16) | (p0 << 24);
-        w1 = dist == 1 ? a1 : dist == 2 ? a2 : p1 | (p2 << 8) | (p0 << 16) | (p1 << 24);
-        w2 = dist == 1 ? a1 : dist == 2 ? a2 : p2 | (p0 << 8) | (p1 << 16) | (p2 << 24);
-        const uint32_t np = per ? nfull : 0u;
-        for (uint32_t u = 0; __ballot(u < np); ++u) {     // unit u repeats word u mod 3
-            const uint32_t r = u % 3u;
-            st32(ring, u < np ? d + 4 * u : RS_DUMMY, r == 0 ? w0 : r == 1 ? w1 : w2);
+    for (uint32_t q = 0; __ballot(q < nb); ++q) {
+        const bool a = q < nb;
+        const uint32_t x0 = ring32[a ? sa + q : 0u], x1 = ring32[a ? sa + q + 1 : 0u];
+        *(a ? ring32 + db + q : dum32) = __builtin_amdgcn_alignbyte(x1, x0, k);
+        RS_CBAR();
+        *(a ? fmap32 + mb + q : dum32) = lw;
+    }
+    // tail: bytes [e, e + r) -- b16 at e, b8 at e + r - 1 for odd r
+    if (__ballot(r != 0)) {
+        uint32_t T = 0;
+        if (__ballot(cp && r)) T = src_word(ring32, cp && r ? s + h + 4 * nf : 0u);
+        const uint32_t pt = dist == 3 ? (h + nf) % 3u : h & (dist - 1u);   // phase (h + 4 nf) mod dist
+        const uint32_t Vt = lit ? t >> (8 * h) : per ? rep4(H, dist, pt) : T;
+        const bool w16 = r >= 2, w8 = r & 1u;
+        *(w16 ? (uint16_t*)(ring + e) : dum16) = (uint16_t)Vt;
+        *(w8 ? ring + e + r - 1 : dum8) = (uint8_t)(Vt >> (8 * (r - 1)));
+        RS_CBAR();
+        *(w16 ? (uint16_t*)(fmap + (mp + (e - d))) : dum16) = (uint16_t)lw;
+        *(w8 ? fmap + (mp + (e - d) + r - 1) : dum8) = (uint8_t)lb;
+    }
+    if (__ballot(slow)) {                                 // across the ring's / map's end: byte-serial
+        for (uint32_t i = 0; __ballot(slow && i < len); ++i) {
+            const bool a = slow && i < len;
+            const uint32_t b = lit ? (t >> (8 * (i & 3u))) & 255u : ring[a && !lit ? ridx((int32_t)(s + i)) : 0u];
+            ring[a ? ridx((int32_t)(d + i)) : RS_DUMMY] = (uint8_t)b;
+            RS_CBAR();
+            const uint32_t m = mp + i;
+            *(a ? fmap + (m & (RS_BM - 1)) : ring + RS_DUMMY) = (uint8_t)(m >= RS_BM ? lap_next(lb) : lb);
         }
-    }
-    const uint32_t tail = fast ? (lit ? len : len & 3u) : 0u;
-    if (__ballot(tail != 0)) {
-        const uint32_t k = 4 * nfull;
-        const uint32_t r = nfull % 3u;
-        uint32_t v = ld32(ring, tail && cp ? s + k : 0u);
-        v = lit ? t : per ? (r == 0 ? w0 : r == 1 ? w1 : w2) : v;
-        st16(ring, tail >= 2 ? d + k : RS_DUMMY, v);
-        ring[tail == 1 ? d + k : tail == 3 ? d + k + 2 : RS_DUMMY] = (uint8_t)(tail == 3 ? v >> 16 : v);
-    }
-    if (__ballot(slow)) {                                 // across the ring's end: byte-serial
-        for (uint32_t k = 0; __ballot(slow && k < len); ++k) {
-            const bool a = slow && k < len;
-            const uint32_t b = lit ? (t >> (8 * (k & 3u))) & 255u : ring[a && !lit ? ridx((int32_t)(s + k)) : 0u];
-            ring[a ? ridx((int32_t)(d + k)) : RS_DUMMY] = (uint8_t)b;
-        }
-    }
-}
-
-// does the unresolved-byte bitmap have any bit in [lo, hi)?  (wave-uniform loop)
-__device__ __forceinline__ bool any_unres(const uint32_t* unres, bool act, uint32_t lo, uint32_t hi) {
-    bool hit = false;
-    const uint32_t w0 = lo >> 5, w1 = act && hi > lo ? (hi - 1) >> 5 : 0u;
-    const uint32_t nw = act && hi > lo ? w1 - w0 + 1 : 0u;
-    for (uint32_t i = 0; __ballot(i < nw); ++i) {
-        const uint32_t wd = w0 + i;
-        const uint32_t m = i < nw ? (~0u << (wd == w0 ? lo & 31u : 0u)) &
-                                    (wd == w1 && (hi & 31u) ? (1u << (hi & 31u)) - 1u : ~0u) : 0u;
-        hit = hit || (unres[i < nw ? wd : 0u] & m) != 0;
-    }
-    return hit;
-}
-// set the bits [lo, hi) (wave-uniform loop)
-__device__ __forceinline__ void mark_unres(uint32_t* unres, uint32_t* dummy, bool act, uint32_t lo, uint32_t hi) {
-    const uint32_t w0 = lo >> 5, w1 = act && hi > lo ? (hi - 1) >> 5 : 0u;
-    const uint32_t nw = act && hi > lo ? w1 - w0 + 1 : 0u;
-    for (uint32_t i = 0; __ballot(i < nw); ++i) {
-        const uint32_t wd = w0 + i;
-        const uint32_t m = i < nw ? (~0u << (wd == w0 ? lo & 31u : 0u)) &
-                                    (wd == w1 && (hi & 31u) ? (1u << (hi & 31u)) - 1u : ~0u) : 0u;
-        atomicOr(i < nw ? &unres[wd] : dummy, m);
     }
 }
 
 __device__ __forceinline__ uint32_t mod65521(uint64_t x) { return (uint32_t)(x % 65521u); }
 
-__global__ __launch_bounds__(RS_THREADS) void k_inflate_resolve(InflateArgs A, uint32_t round) {
-    __shared__ __attribute__((aligned(16))) uint8_t ring[RS_R + 4 * RS_THREADS];   // + per-thread dummies
-    __shared__ uint16_t ei[RS_THREADS];                  // inclusive output ends of the batch's tokens
-    __shared__ uint32_t unres[RS_STAGE / 32];            // bytes of matches that read this batch
-    __shared__ uint64_t remm[RS_WAVES];                  // matches left for the ordered pass
-    __shared__ uint32_t jds[RS_THREADS], jl[RS_THREADS]; // their jobs: d | s << 16, len | dist << 16
-    __shared__ uint32_t wtot[RS_WAVES];
+// wait (bounded) until *p >= v; false if the watchdog tripped (or another wave's did)
+__device__ __forceinline__ bool wait_ge(uint32_t* p, uint32_t v, uint32_t* fail) {
+    for (uint32_t n = 0;; ++n) {
+        if (lds_get(p) >= v) { lds_acquire(); return true; }
+        if (n > RS_SPIN_LIMIT || lds_get(fail)) {
+            lds_put(fail, 1u);
+            return false;
+        }
+        __builtin_amdgcn_s_sleep(1);
+    }
+}
+
+// Finality map over the bytes in flight: map byte (g mod RS_BM) holds the lap byte
+// ((g >> 12) & 127) + 1 of global position g once byte g is in the ring.  A stale value
+// is a different lap, so nothing is ever cleared; a map byte overwritten by a later lap
+// belongs to a byte already below Wf (RS_SLACK <= RS_BM), where the check is skipped.
+// Wave-uniform loop over the aligned map dwords of [lo, hi) (low 32 bits of global
+// positions) of each active lane.
+__device__ __forceinline__ uint32_t lap_of(uint32_t g) { return ((g >> 12) & 127u) + 1u; }
+__device__ __forceinline__ bool map_all(const uint8_t* fmap, bool act, uint32_t lo, uint32_t hi) {
+    const uint32_t* fmap32 = (const uint32_t*)fmap;
+    bool ok = true;
+    const uint32_t n = act ? hi - lo : 0u;               // modulo 2^32: positions are low bits
+    const uint32_t m0 = lo >> 2, nw = n ? ((lo & 3u) + n + 3u) >> 2 : 0u;
+    const uint32_t bt = ((lo + n - 1u) & 3u) + 1u;       // bytes used of the last dword
+    for (uint32_t i = 0; __ballot(i < nw); ++i) {
+        const uint32_t m = m0 + i;
+        const uint32_t bl = i == 0 ? lo & 3u : 0u, bh = i + 1 == nw ? bt : 4u;
+        const uint32_t mask = i < nw ? (bh == 4u ? ~0u : (1u << (8 * bh)) - 1u) & (~0u << (8 * bl)) : 0u;
+        const uint32_t v = fmap32[i < nw ? m & (RS_BM / 4 - 1) : 0u];
+        ok = ok && ((v ^ (lap_of(4 * m) * 0x01010101u)) & mask) == 0;
+    }
+    return ok;
+}
+__device__ __forceinline__ void publish_wf(uint32_t* wf, uint32_t v1) {
+    lds_release();
+    if ((threadIdx.x & 63u) == 0) lds_put(wf, v1);
+}
+
+__global__ __launch_bounds__(RS_THREADS) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_inflate_resolve(InflateArgs A, uint32_t round) {
+    __shared__ __attribute__((aligned(16))) uint8_t ring[RS_R + 256];   // + per-lane dummies
+    __shared__ uint64_t chain;                           // (tag of the last started group) << 32 | its end
+    __shared__ uint32_t wf, wwb, fail;                   // frontiers: final bytes, written-back bytes
+    __shared__ __attribute__((aligned(16))) uint8_t fmap[RS_BM];   // finality map of the bytes in flight
     __shared__ uint64_t red[RS_WAVES][2];
-    __shared__ uint32_t ntk_s;
 
     const uint32_t tid = threadIdx.x, lane = tid & 63u, w = tid >> 6;
     const uint32_t sid = blockIdx.x;
@@ -261,143 +279,156 @@ __global__ __launch_bounds__(RS_THREADS) void k_inflate_resolve(InflateArgs A, u
     const DSave* S = (const DSave*)A.dsave + sid;
     const bool gz = S->container == SDZ_CONTAINER_GZIP;
     const uint64_t pos0 = round == 0 ? 0 : R->pos;
-    uint64_t pos = pos0;
     uint8_t* out = A.out + A.out_off[sid];
     const uint32_t* tk = A.tokens + (uint64_t)sid * A.round_tokens;
     const uint32_t ntok = A.ntok[sid];
     const int64_t dl = S->dict_used && A.dict ? (A.dict_len > 32767 ? 32767 : A.dict_len) : 0;
     const uint8_t* dict = dl ? A.dict + (A.dict_len - dl) : nullptr;
-    uint32_t* dummy = (uint32_t*)(ring + RS_DUMMY);
 
-    // the window: output bytes [pos - 32 KiB, pos), the dictionary / zeros before 0
-    uint32_t rp = (uint32_t)(pos % RS_R);
+    // the window: output bytes [pos0 - 32 KiB, pos0), the dictionary / zeros before 0
+    const uint32_t rp0 = (uint32_t)(pos0 % RS_R);
     for (uint32_t k = tid; k < RS_WIN; k += RS_THREADS) {
-        int64_t p = (int64_t)pos - RS_WIN + k;
+        const int64_t p = (int64_t)pos0 - RS_WIN + k;
         uint32_t b = 0;
         if (p >= 0) b = round ? out[p] : 0u;
         else if (p >= -dl) b = dict[dl + p];
-        ring[ridx((int32_t)((int64_t)rp - RS_WIN + k))] = (uint8_t)b;
+        ring[ridx((int32_t)rp0 - RS_WIN + (int32_t)k)] = (uint8_t)b;
     }
+    if (tid == 0) { chain = 0xffffffff00000000ull; wf = 0; wwb = 0; fail = 0; }
+    for (uint32_t k = tid; k < RS_BM / 4; k += RS_THREADS) ((uint32_t*)fmap)[k] = 0;
+    __syncthreads();
 
     // adler32 as sums over the whole output: s1 = 1 + S, s2 = n + n S - T (mod 65521),
     // S = sum b_i, T = sum i b_i -- per-lane partials, combined once per round
-    uint64_t accS = 0, accT = 0;
-    uint32_t tnext = tid < ntok ? tk[tid] : 0u;
-    const bool timed = A.dbg && tid == 0 && sid < 8;
+    uint32_t accS = 0, accT = 0;                          // accT kept reduced mod 65521 per group
+#ifdef SDZ_TIMING
+    const bool timed = A.dbg && sid < 8 && lane == 0;
+#else
+    const bool timed = false;
+#endif
     unsigned long long tacc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     unsigned long long tlast = timed ? clock64() : 0;
 #define RS_TICK(k) do { if (timed) { unsigned long long tn = clock64(); tacc[k] += tn - tlast; tlast = tn; } } while (0)
-    for (uint32_t base = 0; base < ntok;) {
-        // 1. lengths, block prefix sum
-        const bool inr = base + tid < ntok;
+    const uint32_t ngroups = (ntok + 63u) >> 6;
+    uint32_t tnext = w * 64u + lane < ntok ? tk[w * 64u + lane] : 0u;
+    for (uint32_t g = w; g < ngroups; g += RS_WAVES) {
+        const uint32_t ti = g * 64u + lane;
+        const bool valid = ti < ntok;
         const uint32_t t = tnext;
+        tnext = ti + RS_THREADS < ntok ? tk[ti + RS_THREADS] : 0u;
         const bool ism = (t >> 31) != 0;
-        const uint32_t len = !inr ? 0u : ism ? ((t >> 16) & 255u) + 3u : ((t >> 24) & 3u) + 1u;
-        const uint32_t dist = (t & 0x7fffu) + 1u;
-        uint32_t incl = wave_incl_scan(len);
-        if (lane == 63) wtot[w] = incl;
-        if (tid == 0) ntk_s = RS_THREADS;
-        if (tid < RS_STAGE / 32) unres[tid] = 0;
-        __syncthreads();
-        RS_TICK(1);
-        for (uint32_t q = 0; q < w; ++q) incl += wtot[q];
+        const uint32_t len = !valid ? 0u : ism ? ((t >> 16) & 255u) + 3u : ((t >> 24) & 3u) + 1u;
+        const uint32_t dist = ism ? (t & 0x7fffu) + 1u : 0u;
+        const uint32_t incl = wave_incl_scan(len);
+        const uint32_t T = lane_at(incl, 63);
         const uint32_t off = incl - len;
-        const bool take = inr && incl <= RS_STAGE;       // a prefix: token 0 always fits (len <= 258)
-        ei[tid] = (uint16_t)(incl < RS_STAGE + 258 ? incl : RS_STAGE + 258);
-        const uint64_t nt = ~__ballot(take);
-        if (nt && lane == (uint32_t)__builtin_ctzll(nt)) atomicMin(&ntk_s, 64u * w + lane);
+        RS_TICK(0);
 
-        // 2. literals and matches with their source before the batch; matches reading
-        //    this batch mark their bytes unresolved
-        const bool gen0 = take && (!ism || dist >= off + len);
-        const bool pend = take && ism && !gen0;
-        const uint32_t d = ridx((int32_t)(rp + off));
-        const uint32_t s = ridx((int32_t)rp + (int32_t)off - (int32_t)dist);
-        emit_tokens<true>(ring, gen0, t, d, s, len, dist);
-        mark_unres(unres, dummy, pend, off, off + len);
-        RS_TICK(2);
-        __syncthreads();
-        RS_TICK(3);
-        const uint32_t ntk = ntk_s;
-        const uint32_t B = ei[ntk - 1];
-        tnext = base + ntk + tid < ntok ? tk[base + ntk + tid] : 0u;
-
-        // 3. matches reading only final bytes go in parallel; the rest, in token order
-        const int32_t sb = (int32_t)off - (int32_t)dist;
-        const uint32_t lo = sb > 0 ? (uint32_t)sb : 0u;
-        const uint32_t hi = (uint32_t)(sb + (int32_t)len < (int32_t)off ? sb + (int32_t)len : (int32_t)off);
-        bool ready = false;
-        uint64_t pm = __ballot(pend);
-        if (pm) {
-            ready = pend && !any_unres(unres, pend, lo, hi);
-            emit_tokens<false>(ring, ready, t, d, s, len, dist);
+        // 1. the group's start from its predecessor; pass ours on
+        uint32_t Sg = 0;
+        for (uint32_t n = 0;; ++n) {
+            const uint64_t c = lds_get64(&chain);
+            if ((uint32_t)(c >> 32) == g - 1u) { Sg = uni((uint32_t)c); break; }
+            if (n > RS_SPIN_LIMIT || lds_get(&fail)) { lds_put(&fail, 1u); break; }
+            __builtin_amdgcn_s_sleep(1);
         }
-        const uint64_t rm = __ballot(pend && !ready);
-        if (lane == 0) remm[w] = rm;
-        if (pend && !ready) { jds[tid] = d | (s << 16); jl[tid] = len | (dist << 16); }
-        __syncthreads();
-        RS_TICK(4);
-        const uint64_t r0 = remm[0], r1 = remm[1], r2 = remm[2], r3 = remm[3];
-        if (r0 | r1 | r2 | r3) {
-            if (w == 0) {                                 // ordered pass: one match at a time,
-                for (int q = 0; q < RS_WAVES; ++q) {      // 64 bytes per step across the wave
-                    uint64_t m = q == 0 ? r0 : q == 1 ? r1 : q == 2 ? r2 : r3;
-                    while (m) {
-                        const uint32_t i = 64u * q + (uint32_t)__builtin_ctzll(m);
-                        m &= m - 1;
-                        const uint32_t jdd = jds[i] & 0xffffu, jss = jds[i] >> 16, jll = jl[i];
-                        const uint32_t L = jll & 0xffffu, D = jll >> 16;
-                        for (uint32_t k = lane; k < L; k += 64) {
-                            uint32_t km = k;
-                            if (D < L && k >= D) {        // overlapping: byte k repeats byte k mod D
-                                int32_t r = (int32_t)k - (int32_t)((float)k * __builtin_amdgcn_rcpf((float)D)) * (int32_t)D;
-                                r += r < 0 ? (int32_t)D : 0;
-                                r -= r >= (int32_t)D ? (int32_t)D : 0;
-                                km = (uint32_t)r;
-                            }
-                            ring[ridx((int32_t)(jdd + k))] = ring[ridx((int32_t)(jss + km))];
-                        }
-                    }
+        if (lane == 0) __hip_atomic_store(&chain, ((uint64_t)g << 32) | (Sg + T), __ATOMIC_RELAXED,
+                                          __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (lds_get(&fail)) break;
+        RS_TICK(1);
+
+        // 2. copy rounds
+        const uint32_t sr = (uint32_t)((rp0 + (uint64_t)Sg) % RS_R);   // ring index of byte Sg
+        const uint32_t dst = Sg + off, dend = dst + len;
+        const int32_t src = (int32_t)dst - (int32_t)dist;             // round-relative (may be < 0)
+        const int32_t need = ism ? src + (int32_t)(len < dist ? len : dist) : INT32_MIN;
+        const uint32_t d = ridx((int32_t)(sr + off));
+        const uint32_t s = ridx((int32_t)(sr + off) - (int32_t)dist);
+        const uint32_t gd = (uint32_t)pos0 + dst;                       // low bits of the global position
+        const uint32_t mp = gd & (RS_BM - 1), lb = lap_of(gd);
+        bool done = len == 0;
+        uint64_t nd = __ballot(!done);
+        uint32_t pre = nd ? lane_at(off, (uint32_t)__builtin_ctzll(nd)) : T;   // finished prefix
+        for (uint32_t n = 0; nd; ++n) {
+            uint32_t cwf = lds_get(&wf);
+            const uint32_t cwb = lds_get(&wwb);
+            if (cwf >= Sg && cwf < Sg + pre) {            // head: publish our finished prefix
+                publish_wf(&wf, Sg + pre);
+                cwf = Sg + pre;
+            }
+            const bool room = !done && dend <= cwf + RS_SLACK && dend <= cwb + RS_R;
+            const bool inwin = need <= (int32_t)cwf;
+            const uint32_t blo = src > (int32_t)cwf ? (uint32_t)src : cwf;
+            const uint32_t g32 = (uint32_t)pos0;
+            const bool rdy = room && (inwin || map_all(fmap, room && !inwin, g32 + blo, g32 + (uint32_t)need));
+            if (__ballot(rdy)) {
+                RS_CBAR();
+                emit_tokens(ring, fmap, rdy, t, d, s, len, dist, mp, lb);
+                done = done || rdy;
+                nd = __ballot(!done);
+                pre = nd ? lane_at(off, (uint32_t)__builtin_ctzll(nd)) : T;
+                n = 0;
+                if (timed) tacc[6]++;
+            } else {
+                if (timed) tacc[7]++;
+                if (n > RS_SPIN_LIMIT || lds_get(&fail)) { lds_put(&fail, 1u); break; }
+                __builtin_amdgcn_s_sleep(1);
+            }
+        }
+        if (lds_get(&fail)) break;
+        RS_TICK(2);
+        // finality: publish now if we are the head (no one else can move wf past Sg)
+        const uint32_t cwf = lds_get(&wf);
+        const bool pub = cwf >= Sg;
+        if (pub) publish_wf(&wf, Sg + T);
+
+        // 3. write back as dwords; adler partials
+        {
+            const uint64_t a0 = pos0 + Sg, a1 = a0 + T;
+            const uint32_t h = (uint32_t)(a0 & 3u);
+            const uint32_t nq = (uint32_t)(((a1 + 3u) >> 2) - (a0 >> 2));
+            uint32_t* dstw = (uint32_t*)(out + (a0 - h));
+            const uint32_t* ring32 = (const uint32_t*)ring;
+            const int32_t rb0 = (int32_t)sr - (int32_t)h;  // ring index of the first dword (4-aligned)
+            const uint32_t tl = (uint32_t)(a1 & 3u);
+            uint32_t gi0 = 0;
+            if (!gz) gi0 = mod65521(a0 - h);
+            for (uint32_t q = lane; q < nq; q += 64) {
+                const uint32_t v = ring32[ridx(rb0 + 4 * (int32_t)q) >> 2];
+                const uint32_t blo = q == 0 ? h : 0u;
+                const uint32_t bhi = q + 1 < nq || tl == 0 ? 4u : tl;
+                if (blo == 0 && bhi == 4) dstw[q] = v;
+                else for (uint32_t bb = blo; bb < bhi; ++bb) ((uint8_t*)(dstw + q))[bb] = (uint8_t)(v >> (8 * bb));
+                if (!gz) {
+                    const uint32_t m = (bhi == 4u ? ~0u : (1u << (8 * bhi)) - 1u) & (~0u << (8 * blo));
+                    const uint32_t vm = v & m;
+                    uint32_t gi = gi0 + 4 * q;            // global index of byte 0 of this dword, mod 65521
+                    gi -= gi >= 65521u ? 65521u : 0u;
+                    const uint32_t s4 = __builtin_amdgcn_udot4(vm, 0x01010101u, 0u, false);
+                    accS += s4;
+                    accT = (accT + gi * s4 + __builtin_amdgcn_udot4(vm, 0x03020100u, 0u, false)) % 65521u;
                 }
             }
-            __syncthreads();
         }
-        RS_TICK(5);
 
-        // 4. write back as dwords from the dword-aligned start; adler partials
-        const uint32_t head = rp & 3u;
-        const uint32_t nd = (head + B + 3u) >> 2;
-        const uint32_t rd0 = (rp - head) >> 2;
-        uint32_t* dstw = (uint32_t*)(out + (pos - head));
-        const uint32_t* ring32 = (const uint32_t*)ring;
-        const uint32_t posm = (uint32_t)(pos % 65521u);
-        for (uint32_t q = tid; q < nd; q += RS_THREADS) {
-            uint32_t ri = rd0 + q;
-            ri -= ri >= RS_R / 4 ? RS_R / 4 : 0;
-            const uint32_t v = ring32[ri];
-            if (q + 1 < nd || ((head + B) & 3u) == 0) dstw[q] = v;
-            else for (uint32_t bb = 0; bb < ((head + B) & 3u); ++bb) ((uint8_t*)(dstw + q))[bb] = (uint8_t)(v >> (8 * bb));
-            if (!gz) {
-                const uint32_t blo = q == 0 ? head : 0u;
-                const uint32_t bhi = q + 1 < nd ? 4u : (((head + B) & 3u) ? ((head + B) & 3u) : 4u);
-                const uint32_t m = (bhi == 4u ? ~0u : (1u << (8 * bhi)) - 1u) & (~0u << (8 * blo));
-                const uint32_t vm = v & m;
-                // global index of byte 0 of this dword, mod 65521
-                uint32_t gi = posm + 65521u + 4 * q - head;
-                gi -= gi >= 65521u ? 65521u : 0u;
-                gi -= gi >= 65521u ? 65521u : 0u;
-                const uint32_t s4 = __builtin_amdgcn_udot4(vm, 0x01010101u, 0u, false);
-                accS += s4;
-                accT += (uint64_t)gi * s4 + __builtin_amdgcn_udot4(vm, 0x03020100u, 0u, false);
-            }
+        RS_TICK(3);
+        // 4. frontiers, in group order
+        if (!pub) {
+            if (!wait_ge(&wf, Sg, &fail)) break;
+            publish_wf(&wf, Sg + T);
         }
-        RS_TICK(6);
-        pos += B;
-        rp = ridx((int32_t)(rp + B));
-        base += ntk;
+        RS_TICK(4);
+        if (!wait_ge(&wwb, Sg, &fail)) break;
+        lds_release();                                    // our ring reads are complete
+        if (lane == 0) lds_put(&wwb, Sg + T);
+        RS_TICK(5);
     }
     if (timed) for (int k = 0; k < 8; ++k) atomicAdd(&A.dbg[k], tacc[k]);
+
     // combine the adler partials of this round
+    __syncthreads();
+    const bool failed = fail != 0 || (round && R->ck != 0);   // sticky across rounds
+    const uint64_t pos = pos0 + (uint64_t)(uint32_t)chain;   // end of the last group (all published)
     uint32_t S_all = 0, T_all = 0;
     if (!gz) {
         uint64_t a = accS, b = accT;
@@ -412,13 +443,13 @@ __global__ __launch_bounds__(RS_THREADS) void k_inflate_resolve(InflateArgs A, u
         T_all = mod65521(tT);
     }
     __syncthreads();                                     // R->s1 / s2 were read above
-    if (tid == 0) { R->pos = pos; R->s1 = S_all; R->s2 = T_all; }
+    if (tid == 0) { R->pos = pos; R->s1 = S_all; R->s2 = T_all; R->ck = failed ? 1 : 0; }
     if (flag != 1) return;
     // Inflater chunk-wise checksum (16 KiB chunks, adler32.ts NMAX quirk): only a final
     // chunk of 5552 or 11104 bytes differs from the plain adler32; then replay that
     // chunk from the state at its start, S and T of the bytes before it
     const uint32_t r = (uint32_t)(pos & 16383u);
-    const bool quirk = !gz && (r == 5552u || r == 11104u);
+    const bool quirk = !gz && !failed && (r == 5552u || r == 11104u);
     uint32_t snapS = S_all, snapT = T_all;
     if (quirk) {
         uint64_t a = 0, b = 0;
@@ -441,7 +472,7 @@ __global__ __launch_bounds__(RS_THREADS) void k_inflate_resolve(InflateArgs A, u
     if (tid != 0) return;
     // final: record + verdicts (sd-inflate.ts:134-179); gzip's crc32 comes from k_inflate_finalize
     sdz_inflate_record Rc;
-    Rc.status = S->status;
+    Rc.status = failed ? SDZ_INTERNAL : S->status;
     Rc.zmsg = S->zmsg;
     Rc.out_len = pos;
     uint64_t ib = S->bitpos;
@@ -465,7 +496,7 @@ __global__ __launch_bounds__(RS_THREADS) void k_inflate_resolve(InflateArgs A, u
     Rc.name_off = S->name_off;
     Rc.name_len = S->name_len;
     Rc.container = (uint8_t)S->container;
-    bool complete = S->mode == LM_DONE && (S->status == SDZ_OK || S->status == SDZ_TRAILING);
+    bool complete = !failed && S->mode == LM_DONE && (S->status == SDZ_OK || S->status == SDZ_TRAILING);
     Rc.complete = complete ? 1 : 0;
     uint8_t cv = S->stored_ck == 0 ? SDZ_UNCHECKED : ((have && S->stored_ck == running) ? SDZ_MATCH : SDZ_MISMATCH);
     uint8_t sv = S->stored_size == 0 ? SDZ_UNCHECKED

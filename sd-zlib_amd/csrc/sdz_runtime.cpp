@@ -299,8 +299,12 @@ int sdz_deflate_batch_device(const uint8_t* in, const uint64_t* in_off, const ui
     hipStream_t s = (hipStream_t)stream;
     std::lock_guard<std::mutex> lk(g_mu);
     // per-stream state slabs: process in sub-batches so the slab pool stays bounded
-    const uint32_t kMaxSlabs = 16384;
+    // one lane per stream: fill the chip (64 Ki lanes = one wave per SIMD) when a
+    // quarter of free HBM holds the slabs, else as many as it does
     uint64_t slab = deflate_state_bytes();
+    size_t mem_free = 0, mem_total = 0;
+    if (hipMemGetInfo(&mem_free, &mem_total) != hipSuccess) mem_free = 16ull << 30;
+    const uint32_t kMaxSlabs = (uint32_t)std::max<uint64_t>(1024, std::min<uint64_t>(65536, mem_free / 4 / slab));
     uint32_t chunk = std::min(n, kMaxSlabs);
     void* state = nullptr;
     if (int rc = g_deflate_state.get((size_t)chunk * slab, &state)) return rc;

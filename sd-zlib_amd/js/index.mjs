@@ -85,6 +85,7 @@ function throwFor(r) {
 	case "NEED_DICT": throw new Error("Custom dictionary required for this data");
 	case "DICT_MISMATCH": throw new Error("Custom dictionary is not valid for this data");
 	case "TRAILING": throw new Error("inflate error: trailing data after end of stream");
+	case "INTERNAL": throw new Error("inflate error: engine watchdog");
 	default: break;
 	}
 }

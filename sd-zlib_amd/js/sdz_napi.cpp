@@ -64,6 +64,7 @@ const char* status_name(int s) {
     case SDZ_TRUNCATED: return "TRUNCATED";
     case SDZ_OUT_OVERFLOW: return "OUT_OVERFLOW";
     case SDZ_TRAILING: return "TRAILING";
+    case SDZ_INTERNAL: return "INTERNAL";
     case SDZ_TOO_SMALL: return "TOO_SMALL";
     default: return "BAD_RECORD";
     }

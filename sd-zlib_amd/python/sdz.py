@@ -16,12 +16,12 @@ import os
 import time
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(os.path.dirname(_HERE), "lib", "libsdz.so")
+LIB_PATH = os.environ.get("SDZ_LIB") or os.path.join(os.path.dirname(_HERE), "lib", "libsdz.so")
 
 FMT_AUTO, FMT_RAW, FMT_CONTAINER = 0, 1, 2
 DEFLATE_FORMATS = {"raw": 0, "deflate": 1, "gzip": 2}
 STATUS = {0: "OK", 1: "DATA_ERROR", 2: "NEED_DICT", 3: "DICT_MISMATCH", 4: "TRUNCATED",
-          5: "OUT_OVERFLOW", 6: "TRAILING", 7: "TOO_SMALL", 8: "BAD_RECORD"}
+          5: "OUT_OVERFLOW", 6: "TRAILING", 7: "TOO_SMALL", 8: "BAD_RECORD", 9: "INTERNAL"}
 VERDICT = ("unchecked", "match", "mismatch")
 
 

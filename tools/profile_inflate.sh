@@ -18,11 +18,17 @@ step() {  # name, rocprof args...
     if [ $rc -ne 0 ]; then tail -20 $OUT/$name.log; fi
     return $rc
 }
-rocprofv3 -L > $OUT/counters.txt 2>&1 || true
-step kt --kernel-trace --stats || exit 1
-step pmc_fetch --pmc FETCH_SIZE || exit 1
-step pmc_write --pmc WRITE_SIZE || exit 1
-step pmc_sq1 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVE_CYCLES SQ_BUSY_CYCLES || true
-step pmc_sq2 --pmc SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_BRANCH SQ_LDS_BANK_CONFLICT GRBM_GUI_ACTIVE || true
-step pmc_tcc --pmc TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_sum || true
+PASSES=${PASSES:-"kt fetch write sq1 sq2 tcc"}
+for p in $PASSES; do
+  case $p in
+    kt) step kt --kernel-trace --stats || exit 1 ;;
+    fetch) step pmc_fetch --pmc FETCH_SIZE || exit 1 ;;
+    write) step pmc_write --pmc WRITE_SIZE || exit 1 ;;
+    sq1) step pmc_sq1 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVE_CYCLES SQ_BUSY_CYCLES || exit 1 ;;
+    sq2) step pmc_sq2 --pmc SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_BRANCH SQ_LDS_BANK_CONFLICT GRBM_GUI_ACTIVE || exit 1 ;;
+    sq3) step pmc_sq3 --pmc SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_SCA SQ_INST_CYCLES_SALU SQ_WAIT_INST_LDS SQ_LDS_IDX_ACTIVE || exit 1 ;;
+    tcc) step pmc_tcc --pmc TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_sum || exit 1 ;;
+  esac
+done
+python3 tools/pmc_summary.py $OUT > $OUT/pmc_summary.txt 2>&1 || true
 exit 0
