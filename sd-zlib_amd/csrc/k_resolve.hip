@@ -229,7 +229,7 @@ __device__ __forceinline__ bool wait_ge(uint32_t* p, uint32_t v, uint32_t* fail)
     for (uint32_t n = 0;; ++n) {
         if (lds_get(p) >= v) { lds_acquire(); return true; }
         if (n > RS_SPIN_LIMIT || lds_get(fail)) {
-            lds_put(fail, 1u);
+            if (!lds_get(fail)) lds_put(fail, 2u | (v << 4));   // site | position, for diagnosis
             return false;
         }
         __builtin_amdgcn_s_sleep(1);
@@ -329,7 +329,7 @@ __global__ __launch_bounds__(RS_THREADS) __attribute__((amdgpu_waves_per_eu(8, 8
         for (uint32_t n = 0;; ++n) {
             const uint64_t c = lds_get64(&chain);
             if ((uint32_t)(c >> 32) == g - 1u) { Sg = uni((uint32_t)c); break; }
-            if (n > RS_SPIN_LIMIT || lds_get(&fail)) { lds_put(&fail, 1u); break; }
+            if (n > RS_SPIN_LIMIT || lds_get(&fail)) { if (!lds_get(&fail)) lds_put(&fail, 1u | (g << 4)); break; }
             __builtin_amdgcn_s_sleep(1);
         }
         if (lane == 0) __hip_atomic_store(&chain, ((uint64_t)g << 32) | (Sg + T), __ATOMIC_RELAXED,
@@ -371,7 +371,7 @@ __global__ __launch_bounds__(RS_THREADS) __attribute__((amdgpu_waves_per_eu(8, 8
                 if (timed) tacc[6]++;
             } else {
                 if (timed) tacc[7]++;
-                if (n > RS_SPIN_LIMIT || lds_get(&fail)) { lds_put(&fail, 1u); break; }
+                if (n > RS_SPIN_LIMIT || lds_get(&fail)) { if (!lds_get(&fail)) lds_put(&fail, 3u | (Sg << 4)); break; }
                 __builtin_amdgcn_s_sleep(1);
             }
         }
@@ -473,7 +473,7 @@ __global__ __launch_bounds__(RS_THREADS) __attribute__((amdgpu_waves_per_eu(8, 8
     // final: record + verdicts (sd-inflate.ts:134-179); gzip's crc32 comes from k_inflate_finalize
     sdz_inflate_record Rc;
     Rc.status = failed ? SDZ_INTERNAL : S->status;
-    Rc.zmsg = S->zmsg;
+    Rc.zmsg = failed ? (int32_t)fail : S->zmsg;      // watchdog: site | position << 4
     Rc.out_len = pos;
     uint64_t ib = S->bitpos;
     uint64_t ilen = A.in_len[sid];

@@ -131,7 +131,9 @@ def device_count():
 
 def _record_dict(r, data, src=None):
     d = {
-        "status": STATUS.get(r.status, r.status), "zmsg": zmsg(r.zmsg), "out_len": r.out_len,
+        "status": STATUS.get(r.status, r.status),
+        "zmsg": zmsg(r.zmsg) if r.status != 9 else "watchdog %d@%d" % (r.zmsg & 15, r.zmsg >> 4),
+        "out_len": r.out_len,
         "in_used": r.in_used, "stored_checksum": r.stored_checksum,
         "running_checksum": r.running_checksum, "stored_size": r.stored_size,
         "mtime": r.mtime, "container": ("raw", "deflate", "gzip")[r.container],
