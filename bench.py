@@ -131,7 +131,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--streams", type=int, default=65536, help="streams per GPU (C2: 65536)")
     ap.add_argument("--cpu-seconds", type=float, default=1.5)
-    ap.add_argument("--deflate-streams", type=int, default=512,
+    ap.add_argument("--deflate-streams", type=int, default=65536,
                     help="streams for the deflate leg (64 KiB slices, L6); 0 disables")
     ap.add_argument("--deflate-steps", type=int, default=1)
     args = ap.parse_args()
