@@ -119,10 +119,10 @@ __device__ int32_t adler_quirk_tail(const uint8_t* p, uint32_t r, uint32_t s1, u
 __device__ __forceinline__ uint32_t lap_next(uint32_t lb) { return (lb & 127u) + 1u; }
 // the 4 bytes of a period-`dist` (1..3) pattern P starting at phase ph: byte j = P[(ph + j) mod dist]
 __device__ __forceinline__ uint32_t rep4(uint32_t P, uint32_t dist, uint32_t ph) {
-    const uint32_t sel = dist == 1 ? 0x00000000u
-                       : dist == 2 ? (ph ? 0x00010001u : 0x01000100u)
-                       : (ph == 0 ? 0x00020100u : ph == 1 ? 0x01000201u : 0x02010002u);
-    return __builtin_amdgcn_perm(P, P, sel);
+    // selector bytes (ph + j) mod dist = bytes ph..ph+3 of the sequence 0,1,2,0,1,2,0,1 (or 0,1,...)
+    const uint32_t lo = dist == 3 ? 0x00020100u : dist == 2 ? 0x01000100u : 0u;
+    const uint32_t hi = dist == 3 ? 0x01000201u : lo;
+    return __builtin_amdgcn_perm(P, P, __builtin_amdgcn_alignbyte(hi, lo, ph));
 }
 // 4 bytes of source starting at ring index x, from two aligned reads
 __device__ __forceinline__ uint32_t src_word(const uint32_t* ring32, uint32_t x) {
@@ -287,6 +287,7 @@ __global__ __launch_bounds__(RS_THREADS) __attribute__((amdgpu_waves_per_eu(8, 8
 
     // the window: output bytes [pos0 - 32 KiB, pos0), the dictionary / zeros before 0
     const uint32_t rp0 = (uint32_t)(pos0 % RS_R);
+    const uint32_t pm0 = (uint32_t)(pos0 % 65521u);
     for (uint32_t k = tid; k < RS_WIN; k += RS_THREADS) {
         const int64_t p = (int64_t)pos0 - RS_WIN + k;
         uint32_t b = 0;
@@ -338,7 +339,7 @@ __global__ __launch_bounds__(RS_THREADS) __attribute__((amdgpu_waves_per_eu(8, 8
         RS_TICK(1);
 
         // 2. copy rounds
-        const uint32_t sr = (uint32_t)((rp0 + (uint64_t)Sg) % RS_R);   // ring index of byte Sg
+        const uint32_t sr = (rp0 + Sg) % RS_R;                         // ring index of byte Sg (u32: Sg < 2^26)
         const uint32_t dst = Sg + off, dend = dst + len;
         const int32_t src = (int32_t)dst - (int32_t)dist;             // round-relative (may be < 0)
         const int32_t need = ism ? src + (int32_t)(len < dist ? len : dist) : INT32_MIN;
@@ -392,7 +393,7 @@ __global__ __launch_bounds__(RS_THREADS) __attribute__((amdgpu_waves_per_eu(8, 8
             const int32_t rb0 = (int32_t)sr - (int32_t)h;  // ring index of the first dword (4-aligned)
             const uint32_t tl = (uint32_t)(a1 & 3u);
             uint32_t gi0 = 0;
-            if (!gz) gi0 = mod65521(a0 - h);
+            if (!gz) gi0 = (pm0 + 65521u + Sg - h) % 65521u;
             for (uint32_t q = lane; q < nq; q += 64) {
                 const uint32_t v = ring32[ridx(rb0 + 4 * (int32_t)q) >> 2];
                 const uint32_t blo = q == 0 ? h : 0u;
