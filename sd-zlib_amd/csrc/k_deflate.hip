@@ -20,6 +20,8 @@
 namespace sdz {
 
 #define DF_THREADS 64
+#define GLB __attribute__((address_space(1)))   // global memory (no flat ops)
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 #define W_SIZE 32768
 #define W_MASK (W_SIZE - 1)
 #define WINDOW_SIZE (2 * W_SIZE)
@@ -65,7 +67,9 @@ struct DTables {
     uint16_t base_dist[30];
     uint16_t static_ltree[288 * 2];
     uint16_t static_dtree[30 * 2];
+    uint8_t extra_lbits[29], extra_dbits[30], extra_blbits[19];
 };
+__device__ DTables g_dt;                                     // built once per launch (k_deflate_tables)
 __constant__ uint8_t c_extra_lbits[29] = { 0, 0, 0, 0, 0, 0, 0, 0, 1, 1, 1, 1, 2, 2, 2, 2, 3, 3, 3, 3, 4, 4, 4, 4, 5, 5, 5, 5, 0 };
 __constant__ uint8_t c_extra_dbits[30] = { 0, 0, 0, 0, 1, 1, 2, 2, 3, 3, 4, 4, 5, 5, 6, 6, 7, 7, 8, 8, 9, 9, 10, 10, 11, 11, 12, 12, 13, 13 };
 __constant__ uint8_t c_extra_blbits[19] = { 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 2, 3, 7 };
@@ -81,8 +85,12 @@ __device__ __forceinline__ uint32_t bitrev_n(uint32_t code, int len) {
 }
 
 // build the shared tables in LDS (zlib trees.h derivation, deftree.ts literals)
-__device__ void build_tables(DTables& T) {
-    if (threadIdx.x == 0) {
+__global__ void k_deflate_tables() {
+    DTables& T = g_dt;
+    {
+        for (int i = 0; i < 29; ++i) T.extra_lbits[i] = c_extra_lbits[i];
+        for (int i = 0; i < 30; ++i) T.extra_dbits[i] = c_extra_dbits[i];
+        for (int i = 0; i < 19; ++i) T.extra_blbits[i] = c_extra_blbits[i];
         int length = 0, code, n, dist;
         for (code = 0; code < 28; code++) {
             T.base_length[code] = (uint16_t)length;
@@ -115,16 +123,15 @@ __device__ void build_tables(DTables& T) {
         }
         for (n = 0; n < 30; n++) { T.static_dtree[n * 2 + 1] = 5; T.static_dtree[n * 2] = (uint16_t)bitrev_n((uint32_t)n, 5); }
     }
-    __syncthreads();
 }
 
 // scalar state of one stream (deflate.ts:102-194), registers
 struct DS {
-    DSlab* S;
-    const DTables* T;
-    const uint8_t* in;
+    GLB DSlab* S;
+    const GLB DTables* T;
+    const GLB uint8_t* in;
     uint64_t in_len, in_pos;
-    uint8_t* out;
+    GLB uint8_t* out;
     uint64_t out_cap, out_len;
     int pending;
     int ins_h, block_start, match_length, match_available, strstart, match_start, lookahead, prev_length;
@@ -160,20 +167,20 @@ __device__ __forceinline__ void send_bits(DS& s, uint32_t value, int length) {
         s.bi_valid += length;
     }
 }
-__device__ __forceinline__ void send_code(DS& s, int c, const uint16_t* tree) {
+__device__ __forceinline__ void send_code(DS& s, int c, const GLB uint16_t* tree) {
     send_bits(s, tree[c * 2], tree[c * 2 + 1]);
 }
 
 // ------------------------------------------------------------------ trees (deftree.ts)
 
-__device__ __forceinline__ bool smaller(const uint16_t* tree, int n, int m, const uint16_t* depth) {
+__device__ __forceinline__ bool smaller(const GLB uint16_t* tree, int n, int m, const GLB uint16_t* depth) {
     int tn = tree[n * 2], tm = tree[m * 2];
     return tn < tm || (tn == tm && depth[n] <= depth[m]);
 }
 
-__device__ void pqdownheap(DS& s, uint16_t* tree, int k) {                 // deflate.ts:241-263
-    uint16_t* heap = s.S->heap;
-    const uint16_t* depth = s.S->depth;
+__device__ void pqdownheap(DS& s, GLB uint16_t* tree, int k) {                 // deflate.ts:241-263
+    auto* heap = s.S->heap;
+    auto* depth = s.S->depth;
     int v = heap[k];
     int j = k << 1;
     while (j <= s.heap_len) {
@@ -187,10 +194,10 @@ __device__ void pqdownheap(DS& s, uint16_t* tree, int k) {                 // de
 }
 
 // deftree.ts:60-132 gen_bitlen
-__device__ void gen_bitlen(DS& s, uint16_t* tree, int max_code, const uint16_t* stree,
-                           const uint8_t* extra, int base, int max_length) {
-    uint16_t* heap = s.S->heap;
-    uint16_t* bl_count = s.S->bl_count;
+__device__ void gen_bitlen(DS& s, GLB uint16_t* tree, int max_code, const GLB uint16_t* stree,
+                           const GLB uint8_t* extra, int base, int max_length) {
+    auto* heap = s.S->heap;
+    auto* bl_count = s.S->bl_count;
     int h, n, m, bits, xbits, f, overflow = 0;
     for (bits = 0; bits <= 15; bits++) bl_count[bits] = 0;
     tree[heap[s.heap_max] * 2 + 1] = 0;
@@ -231,9 +238,9 @@ __device__ void gen_bitlen(DS& s, uint16_t* tree, int max_code, const uint16_t* 
 }
 
 // deftree.ts:155-182 gen_codes
-__device__ void gen_codes(DS& s, uint16_t* tree, int max_code) {
-    uint16_t* next_code = s.S->next_code;
-    const uint16_t* bl_count = s.S->bl_count;
+__device__ void gen_codes(DS& s, GLB uint16_t* tree, int max_code) {
+    auto* next_code = s.S->next_code;
+    auto* bl_count = s.S->bl_count;
     int code = 0;
     for (int bits = 1; bits <= 15; bits++) {
         code = (code + bl_count[bits - 1]) << 1;
@@ -247,10 +254,10 @@ __device__ void gen_codes(DS& s, uint16_t* tree, int max_code) {
 }
 
 // deftree.ts:190-267 build_tree; returns max_code
-__device__ int build_tree(DS& s, uint16_t* tree, const uint16_t* stree, const uint8_t* extra,
+__device__ int build_tree(DS& s, GLB uint16_t* tree, const GLB uint16_t* stree, const GLB uint8_t* extra,
                           int base, int elems, int max_length) {
-    uint16_t* heap = s.S->heap;
-    uint16_t* depth = s.S->depth;
+    auto* heap = s.S->heap;
+    auto* depth = s.S->depth;
     int n, m, max_code = -1, node;
     s.heap_len = 0;
     s.heap_max = HEAP_SIZE;
@@ -288,8 +295,8 @@ __device__ int build_tree(DS& s, uint16_t* tree, const uint16_t* stree, const ui
 }
 
 // deflate.ts:267-312 scan_tree
-__device__ void scan_tree(DS& s, uint16_t* tree, int max_code) {
-    uint16_t* bl = s.S->bltree;
+__device__ void scan_tree(DS& s, GLB uint16_t* tree, int max_code) {
+    auto* bl = s.S->bltree;
     int prevlen = -1, curlen, nextlen = tree[1], count = 0, max_count = 7, min_count = 4;
     if (nextlen == 0) { max_count = 138; min_count = 3; }
     tree[(max_code + 1) * 2 + 1] = 0xffff;
@@ -310,8 +317,8 @@ __device__ void scan_tree(DS& s, uint16_t* tree, int max_code) {
 }
 
 // deflate.ts:378-429 send_tree
-__device__ void send_tree(DS& s, const uint16_t* tree, int max_code) {
-    const uint16_t* bl = s.S->bltree;
+__device__ void send_tree(DS& s, const GLB uint16_t* tree, int max_code) {
+    auto* bl = s.S->bltree;
     int prevlen = -1, curlen, nextlen = tree[1], count = 0, max_count = 7, min_count = 4;
     if (nextlen == 0) { max_count = 138; min_count = 3; }
     for (int n = 0; n <= max_code; n++) {
@@ -333,7 +340,7 @@ __device__ void send_tree(DS& s, const uint16_t* tree, int max_code) {
     }
 }
 
-__device__ __forceinline__ int d_code(const DTables* T, int dist) {
+__device__ __forceinline__ int d_code(const GLB DTables* T, int dist) {
     return dist < 256 ? T->dist_code[dist] : T->dist_code[256 + (dist >> 7)];
 }
 
@@ -349,7 +356,7 @@ __device__ void init_block(DS& s) {
 
 // deflate.ts:488-524 _tr_tally (TRUNCATE_BLOCK heuristic kept)
 __device__ __forceinline__ bool tr_tally(DS& s, int dist, int lc) {
-    uint8_t* pb = s.S->pending;
+    auto* pb = s.S->pending;
     pb[D_BUF + s.last_lit * 2] = (uint8_t)(dist >> 8);
     pb[D_BUF + s.last_lit * 2 + 1] = (uint8_t)dist;
     pb[L_BUF + s.last_lit] = (uint8_t)lc;
@@ -373,8 +380,8 @@ __device__ __forceinline__ bool tr_tally(DS& s, int dist, int lc) {
 }
 
 // deflate.ts:527-571 compress_block: reads d_buf/l_buf out of the pending_buf it writes
-__device__ void compress_block(DS& s, const uint16_t* ltree, const uint16_t* dtree) {
-    const uint8_t* pb = s.S->pending;
+__device__ void compress_block(DS& s, const GLB uint16_t* ltree, const GLB uint16_t* dtree) {
+    auto* pb = s.S->pending;
     int lx = 0;
     if (s.last_lit != 0) {
         do {
@@ -413,22 +420,22 @@ __device__ void flush_pending(DS& s) {
     if (len == 0) return;
     if (s.out_len + (uint64_t)len > s.out_cap) { s.err |= 2; s.pending = 0; return; }
     if (len > PENDING_SIZE) { s.err |= 1; len = PENDING_SIZE; }
-    const uint8_t* pb = s.S->pending;
+    auto* pb = s.S->pending;
     for (int i = 0; i < len; i++) s.out[s.out_len + i] = pb[i];
     s.out_len += (uint64_t)s.pending;
     s.pending = 0;
 }
 
 // deflate.ts:614-674 _tr_flush_block (+ flush_block_only 676-680)
-__device__ void flush_block(DS& s, bool eof) {
+__device__ __noinline__ void flush_block(DS& s, bool eof) {
     int buf = s.block_start >= 0 ? s.block_start : -1;
     int stored_len = s.strstart - s.block_start;
-    s.l_max_code = build_tree(s, s.S->ltree, s.T->static_ltree, c_extra_lbits, 257, L_CODES, 15);
-    s.d_max_code = build_tree(s, s.S->dtree, s.T->static_dtree, c_extra_dbits, 0, D_CODES, 15);
+    s.l_max_code = build_tree(s, s.S->ltree, s.T->static_ltree, s.T->extra_lbits, 257, L_CODES, 15);
+    s.d_max_code = build_tree(s, s.S->dtree, s.T->static_dtree, s.T->extra_dbits, 0, D_CODES, 15);
     // build_bl_tree (deflate.ts:316-339)
     scan_tree(s, s.S->ltree, s.l_max_code);
     scan_tree(s, s.S->dtree, s.d_max_code);
-    build_tree(s, s.S->bltree, nullptr, c_extra_blbits, 0, BL_CODES, 7);
+    build_tree(s, s.S->bltree, nullptr, s.T->extra_blbits, 0, BL_CODES, 7);
     int max_blindex;
     for (max_blindex = BL_CODES - 1; max_blindex >= 3; max_blindex--)
         if (s.S->bltree[c_bl_order[max_blindex] * 2 + 1] != 0) break;
@@ -467,13 +474,13 @@ __device__ void flush_block(DS& s, bool eof) {
 }
 
 // deflate.ts:690-766 fill_window (the whole input is available: one-shot append)
-__device__ void fill_window(DS& s) {
+__device__ __forceinline__ void fill_window(DS& s) {
     do {
         int more = WINDOW_SIZE - s.lookahead - s.strstart;
         if (more == 0 && s.strstart == 0 && s.lookahead == 0) more = W_SIZE;
         else if (more == -1) more--;
         else if (s.strstart >= W_SIZE + W_SIZE - MIN_LOOKAHEAD) {
-            uint4* w4 = (uint4*)s.S->window;
+            GLB u32x4* w4 = (GLB u32x4*)s.S->window;
             for (int i = 0; i < W_SIZE / 16; i++) w4[i] = w4[i + W_SIZE / 16];
             s.match_start -= W_SIZE;
             s.strstart -= W_SIZE;
@@ -485,7 +492,7 @@ __device__ void fill_window(DS& s) {
         uint64_t avail = s.in_len - s.in_pos;
         if (avail == 0) return;
         int n = avail > (uint64_t)more ? more : (int)avail;
-        uint8_t* dst = s.S->window + s.strstart + s.lookahead;
+        auto* dst = s.S->window + s.strstart + s.lookahead;
         for (int i = 0; i < n; i++) dst[i] = s.in[s.in_pos + i];
         s.in_pos += (uint64_t)n;
         s.lookahead += n;
@@ -496,10 +503,13 @@ __device__ void fill_window(DS& s) {
     } while (s.lookahead < MIN_LOOKAHEAD && s.in_pos < s.in_len);
 }
 
+__device__ __forceinline__ uint32_t ld_u32(const GLB uint8_t* p) { uint32_t v; __builtin_memcpy(&v, p, 4); return v; }
+__device__ __forceinline__ uint32_t ld_u16(const GLB uint8_t* p) { uint16_t v; __builtin_memcpy(&v, p, 2); return v; }
+
 // deflate.ts:827-946 longest_match
-__device__ int longest_match(DS& s, int cur_match) {
-    const uint8_t* win = s.S->window;
-    const uint16_t* prev = s.S->prev;
+__device__ __forceinline__ int longest_match(DS& s, int cur_match) {
+    auto* win = s.S->window;
+    auto* prev = s.S->prev;
     int chain_length = s.max_chain;
     int scan = s.strstart;
     int best_len = s.prev_length;
@@ -508,33 +518,36 @@ __device__ int longest_match(DS& s, int cur_match) {
     int strend = s.strstart + MAX_MATCH;
     int scan_end1 = win[scan + best_len - 1];
     int scan_end = win[scan + best_len];
-    int scan_start = win[scan];
-    int scan_start1 = win[scan + 1];
     if (s.prev_length >= s.good_match) chain_length >>= 2;
     if (nice > s.lookahead) nice = s.lookahead;
+    // scan bytes kept in registers; each candidate is loaded with unaligned dword reads and
+    // its next chain link is fetched together with them (one dependent round trip per candidate)
+    const uint32_t s0 = ld_u32(win + scan);                    // bytes scan .. scan+3
+    int next = prev[cur_match & W_MASK];
     do {
-        int match = cur_match;
-        if (win[match + best_len] != scan_end || win[match + best_len - 1] != scan_end1 ||
-            win[match] != scan_start || win[match + 1] != scan_start1)
-            continue;
+        const int match = cur_match;
+        const uint32_t m0 = ld_u32(win + match);
+        const uint32_t be = ld_u16(win + match + best_len - 1);  // bytes best_len-1, best_len
+        cur_match = next;
+        next = prev[cur_match & W_MASK];                        // prefetch the link after this one
+        if (be != ((uint32_t)scan_end1 | ((uint32_t)scan_end << 8)) || ((m0 ^ s0) & 0xffffu) != 0) continue;
+        // compare 4 bytes at a time from offset 2 (deflate.ts:899-921): first differing byte
         int sp = scan + 2, mp = match + 2;
         do {
-            uint32_t sv = ((uint32_t)win[sp] << 24) | ((uint32_t)win[sp + 1] << 16) | ((uint32_t)win[sp + 2] << 8) | win[sp + 3];
-            uint32_t mv = ((uint32_t)win[mp] << 24) | ((uint32_t)win[mp + 1] << 16) | ((uint32_t)win[mp + 2] << 8) | win[mp + 3];
-            uint32_t x = sv ^ mv;
-            if (x) { int mb = __builtin_clz(x) >> 3; sp += mb; mp += mb; break; }
+            const uint32_t x = ld_u32(win + sp) ^ ld_u32(win + mp);
+            if (x) { const int mb = __builtin_ctz(x) >> 3; sp += mb; mp += mb; break; }
             sp += 4; mp += 4;
         } while (sp < strend);
         if (sp > strend) sp = strend;
         int len = MAX_MATCH - (strend - sp);
         if (len > best_len) {
-            s.match_start = cur_match;
+            s.match_start = match;
             best_len = len;
             if (len >= nice) break;
             scan_end1 = win[scan + best_len - 1];
             scan_end = win[scan + best_len];
         }
-    } while ((cur_match = prev[cur_match & W_MASK]) > limit && --chain_length != 0);
+    } while (cur_match > limit && --chain_length != 0);
     return best_len <= s.lookahead ? best_len : s.lookahead;
 }
 
@@ -547,7 +560,7 @@ __device__ __forceinline__ int insert_string(DS& s) {
 }
 
 // deflate.ts:953-1049 (levels 1-3), run to FINISH
-__device__ void deflate_fast(DS& s) {
+__device__ __forceinline__ void deflate_fast(DS& s) {
     int hash_head = 0;
     for (;;) {
         if (s.lookahead < MIN_LOOKAHEAD) {
@@ -582,7 +595,7 @@ __device__ void deflate_fast(DS& s) {
 }
 
 // deflate.ts:1054-1182 (levels 4-9), run to FINISH
-__device__ void deflate_slow(DS& s) {
+__device__ __forceinline__ void deflate_slow(DS& s) {
     int hash_head = 0;
     for (;;) {
         if (s.lookahead < MIN_LOOKAHEAD) {
@@ -629,7 +642,7 @@ __device__ void deflate_slow(DS& s) {
 }
 
 // adler32.ts:34-105 / crc32.ts:48-106 over the input (Deflater.append, sd-deflate.ts:185-190)
-__device__ int32_t input_checksum(const uint8_t* p, uint64_t n, bool gzip, const uint32_t* crct) {
+__device__ int32_t input_checksum(const GLB uint8_t* p, uint64_t n, bool gzip, const uint32_t* crct) {
     if (gzip) {
         uint32_t c = 0xffffffffu;
         for (uint64_t i = 0; i < n; i++) c = crct[(c ^ p[i]) & 255] ^ (c >> 8);
@@ -651,9 +664,7 @@ __device__ int32_t input_checksum(const uint8_t* p, uint64_t n, bool gzip, const
 }
 
 __global__ __launch_bounds__(DF_THREADS) void k_deflate(DeflateArgs A) {
-    __shared__ DTables T;
     __shared__ uint32_t crct[256];
-    build_tables(T);
     for (int n = threadIdx.x; n < 256; n += DF_THREADS) {
         uint32_t c = (uint32_t)n;
         for (int k = 0; k < 8; ++k) c = (c & 1) ? 0xedb88320u ^ (c >> 1) : c >> 1;
@@ -664,12 +675,12 @@ __global__ __launch_bounds__(DF_THREADS) void k_deflate(DeflateArgs A) {
     if (sid >= A.n) return;
 
     DS s;
-    s.S = (DSlab*)(A.state + (uint64_t)sid * SLAB_BYTES);
-    s.T = &T;
-    s.in = A.in + A.in_off[sid];
+    s.S = (GLB DSlab*)(A.state + (uint64_t)sid * SLAB_BYTES);
+    s.T = (const GLB DTables*)&g_dt;
+    s.in = (const GLB uint8_t*)(A.in + A.in_off[sid]);
     s.in_len = A.in_len[sid];
     s.in_pos = 0;
-    s.out = A.out + A.out_off[sid];
+    s.out = (GLB uint8_t*)(A.out + A.out_off[sid]);
     s.out_cap = A.out_cap[sid];
     s.out_len = 0;
     s.err = 0;
@@ -682,12 +693,12 @@ __global__ __launch_bounds__(DF_THREADS) void k_deflate(DeflateArgs A) {
     }
     // Deflate constructor (deflate.ts:196-220) + window zero fill (deflate.ts:119)
     {
-        uint4 z = make_uint4(0, 0, 0, 0);
-        uint4* w4 = (uint4*)s.S->window;
+        const u32x4 z = {0u, 0u, 0u, 0u};
+        GLB u32x4* w4 = (GLB u32x4*)s.S->window;
         for (int i = 0; i < WINDOW_SIZE / 16; i++) w4[i] = z;
-        uint4* h4 = (uint4*)s.S->head;
+        GLB u32x4* h4 = (GLB u32x4*)s.S->head;
         for (int i = 0; i < HASH_SIZE * 2 / 16; i++) h4[i] = z;
-        uint4* p4 = (uint4*)s.S->prev;
+        GLB u32x4* p4 = (GLB u32x4*)s.S->prev;
         for (int i = 0; i < W_SIZE * 2 / 16; i++) p4[i] = z;
         for (int i = 0; i < HEAP_SIZE * 2; i++) s.S->ltree[i] = 0;
         for (int i = 0; i < (2 * D_CODES + 1) * 2; i++) s.S->dtree[i] = 0;
@@ -747,6 +758,7 @@ __global__ __launch_bounds__(DF_THREADS) void k_deflate(DeflateArgs A) {
 void launch_deflate(const DeflateArgs& a, hipStream_t st) {
     if (a.n == 0) return;
     dim3 grid((a.n + DF_THREADS - 1) / DF_THREADS);
+    hipLaunchKernelGGL(k_deflate_tables, dim3(1), dim3(1), 0, st);
     hipLaunchKernelGGL(k_deflate, grid, dim3(DF_THREADS), 0, st, a);
 }
 
