@@ -31,6 +31,9 @@ namespace sdz {
 #define RS_WIN 32768
 #define RS_R 36352                    // ring bytes: 32 KiB window + bytes in flight
 #define RS_SLACK (RS_R - RS_WIN)
+#ifndef RS_NAP
+#define RS_NAP 4                      // s_sleep units (64 clocks) between polls
+#endif
 #define RS_BM 4096                    // finality map bytes (>= RS_SLACK; lap = position >> 12)
 #define RS_SPIN_LIMIT (1u << 22)      // watchdog: polls per wait (~0.2 s)
 
@@ -232,7 +235,7 @@ __device__ __forceinline__ bool wait_ge(uint32_t* p, uint32_t v, uint32_t* fail)
             if (!lds_get(fail)) lds_put(fail, 2u | (v << 4));   // site | position, for diagnosis
             return false;
         }
-        __builtin_amdgcn_s_sleep(1);
+        __builtin_amdgcn_s_sleep(RS_NAP);
     }
 }
 
@@ -331,7 +334,7 @@ __global__ __launch_bounds__(RS_THREADS) __attribute__((amdgpu_waves_per_eu(8, 8
             const uint64_t c = lds_get64(&chain);
             if ((uint32_t)(c >> 32) == g - 1u) { Sg = uni((uint32_t)c); break; }
             if (n > RS_SPIN_LIMIT || lds_get(&fail)) { if (!lds_get(&fail)) lds_put(&fail, 1u | (g << 4)); break; }
-            __builtin_amdgcn_s_sleep(1);
+            __builtin_amdgcn_s_sleep(RS_NAP);
         }
         if (lane == 0) __hip_atomic_store(&chain, ((uint64_t)g << 32) | (Sg + T), __ATOMIC_RELAXED,
                                           __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -373,7 +376,7 @@ __global__ __launch_bounds__(RS_THREADS) __attribute__((amdgpu_waves_per_eu(8, 8
             } else {
                 if (timed) tacc[7]++;
                 if (n > RS_SPIN_LIMIT || lds_get(&fail)) { if (!lds_get(&fail)) lds_put(&fail, 3u | (Sg << 4)); break; }
-                __builtin_amdgcn_s_sleep(1);
+                __builtin_amdgcn_s_sleep(RS_NAP);
             }
         }
         if (lds_get(&fail)) break;

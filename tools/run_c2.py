@@ -30,9 +30,10 @@ def main():
         comp = open(os.path.join(golden, "paradiselost.deflate"), "rb").read()
         b = DeviceBatch(sdz, comp, args.streams, len(text))
         for i in range(args.steps):
-            ms = inflate_step(sdz, b)
-            print("inflate step %d: kernel %.3f ms, %.1f GB/s out" % (i, ms, len(text) * args.streams / ms / 1e6),
-                  flush=True)
+            split = []
+            ms = inflate_step(sdz, b, split)
+            print("inflate step %d: kernel %.3f ms (decode %.2f resolve %.2f), %.1f GB/s out"
+                  % (i, ms, split[0][0], split[0][1], len(text) * args.streams / ms / 1e6), flush=True)
     else:
         sl = text[:65536]
         b = DeviceBatch(sdz, sl, args.streams, int(L.sdz_deflate_bound(65536, 1, 0)))
