@@ -143,6 +143,11 @@ struct DS {
     int heap_len, heap_max;
     int l_max_code, d_max_code, bl_max_code;
     int err;                        // 1 = pending_buf overflow (reference undefined), 2 = out overflow
+    // record path (levels 4-9, inputs <= 64 KiB): window = the input, no head/prev tables
+    const GLB uint64_t* rec;        // per position: matches found by k_dfl_match (null: classic path)
+    const GLB uint16_t* pvp;        // per position: previous position of the same hash (k_dfl_chain)
+    int off;                        // original position of window index 0 (32768 after the slide)
+    int tail;                       // first position whose match search runs here (end of input)
 };
 
 // ------------------------------------------------------------------ bit writer (deflate.ts:347-374)
@@ -450,7 +455,10 @@ __device__ __noinline__ void flush_block(DS& s, bool eof) {
         put_short(s, ~(uint32_t)stored_len);
         if (s.pending + stored_len > PENDING_SIZE) s.err |= 1;
         else {
-            for (int i = 0; i < stored_len; i++) s.S->pending[s.pending + i] = s.S->window[buf + i];
+            if (s.rec)
+                for (int i = 0; i < stored_len; i++) s.S->pending[s.pending + i] = s.in[s.off + buf + i];
+            else
+                for (int i = 0; i < stored_len; i++) s.S->pending[s.pending + i] = s.S->window[buf + i];
             s.pending += stored_len;
         }
     } else if (static_lenb == opt_lenb) {
@@ -641,6 +649,135 @@ __device__ __forceinline__ void deflate_slow(DS& s) {
     flush_block(s, true);
 }
 
+// ------------------------------------------------------------------ record path (levels 4-9)
+// The reference's deflate_slow with its two expensive parts precomputed in parallel:
+//   k_dfl_chain  pvp[p]: the hash chain link insert_string leaves for position p (the previous
+//                position with the same 3-byte hash) -- every position is inserted once, in
+//                order, in deflate_slow (deflate.ts:1077-1080, 1119-1126);
+//   k_dfl_match  rec[p]: what longest_match (deflate.ts:827-946) returns at p for
+//                prev_length < good_match (full chain) and >= good_match (chain >> 2), as
+//                (length, distance) of the first candidate reaching the chain's best length
+//                (or nice_match).  Called with best_len = prev_length, the reference returns
+//                that entry if its length exceeds prev_length and prev_length otherwise.
+// Positions within 262 bytes of the end search here, exactly as the reference does: their
+// comparisons may read past the input (zeros; after the window slide, the stale upper
+// half -- SURVEY A6) and nice_match / the result are clamped to the lookahead.
+// The parser below keeps the reference's (rebased) coordinates; window index i is original
+// position i + off.  Only inputs of at most 64 KiB take this path: the window then holds
+// the whole input and slides at most once, at the end.
+#define PM_TAIL (MAX_MATCH + MIN_MATCH + 1)
+__device__ __forceinline__ uint32_t rp_byte(const DS& s, int i) {     // window[i] on the record path
+    const int P = i + s.off;
+    if ((uint64_t)P < s.in_len) return s.in[P];
+    return (s.off && P >= WINDOW_SIZE) ? s.in[P - W_SIZE] : 0u;      // stale half after the slide
+}
+__device__ __forceinline__ int rp_head(const DS& s) {                  // insert_string's hash_head
+    const int v = s.pvp[s.strstart + s.off];
+    return s.off ? (v >= W_SIZE ? v - W_SIZE : 0) : v;                   // head[] rebased at the slide
+}
+__device__ __forceinline__ int rp_prev(const DS& s, int cur) {          // prev[cur & W_MASK]
+    const int v = s.pvp[cur + s.off];
+    return s.off ? (v >= W_SIZE ? v - W_SIZE : 0) : v;
+}
+// deflate.ts:827-946 verbatim over rp_byte / rp_prev (end of input only)
+__device__ int longest_match_tail(DS& s, int cur_match) {
+    int chain_length = s.max_chain;
+    const int scan = s.strstart;
+    int best_len = s.prev_length;
+    const int limit = s.strstart > MAX_DIST ? s.strstart - MAX_DIST : 0;
+    int nice = s.nice_match;
+    const int strend = s.strstart + MAX_MATCH;
+    int scan_end1 = rp_byte(s, scan + best_len - 1);
+    int scan_end = rp_byte(s, scan + best_len);
+    const int scan_start = rp_byte(s, scan), scan_start1 = rp_byte(s, scan + 1);
+    if (s.prev_length >= s.good_match) chain_length >>= 2;
+    if (nice > s.lookahead) nice = s.lookahead;
+    do {
+        const int match = cur_match;
+        if ((int)rp_byte(s, match + best_len) != scan_end || (int)rp_byte(s, match + best_len - 1) != scan_end1 ||
+            (int)rp_byte(s, match) != scan_start || (int)rp_byte(s, match + 1) != scan_start1)
+            continue;
+        int sp = scan + 2, mp = match + 2;
+        do {                                             // 4 bytes at a time from +2 (deflate.ts:899-921)
+            int k = 0;
+            while (k < 4 && rp_byte(s, sp + k) == rp_byte(s, mp + k)) ++k;
+            if (k < 4) { sp += k; mp += k; break; }
+            sp += 4; mp += 4;
+        } while (sp < strend);
+        if (sp > strend) sp = strend;
+        const int len = MAX_MATCH - (strend - sp);
+        if (len > best_len) {
+            s.match_start = match;
+            best_len = len;
+            if (len >= nice) break;
+            scan_end1 = rp_byte(s, scan + best_len - 1);
+            scan_end = rp_byte(s, scan + best_len);
+        }
+    } while ((cur_match = rp_prev(s, cur_match)) > limit && --chain_length != 0);
+    return best_len <= s.lookahead ? best_len : s.lookahead;
+}
+// deflate.ts:1054-1182 (levels 4-9) on the records
+__device__ __forceinline__ void deflate_slow_rec(DS& s) {
+    int hash_head = 0;
+    s.lookahead = (int)s.in_len;                         // fill_window's first call loads everything
+    for (;;) {
+        if (s.lookahead < MIN_LOOKAHEAD) {               // fill_window: no input left; it may slide
+            if (!s.off && s.strstart >= W_SIZE + W_SIZE - MIN_LOOKAHEAD) {
+                s.match_start -= W_SIZE;
+                s.strstart -= W_SIZE;
+                s.block_start -= W_SIZE;
+                s.off = W_SIZE;
+            }
+            if (s.lookahead == 0) break;
+        }
+        if (s.lookahead >= MIN_MATCH) hash_head = rp_head(s);
+        s.prev_length = s.match_length;
+        const int prev_match = s.match_start;
+        s.match_length = MIN_MATCH - 1;
+        if (hash_head != 0 && s.prev_length < s.max_lazy && ((s.strstart - hash_head) & 0xffff) <= MAX_DIST) {
+            const int P = s.strstart + s.off;
+            if (P < s.tail) {
+                const uint64_t r = s.rec[P];
+                const uint32_t e = s.prev_length >= s.good_match ? (uint32_t)(r >> 32) : (uint32_t)r;
+                const int len = (int)(e >> 16);
+                if (len > s.prev_length) { s.match_length = len; s.match_start = s.strstart - (int)(e & 0xffffu); }
+                else s.match_length = s.prev_length;
+            } else {
+                s.match_length = longest_match_tail(s, hash_head);
+            }
+            if (s.match_length <= 5 && s.match_length == MIN_MATCH && s.strstart - s.match_start > 4096)
+                s.match_length = MIN_MATCH - 1;
+        }
+        if (s.prev_length >= MIN_MATCH && s.match_length <= s.prev_length) {
+            const int max_insert = s.strstart + s.lookahead - MIN_MATCH;
+            const bool bflush = tr_tally(s, s.strstart - 1 - prev_match, s.prev_length - MIN_MATCH);
+            s.lookahead -= s.prev_length - 1;
+            s.prev_length -= 2;
+            do {
+                if (++s.strstart <= max_insert) hash_head = rp_head(s);
+            } while (--s.prev_length != 0);
+            s.match_available = 0;
+            s.match_length = MIN_MATCH - 1;
+            s.strstart++;
+            if (bflush) flush_block(s, false);
+        } else if (s.match_available) {
+            const bool bflush = tr_tally(s, 0, rp_byte(s, s.strstart - 1));
+            if (bflush) flush_block(s, false);
+            s.strstart++;
+            s.lookahead--;
+        } else {
+            s.match_available = 1;
+            s.strstart++;
+            s.lookahead--;
+        }
+    }
+    if (s.match_available) {
+        tr_tally(s, 0, rp_byte(s, s.strstart - 1));
+        s.match_available = 0;
+    }
+    flush_block(s, true);
+}
+
 // adler32.ts:34-105 / crc32.ts:48-106 over the input (Deflater.append, sd-deflate.ts:185-190)
 __device__ int32_t input_checksum(const GLB uint8_t* p, uint64_t n, bool gzip, const uint32_t* crct) {
     if (gzip) {
@@ -684,6 +821,12 @@ __global__ __launch_bounds__(DF_THREADS) void k_deflate(DeflateArgs A) {
     s.out_cap = A.out_cap[sid];
     s.out_len = 0;
     s.err = 0;
+    s.rec = nullptr; s.pvp = nullptr; s.off = 0; s.tail = 0;
+    if (A.rec_buf && s.in_len <= A.rec_stride) {
+        s.rec = (const GLB uint64_t*)A.rec_buf + (uint64_t)sid * A.rec_stride;
+        s.pvp = (const GLB uint16_t*)A.pv_buf + (uint64_t)sid * A.rec_stride;
+        s.tail = s.in_len > PM_TAIL ? (int)s.in_len - PM_TAIL : 0;
+    }
     sdz_deflate_record R;
     R.status = SDZ_OK; R.checksum = 0; R.out_len = 0; R.reserved = 0;
     if (s.in_len == 0) {                        // sd-deflate.ts:180-182 + 232-234
@@ -692,7 +835,7 @@ __global__ __launch_bounds__(DF_THREADS) void k_deflate(DeflateArgs A) {
         return;
     }
     // Deflate constructor (deflate.ts:196-220) + window zero fill (deflate.ts:119)
-    {
+    if (!s.rec) {
         const u32x4 z = {0u, 0u, 0u, 0u};
         GLB u32x4* w4 = (GLB u32x4*)s.S->window;
         for (int i = 0; i < WINDOW_SIZE / 16; i++) w4[i] = z;
@@ -700,6 +843,8 @@ __global__ __launch_bounds__(DF_THREADS) void k_deflate(DeflateArgs A) {
         for (int i = 0; i < HASH_SIZE * 2 / 16; i++) h4[i] = z;
         GLB u32x4* p4 = (GLB u32x4*)s.S->prev;
         for (int i = 0; i < W_SIZE * 2 / 16; i++) p4[i] = z;
+    }
+    {
         for (int i = 0; i < HEAP_SIZE * 2; i++) s.S->ltree[i] = 0;
         for (int i = 0; i < (2 * D_CODES + 1) * 2; i++) s.S->dtree[i] = 0;
         for (int i = 0; i < (2 * BL_CODES + 1) * 2; i++) s.S->bltree[i] = 0;
@@ -733,7 +878,9 @@ __global__ __launch_bounds__(DF_THREADS) void k_deflate(DeflateArgs A) {
     }
     s.out_len = hdr;
 
-    if (c_config[A.level][4]) deflate_fast(s); else deflate_slow(s);
+    if (c_config[A.level][4]) deflate_fast(s);
+    else if (s.rec) deflate_slow_rec(s);
+    else deflate_slow(s);
 
     // trailer (sd-deflate.ts:154-165)
     uint64_t tl = A.format == SDZ_DEFLATE_ZLIB ? 4 : gzip ? 8 : 0;
@@ -755,10 +902,144 @@ __global__ __launch_bounds__(DF_THREADS) void k_deflate(DeflateArgs A) {
     A.rec[sid] = R;
 }
 
+
+// ------------------------------------------------------------------ record path kernels
+
+// k_dfl_chain: one wave per stream walks its positions in order, 64 at a time; each lane
+// swaps its position into the LDS head table.  Same-address lanes of one ds_wrxchg are
+// served in lane order (tools/ubench/lds_xchg_order.hip), so a lane receives the position
+// of the previous lane with the same hash, or the head: exactly insert_string's sequence.
+__global__ __launch_bounds__(64) void k_dfl_chain(DeflateArgs A) {
+    __shared__ uint32_t head[HASH_SIZE];                 // 128 KiB
+    const uint32_t sid = blockIdx.x, lane = threadIdx.x;
+    if (sid >= A.n) return;
+    const uint64_t in_len = A.in_len[sid];
+    if (in_len > A.rec_stride) return;
+    const GLB uint8_t* in = (const GLB uint8_t*)(A.in + A.in_off[sid]);
+    GLB uint16_t* pv = (GLB uint16_t*)A.pv_buf + (uint64_t)sid * A.rec_stride;
+    for (uint32_t i = lane; i < HASH_SIZE; i += 64) head[i] = 0;
+    const uint32_t n = (uint32_t)in_len;
+    // rolling bytes: b0 b1 b2 of position p are in[p], in[p+1], in[p+2]
+    for (uint32_t base = 0; base < n; base += 64) {
+        const uint32_t p = base + lane;
+        const bool ins = p + 2 < n;                      // insert_string runs while lookahead >= 3
+        uint32_t h = 0;
+        if (ins) h = (((uint32_t)in[p] << 10) ^ ((uint32_t)in[p + 1] << 5) ^ in[p + 2]) & HASH_MASK;
+        uint32_t old = 0;
+        if (ins) old = atomicExch(&head[h], p);
+        if (p < n) pv[p] = (uint16_t)old;
+    }
+}
+
+// k_dfl_match: what longest_match returns at every position (but the last PM_TAIL), for both
+// chain lengths.  A workgroup takes PM_SEG positions of one stream with the 32 KiB before
+// them staged in LDS: window bytes and chain links.  Record per position:
+//   bits 0-15 distance, 16-24 length (<= 2: no candidate beats MIN_MATCH - 1) -- chain
+//   max_chain in the low word, max_chain >> 2 in the high word.
+#define PM_SEG 8192
+#define PM_THREADS 1024
+#define PM_WINB (W_SIZE + PM_SEG + MAX_MATCH + 16)     // staged window bytes
+#define PM_PV (W_SIZE + PM_SEG)                         // staged links
+__device__ __forceinline__ uint32_t pm_w4(const uint8_t* w, uint32_t x) {   // 4 bytes at x, aligned reads
+    const uint32_t* w32 = (const uint32_t*)w;
+    return __builtin_amdgcn_alignbyte(w32[(x >> 2) + 1], w32[x >> 2], x & 3u);
+}
+__global__ __launch_bounds__(PM_THREADS) void k_dfl_match(DeflateArgs A, uint32_t nseg) {
+    __shared__ __attribute__((aligned(16))) uint8_t win[(PM_WINB + 15) & ~15];
+    __shared__ uint16_t pvl[PM_PV];
+    const uint32_t sid = blockIdx.x / nseg, seg = blockIdx.x % nseg, tid = threadIdx.x;
+    if (sid >= A.n) return;
+    const uint64_t in_len = A.in_len[sid];
+    if (in_len > A.rec_stride) return;
+    const int n = (int)in_len;
+    const int tail = n > PM_TAIL ? n - PM_TAIL : 0;
+    const int s0 = (int)(seg * PM_SEG), s1 = s0 + PM_SEG < tail ? s0 + PM_SEG : tail;
+    if (s0 >= s1) return;
+    const int ws = s0 > W_SIZE ? s0 - W_SIZE : 0;          // staged range [ws, we)
+    const int we = s1 + MAX_MATCH + 8 < n ? s1 + MAX_MATCH + 8 : n;
+    const GLB uint8_t* in = (const GLB uint8_t*)(A.in + A.in_off[sid]);
+    const GLB uint16_t* pv = (const GLB uint16_t*)A.pv_buf + (uint64_t)sid * A.rec_stride;
+    for (int i = (int)tid; i < we - ws; i += PM_THREADS) win[i] = in[ws + i];
+    for (int i = (int)tid; i < s1 - ws; i += PM_THREADS) pvl[i] = pv[ws + i];
+    __syncthreads();
+    GLB uint64_t* rec = (GLB uint64_t*)A.rec_buf + (uint64_t)sid * A.rec_stride;
+    const int max_chain = c_config[A.level][3], qchain = max_chain >> 2, nice = c_config[A.level][2];
+    for (int p = s0 + (int)tid; p < s1; p += PM_THREADS) {
+        const int hh = pvl[p - ws];
+        uint32_t full = 0, quarter = 0;
+        if (hh != 0 && p - hh <= MAX_DIST) {
+            const int limit = p > MAX_DIST ? p - MAX_DIST : 0;
+            const uint32_t sp = (uint32_t)(p - ws);
+            const uint32_t s4 = pm_w4(win, sp);
+            int best = MIN_MATCH - 1, bpos = 0, qbest = 0, qpos = 0, k = 0;
+            bool qdone = false;
+            uint32_t sb = win[sp + best];
+            int cur = hh, chain = max_chain;
+            do {
+                ++k;
+                const uint32_t cp = (uint32_t)(cur - ws);
+                if (win[cp + best] == sb) {              // can beat best (deflate.ts:866-882)
+                    uint32_t x = pm_w4(win, cp) ^ s4;
+                    int len;
+                    if (x) len = __builtin_ctz(x) >> 3;
+                    else {
+                        len = 4;
+                        for (;;) {
+                            x = pm_w4(win, cp + len) ^ pm_w4(win, sp + len);
+                            if (x) { len += __builtin_ctz(x) >> 3; break; }
+                            len += 4;
+                            if (len >= MAX_MATCH) break;
+                        }
+                        if (len > MAX_MATCH) len = MAX_MATCH;
+                    }
+                    if (len > best) {
+                        best = len;
+                        bpos = cur;
+                        if (len >= nice) break;
+                        sb = win[sp + best];
+                    }
+                }
+                if (k == qchain) { qbest = best; qpos = bpos; qdone = true; }
+            } while ((cur = pvl[cur - ws]) > limit && --chain != 0);
+            if (!qdone) { qbest = best; qpos = bpos; }
+            full = best > MIN_MATCH - 1 ? ((uint32_t)best << 16) | (uint32_t)(p - bpos) : 0u;
+            quarter = qbest > MIN_MATCH - 1 ? ((uint32_t)qbest << 16) | (uint32_t)(p - qpos) : 0u;
+        }
+        rec[p] = ((uint64_t)quarter << 32) | full;
+    }
+}
+
+__global__ void k_max_u64(const uint64_t* v, uint32_t n, unsigned long long* out) {
+    unsigned long long m = 0;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
+        m = v[i] > m ? v[i] : m;
+    for (int o = 32; o > 0; o >>= 1) { unsigned long long x = __shfl_xor(m, o); m = x > m ? x : m; }
+    if ((threadIdx.x & 63) == 0) atomicMax(out, m);
+}
+int device_max_u64(const uint64_t* v, uint32_t n, uint64_t* out, hipStream_t st) {
+    unsigned long long* d = nullptr;
+    if (hipMalloc(&d, sizeof *d) != hipSuccess) return -1;
+    bool ok = hipMemsetAsync(d, 0, sizeof *d, st) == hipSuccess;
+    hipLaunchKernelGGL(k_max_u64, dim3(64), dim3(256), 0, st, v, n, d);
+    unsigned long long h = 0;
+    ok = ok && hipMemcpyAsync(&h, d, sizeof h, hipMemcpyDeviceToHost, st) == hipSuccess;
+    ok = ok && hipStreamSynchronize(st) == hipSuccess;
+    ok = hipFree(d) == hipSuccess && ok;
+    *out = h;
+    return ok ? 0 : -1;
+}
+
+static bool c_config_host_fast(int level) { return level >= 1 && level <= 3; }
+
 void launch_deflate(const DeflateArgs& a, hipStream_t st) {
     if (a.n == 0) return;
     dim3 grid((a.n + DF_THREADS - 1) / DF_THREADS);
     hipLaunchKernelGGL(k_deflate_tables, dim3(1), dim3(1), 0, st);
+    if (a.rec_buf && !c_config_host_fast(a.level)) {
+        const uint32_t nseg = (a.rec_stride + PM_SEG - 1) / PM_SEG;
+        hipLaunchKernelGGL(k_dfl_chain, dim3(a.n), dim3(64), 0, st, a);
+        hipLaunchKernelGGL(k_dfl_match, dim3(a.n * nseg), dim3(PM_THREADS), 0, st, a, nseg);
+    }
     hipLaunchKernelGGL(k_deflate, grid, dim3(DF_THREADS), 0, st, a);
 }
 

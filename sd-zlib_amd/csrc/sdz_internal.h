@@ -61,10 +61,17 @@ struct DeflateArgs {
     uint32_t n;
     int32_t level;
     int32_t format;
+    // record path (levels 4-9, inputs <= rec_stride <= 64 KiB): per stream rec_stride positions
+    uint64_t* rec_buf;           // n * rec_stride match records (null: classic path only)
+    uint16_t* pv_buf;            // n * rec_stride hash chain links
+    uint32_t rec_stride;
 };
 
 uint64_t deflate_state_bytes();
 void launch_deflate(const DeflateArgs& a, hipStream_t s);
+constexpr uint32_t kDeflateRecMax = 65536;   // longest input on the record path
+// max of n device-resident u64 values (blocking; for scratch sizing)
+int device_max_u64(const uint64_t* v, uint32_t n, uint64_t* out, hipStream_t s);
 
 void launch_checksum(const uint8_t* in, const uint64_t* in_off, const uint64_t* in_len,
                      const int32_t* seed, int32_t* result, uint32_t n, int kind, hipStream_t s);

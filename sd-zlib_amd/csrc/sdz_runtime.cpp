@@ -304,10 +304,19 @@ int sdz_deflate_batch_device(const uint8_t* in, const uint64_t* in_off, const ui
     uint64_t slab = deflate_state_bytes();
     size_t mem_free = 0, mem_total = 0;
     if (hipMemGetInfo(&mem_free, &mem_total) != hipSuccess) mem_free = 16ull << 30;
-    const uint32_t kMaxSlabs = (uint32_t)std::max<uint64_t>(1024, std::min<uint64_t>(65536, mem_free / 4 / slab));
+    // record path (levels 4-9, every input <= 64 KiB): hash chains and match records per
+    // position, found in parallel before the serial parse (k_deflate.hip)
+    uint32_t stride = 0;
+    if (level >= 4) {
+        uint64_t mx = 0;
+        if (device_max_u64(in_len, n, &mx, s)) return hip_fail(hipGetLastError(), "deflate: input sizes");
+        if (mx <= kDeflateRecMax) stride = (uint32_t)std::max<uint64_t>(64, (mx + 63) & ~63ull);
+    }
+    const uint64_t per_stream = slab + (uint64_t)stride * (sizeof(uint64_t) + sizeof(uint16_t));
+    const uint32_t kMaxSlabs = (uint32_t)std::max<uint64_t>(1024, std::min<uint64_t>(65536, mem_free / 2 / per_stream));
     uint32_t chunk = std::min(n, kMaxSlabs);
     void* state = nullptr;
-    if (int rc = g_deflate_state.get((size_t)chunk * slab, &state)) return rc;
+    if (int rc = g_deflate_state.get((size_t)chunk * per_stream, &state)) return rc;
     uint8_t* d_fname = nullptr;
     void* tmp = nullptr;
     if (fname_len) {
@@ -322,6 +331,9 @@ int sdz_deflate_batch_device(const uint8_t* in, const uint64_t* in_off, const ui
         a.in = in; a.in_off = in_off + b; a.in_len = in_len + b;
         a.out = out; a.out_off = out_off + b; a.out_cap = out_cap + b;
         a.rec = rec + b; a.state = (uint8_t*)state;
+        a.rec_stride = stride;
+        a.rec_buf = stride ? (uint64_t*)((uint8_t*)state + (size_t)chunk * slab) : nullptr;
+        a.pv_buf = stride ? (uint16_t*)((uint8_t*)a.rec_buf + (size_t)chunk * stride * sizeof(uint64_t)) : nullptr;
         a.fname = d_fname; a.fname_len = fname_len; a.mtime = mtime;
         a.n = m; a.level = level; a.format = format;
         launch_deflate(a, s);
