@@ -752,10 +752,13 @@ __device__ __forceinline__ void deflate_slow_rec(DS& s) {
             const int max_insert = s.strstart + s.lookahead - MIN_MATCH;
             const bool bflush = tr_tally(s, s.strstart - 1 - prev_match, s.prev_length - MIN_MATCH);
             s.lookahead -= s.prev_length - 1;
-            s.prev_length -= 2;
-            do {
-                if (++s.strstart <= max_insert) hash_head = rp_head(s);
-            } while (--s.prev_length != 0);
+            // the reference inserts strstart+1 .. strstart+prev_length-2 (up to max_insert);
+            // only the last insertion's hash_head survives
+            const int last = s.strstart + s.prev_length - 2;
+            const int lastins = last < max_insert ? last : max_insert;
+            if (lastins > s.strstart) { const int st = s.strstart; s.strstart = lastins; hash_head = rp_head(s); s.strstart = st; }
+            s.strstart = last;
+            s.prev_length = 0;
             s.match_available = 0;
             s.match_length = MIN_MATCH - 1;
             s.strstart++;
@@ -933,10 +936,12 @@ __global__ __launch_bounds__(64) void k_dfl_chain(DeflateArgs A) {
 
 // k_dfl_match: what longest_match returns at every position (but the last PM_TAIL), for both
 // chain lengths.  A workgroup takes PM_SEG positions of one stream with the 32 KiB before
-// them staged in LDS: window bytes and chain links.  Record per position:
-//   bits 0-15 distance, 16-24 length (<= 2: no candidate beats MIN_MATCH - 1) -- chain
-//   max_chain in the low word, max_chain >> 2 in the high word.
-#define PM_SEG 8192
+// them staged in LDS: window bytes and chain links.  Each wave works through its share of
+// positions with persistent lanes: a lane whose chain walk ends takes the next position,
+// so the wave runs ~ (total candidates / 64) steps, not (longest chain x positions / 64).
+// Record per position: bits 0-15 distance, 16-24 length (<= 2: no candidate beats
+// MIN_MATCH - 1) -- chain max_chain in the low word, max_chain >> 2 in the high word.
+#define PM_SEG 16384
 #define PM_THREADS 1024
 #define PM_WINB (W_SIZE + PM_SEG + MAX_MATCH + 16)     // staged window bytes
 #define PM_PV (W_SIZE + PM_SEG)                         // staged links
@@ -946,8 +951,9 @@ __device__ __forceinline__ uint32_t pm_w4(const uint8_t* w, uint32_t x) {   // 4
 }
 __global__ __launch_bounds__(PM_THREADS) void k_dfl_match(DeflateArgs A, uint32_t nseg) {
     __shared__ __attribute__((aligned(16))) uint8_t win[(PM_WINB + 15) & ~15];
-    __shared__ uint16_t pvl[PM_PV];
+    __shared__ __attribute__((aligned(16))) uint16_t pvl[PM_PV];
     const uint32_t sid = blockIdx.x / nseg, seg = blockIdx.x % nseg, tid = threadIdx.x;
+    const uint32_t lane = tid & 63u, wv = tid >> 6;
     if (sid >= A.n) return;
     const uint64_t in_len = A.in_len[sid];
     if (in_len > A.rec_stride) return;
@@ -955,57 +961,90 @@ __global__ __launch_bounds__(PM_THREADS) void k_dfl_match(DeflateArgs A, uint32_
     const int tail = n > PM_TAIL ? n - PM_TAIL : 0;
     const int s0 = (int)(seg * PM_SEG), s1 = s0 + PM_SEG < tail ? s0 + PM_SEG : tail;
     if (s0 >= s1) return;
-    const int ws = s0 > W_SIZE ? s0 - W_SIZE : 0;          // staged range [ws, we)
+    const int ws = s0 > W_SIZE ? s0 - W_SIZE : 0;          // staged range [ws, we) (ws even)
     const int we = s1 + MAX_MATCH + 8 < n ? s1 + MAX_MATCH + 8 : n;
     const GLB uint8_t* in = (const GLB uint8_t*)(A.in + A.in_off[sid]);
     const GLB uint16_t* pv = (const GLB uint16_t*)A.pv_buf + (uint64_t)sid * A.rec_stride;
-    for (int i = (int)tid; i < we - ws; i += PM_THREADS) win[i] = in[ws + i];
-    for (int i = (int)tid; i < s1 - ws; i += PM_THREADS) pvl[i] = pv[ws + i];
+    {
+        const int nw = (we - ws) >> 2;                     // whole dwords (unaligned global reads)
+        uint32_t* w32 = (uint32_t*)win;
+        for (int i = (int)tid; i < nw; i += PM_THREADS) {
+            uint32_t v;
+            __builtin_memcpy(&v, (const uint8_t*)(in + ws + 4 * i), 4);
+            w32[i] = v;
+        }
+        for (int i = 4 * nw + (int)tid; i < we - ws; i += PM_THREADS) win[i] = in[ws + i];
+        const int np = (s1 - ws) >> 1;                     // link pairs (ws even)
+        uint32_t* p32 = (uint32_t*)pvl;
+        for (int i = (int)tid; i < np; i += PM_THREADS) p32[i] = *(const GLB uint32_t*)(pv + ws + 2 * i);
+        for (int i = 2 * np + (int)tid; i < s1 - ws; i += PM_THREADS) pvl[i] = pv[ws + i];
+    }
     __syncthreads();
     GLB uint64_t* rec = (GLB uint64_t*)A.rec_buf + (uint64_t)sid * A.rec_stride;
     const int max_chain = c_config[A.level][3], qchain = max_chain >> 2, nice = c_config[A.level][2];
-    for (int p = s0 + (int)tid; p < s1; p += PM_THREADS) {
-        const int hh = pvl[p - ws];
-        uint32_t full = 0, quarter = 0;
-        if (hh != 0 && p - hh <= MAX_DIST) {
-            const int limit = p > MAX_DIST ? p - MAX_DIST : 0;
-            const uint32_t sp = (uint32_t)(p - ws);
-            const uint32_t s4 = pm_w4(win, sp);
-            int best = MIN_MATCH - 1, bpos = 0, qbest = 0, qpos = 0, k = 0;
-            bool qdone = false;
-            uint32_t sb = win[sp + best];
-            int cur = hh, chain = max_chain;
-            do {
-                ++k;
-                const uint32_t cp = (uint32_t)(cur - ws);
-                if (win[cp + best] == sb) {              // can beat best (deflate.ts:866-882)
-                    uint32_t x = pm_w4(win, cp) ^ s4;
-                    int len;
-                    if (x) len = __builtin_ctz(x) >> 3;
-                    else {
-                        len = 4;
-                        for (;;) {
-                            x = pm_w4(win, cp + len) ^ pm_w4(win, sp + len);
-                            if (x) { len += __builtin_ctz(x) >> 3; break; }
-                            len += 4;
-                            if (len >= MAX_MATCH) break;
-                        }
-                        if (len > MAX_MATCH) len = MAX_MATCH;
-                    }
-                    if (len > best) {
-                        best = len;
-                        bpos = cur;
-                        if (len >= nice) break;
-                        sb = win[sp + best];
-                    }
-                }
-                if (k == qchain) { qbest = best; qpos = bpos; qdone = true; }
-            } while ((cur = pvl[cur - ws]) > limit && --chain != 0);
-            if (!qdone) { qbest = best; qpos = bpos; }
-            full = best > MIN_MATCH - 1 ? ((uint32_t)best << 16) | (uint32_t)(p - bpos) : 0u;
-            quarter = qbest > MIN_MATCH - 1 ? ((uint32_t)qbest << 16) | (uint32_t)(p - qpos) : 0u;
+    // this wave's positions
+    const int per = (s1 - s0 + PM_THREADS / 64 - 1) / (PM_THREADS / 64);
+    const int q0 = s0 + (int)wv * per, q1 = q0 + per < s1 ? q0 + per : s1;
+    int next = q0;                                          // wave-uniform queue head
+    bool act = false;
+    int p = s0, cur = 0, best = 0, bpos = 0, qbest = 0, qpos = 0, k = 0, chain = 0, limit = 0;
+    uint32_t sb = 0, s4 = 0;
+    for (;;) {
+        // idle lanes take the next positions
+        const uint64_t im = __ballot(!act);
+        if (im && next < q1) {
+            const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(im >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)im, 0u));
+            const int pn = next + (int)rank;
+            const bool take = !act && pn < q1;
+            next += __popcll(im);
+            if (take) {
+                p = pn;
+                act = true;
+                cur = pvl[p - ws];                              // hash_head
+                best = MIN_MATCH - 1; bpos = 0; qbest = -1; k = 0; chain = max_chain;
+                limit = p > MAX_DIST ? p - MAX_DIST : 0;
+                const uint32_t sp = (uint32_t)(p - ws);
+                s4 = pm_w4(win, sp);
+                sb = win[sp + best];
+                if (cur == 0 || p - cur > MAX_DIST) chain = 0;  // no search (deflate.ts:1092)
+            }
         }
-        rec[p] = ((uint64_t)quarter << 32) | full;
+        if (!__ballot(act)) break;
+        // one candidate per active lane, branch-free but for the rare long compare
+        const bool live = act && chain > 0;
+        const uint32_t cp = (uint32_t)((live ? cur : p) - ws), sp = (uint32_t)(p - ws);
+        const bool cand = live && win[cp + best] == sb;      // can beat best (deflate.ts:866-882)
+        uint32_t x = pm_w4(win, cp) ^ s4;
+        int len = x ? (int)(__builtin_ctz(x) >> 3) : 4;
+        bool more = cand && x == 0;
+        if (__ballot(more)) {                                // matches of more than 4 bytes
+            while (__ballot(more)) {
+                x = more ? pm_w4(win, cp + (uint32_t)len) ^ pm_w4(win, sp + (uint32_t)len) : 1u;
+                len += more ? (x ? (int)(__builtin_ctz(x) >> 3) : 4) : 0;
+                more = more && x == 0 && len < MAX_MATCH;
+            }
+            len = len > MAX_MATCH ? MAX_MATCH : len;
+        }
+        const bool upd = cand && len > best;
+        best = upd ? len : best;
+        bpos = upd ? cur : bpos;
+        bool fin = upd && len >= nice;
+        sb = win[sp + (best < MAX_MATCH ? best : MAX_MATCH)];
+        k += live ? 1 : 0;
+        const bool cap = live && k == qchain;
+        qbest = cap ? best : qbest;
+        qpos = cap ? bpos : qpos;
+        const int ncur = pvl[(uint32_t)((live ? cur : p) - ws)];
+        fin = act && (fin || !live || !(ncur > limit && chain - 1 != 0));
+        cur = ncur;
+        chain -= 1;
+        if (fin) {
+            if (qbest < 0) { qbest = best; qpos = bpos; }
+            const uint32_t full = best > MIN_MATCH - 1 ? ((uint32_t)best << 16) | (uint32_t)(p - bpos) : 0u;
+            const uint32_t quarter = qbest > MIN_MATCH - 1 ? ((uint32_t)qbest << 16) | (uint32_t)(p - qpos) : 0u;
+            rec[p] = ((uint64_t)quarter << 32) | full;
+            act = false;
+        }
     }
 }
 
