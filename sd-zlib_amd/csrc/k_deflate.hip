@@ -57,6 +57,34 @@ struct DSlab {                      // per-stream HBM state
 };
 
 #define SLAB_BYTES ((sizeof(DSlab) + 255) & ~(uint64_t)255)
+
+// record path (levels 4-9, inputs <= 64 KiB): the stream's bookkeeping lives in its slab,
+// FStream over the window area and per-block code tables over the pending area.
+#define PM_TAIL (MAX_MATCH + MIN_MATCH + 1)       // last positions: searched by k_dfl_tail
+#define FB_MAXB 16                                  // blocks per stream (<= 9 for 64 KiB)
+#define FB_TAB_BYTES 2048                           // per block: codes + header words
+#define FB_HDR_OFF 1280                             // header words within a block's table
+#define FB_HDR_WORDS 176
+struct FBlock {
+    uint32_t sym0, nsym;            // the block's symbols in the stream's symbol buffer
+    int32_t block_start, strstart;  // reference coordinates at the flush (rebased after the slide)
+    int32_t off;                    // original position of window index 0 at the flush
+    uint32_t eof;
+    uint32_t type;                  // k_dfl_trees: 0 stored, 1 static, 2 dynamic
+    uint32_t hbits;                 // header bits (3 block-type bits + dynamic tree description)
+    uint32_t dbits;                 // symbol bits incl. END_BLOCK (static / dynamic)
+    uint32_t stored_len;
+};
+struct FStream {
+    uint32_t nblk;
+    uint32_t flag;                  // nonzero: the stream is redone by the serial kernel
+    uint32_t pad[2];
+    FBlock blk[FB_MAXB];
+};
+static_assert(sizeof(FStream) <= WINDOW_SIZE, "FStream fits the window area");
+static_assert(FB_MAXB * FB_TAB_BYTES <= PENDING_SIZE, "block tables fit the pending area");
+static_assert(FB_HDR_OFF >= (L_CODES + D_CODES) * 4 && FB_HDR_OFF + FB_HDR_WORDS * 4 <= FB_TAB_BYTES, "table layout");
+
 uint64_t deflate_state_bytes() { return SLAB_BYTES; }
 
 // tables shared by all streams (deftree.ts:25-38, 269-298, 319-337)
@@ -143,12 +171,16 @@ struct DS {
     int heap_len, heap_max;
     int l_max_code, d_max_code, bl_max_code;
     int err;                        // 1 = pending_buf overflow (reference undefined), 2 = out overflow
-    // record path (levels 4-9, inputs <= 64 KiB): window = the input, no head/prev tables
-    const GLB uint64_t* rec;        // per position: matches found by k_dfl_match (null: classic path)
-    const GLB uint16_t* pvp;        // per position: previous position of the same hash (k_dfl_chain)
-    int off;                        // original position of window index 0 (32768 after the slide)
-    int tail;                       // first position whose match search runs here (end of input)
+#ifdef SDZ_TIMING
+    bool timed;
+    unsigned long long tlast, tacc[8];
+#endif
 };
+#ifdef SDZ_TIMING                   // development aid: cycles per phase, lane 0 of a few waves
+#define DF_STAMP(s, k) do { if ((s).timed) { const unsigned long long t_ = clock64(); (s).tacc[k] += t_ - (s).tlast; (s).tlast = t_; } } while (0)
+#else
+#define DF_STAMP(s, k) do {} while (0)
+#endif
 
 // ------------------------------------------------------------------ bit writer (deflate.ts:347-374)
 
@@ -178,14 +210,19 @@ __device__ __forceinline__ void send_code(DS& s, int c, const GLB uint16_t* tree
 
 // ------------------------------------------------------------------ trees (deftree.ts)
 
-__device__ __forceinline__ bool smaller(const GLB uint16_t* tree, int n, int m, const GLB uint16_t* depth) {
+// The tree builders are templated on a context C (heap / depth / bl_count / next_code /
+// bltree arrays + heap_len, heap_max, opt_len, static_len) so the serial path (HBM slab)
+// and the record path's tree kernel (LDS) run the same code.
+template <class TP, class DP>
+__device__ __forceinline__ bool smaller(TP tree, int n, int m, DP depth) {
     int tn = tree[n * 2], tm = tree[m * 2];
     return tn < tm || (tn == tm && depth[n] <= depth[m]);
 }
 
-__device__ void pqdownheap(DS& s, GLB uint16_t* tree, int k) {                 // deflate.ts:241-263
-    auto* heap = s.S->heap;
-    auto* depth = s.S->depth;
+template <class C, class TP>
+__device__ void pqdownheap(C& s, TP tree, int k) {                            // deflate.ts:241-263
+    auto* heap = s.heap;
+    auto* depth = s.depth;
     int v = heap[k];
     int j = k << 1;
     while (j <= s.heap_len) {
@@ -199,10 +236,11 @@ __device__ void pqdownheap(DS& s, GLB uint16_t* tree, int k) {                 /
 }
 
 // deftree.ts:60-132 gen_bitlen
-__device__ void gen_bitlen(DS& s, GLB uint16_t* tree, int max_code, const GLB uint16_t* stree,
+template <class C, class TP>
+__device__ void gen_bitlen(C& s, TP tree, int max_code, const GLB uint16_t* stree,
                            const GLB uint8_t* extra, int base, int max_length) {
-    auto* heap = s.S->heap;
-    auto* bl_count = s.S->bl_count;
+    auto* heap = s.heap;
+    auto* bl_count = s.bl_count;
     int h, n, m, bits, xbits, f, overflow = 0;
     for (bits = 0; bits <= 15; bits++) bl_count[bits] = 0;
     tree[heap[s.heap_max] * 2 + 1] = 0;
@@ -243,9 +281,10 @@ __device__ void gen_bitlen(DS& s, GLB uint16_t* tree, int max_code, const GLB ui
 }
 
 // deftree.ts:155-182 gen_codes
-__device__ void gen_codes(DS& s, GLB uint16_t* tree, int max_code) {
-    auto* next_code = s.S->next_code;
-    auto* bl_count = s.S->bl_count;
+template <class C, class TP>
+__device__ void gen_codes(C& s, TP tree, int max_code) {
+    auto* next_code = s.next_code;
+    auto* bl_count = s.bl_count;
     int code = 0;
     for (int bits = 1; bits <= 15; bits++) {
         code = (code + bl_count[bits - 1]) << 1;
@@ -259,10 +298,11 @@ __device__ void gen_codes(DS& s, GLB uint16_t* tree, int max_code) {
 }
 
 // deftree.ts:190-267 build_tree; returns max_code
-__device__ int build_tree(DS& s, GLB uint16_t* tree, const GLB uint16_t* stree, const GLB uint8_t* extra,
+template <class C, class TP>
+__device__ int build_tree(C& s, TP tree, const GLB uint16_t* stree, const GLB uint8_t* extra,
                           int base, int elems, int max_length) {
-    auto* heap = s.S->heap;
-    auto* depth = s.S->depth;
+    auto* heap = s.heap;
+    auto* depth = s.depth;
     int n, m, max_code = -1, node;
     s.heap_len = 0;
     s.heap_max = HEAP_SIZE;
@@ -300,8 +340,9 @@ __device__ int build_tree(DS& s, GLB uint16_t* tree, const GLB uint16_t* stree, 
 }
 
 // deflate.ts:267-312 scan_tree
-__device__ void scan_tree(DS& s, GLB uint16_t* tree, int max_code) {
-    auto* bl = s.S->bltree;
+template <class C, class TP>
+__device__ void scan_tree(C& s, TP tree, int max_code) {
+    auto* bl = s.bltree;
     int prevlen = -1, curlen, nextlen = tree[1], count = 0, max_count = 7, min_count = 4;
     if (nextlen == 0) { max_count = 138; min_count = 3; }
     tree[(max_code + 1) * 2 + 1] = 0xffff;
@@ -321,22 +362,23 @@ __device__ void scan_tree(DS& s, GLB uint16_t* tree, int max_code) {
     }
 }
 
-// deflate.ts:378-429 send_tree
-__device__ void send_tree(DS& s, const GLB uint16_t* tree, int max_code) {
-    auto* bl = s.S->bltree;
+// deflate.ts:378-429 send_tree, through the context's bit writer
+template <class C, class TP>
+__device__ void send_tree(C& s, TP tree, int max_code) {
+    auto* bl = s.bltree;
     int prevlen = -1, curlen, nextlen = tree[1], count = 0, max_count = 7, min_count = 4;
     if (nextlen == 0) { max_count = 138; min_count = 3; }
     for (int n = 0; n <= max_code; n++) {
         curlen = nextlen;
         nextlen = tree[(n + 1) * 2 + 1];
         if (++count < max_count && curlen == nextlen) continue;
-        else if (count < min_count) { do { send_code(s, curlen, bl); } while (--count != 0); }
+        else if (count < min_count) { do { s.bits(bl[curlen * 2], bl[curlen * 2 + 1]); } while (--count != 0); }
         else if (curlen != 0) {
-            if (curlen != prevlen) { send_code(s, curlen, bl); count--; }
-            send_code(s, 16, bl);
-            send_bits(s, (uint32_t)(count - 3), 2);
-        } else if (count <= 10) { send_code(s, 17, bl); send_bits(s, (uint32_t)(count - 3), 3); }
-        else { send_code(s, 18, bl); send_bits(s, (uint32_t)(count - 11), 7); }
+            if (curlen != prevlen) { s.bits(bl[curlen * 2], bl[curlen * 2 + 1]); count--; }
+            s.bits(bl[16 * 2], bl[16 * 2 + 1]);
+            s.bits((uint32_t)(count - 3), 2);
+        } else if (count <= 10) { s.bits(bl[17 * 2], bl[17 * 2 + 1]); s.bits((uint32_t)(count - 3), 3); }
+        else { s.bits(bl[18 * 2], bl[18 * 2 + 1]); s.bits((uint32_t)(count - 11), 7); }
         count = 0;
         prevlen = curlen;
         if (nextlen == 0) { max_count = 138; min_count = 3; }
@@ -344,6 +386,14 @@ __device__ void send_tree(DS& s, const GLB uint16_t* tree, int max_code) {
         else { max_count = 7; min_count = 4; }
     }
 }
+
+// tree context of the serial path: the slab's arrays, the stream's scalars, its bit writer
+struct GTreeCtx {
+    DS& ds;
+    GLB uint16_t *heap, *depth, *bl_count, *next_code, *bltree;
+    int heap_len, heap_max, opt_len, static_len;
+    __device__ void bits(uint32_t v, int len) { send_bits(ds, v, len); }
+};
 
 __device__ __forceinline__ int d_code(const GLB DTables* T, int dist) {
     return dist < 256 ? T->dist_code[dist] : T->dist_code[256 + (dist >> 7)];
@@ -433,14 +483,18 @@ __device__ void flush_pending(DS& s) {
 
 // deflate.ts:614-674 _tr_flush_block (+ flush_block_only 676-680)
 __device__ __noinline__ void flush_block(DS& s, bool eof) {
+    DF_STAMP(s, 1);
     int buf = s.block_start >= 0 ? s.block_start : -1;
     int stored_len = s.strstart - s.block_start;
-    s.l_max_code = build_tree(s, s.S->ltree, s.T->static_ltree, s.T->extra_lbits, 257, L_CODES, 15);
-    s.d_max_code = build_tree(s, s.S->dtree, s.T->static_dtree, s.T->extra_dbits, 0, D_CODES, 15);
+    GTreeCtx c{s, s.S->heap, s.S->depth, s.S->bl_count, s.S->next_code, s.S->bltree,
+               s.heap_len, s.heap_max, s.opt_len, s.static_len};
+    s.l_max_code = build_tree(c, s.S->ltree, s.T->static_ltree, s.T->extra_lbits, 257, L_CODES, 15);
+    s.d_max_code = build_tree(c, s.S->dtree, s.T->static_dtree, s.T->extra_dbits, 0, D_CODES, 15);
     // build_bl_tree (deflate.ts:316-339)
-    scan_tree(s, s.S->ltree, s.l_max_code);
-    scan_tree(s, s.S->dtree, s.d_max_code);
-    build_tree(s, s.S->bltree, nullptr, s.T->extra_blbits, 0, BL_CODES, 7);
+    scan_tree(c, s.S->ltree, s.l_max_code);
+    scan_tree(c, s.S->dtree, s.d_max_code);
+    build_tree(c, s.S->bltree, (const GLB uint16_t*)nullptr, s.T->extra_blbits, 0, BL_CODES, 7);
+    s.heap_len = c.heap_len; s.heap_max = c.heap_max; s.opt_len = c.opt_len; s.static_len = c.static_len;
     int max_blindex;
     for (max_blindex = BL_CODES - 1; max_blindex >= 3; max_blindex--)
         if (s.S->bltree[c_bl_order[max_blindex] * 2 + 1] != 0) break;
@@ -448,6 +502,7 @@ __device__ __noinline__ void flush_block(DS& s, bool eof) {
     uint32_t opt_lenb = (uint32_t)(s.opt_len + 3 + 7) >> 3;
     uint32_t static_lenb = (uint32_t)(s.static_len + 3 + 7) >> 3;
     if (static_lenb <= opt_lenb) opt_lenb = static_lenb;
+    DF_STAMP(s, 2);
     if ((uint32_t)(stored_len + 4) <= opt_lenb && buf != -1) {
         send_bits(s, eof ? 1u : 0u, 3);                     // _tr_stored_block
         bi_windup(s);
@@ -455,10 +510,7 @@ __device__ __noinline__ void flush_block(DS& s, bool eof) {
         put_short(s, ~(uint32_t)stored_len);
         if (s.pending + stored_len > PENDING_SIZE) s.err |= 1;
         else {
-            if (s.rec)
-                for (int i = 0; i < stored_len; i++) s.S->pending[s.pending + i] = s.in[s.off + buf + i];
-            else
-                for (int i = 0; i < stored_len; i++) s.S->pending[s.pending + i] = s.S->window[buf + i];
+            for (int i = 0; i < stored_len; i++) s.S->pending[s.pending + i] = s.S->window[buf + i];
             s.pending += stored_len;
         }
     } else if (static_lenb == opt_lenb) {
@@ -471,14 +523,17 @@ __device__ __noinline__ void flush_block(DS& s, bool eof) {
         send_bits(s, (uint32_t)(dcodes - 1), 5);
         send_bits(s, (uint32_t)(blcodes - 4), 4);
         for (int rank = 0; rank < blcodes; rank++) send_bits(s, s.S->bltree[c_bl_order[rank] * 2 + 1], 3);
-        send_tree(s, s.S->ltree, lcodes - 1);
-        send_tree(s, s.S->dtree, dcodes - 1);
+        GTreeCtx c{s, s.S->heap, s.S->depth, s.S->bl_count, s.S->next_code, s.S->bltree, 0, 0, 0, 0};
+        send_tree(c, s.S->ltree, lcodes - 1);
+        send_tree(c, s.S->dtree, dcodes - 1);
         compress_block(s, s.S->ltree, s.S->dtree);
     }
+    DF_STAMP(s, 3);
     init_block(s);
     if (eof) bi_windup(s);
     s.block_start = s.strstart;
     flush_pending(s);
+    DF_STAMP(s, 4);
 }
 
 // deflate.ts:690-766 fill_window (the whole input is available: one-shot append)
@@ -649,138 +704,6 @@ __device__ __forceinline__ void deflate_slow(DS& s) {
     flush_block(s, true);
 }
 
-// ------------------------------------------------------------------ record path (levels 4-9)
-// The reference's deflate_slow with its two expensive parts precomputed in parallel:
-//   k_dfl_chain  pvp[p]: the hash chain link insert_string leaves for position p (the previous
-//                position with the same 3-byte hash) -- every position is inserted once, in
-//                order, in deflate_slow (deflate.ts:1077-1080, 1119-1126);
-//   k_dfl_match  rec[p]: what longest_match (deflate.ts:827-946) returns at p for
-//                prev_length < good_match (full chain) and >= good_match (chain >> 2), as
-//                (length, distance) of the first candidate reaching the chain's best length
-//                (or nice_match).  Called with best_len = prev_length, the reference returns
-//                that entry if its length exceeds prev_length and prev_length otherwise.
-// Positions within 262 bytes of the end search here, exactly as the reference does: their
-// comparisons may read past the input (zeros; after the window slide, the stale upper
-// half -- SURVEY A6) and nice_match / the result are clamped to the lookahead.
-// The parser below keeps the reference's (rebased) coordinates; window index i is original
-// position i + off.  Only inputs of at most 64 KiB take this path: the window then holds
-// the whole input and slides at most once, at the end.
-#define PM_TAIL (MAX_MATCH + MIN_MATCH + 1)
-__device__ __forceinline__ uint32_t rp_byte(const DS& s, int i) {     // window[i] on the record path
-    const int P = i + s.off;
-    if ((uint64_t)P < s.in_len) return s.in[P];
-    return (s.off && P >= WINDOW_SIZE) ? s.in[P - W_SIZE] : 0u;      // stale half after the slide
-}
-__device__ __forceinline__ int rp_head(const DS& s) {                  // insert_string's hash_head
-    const int v = s.pvp[s.strstart + s.off];
-    return s.off ? (v >= W_SIZE ? v - W_SIZE : 0) : v;                   // head[] rebased at the slide
-}
-__device__ __forceinline__ int rp_prev(const DS& s, int cur) {          // prev[cur & W_MASK]
-    const int v = s.pvp[cur + s.off];
-    return s.off ? (v >= W_SIZE ? v - W_SIZE : 0) : v;
-}
-// deflate.ts:827-946 verbatim over rp_byte / rp_prev (end of input only)
-__device__ int longest_match_tail(DS& s, int cur_match) {
-    int chain_length = s.max_chain;
-    const int scan = s.strstart;
-    int best_len = s.prev_length;
-    const int limit = s.strstart > MAX_DIST ? s.strstart - MAX_DIST : 0;
-    int nice = s.nice_match;
-    const int strend = s.strstart + MAX_MATCH;
-    int scan_end1 = rp_byte(s, scan + best_len - 1);
-    int scan_end = rp_byte(s, scan + best_len);
-    const int scan_start = rp_byte(s, scan), scan_start1 = rp_byte(s, scan + 1);
-    if (s.prev_length >= s.good_match) chain_length >>= 2;
-    if (nice > s.lookahead) nice = s.lookahead;
-    do {
-        const int match = cur_match;
-        if ((int)rp_byte(s, match + best_len) != scan_end || (int)rp_byte(s, match + best_len - 1) != scan_end1 ||
-            (int)rp_byte(s, match) != scan_start || (int)rp_byte(s, match + 1) != scan_start1)
-            continue;
-        int sp = scan + 2, mp = match + 2;
-        do {                                             // 4 bytes at a time from +2 (deflate.ts:899-921)
-            int k = 0;
-            while (k < 4 && rp_byte(s, sp + k) == rp_byte(s, mp + k)) ++k;
-            if (k < 4) { sp += k; mp += k; break; }
-            sp += 4; mp += 4;
-        } while (sp < strend);
-        if (sp > strend) sp = strend;
-        const int len = MAX_MATCH - (strend - sp);
-        if (len > best_len) {
-            s.match_start = match;
-            best_len = len;
-            if (len >= nice) break;
-            scan_end1 = rp_byte(s, scan + best_len - 1);
-            scan_end = rp_byte(s, scan + best_len);
-        }
-    } while ((cur_match = rp_prev(s, cur_match)) > limit && --chain_length != 0);
-    return best_len <= s.lookahead ? best_len : s.lookahead;
-}
-// deflate.ts:1054-1182 (levels 4-9) on the records
-__device__ __forceinline__ void deflate_slow_rec(DS& s) {
-    int hash_head = 0;
-    s.lookahead = (int)s.in_len;                         // fill_window's first call loads everything
-    for (;;) {
-        if (s.lookahead < MIN_LOOKAHEAD) {               // fill_window: no input left; it may slide
-            if (!s.off && s.strstart >= W_SIZE + W_SIZE - MIN_LOOKAHEAD) {
-                s.match_start -= W_SIZE;
-                s.strstart -= W_SIZE;
-                s.block_start -= W_SIZE;
-                s.off = W_SIZE;
-            }
-            if (s.lookahead == 0) break;
-        }
-        if (s.lookahead >= MIN_MATCH) hash_head = rp_head(s);
-        s.prev_length = s.match_length;
-        const int prev_match = s.match_start;
-        s.match_length = MIN_MATCH - 1;
-        if (hash_head != 0 && s.prev_length < s.max_lazy && ((s.strstart - hash_head) & 0xffff) <= MAX_DIST) {
-            const int P = s.strstart + s.off;
-            if (P < s.tail) {
-                const uint64_t r = s.rec[P];
-                const uint32_t e = s.prev_length >= s.good_match ? (uint32_t)(r >> 32) : (uint32_t)r;
-                const int len = (int)(e >> 16);
-                if (len > s.prev_length) { s.match_length = len; s.match_start = s.strstart - (int)(e & 0xffffu); }
-                else s.match_length = s.prev_length;
-            } else {
-                s.match_length = longest_match_tail(s, hash_head);
-            }
-            if (s.match_length <= 5 && s.match_length == MIN_MATCH && s.strstart - s.match_start > 4096)
-                s.match_length = MIN_MATCH - 1;
-        }
-        if (s.prev_length >= MIN_MATCH && s.match_length <= s.prev_length) {
-            const int max_insert = s.strstart + s.lookahead - MIN_MATCH;
-            const bool bflush = tr_tally(s, s.strstart - 1 - prev_match, s.prev_length - MIN_MATCH);
-            s.lookahead -= s.prev_length - 1;
-            // the reference inserts strstart+1 .. strstart+prev_length-2 (up to max_insert);
-            // only the last insertion's hash_head survives
-            const int last = s.strstart + s.prev_length - 2;
-            const int lastins = last < max_insert ? last : max_insert;
-            if (lastins > s.strstart) { const int st = s.strstart; s.strstart = lastins; hash_head = rp_head(s); s.strstart = st; }
-            s.strstart = last;
-            s.prev_length = 0;
-            s.match_available = 0;
-            s.match_length = MIN_MATCH - 1;
-            s.strstart++;
-            if (bflush) flush_block(s, false);
-        } else if (s.match_available) {
-            const bool bflush = tr_tally(s, 0, rp_byte(s, s.strstart - 1));
-            if (bflush) flush_block(s, false);
-            s.strstart++;
-            s.lookahead--;
-        } else {
-            s.match_available = 1;
-            s.strstart++;
-            s.lookahead--;
-        }
-    }
-    if (s.match_available) {
-        tr_tally(s, 0, rp_byte(s, s.strstart - 1));
-        s.match_available = 0;
-    }
-    flush_block(s, true);
-}
-
 // adler32.ts:34-105 / crc32.ts:48-106 over the input (Deflater.append, sd-deflate.ts:185-190)
 __device__ int32_t input_checksum(const GLB uint8_t* p, uint64_t n, bool gzip, const uint32_t* crct) {
     if (gzip) {
@@ -815,6 +738,11 @@ __global__ __launch_bounds__(DF_THREADS) void k_deflate(DeflateArgs A) {
     if (sid >= A.n) return;
 
     DS s;
+#ifdef SDZ_TIMING
+    s.timed = A.dbg && (sid & 63) == 0 && sid < 64 * 16;
+    for (int k = 0; k < 8; ++k) s.tacc[k] = 0;
+    s.tlast = clock64();
+#endif
     s.S = (GLB DSlab*)(A.state + (uint64_t)sid * SLAB_BYTES);
     s.T = (const GLB DTables*)&g_dt;
     s.in = (const GLB uint8_t*)(A.in + A.in_off[sid]);
@@ -824,12 +752,8 @@ __global__ __launch_bounds__(DF_THREADS) void k_deflate(DeflateArgs A) {
     s.out_cap = A.out_cap[sid];
     s.out_len = 0;
     s.err = 0;
-    s.rec = nullptr; s.pvp = nullptr; s.off = 0; s.tail = 0;
-    if (A.rec_buf && s.in_len <= A.rec_stride) {
-        s.rec = (const GLB uint64_t*)A.rec_buf + (uint64_t)sid * A.rec_stride;
-        s.pvp = (const GLB uint16_t*)A.pv_buf + (uint64_t)sid * A.rec_stride;
-        s.tail = s.in_len > PM_TAIL ? (int)s.in_len - PM_TAIL : 0;
-    }
+    // after the record path (A.fast) only the streams it handed back run here
+    if (A.fast && !((const GLB FStream*)s.S->window)->flag) return;
     sdz_deflate_record R;
     R.status = SDZ_OK; R.checksum = 0; R.out_len = 0; R.reserved = 0;
     if (s.in_len == 0) {                        // sd-deflate.ts:180-182 + 232-234
@@ -838,7 +762,7 @@ __global__ __launch_bounds__(DF_THREADS) void k_deflate(DeflateArgs A) {
         return;
     }
     // Deflate constructor (deflate.ts:196-220) + window zero fill (deflate.ts:119)
-    if (!s.rec) {
+    {
         const u32x4 z = {0u, 0u, 0u, 0u};
         GLB u32x4* w4 = (GLB u32x4*)s.S->window;
         for (int i = 0; i < WINDOW_SIZE / 16; i++) w4[i] = z;
@@ -866,7 +790,9 @@ __global__ __launch_bounds__(DF_THREADS) void k_deflate(DeflateArgs A) {
     init_block(s);
 
     bool gzip = A.format == SDZ_DEFLATE_GZIP;
+    DF_STAMP(s, 5);
     int32_t cks = input_checksum(s.in, s.in_len, gzip, crct);
+    DF_STAMP(s, 0);
     // container header (sd-deflate.ts:98-152): written straight to the output slot
     uint64_t hdr = A.format == SDZ_DEFLATE_ZLIB ? 2 : gzip ? 10 + (A.fname_len ? A.fname_len + 1 : 0) : 0;
     if (hdr > s.out_cap) { R.status = SDZ_OUT_OVERFLOW; A.rec[sid] = R; return; }
@@ -882,7 +808,6 @@ __global__ __launch_bounds__(DF_THREADS) void k_deflate(DeflateArgs A) {
     s.out_len = hdr;
 
     if (c_config[A.level][4]) deflate_fast(s);
-    else if (s.rec) deflate_slow_rec(s);
     else deflate_slow(s);
 
     // trailer (sd-deflate.ts:154-165)
@@ -900,6 +825,10 @@ __global__ __launch_bounds__(DF_THREADS) void k_deflate(DeflateArgs A) {
         s.out_len += 8;
     }
     R.status = (s.err & 2) ? SDZ_OUT_OVERFLOW : (s.err & 1) ? SDZ_DATA_ERROR : SDZ_OK;
+    DF_STAMP(s, 5);
+#ifdef SDZ_TIMING
+    if (s.timed) for (int k = 0; k < 8; ++k) atomicAdd(&A.dbg[k], s.tacc[k]);
+#endif
     R.checksum = cks;
     R.out_len = s.out_len;
     A.rec[sid] = R;
@@ -1048,6 +977,507 @@ __global__ __launch_bounds__(PM_THREADS) void k_dfl_match(DeflateArgs A, uint32_
     }
 }
 
+// ------------------------------------------------------------------ record path: tail, parse, trees, encode
+// After k_dfl_chain / k_dfl_match the rest of deflate_slow is split by what it depends on:
+//   k_dfl_tail   records of the last PM_TAIL positions (the reference's longest_match itself);
+//   k_dfl_parse  the lazy parse (deflate.ts:1054-1182) and _tr_tally (deflate.ts:488-524):
+//                serial per stream but only registers + one round trip per position; emits
+//                the symbols and where each block ends (the flush points);
+//   k_dfl_trees  per block: frequencies, build_tree / build_bl_tree, the block type choice of
+//                _tr_flush_block (deflate.ts:614-674), the code table and the header bits;
+//   k_dfl_encode per stream: bit layout of its blocks, then the symbols of each block packed
+//                by all threads at prefix-summed bit offsets (compress_block, deflate.ts:527-571).
+// A stream leaves the path (flag) where the reference's output would not be the plain
+// bitstream -- its pending_buf overlay overtaken by the output, a pending_buf or
+// output slot overflow -- and is redone by the serial kernel (k_deflate, A.fast).
+
+// window byte i in the rebased coordinates of a search at a position with window offset off
+__device__ __forceinline__ uint32_t tail_byte(const GLB uint8_t* in, int n, int off, int i) {
+    const int P = i + off;
+    if (P < n) return in[P];
+    return (off && P >= WINDOW_SIZE) ? in[P - W_SIZE] : 0u;          // stale half after the slide
+}
+// deflate.ts:827-946 at original position P (lookahead >= MIN_MATCH), from best_len = 2.
+// The window slides when the parse reaches P >= 65274 with lookahead < MIN_LOOKAHEAD
+// (deflate.ts:711-738, 1075); the search runs in the coordinates the reference has then.
+__device__ uint32_t tail_search(const GLB uint8_t* in, const GLB uint16_t* pv, int n, int P, int chain_length, int nice) {
+    const int off = (P >= WINDOW_SIZE - MIN_LOOKAHEAD && n - P < MIN_LOOKAHEAD) ? W_SIZE : 0;
+    const int strstart = P - off;
+    auto rb = [&](int v) { return off ? (v >= W_SIZE ? v - W_SIZE : 0) : v; };
+    int cur = rb(pv[P]);
+    if (cur == 0 || ((strstart - cur) & 0xffff) > MAX_DIST) return 0u;      // no search (deflate.ts:1092)
+    const int lookahead = n - P;
+    if (nice > lookahead) nice = lookahead;
+    const int limit = strstart > MAX_DIST ? strstart - MAX_DIST : 0;
+    int best = MIN_MATCH - 1, bstart = 0;
+    uint32_t scan_end1 = tail_byte(in, n, off, strstart + best - 1), scan_end = tail_byte(in, n, off, strstart + best);
+    const uint32_t c0 = tail_byte(in, n, off, strstart), c1 = tail_byte(in, n, off, strstart + 1);
+    do {
+        const int match = cur;
+        if (tail_byte(in, n, off, match + best) != scan_end || tail_byte(in, n, off, match + best - 1) != scan_end1 ||
+            tail_byte(in, n, off, match) != c0 || tail_byte(in, n, off, match + 1) != c1)
+            continue;
+        int len = 3;                          // byte 2 is not compared (equal hash, deflate.ts:891-897)
+        while (len < MAX_MATCH && tail_byte(in, n, off, strstart + len) == tail_byte(in, n, off, match + len)) ++len;
+        if (len > best) {
+            bstart = match;
+            best = len;
+            if (len >= nice) break;
+            scan_end1 = tail_byte(in, n, off, strstart + best - 1);
+            scan_end = tail_byte(in, n, off, strstart + best);
+        }
+    } while ((cur = rb(pv[cur + off])) > limit && --chain_length != 0);
+    return best > MIN_MATCH - 1 ? ((uint32_t)best << 16) | (uint32_t)(strstart - bstart) : 0u;
+}
+__global__ __launch_bounds__(256) void k_dfl_tail(DeflateArgs A) {
+    const uint32_t sid = blockIdx.x;
+    if (sid >= A.n) return;
+    const uint64_t in_len = A.in_len[sid];
+    if (in_len > A.rec_stride || in_len < MIN_MATCH) return;
+    const int n = (int)in_len, tail = n > PM_TAIL ? n - PM_TAIL : 0;
+    const GLB uint8_t* in = (const GLB uint8_t*)(A.in + A.in_off[sid]);
+    const GLB uint16_t* pv = (const GLB uint16_t*)A.pv_buf + (uint64_t)sid * A.rec_stride;
+    GLB uint64_t* rec = (GLB uint64_t*)A.rec_buf + (uint64_t)sid * A.rec_stride;
+    const int max_chain = c_config[A.level][3], nice = c_config[A.level][2];
+    for (int P = tail + (int)threadIdx.x; P <= n - MIN_MATCH; P += 256) {
+        const uint32_t full = tail_search(in, pv, n, P, max_chain, nice);
+        const uint32_t quarter = tail_search(in, pv, n, P, max_chain >> 2, nice);
+        rec[P] = ((uint64_t)quarter << 32) | full;
+    }
+}
+
+// k_dfl_parse: one lane per stream, the reference's loop with its scalars in registers.
+// At each position the record gives longest_match(prev_length): the record's candidate if
+// it is longer than prev_length, else prev_length, clamped to the lookahead.  (In the tail
+// with prev_length >= min(nice, lookahead) the reference returns the lookahead, and so does
+// this; otherwise its walk stops at the same candidate as the record's.)  Positions with
+// lookahead < MIN_MATCH are not searched here: the reference's result there is <= 2 either
+// way and nothing downstream tells the values apart.
+// Symbols go to the stream's symbol buffer -- the front of its record buffer: symbol k is
+// written after record k/2 has been read -- as lc | dist << 8 (dist 0: literal lc).
+__global__ __launch_bounds__(64) void k_dfl_parse(DeflateArgs A) {
+    __shared__ uint32_t dfq[D_CODES][64];                   // dist-code counts of the open block
+    __shared__ uint8_t dcode[512];
+    const uint32_t lane = threadIdx.x, sid = blockIdx.x * 64 + lane;
+    for (int i = (int)lane; i < 512; i += 64) dcode[i] = g_dt.dist_code[i];
+    for (int c = 0; c < D_CODES; ++c) dfq[c][lane] = 0;
+    __syncthreads();
+    if (sid >= A.n) return;
+    GLB DSlab* S = (GLB DSlab*)(A.state + (uint64_t)sid * SLAB_BYTES);
+    GLB FStream* F = (GLB FStream*)S->window;
+    const uint64_t in_len = A.in_len[sid];
+    if (in_len == 0 || in_len > A.rec_stride) { F->nblk = 0; F->flag = 1; return; }
+    const int n = (int)in_len;
+    const GLB uint8_t* in = (const GLB uint8_t*)(A.in + A.in_off[sid]);
+    const GLB uint16_t* pv = (const GLB uint16_t*)A.pv_buf + (uint64_t)sid * A.rec_stride;
+    const GLB uint64_t* rec = (const GLB uint64_t*)A.rec_buf + (uint64_t)sid * A.rec_stride;
+    GLB uint32_t* sym = (GLB uint32_t*)A.rec_buf + (uint64_t)sid * A.rec_stride * 2;
+    const int level = A.level, good = c_config[level][0], max_lazy = c_config[level][1];
+    int strstart = 0, lookahead = n, match_length = MIN_MATCH - 1, match_start = 0, match_available = 0;
+    int block_start = 0, off = 0, hash_head = 0;
+    uint32_t last_lit = 0, matches = 0, lx = 0, nblk = 0, sym0 = 0;
+    auto tally = [&](int dist, int lc) -> bool {             // _tr_tally, deflate.ts:488-524
+        sym[lx++] = (uint32_t)lc | ((uint32_t)dist << 8);
+        last_lit++;
+        if (dist) {
+            matches++;
+            const int d = dist - 1;
+            dfq[d < 256 ? dcode[d] : dcode[256 + (d >> 7)]][lane]++;
+        }
+        if ((last_lit & 0x1fff) == 0 && level > 2) {         // TRUNCATE_BLOCK
+            uint32_t out_length = last_lit * 8;
+            const int in_length = strstart - block_start;
+            for (int dc = 0; dc < D_CODES; dc++) out_length += dfq[dc][lane] * (5 + c_extra_dbits[dc]);
+            out_length >>= 3;
+            if (matches < last_lit / 2 && (int)out_length < in_length / 2) return true;
+        }
+        return last_lit == LIT_BUFSIZE - 1;
+    };
+    auto flush = [&](uint32_t eof) {                        // flush_block_only's bookkeeping
+        if (nblk < FB_MAXB) {
+            GLB FBlock* B = &F->blk[nblk];
+            B->sym0 = sym0; B->nsym = last_lit;
+            B->block_start = block_start; B->strstart = strstart; B->off = off; B->eof = eof;
+        }
+        nblk++;
+        sym0 = lx; last_lit = 0; matches = 0;
+        for (int c = 0; c < D_CODES; ++c) dfq[c][lane] = 0;
+        block_start = strstart;
+    };
+    for (;;) {
+        if (lookahead < MIN_LOOKAHEAD) {                     // fill_window: input exhausted; it may slide
+            if (!off && strstart >= W_SIZE + W_SIZE - MIN_LOOKAHEAD) {
+                match_start -= W_SIZE;
+                strstart -= W_SIZE;
+                block_start -= W_SIZE;
+                off = W_SIZE;
+            }
+            if (lookahead == 0) break;
+        }
+        const int P = strstart + off;                        // everything this step reads, at once
+        const uint32_t v = pv[P];
+        const uint64_t r = rec[P];
+        const uint32_t lb = in[P > 0 ? P - 1 : 0];
+        if (lookahead >= MIN_MATCH) hash_head = off ? (v >= W_SIZE ? (int)v - W_SIZE : 0) : (int)v;
+        const int prev_length = match_length, prev_match = match_start;
+        match_length = MIN_MATCH - 1;
+        if (lookahead >= MIN_MATCH && hash_head != 0 && prev_length < max_lazy &&
+            ((strstart - hash_head) & 0xffff) <= MAX_DIST) {
+            const uint32_t e = prev_length >= good ? (uint32_t)(r >> 32) : (uint32_t)r;
+            const int len = (int)(e >> 16);
+            int ml = prev_length;
+            if (len > prev_length) { ml = len; match_start = strstart - (int)(e & 0xffffu); }
+            match_length = ml < lookahead ? ml : lookahead;
+            if (match_length <= 5 && match_length == MIN_MATCH && strstart - match_start > 4096)
+                match_length = MIN_MATCH - 1;
+        }
+        if (prev_length >= MIN_MATCH && match_length <= prev_length) {
+            const int max_insert = strstart + lookahead - MIN_MATCH;
+            const bool bflush = tally(strstart - 1 - prev_match, prev_length - MIN_MATCH);
+            lookahead -= prev_length - 1;
+            // strstart+1 .. strstart+prev_length-2 are inserted (up to max_insert); only the
+            // last insertion's hash_head survives
+            const int last = strstart + prev_length - 2;
+            const int lastins = last < max_insert ? last : max_insert;
+            if (lastins > strstart) {
+                const uint32_t w = pv[lastins + off];
+                hash_head = off ? (w >= W_SIZE ? (int)w - W_SIZE : 0) : (int)w;
+            }
+            strstart = last + 1;
+            match_available = 0;
+            match_length = MIN_MATCH - 1;
+            if (bflush) flush(0);
+        } else if (match_available) {
+            const bool bflush = tally(0, (int)lb);
+            if (bflush) flush(0);
+            strstart++;
+            lookahead--;
+        } else {
+            match_available = 1;
+            strstart++;
+            lookahead--;
+        }
+    }
+    if (match_available) tally(0, in[strstart - 1 + off]);
+    flush(1);
+    F->nblk = nblk;
+    F->flag = nblk > FB_MAXB ? 1u : 0u;
+}
+
+// tree context of the record path: LDS arrays, header bits into LDS words
+struct LTreeCtx {
+    uint16_t *heap, *depth, *bl_count, *next_code, *bltree;
+    int heap_len, heap_max, opt_len, static_len;
+    uint32_t* hdr;
+    uint32_t nb;
+    __device__ void bits(uint32_t v, int len) {
+        const uint32_t w = nb >> 5, sh = nb & 31;
+        hdr[w] |= v << sh;
+        if (sh + (uint32_t)len > 32) hdr[w + 1] |= v >> (32 - sh);
+        nb += (uint32_t)len;
+    }
+};
+
+// k_dfl_trees: one wave per stream, its blocks in turn.  Frequencies from the symbols (LDS
+// atomics), then lane 0 runs build_tree / scan_tree / build_bl_tree and the block type choice
+// exactly as _tr_flush_block does, and the wave exports the code table (code | len << 16)
+// and the block header bits.
+__global__ __launch_bounds__(64) void k_dfl_trees(DeflateArgs A) {
+    __shared__ uint16_t ltree[HEAP_SIZE * 2], dtree[(2 * D_CODES + 1) * 2], bltree[(2 * BL_CODES + 1) * 2];
+    __shared__ uint16_t depth[2 * L_CODES + 1], heap[2 * L_CODES + 1], bl_count[16], next_code[16];
+    __shared__ uint32_t hist[L_CODES + D_CODES];
+    __shared__ uint32_t hdr[FB_HDR_WORDS];
+    __shared__ uint32_t info[4];
+    __shared__ uint8_t lcode_t[256], dcode_t[512];
+    const uint32_t sid = blockIdx.x, lane = threadIdx.x;
+    if (sid >= A.n) return;
+    GLB DSlab* S = (GLB DSlab*)(A.state + (uint64_t)sid * SLAB_BYTES);
+    GLB FStream* F = (GLB FStream*)S->window;
+    if (F->flag) return;
+    const GLB DTables* T = (const GLB DTables*)&g_dt;
+    for (int i = (int)lane; i < 256; i += 64) lcode_t[i] = T->length_code[i];
+    for (int i = (int)lane; i < 512; i += 64) dcode_t[i] = T->dist_code[i];
+    const GLB uint32_t* sym = (const GLB uint32_t*)A.rec_buf + (uint64_t)sid * A.rec_stride * 2;
+    const uint32_t nblk = F->nblk;
+    for (uint32_t b = 0; b < nblk; ++b) {
+        const uint32_t sym0 = F->blk[b].sym0, nsym = F->blk[b].nsym, eof = F->blk[b].eof;
+        const int block_start = F->blk[b].block_start, strstart = F->blk[b].strstart;
+        for (int i = (int)lane; i < L_CODES + D_CODES; i += 64) hist[i] = 0;
+        for (int i = (int)lane; i < FB_HDR_WORDS; i += 64) hdr[i] = 0;
+        for (int i = (int)lane; i < HEAP_SIZE * 2; i += 64) ltree[i] = 0;
+        for (int i = (int)lane; i < (2 * D_CODES + 1) * 2; i += 64) dtree[i] = 0;
+        for (int i = (int)lane; i < (2 * BL_CODES + 1) * 2; i += 64) bltree[i] = 0;
+        __syncthreads();
+        for (uint32_t i = lane; i < nsym; i += 64) {
+            const uint32_t s = sym[sym0 + i], lc = s & 255u, dist = s >> 8;
+            if (dist == 0) atomicAdd(&hist[lc], 1u);
+            else {
+                const uint32_t d = dist - 1;
+                atomicAdd(&hist[257 + lcode_t[lc]], 1u);
+                atomicAdd(&hist[L_CODES + (d < 256 ? dcode_t[d] : dcode_t[256 + (d >> 7)])], 1u);
+            }
+        }
+        __syncthreads();
+        if (lane == 0) hist[END_BLOCK] += 1;                 // init_block's END_BLOCK count
+        __syncthreads();
+        for (int i = (int)lane; i < L_CODES; i += 64) ltree[i * 2] = (uint16_t)hist[i];
+        for (int i = (int)lane; i < D_CODES; i += 64) dtree[i * 2] = (uint16_t)hist[L_CODES + i];
+        __syncthreads();
+        if (lane == 0) {
+            LTreeCtx c{heap, depth, bl_count, next_code, bltree, 0, 0, 0, 0, hdr, 0};
+            const int l_max = build_tree(c, ltree, T->static_ltree, T->extra_lbits, 257, L_CODES, 15);
+            const int d_max = build_tree(c, dtree, T->static_dtree, T->extra_dbits, 0, D_CODES, 15);
+            scan_tree(c, ltree, l_max);
+            scan_tree(c, dtree, d_max);
+            build_tree(c, bltree, (const GLB uint16_t*)nullptr, T->extra_blbits, 0, BL_CODES, 7);
+            int max_blindex;
+            for (max_blindex = BL_CODES - 1; max_blindex >= 3; max_blindex--)
+                if (bltree[c_bl_order[max_blindex] * 2 + 1] != 0) break;
+            c.opt_len += 3 * (max_blindex + 1) + 5 + 5 + 4;
+            uint32_t opt_lenb = (uint32_t)(c.opt_len + 3 + 7) >> 3;
+            const uint32_t static_lenb = (uint32_t)(c.static_len + 3 + 7) >> 3;
+            if (static_lenb <= opt_lenb) opt_lenb = static_lenb;
+            const int stored_len = strstart - block_start;
+            uint32_t type, dbits = 0;
+            if ((uint32_t)(stored_len + 4) <= opt_lenb && block_start >= 0) {
+                type = 0;
+                c.bits(eof, 3);
+            } else {
+                const bool st = static_lenb == opt_lenb;
+                type = st ? 1 : 2;
+                if (st) c.bits(2u + eof, 3);
+                else {
+                    c.bits(4u + eof, 3);
+                    const int lcodes = l_max + 1, dcodes = d_max + 1, blcodes = max_blindex + 1;
+                    c.bits((uint32_t)(lcodes - 257), 5);
+                    c.bits((uint32_t)(dcodes - 1), 5);
+                    c.bits((uint32_t)(blcodes - 4), 4);
+                    for (int rank = 0; rank < blcodes; rank++) c.bits(bltree[c_bl_order[rank] * 2 + 1], 3);
+                    send_tree(c, ltree, lcodes - 1);
+                    send_tree(c, dtree, dcodes - 1);
+                }
+                for (int i = 0; i < L_CODES; ++i)
+                    if (hist[i]) dbits += hist[i] * (uint32_t)(st ? T->static_ltree[i * 2 + 1] : ltree[i * 2 + 1]);
+                for (int i = 0; i < 29; ++i) dbits += hist[257 + i] * c_extra_lbits[i];
+                for (int i = 0; i < D_CODES; ++i)
+                    if (hist[L_CODES + i])
+                        dbits += hist[L_CODES + i] * ((uint32_t)(st ? 5 : dtree[i * 2 + 1]) + c_extra_dbits[i]);
+            }
+            info[0] = type; info[1] = c.nb; info[2] = dbits; info[3] = (uint32_t)stored_len;
+        }
+        __syncthreads();
+        const uint32_t type = info[0], hbits = info[1];
+        GLB uint32_t* tab = (GLB uint32_t*)(S->pending + b * FB_TAB_BYTES);
+        if (type != 0)
+            for (int i = (int)lane; i < L_CODES + D_CODES; i += 64) {
+                uint32_t code, len;
+                if (i < L_CODES) {
+                    code = type == 2 ? ltree[i * 2] : T->static_ltree[i * 2];
+                    len = type == 2 ? ltree[i * 2 + 1] : T->static_ltree[i * 2 + 1];
+                } else {
+                    const int d = i - L_CODES;
+                    code = type == 2 ? dtree[d * 2] : T->static_dtree[d * 2];
+                    len = type == 2 ? dtree[d * 2 + 1] : T->static_dtree[d * 2 + 1];
+                }
+                tab[i] = (code & 0xffffu) | ((len & 0xffffu) << 16);
+            }
+        for (uint32_t i = lane; i < (hbits + 31) / 32; i += 64) tab[FB_HDR_OFF / 4 + i] = hdr[i];
+        if (lane == 0) {
+            F->blk[b].type = type; F->blk[b].hbits = hbits; F->blk[b].dbits = info[2]; F->blk[b].stored_len = info[3];
+        }
+        __syncthreads();
+    }
+}
+
+// k_dfl_encode: one workgroup per stream.  Thread 0 lays the blocks out (bit offsets; the
+// 16-bit pending units behind the overlay check; stored blocks' byte alignment), the group
+// zeroes the output slot, then for each block every thread packs a run of symbols at its
+// prefix-summed bit offset: whole words are stored, the partial words at run edges OR-ed.
+#define EN_THREADS 256
+__device__ __forceinline__ uint32_t en_exclusive_scan(uint32_t v, uint32_t* wsum) {
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
+    uint32_t x = v;
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(x, o);
+        if (lane >= (uint32_t)o) x += y;
+    }
+    if (lane == 63) wsum[wv] = x;
+    __syncthreads();
+    uint32_t base = 0;
+    for (uint32_t w = 0; w < wv; ++w) base += wsum[w];
+    __syncthreads();
+    return base + x - v;
+}
+__global__ __launch_bounds__(EN_THREADS) void k_dfl_encode(DeflateArgs A) {
+    __shared__ uint32_t codes[L_CODES + D_CODES];
+    __shared__ uint8_t lcode_t[256], dcode_t[512];
+    __shared__ uint16_t lbase[29], dbase[30];
+    __shared__ uint64_t bstart[FB_MAXB];
+    __shared__ uint32_t bcarry[FB_MAXB], wsum[EN_THREADS / 64];
+    __shared__ uint64_t sh_end;
+    __shared__ uint32_t sh_bad;
+    const uint32_t sid = blockIdx.x, tid = threadIdx.x;
+    if (sid >= A.n) return;
+    GLB DSlab* S = (GLB DSlab*)(A.state + (uint64_t)sid * SLAB_BYTES);
+    GLB FStream* F = (GLB FStream*)S->window;
+    if (F->flag) return;
+    const GLB DTables* T = (const GLB DTables*)&g_dt;
+    for (uint32_t i = tid; i < 256; i += EN_THREADS) lcode_t[i] = T->length_code[i];
+    for (uint32_t i = tid; i < 512; i += EN_THREADS) dcode_t[i] = T->dist_code[i];
+    if (tid < 29) lbase[tid] = T->base_length[tid];
+    if (tid < 30) dbase[tid] = T->base_dist[tid];
+    const uint32_t nblk = F->nblk;
+    const bool gzip = A.format == SDZ_DEFLATE_GZIP;
+    const uint32_t hdr_bytes = A.format == SDZ_DEFLATE_ZLIB ? 2 : gzip ? 10 + (A.fname_len ? A.fname_len + 1 : 0) : 0;
+    const uint32_t trl_bytes = A.format == SDZ_DEFLATE_ZLIB ? 4 : gzip ? 8 : 0;
+    const uint64_t in_len = A.in_len[sid];
+    if (tid == 0) {
+        uint64_t Tb = 8ull * hdr_bytes, al = Tb;             // bit position; last byte alignment
+        uint32_t bad = 0;
+        for (uint32_t b = 0; b < nblk; ++b) {
+            bstart[b] = Tb;
+            const uint32_t carry = (uint32_t)((Tb - al) & 15);  // bi_valid at the block's start
+            bcarry[b] = carry;
+            if (F->blk[b].type == 0) {
+                const uint32_t K = carry + 3, rem = K & 15;
+                const uint32_t pend = 2 * (K >> 4) + (rem > 8 ? 2 : rem > 0 ? 1 : 0) + 4;
+                if (pend + F->blk[b].stored_len > PENDING_SIZE) bad = 1;
+                Tb = ((Tb + 3 + 7) & ~7ull) + 32 + 8ull * F->blk[b].stored_len;
+                al = Tb;
+            } else {
+                Tb += F->blk[b].hbits + F->blk[b].dbits;
+            }
+            if (F->blk[b].eof) { Tb = (Tb + 7) & ~7ull; al = Tb; }
+        }
+        if (Tb / 8 + trl_bytes > A.out_cap[sid]) bad = 1;
+        sh_end = Tb;
+        sh_bad = bad;
+    }
+    __syncthreads();
+    if (sh_bad) { if (tid == 0) F->flag = 1; return; }
+    const uint64_t total = sh_end / 8 + trl_bytes;
+    GLB uint8_t* out = (GLB uint8_t*)(A.out + A.out_off[sid]);
+    {                                                        // zero the slot's bytes [0, total)
+        const uint64_t mis = (4 - ((uintptr_t)out & 3)) & 3, head = mis < total ? mis : total;
+        if (tid < head) out[tid] = 0;
+        const uint64_t nw = (total - head) / 4;
+        GLB uint32_t* w = (GLB uint32_t*)(out + head);
+        for (uint64_t i = tid; i < nw; i += EN_THREADS) w[i] = 0;
+        for (uint64_t i = head + 4 * nw + tid; i < total; i += EN_THREADS) out[i] = 0;
+    }
+    __threadfence();
+    __syncthreads();
+    GLB uint32_t* ow = (GLB uint32_t*)((uintptr_t)out & ~(uintptr_t)3);
+    const uint64_t bias = ((uintptr_t)out & 3) * 8;
+    auto orbits = [&](uint64_t bit, uint32_t v) {           // OR 32 bits of v at bit (slot-relative)
+        bit += bias;
+        const uint64_t w = bit >> 5;
+        const uint32_t sh = (uint32_t)(bit & 31);
+        if (v << sh) atomicOr((uint32_t*)&ow[w], v << sh);
+        if (sh && (v >> (32 - sh))) atomicOr((uint32_t*)&ow[w + 1], v >> (32 - sh));
+    };
+    if (tid == 0) {                                          // container header (sd-deflate.ts:98-152)
+        if (A.format == SDZ_DEFLATE_ZLIB) orbits(0, 0x0178u);
+        else if (gzip) {
+            orbits(0, 0x00088b1fu | ((A.fname_len ? 8u : 0u) << 24));
+            orbits(32, A.mtime);
+            orbits(64, 0xff00u);
+            for (uint32_t i = 0; i < A.fname_len; i++) orbits(80 + 8 * i, A.fname[i]);
+        }
+    }
+    const GLB uint32_t* sym = (const GLB uint32_t*)A.rec_buf + (uint64_t)sid * A.rec_stride * 2;
+    uint32_t bad = 0;
+    for (uint32_t b = 0; b < nblk; ++b) {
+        const uint32_t type = F->blk[b].type, hbits = F->blk[b].hbits;
+        const GLB uint32_t* tab = (const GLB uint32_t*)(S->pending + b * FB_TAB_BYTES);
+        const uint64_t b0 = bstart[b];
+        for (uint32_t i = tid; i < (hbits + 31) / 32; i += EN_THREADS) orbits(b0 + 32 * i, tab[FB_HDR_OFF / 4 + i]);
+        if (type == 0) {                                     // _tr_stored_block: aligned LEN NLEN bytes
+            const uint32_t len = F->blk[b].stored_len;
+            const uint64_t pay = ((b0 + 3 + 7) & ~7ull) / 8;
+            const GLB uint8_t* src = (const GLB uint8_t*)(A.in + A.in_off[sid]) + F->blk[b].off + F->blk[b].block_start;
+            for (uint32_t i = tid; i < 4 + len; i += EN_THREADS) {
+                uint8_t v;
+                if (i < 4) v = (uint8_t)((i < 2 ? len : ~len) >> (8 * (i & 1)));
+                else v = src[i - 4];
+                out[pay + i] = v;
+            }
+            __syncthreads();
+            continue;
+        }
+        for (uint32_t i = tid; i < L_CODES + D_CODES; i += EN_THREADS) codes[i] = tab[i];
+        __syncthreads();
+        const uint32_t sym0 = F->blk[b].sym0, nsym = F->blk[b].nsym, items = nsym + 1;   // + END_BLOCK
+        const uint32_t per = (items + EN_THREADS - 1) / EN_THREADS;
+        const uint32_t t0 = tid * per < items ? tid * per : items, t1 = t0 + per < items ? t0 + per : items;
+        auto sym_bits = [&](uint32_t j, uint32_t& lo, uint32_t& nlo, uint32_t& hi, uint32_t& nhi) {
+            if (j == nsym) { const uint32_t c = codes[END_BLOCK]; lo = c & 0xffffu; nlo = c >> 16; nhi = 0; hi = 0; return; }
+            const uint32_t s = sym[sym0 + j], lc = s & 255u, dist = s >> 8;
+            if (dist == 0) { const uint32_t c = codes[lc]; lo = c & 0xffffu; nlo = c >> 16; nhi = 0; hi = 0; return; }
+            const uint32_t lcode = lcode_t[lc], c = codes[257 + lcode], cl = c >> 16, xl = c_extra_lbits[lcode];
+            lo = (c & 0xffffu) | (xl ? (lc - lbase[lcode]) << cl : 0u);   // code 28 (258): no extra bits
+            nlo = cl + xl;
+            const uint32_t d = dist - 1, dc = d < 256 ? dcode_t[d] : dcode_t[256 + (d >> 7)];
+            const uint32_t e = codes[L_CODES + dc], el = e >> 16;
+            hi = (e & 0xffffu) | ((d - dbase[dc]) << el);
+            nhi = el + c_extra_dbits[dc];
+        };
+        uint32_t mybits = 0;
+        for (uint32_t j = t0; j < t1; ++j) {
+            uint32_t lo, nlo, hi, nhi;
+            sym_bits(j, lo, nlo, hi, nhi);
+            mybits += nlo + nhi;
+        }
+        const uint32_t excl = en_exclusive_scan(mybits, wsum);
+        if (t0 < t1) {
+            const uint32_t carry = bcarry[b];
+            uint64_t bit = b0 + hbits + excl;                // slot-relative start of symbol j
+            const uint64_t ab = bit + bias;
+            uint64_t wpos = ab >> 5;
+            uint32_t nacc = (uint32_t)(ab & 31);
+            uint64_t acc = 0;
+            bool first = nacc != 0;
+            auto put = [&](uint32_t v, uint32_t len) {
+                acc |= (uint64_t)v << nacc;
+                nacc += len;
+                if (nacc >= 32) {
+                    if (first) atomicOr((uint32_t*)&ow[wpos], (uint32_t)acc);
+                    else ow[wpos] = (uint32_t)acc;
+                    first = false;
+                    wpos++;
+                    acc >>= 32;
+                    nacc -= 32;
+                }
+            };
+            for (uint32_t j = t0; j < t1; ++j) {
+                // pending_buf bytes written before symbol j is read (SURVEY A7 overlay)
+                const uint64_t pend = 2 * ((carry + (bit - b0)) >> 4);
+                if (j < nsym && pend > (uint64_t)D_BUF + 2 * j) bad = 1;
+                uint32_t lo, nlo, hi, nhi;
+                sym_bits(j, lo, nlo, hi, nhi);
+                put(lo, nlo);
+                if (nhi) put(hi, nhi);
+                bit += nlo + nhi;
+            }
+            if (nacc) atomicOr((uint32_t*)&ow[wpos], (uint32_t)acc);
+        }
+        __syncthreads();
+    }
+    if (bad) atomicOr(&sh_bad, 1u);
+    __syncthreads();
+    if (tid == 0) {
+        if (sh_bad) { F->flag = 1; return; }
+        const uint32_t cks = (uint32_t)A.cks[sid];
+        const uint64_t e = sh_end;
+        if (A.format == SDZ_DEFLATE_ZLIB)
+            orbits(e, ((cks >> 24) & 0xff) | ((cks >> 8) & 0xff00) | ((cks << 8) & 0xff0000) | (cks << 24));
+        else if (gzip) { orbits(e, cks); orbits(e + 32, (uint32_t)in_len); }
+        sdz_deflate_record R;
+        R.status = SDZ_OK; R.checksum = (int32_t)cks; R.out_len = total; R.reserved = 0;
+        A.rec[sid] = R;
+    }
+}
+
 __global__ void k_max_u64(const uint64_t* v, uint32_t n, unsigned long long* out) {
     unsigned long long m = 0;
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
@@ -1078,6 +1508,15 @@ void launch_deflate(const DeflateArgs& a, hipStream_t st) {
         const uint32_t nseg = (a.rec_stride + PM_SEG - 1) / PM_SEG;
         hipLaunchKernelGGL(k_dfl_chain, dim3(a.n), dim3(64), 0, st, a);
         hipLaunchKernelGGL(k_dfl_match, dim3(a.n * nseg), dim3(PM_THREADS), 0, st, a, nseg);
+        hipLaunchKernelGGL(k_dfl_tail, dim3(a.n), dim3(256), 0, st, a);
+        hipLaunchKernelGGL(k_dfl_parse, grid, dim3(64), 0, st, a);
+        hipLaunchKernelGGL(k_dfl_trees, dim3(a.n), dim3(64), 0, st, a);
+        launch_checksum(a.in, a.in_off, a.in_len, nullptr, a.cks, a.n, a.format == SDZ_DEFLATE_GZIP ? 1 : 0, st);
+        hipLaunchKernelGGL(k_dfl_encode, dim3(a.n), dim3(EN_THREADS), 0, st, a);
+        DeflateArgs f = a;
+        f.fast = 1;                                          // streams the record path handed back
+        hipLaunchKernelGGL(k_deflate, grid, dim3(DF_THREADS), 0, st, f);
+        return;
     }
     hipLaunchKernelGGL(k_deflate, grid, dim3(DF_THREADS), 0, st, a);
 }

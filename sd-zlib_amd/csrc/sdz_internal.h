@@ -65,6 +65,9 @@ struct DeflateArgs {
     uint64_t* rec_buf;           // n * rec_stride match records (null: classic path only)
     uint16_t* pv_buf;            // n * rec_stride hash chain links
     uint32_t rec_stride;
+    int32_t* cks;                // n input checksums (record path)
+    uint32_t fast;               // set by launch_deflate: k_deflate redoes flagged streams only
+    unsigned long long* dbg;     // phase cycle counters (SDZ_PHASE_TIMING), normally null
 };
 
 uint64_t deflate_state_bytes();

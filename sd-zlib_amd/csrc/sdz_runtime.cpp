@@ -312,7 +312,7 @@ int sdz_deflate_batch_device(const uint8_t* in, const uint64_t* in_off, const ui
         if (device_max_u64(in_len, n, &mx, s)) return hip_fail(hipGetLastError(), "deflate: input sizes");
         if (mx <= kDeflateRecMax) stride = (uint32_t)std::max<uint64_t>(64, (mx + 63) & ~63ull);
     }
-    const uint64_t per_stream = slab + (uint64_t)stride * (sizeof(uint64_t) + sizeof(uint16_t));
+    const uint64_t per_stream = slab + (uint64_t)stride * (sizeof(uint64_t) + sizeof(uint16_t)) + sizeof(int32_t);
     const uint32_t kMaxSlabs = (uint32_t)std::max<uint64_t>(1024, std::min<uint64_t>(65536, mem_free / 2 / per_stream));
     uint32_t chunk = std::min(n, kMaxSlabs);
     void* state = nullptr;
@@ -324,9 +324,16 @@ int sdz_deflate_batch_device(const uint8_t* in, const uint64_t* in_off, const ui
         d_fname = (uint8_t*)tmp;
         HIPCHK(hipMemcpyAsync(d_fname, fname, fname_len, hipMemcpyHostToDevice, s));
     }
+    unsigned long long* dbg = nullptr;
+    const bool phases = getenv("SDZ_PHASE_TIMING") != nullptr;   // development aid
+    if (phases) {
+        HIPCHK(hipMalloc(&dbg, 64 * sizeof(unsigned long long)));
+        HIPCHK(hipMemsetAsync(dbg, 0, 64 * sizeof(unsigned long long), s));
+    }
     timing_begin(s);
     for (uint32_t b = 0; b < n; b += chunk) {
         DeflateArgs a;
+        a.dbg = dbg;
         uint32_t m = std::min(chunk, n - b);
         a.in = in; a.in_off = in_off + b; a.in_len = in_len + b;
         a.out = out; a.out_off = out_off + b; a.out_cap = out_cap + b;
@@ -334,11 +341,22 @@ int sdz_deflate_batch_device(const uint8_t* in, const uint64_t* in_off, const ui
         a.rec_stride = stride;
         a.rec_buf = stride ? (uint64_t*)((uint8_t*)state + (size_t)chunk * slab) : nullptr;
         a.pv_buf = stride ? (uint16_t*)((uint8_t*)a.rec_buf + (size_t)chunk * stride * sizeof(uint64_t)) : nullptr;
+        a.cks = stride ? (int32_t*)((uint8_t*)a.pv_buf + (size_t)chunk * stride * sizeof(uint16_t)) : nullptr;
+        a.fast = 0;
         a.fname = d_fname; a.fname_len = fname_len; a.mtime = mtime;
         a.n = m; a.level = level; a.format = format;
         launch_deflate(a, s);
     }
     timing_end(s);
+    if (phases) {
+        unsigned long long h[64];
+        HIPCHK(hipMemcpyAsync(h, dbg, sizeof h, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        fprintf(stderr, "sdz deflate phases:");
+        for (int k = 0; k < 8; ++k) fprintf(stderr, " %llu", h[k]);
+        fprintf(stderr, "\n");
+        hipFree(dbg);
+    }
     HIPCHK(hipGetLastError());
     if (fname_len) HIPCHK(hipStreamSynchronize(s));   // tmp pool is reused
     return SDZ_API_OK;

@@ -175,12 +175,14 @@ def inflate_one(data, fmt=FMT_AUTO, dictionary=None):
         cap *= 4
 
 
-def deflate_batch(streams, level=6, format="deflate", file_name_latin1=b"", mtime=0):
+def deflate_batch(streams, level=6, format="deflate", file_name_latin1=b"", mtime=0, out_caps=None):
     L = lib()
     n = len(streams)
     streams = [bytes(s) for s in streams]
     fmt = DEFLATE_FORMATS[format]
     caps_l = [int(L.sdz_deflate_bound(len(s), fmt, len(file_name_latin1))) for s in streams]
+    if out_caps is not None:                       # explicit output slot sizes (overflow tests)
+        caps_l = [max(1, int(c)) for c in out_caps]
     ins = (ctypes.c_char_p * n)(*streams)
     in_len = (ctypes.c_size_t * n)(*[len(s) for s in streams])
     bufs = [ctypes.create_string_buffer(c) for c in caps_l]

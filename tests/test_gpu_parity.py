@@ -316,6 +316,46 @@ def test_deflate_full_paradiselost_sizes(paradise):
         assert len(g["data"]) == size
 
 
+def _overlay_stress(rng, n):
+    """Random bytes, then 4-byte copies from 16-30 KiB back: ~25 bits per 4-byte match, so
+    the block's output overtakes its d_buf/l_buf overlay inside one block."""
+    out = bytearray(rng.getrandbits(8) for _ in range(32768))
+    while len(out) < n:
+        src = rng.randrange(len(out) - 30000, len(out) - 16000)
+        out += out[src:src + 4]
+    return bytes(out[:n])
+
+
+def test_deflate_record_path_bitexact(paradise):
+    """Every input <= 64 KiB, so levels 4-9 run the record path (k_dfl_* kernels): tail
+    searches, the window slide at 65274, stored / static / dynamic blocks, TRUNCATE_BLOCK,
+    and the overlay-overtaken streams handed back to the serial kernel."""
+    rng = random.Random(11)
+    sizes = [1, 2, 3, 4, 5, 257, 258, 259, 261, 262, 263, 264, 5552, 32767, 32768, 32769,
+             65273, 65274, 65275, 65535, 65536]
+    inputs = [text_corpus(rng, n) for n in sizes]
+    inputs += [paradise[i * 65536:(i + 1) * 65536] for i in range(3)]
+    inputs += [binary_corpus(rng, 65536), bytes(rng.getrandbits(8) for _ in range(65536)),
+               b"a" * 65536, _periodic(rng, 65536), _overlay_stress(rng, 65536), bytes(65536),
+               _periodic(rng, 40000) + bytes(rng.getrandbits(8) for _ in range(25536))]
+    for level in range(4, 10):
+        for fmt in ("deflate", "gzip", "raw"):
+            gpu = sdz.deflate_batch(inputs, level=level, format=fmt, file_name_latin1=b"x.txt", mtime=77)
+            for g, d in zip(gpu, inputs):
+                exp = O.deflate(d, level=level, format=fmt, file_name="x.txt", mtime=77)
+                assert g["status"] == "OK" and g["data"] == exp, (level, fmt, len(d))
+
+
+def test_deflate_record_path_output_overflow(paradise):
+    """An output slot one byte short is an overflow; an exact one is not."""
+    inputs = [paradise[:65536], paradise[65536:100000]]
+    exp = [O.deflate(d, level=6) for d in inputs]
+    short = sdz.deflate_batch(inputs, level=6, out_caps=[len(e) - 1 for e in exp])
+    assert all(g["status"] != "OK" for g in short)
+    exact = sdz.deflate_batch(inputs, level=6, out_caps=[len(e) for e in exp])
+    assert [g["data"] for g in exact] == exp and all(g["status"] == "OK" for g in exact)
+
+
 def test_deflate_empty_input_is_an_error():
     g = sdz.deflate_batch([b""])[0]
     assert g["status"] != "OK"
