@@ -837,12 +837,30 @@ __global__ __launch_bounds__(DF_THREADS) void k_deflate(DeflateArgs A) {
 
 // ------------------------------------------------------------------ record path kernels
 
-// k_dfl_chain: one wave per stream walks its positions in order, 64 at a time; each lane
-// swaps its position into the LDS head table.  Same-address lanes of one ds_wrxchg are
-// served in lane order (tools/ubench/lds_xchg_order.hip), so a lane receives the position
-// of the previous lane with the same hash, or the head: exactly insert_string's sequence.
+// k_dfl_chain: one wave per stream walks its positions in order, 1024 at a time: each lane
+// hashes 16 consecutive positions from registers (the next chunk's bytes are already in
+// flight) into LDS, then 16 rounds of 64 positions swap themselves into the LDS head table.
+// Same-address lanes of one ds_wrxchg are served in lane order (tools/ubench/
+// lds_xchg_order.hip), so a lane receives the position of the previous lane with the same
+// hash, or the head: exactly insert_string's sequence.
+#define CH_CHUNK 1024
+__device__ __forceinline__ void ch_load(const GLB uint8_t* in, uint32_t n, uint32_t at, uint32_t (&w)[5]) {
+    if (at + 20 <= n) {
+        for (int i = 0; i < 5; ++i) __builtin_memcpy(&w[i], (const uint8_t*)(in + at + 4 * i), 4);
+    } else {
+        for (int i = 0; i < 5; ++i) {
+            uint32_t v = 0;
+            for (int b = 0; b < 4; ++b) {
+                const uint32_t q = at + 4 * i + b;
+                v |= (q < n ? (uint32_t)in[q] : 0u) << (8 * b);
+            }
+            w[i] = v;
+        }
+    }
+}
 __global__ __launch_bounds__(64) void k_dfl_chain(DeflateArgs A) {
     __shared__ uint32_t head[HASH_SIZE];                 // 128 KiB
+    __shared__ uint16_t hs[CH_CHUNK];
     const uint32_t sid = blockIdx.x, lane = threadIdx.x;
     if (sid >= A.n) return;
     const uint64_t in_len = A.in_len[sid];
@@ -851,15 +869,32 @@ __global__ __launch_bounds__(64) void k_dfl_chain(DeflateArgs A) {
     GLB uint16_t* pv = (GLB uint16_t*)A.pv_buf + (uint64_t)sid * A.rec_stride;
     for (uint32_t i = lane; i < HASH_SIZE; i += 64) head[i] = 0;
     const uint32_t n = (uint32_t)in_len;
-    // rolling bytes: b0 b1 b2 of position p are in[p], in[p+1], in[p+2]
-    for (uint32_t base = 0; base < n; base += 64) {
-        const uint32_t p = base + lane;
-        const bool ins = p + 2 < n;                      // insert_string runs while lookahead >= 3
-        uint32_t h = 0;
-        if (ins) h = (((uint32_t)in[p] << 10) ^ ((uint32_t)in[p + 1] << 5) ^ in[p + 2]) & HASH_MASK;
-        uint32_t old = 0;
-        if (ins) old = atomicExch(&head[h], p);
-        if (p < n) pv[p] = (uint16_t)old;
+    uint32_t w[5];
+    ch_load(in, n, 16 * lane, w);
+    for (uint32_t base = 0; base < n; base += CH_CHUNK) {
+        uint32_t wn[5];
+        if (base + CH_CHUNK < n) ch_load(in, n, base + CH_CHUNK + 16 * lane, wn);
+        for (int q = 0; q < 16; q += 2) {                // hashes of positions base + 16 lane + q
+            uint32_t h2 = 0;
+            for (int r = 0; r < 2; ++r) {
+                const int o = q + r;
+                const uint32_t b0 = (w[o >> 2] >> (8 * (o & 3))) & 255u;
+                const uint32_t b1 = (w[(o + 1) >> 2] >> (8 * ((o + 1) & 3))) & 255u;
+                const uint32_t b2 = (w[(o + 2) >> 2] >> (8 * ((o + 2) & 3))) & 255u;
+                h2 |= (((b0 << 10) ^ (b1 << 5) ^ b2) & HASH_MASK) << (16 * r);
+            }
+            *(uint32_t*)&hs[16 * lane + q] = h2;
+        }
+        __syncthreads();
+        for (uint32_t j = 0; j < CH_CHUNK / 64; ++j) {
+            const uint32_t p = base + 64 * j + lane;
+            if (p >= n) break;
+            uint32_t old = 0;
+            if (p + 2 < n) old = atomicExch(&head[hs[64 * j + lane]], p);   // insert_string runs while lookahead >= 3
+            pv[p] = (uint16_t)old;
+        }
+        __syncthreads();
+        for (int i = 0; i < 5; ++i) w[i] = wn[i];
     }
 }
 
@@ -916,7 +951,9 @@ __global__ __launch_bounds__(PM_THREADS) void k_dfl_match(DeflateArgs A, uint32_
     const int q0 = s0 + (int)wv * per, q1 = q0 + per < s1 ? q0 + per : s1;
     int next = q0;                                          // wave-uniform queue head
     bool act = false;
-    int p = s0, cur = 0, best = 0, bpos = 0, qbest = 0, qpos = 0, k = 0, chain = 0, limit = 0;
+    // cur: this step's candidate; nxt: the link after it (read a step ahead, so the chain
+    // link of a step does not wait on the previous one)
+    int p = s0, cur = 0, nxt = 0, best = 0, bpos = 0, qbest = 0, qpos = 0, k = 0, chain = 0, limit = 0;
     uint32_t sb = 0, s4 = 0;
     for (;;) {
         // idle lanes take the next positions
@@ -929,21 +966,25 @@ __global__ __launch_bounds__(PM_THREADS) void k_dfl_match(DeflateArgs A, uint32_
             if (take) {
                 p = pn;
                 act = true;
-                cur = pvl[p - ws];                              // hash_head
+                const uint32_t sp = (uint32_t)(p - ws);
+                cur = pvl[sp];                                  // hash_head
                 best = MIN_MATCH - 1; bpos = 0; qbest = -1; k = 0; chain = max_chain;
                 limit = p > MAX_DIST ? p - MAX_DIST : 0;
-                const uint32_t sp = (uint32_t)(p - ws);
                 s4 = pm_w4(win, sp);
                 sb = win[sp + best];
                 if (cur == 0 || p - cur > MAX_DIST) chain = 0;  // no search (deflate.ts:1092)
+                nxt = pvl[(uint32_t)((chain ? cur : p) - ws)];
             }
         }
         if (!__ballot(act)) break;
         // one candidate per active lane, branch-free but for the rare long compare
         const bool live = act && chain > 0;
+        const bool goes_on = nxt > limit && chain - 1 != 0;  // the walk continues after cur
         const uint32_t cp = (uint32_t)((live ? cur : p) - ws), sp = (uint32_t)(p - ws);
-        const bool cand = live && win[cp + best] == sb;      // can beat best (deflate.ts:866-882)
+        const uint32_t wb = win[cp + best];
         uint32_t x = pm_w4(win, cp) ^ s4;
+        const int nn = pvl[(uint32_t)((live && goes_on ? nxt : p) - ws)];
+        const bool cand = live && wb == sb;                  // can beat best (deflate.ts:866-882)
         int len = x ? (int)(__builtin_ctz(x) >> 3) : 4;
         bool more = cand && x == 0;
         if (__ballot(more)) {                                // matches of more than 4 bytes
@@ -958,14 +999,14 @@ __global__ __launch_bounds__(PM_THREADS) void k_dfl_match(DeflateArgs A, uint32_
         best = upd ? len : best;
         bpos = upd ? cur : bpos;
         bool fin = upd && len >= nice;
-        sb = win[sp + (best < MAX_MATCH ? best : MAX_MATCH)];
+        if (__ballot(upd)) sb = win[sp + (best < MAX_MATCH ? best : MAX_MATCH)];
         k += live ? 1 : 0;
         const bool cap = live && k == qchain;
         qbest = cap ? best : qbest;
         qpos = cap ? bpos : qpos;
-        const int ncur = pvl[(uint32_t)((live ? cur : p) - ws)];
-        fin = act && (fin || !live || !(ncur > limit && chain - 1 != 0));
-        cur = ncur;
+        fin = act && (fin || !live || !goes_on);
+        cur = nxt;
+        nxt = nn;
         chain -= 1;
         if (fin) {
             if (qbest < 0) { qbest = best; qpos = bpos; }
