@@ -1335,7 +1335,8 @@ __global__ __launch_bounds__(64) void k_dfl_trees(DeflateArgs A) {
 // zeroes the output slot, then for each block every thread packs a run of symbols at its
 // prefix-summed bit offset: whole words are stored, the partial words at run edges OR-ed.
 #define EN_THREADS 256
-__device__ __forceinline__ uint32_t en_exclusive_scan(uint32_t v, uint32_t* wsum) {
+#define EN_STG_WORDS (EN_THREADS * 48 / 32 + 2)        // one row's bits (<= 48 per symbol)
+__device__ __forceinline__ uint32_t en_scan(uint32_t v, uint32_t* wsum, uint32_t& total) {
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
     uint32_t x = v;
     for (int o = 1; o < 64; o <<= 1) {
@@ -1344,9 +1345,10 @@ __device__ __forceinline__ uint32_t en_exclusive_scan(uint32_t v, uint32_t* wsum
     }
     if (lane == 63) wsum[wv] = x;
     __syncthreads();
-    uint32_t base = 0;
-    for (uint32_t w = 0; w < wv; ++w) base += wsum[w];
+    uint32_t base = 0, all = 0;
+    for (uint32_t w = 0; w < EN_THREADS / 64; ++w) { base += w < wv ? wsum[w] : 0u; all += wsum[w]; }
     __syncthreads();
+    total = all;
     return base + x - v;
 }
 __global__ __launch_bounds__(EN_THREADS) void k_dfl_encode(DeflateArgs A) {
@@ -1355,6 +1357,7 @@ __global__ __launch_bounds__(EN_THREADS) void k_dfl_encode(DeflateArgs A) {
     __shared__ uint16_t lbase[29], dbase[30];
     __shared__ uint64_t bstart[FB_MAXB];
     __shared__ uint32_t bcarry[FB_MAXB], wsum[EN_THREADS / 64];
+    __shared__ uint32_t stg[EN_STG_WORDS];
     __shared__ uint64_t sh_end;
     __shared__ uint32_t sh_bad;
     const uint32_t sid = blockIdx.x, tid = threadIdx.x;
@@ -1449,8 +1452,6 @@ __global__ __launch_bounds__(EN_THREADS) void k_dfl_encode(DeflateArgs A) {
         for (uint32_t i = tid; i < L_CODES + D_CODES; i += EN_THREADS) codes[i] = tab[i];
         __syncthreads();
         const uint32_t sym0 = F->blk[b].sym0, nsym = F->blk[b].nsym, items = nsym + 1;   // + END_BLOCK
-        const uint32_t per = (items + EN_THREADS - 1) / EN_THREADS;
-        const uint32_t t0 = tid * per < items ? tid * per : items, t1 = t0 + per < items ? t0 + per : items;
         auto sym_bits = [&](uint32_t j, uint32_t& lo, uint32_t& nlo, uint32_t& hi, uint32_t& nhi) {
             if (j == nsym) { const uint32_t c = codes[END_BLOCK]; lo = c & 0xffffu; nlo = c >> 16; nhi = 0; hi = 0; return; }
             const uint32_t s = sym[sym0 + j], lc = s & 255u, dist = s >> 8;
@@ -1463,46 +1464,44 @@ __global__ __launch_bounds__(EN_THREADS) void k_dfl_encode(DeflateArgs A) {
             hi = (e & 0xffffu) | ((d - dbase[dc]) << el);
             nhi = el + c_extra_dbits[dc];
         };
-        uint32_t mybits = 0;
-        for (uint32_t j = t0; j < t1; ++j) {
-            uint32_t lo, nlo, hi, nhi;
-            sym_bits(j, lo, nlo, hi, nhi);
-            mybits += nlo + nhi;
-        }
-        const uint32_t excl = en_exclusive_scan(mybits, wsum);
-        if (t0 < t1) {
-            const uint32_t carry = bcarry[b];
-            uint64_t bit = b0 + hbits + excl;                // slot-relative start of symbol j
-            const uint64_t ab = bit + bias;
-            uint64_t wpos = ab >> 5;
-            uint32_t nacc = (uint32_t)(ab & 31);
-            uint64_t acc = 0;
-            bool first = nacc != 0;
-            auto put = [&](uint32_t v, uint32_t len) {
-                acc |= (uint64_t)v << nacc;
-                nacc += len;
-                if (nacc >= 32) {
-                    if (first) atomicOr((uint32_t*)&ow[wpos], (uint32_t)acc);
-                    else ow[wpos] = (uint32_t)acc;
-                    first = false;
-                    wpos++;
-                    acc >>= 32;
-                    nacc -= 32;
-                }
-            };
-            for (uint32_t j = t0; j < t1; ++j) {
-                // pending_buf bytes written before symbol j is read (SURVEY A7 overlay)
-                const uint64_t pend = 2 * ((carry + (bit - b0)) >> 4);
-                if (j < nsym && pend > (uint64_t)D_BUF + 2 * j) bad = 1;
-                uint32_t lo, nlo, hi, nhi;
-                sym_bits(j, lo, nlo, hi, nhi);
-                put(lo, nlo);
-                if (nhi) put(hi, nhi);
-                bit += nlo + nhi;
+        // rows of EN_THREADS symbols (coalesced reads): scan the bit counts, OR each symbol's
+        // bits into an LDS image of the row, write the image out (edge words OR-ed)
+        const uint32_t carry = bcarry[b];
+        uint64_t rowbit = b0 + hbits;                        // slot-relative bit of the row's start
+        for (uint32_t r0 = 0; r0 < items; r0 += EN_THREADS) {
+            const uint32_t j = r0 + tid;
+            uint32_t lo = 0, nlo = 0, hi = 0, nhi = 0;
+            if (j < items) sym_bits(j, lo, nlo, hi, nhi);
+            uint32_t tot;
+            const uint32_t excl = en_scan(nlo + nhi, wsum, tot);
+            // pending_buf bytes written before symbol j is read (SURVEY A7 overlay)
+            const uint64_t pend = 2 * ((carry + (rowbit + excl - b0)) >> 4);
+            if (j < nsym && pend > (uint64_t)D_BUF + 2 * j) bad = 1;
+            const uint64_t a0 = rowbit + bias, wbase = a0 >> 5;
+            const uint32_t nw = (uint32_t)(((a0 + tot + 31) >> 5) - wbase);
+            for (uint32_t i = tid; i < nw; i += EN_THREADS) stg[i] = 0;
+            __syncthreads();
+            const uint32_t at = (uint32_t)(a0 - wbase * 32) + excl;
+            if (nlo) {
+                const uint32_t w = at >> 5, sh = at & 31;
+                atomicOr(&stg[w], lo << sh);
+                if (sh + nlo > 32) atomicOr(&stg[w + 1], lo >> (32 - sh));
             }
-            if (nacc) atomicOr((uint32_t*)&ow[wpos], (uint32_t)acc);
+            if (nhi) {
+                const uint32_t a2 = at + nlo, w = a2 >> 5, sh = a2 & 31;
+                atomicOr(&stg[w], hi << sh);
+                if (sh + nhi > 32) atomicOr(&stg[w + 1], hi >> (32 - sh));
+            }
+            __syncthreads();
+            for (uint32_t i = tid; i < nw; i += EN_THREADS) {
+                const uint32_t v = stg[i];
+                const bool edge = (i == 0 && (a0 & 31)) || (i == nw - 1 && ((a0 + tot) & 31));
+                if (!edge) ow[wbase + i] = v;
+                else if (v) atomicOr((uint32_t*)&ow[wbase + i], v);
+            }
+            __syncthreads();
+            rowbit += tot;
         }
-        __syncthreads();
     }
     if (bad) atomicOr(&sh_bad, 1u);
     __syncthreads();
