@@ -390,7 +390,8 @@ __global__ __launch_bounds__(RS_THREADS) __attribute__((amdgpu_waves_per_eu(8, 8
 
     // adler32 as sums over the whole output: s1 = 1 + S, s2 = n + n S - T (mod 65521),
     // S = sum b_i, T = sum i b_i -- per-lane partials, combined once per round
-    uint32_t accS = 0, accT = 0;                          // accT kept reduced mod 65521 per group
+    uint32_t accS = 0;
+    uint64_t accT = 0;                                    // < 2^47 per lane and round: reduced once at the end
 #ifdef SDZ_TIMING
     const bool timed = A.dbg && sid < 8 && lane == 0;
 #else
@@ -496,7 +497,7 @@ __global__ __launch_bounds__(RS_THREADS) __attribute__((amdgpu_waves_per_eu(8, 8
                     gi -= gi >= 65521u ? 65521u : 0u;
                     const uint32_t s4 = __builtin_amdgcn_udot4(vm, 0x01010101u, 0u, false);
                     accS += s4;
-                    accT = (accT + gi * s4 + __builtin_amdgcn_udot4(vm, 0x03020100u, 0u, false)) % 65521u;
+                    accT += (uint64_t)gi * s4 + __builtin_amdgcn_udot4(vm, 0x03020100u, 0u, false);
                 }
             }
         }
