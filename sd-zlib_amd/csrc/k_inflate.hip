@@ -45,7 +45,9 @@ __constant__ uint8_t c_border[19] = { 16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 1
 
 #if defined(__HIP_DEVICE_COMPILE__)
 typedef __attribute__((address_space(1))) const uint4 g_uint4;   // global_load, not flat_load
+#define GLB __attribute__((address_space(1)))
 #else
+#define GLB
 typedef const uint4 g_uint4;
 #endif
 
@@ -371,14 +373,17 @@ __device__ __forceinline__ void with_dummies(const Tree& T, uint32_t (&c)[5]) {
 
 // token: bit31=0 -> literals: bits 24-25 = count-1 (1..3 bytes in bits 0-23)
 //        bit31=1 -> match: bits 16-23 = length-3, bits 0-14 = distance-1
-__device__ __forceinline__ void tok_flush_stage(Core& L) {       // 32 staged tokens -> HBM
+// 32 staged tokens -> HBM.  Some lane of the wave fills its stage at most steps (64 lanes,
+// one flush per 32 tokens each), so this block runs nearly every step: all LDS reads are
+// issued before the first store (one wait, not one per 16 bytes).
+__device__ __forceinline__ void tok_flush_stage(Core& L) {
     const uint2* s = (const uint2*)L.ts;
-    uint4* d = (uint4*)(L.tb + (L.ntok - IL_TSTAGE));
+    GLB uint4* d = (GLB uint4*)(L.tb + (L.ntok - IL_TSTAGE));
+    uint2 v[IL_TSTAGE / 2];
 #pragma unroll
-    for (int k = 0; k < IL_TSTAGE / 4; ++k) {
-        uint2 a = s[2 * k], b = s[2 * k + 1];
-        d[k] = make_uint4(a.x, a.y, b.x, b.y);
-    }
+    for (int k = 0; k < IL_TSTAGE / 2; ++k) v[k] = s[k];
+#pragma unroll
+    for (int k = 0; k < IL_TSTAGE / 4; ++k) d[k] = make_uint4(v[2 * k].x, v[2 * k].y, v[2 * k + 1].x, v[2 * k + 1].y);
 }
 __device__ __forceinline__ void tok_push(Core& L, uint32_t t) {
     uint32_t k = L.ntok & (IL_TSTAGE - 1);
