@@ -27,7 +27,9 @@
 
 namespace sdz {
 
+#ifndef RS_WAVES
 #define RS_WAVES 8
+#endif
 #define RS_THREADS (64 * RS_WAVES)
 #define RS_WIN 32768
 #define RS_R 36352                    // ring bytes: 32 KiB window + bytes in flight
@@ -247,12 +249,13 @@ __device__ __forceinline__ void lds_mskor_at(uint32_t* base32, uint32_t i, uint3
 // tools/ubench/emit.hip): every token is written as dwords v_j = alignbyte(x[j+1], x[j], k)
 // masked to its bytes -- a copy's x are its source dwords (aligned reads, all issued before
 // the writes), a literal's are its 1-3 bytes placed so that the same formula lands them at
-// d, a period's (dist 1-3) its repeating pattern words (k = 0) -- RS_MW dwords per step
-// (tokens up to 4 RS_MW - 3 bytes take one step), then the same masks on the finality map
-// (map index = ring index mod 4).  Masked writes outside a token are no-ops.  Copies that
-// overlap themselves with dist >= 4, and tokens across the ring's or map's end, go through
-// emit_tokens.
+// d -- RS_MW dwords per step (tokens up to 4 RS_MW - 3 bytes take one step), each followed
+// by the same mask on the finality map (map index = ring index mod 4).  Masked writes
+// outside a token are no-ops.  Copies that overlap themselves (periods included), and
+// tokens across the ring's or map's end, go through emit_tokens.
+#ifndef RS_MW
 #define RS_MW 4
+#endif
 __device__ __forceinline__ void emit_msk(uint8_t* ring, uint8_t* fmap, bool act, uint32_t t, uint32_t d,
                                          uint32_t s, uint32_t len, uint32_t dist, uint32_t mp, uint32_t lb) {
     uint32_t* ring32 = (uint32_t*)ring;
@@ -260,29 +263,22 @@ __device__ __forceinline__ void emit_msk(uint8_t* ring, uint8_t* fmap, bool act,
     const uint32_t dumi = RS_R / 4 + (threadIdx.x & 31u);   // reads run RS_MW dwords on
     const bool lit = (t >> 31) == 0;
     const bool slow = act && (d + len > RS_R || (!lit && (s + len > RS_R || s < 4u)) || mp + len > RS_BM);
-    const bool ov = act && !lit && dist >= 4u && dist < len;
-    const bool one = act && !slow && !ov;
-    if (__ballot(act && !one)) emit_tokens(ring, fmap, act && !one, t, d, s, len, dist, mp, lb);
-    const bool per = !lit && dist < 4u;
+    const bool gen = act && (slow || (!lit && dist < len));  // periods and self-overlapping copies too
+    if (__ballot(gen)) emit_tokens(ring, fmap, gen, t, d, s, len, dist, mp, lb);
+    const bool one = act && !gen;
     const uint32_t kd = d & 3u, D0 = d >> 2, M0 = mp >> 2;
     const uint32_t sx = s - kd, k = sx & 3u;
     const uint32_t xa = one && !lit ? sx >> 2 : dumi;
     const uint32_t e = one ? kd + len : 0u;               // token end, in bytes from dword D0
     const uint32_t lw = lb * 0x01010101u;
+    // a literal: x0 = t (kd = 0), or x0 = 0, x1 = t with shift 4 - kd
+    const uint32_t kk = lit ? (4u - kd) & 3u : k;
     uint32_t x[RS_MW + 1];
 #pragma unroll
-    for (int j = 0; j <= RS_MW; ++j) x[j] = ring32[xa + (uint32_t)j];
-    // period words: pattern P = 4 bytes at s (bytes k + kd.. of the reads), phases (-kd + 4j) mod dist
-    const uint32_t m = (k + kd) >> 2, ks = (k + kd) & 3u;
-    const uint32_t H = __builtin_amdgcn_alignbyte(m ? x[2] : x[1], m ? x[1] : x[0], ks);
-    const uint32_t p0 = dist == 3u ? (3u - kd % 3u) % 3u : dist == 2u ? kd & 1u : 0u;
-    const uint32_t p1 = dist == 3u ? (p0 == 2u ? 0u : p0 + 1u) : p0, p2 = dist == 3u ? (p1 == 2u ? 0u : p1 + 1u) : p0;
-    const uint32_t R[3] = {rep4(H, dist, p0), rep4(H, dist, p1), rep4(H, dist, p2)};
-    // a literal: x0 = t (kd = 0), or x0 = 0, x1 = t with shift 4 - kd
-    const uint32_t kk = per ? 0u : lit ? (4u - kd) & 3u : k;
-    const uint32_t l0 = kd ? 0u : t, l1 = kd ? t : 0u;
-#pragma unroll
-    for (int j = 0; j <= RS_MW; ++j) x[j] = per ? R[j % 3] : lit ? (j == 0 ? l0 : j == 1 ? l1 : 0u) : x[j];
+    for (int j = 0; j <= RS_MW; ++j) {
+        const uint32_t r = ring32[xa + (uint32_t)j];
+        x[j] = !lit ? r : j == 0 ? (kd ? 0u : t) : j == 1 ? (kd ? t : 0u) : 0u;
+    }
     const uint32_t lom = 0xffffffffu << (8 * kd);
     static_for<0, RS_MW>([&](auto jc) {                   // each dword's data, then its finality
         constexpr int j = decltype(jc)::value;
@@ -292,20 +288,16 @@ __device__ __forceinline__ void emit_msk(uint8_t* ring, uint8_t* fmap, bool act,
         lds_mskor_at<j>(ring32, D0, mk, __builtin_amdgcn_alignbyte(x[j + 1], x[j], kk));
         lds_mskor_at<j>(fmap32, M0, mk, lw);
     });
-    // later steps of copies longer than 4 RS_MW - 3 bytes (periods: the pattern words go on)
+    // later steps of copies longer than 4 RS_MW - 3 bytes
     for (uint32_t w0 = RS_MW; __ballot(e > 4u * w0); w0 += RS_MW) {
         const bool on = e > 4u * w0;
-        uint32_t z[RS_MW + 1];
 #pragma unroll
-        for (int j = 0; j <= RS_MW; ++j) z[j] = ring32[on && !per ? xa + w0 + (uint32_t)j : dumi + (uint32_t)j];
-        uint32_t p = dist == 3u ? (p0 + w0) % 3u : p0;
+        for (int j = 0; j <= RS_MW; ++j) x[j] = ring32[on ? xa + w0 + (uint32_t)j : dumi + (uint32_t)j];
 #pragma unroll
         for (int j = 0; j < RS_MW; ++j) {
             const int32_t hb = (int32_t)e - 4 * (int32_t)(w0 + j);
             const uint32_t mw = !on || hb <= 0 ? 0u : hb >= 4 ? 0xffffffffu : (1u << (8 * hb)) - 1u;
-            const uint32_t v = per ? rep4(H, dist, p) : __builtin_amdgcn_alignbyte(z[j + 1], z[j], k);
-            p = dist == 3u ? (p == 2u ? 0u : p + 1u) : p;
-            lds_mskor_at<0>(ring32, D0 + w0 + (uint32_t)j, mw, v);
+            lds_mskor_at<0>(ring32, D0 + w0 + (uint32_t)j, mw, __builtin_amdgcn_alignbyte(x[j + 1], x[j], k));
             lds_mskor_at<0>(fmap32, M0 + w0 + (uint32_t)j, mw, lw);
         }
     }
@@ -352,7 +344,7 @@ __device__ __forceinline__ void publish_wf(uint32_t* wf, uint32_t v1) {
     if ((threadIdx.x & 63u) == 0) lds_put(wf, v1);
 }
 
-__global__ __launch_bounds__(RS_THREADS) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_inflate_resolve(InflateArgs A, uint32_t round) {
+__global__ __launch_bounds__(RS_THREADS) __attribute__((amdgpu_waves_per_eu(RS_WAVES, RS_WAVES))) void k_inflate_resolve(InflateArgs A, uint32_t round) {
     __shared__ __attribute__((aligned(16))) uint8_t ring[RS_R + 256];   // + per-lane dummies
     __shared__ uint64_t chain;                           // (tag of the last started group) << 32 | its end
     __shared__ uint32_t wf, wwb, fail;                   // frontiers: final bytes, written-back bytes
