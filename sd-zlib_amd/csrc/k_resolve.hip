@@ -254,7 +254,7 @@ __device__ __forceinline__ void lds_mskor_at(uint32_t* base32, uint32_t i, uint3
 // outside a token are no-ops.  Copies that overlap themselves (periods included), and
 // tokens across the ring's or map's end, go through emit_tokens.
 #ifndef RS_MW
-#define RS_MW 4
+#define RS_MW 3
 #endif
 __device__ __forceinline__ void emit_msk(uint8_t* ring, uint8_t* fmap, bool act, uint32_t t, uint32_t d,
                                          uint32_t s, uint32_t len, uint32_t dist, uint32_t mp, uint32_t lb) {
