@@ -30,6 +30,7 @@ namespace sdz {
 #ifndef RS_WAVES
 #define RS_WAVES 8
 #endif
+#define RS_EW (RS_WAVES - 1)           // emitter waves; the last wave writes back
 #define RS_THREADS (64 * RS_WAVES)
 #define RS_WIN 32768
 #define RS_R 36352                    // ring bytes: 32 KiB window + bytes in flight
@@ -347,7 +348,7 @@ __device__ __forceinline__ void publish_wf(uint32_t* wf, uint32_t v1) {
 __global__ __launch_bounds__(RS_THREADS) __attribute__((amdgpu_waves_per_eu(RS_WAVES, RS_WAVES))) void k_inflate_resolve(InflateArgs A, uint32_t round) {
     __shared__ __attribute__((aligned(16))) uint8_t ring[RS_R + 256];   // + per-lane dummies
     __shared__ uint64_t chain;                           // (tag of the last started group) << 32 | its end
-    __shared__ uint32_t wf, wwb, fail;                   // frontiers: final bytes, written-back bytes
+    __shared__ uint32_t wf, wwb, fail, edone;            // frontiers: final bytes, written-back bytes; emitters done
     __shared__ __attribute__((aligned(16))) uint8_t fmap[RS_BM];   // finality map of the bytes in flight
     __shared__ uint64_t red[RS_WAVES][2];
 
@@ -376,7 +377,7 @@ __global__ __launch_bounds__(RS_THREADS) __attribute__((amdgpu_waves_per_eu(RS_W
         else if (p >= -dl) b = dict[dl + p];
         ring[ridx((int32_t)rp0 - RS_WIN + (int32_t)k)] = (uint8_t)b;
     }
-    if (tid == 0) { chain = 0xffffffff00000000ull; wf = 0; wwb = 0; fail = 0; }
+    if (tid == 0) { chain = 0xffffffff00000000ull; wf = 0; wwb = 0; fail = 0; edone = 0; }
     for (uint32_t k = tid; k < RS_BM / 4; k += RS_THREADS) ((uint32_t*)fmap)[k] = 0;
     __syncthreads();
 
@@ -393,12 +394,14 @@ __global__ __launch_bounds__(RS_THREADS) __attribute__((amdgpu_waves_per_eu(RS_W
     unsigned long long tlast = timed ? clock64() : 0;
 #define RS_TICK(k) do { if (timed) { unsigned long long tn = clock64(); tacc[k] += tn - tlast; tlast = tn; } } while (0)
     const uint32_t ngroups = (ntok + 63u) >> 6;
-    uint32_t tnext = w * 64u + lane < ntok ? tk[w * 64u + lane] : 0u;
-    for (uint32_t g = w; g < ngroups; g += RS_WAVES) {
+    // emitter waves: no global stores, so the token prefetch is their only vector-memory
+    // traffic and its wait does not cover write-back stores
+    uint32_t tnext = tk[w * 64u + lane < ntok ? w * 64u + lane : 0u];
+    for (uint32_t g = w; w < RS_EW && g < ngroups; g += RS_EW) {
         const uint32_t ti = g * 64u + lane;
         const bool valid = ti < ntok;
         const uint32_t t = tnext;
-        tnext = ti + RS_THREADS < ntok ? tk[ti + RS_THREADS] : 0u;
+        tnext = tk[ti + 64u * RS_EW < ntok ? ti + 64u * RS_EW : 0u];
         const bool ism = (t >> 31) != 0;
         const uint32_t len = !valid ? 0u : ism ? ((t >> 16) & 255u) + 3u : ((t >> 24) & 3u) + 1u;
         const uint32_t dist = ism ? (t & 0x7fffu) + 1u : 0u;
@@ -421,7 +424,8 @@ __global__ __launch_bounds__(RS_THREADS) __attribute__((amdgpu_waves_per_eu(RS_W
         RS_TICK(1);
 
         // 2. copy rounds
-        const uint32_t sr = (rp0 + Sg) % RS_R;                         // ring index of byte Sg (u32: Sg < 2^26)
+        Sg = uni(Sg);                                                  // wave-uniform (keeps it and sr in SGPRs)
+        const uint32_t sr = uni((rp0 + Sg) % RS_R);                    // ring index of byte Sg (u32: Sg < 2^26)
         const uint32_t dst = Sg + off, dend = dst + len;
         const int32_t src = (int32_t)dst - (int32_t)dist;             // round-relative (may be < 0)
         const int32_t need = ism ? src + (int32_t)(len < dist ? len : dist) : INT32_MIN;
@@ -465,17 +469,45 @@ __global__ __launch_bounds__(RS_THREADS) __attribute__((amdgpu_waves_per_eu(RS_W
         const bool pub = cwf >= Sg;
         if (pub) publish_wf(&wf, Sg + T);
 
-        // 3. write back as dwords; adler partials
-        {
-            const uint64_t a0 = pos0 + Sg, a1 = a0 + T;
-            const uint32_t h = (uint32_t)(a0 & 3u);
-            const uint32_t nq = (uint32_t)(((a1 + 3u) >> 2) - (a0 >> 2));
-            uint32_t* dstw = (uint32_t*)(out + (a0 - h));
-            const uint32_t* ring32 = (const uint32_t*)ring;
-            const int32_t rb0 = (int32_t)sr - (int32_t)h;  // ring index of the first dword (4-aligned)
-            const uint32_t tl = (uint32_t)(a1 & 3u);
-            uint32_t gi0 = 0;
-            if (!gz) gi0 = (pm0 + 65521u + Sg - h) % 65521u;
+        RS_TICK(3);
+        // 3. the frontier, in group order
+        if (!pub) {
+            if (!wait_ge(&wf, Sg, &fail)) break;
+            publish_wf(&wf, Sg + T);
+        }
+        RS_TICK(4);
+    }
+    if (w < RS_EW) {
+        lds_release();
+        if (lane == 0) __hip_atomic_fetch_add(&edone, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    } else {
+        // the writer wave: final bytes -> HBM in output-aligned 1 KiB chunks, folded into the
+        // adler32 sums; publishes wwb, which frees ring slots
+        uint32_t WB = 0, Wr = rp0, gm = pm0;              // written back (round-relative), its ring index, (pos0 + WB) mod 65521
+        const uint32_t* ring32 = (const uint32_t*)ring;
+        for (uint32_t n = 0;; ++n) {
+            const bool fi = lds_get(&edone) == RS_EW;     // every group published: wf is the round's end
+            lds_acquire();
+            const uint32_t Fv = lds_get(&wf);
+            const uint64_t ab = pos0 + WB;
+            const uint32_t nk = 1024u - (uint32_t)(ab & 1023u);
+            uint32_t m;
+            if (Fv - WB >= nk) m = nk;
+            else if (fi) {
+                if (Fv == WB) break;
+                m = Fv - WB;
+            } else {
+                if (n > RS_SPIN_LIMIT || lds_get(&fail)) { if (!lds_get(&fail)) lds_put(&fail, 4u | (WB << 4)); break; }
+                __builtin_amdgcn_s_sleep(RS_NAP);
+                continue;
+            }
+            n = 0;
+            const uint32_t h = (uint32_t)(ab & 3u);
+            const uint32_t nq = (uint32_t)(((ab + m + 3u) >> 2) - (ab >> 2));
+            uint32_t* dstw = (uint32_t*)(out + (ab - h));
+            const int32_t rb0 = (int32_t)Wr - (int32_t)h;  // ring index of the first dword (4-aligned)
+            const uint32_t tl = (uint32_t)((ab + m) & 3u);
+            const uint32_t gi0 = gm + 65521u - h;          // index of byte 0 of dword 0, mod 65521 (+ 65521)
             for (uint32_t q = lane; q < nq; q += 64) {
                 const uint32_t v = ring32[ridx(rb0 + 4 * (int32_t)q) >> 2];
                 const uint32_t blo = q == 0 ? h : 0u;
@@ -483,28 +515,21 @@ __global__ __launch_bounds__(RS_THREADS) __attribute__((amdgpu_waves_per_eu(RS_W
                 if (blo == 0 && bhi == 4) dstw[q] = v;
                 else for (uint32_t bb = blo; bb < bhi; ++bb) ((uint8_t*)(dstw + q))[bb] = (uint8_t)(v >> (8 * bb));
                 if (!gz) {
-                    const uint32_t m = (bhi == 4u ? ~0u : (1u << (8 * bhi)) - 1u) & (~0u << (8 * blo));
-                    const uint32_t vm = v & m;
-                    uint32_t gi = gi0 + 4 * q;            // global index of byte 0 of this dword, mod 65521
-                    gi -= gi >= 65521u ? 65521u : 0u;
+                    const uint32_t mk = (bhi == 4u ? ~0u : (1u << (8 * bhi)) - 1u) & (~0u << (8 * blo));
+                    const uint32_t vm = v & mk;
                     const uint32_t s4 = __builtin_amdgcn_udot4(vm, 0x01010101u, 0u, false);
                     accS += s4;
-                    accT += (uint64_t)gi * s4 + __builtin_amdgcn_udot4(vm, 0x03020100u, 0u, false);
+                    accT += (uint64_t)(gi0 + 4 * q) * s4 + __builtin_amdgcn_udot4(vm, 0x03020100u, 0u, false);
                 }
             }
+            WB += m;
+            Wr += m;
+            Wr -= Wr >= RS_R ? RS_R : 0u;
+            gm += m;
+            gm -= gm >= 65521u ? 65521u : 0u;
+            lds_release();                                // our ring reads are complete
+            if (lane == 0) lds_put(&wwb, WB);
         }
-
-        RS_TICK(3);
-        // 4. frontiers, in group order
-        if (!pub) {
-            if (!wait_ge(&wf, Sg, &fail)) break;
-            publish_wf(&wf, Sg + T);
-        }
-        RS_TICK(4);
-        if (!wait_ge(&wwb, Sg, &fail)) break;
-        lds_release();                                    // our ring reads are complete
-        if (lane == 0) lds_put(&wwb, Sg + T);
-        RS_TICK(5);
     }
     if (timed) for (int k = 0; k < 8; ++k) atomicAdd(&A.dbg[k], tacc[k]);
 
