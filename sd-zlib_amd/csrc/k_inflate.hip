@@ -204,18 +204,32 @@ __device__ __forceinline__ void cnt_add(uint32_t (&c)[5], int len, uint32_t v) {
 
 // packed word for the code (rank offset / threshold / shift) whose 15-bit bit-reversed
 // prefix is rc: pk[1 + #{k : rc >= lim[k]}], as a depth-4 select tree (limits ascend)
+// The selects use VGPR masks (all ones where rc >= lim[k]) and v_bfi_b32, written as
+// inline asm so they stay VALU-only: compare-into-SGPR + v_cndmask pairs serialise on
+// one SGPR pair with wait states between them (gfx950), 15 times per tree.
+__device__ __forceinline__ uint32_t ge_mask(uint32_t rc, uint32_t lim) {   // lim, rc <= 32768
+    uint32_t m;
+    asm("v_sub_u32 %0, %1, %2\n\tv_ashrrev_i32 %0, 31, %0" : "=&v"(m) : "v"(lim - 1u), "v"(rc));
+    return m;
+}
+__device__ __forceinline__ uint32_t bfi(uint32_t m, uint32_t a, uint32_t b) {   // m ? a : b, bitwise
+    uint32_t r;
+    asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "v"(m), "v"(a), "v"(b));
+    return r;
+}
 __device__ __forceinline__ uint32_t tsel(const HTree& T, uint32_t rc) {
-    bool g1 = rc >= T.lim[1], g2 = rc >= T.lim[2], g3 = rc >= T.lim[3], g4 = rc >= T.lim[4];
-    bool g5 = rc >= T.lim[5], g6 = rc >= T.lim[6], g7 = rc >= T.lim[7], g8 = rc >= T.lim[8];
-    bool g9 = rc >= T.lim[9], g10 = rc >= T.lim[10], g11 = rc >= T.lim[11], g12 = rc >= T.lim[12];
-    bool g13 = rc >= T.lim[13], g14 = rc >= T.lim[14], g15 = rc >= T.lim[15];
-    uint32_t a1 = g1 ? T.pk[2] : T.pk[1], a3 = g3 ? T.pk[4] : T.pk[3];
-    uint32_t a5 = g5 ? T.pk[6] : T.pk[5], a7 = g7 ? T.pk[8] : T.pk[7];
-    uint32_t a9 = g9 ? T.pk[10] : T.pk[9], a11 = g11 ? T.pk[12] : T.pk[11];
-    uint32_t a13 = g13 ? T.pk[14] : T.pk[13], a15 = g15 ? T.pk[16] : T.pk[15];
-    uint32_t b1 = g2 ? a3 : a1, b5 = g6 ? a7 : a5, b9 = g10 ? a11 : a9, b13 = g14 ? a15 : a13;
-    uint32_t c1 = g4 ? b5 : b1, c9 = g12 ? b13 : b9;
-    return g8 ? c9 : c1;
+    uint32_t g1 = ge_mask(rc, T.lim[1]), g2 = ge_mask(rc, T.lim[2]), g3 = ge_mask(rc, T.lim[3]);
+    uint32_t g4 = ge_mask(rc, T.lim[4]), g5 = ge_mask(rc, T.lim[5]), g6 = ge_mask(rc, T.lim[6]);
+    uint32_t g7 = ge_mask(rc, T.lim[7]), g8 = ge_mask(rc, T.lim[8]), g9 = ge_mask(rc, T.lim[9]);
+    uint32_t g10 = ge_mask(rc, T.lim[10]), g11 = ge_mask(rc, T.lim[11]), g12 = ge_mask(rc, T.lim[12]);
+    uint32_t g13 = ge_mask(rc, T.lim[13]), g14 = ge_mask(rc, T.lim[14]), g15 = ge_mask(rc, T.lim[15]);
+    uint32_t a1 = bfi(g1, T.pk[2], T.pk[1]), a3 = bfi(g3, T.pk[4], T.pk[3]);
+    uint32_t a5 = bfi(g5, T.pk[6], T.pk[5]), a7 = bfi(g7, T.pk[8], T.pk[7]);
+    uint32_t a9 = bfi(g9, T.pk[10], T.pk[9]), a11 = bfi(g11, T.pk[12], T.pk[11]);
+    uint32_t a13 = bfi(g13, T.pk[14], T.pk[13]), a15 = bfi(g15, T.pk[16], T.pk[15]);
+    uint32_t b1 = bfi(g2, a3, a1), b5 = bfi(g6, a7, a5), b9 = bfi(g10, a11, a9), b13 = bfi(g14, a15, a13);
+    uint32_t c1 = bfi(g4, b5, b1), c9 = bfi(g12, b13, b9);
+    return bfi(g8, c9, c1);
 }
 __device__ __forceinline__ int32_t pk_rank(uint32_t v, uint32_t rc) {
     return (int32_t)(v >> 16) + (int32_t)(rc >> (v & 15u)) - 32768;
