@@ -2,21 +2,23 @@
 // Inflater verdicts (src/sd-inflate.ts:134-179); k_inflate_finalize adds crc32 for gzip.
 //
 // One WORKGROUP of RS_WAVES waves per stream, four streams per CU.  The stream's LZ77
-// window lives in LDS: a ~39 KiB ring holds the last 32 KiB of output plus the bytes in
+// window lives in LDS: a 35.5 KiB ring holds the last 32 KiB of output plus the bytes in
 // flight, so back-references never leave the CU.
 //
-// The waves form a pipeline without block barriers.  The round's tokens are cut into
-// GROUPS of 64 (one per lane); wave w takes groups w, w + RS_WAVES, ...  Per group:
+// Waves 0 .. RS_EW-1 (the emitters) form a pipeline without block barriers.  The round's
+// tokens are cut into GROUPS of 64 (one per lane); emitter w takes groups w, w + RS_EW,
+// ...  Per group:
 //   1. lengths and a DPP wave scan give the group's byte count T; the group's start S
 //      comes from its predecessor through a one-word LDS chain (tag, end), and S + T
 //      is passed on at once, so starts run ahead of the copying;
-//   2. rounds: every token whose source bytes are final is written (4-byte unaligned
-//      LDS copies; distances 1-3 as repeating words).  "Final" means below the
-//      stream-wide frontier Wf, or inside this group's own finished prefix;
-//   3. the group's bytes go to HBM as coalesced dwords, folded into adler32
-//      (S = sum b, T = sum i b as whole-output sums);
-//   4. the group publishes Wf = S + T once Wf reached S (in order), then Wwb (bytes
-//      written back, which frees their ring slots) the same way.
+//   2. rounds: every token whose source bytes are final is written -- literals and plain
+//      copies as masked dword read-modify-writes (emit_msk), the rest by emit_tokens.
+//      "Final" means below the stream-wide frontier Wf, or marked in the finality map;
+//   3. the group publishes Wf = S + T once Wf reached S (in order).
+// The last wave (the writer) copies final bytes to HBM in output-aligned 1 KiB chunks,
+// folds them into adler32 (S = sum b, T = sum i b as whole-output sums) and publishes Wwb
+// (bytes written back, which frees their ring slots).  The emitters issue no global
+// stores, so the wait for their token prefetch never covers write-back stores.
 // A head group (Wf == S) publishes its finished prefix as it goes, so a large group
 // never waits on its own ring space.  Ring-space rule: writing byte p needs
 // p < Wf + (R - 32 KiB) (no reader needs byte p - R any more) and p < Wwb + R (byte
