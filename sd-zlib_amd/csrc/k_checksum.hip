@@ -5,55 +5,21 @@
 // remainder exists) is reproduced exactly: per block the wave reduces the byte
 // sum T and the weighted sum W = sum (5552 - i) * b_i, and lane 0 chains
 //   sum2 += 5552 * s1 + W + BASE;  s1 = (s1 + T) mod BASE.
-// crc32 splits the buffer into 64 lane chunks (byte-wise LDS table) and merges
-// them with GF(2) polynomial shifts (x^(8 len) mod P), a log2(64)-step tree.
+// crc32 (crc32_dev.h): 64 lane chunks, slicing-by-8 over 8-byte loads, merged with GF(2)
+// polynomial shifts (x^(8 len) mod P) in a log2(64)-step tree.
 #include "sdz_internal.h"
+#include "crc32_dev.h"
 
 namespace sdz {
 
 #define CK_THREADS 64
 
-__device__ uint32_t multmodp(uint32_t a, uint32_t b) {
-    uint32_t m = 1u << 31, p = 0;
-    for (;;) {
-        if (a & m) {
-            p ^= b;
-            if ((a & (m - 1)) == 0) break;
-        }
-        m >>= 1;
-        b = b & 1 ? (b >> 1) ^ 0xedb88320u : b >> 1;
-    }
-    return p;
-}
-
-// x^(n * 2^3) mod P, i.e. the shift for n bytes
-__device__ uint32_t xbytes(uint64_t n, const uint32_t* x2n) {
-    uint32_t p = 1u << 31;
-    unsigned k = 3;
-    while (n) {
-        if (n & 1) p = multmodp(x2n[k & 31], p);
-        n >>= 1;
-        k++;
-    }
-    return p;
-}
-
 __global__ __launch_bounds__(CK_THREADS) void k_checksum(const uint8_t* in, const uint64_t* in_off,
                                                          const uint64_t* in_len, const int32_t* seed,
                                                          int32_t* result, uint32_t n, int kind) {
-    __shared__ uint32_t tab[256];
-    __shared__ uint32_t x2n[32];
+    __shared__ CrcTables ct;
     uint32_t lane = threadIdx.x;
-    for (uint32_t v = lane; v < 256; v += CK_THREADS) {
-        uint32_t c = v;
-        for (int k = 0; k < 8; ++k) c = (c & 1) ? 0xedb88320u ^ (c >> 1) : c >> 1;
-        tab[v] = c;
-    }
-    if (lane == 0) {
-        uint32_t p = 1u << 30;
-        x2n[0] = p;
-        for (int k = 1; k < 32; ++k) x2n[k] = p = multmodp(p, p);
-    }
+    if (kind != 0) crc_tables_init(ct);
     __syncthreads();
     uint32_t sid = blockIdx.x;
     if (sid >= n) return;
@@ -85,23 +51,8 @@ __global__ __launch_bounds__(CK_THREADS) void k_checksum(const uint8_t* in, cons
         }
         if (lane == 0) result[sid] = (int32_t)((uint32_t)s1 | ((uint32_t)s2 << 16));
     } else {                                             // crc32
-        uint64_t chunk = (len + CK_THREADS - 1) / CK_THREADS;
-        uint64_t b0 = (uint64_t)lane * chunk;
-        uint64_t b1 = b0 + chunk < len ? b0 + chunk : len;
-        uint64_t clen = b1 > b0 ? b1 - b0 : 0;
-        uint32_t c = 0xffffffffu;
-        for (uint64_t i = b0; i < b1; ++i) c = tab[(c ^ p[i]) & 255] ^ (c >> 8);
-        uint32_t crc = ~c;
-        uint64_t l = clen;
-        for (int o = 1; o < CK_THREADS; o <<= 1) {
-            uint32_t rc = __shfl_down(crc, o);
-            uint64_t rl = __shfl_down(l, o);
-            if ((lane & (2 * o - 1)) == 0 && lane + o < CK_THREADS) {
-                crc = multmodp(xbytes(rl, x2n), crc) ^ rc;
-                l += rl;
-            }
-        }
-        if (lane == 0) result[sid] = (int32_t)(multmodp(xbytes(len, x2n), sd) ^ crc);
+        const uint32_t crc = crc32_wave(p, len, ct);
+        if (lane == 0) result[sid] = (int32_t)(gf2_mulmod(gf2_xbytes(len, ct.x2n), sd) ^ crc);
     }
 }
 

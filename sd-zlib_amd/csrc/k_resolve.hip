@@ -25,6 +25,7 @@
 // p - R is in HBM).  Every wait is bounded (SDZ_INTERNAL if a bound trips).
 // Positions before the output start read the preset dictionary or zeros.
 #include "inflate_state.h"
+#include "crc32_dev.h"
 #include <type_traits>
 
 namespace sdz {
@@ -620,68 +621,19 @@ __global__ __launch_bounds__(RS_THREADS) __attribute__((amdgpu_waves_per_eu(RS_W
 
 // ------------------------------------------------------------------ gzip: crc32 + verdicts
 
-__device__ uint32_t gf2_mul(uint32_t a, uint32_t b) {       // a * b mod P (reflected)
-    uint32_t m = 1u << 31, p = 0;
-    for (;;) {
-        if (a & m) {
-            p ^= b;
-            if ((a & (m - 1)) == 0) break;
-        }
-        m >>= 1;
-        b = b & 1 ? (b >> 1) ^ 0xedb88320u : b >> 1;
-    }
-    return p;
-}
-__device__ uint32_t gf2_xbytes(uint64_t n, const uint32_t* x2n) {   // x^(8n) mod P
-    uint32_t p = 1u << 31;
-    unsigned k = 3;
-    while (n) {
-        if (n & 1) p = gf2_mul(x2n[k & 31], p);
-        n >>= 1;
-        k++;
-    }
-    return p;
-}
-
-// one wave per finished gzip stream: crc32 of its output (64 lane chunks merged with
-// polynomial shifts) and the checksum verdicts that depend on it
+// one wave per finished gzip stream: crc32 of its output (crc32_dev.h) and the checksum
+// verdicts that depend on it
 __global__ __launch_bounds__(64) void k_inflate_finalize(InflateArgs A) {
-    __shared__ uint32_t tab[256];
-    __shared__ uint32_t x2n[32];
+    __shared__ CrcTables ct;
+    crc_tables_init(ct);
+    __syncthreads();
     const uint32_t sid = blockIdx.x;
     if (sid >= A.n) return;
     sdz_inflate_record* rec = A.rec + sid;
     if (rec->container != SDZ_CONTAINER_GZIP) return;
-    const uint32_t lane = threadIdx.x;
-    for (uint32_t v = lane; v < 256; v += 64) {
-        uint32_t c = v;
-        for (int k = 0; k < 8; ++k) c = (c & 1) ? 0xedb88320u ^ (c >> 1) : c >> 1;
-        tab[v] = c;
-    }
-    if (lane == 0) {
-        uint32_t p = 1u << 30;
-        x2n[0] = p;
-        for (int k = 1; k < 32; ++k) x2n[k] = p = gf2_mul(p, p);
-    }
-    __syncthreads();
-    const uint8_t* p = A.out + A.out_off[sid];
     const uint64_t len = rec->out_len;
-    const uint64_t chunk = (len + 63) / 64;
-    const uint64_t b0 = (uint64_t)lane * chunk;
-    const uint64_t b1 = b0 + chunk < len ? b0 + chunk : len;
-    uint64_t l = b1 > b0 ? b1 - b0 : 0;
-    uint32_t cr = 0xffffffffu;
-    for (uint64_t i = b0; i < b1; ++i) cr = tab[(cr ^ p[i]) & 255] ^ (cr >> 8);
-    uint32_t crc = ~cr;
-    for (int o = 1; o < 64; o <<= 1) {
-        uint32_t rc = __shfl_down(crc, o);
-        uint64_t rl = __shfl_down(l, o);
-        if ((lane & (2 * o - 1)) == 0 && lane + o < 64) {
-            crc = gf2_mul(gf2_xbytes(rl, x2n), crc) ^ rc;
-            l += rl;
-        }
-    }
-    if (lane != 0) return;
+    const uint32_t crc = crc32_wave(A.out + A.out_off[sid], len, ct);
+    if (threadIdx.x != 0) return;
     const bool have = len > 0;
     const int32_t running = (int32_t)crc;
     rec->running_checksum = have ? running : 0;
