@@ -625,12 +625,12 @@ __global__ __launch_bounds__(RS_THREADS) __attribute__((amdgpu_waves_per_eu(RS_W
 // verdicts that depend on it
 __global__ __launch_bounds__(64) void k_inflate_finalize(InflateArgs A) {
     __shared__ CrcTables ct;
-    crc_tables_init(ct);
-    __syncthreads();
     const uint32_t sid = blockIdx.x;
     if (sid >= A.n) return;
     sdz_inflate_record* rec = A.rec + sid;
-    if (rec->container != SDZ_CONTAINER_GZIP) return;
+    if (rec->container != SDZ_CONTAINER_GZIP) return;    // block-uniform: no table build for zlib / raw
+    crc_tables_init(ct);
+    __syncthreads();
     const uint64_t len = rec->out_len;
     const uint32_t crc = crc32_wave(A.out + A.out_off[sid], len, ct);
     if (threadIdx.x != 0) return;
