@@ -134,6 +134,9 @@ def main():
     ap.add_argument("--deflate-streams", type=int, default=65536,
                     help="streams for the deflate leg (64 KiB slices, L6); 0 disables")
     ap.add_argument("--deflate-steps", type=int, default=1)
+    ap.add_argument("--copy-gib", type=float, default=4.0, help="device copy peak probe size; 0 disables")
+    ap.add_argument("--host-streams", type=int, default=2048,
+                    help="streams for the host-buffer (PCIe-inclusive) inflate probe; 0 disables")
     args = ap.parse_args()
 
     import torch
@@ -205,6 +208,45 @@ def main():
     bytes_in, bytes_out = len(comp) * n, len(text) * n
     b.free()
 
+    # ---- measured device copy peak (report against it in the same run)
+    copy_gbs = None
+    if args.copy_gib > 0:
+        nb = int(args.copy_gib * (1 << 30))
+        src = torch.empty(nb, dtype=torch.uint8, device="cuda")
+        dst = torch.empty_like(src)
+        dst.copy_(src)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(5):
+            dst.copy_(src)
+        e1.record()
+        e1.synchronize()
+        copy_gbs = 2.0 * nb * 5 / (e0.elapsed_time(e1) / 1000.0) / 1e9   # read + write bytes
+        del src, dst
+        torch.cuda.empty_cache()
+
+    # ---- host-buffer path (PCIe-inclusive, never `value`): sdz.inflate_batch on host bytes
+    host = None
+    if rank == 0 and args.host_streams > 0:
+        hn = args.host_streams
+        ins = (ctypes.c_char_p * hn)(*([comp] * hn))
+        in_len = (ctypes.c_size_t * hn)(*([len(comp)] * hn))
+        hbufs = [ctypes.create_string_buffer(len(text)) for _ in range(hn)]
+        outs = (ctypes.c_void_p * hn)(*[ctypes.addressof(x) for x in hbufs])
+        caps = (ctypes.c_size_t * hn)(*([len(text)] * hn))
+        hrec = (sdz.InflateRecord * hn)()
+        hdt = None
+        for _ in range(2):                                  # the first call sizes the pools
+            h0 = time.perf_counter()
+            hrc = L.sdz_inflate_batch(ins, in_len, outs, caps, hrec, hn, sdz.FMT_AUTO, None, 0)
+            hdt = time.perf_counter() - h0
+        hok = hrc == 0 and all(r.success and r.out_len == len(text) for r in hrec) and \
+            all(hbufs[i].raw == text for i in (0, hn - 1))
+        host = {"streams": hn, "MBps_out": round(hn * len(text) / hdt / 1e6, 2),
+                "seconds": round(hdt, 3), "parity": bool(hok),
+                "note": "sdz_inflate_batch on host buffers: H2D + kernels + D2H, PCIe-inclusive"}
+        del hbufs
+
     # ---- deflate leg (configs[2]: 64 KiB text slices, level 6, "deflate" container)
     deflate = None
     if args.deflate_streams > 0:
@@ -248,10 +290,12 @@ def main():
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
         threads = max(1, min(16, os.cpu_count() or 1))
         cnt, dt = cpu_baseline_inflate(comp, args.cpu_seconds, threads)
+        c1, d1 = cpu_baseline_inflate(comp, max(0.5, args.cpu_seconds / 2), 1)
         cpu = {"value": round(cnt * len(text) / dt / 1e6, 2), "unit": "MB/s", "cores": threads,
                "kind": "port",
+               "per_core_MBps": round(c1 * len(text) / d1 / 1e6, 2),
                "sample": "%d x paradiselost.deflate inflated by the oracle C restatement on %d threads "
-                         "in %.1f s" % (cnt, threads, dt)}
+                         "in %.1f s; per core: %d in %.1f s on 1 thread" % (cnt, threads, dt, c1, d1)}
 
     traffic = None
     pmc = os.path.join(ROOT, "profiles", "r01_inflate_pmc.json")
@@ -280,7 +324,10 @@ def main():
                                     "k_inflate_resolve": round(kparts[1], 3),
                                     "k_inflate_finalize": round(kparts[2], 3)},
                      "launch": "one sdz_inflate_batch_device call = decode + resolve + finalize kernels",
-                     "algorithmic_bytes_per_launch": bytes_in + bytes_out},
+                     "algorithmic_bytes_per_launch": bytes_in + bytes_out,
+                     "measured_copy_GBps": None if copy_gbs is None else round(copy_gbs, 1),
+                     "frac_of_copy": None if copy_gbs is None else round(achieved / copy_gbs, 5)},
+        "host_path": host,
         "cpu_baseline": cpu,
         "parity": bool(okall),
         "gather_ms": None if gather_ms is None else round(gather_ms, 3),
