@@ -907,6 +907,9 @@ __global__ __launch_bounds__(64) void k_dfl_chain(DeflateArgs A) {
 // MIN_MATCH - 1) -- chain max_chain in the low word, max_chain >> 2 in the high word.
 #define PM_SEG 16384
 #define PM_THREADS 1024
+#ifndef PM_REFILL
+#define PM_REFILL 8                                     // idle lanes that trigger a refill
+#endif
 #define PM_WINB (W_SIZE + PM_SEG + MAX_MATCH + 16)     // staged window bytes
 #define PM_PV (W_SIZE + PM_SEG)                         // staged links
 __device__ __forceinline__ uint32_t pm_w4(const uint8_t* w, uint32_t x) {   // 4 bytes at x, aligned reads
@@ -950,19 +953,34 @@ __global__ __launch_bounds__(PM_THREADS) void k_dfl_match(DeflateArgs A, uint32_
     const int per = (s1 - s0 + PM_THREADS / 64 - 1) / (PM_THREADS / 64);
     const int q0 = s0 + (int)wv * per, q1 = q0 + per < s1 ? q0 + per : s1;
     int next = q0;                                          // wave-uniform queue head
-    bool act = false;
+    bool act = false, pend = false;
     // cur: this step's candidate; nxt: the link after it (read a step ahead, so the chain
     // link of a step does not wait on the previous one)
     int p = s0, cur = 0, nxt = 0, best = 0, bpos = 0, qbest = 0, qpos = 0, k = 0, chain = 0, limit = 0;
     uint32_t sb = 0, s4 = 0;
     for (;;) {
-        // idle lanes take the next positions
+        // Idle lanes store their records and take the next positions once PM_REFILL lanes
+        // are idle (or all are): the refill and the record store then run once per several
+        // steps rather than at nearly every step (some lane ends its walk at most steps).
         const uint64_t im = __ballot(!act);
-        if (im && next < q1) {
+        const int nidle = __popcll(im);
+        if (nidle < PM_REFILL && nidle != 64) {
+            // keep walking
+        } else {
+            if (pend) {
+                if (qbest < 0) { qbest = best; qpos = bpos; }
+                const uint32_t full = best > MIN_MATCH - 1 ? ((uint32_t)best << 16) | (uint32_t)(p - bpos) : 0u;
+                const uint32_t quarter = qbest > MIN_MATCH - 1 ? ((uint32_t)qbest << 16) | (uint32_t)(p - qpos) : 0u;
+                rec[p] = ((uint64_t)quarter << 32) | full;
+                pend = false;
+            }
+            if (next >= q1 && nidle == 64) break;
+        }
+        if (nidle >= PM_REFILL && next < q1) {
             const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(im >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)im, 0u));
             const int pn = next + (int)rank;
             const bool take = !act && pn < q1;
-            next += __popcll(im);
+            next += nidle;
             if (take) {
                 p = pn;
                 act = true;
@@ -976,7 +994,7 @@ __global__ __launch_bounds__(PM_THREADS) void k_dfl_match(DeflateArgs A, uint32_
                 nxt = pvl[(uint32_t)((chain ? cur : p) - ws)];
             }
         }
-        if (!__ballot(act)) break;
+        if (!__ballot(act)) continue;                          // all idle: store (and end) above
         // one candidate per active lane, branch-free but for the rare long compare
         const bool live = act && chain > 0;
         const bool goes_on = nxt > limit && chain - 1 != 0;  // the walk continues after cur
@@ -1008,13 +1026,8 @@ __global__ __launch_bounds__(PM_THREADS) void k_dfl_match(DeflateArgs A, uint32_
         cur = nxt;
         nxt = nn;
         chain -= 1;
-        if (fin) {
-            if (qbest < 0) { qbest = best; qpos = bpos; }
-            const uint32_t full = best > MIN_MATCH - 1 ? ((uint32_t)best << 16) | (uint32_t)(p - bpos) : 0u;
-            const uint32_t quarter = qbest > MIN_MATCH - 1 ? ((uint32_t)qbest << 16) | (uint32_t)(p - qpos) : 0u;
-            rec[p] = ((uint64_t)quarter << 32) | full;
-            act = false;
-        }
+        pend = pend || fin;                                   // stored at the next refill
+        act = act && !fin;
     }
 }
 
