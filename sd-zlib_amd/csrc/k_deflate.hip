@@ -920,7 +920,7 @@ __global__ __launch_bounds__(PM_THREADS) void k_dfl_match(DeflateArgs A, uint32_
     __shared__ __attribute__((aligned(16))) uint8_t win[(PM_WINB + 15) & ~15];
     __shared__ __attribute__((aligned(16))) uint16_t pvl[PM_PV];
     const uint32_t sid = blockIdx.x / nseg, seg = blockIdx.x % nseg, tid = threadIdx.x;
-    const uint32_t lane = tid & 63u, wv = tid >> 6;
+    const uint32_t wv = tid >> 6;
     if (sid >= A.n) return;
     const uint64_t in_len = A.in_len[sid];
     if (in_len > A.rec_stride) return;
@@ -1186,17 +1186,13 @@ __global__ __launch_bounds__(64) void k_dfl_parse(DeflateArgs A) {
                 match_length = MIN_MATCH - 1;
         }
         if (prev_length >= MIN_MATCH && match_length <= prev_length) {
-            const int max_insert = strstart + lookahead - MIN_MATCH;
             const bool bflush = tally(strstart - 1 - prev_match, prev_length - MIN_MATCH);
             lookahead -= prev_length - 1;
-            // strstart+1 .. strstart+prev_length-2 are inserted (up to max_insert); only the
-            // last insertion's hash_head survives
+            // strstart+1 .. strstart+prev_length-2 are inserted (up to max_insert).  The last
+            // insertion's hash_head is never read: the next step reads hash_head only with
+            // lookahead >= MIN_MATCH, and then sets it from its own position first.  So the
+            // record path skips that load (a memory round trip per match).
             const int last = strstart + prev_length - 2;
-            const int lastins = last < max_insert ? last : max_insert;
-            if (lastins > strstart) {
-                const uint32_t w = pv[lastins + off];
-                hash_head = off ? (w >= W_SIZE ? (int)w - W_SIZE : 0) : (int)w;
-            }
             strstart = last + 1;
             match_available = 0;
             match_length = MIN_MATCH - 1;
