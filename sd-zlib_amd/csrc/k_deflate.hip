@@ -953,20 +953,22 @@ __global__ __launch_bounds__(PM_THREADS) void k_dfl_match(DeflateArgs A, uint32_
     const int per = (s1 - s0 + PM_THREADS / 64 - 1) / (PM_THREADS / 64);
     const int q0 = s0 + (int)wv * per, q1 = q0 + per < s1 ? q0 + per : s1;
     int next = q0;                                          // wave-uniform queue head
-    bool act = false, pend = false;
+    // A lane walks while chain > 0 (chain counts the candidates left); a finished lane keeps
+    // its results (pend) until the next refill stores them.  The quarter walk ends at the
+    // step where chain == cq, i.e. after qchain candidates.
+    bool pend = false;
+    const int cq = max_chain - qchain + 1;
     // cur: this step's candidate; nxt: the link after it (read a step ahead, so the chain
     // link of a step does not wait on the previous one)
-    int p = s0, cur = 0, nxt = 0, best = 0, bpos = 0, qbest = 0, qpos = 0, k = 0, chain = 0, limit = 0;
-    uint32_t sb = 0, s4 = 0;
+    int p = s0, cur = 0, nxt = 0, best = 0, bpos = 0, qbest = 0, qpos = 0, chain = 0, limit = 0;
+    uint32_t s4 = 0;
     for (;;) {
         // Idle lanes store their records and take the next positions once PM_REFILL lanes
         // are idle (or all are): the refill and the record store then run once per several
         // steps rather than at nearly every step (some lane ends its walk at most steps).
-        const uint64_t im = __ballot(!act);
+        const uint64_t im = __ballot(chain <= 0);
         const int nidle = __popcll(im);
-        if (nidle < PM_REFILL && nidle != 64) {
-            // keep walking
-        } else {
+        if (nidle >= PM_REFILL || nidle == 64) {
             if (pend) {
                 if (qbest < 0) { qbest = best; qpos = bpos; }
                 const uint32_t full = best > MIN_MATCH - 1 ? ((uint32_t)best << 16) | (uint32_t)(p - bpos) : 0u;
@@ -975,31 +977,30 @@ __global__ __launch_bounds__(PM_THREADS) void k_dfl_match(DeflateArgs A, uint32_
                 pend = false;
             }
             if (next >= q1 && nidle == 64) break;
-        }
-        if (nidle >= PM_REFILL && next < q1) {
-            const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(im >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)im, 0u));
-            const int pn = next + (int)rank;
-            const bool take = !act && pn < q1;
-            next += nidle;
-            if (take) {
-                p = pn;
-                act = true;
-                const uint32_t sp = (uint32_t)(p - ws);
-                cur = pvl[sp];                                  // hash_head
-                best = MIN_MATCH - 1; bpos = 0; qbest = -1; k = 0; chain = max_chain;
-                limit = p > MAX_DIST ? p - MAX_DIST : 0;
-                s4 = pm_w4(win, sp);
-                sb = win[sp + best];
-                if (cur == 0 || p - cur > MAX_DIST) chain = 0;  // no search (deflate.ts:1092)
-                nxt = pvl[(uint32_t)((chain ? cur : p) - ws)];
+            if (next < q1) {
+                const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(im >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)im, 0u));
+                const int pn = next + (int)rank;
+                next += nidle;
+                if (chain <= 0 && pn < q1) {
+                    p = pn;
+                    const uint32_t sp = (uint32_t)(p - ws);
+                    cur = pvl[sp];                              // hash_head
+                    best = MIN_MATCH - 1; bpos = 0; qbest = -1;
+                    limit = p > MAX_DIST ? p - MAX_DIST : 0;
+                    s4 = pm_w4(win, sp);
+                    const bool search = cur != 0 && p - cur <= MAX_DIST;   // deflate.ts:1092
+                    chain = search ? max_chain : 0;
+                    pend = !search;                             // no search: record 0
+                    nxt = pvl[(uint32_t)((search ? cur : p) - ws)];
+                }
             }
         }
-        if (!__ballot(act)) continue;                          // all idle: store (and end) above
-        // one candidate per active lane, branch-free but for the rare long compare
-        const bool live = act && chain > 0;
-        const bool goes_on = nxt > limit && chain - 1 != 0;  // the walk continues after cur
+        if (!__ballot(chain > 0)) continue;                    // all idle: store (and end) above
+        // one candidate per walking lane, branch-free but for the rare long compare
+        const bool live = chain > 0;
+        const bool goes_on = nxt > limit && chain > 1;       // the walk continues after cur
         const uint32_t cp = (uint32_t)((live ? cur : p) - ws), sp = (uint32_t)(p - ws);
-        const uint32_t wb = win[cp + best];
+        const uint32_t wb = win[cp + best], sb = win[sp + best];
         uint32_t x = pm_w4(win, cp) ^ s4;
         const int nn = pvl[(uint32_t)((live && goes_on ? nxt : p) - ws)];
         const bool cand = live && wb == sb;                  // can beat best (deflate.ts:866-882)
@@ -1016,18 +1017,14 @@ __global__ __launch_bounds__(PM_THREADS) void k_dfl_match(DeflateArgs A, uint32_
         const bool upd = cand && len > best;
         best = upd ? len : best;
         bpos = upd ? cur : bpos;
-        bool fin = upd && len >= nice;
-        if (__ballot(upd)) sb = win[sp + (best < MAX_MATCH ? best : MAX_MATCH)];
-        k += live ? 1 : 0;
-        const bool cap = live && k == qchain;
+        const bool cap = live && chain == cq;
         qbest = cap ? best : qbest;
         qpos = cap ? bpos : qpos;
-        fin = act && (fin || !live || !goes_on);
+        const bool fin = live && ((upd && len >= nice) || !goes_on);
         cur = nxt;
         nxt = nn;
-        chain -= 1;
         pend = pend || fin;                                   // stored at the next refill
-        act = act && !fin;
+        chain = fin ? 0 : chain - 1;
     }
 }
 
