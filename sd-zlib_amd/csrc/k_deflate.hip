@@ -995,7 +995,6 @@ __global__ __launch_bounds__(PM_THREADS) void k_dfl_match(DeflateArgs A, uint32_
                 }
             }
         }
-        if (!__ballot(chain > 0)) continue;                    // all idle: store (and end) above
         // one candidate per walking lane, branch-free but for the rare long compare
         const bool live = chain > 0;
         const bool goes_on = nxt > limit && chain > 1;       // the walk continues after cur
@@ -1006,14 +1005,12 @@ __global__ __launch_bounds__(PM_THREADS) void k_dfl_match(DeflateArgs A, uint32_
         const bool cand = live && wb == sb;                  // can beat best (deflate.ts:866-882)
         int len = x ? (int)(__builtin_ctz(x) >> 3) : 4;
         bool more = cand && x == 0;
-        if (__ballot(more)) {                                // matches of more than 4 bytes
-            while (__ballot(more)) {
-                x = more ? pm_w4(win, cp + (uint32_t)len) ^ pm_w4(win, sp + (uint32_t)len) : 1u;
-                len += more ? (x ? (int)(__builtin_ctz(x) >> 3) : 4) : 0;
-                more = more && x == 0 && len < MAX_MATCH;
-            }
-            len = len > MAX_MATCH ? MAX_MATCH : len;
+        while (__ballot(more)) {                             // matches of more than 4 bytes
+            x = more ? pm_w4(win, cp + (uint32_t)len) ^ pm_w4(win, sp + (uint32_t)len) : 1u;
+            len += more ? (x ? (int)(__builtin_ctz(x) >> 3) : 4) : 0;
+            more = more && x == 0 && len < MAX_MATCH;
         }
+        len = len > MAX_MATCH ? MAX_MATCH : len;
         const bool upd = cand && len > best;
         best = upd ? len : best;
         bpos = upd ? cur : bpos;
