@@ -39,10 +39,10 @@ namespace sdz {
 #define RS_R 36352                    // ring bytes: 32 KiB window + bytes in flight
 #define RS_SLACK (RS_R - RS_WIN)
 #ifndef RS_NAP
-#define RS_NAP 4                      // s_sleep units (64 clocks) between polls
+#define RS_NAP 8                      // s_sleep units (64 clocks) between polls
 #endif
 #define RS_BM 4096                    // finality map bytes (>= RS_SLACK; lap = position >> 12)
-#define RS_SPIN_LIMIT (1u << 22)      // watchdog: polls per wait (~0.2 s)
+#define RS_SPIN_LIMIT (1u << 22)      // watchdog: polls per wait (~0.4 s)
 
 __device__ __forceinline__ uint32_t ridx(int32_t x) {            // x in (-R, 2R)
     x += x < 0 ? RS_R : 0;
@@ -258,7 +258,7 @@ __device__ __forceinline__ void lds_mskor_at(uint32_t* base32, uint32_t i, uint3
 // outside a token are no-ops.  Copies that overlap themselves (periods included), and
 // tokens across the ring's or map's end, go through emit_tokens.
 #ifndef RS_MW
-#define RS_MW 3
+#define RS_MW 2
 #endif
 __device__ __forceinline__ void emit_msk(uint8_t* ring, uint8_t* fmap, bool act, uint32_t t, uint32_t d,
                                          uint32_t s, uint32_t len, uint32_t dist, uint32_t mp, uint32_t lb) {
