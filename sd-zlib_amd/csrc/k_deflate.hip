@@ -907,6 +907,9 @@ __global__ __launch_bounds__(64) void k_dfl_chain(DeflateArgs A) {
 // MIN_MATCH - 1) -- chain max_chain in the low word, max_chain >> 2 in the high word.
 #define PM_SEG 16384
 #define PM_THREADS 1024
+#ifndef PM_PAIR
+#define PM_PAIR 1                                       // two chain candidates per step
+#endif
 #ifndef PM_REFILL
 #define PM_REFILL 8                                     // idle lanes that trigger a refill
 #endif
@@ -995,6 +998,60 @@ __global__ __launch_bounds__(PM_THREADS) void k_dfl_match(DeflateArgs A, uint32_
                 }
             }
         }
+#if PM_PAIR
+        // two candidates per walking lane and step: cur (c1) and nxt (c2).  Both pass the
+        // reference's pre-check against the step's starting best: a candidate that beats the
+        // best after c1 also beats that, so the check only filters (deflate.ts:866-882), and
+        // a candidate that passes gets its exact length.  The links after c2 (c3, then c4)
+        // are read in turn, so the next step starts with two candidates again.
+        const bool live = chain > 0;
+        const bool go1 = nxt > limit && chain > 1;           // the walk continues after c1
+        const bool l2 = live && go1;                          // c2 is walked (unless nice at c1)
+        const uint32_t sp = (uint32_t)(p - ws);
+        const uint32_t c1 = (uint32_t)((live ? cur : p) - ws), c2 = (uint32_t)((l2 ? nxt : p) - ws);
+        const int c3 = pvl[c2];
+        const uint32_t sb = win[sp + best], wb1 = win[c1 + best], wb2 = win[c2 + best];
+        uint32_t x1 = pm_w4(win, c1) ^ s4, x2 = pm_w4(win, c2) ^ s4;
+        const bool go2 = c3 > limit && chain > 2;            // ... and after c2
+        const int c4 = pvl[(uint32_t)((l2 && go2 ? c3 : p) - ws)];
+        const bool cand1 = live && wb1 == sb, cand2 = l2 && wb2 == sb;
+        int len1 = x1 ? (int)(__builtin_ctz(x1) >> 3) : 4;
+        int len2 = x2 ? (int)(__builtin_ctz(x2) >> 3) : 4;
+        bool more1 = cand1 && x1 == 0, more2 = cand2 && x2 == 0;
+        while (__ballot(more1 || more2)) {                   // matches of more than 4 bytes
+            const uint32_t cm = more1 ? c1 : c2;
+            const int lm = more1 ? len1 : len2;
+            const uint32_t x = pm_w4(win, cm + (uint32_t)lm) ^ pm_w4(win, sp + (uint32_t)lm);
+            const int d = x ? (int)(__builtin_ctz(x) >> 3) : 4;
+            const bool m1 = more1, m2 = !more1 && more2;
+            len1 += m1 ? d : 0;
+            len2 += m2 ? d : 0;
+            more1 = m1 ? x == 0 && len1 < MAX_MATCH : more1;
+            more2 = m2 ? x == 0 && len2 < MAX_MATCH : more2;
+        }
+        len1 = len1 > MAX_MATCH ? MAX_MATCH : len1;
+        len2 = len2 > MAX_MATCH ? MAX_MATCH : len2;
+        // c1
+        const bool upd1 = cand1 && len1 > best;
+        best = upd1 ? len1 : best;
+        bpos = upd1 ? cur : bpos;
+        const bool cap1 = live && chain == cq;
+        qbest = cap1 ? best : qbest;
+        qpos = cap1 ? bpos : qpos;
+        const bool w2 = l2 && !(upd1 && len1 >= nice);
+        // c2
+        const bool upd2 = w2 && cand2 && len2 > best;
+        best = upd2 ? len2 : best;
+        bpos = upd2 ? nxt : bpos;
+        const bool cap2 = w2 && chain - 1 == cq;
+        qbest = cap2 ? best : qbest;
+        qpos = cap2 ? bpos : qpos;
+        const bool fin = live && (!w2 || (upd2 && len2 >= nice) || !go2);
+        cur = c3;
+        nxt = c4;
+        pend = pend || fin;                                   // stored at the next refill
+        chain = fin ? 0 : chain - 2;
+#else
         // one candidate per walking lane, branch-free but for the rare long compare
         const bool live = chain > 0;
         const bool goes_on = nxt > limit && chain > 1;       // the walk continues after cur
@@ -1022,6 +1079,7 @@ __global__ __launch_bounds__(PM_THREADS) void k_dfl_match(DeflateArgs A, uint32_
         nxt = nn;
         pend = pend || fin;                                   // stored at the next refill
         chain = fin ? 0 : chain - 1;
+#endif
     }
 }
 
