@@ -1103,10 +1103,12 @@ __device__ __forceinline__ uint32_t tail_byte(const GLB uint8_t* in, int n, int 
     if (P < n) return in[P];
     return (off && P >= WINDOW_SIZE) ? in[P - W_SIZE] : 0u;          // stale half after the slide
 }
-// deflate.ts:827-946 at original position P (lookahead >= MIN_MATCH), from best_len = 2.
+// deflate.ts:827-946 at original position P (lookahead >= MIN_MATCH), from best_len = 2, for
+// chain_length and chain_length >> 2 in one walk: the shorter walk is the longer one's first
+// qchain candidates.  Record word as in k_dfl_match (quarter in the high half).
 // The window slides when the parse reaches P >= 65274 with lookahead < MIN_LOOKAHEAD
 // (deflate.ts:711-738, 1075); the search runs in the coordinates the reference has then.
-__device__ uint32_t tail_search(const GLB uint8_t* in, const GLB uint16_t* pv, int n, int P, int chain_length, int nice) {
+__device__ uint64_t tail_search(const GLB uint8_t* in, const GLB uint16_t* pv, int n, int P, int chain_length, int nice) {
     const int off = (P >= WINDOW_SIZE - MIN_LOOKAHEAD && n - P < MIN_LOOKAHEAD) ? W_SIZE : 0;
     const int strstart = P - off;
     auto rb = [&](int v) { return off ? (v >= W_SIZE ? v - W_SIZE : 0) : v; };
@@ -1115,25 +1117,30 @@ __device__ uint32_t tail_search(const GLB uint8_t* in, const GLB uint16_t* pv, i
     const int lookahead = n - P;
     if (nice > lookahead) nice = lookahead;
     const int limit = strstart > MAX_DIST ? strstart - MAX_DIST : 0;
-    int best = MIN_MATCH - 1, bstart = 0;
+    const int qchain = chain_length >> 2;
+    int best = MIN_MATCH - 1, bstart = 0, qbest = -1, qstart = 0, k = 0;
     uint32_t scan_end1 = tail_byte(in, n, off, strstart + best - 1), scan_end = tail_byte(in, n, off, strstart + best);
     const uint32_t c0 = tail_byte(in, n, off, strstart), c1 = tail_byte(in, n, off, strstart + 1);
     do {
         const int match = cur;
-        if (tail_byte(in, n, off, match + best) != scan_end || tail_byte(in, n, off, match + best - 1) != scan_end1 ||
-            tail_byte(in, n, off, match) != c0 || tail_byte(in, n, off, match + 1) != c1)
-            continue;
-        int len = 3;                          // byte 2 is not compared (equal hash, deflate.ts:891-897)
-        while (len < MAX_MATCH && tail_byte(in, n, off, strstart + len) == tail_byte(in, n, off, match + len)) ++len;
-        if (len > best) {
-            bstart = match;
-            best = len;
-            if (len >= nice) break;
-            scan_end1 = tail_byte(in, n, off, strstart + best - 1);
-            scan_end = tail_byte(in, n, off, strstart + best);
+        if (tail_byte(in, n, off, match + best) == scan_end && tail_byte(in, n, off, match + best - 1) == scan_end1 &&
+            tail_byte(in, n, off, match) == c0 && tail_byte(in, n, off, match + 1) == c1) {
+            int len = 3;                      // byte 2 is not compared (equal hash, deflate.ts:891-897)
+            while (len < MAX_MATCH && tail_byte(in, n, off, strstart + len) == tail_byte(in, n, off, match + len)) ++len;
+            if (len > best) {
+                bstart = match;
+                best = len;
+                if (len >= nice) break;
+                scan_end1 = tail_byte(in, n, off, strstart + best - 1);
+                scan_end = tail_byte(in, n, off, strstart + best);
+            }
         }
+        if (++k == qchain) { qbest = best; qstart = bstart; }
     } while ((cur = rb(pv[cur + off])) > limit && --chain_length != 0);
-    return best > MIN_MATCH - 1 ? ((uint32_t)best << 16) | (uint32_t)(strstart - bstart) : 0u;
+    if (qbest < 0) { qbest = best; qstart = bstart; }
+    const uint32_t full = best > MIN_MATCH - 1 ? ((uint32_t)best << 16) | (uint32_t)(strstart - bstart) : 0u;
+    const uint32_t quarter = qbest > MIN_MATCH - 1 ? ((uint32_t)qbest << 16) | (uint32_t)(strstart - qstart) : 0u;
+    return ((uint64_t)quarter << 32) | full;
 }
 __global__ __launch_bounds__(256) void k_dfl_tail(DeflateArgs A) {
     const uint32_t sid = blockIdx.x;
@@ -1145,11 +1152,7 @@ __global__ __launch_bounds__(256) void k_dfl_tail(DeflateArgs A) {
     const GLB uint16_t* pv = (const GLB uint16_t*)A.pv_buf + (uint64_t)sid * A.rec_stride;
     GLB uint64_t* rec = (GLB uint64_t*)A.rec_buf + (uint64_t)sid * A.rec_stride;
     const int max_chain = c_config[A.level][3], nice = c_config[A.level][2];
-    for (int P = tail + (int)threadIdx.x; P <= n - MIN_MATCH; P += 256) {
-        const uint32_t full = tail_search(in, pv, n, P, max_chain, nice);
-        const uint32_t quarter = tail_search(in, pv, n, P, max_chain >> 2, nice);
-        rec[P] = ((uint64_t)quarter << 32) | full;
-    }
+    for (int P = tail + (int)threadIdx.x; P <= n - MIN_MATCH; P += 256) rec[P] = tail_search(in, pv, n, P, max_chain, nice);
 }
 
 // k_dfl_parse: one lane per stream, the reference's loop with its scalars in registers.
