@@ -867,7 +867,7 @@ __global__ __launch_bounds__(64) void k_dfl_chain(DeflateArgs A) {
     if (in_len > A.rec_stride) return;
     const GLB uint8_t* in = (const GLB uint8_t*)(A.in + A.in_off[sid]);
     GLB uint16_t* pv = (GLB uint16_t*)A.pv_buf + (uint64_t)sid * A.rec_stride;
-    for (uint32_t i = lane; i < HASH_SIZE; i += 64) head[i] = 0;
+    for (uint32_t i = lane; i < HASH_SIZE / 4; i += 64) ((uint4*)head)[i] = make_uint4(0, 0, 0, 0);
     const uint32_t n = (uint32_t)in_len;
     uint32_t w[5];
     ch_load(in, n, 16 * lane, w);
@@ -886,12 +886,21 @@ __global__ __launch_bounds__(64) void k_dfl_chain(DeflateArgs A) {
             *(uint32_t*)&hs[16 * lane + q] = h2;
         }
         __syncthreads();
+        // all hash reads, then the 16 exchanges back to back (one wave's LDS operations run in
+        // order, so position order holds), then the stores: a few LDS round trips per chunk
+        uint32_t hv[CH_CHUNK / 64], old[CH_CHUNK / 64];
+#pragma unroll
+        for (uint32_t j = 0; j < CH_CHUNK / 64; ++j) hv[j] = hs[64 * j + lane];
+#pragma unroll
         for (uint32_t j = 0; j < CH_CHUNK / 64; ++j) {
             const uint32_t p = base + 64 * j + lane;
-            if (p >= n) break;
-            uint32_t old = 0;
-            if (p + 2 < n) old = atomicExch(&head[hs[64 * j + lane]], p);   // insert_string runs while lookahead >= 3
-            pv[p] = (uint16_t)old;
+            old[j] = 0;
+            if (p + 2 < n) old[j] = atomicExch(&head[hv[j]], p);   // insert_string runs while lookahead >= 3
+        }
+#pragma unroll
+        for (uint32_t j = 0; j < CH_CHUNK / 64; ++j) {
+            const uint32_t p = base + 64 * j + lane;
+            if (p < n) pv[p] = (uint16_t)old[j];
         }
         __syncthreads();
         for (int i = 0; i < 5; ++i) w[i] = wn[i];
