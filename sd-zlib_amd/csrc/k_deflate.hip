@@ -858,16 +858,31 @@ __device__ __forceinline__ void ch_load(const GLB uint8_t* in, uint32_t n, uint3
         }
     }
 }
-__global__ __launch_bounds__(64) void k_dfl_chain(DeflateArgs A) {
-    __shared__ uint32_t head[HASH_SIZE];                 // 128 KiB
-    __shared__ uint16_t hs[CH_CHUNK];
-    const uint32_t sid = blockIdx.x, lane = threadIdx.x;
+// Two streams share one block and one head table: wave w keeps its heads in half w of each
+// dword (positions < 2^16) and swaps them in with ds_mskor_rtn_b32, a masked exchange that,
+// like ds_wrxchg, serves same-address lanes in lane order.  That is two waves per CU where one
+// stream's 128 KiB table allowed one.  Each wave only syncs with itself.
+#define CH_WAVES 2
+__device__ __forceinline__ uint32_t lds_mskor_rtn(uint32_t* p, uint32_t mask, uint32_t v) {
+    uint32_t r;
+    const uint32_t a = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint32_t*)p;
+    asm volatile("ds_mskor_rtn_b32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(mask), "v"(v) : "memory");
+    return r;
+}
+__global__ __launch_bounds__(64 * CH_WAVES) void k_dfl_chain(DeflateArgs A) {
+    __shared__ __attribute__((aligned(16))) uint32_t head[HASH_SIZE];   // 128 KiB, a 16-bit half per wave
+    __shared__ uint16_t hsw[CH_WAVES][CH_CHUNK];
+    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+    const uint32_t sid = blockIdx.x * CH_WAVES + wv;
+    for (uint32_t i = threadIdx.x; i < HASH_SIZE / 4; i += 64 * CH_WAVES) ((uint4*)head)[i] = make_uint4(0, 0, 0, 0);
+    __syncthreads();
     if (sid >= A.n) return;
     const uint64_t in_len = A.in_len[sid];
     if (in_len > A.rec_stride) return;
     const GLB uint8_t* in = (const GLB uint8_t*)(A.in + A.in_off[sid]);
     GLB uint16_t* pv = (GLB uint16_t*)A.pv_buf + (uint64_t)sid * A.rec_stride;
-    for (uint32_t i = lane; i < HASH_SIZE / 4; i += 64) ((uint4*)head)[i] = make_uint4(0, 0, 0, 0);
+    uint16_t* hs = hsw[wv];
+    const uint32_t sh = 16u * wv, msk = 0xffffu << sh;
     const uint32_t n = (uint32_t)in_len;
     uint32_t w[5];
     ch_load(in, n, 16 * lane, w);
@@ -885,7 +900,9 @@ __global__ __launch_bounds__(64) void k_dfl_chain(DeflateArgs A) {
             }
             *(uint32_t*)&hs[16 * lane + q] = h2;
         }
-        __syncthreads();
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         // all hash reads, then the 16 exchanges back to back (one wave's LDS operations run in
         // order, so position order holds), then the stores: a few LDS round trips per chunk
         uint32_t hv[CH_CHUNK / 64], old[CH_CHUNK / 64];
@@ -895,14 +912,16 @@ __global__ __launch_bounds__(64) void k_dfl_chain(DeflateArgs A) {
         for (uint32_t j = 0; j < CH_CHUNK / 64; ++j) {
             const uint32_t p = base + 64 * j + lane;
             old[j] = 0;
-            if (p + 2 < n) old[j] = atomicExch(&head[hv[j]], p);   // insert_string runs while lookahead >= 3
+            if (p + 2 < n) old[j] = lds_mskor_rtn(&head[hv[j]], msk, p << sh);   // insert_string runs while lookahead >= 3
         }
 #pragma unroll
         for (uint32_t j = 0; j < CH_CHUNK / 64; ++j) {
             const uint32_t p = base + 64 * j + lane;
-            if (p < n) pv[p] = (uint16_t)old[j];
+            if (p < n) pv[p] = (uint16_t)(old[j] >> sh);
         }
-        __syncthreads();
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         for (int i = 0; i < 5; ++i) w[i] = wn[i];
     }
 }
@@ -1619,7 +1638,7 @@ void launch_deflate(const DeflateArgs& a, hipStream_t st) {
     hipLaunchKernelGGL(k_deflate_tables, dim3(1), dim3(1), 0, st);
     if (a.rec_buf && !c_config_host_fast(a.level)) {
         const uint32_t nseg = (a.rec_stride + PM_SEG - 1) / PM_SEG;
-        hipLaunchKernelGGL(k_dfl_chain, dim3(a.n), dim3(64), 0, st, a);
+        hipLaunchKernelGGL(k_dfl_chain, dim3((a.n + CH_WAVES - 1) / CH_WAVES), dim3(64 * CH_WAVES), 0, st, a);
         hipLaunchKernelGGL(k_dfl_match, dim3(a.n * nseg), dim3(PM_THREADS), 0, st, a, nseg);
         hipLaunchKernelGGL(k_dfl_tail, dim3(a.n), dim3(256), 0, st, a);
         hipLaunchKernelGGL(k_dfl_parse, grid, dim3(64), 0, st, a);
