@@ -1253,8 +1253,12 @@ __global__ __launch_bounds__(64) void k_dfl_parse(DeflateArgs A) {
         }
         const int P = strstart + off;                        // everything this step reads, at once
         const uint32_t v = pv[P];
-        const uint64_t r = rec[P];
+        uint64_t r = rec[P];
         const uint32_t lb = in[P > 0 ? P - 1 : 0];
+        // r is used only when this position is searched; pinning it here keeps its load next to
+        // the others instead of after the search test (which waits for pv): one memory round
+        // trip per step, not two
+        asm volatile("" : "+v"(r));
         if (lookahead >= MIN_MATCH) hash_head = off ? (v >= W_SIZE ? (int)v - W_SIZE : 0) : (int)v;
         const int prev_length = match_length, prev_match = match_start;
         match_length = MIN_MATCH - 1;

@@ -18,6 +18,7 @@ from bench import DeviceBatch, inflate_step, deflate_step  # noqa: E402
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--mode", default="inflate", choices=["inflate", "deflate"])
+    ap.add_argument("--same", action="store_true", help="deflate: one slice in every stream")
     ap.add_argument("--steps", type=int, default=2)
     ap.add_argument("--streams", type=int, default=65536)
     ap.add_argument("--level", type=int, default=6)
@@ -35,8 +36,14 @@ def main():
             print("inflate step %d: kernel %.3f ms (decode %.2f resolve %.2f), %.1f GB/s out"
                   % (i, ms, split[0][0], split[0][1], len(text) * args.streams / ms / 1e6), flush=True)
     else:
-        sl = text[:65536]
-        b = DeviceBatch(sdz, sl, args.streams, int(L.sdz_deflate_bound(65536, 1, 0)))
+        # the bench's C3 layout: 64 distinct slices of paradiselost.txt, cycled over the streams
+        # (identical streams would run the serial parse without any lane divergence)
+        offs = [(i * 65521) % (len(text) - 65536) for i in range(64)]
+        payloads = [text[o:o + 65536] for o in offs] if not args.same else [text[:65536]] * 64
+        b = DeviceBatch(sdz, payloads[0], args.streams, int(L.sdz_deflate_bound(65536, 1, 0)))
+        for i, pl in enumerate(payloads[1:], 1):
+            for j in range(i, args.streams, 64):
+                b.d_in.upload(pl, j * b.in_stride)
         for i in range(args.steps):
             ms = deflate_step(sdz, b, args.level, 1)
             print("deflate step %d: kernel %.3f ms, %.2f GB/s in" % (i, ms, 65536 * args.streams / ms / 1e6),
