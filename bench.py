@@ -135,8 +135,9 @@ def main():
                     help="streams for the deflate leg (64 KiB slices, L6); 0 disables")
     ap.add_argument("--deflate-steps", type=int, default=1)
     ap.add_argument("--copy-gib", type=float, default=4.0, help="device copy peak probe size; 0 disables")
-    ap.add_argument("--host-streams", type=int, default=2048,
-                    help="streams for the host-buffer (PCIe-inclusive) inflate probe; 0 disables")
+    ap.add_argument("--host-streams", type=int, default=0,
+                    help="streams for the host-buffer (PCIe-inclusive) inflate probe, e.g. 2048; off by "
+                         "default so that the rocprofv3 stats of the default command hold C2 launches only")
     args = ap.parse_args()
 
     import torch
