@@ -938,6 +938,9 @@ __global__ __launch_bounds__(64 * CH_WAVES) void k_dfl_chain(DeflateArgs A) {
 #ifndef PM_PAIR
 #define PM_PAIR 1                                       // two chain candidates per step
 #endif
+#ifndef PM_CHUNK
+#define PM_CHUNK 128                                    // positions a wave takes at a time
+#endif
 #ifndef PM_REFILL
 #define PM_REFILL 8                                     // idle lanes that trigger a refill
 #endif
@@ -950,8 +953,9 @@ __device__ __forceinline__ uint32_t pm_w4(const uint8_t* w, uint32_t x) {   // 4
 __global__ __launch_bounds__(PM_THREADS) void k_dfl_match(DeflateArgs A, uint32_t nseg) {
     __shared__ __attribute__((aligned(16))) uint8_t win[(PM_WINB + 15) & ~15];
     __shared__ __attribute__((aligned(16))) uint16_t pvl[PM_PV];
+    __shared__ int pm_next;                                 // first position not yet handed to a wave
     const uint32_t sid = blockIdx.x / nseg, seg = blockIdx.x % nseg, tid = threadIdx.x;
-    const uint32_t wv = tid >> 6;
+    const uint32_t lane = tid & 63u, wv = tid >> 6;
     if (sid >= A.n) return;
     const uint64_t in_len = A.in_len[sid];
     if (in_len > A.rec_stride) return;
@@ -976,14 +980,17 @@ __global__ __launch_bounds__(PM_THREADS) void k_dfl_match(DeflateArgs A, uint32_
         uint32_t* p32 = (uint32_t*)pvl;
         for (int i = (int)tid; i < np; i += PM_THREADS) p32[i] = *(const GLB uint32_t*)(pv + ws + 2 * i);
         for (int i = 2 * np + (int)tid; i < s1 - ws; i += PM_THREADS) pvl[i] = pv[ws + i];
+        if (tid == 0) pm_next = s0 + (PM_THREADS / 64) * PM_CHUNK;
     }
     __syncthreads();
     GLB uint64_t* rec = (GLB uint64_t*)A.rec_buf + (uint64_t)sid * A.rec_stride;
     const int max_chain = c_config[A.level][3], qchain = max_chain >> 2, nice = c_config[A.level][2];
-    // this wave's positions
-    const int per = (s1 - s0 + PM_THREADS / 64 - 1) / (PM_THREADS / 64);
-    const int q0 = s0 + (int)wv * per, q1 = q0 + per < s1 ? q0 + per : s1;
-    int next = q0;                                          // wave-uniform queue head
+    // Positions in chunks of PM_CHUNK: each wave starts on its own chunk and takes the next
+    // free one from an LDS counter when it has handed out its last position, so waves whose
+    // positions have long chains do not hold up the workgroup.
+    const int c0 = s0 + (int)wv * PM_CHUNK;
+    int next = c0 < s1 ? c0 : s1;                           // wave-uniform queue head
+    int q1 = c0 + PM_CHUNK < s1 ? c0 + PM_CHUNK : s1;
     // A lane walks while chain > 0 (chain counts the candidates left); a finished lane keeps
     // its results (pend) until the next refill stores them.  The quarter walk ends at the
     // step where chain == cq, i.e. after qchain candidates.
@@ -1006,6 +1013,13 @@ __global__ __launch_bounds__(PM_THREADS) void k_dfl_match(DeflateArgs A, uint32_
                 const uint32_t quarter = qbest > MIN_MATCH - 1 ? ((uint32_t)qbest << 16) | (uint32_t)(p - qpos) : 0u;
                 rec[p] = ((uint64_t)quarter << 32) | full;
                 pend = false;
+            }
+            if (next >= q1) {                               // chunk handed out: take another
+                const int b = __builtin_amdgcn_readfirstlane(lane == 0 ? atomicAdd(&pm_next, PM_CHUNK) : 0);
+                if (b < s1) {
+                    next = b;
+                    q1 = b + PM_CHUNK < s1 ? b + PM_CHUNK : s1;
+                }
             }
             if (next >= q1 && nidle == 64) break;
             if (next < q1) {
