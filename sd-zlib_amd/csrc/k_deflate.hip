@@ -1220,12 +1220,11 @@ __global__ __launch_bounds__(64) void k_dfl_parse(DeflateArgs A) {
     if (in_len == 0 || in_len > A.rec_stride) { F->nblk = 0; F->flag = 1; return; }
     const int n = (int)in_len;
     const GLB uint8_t* in = (const GLB uint8_t*)(A.in + A.in_off[sid]);
-    const GLB uint16_t* pv = (const GLB uint16_t*)A.pv_buf + (uint64_t)sid * A.rec_stride;
     const GLB uint64_t* rec = (const GLB uint64_t*)A.rec_buf + (uint64_t)sid * A.rec_stride;
     GLB uint32_t* sym = (GLB uint32_t*)A.rec_buf + (uint64_t)sid * A.rec_stride * 2;
     const int level = A.level, good = c_config[level][0], max_lazy = c_config[level][1];
     int strstart = 0, lookahead = n, match_length = MIN_MATCH - 1, match_start = 0, match_available = 0;
-    int block_start = 0, off = 0, hash_head = 0;
+    int block_start = 0, off = 0;
     uint32_t last_lit = 0, matches = 0, lx = 0, nblk = 0, sym0 = 0;
     auto tally = [&](int dist, int lc) -> bool {             // _tr_tally, deflate.ts:488-524
         sym[lx++] = (uint32_t)lc | ((uint32_t)dist << 8);
@@ -1266,18 +1265,19 @@ __global__ __launch_bounds__(64) void k_dfl_parse(DeflateArgs A) {
             if (lookahead == 0) break;
         }
         const int P = strstart + off;                        // everything this step reads, at once
-        const uint32_t v = pv[P];
         uint64_t r = rec[P];
         const uint32_t lb = in[P > 0 ? P - 1 : 0];
         // r is used only when this position is searched; pinning it here keeps its load next to
-        // the others instead of after the search test (which waits for pv): one memory round
-        // trip per step, not two
+        // the other one: one memory round trip per step
         asm volatile("" : "+v"(r));
-        if (lookahead >= MIN_MATCH) hash_head = off ? (v >= W_SIZE ? (int)v - W_SIZE : 0) : (int)v;
         const int prev_length = match_length, prev_match = match_start;
         match_length = MIN_MATCH - 1;
-        if (lookahead >= MIN_MATCH && hash_head != 0 && prev_length < max_lazy &&
-            ((strstart - hash_head) & 0xffff) <= MAX_DIST) {
+        // The reference also requires hash_head != 0 and (strstart - hash_head) <= MAX_DIST
+        // (deflate.ts:1092).  Where that fails the record is 0 (k_dfl_match / k_dfl_tail test
+        // the same), and a 0 record gives the step the same outcome as no search: match_length
+        // ends <= prev_length, so with prev_length >= MIN_MATCH the previous match is emitted
+        // either way, and otherwise it stays MIN_MATCH - 1.  So the link load is not needed.
+        if (lookahead >= MIN_MATCH && prev_length < max_lazy) {
             const uint32_t e = prev_length >= good ? (uint32_t)(r >> 32) : (uint32_t)r;
             const int len = (int)(e >> 16);
             int ml = prev_length;
@@ -1289,10 +1289,9 @@ __global__ __launch_bounds__(64) void k_dfl_parse(DeflateArgs A) {
         if (prev_length >= MIN_MATCH && match_length <= prev_length) {
             const bool bflush = tally(strstart - 1 - prev_match, prev_length - MIN_MATCH);
             lookahead -= prev_length - 1;
-            // strstart+1 .. strstart+prev_length-2 are inserted (up to max_insert).  The last
-            // insertion's hash_head is never read: the next step reads hash_head only with
-            // lookahead >= MIN_MATCH, and then sets it from its own position first.  So the
-            // record path skips that load (a memory round trip per match).
+            // strstart+1 .. strstart+prev_length-2 are inserted (up to max_insert); their links
+            // are already in the chain buffer (k_dfl_chain), and the records carry the search
+            // test, so nothing is read here
             const int last = strstart + prev_length - 2;
             strstart = last + 1;
             match_available = 0;
