@@ -946,6 +946,13 @@ __global__ __launch_bounds__(64 * CH_WAVES) void k_dfl_chain(DeflateArgs A) {
 #endif
 #define PM_WINB (W_SIZE + PM_SEG + MAX_MATCH + 16)     // staged window bytes
 #define PM_PV (W_SIZE + PM_SEG)                         // staged links
+// record word of position p: the full-chain result (len << 16 | dist) in the low half, the
+// quarter-chain result in the high half, and input byte p - 1 (the literal the parse emits
+// from there) in bits 25-31 of the low half and bit 25 of the high half: the parse then
+// needs one load per step
+__device__ __forceinline__ uint64_t rec_word(uint32_t full, uint32_t quarter, uint32_t lb) {
+    return ((uint64_t)(quarter | ((lb >> 7) << 25)) << 32) | (full | ((lb & 127u) << 25));
+}
 __device__ __forceinline__ uint32_t pm_w4(const uint8_t* w, uint32_t x) {   // 4 bytes at x, aligned reads
     const uint32_t* w32 = (const uint32_t*)w;
     return __builtin_amdgcn_alignbyte(w32[(x >> 2) + 1], w32[x >> 2], x & 3u);
@@ -1011,7 +1018,7 @@ __global__ __launch_bounds__(PM_THREADS) void k_dfl_match(DeflateArgs A, uint32_
                 if (qbest < 0) { qbest = best; qpos = bpos; }
                 const uint32_t full = best > MIN_MATCH - 1 ? ((uint32_t)best << 16) | (uint32_t)(p - bpos) : 0u;
                 const uint32_t quarter = qbest > MIN_MATCH - 1 ? ((uint32_t)qbest << 16) | (uint32_t)(p - qpos) : 0u;
-                rec[p] = ((uint64_t)quarter << 32) | full;
+                rec[p] = rec_word(full, quarter, win[p > 0 ? p - 1 - ws : 0]);
                 pend = false;
             }
             if (next >= q1) {                               // chunk handed out: take another
@@ -1188,13 +1195,17 @@ __global__ __launch_bounds__(256) void k_dfl_tail(DeflateArgs A) {
     const uint32_t sid = blockIdx.x;
     if (sid >= A.n) return;
     const uint64_t in_len = A.in_len[sid];
-    if (in_len > A.rec_stride || in_len < MIN_MATCH) return;
+    if (in_len > A.rec_stride) return;
     const int n = (int)in_len, tail = n > PM_TAIL ? n - PM_TAIL : 0;
     const GLB uint8_t* in = (const GLB uint8_t*)(A.in + A.in_off[sid]);
     const GLB uint16_t* pv = (const GLB uint16_t*)A.pv_buf + (uint64_t)sid * A.rec_stride;
     GLB uint64_t* rec = (GLB uint64_t*)A.rec_buf + (uint64_t)sid * A.rec_stride;
     const int max_chain = c_config[A.level][3], nice = c_config[A.level][2];
-    for (int P = tail + (int)threadIdx.x; P <= n - MIN_MATCH; P += 256) rec[P] = tail_search(in, pv, n, P, max_chain, nice);
+    // the last MIN_MATCH - 1 positions are not searched; their records carry only the byte
+    for (int P = tail + (int)threadIdx.x; P < n; P += 256) {
+        const uint64_t r = P <= n - MIN_MATCH ? tail_search(in, pv, n, P, max_chain, nice) : 0ull;
+        rec[P] = rec_word((uint32_t)r, (uint32_t)(r >> 32), in[P > 0 ? P - 1 : 0]);
+    }
 }
 
 // k_dfl_parse: one lane per stream, the reference's loop with its scalars in registers.
@@ -1265,11 +1276,9 @@ __global__ __launch_bounds__(64) void k_dfl_parse(DeflateArgs A) {
             if (lookahead == 0) break;
         }
         const int P = strstart + off;                        // everything this step reads, at once
-        uint64_t r = rec[P];
-        const uint32_t lb = in[P > 0 ? P - 1 : 0];
-        // r is used only when this position is searched; pinning it here keeps its load next to
-        // the other one: one memory round trip per step
-        asm volatile("" : "+v"(r));
+        uint64_t r = rec[P];                                  // the step's one load (rec_word)
+        asm volatile("" : "+v"(r));                           // here, not sunk into the branches
+        const uint32_t lb = ((uint32_t)r >> 25) | (((uint32_t)(r >> 32) >> 18) & 128u);
         const int prev_length = match_length, prev_match = match_start;
         match_length = MIN_MATCH - 1;
         // The reference also requires hash_head != 0 and (strstart - hash_head) <= MAX_DIST
@@ -1279,7 +1288,7 @@ __global__ __launch_bounds__(64) void k_dfl_parse(DeflateArgs A) {
         // either way, and otherwise it stays MIN_MATCH - 1.  So the link load is not needed.
         if (lookahead >= MIN_MATCH && prev_length < max_lazy) {
             const uint32_t e = prev_length >= good ? (uint32_t)(r >> 32) : (uint32_t)r;
-            const int len = (int)(e >> 16);
+            const int len = (int)((e >> 16) & 511u);
             int ml = prev_length;
             if (len > prev_length) { ml = len; match_start = strstart - (int)(e & 0xffffu); }
             match_length = ml < lookahead ? ml : lookahead;
