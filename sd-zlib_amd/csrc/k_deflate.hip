@@ -935,9 +935,6 @@ __global__ __launch_bounds__(64 * CH_WAVES) void k_dfl_chain(DeflateArgs A) {
 // MIN_MATCH - 1) -- chain max_chain in the low word, max_chain >> 2 in the high word.
 #define PM_SEG 16384
 #define PM_THREADS 1024
-#ifndef PM_PAIR
-#define PM_PAIR 1                                       // two chain candidates per step
-#endif
 #ifndef PM_CHUNK
 #define PM_CHUNK 128                                    // positions a wave takes at a time
 #endif
@@ -985,8 +982,18 @@ __global__ __launch_bounds__(PM_THREADS) void k_dfl_match(DeflateArgs A, uint32_
         for (int i = 4 * nw + (int)tid; i < we - ws; i += PM_THREADS) win[i] = in[ws + i];
         const int np = (s1 - ws) >> 1;                     // link pairs (ws even)
         uint32_t* p32 = (uint32_t*)pvl;
-        for (int i = (int)tid; i < np; i += PM_THREADS) p32[i] = *(const GLB uint32_t*)(pv + ws + 2 * i);
-        for (int i = 2 * np + (int)tid; i < s1 - ws; i += PM_THREADS) pvl[i] = pv[ws + i];
+        // links are staged relative to ws (0 for none, or at or below ws: below every walk's
+        // limit, and never a searchable head), so the walk indexes LDS with them directly
+        const uint32_t wsu = (uint32_t)ws;
+        for (int i = (int)tid; i < np; i += PM_THREADS) {
+            const uint32_t v = *(const GLB uint32_t*)(pv + ws + 2 * i);
+            const uint32_t lo = v & 0xffffu, hi = v >> 16;
+            p32[i] = (lo > wsu ? lo - wsu : 0u) | ((hi > wsu ? hi - wsu : 0u) << 16);
+        }
+        for (int i = 2 * np + (int)tid; i < s1 - ws; i += PM_THREADS) {
+            const uint32_t v = pv[ws + i];
+            pvl[i] = (uint16_t)(v > wsu ? v - wsu : 0u);
+        }
         if (tid == 0) pm_next = s0 + (PM_THREADS / 64) * PM_CHUNK;
     }
     __syncthreads();
@@ -1004,8 +1011,9 @@ __global__ __launch_bounds__(PM_THREADS) void k_dfl_match(DeflateArgs A, uint32_
     bool pend = false;
     const int cq = max_chain - qchain + 1;
     // cur: this step's candidate; nxt: the link after it (read a step ahead, so the chain
-    // link of a step does not wait on the previous one)
-    int p = s0, cur = 0, nxt = 0, best = 0, bpos = 0, qbest = 0, qpos = 0, chain = 0, limit = 0;
+    // link of a step does not wait on the previous one).  cur, nxt, bpos, qpos, limit and sp
+    // (the position itself) are relative to ws; p is absolute.
+    int p = s0, sp = 0, cur = 0, nxt = 0, best = 0, bpos = 0, qbest = 0, qpos = 0, chain = 0, limit = 0;
     uint32_t s4 = 0;
     for (;;) {
         // Idle lanes store their records and take the next positions once PM_REFILL lanes
@@ -1016,9 +1024,9 @@ __global__ __launch_bounds__(PM_THREADS) void k_dfl_match(DeflateArgs A, uint32_
         if (nidle >= PM_REFILL || nidle == 64) {
             if (pend) {
                 if (qbest < 0) { qbest = best; qpos = bpos; }
-                const uint32_t full = best > MIN_MATCH - 1 ? ((uint32_t)best << 16) | (uint32_t)(p - bpos) : 0u;
-                const uint32_t quarter = qbest > MIN_MATCH - 1 ? ((uint32_t)qbest << 16) | (uint32_t)(p - qpos) : 0u;
-                rec[p] = rec_word(full, quarter, win[p > 0 ? p - 1 - ws : 0]);
+                const uint32_t full = best > MIN_MATCH - 1 ? ((uint32_t)best << 16) | (uint32_t)(sp - bpos) : 0u;
+                const uint32_t quarter = qbest > MIN_MATCH - 1 ? ((uint32_t)qbest << 16) | (uint32_t)(sp - qpos) : 0u;
+                rec[p] = rec_word(full, quarter, win[p > 0 ? sp - 1 : 0]);
                 pend = false;
             }
             if (next >= q1) {                               // chunk handed out: take another
@@ -1035,19 +1043,18 @@ __global__ __launch_bounds__(PM_THREADS) void k_dfl_match(DeflateArgs A, uint32_
                 next += nidle;
                 if (chain <= 0 && pn < q1) {
                     p = pn;
-                    const uint32_t sp = (uint32_t)(p - ws);
+                    sp = p - ws;
                     cur = pvl[sp];                              // hash_head
                     best = MIN_MATCH - 1; bpos = 0; qbest = -1;
-                    limit = p > MAX_DIST ? p - MAX_DIST : 0;
-                    s4 = pm_w4(win, sp);
-                    const bool search = cur != 0 && p - cur <= MAX_DIST;   // deflate.ts:1092
+                    limit = (p > MAX_DIST ? p - MAX_DIST : 0) - ws;   // >= 0
+                    s4 = pm_w4(win, (uint32_t)sp);
+                    const bool search = cur != 0 && sp - cur <= MAX_DIST;  // deflate.ts:1092
                     chain = search ? max_chain : 0;
                     pend = !search;                             // no search: record 0
-                    nxt = pvl[(uint32_t)((search ? cur : p) - ws)];
+                    nxt = pvl[search ? cur : sp];
                 }
             }
         }
-#if PM_PAIR
         // two candidates per walking lane and step: cur (c1) and nxt (c2).  Both pass the
         // reference's pre-check against the step's starting best: a candidate that beats the
         // best after c1 also beats that, so the check only filters (deflate.ts:866-882), and
@@ -1056,13 +1063,12 @@ __global__ __launch_bounds__(PM_THREADS) void k_dfl_match(DeflateArgs A, uint32_
         const bool live = chain > 0;
         const bool go1 = nxt > limit && chain > 1;           // the walk continues after c1
         const bool l2 = live && go1;                          // c2 is walked (unless nice at c1)
-        const uint32_t sp = (uint32_t)(p - ws);
-        const uint32_t c1 = (uint32_t)((live ? cur : p) - ws), c2 = (uint32_t)((l2 ? nxt : p) - ws);
+        const uint32_t c1 = (uint32_t)(live ? cur : sp), c2 = (uint32_t)(l2 ? nxt : sp);
         const int c3 = pvl[c2];
         const uint32_t sb = win[sp + best], wb1 = win[c1 + best], wb2 = win[c2 + best];
         uint32_t x1 = pm_w4(win, c1) ^ s4, x2 = pm_w4(win, c2) ^ s4;
         const bool go2 = c3 > limit && chain > 2;            // ... and after c2
-        const int c4 = pvl[(uint32_t)((l2 && go2 ? c3 : p) - ws)];
+        const int c4 = pvl[l2 && go2 ? c3 : sp];
         const bool cand1 = live && wb1 == sb, cand2 = l2 && wb2 == sb;
         int len1 = x1 ? (int)(__builtin_ctz(x1) >> 3) : 4;
         int len2 = x2 ? (int)(__builtin_ctz(x2) >> 3) : 4;
@@ -1100,35 +1106,6 @@ __global__ __launch_bounds__(PM_THREADS) void k_dfl_match(DeflateArgs A, uint32_
         nxt = c4;
         pend = pend || fin;                                   // stored at the next refill
         chain = fin ? 0 : chain - 2;
-#else
-        // one candidate per walking lane, branch-free but for the rare long compare
-        const bool live = chain > 0;
-        const bool goes_on = nxt > limit && chain > 1;       // the walk continues after cur
-        const uint32_t cp = (uint32_t)((live ? cur : p) - ws), sp = (uint32_t)(p - ws);
-        const uint32_t wb = win[cp + best], sb = win[sp + best];
-        uint32_t x = pm_w4(win, cp) ^ s4;
-        const int nn = pvl[(uint32_t)((live && goes_on ? nxt : p) - ws)];
-        const bool cand = live && wb == sb;                  // can beat best (deflate.ts:866-882)
-        int len = x ? (int)(__builtin_ctz(x) >> 3) : 4;
-        bool more = cand && x == 0;
-        while (__ballot(more)) {                             // matches of more than 4 bytes
-            x = more ? pm_w4(win, cp + (uint32_t)len) ^ pm_w4(win, sp + (uint32_t)len) : 1u;
-            len += more ? (x ? (int)(__builtin_ctz(x) >> 3) : 4) : 0;
-            more = more && x == 0 && len < MAX_MATCH;
-        }
-        len = len > MAX_MATCH ? MAX_MATCH : len;
-        const bool upd = cand && len > best;
-        best = upd ? len : best;
-        bpos = upd ? cur : bpos;
-        const bool cap = live && chain == cq;
-        qbest = cap ? best : qbest;
-        qpos = cap ? bpos : qpos;
-        const bool fin = live && ((upd && len >= nice) || !goes_on);
-        cur = nxt;
-        nxt = nn;
-        pend = pend || fin;                                   // stored at the next refill
-        chain = fin ? 0 : chain - 1;
-#endif
     }
 }
 
