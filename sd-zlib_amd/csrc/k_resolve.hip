@@ -373,12 +373,19 @@ __global__ __launch_bounds__(RS_THREADS) __attribute__((amdgpu_waves_per_eu(RS_W
     // the window: output bytes [pos0 - 32 KiB, pos0), the dictionary / zeros before 0
     const uint32_t rp0 = (uint32_t)(pos0 % RS_R);
     const uint32_t pm0 = (uint32_t)(pos0 % 65521u);
-    for (uint32_t k = tid; k < RS_WIN; k += RS_THREADS) {
-        const int64_t p = (int64_t)pos0 - RS_WIN + k;
-        uint32_t b = 0;
-        if (p >= 0) b = round ? out[p] : 0u;
-        else if (p >= -dl) b = dict[dl + p];
-        ring[ridx((int32_t)rp0 - RS_WIN + (int32_t)k)] = (uint8_t)b;
+    if (pos0 == 0 && dl == 0) {
+        // a stream's first round without a dictionary: zeros, ring bytes [RS_R - RS_WIN, RS_R)
+        static_assert((RS_R - RS_WIN) % 16 == 0, "ring window start must be 16-aligned");
+        for (uint32_t k = tid; k < RS_WIN / 16; k += RS_THREADS)
+            ((uint4*)(ring + (RS_R - RS_WIN)))[k] = make_uint4(0, 0, 0, 0);
+    } else {
+        for (uint32_t k = tid; k < RS_WIN; k += RS_THREADS) {
+            const int64_t p = (int64_t)pos0 - RS_WIN + k;
+            uint32_t b = 0;
+            if (p >= 0) b = round ? out[p] : 0u;
+            else if (p >= -dl) b = dict[dl + p];
+            ring[ridx((int32_t)rp0 - RS_WIN + (int32_t)k)] = (uint8_t)b;
+        }
     }
     if (tid == 0) { chain = 0xffffffff00000000ull; wf = 0; wwb = 0; fail = 0; edone = 0; }
     for (uint32_t k = tid; k < RS_BM / 4; k += RS_THREADS) ((uint32_t*)fmap)[k] = 0;
