@@ -1147,12 +1147,29 @@ __device__ uint64_t tail_search(const GLB uint8_t* in, const GLB uint16_t* pv, i
     int best = MIN_MATCH - 1, bstart = 0, qbest = -1, qstart = 0, k = 0;
     uint32_t scan_end1 = tail_byte(in, n, off, strstart + best - 1), scan_end = tail_byte(in, n, off, strstart + best);
     const uint32_t c0 = tail_byte(in, n, off, strstart), c1 = tail_byte(in, n, off, strstart + 1);
+    // The link and the four checked bytes of a candidate are loaded together, and a long
+    // compare takes 4 byte pairs per step, so the walk waits on one memory round trip per
+    // candidate rather than on one per load.
     do {
         const int match = cur;
-        if (tail_byte(in, n, off, match + best) == scan_end && tail_byte(in, n, off, match + best - 1) == scan_end1 &&
-            tail_byte(in, n, off, match) == c0 && tail_byte(in, n, off, match + 1) == c1) {
+        const int nx = rb(pv[cur + off]);
+        const uint32_t e0 = tail_byte(in, n, off, match + best), e1 = tail_byte(in, n, off, match + best - 1);
+        const uint32_t m0 = tail_byte(in, n, off, match), m1 = tail_byte(in, n, off, match + 1);
+        if ((e0 == scan_end) & (e1 == scan_end1) & (m0 == c0) & (m1 == c1)) {
             int len = 3;                      // byte 2 is not compared (equal hash, deflate.ts:891-897)
-            while (len < MAX_MATCH && tail_byte(in, n, off, strstart + len) == tail_byte(in, n, off, match + len)) ++len;
+            for (bool go = true; go && len < MAX_MATCH;) {
+                uint32_t a[4], b[4];
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    a[i] = tail_byte(in, n, off, strstart + len + i);
+                    b[i] = tail_byte(in, n, off, match + len + i);
+                }
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    if (go && len < MAX_MATCH && a[i] == b[i]) ++len;
+                    else go = false;
+                }
+            }
             if (len > best) {
                 bstart = match;
                 best = len;
@@ -1162,7 +1179,8 @@ __device__ uint64_t tail_search(const GLB uint8_t* in, const GLB uint16_t* pv, i
             }
         }
         if (++k == qchain) { qbest = best; qstart = bstart; }
-    } while ((cur = rb(pv[cur + off])) > limit && --chain_length != 0);
+        cur = nx;
+    } while (cur > limit && --chain_length != 0);
     if (qbest < 0) { qbest = best; qstart = bstart; }
     const uint32_t full = best > MIN_MATCH - 1 ? ((uint32_t)best << 16) | (uint32_t)(strstart - bstart) : 0u;
     const uint32_t quarter = qbest > MIN_MATCH - 1 ? ((uint32_t)qbest << 16) | (uint32_t)(strstart - qstart) : 0u;
