@@ -142,7 +142,12 @@ uint64_t sdz_deflate_bound(uint64_t in_len, int32_t format, uint32_t fname_len);
 
 /* adler32(src, seed = 1) / crc32(src, seed = 0): adler32.ts:17-24 (including the
  * adler32.ts:67 NMAX quirk) and crc32.ts:17-23.  Signed int32 results.  Run on
- * the GPU (host buffer copied in). */
+ * the GPU (host buffer copied in).  The *_checked forms return SDZ_API_OK or an
+ * error code (message in sdz_last_error()) and write the checksum to *result; the
+ * plain forms return 0 on failure (0 is also a valid checksum: bindings use the
+ * checked forms and throw). */
+int sdz_adler32_checked(const uint8_t* buf, size_t len, int32_t seed, int32_t* result);
+int sdz_crc32_checked(const uint8_t* buf, size_t len, int32_t seed, int32_t* result);
 int32_t sdz_adler32(const uint8_t* buf, size_t len, int32_t seed);
 int32_t sdz_crc32(const uint8_t* buf, size_t len, int32_t seed);
 
@@ -168,6 +173,9 @@ int sdz_copy_to_host(void* dst, const void* src, uint64_t bytes);
 int sdz_memset_device(void* dst, int value, uint64_t bytes);
 int sdz_copy_device_to_device(void* dst, const void* src, uint64_t bytes);
 int sdz_sync(void* stream);
+/* a non-blocking hipStream_t (as void*) for the *_device calls; NULL on failure */
+void* sdz_stream_create(void);
+int sdz_stream_destroy(void* stream);
 
 /* Kernel timing: when enabled, *_device calls record HIP events on their launch
  * stream around the codec kernel(s); sdz_last_kernel_ms() waits for the stop

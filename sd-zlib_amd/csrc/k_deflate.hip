@@ -1638,15 +1638,13 @@ __global__ void k_max_u64(const uint64_t* v, uint32_t n, unsigned long long* out
     for (int o = 32; o > 0; o >>= 1) { unsigned long long x = __shfl_xor(m, o); m = x > m ? x : m; }
     if ((threadIdx.x & 63) == 0) atomicMax(out, m);
 }
-int device_max_u64(const uint64_t* v, uint32_t n, uint64_t* out, hipStream_t st) {
-    unsigned long long* d = nullptr;
-    if (hipMalloc(&d, sizeof *d) != hipSuccess) return -1;
-    bool ok = hipMemsetAsync(d, 0, sizeof *d, st) == hipSuccess;
-    hipLaunchKernelGGL(k_max_u64, dim3(64), dim3(256), 0, st, v, n, d);
+int device_max_u64(const uint64_t* v, uint32_t n, unsigned long long* d_slot, uint64_t* out, hipStream_t st) {
+    bool ok = hipMemsetAsync(d_slot, 0, sizeof *d_slot, st) == hipSuccess;
+    hipLaunchKernelGGL(k_max_u64, dim3(64), dim3(256), 0, st, v, n, d_slot);
     unsigned long long h = 0;
-    ok = ok && hipMemcpyAsync(&h, d, sizeof h, hipMemcpyDeviceToHost, st) == hipSuccess;
+    ok = ok && hipGetLastError() == hipSuccess;
+    ok = ok && hipMemcpyAsync(&h, d_slot, sizeof h, hipMemcpyDeviceToHost, st) == hipSuccess;
     ok = ok && hipStreamSynchronize(st) == hipSuccess;
-    ok = hipFree(d) == hipSuccess && ok;
     *out = h;
     return ok ? 0 : -1;
 }

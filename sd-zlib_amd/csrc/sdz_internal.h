@@ -73,8 +73,8 @@ struct DeflateArgs {
 uint64_t deflate_state_bytes();
 void launch_deflate(const DeflateArgs& a, hipStream_t s);
 constexpr uint32_t kDeflateRecMax = 65536;   // longest input on the record path
-// max of n device-resident u64 values (blocking; for scratch sizing)
-int device_max_u64(const uint64_t* v, uint32_t n, uint64_t* out, hipStream_t s);
+// max of n device-resident u64 values (blocking; for scratch sizing); d_slot: 8 device bytes
+int device_max_u64(const uint64_t* v, uint32_t n, unsigned long long* d_slot, uint64_t* out, hipStream_t s);
 
 void launch_checksum(const uint8_t* in, const uint64_t* in_off, const uint64_t* in_len,
                      const int32_t* seed, int32_t* result, uint32_t n, int kind, hipStream_t s);

@@ -49,34 +49,69 @@ int ensure_device() {
     return SDZ_API_OK;
 }
 
-// grow-only device scratch, one per (device, purpose)
+// Grow-only device scratch, one allocation per (purpose, device).  The *_device entry
+// points are asynchronous on the caller's stream, so a pool is stream-ordered: get()
+// makes the caller's stream wait for the event recorded after the pool's previous use
+// (on whatever stream that was), and done() records that event once this call's work
+// is enqueued.  Callers hold g_mu between get() and done().
 struct Pool {
-    void* p = nullptr;
-    size_t cap = 0;
-    int dev = -1;
-    int get(size_t bytes, void** out) {
+    struct Slot {
+        void* p = nullptr;
+        size_t cap = 0;
+        hipEvent_t ev = nullptr;      // recorded after the last enqueued use
+        bool pending = false;
+    };
+    std::vector<Slot> slots;          // indexed by device id
+    Slot* cur = nullptr;
+    int get(size_t bytes, hipStream_t s, void** out) {
         int d = 0;
-        hipGetDevice(&d);
-        if (p && (cap < bytes || dev != d)) {
-            int cur = d;
-            hipSetDevice(dev);
-            hipFree(p);
-            hipSetDevice(cur);
-            p = nullptr;
-            cap = 0;
+        HIPCHK(hipGetDevice(&d));
+        if ((size_t)d >= slots.size()) slots.resize((size_t)d + 1);
+        Slot& S = slots[(size_t)d];
+        if (!S.ev) HIPCHK(hipEventCreateWithFlags(&S.ev, hipEventDisableTiming));
+        if (S.p && S.cap < bytes) {
+            if (S.pending) HIPCHK(hipEventSynchronize(S.ev));
+            HIPCHK(hipFree(S.p));
+            S.p = nullptr;
+            S.cap = 0;
+            S.pending = false;
         }
-        if (!p) {
+        if (!S.p) {
             size_t want = std::max(bytes, (size_t)1 << 20);
-            hipError_t e = hipMalloc(&p, want);
-            if (e != hipSuccess) { p = nullptr; return hip_fail(e, "hipMalloc(scratch)"); }
-            cap = want;
-            dev = d;
+            hipError_t e = hipMalloc(&S.p, want);
+            if (e != hipSuccess) { S.p = nullptr; return hip_fail(e, "hipMalloc(scratch)"); }
+            S.cap = want;
         }
-        *out = p;
+        if (S.pending) HIPCHK(hipStreamWaitEvent(s, S.ev, 0));
+        cur = &S;
+        *out = S.p;
+        return SDZ_API_OK;
+    }
+    int done(hipStream_t s) {
+        if (!cur) return SDZ_API_OK;
+        Slot& S = *cur;
+        cur = nullptr;
+        HIPCHK(hipEventRecord(S.ev, s));
+        S.pending = true;
         return SDZ_API_OK;
     }
 };
-Pool g_inflate_scratch, g_deflate_state, g_tmp;
+Pool g_inflate_scratch, g_deflate_state, g_tmp, g_stage;
+constexpr size_t kTmpFname = 256;     // g_tmp layout: [0, 256) small results, then the file name
+
+// records the pool's event on every exit path once get() succeeded
+struct PoolUse {
+    Pool& pool;
+    hipStream_t s;
+    bool held = false;
+    PoolUse(Pool& p, hipStream_t st) : pool(p), s(st) {}
+    int get(size_t bytes, void** out) {
+        int rc = pool.get(bytes, s, out);
+        held = rc == SDZ_API_OK;
+        return rc;
+    }
+    ~PoolUse() { if (held) pool.done(s); }
+};
 
 void timing_begin(hipStream_t s) {
     if (!g_timing) return;
@@ -115,19 +150,23 @@ const char* const kZmsg[ZM_COUNT] = {
 int device_checksum(const uint8_t* d_buf, uint64_t len, int kind, int32_t seed, int32_t* out,
                     hipStream_t s) {
     void* tmp = nullptr;
-    int rc = g_tmp.get(64, &tmp);
-    if (rc) return rc;
+    if (int rc = g_tmp.get(kTmpFname, s, &tmp)) return rc;
     uint64_t* d_off = (uint64_t*)tmp;
     uint64_t* d_len = d_off + 1;
     int32_t* d_seed = (int32_t*)(d_off + 2);
     int32_t* d_res = d_seed + 1;
-    uint64_t hv[2] = { 0, len };
-    HIPCHK(hipMemcpyAsync(d_off, hv, sizeof hv, hipMemcpyHostToDevice, s));
-    HIPCHK(hipMemcpyAsync(d_seed, &seed, sizeof seed, hipMemcpyHostToDevice, s));
-    launch_checksum(d_buf, d_off, d_len, d_seed, d_res, 1, kind, s);
-    HIPCHK(hipGetLastError());
-    HIPCHK(hipMemcpyAsync(out, d_res, sizeof(int32_t), hipMemcpyDeviceToHost, s));
-    HIPCHK(hipStreamSynchronize(s));
+    struct { uint64_t off, len; int32_t seed, pad; } hv = { 0, len, seed, 0 };
+    int32_t res = 0;
+    hipError_t e = hipMemcpyAsync(d_off, &hv, sizeof hv, hipMemcpyHostToDevice, s);
+    if (e == hipSuccess) {
+        launch_checksum(d_buf, d_off, d_len, d_seed, d_res, 1, kind, s);
+        e = hipGetLastError();
+    }
+    if (e == hipSuccess) e = hipMemcpyAsync(&res, d_res, sizeof res, hipMemcpyDeviceToHost, s);
+    if (int rc = g_tmp.done(s)) return rc;
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    if (e != hipSuccess) return hip_fail(e, "device checksum");
+    *out = res;
     return SDZ_API_OK;
 }
 
@@ -180,6 +219,18 @@ int sdz_sync(void* stream) {
     else { HIPCHK(hipDeviceSynchronize()); }
     return SDZ_API_OK;
 }
+void* sdz_stream_create(void) {
+    if (ensure_device()) return nullptr;
+    hipStream_t s = nullptr;
+    hipError_t e = hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
+    if (e != hipSuccess) { hip_fail(e, "hipStreamCreate"); return nullptr; }
+    return (void*)s;
+}
+int sdz_stream_destroy(void* stream) {
+    if (!stream) return fail(SDZ_API_BAD_ARG, "sdz_stream_destroy: null stream");
+    HIPCHK(hipStreamDestroy((hipStream_t)stream));
+    return SDZ_API_OK;
+}
 int sdz_set_timing(int enabled) { g_timing = enabled; return SDZ_API_OK; }
 int sdz_last_kernel_breakdown(float* ms3) {
     if (!ms3) return fail(SDZ_API_BAD_ARG, "sdz_last_kernel_breakdown: null pointer");
@@ -228,13 +279,14 @@ int sdz_inflate_batch_device(const uint8_t* in, const uint64_t* in_off, const ui
     const size_t off_tk = (off_rs + (size_t)n * rsb + 255) & ~(size_t)255;
     const size_t off_nt = off_tk + (size_t)n * T * 4;
     size_t bytes = off_nt + (size_t)n * 8 + 256;
-    void* scratch = nullptr;
-    if (int rc = g_inflate_scratch.get(bytes, &scratch)) return rc;
-    uint8_t* base = (uint8_t*)scratch;
     int32_t dict_adler = 1;
     if (dict) {
         if (int rc = device_checksum(dict, dict_len, 0, 1, &dict_adler, s)) return rc;
     }
+    void* scratch = nullptr;
+    PoolUse use(g_inflate_scratch, s);
+    if (int rc = use.get(bytes, &scratch)) return rc;
+    uint8_t* base = (uint8_t*)scratch;
     InflateArgs a;
     a.in = in; a.in_off = in_off; a.in_len = in_len;
     a.out = out; a.out_off = out_off; a.out_cap = out_cap;
@@ -306,22 +358,25 @@ int sdz_deflate_batch_device(const uint8_t* in, const uint64_t* in_off, const ui
     if (hipMemGetInfo(&mem_free, &mem_total) != hipSuccess) mem_free = 16ull << 30;
     // record path (levels 4-9, every input <= 64 KiB): hash chains and match records per
     // position, found in parallel before the serial parse (k_deflate.hip)
+    void* tmp = nullptr;
+    PoolUse tmp_use(g_tmp, s);
+    if (int rc = tmp_use.get(kTmpFname + fname_len + 64, &tmp)) return rc;
     uint32_t stride = 0;
     if (level >= 4) {
         uint64_t mx = 0;
-        if (device_max_u64(in_len, n, &mx, s)) return hip_fail(hipGetLastError(), "deflate: input sizes");
+        if (device_max_u64(in_len, n, (unsigned long long*)tmp, &mx, s))
+            return hip_fail(hipGetLastError(), "deflate: input sizes");
         if (mx <= kDeflateRecMax) stride = (uint32_t)std::max<uint64_t>(64, (mx + 63) & ~63ull);
     }
     const uint64_t per_stream = slab + (uint64_t)stride * (sizeof(uint64_t) + sizeof(uint16_t)) + sizeof(int32_t);
     const uint32_t kMaxSlabs = (uint32_t)std::max<uint64_t>(1024, std::min<uint64_t>(65536, mem_free / 2 / per_stream));
     uint32_t chunk = std::min(n, kMaxSlabs);
     void* state = nullptr;
-    if (int rc = g_deflate_state.get((size_t)chunk * per_stream, &state)) return rc;
+    PoolUse state_use(g_deflate_state, s);
+    if (int rc = state_use.get((size_t)chunk * per_stream, &state)) return rc;
     uint8_t* d_fname = nullptr;
-    void* tmp = nullptr;
     if (fname_len) {
-        if (int rc = g_tmp.get(fname_len + 64, &tmp)) return rc;
-        d_fname = (uint8_t*)tmp;
+        d_fname = (uint8_t*)tmp + kTmpFname;
         HIPCHK(hipMemcpyAsync(d_fname, fname, fname_len, hipMemcpyHostToDevice, s));
     }
     unsigned long long* dbg = nullptr;
@@ -358,7 +413,6 @@ int sdz_deflate_batch_device(const uint8_t* in, const uint64_t* in_off, const ui
         hipFree(dbg);
     }
     HIPCHK(hipGetLastError());
-    if (fname_len) HIPCHK(hipStreamSynchronize(s));   // tmp pool is reused
     return SDZ_API_OK;
 }
 
@@ -380,20 +434,33 @@ int sdz_crc32_batch_device(const uint8_t* in, const uint64_t* in_off, const uint
     return SDZ_API_OK;
 }
 
-static int32_t host_checksum(const uint8_t* buf, size_t len, int32_t seed, int kind) {
-    if (ensure_device()) return 0;
+// host buffer -> staging pool -> k_checksum; every failure is reported (never a silent 0)
+static int host_checksum(const uint8_t* buf, size_t len, int32_t seed, int kind, int32_t* out) {
+    if (int rc = ensure_device()) return rc;
+    if (!out || (!buf && len)) return fail(SDZ_API_BAD_ARG, "checksum: null pointer");
     std::lock_guard<std::mutex> lk(g_mu);
-    uint8_t* d = nullptr;
-    if (hipMalloc(&d, len + 64) != hipSuccess) { fail(SDZ_API_OOM, "hipMalloc"); return 0; }
-    int32_t r = 0;
-    if (len && hipMemcpy(d, buf, len, hipMemcpyHostToDevice) != hipSuccess) { hipFree(d); return 0; }
-    device_checksum(d, len, kind, seed, &r, nullptr);
-    hipFree(d);
-    return r;
+    hipStream_t s = nullptr;
+    void* d = nullptr;
+    PoolUse use(g_stage, s);
+    if (int rc = use.get(len + 64, &d)) return rc;
+    if (len) HIPCHK(hipMemcpyAsync(d, buf, len, hipMemcpyHostToDevice, s));
+    return device_checksum((const uint8_t*)d, len, kind, seed, out, s);
 }
 
-int32_t sdz_adler32(const uint8_t* buf, size_t len, int32_t seed) { return host_checksum(buf, len, seed, 0); }
-int32_t sdz_crc32(const uint8_t* buf, size_t len, int32_t seed) { return host_checksum(buf, len, seed, 1); }
+int sdz_adler32_checked(const uint8_t* buf, size_t len, int32_t seed, int32_t* result) {
+    return host_checksum(buf, len, seed, 0, result);
+}
+int sdz_crc32_checked(const uint8_t* buf, size_t len, int32_t seed, int32_t* result) {
+    return host_checksum(buf, len, seed, 1, result);
+}
+int32_t sdz_adler32(const uint8_t* buf, size_t len, int32_t seed) {
+    int32_t r = 0;
+    return sdz_adler32_checked(buf, len, seed, &r) == SDZ_API_OK ? r : 0;
+}
+int32_t sdz_crc32(const uint8_t* buf, size_t len, int32_t seed) {
+    int32_t r = 0;
+    return sdz_crc32_checked(buf, len, seed, &r) == SDZ_API_OK ? r : 0;
+}
 
 // ----------------------------------------------------------------- host wrappers
 

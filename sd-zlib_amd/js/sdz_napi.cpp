@@ -205,11 +205,12 @@ napi_value Checksum(napi_env env, napi_callback_info info, bool crc) {
     }
     int32_t seed = 0;
     NAPI_OK(napi_get_value_int32(env, argv[1], &seed));
-    if (sdz_device_count() < 1) {
-        napi_throw_error(env, nullptr, "libsdz: no HIP device available");
+    int32_t r = 0;
+    int rc = crc ? sdz_crc32_checked(p, n, seed, &r) : sdz_adler32_checked(p, n, seed, &r);
+    if (rc) {
+        napi_throw_error(env, nullptr, (std::string("libsdz: ") + sdz_last_error()).c_str());
         return nullptr;
     }
-    int32_t r = crc ? sdz_crc32(p, n, seed) : sdz_adler32(p, n, seed);
     napi_value x;
     NAPI_OK(napi_create_int32(env, r, &x));
     return x;

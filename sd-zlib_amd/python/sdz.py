@@ -53,11 +53,12 @@ assert ctypes.sizeof(DeflateRecord) == 24
 EXPORTS = [
     "sdz_inflate_batch_device", "sdz_inflate_batch", "sdz_deflate_batch_device",
     "sdz_deflate_batch", "sdz_deflate_bound", "sdz_adler32", "sdz_crc32",
+    "sdz_adler32_checked", "sdz_crc32_checked",
     "sdz_adler32_batch_device", "sdz_crc32_batch_device", "sdz_zmsg", "sdz_last_error",
     "sdz_version", "sdz_device_count", "sdz_set_device", "sdz_device_alloc",
     "sdz_device_free", "sdz_copy_to_device", "sdz_copy_to_host", "sdz_memset_device",
     "sdz_copy_device_to_device",
-    "sdz_sync", "sdz_set_timing", "sdz_last_kernel_ms", "sdz_last_kernel_breakdown",
+    "sdz_sync", "sdz_stream_create", "sdz_stream_destroy", "sdz_set_timing", "sdz_last_kernel_ms", "sdz_last_kernel_breakdown",
 ]
 
 _lib = None
@@ -91,6 +92,9 @@ def lib():
     L.sdz_adler32.restype = i32
     L.sdz_crc32.argtypes = [u8p, sz, i32]
     L.sdz_crc32.restype = i32
+    for f in ("sdz_adler32_checked", "sdz_crc32_checked"):
+        getattr(L, f).argtypes = [u8p, sz, i32, ctypes.POINTER(i32)]
+        getattr(L, f).restype = ctypes.c_int
     for f in ("sdz_adler32_batch_device", "sdz_crc32_batch_device"):
         getattr(L, f).argtypes = [vp, vp, vp, vp, vp, u32, vp]
         getattr(L, f).restype = ctypes.c_int
@@ -105,6 +109,8 @@ def lib():
     L.sdz_memset_device.argtypes = [vp, ctypes.c_int, ctypes.c_uint64]
     L.sdz_copy_device_to_device.argtypes = [vp, vp, ctypes.c_uint64]
     L.sdz_sync.argtypes = [vp]
+    L.sdz_stream_create.restype = vp
+    L.sdz_stream_destroy.argtypes = [vp]
     L.sdz_set_timing.argtypes = [ctypes.c_int]
     L.sdz_last_kernel_ms.restype = ctypes.c_float
     L.sdz_last_kernel_breakdown.argtypes = [ctypes.POINTER(ctypes.c_float)]
@@ -238,16 +244,22 @@ def _u8(source, what="data must be an ArrayBuffer or buffer view"):
     raise TypeError(what)
 
 
+def _checksum(fn, d, seed):
+    r = ctypes.c_int32(0)
+    _check(fn(d, len(d), ctypes.c_int32(seed).value, ctypes.byref(r)))
+    return r.value
+
+
 def adler32(source, seed=1):
     """adler32.ts:17-24 (signed int32; NMAX quirk of adler32.ts:67 included)."""
     d = _u8(source, "source must be a BufferSource")
-    return lib().sdz_adler32(d, len(d), ctypes.c_int32(seed).value)
+    return _checksum(lib().sdz_adler32_checked, d, seed)
 
 
 def crc32(source, seed=0):
     """crc32.ts:17-23 (signed int32)."""
     d = _u8(source, "source must be a BufferSource")
-    return lib().sdz_crc32(d, len(d), ctypes.c_int32(seed).value)
+    return _checksum(lib().sdz_crc32_checked, d, seed)
 
 
 def mergeBuffers(buffers):

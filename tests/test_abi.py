@@ -69,6 +69,14 @@ def test_no_cpu_fallback_without_device(built):
         sdz.inflate_batch([b"\x78\x01\x03\x00\x00\x00\x00\x01"])
     with pytest.raises(sdz.SdzError):
         sdz.deflate_batch([b"abc"])
+    # checksums report the failure instead of returning a wrong value (0)
+    with pytest.raises(sdz.SdzError):
+        sdz.adler32(b"abc")
+    with pytest.raises(sdz.SdzError):
+        sdz.crc32(b"abc")
+    r = ctypes.c_int32(7)
+    assert sdz.lib().sdz_adler32_checked(b"abc", 3, 1, ctypes.byref(r)) == -2   # SDZ_API_NO_DEVICE
+    assert r.value == 7
 
 
 def test_gpu_sources_are_gfx950_only():

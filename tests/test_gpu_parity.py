@@ -429,3 +429,84 @@ def test_small_rounds_rebuild_the_window(monkeypatch, paradise):
     dgpu = sdz.inflate_batch([golden("simple.deflate")], [4096], sdz.FMT_CONTAINER,
                              None)[0]
     assert dgpu["data"] == golden("simple.txt")
+
+
+# ------------------------------------------------------------------ stream ordering
+
+class _DevBatch:
+    """Distinct device-resident payloads with their own output slots (8-aligned)."""
+
+    def __init__(self, payloads, caps):
+        import ctypes
+        self.n = len(payloads)
+        offs, o = [], 0
+        for p in payloads:
+            offs.append(o)
+            o += (len(p) + 255) // 256 * 256
+        self.d_in = sdz.DeviceBuffer(o + 128)
+        for p, off in zip(payloads, offs):
+            if p:
+                self.d_in.upload(p, off)
+        oo, q = [], 0
+        for c in caps:
+            oo.append(q)
+            q += (c + 255) // 256 * 256
+        self.caps = list(caps)
+        self.out_off = oo
+        self.d_out = sdz.DeviceBuffer(q + 64)
+        meta = offs + [len(p) for p in payloads] + oo + list(caps)
+        self.d_meta = sdz.DeviceBuffer(8 * len(meta))
+        self.d_meta.upload(bytes((ctypes.c_uint64 * len(meta))(*meta)))
+        self.d_rec = sdz.DeviceBuffer(64 * self.n)
+
+    def ptrs(self):
+        m, n = self.d_meta.ptr, self.n
+        return m, m + 8 * n, m + 16 * n, m + 24 * n
+
+    def output(self, i, length):
+        return self.d_out.download(length, self.out_off[i])
+
+
+def test_concurrent_streams_do_not_share_scratch(paradise):
+    """Two non-blocking streams run deflate and inflate batches at the same time: the
+    runtime's scratch pools are stream-ordered, so both results stay bit-exact."""
+    import ctypes
+    L = sdz.lib()
+    rng = random.Random(21)
+    sets = [[paradise[o:o + 60000] for o in rng.sample(range(0, len(paradise) - 60000), 48)],
+            [text_corpus(rng, rng.randint(30000, 65536)) for _ in range(48)]]
+    bound = lambda d: int(L.sdz_deflate_bound(len(d), 1, 0))
+    dfl = [_DevBatch(s, [bound(d) for d in s]) for s in sets]
+    comp = [golden("paradiselost.deflate")] * 40, [zlib.compress(d, 9) for d in sets[1][:40]]
+    exp_inf = [[paradise] * 40, sets[1][:40]]
+    inf = [_DevBatch(c, [len(e) + 64 for e in x]) for c, x in zip(comp, exp_inf)]
+    streams = [L.sdz_stream_create(), L.sdz_stream_create()]
+    assert all(streams)
+    for rep in range(2):
+        for k in range(2):                     # no synchronisation between the launches
+            b = dfl[k]
+            rc = L.sdz_deflate_batch_device(b.d_in.ptr, *b.ptrs()[:2], b.d_out.ptr, *b.ptrs()[2:],
+                                            b.d_rec.ptr, b.n, 6 + 3 * k - 3 * k * rep, 1, None, 0, 0,
+                                            streams[k])
+            assert rc == 0, L.sdz_last_error()
+        for k in range(2):
+            b = inf[k]
+            rc = L.sdz_inflate_batch_device(b.d_in.ptr, *b.ptrs()[:2], b.d_out.ptr, *b.ptrs()[2:],
+                                            b.d_rec.ptr, b.n, sdz.FMT_CONTAINER, None, 0, streams[1 - k])
+            assert rc == 0, L.sdz_last_error()
+        for s in streams:
+            assert L.sdz_sync(s) == 0
+        for k in range(2):
+            level = 6 + 3 * k - 3 * k * rep
+            b = dfl[k]
+            recs = (sdz.DeflateRecord * b.n).from_buffer_copy(b.d_rec.download(24 * b.n))
+            for i in range(0, b.n, 7):
+                assert recs[i].status == 0
+                assert b.output(i, recs[i].out_len) == O.deflate(sets[k][i], level=level), (rep, k, i)
+            b = inf[k]
+            recs = (sdz.InflateRecord * b.n).from_buffer_copy(b.d_rec.download(64 * b.n))
+            for i in range(b.n):
+                assert recs[i].status == 0 and recs[i].success
+                assert b.output(i, recs[i].out_len) == exp_inf[k][i]
+    for s in streams:
+        assert L.sdz_stream_destroy(s) == 0
