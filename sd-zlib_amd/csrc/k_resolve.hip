@@ -330,7 +330,7 @@ __device__ __forceinline__ bool wait_ge(uint32_t* p, uint32_t v, uint32_t* fail)
 __device__ __forceinline__ uint32_t lap_of(uint32_t g) { return ((g >> 12) & 127u) + 1u; }
 __device__ __forceinline__ bool map_all(const uint8_t* fmap, bool act, uint32_t lo, uint32_t hi) {
     const uint32_t* fmap32 = (const uint32_t*)fmap;
-    bool ok = true;
+    uint32_t miss = 0;                                    // VGPR accumulation: no lane-mask (SALU) ops
     const uint32_t n = act ? hi - lo : 0u;               // modulo 2^32: positions are low bits
     const uint32_t m0 = lo >> 2, nw = n ? ((lo & 3u) + n + 3u) >> 2 : 0u;
     const uint32_t bt = ((lo + n - 1u) & 3u) + 1u;       // bytes used of the last dword
@@ -339,9 +339,9 @@ __device__ __forceinline__ bool map_all(const uint8_t* fmap, bool act, uint32_t 
         const uint32_t bl = i == 0 ? lo & 3u : 0u, bh = i + 1 == nw ? bt : 4u;
         const uint32_t mask = i < nw ? (bh == 4u ? ~0u : (1u << (8 * bh)) - 1u) & (~0u << (8 * bl)) : 0u;
         const uint32_t v = fmap32[i < nw ? m & (RS_BM / 4 - 1) : 0u];
-        ok = ok && ((v ^ (lap_of(4 * m) * 0x01010101u)) & mask) == 0;
+        miss |= (v ^ (lap_of(4 * m) * 0x01010101u)) & mask;
     }
-    return ok;
+    return miss == 0;
 }
 __device__ __forceinline__ void publish_wf(uint32_t* wf, uint32_t v1) {
     lds_release();
@@ -404,15 +404,22 @@ __global__ __launch_bounds__(RS_THREADS) __attribute__((amdgpu_waves_per_eu(RS_W
     unsigned long long tlast = timed ? clock64() : 0;
 #define RS_TICK(k) do { if (timed) { unsigned long long tn = clock64(); tacc[k] += tn - tlast; tlast = tn; } } while (0)
     const uint32_t ngroups = (ntok + 63u) >> 6;
+    // Control flow below is kept wave-uniform (values read from LDS go through
+    // readfirstlane, lane predicates are selects): the scalar unit, shared by the CU's
+    // four SIMDs, is the busiest resource of this kernel (an extra SALU per copy round
+    // costs ~3 SIMD cycles, measured), so divergent ifs and their exec-mask juggling
+    // are avoided on the hot path.  `fail` is polled once per 64 waits only.
+    const uint32_t wu = uni(w);
     // emitter waves: no global stores, so the token prefetch is their only vector-memory
     // traffic and its wait does not cover write-back stores
-    uint32_t tnext = tk[w * 64u + lane < ntok ? w * 64u + lane : 0u];
-    for (uint32_t g = w; w < RS_EW && g < ngroups; g += RS_EW) {
+    uint32_t tnext = tk[wu * 64u + lane < ntok ? wu * 64u + lane : 0u];
+    bool bad = false;                                     // this wave's watchdog tripped
+    for (uint32_t g = wu; wu < RS_EW && g < ngroups; g += RS_EW) {
         const uint32_t ti = g * 64u + lane;
         const bool valid = ti < ntok;
         const uint32_t t = tnext;
         tnext = tk[ti + 64u * RS_EW < ntok ? ti + 64u * RS_EW : 0u];
-        const bool ism = (t >> 31) != 0;
+        const bool ism = (int32_t)t < 0;
         const uint32_t len = !valid ? 0u : ism ? ((t >> 16) & 255u) + 3u : ((t >> 24) & 3u) + 1u;
         const uint32_t dist = ism ? (t & 0x7fffu) + 1u : 0u;
         const uint32_t incl = wave_incl_scan(len);
@@ -422,19 +429,22 @@ __global__ __launch_bounds__(RS_THREADS) __attribute__((amdgpu_waves_per_eu(RS_W
 
         // 1. the group's start from its predecessor; pass ours on
         uint32_t Sg = 0;
-        for (uint32_t n = 0;; ++n) {
+        for (uint32_t n = 1;; ++n) {
             const uint64_t c = lds_get64(&chain);
-            if ((uint32_t)(c >> 32) == g - 1u) { Sg = uni((uint32_t)c); break; }
-            if (n > RS_SPIN_LIMIT || lds_get(&fail)) { if (!lds_get(&fail)) lds_put(&fail, 1u | (g << 4)); break; }
+            if (uni((uint32_t)(c >> 32)) == g - 1u) { Sg = uni((uint32_t)c); break; }
+            if ((n & 63u) == 0 && (n > RS_SPIN_LIMIT || lds_get(&fail))) {
+                if (!lds_get(&fail)) lds_put(&fail, 1u | (g << 4));
+                bad = true;
+                break;
+            }
             __builtin_amdgcn_s_sleep(RS_NAP);
         }
+        if (bad) break;
         if (lane == 0) __hip_atomic_store(&chain, ((uint64_t)g << 32) | (Sg + T), __ATOMIC_RELAXED,
                                           __HIP_MEMORY_SCOPE_WORKGROUP);
-        if (lds_get(&fail)) break;
         RS_TICK(1);
 
         // 2. copy rounds
-        Sg = uni(Sg);                                                  // wave-uniform (keeps it and sr in SGPRs)
         const uint32_t sr = uni((rp0 + Sg) % RS_R);                    // ring index of byte Sg (u32: Sg < 2^26)
         const uint32_t dst = Sg + off, dend = dst + len;
         const int32_t src = (int32_t)dst - (int32_t)dist;             // round-relative (may be < 0)
@@ -443,10 +453,11 @@ __global__ __launch_bounds__(RS_THREADS) __attribute__((amdgpu_waves_per_eu(RS_W
         const uint32_t s = ridx((int32_t)(sr + off) - (int32_t)dist);
         const uint32_t gd = (uint32_t)pos0 + dst;                       // low bits of the global position
         const uint32_t mp = gd & (RS_BM - 1), lb = lap_of(gd);
+        const uint32_t g32 = (uint32_t)pos0;
         bool done = len == 0;
         uint64_t nd = __ballot(!done);
-        uint32_t pre = nd ? lane_at(off, (uint32_t)__builtin_ctzll(nd)) : T;   // finished prefix
-        for (uint32_t n = 0; nd; ++n) {
+        for (uint32_t n = 1; nd; ++n) {
+            const uint32_t pre = lane_at(off, (uint32_t)__builtin_ctzll(nd));   // finished prefix
             uint32_t cwf = lds_get(&wf);
             const uint32_t cwb = lds_get(&wwb);
             if (cwf >= Sg && cwf < Sg + pre) {            // head: publish our finished prefix
@@ -456,38 +467,54 @@ __global__ __launch_bounds__(RS_THREADS) __attribute__((amdgpu_waves_per_eu(RS_W
             const bool room = !done && dend <= cwf + RS_SLACK && dend <= cwb + RS_R;
             const bool inwin = need <= (int32_t)cwf;
             const uint32_t blo = src > (int32_t)cwf ? (uint32_t)src : cwf;
-            const uint32_t g32 = (uint32_t)pos0;
-            const bool rdy = room && (inwin || map_all(fmap, room && !inwin, g32 + blo, g32 + (uint32_t)need));
-            if (__ballot(rdy)) {
+            const bool chk = room && !inwin;
+            bool ok = true;
+            if (__ballot(chk)) ok = map_all(fmap, chk, g32 + blo, g32 + (uint32_t)need);
+            const bool rdy = room && (inwin || ok);
+            const uint64_t rm = __ballot(rdy);
+            if (rm) {
                 RS_CBAR();
                 emit_msk(ring, fmap, rdy, t, d, s, len, dist, mp, lb);
+#ifdef RS_XSALU
+                {   // experiment: extra SALU per emit round
+                    uint32_t z = uni(len);
+#pragma unroll
+                    for (int q = 0; q < RS_XSALU; ++q) asm volatile("s_add_u32 %0, %0, 1" : "+s"(z));
+                    if (z == 0xdeadbeef) tacc[5]++;
+                }
+#endif
                 done = done || rdy;
-                nd = __ballot(!done);
-                pre = nd ? lane_at(off, (uint32_t)__builtin_ctzll(nd)) : T;
+                nd &= ~rm;
                 n = 0;
                 if (timed) tacc[6]++;
             } else {
                 if (timed) tacc[7]++;
-                if (n > RS_SPIN_LIMIT || lds_get(&fail)) { if (!lds_get(&fail)) lds_put(&fail, 3u | (Sg << 4)); break; }
+                if ((n & 63u) == 0 && (n > RS_SPIN_LIMIT || lds_get(&fail))) {
+                    if (!lds_get(&fail)) lds_put(&fail, 3u | (Sg << 4));
+                    bad = true;
+                    break;
+                }
                 __builtin_amdgcn_s_sleep(RS_NAP);
             }
         }
-        if (lds_get(&fail)) break;
+        if (bad) break;
         RS_TICK(2);
-        // finality: publish now if we are the head (no one else can move wf past Sg)
-        const uint32_t cwf = lds_get(&wf);
-        const bool pub = cwf >= Sg;
-        if (pub) publish_wf(&wf, Sg + T);
-
-        RS_TICK(3);
-        // 3. the frontier, in group order
-        if (!pub) {
-            if (!wait_ge(&wf, Sg, &fail)) break;
-            publish_wf(&wf, Sg + T);
+        // 3. finality, in group order: publish now if we are the head (no one else can
+        // move wf past Sg), else once the frontier reaches us
+        for (uint32_t n = 1;; ++n) {
+            if (lds_get(&wf) >= Sg) { lds_acquire(); break; }
+            if ((n & 63u) == 0 && (n > RS_SPIN_LIMIT || lds_get(&fail))) {
+                if (!lds_get(&fail)) lds_put(&fail, 2u | (Sg << 4));
+                bad = true;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(RS_NAP);
         }
+        if (bad) break;
+        publish_wf(&wf, Sg + T);
         RS_TICK(4);
     }
-    if (w < RS_EW) {
+    if (wu < RS_EW) {
         lds_release();
         if (lane == 0) __hip_atomic_fetch_add(&edone, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     } else {
@@ -495,7 +522,7 @@ __global__ __launch_bounds__(RS_THREADS) __attribute__((amdgpu_waves_per_eu(RS_W
         // adler32 sums; publishes wwb, which frees ring slots
         uint32_t WB = 0, Wr = rp0, gm = pm0;              // written back (round-relative), its ring index, (pos0 + WB) mod 65521
         const uint32_t* ring32 = (const uint32_t*)ring;
-        for (uint32_t n = 0;; ++n) {
+        for (uint32_t n = 1;; ++n) {
             const bool fi = lds_get(&edone) == RS_EW;     // every group published: wf is the round's end
             lds_acquire();
             const uint32_t Fv = lds_get(&wf);
@@ -507,29 +534,48 @@ __global__ __launch_bounds__(RS_THREADS) __attribute__((amdgpu_waves_per_eu(RS_W
                 if (Fv == WB) break;
                 m = Fv - WB;
             } else {
-                if (n > RS_SPIN_LIMIT || lds_get(&fail)) { if (!lds_get(&fail)) lds_put(&fail, 4u | (WB << 4)); break; }
+                if ((n & 63u) == 0 && (n > RS_SPIN_LIMIT || lds_get(&fail))) {
+                    if (!lds_get(&fail)) lds_put(&fail, 4u | (WB << 4));
+                    break;
+                }
                 __builtin_amdgcn_s_sleep(RS_NAP);
                 continue;
             }
             n = 0;
             const uint32_t h = (uint32_t)(ab & 3u);
-            const uint32_t nq = (uint32_t)(((ab + m + 3u) >> 2) - (ab >> 2));
-            uint32_t* dstw = (uint32_t*)(out + (ab - h));
-            const int32_t rb0 = (int32_t)Wr - (int32_t)h;  // ring index of the first dword (4-aligned)
-            const uint32_t tl = (uint32_t)((ab + m) & 3u);
             const uint32_t gi0 = gm + 65521u - h;          // index of byte 0 of dword 0, mod 65521 (+ 65521)
-            for (uint32_t q = lane; q < nq; q += 64) {
-                const uint32_t v = ring32[ridx(rb0 + 4 * (int32_t)q) >> 2];
-                const uint32_t blo = q == 0 ? h : 0u;
-                const uint32_t bhi = q + 1 < nq || tl == 0 ? 4u : tl;
-                if (blo == 0 && bhi == 4) dstw[q] = v;
-                else for (uint32_t bb = blo; bb < bhi; ++bb) ((uint8_t*)(dstw + q))[bb] = (uint8_t)(v >> (8 * bb));
-                if (!gz) {
-                    const uint32_t mk = (bhi == 4u ? ~0u : (1u << (8 * bhi)) - 1u) & (~0u << (8 * blo));
-                    const uint32_t vm = v & mk;
-                    const uint32_t s4 = __builtin_amdgcn_udot4(vm, 0x01010101u, 0u, false);
-                    accS += s4;
-                    accT += (uint64_t)(gi0 + 4 * q) * s4 + __builtin_amdgcn_udot4(vm, 0x03020100u, 0u, false);
+            if (m == 1024u) {
+                // a whole aligned KiB: 4 full dwords per lane, no edge bytes
+                uint32_t* dstw = (uint32_t*)(out + ab);
+#pragma unroll
+                for (uint32_t k = 0; k < 4; ++k) {
+                    const uint32_t q = lane + 64u * k;
+                    const uint32_t v = ring32[ridx((int32_t)Wr + 4 * (int32_t)q) >> 2];
+                    dstw[q] = v;
+                    if (!gz) {
+                        const uint32_t s4 = __builtin_amdgcn_udot4(v, 0x01010101u, 0u, false);
+                        accS += s4;
+                        accT += (uint64_t)(gi0 + 4 * q) * s4 + __builtin_amdgcn_udot4(v, 0x03020100u, 0u, false);
+                    }
+                }
+            } else {
+                const uint32_t nq = (uint32_t)(((ab + m + 3u) >> 2) - (ab >> 2));
+                uint32_t* dstw = (uint32_t*)(out + (ab - h));
+                const int32_t rb0 = (int32_t)Wr - (int32_t)h;  // ring index of the first dword (4-aligned)
+                const uint32_t tl = (uint32_t)((ab + m) & 3u);
+                for (uint32_t q = lane; q < nq; q += 64) {
+                    const uint32_t v = ring32[ridx(rb0 + 4 * (int32_t)q) >> 2];
+                    const uint32_t blo = q == 0 ? h : 0u;
+                    const uint32_t bhi = q + 1 < nq || tl == 0 ? 4u : tl;
+                    if (blo == 0 && bhi == 4) dstw[q] = v;
+                    else for (uint32_t bb = blo; bb < bhi; ++bb) ((uint8_t*)(dstw + q))[bb] = (uint8_t)(v >> (8 * bb));
+                    if (!gz) {
+                        const uint32_t mk = (bhi == 4u ? ~0u : (1u << (8 * bhi)) - 1u) & (~0u << (8 * blo));
+                        const uint32_t vm = v & mk;
+                        const uint32_t s4 = __builtin_amdgcn_udot4(vm, 0x01010101u, 0u, false);
+                        accS += s4;
+                        accT += (uint64_t)(gi0 + 4 * q) * s4 + __builtin_amdgcn_udot4(vm, 0x03020100u, 0u, false);
+                    }
                 }
             }
             WB += m;
