@@ -75,6 +75,87 @@ class DeviceBatch:
             b.free()
 
 
+def slice_offsets(n, span, seed=0x5D5A1B1E):
+    """n slice offsets in [0, span) from a seeded xorshift64."""
+    x, out = seed, []
+    for _ in range(n):
+        x ^= (x << 13) & 0xFFFFFFFFFFFFFFFF
+        x ^= x >> 7
+        x ^= (x << 17) & 0xFFFFFFFFFFFFFFFF
+        out.append(x % span)
+    return out
+
+
+def fill_slices(sdz, b, text, offs, slice_len):
+    """Stream j of batch b <- text[offs[j] : offs[j] + slice_len], copied on the device."""
+    L = sdz.lib()
+    src = sdz.DeviceBuffer(len(text) + 64)
+    src.upload(text)
+    for j, o in enumerate(offs):
+        rc = L.sdz_copy_device_to_device(b.d_in.ptr + j * b.in_stride, src.ptr + o, slice_len)
+        assert rc == 0, L.sdz_last_error()
+    src.free()
+
+
+def inflate_distinct(sdz, L, bd, drec, text, offs, slice_len, steps, barrier, allmax, world):
+    """Inflate the deflate leg's n distinct compressed streams (device-resident) back into
+    64 KiB slots: every stream has its own Huffman tables and LZ77 history."""
+    n = bd.n
+    in_len = [r.out_len for r in drec]
+    meta = [j * bd.out_stride for j in range(n)] + in_len + \
+           [j * round_up(slice_len, 256) for j in range(n)] + [slice_len] * n
+    d_meta = sdz.DeviceBuffer(8 * len(meta))
+    d_meta.upload(bytes((ctypes.c_uint64 * len(meta))(*meta)))
+    d_out = sdz.DeviceBuffer(round_up(slice_len, 256) * n + 64)
+    rec_size = ctypes.sizeof(sdz.InflateRecord)
+    d_rec = sdz.DeviceBuffer(rec_size * n)
+    m = d_meta.ptr
+
+    def step(split):
+        rc = L.sdz_inflate_batch_device(bd.d_out.ptr, m, m + 8 * n, d_out.ptr, m + 16 * n, m + 24 * n,
+                                        d_rec.ptr, n, sdz.FMT_AUTO, None, 0, None)
+        if rc:
+            raise RuntimeError(L.sdz_last_error().decode())
+        ms = L.sdz_last_kernel_ms()
+        f3 = (ctypes.c_float * 3)()
+        L.sdz_last_kernel_breakdown(f3)
+        split.append(list(f3))
+        return ms
+
+    step([])
+    L.sdz_sync(None)
+    barrier()
+    t0 = time.perf_counter()
+    kms, split = [], []
+    for _ in range(steps):
+        kms.append(step(split))
+    L.sdz_sync(None)
+    barrier()
+    wall = allmax(time.perf_counter() - t0) / steps
+    recs = (sdz.InflateRecord * n).from_buffer_copy(d_rec.download(n * rec_size))
+    ok = all(r.status == 0 and r.success and r.out_len == slice_len and r.checksum_verdict == 1 for r in recs)
+    for j in sorted({0, n // 2, n - 1}):
+        ok = ok and d_out.download(slice_len, j * round_up(slice_len, 256)) == text[offs[j]:offs[j] + slice_len]
+    ok = allmax(0.0 if ok else 1.0) == 0.0
+    for x in (d_meta, d_out, d_rec):
+        x.free()
+    kernel_ms = sum(kms) / len(kms)
+    bin_, bout = sum(in_len), n * slice_len
+    achieved = (bin_ + bout) / (kernel_ms / 1000.0) / 1e9
+    return {
+        "value": round(world * bout / wall / 1e6, 2), "unit": "MB/s", "ms_per_step": round(1000 * wall, 3),
+        "config": {"workload": "64 Ki distinct 64 KiB dynamic-Huffman zlib streams (the deflate leg's "
+                               "outputs; north-star target)", "streams_per_gpu": n,
+                   "bytes_in_per_gpu": bin_, "bytes_out_per_gpu": bout},
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 5), "kernel_ms": round(kernel_ms, 3),
+                     "kernels_ms": {"k_inflate_decode": round(sum(x[0] for x in split) / len(split), 3),
+                                    "k_inflate_resolve": round(sum(x[1] for x in split) / len(split), 3),
+                                    "k_inflate_finalize": round(sum(x[2] for x in split) / len(split), 3)}},
+        "parity": bool(ok),
+    }
+
+
 def inflate_step(sdz, b, split=None):
     in_off, in_len, out_off, out_cap = b.ptrs()
     rc = sdz.lib().sdz_inflate_batch_device(b.d_in.ptr, in_off, in_len, b.d_out.ptr, out_off, out_cap,
@@ -134,6 +215,8 @@ def main():
     ap.add_argument("--deflate-streams", type=int, default=65536,
                     help="streams for the deflate leg (64 KiB slices, L6); 0 disables")
     ap.add_argument("--deflate-steps", type=int, default=1)
+    ap.add_argument("--distinct-steps", type=int, default=3,
+                    help="steps of the distinct-stream inflate leg (the deflate leg's outputs); 0 disables")
     ap.add_argument("--copy-gib", type=float, default=4.0, help="device copy peak probe size; 0 disables")
     ap.add_argument("--host-streams", type=int, default=0,
                     help="streams for the host-buffer (PCIe-inclusive) inflate probe, e.g. 2048; off by "
@@ -248,19 +331,17 @@ def main():
                 "note": "sdz_inflate_batch on host buffers: H2D + kernels + D2H, PCIe-inclusive"}
         del hbufs
 
-    # ---- deflate leg (configs[2]: 64 KiB text slices, level 6, "deflate" container)
+    # ---- deflate leg (configs[2]: 64 KiB text slices, level 6, "deflate" container); every
+    # stream is a distinct slice (xorshift64 offsets), and the compressed outputs then feed
+    # the distinct-stream inflate leg (the north star's 64 Ki x 64 KiB dynamic-Huffman target)
     deflate = None
+    distinct = None
     if args.deflate_streams > 0:
-        import random
-        rng = random.Random(0x5D5A1B1E)
         nd = args.deflate_streams
         slice_len = 65536
-        offs = [(i * 65521) % (len(text) - slice_len) for i in range(64)]
-        payloads = [text[o:o + slice_len] for o in offs]
-        bd = DeviceBatch(sdz, payloads[0], nd, int(L.sdz_deflate_bound(slice_len, 1, 0)))
-        for i, pl in enumerate(payloads[1:], 1):           # 64 distinct slices, cycled
-            for j in range(i, nd, 64):
-                bd.d_in.upload(pl, j * bd.in_stride)
+        offs = slice_offsets(nd, len(text) - slice_len)
+        bd = DeviceBatch(sdz, text[:slice_len], nd, int(L.sdz_deflate_bound(slice_len, 1, 0)))
+        fill_slices(sdz, bd, text, offs, slice_len)
         deflate_step(sdz, bd, 6, 1)
         L.sdz_sync(None)
         barrier()
@@ -274,18 +355,22 @@ def main():
         dok = all(r.status == 0 for r in drec)
         if rank == 0:
             import oracle as O
-            for j in (0, 1, nd - 1):
+            for j in sorted({0, 1, nd // 2, nd - 1}):
                 got = bd.d_out.download(drec[j].out_len, j * bd.out_stride)
-                dok = dok and got == O.deflate(payloads[j % 64], level=6)
-        bd.free()
+                dok = dok and got == O.deflate(text[offs[j]:offs[j] + slice_len], level=6)
         deflate = {
             "value": round(world * comp_total / dwall / 1e6, 2), "unit": "compressed MB/s",
             "input_MBps": round(world * nd * slice_len / dwall / 1e6, 2),
             "kernel_ms": round(sum(dk) / len(dk), 3), "ms_per_step": round(1000 * dwall, 3),
             "config": {"workload": "C3 deflate level=6 format=deflate", "streams_per_gpu": nd,
-                       "slice_bytes": slice_len, "data": "paradiselost.txt slices (enwik8 absent offline)"},
+                       "slice_bytes": slice_len,
+                       "data": "%d distinct paradiselost.txt slices at xorshift64 offsets (enwik8 absent offline)" % nd},
             "parity": bool(dok),
         }
+        if args.distinct_steps > 0:
+            distinct = inflate_distinct(sdz, L, bd, drec, text, offs, slice_len, args.distinct_steps,
+                                        barrier, allmax, world)
+        bd.free()
 
     cpu = None
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
@@ -333,6 +418,7 @@ def main():
         "parity": bool(okall),
         "gather_ms": None if gather_ms is None else round(gather_ms, 3),
         "deflate": deflate,
+        "inflate_distinct": distinct,
     }
     if rank == 0:
         print(json.dumps(line), flush=True)

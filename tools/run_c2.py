@@ -12,12 +12,12 @@ sys.path.insert(0, os.path.join(ROOT, "sd-zlib_amd", "python"))
 sys.path.insert(0, ROOT)
 
 import sdz  # noqa: E402
-from bench import DeviceBatch, inflate_step, deflate_step  # noqa: E402
+from bench import DeviceBatch, inflate_step, deflate_step, slice_offsets, fill_slices, inflate_distinct  # noqa: E402
 
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--mode", default="inflate", choices=["inflate", "deflate"])
+    ap.add_argument("--mode", default="inflate", choices=["inflate", "deflate", "distinct"])
     ap.add_argument("--same", action="store_true", help="deflate: one slice in every stream")
     ap.add_argument("--steps", type=int, default=2)
     ap.add_argument("--streams", type=int, default=65536)
@@ -35,15 +35,26 @@ def main():
             ms = inflate_step(sdz, b, split)
             print("inflate step %d: kernel %.3f ms (decode %.2f resolve %.2f), %.1f GB/s out"
                   % (i, ms, split[0][0], split[0][1], len(text) * args.streams / ms / 1e6), flush=True)
+    elif args.mode == "distinct":
+        # the bench's distinct-stream inflate leg: deflate n distinct slices (L6), inflate them
+        import ctypes
+        offs = slice_offsets(args.streams, len(text) - 65536)
+        b = DeviceBatch(sdz, text[:65536], args.streams, int(L.sdz_deflate_bound(65536, 1, 0)))
+        fill_slices(sdz, b, text, offs, 65536)
+        deflate_step(sdz, b, args.level, 1)
+        L.sdz_sync(None)
+        drec = (sdz.DeflateRecord * args.streams).from_buffer_copy(
+            b.d_rec.download(args.streams * ctypes.sizeof(sdz.DeflateRecord)))
+        r = inflate_distinct(sdz, L, b, drec, text, offs, 65536, args.steps, lambda: None, lambda x: x, 1)
+        print("distinct inflate: kernel %.3f ms %s, %.1f GB/s out, parity %s"
+              % (r["roofline"]["kernel_ms"], r["roofline"]["kernels_ms"],
+                 r["config"]["bytes_out_per_gpu"] / r["roofline"]["kernel_ms"] / 1e6, r["parity"]), flush=True)
     else:
-        # the bench's C3 layout: 64 distinct slices of paradiselost.txt, cycled over the streams
+        # the bench's C3 layout: distinct slices of paradiselost.txt at xorshift64 offsets
         # (identical streams would run the serial parse without any lane divergence)
-        offs = [(i * 65521) % (len(text) - 65536) for i in range(64)]
-        payloads = [text[o:o + 65536] for o in offs] if not args.same else [text[:65536]] * 64
-        b = DeviceBatch(sdz, payloads[0], args.streams, int(L.sdz_deflate_bound(65536, 1, 0)))
-        for i, pl in enumerate(payloads[1:], 1):
-            for j in range(i, args.streams, 64):
-                b.d_in.upload(pl, j * b.in_stride)
+        b = DeviceBatch(sdz, text[:65536], args.streams, int(L.sdz_deflate_bound(65536, 1, 0)))
+        if not args.same:
+            fill_slices(sdz, b, text, slice_offsets(args.streams, len(text) - 65536), 65536)
         for i in range(args.steps):
             ms = deflate_step(sdz, b, args.level, 1)
             print("deflate step %d: kernel %.3f ms, %.2f GB/s in" % (i, ms, 65536 * args.streams / ms / 1e6),
