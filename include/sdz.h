@@ -63,6 +63,9 @@ enum {
     SDZ_TOO_SMALL = 7,     /* AUTO and < 2 bytes: "data buffer is too small" :195 */
     SDZ_BAD_RECORD = 8,    /* misaligned output offset (must be a multiple of 8) */
     SDZ_INTERNAL = 9,      /* engine watchdog: a resolve wait did not complete (never expected) */
+    SDZ_CARRY_OVERFLOW = 10, /* incremental mode: one header or block header needed more than
+                              SDZ_INFLATE_CARRY bytes of buffered input (a gzip FNAME/FCOMMENT
+                              longer than that); the stream cannot continue */
 };
 
 /* Checksum / size verdicts ("unchecked" | "match" | "mismatch") */
@@ -87,7 +90,9 @@ typedef struct sdz_inflate_record {
     uint8_t  checksum_verdict;  /* SDZ_UNCHECKED / SDZ_MATCH / SDZ_MISMATCH */
     uint8_t  size_verdict;
     uint8_t  success;           /* complete && no mismatch */
-    uint8_t  reserved[11];
+    uint8_t  out_full;          /* incremental mode: stopped at out_cap; pass the input from
+                                   in_used on again (sdz_inflate_append_batch_device) */
+    uint8_t  reserved[10];
 } sdz_inflate_record;
 
 typedef struct sdz_deflate_record {
@@ -116,6 +121,49 @@ int sdz_inflate_batch_device(const uint8_t* in, const uint64_t* in_off, const ui
 int sdz_inflate_batch(const uint8_t* const* in, const size_t* in_len, uint8_t* const* out,
                       const size_t* out_cap, sdz_inflate_record* rec, uint32_t n,
                       int32_t format, const uint8_t* dict, size_t dict_len);
+
+/* ------------------------------------------------- incremental inflate */
+
+/* Inflater.append(chunk) across calls, as many Inflaters at once (sd-inflate.ts:54-179;
+ * engine state inflate.ts:79-95, infblocks.ts:45-50, infcodes.ts:35-55).  A state slab
+ * holds n independent streams' decoder state in device memory between calls: the bit
+ * position, block mode and Huffman tables, the last 32 KiB of output (the LZ77 window),
+ * the input bytes of a unit (header, block header, symbol) not yet complete, and the
+ * running checksum exactly as the reference's Inflater keeps it (adler32 per 16 KiB
+ * output chunk with the adler32.ts:67 NMAX quirk; crc32 for gzip).
+ *
+ * Each sdz_inflate_append_batch_device call hands every stream its next input chunk
+ * (in_len[i] may be 0) and an output slot; the stream decodes as far as its input allows
+ * -- output ends where the reference's append() output would end -- and writes a record:
+ *  - out_len: bytes written by this call (out[out_off[i] ..]);
+ *  - status SDZ_TRUNCATED with complete = 0: more input is needed (not an error);
+ *  - in_used: the stream offset up to which input is consumed or held on the device;
+ *  - out_full = 1: out_cap was reached before the chunk was used up; the chunk's bytes
+ *    from stream offset in_used on were not taken: pass them again (before any new
+ *    bytes) in the next call, which continues the output;
+ *  - name_off: gzip FNAME offset from the stream's first input byte;
+ *  - checksum/size verdicts and success as finish() would report them now.
+ * A stream that already finished reports SDZ_TRAILING if it is given more bytes.
+ * Divergences from the reference are its defects: a stored block or a dynamic block
+ * header split across calls decodes correctly here. */
+#define SDZ_INFLATE_CARRY 16384u
+uint64_t sdz_inflate_state_bytes(uint32_t n);
+/* fresh Inflaters: format SDZ_FMT_RAW (options.raw) or SDZ_FMT_CONTAINER */
+int sdz_inflate_state_reset_device(void* state, uint32_t n, void* stream);
+int sdz_inflate_append_batch_device(void* state, const uint8_t* in, const uint64_t* in_off,
+                                    const uint64_t* in_len, uint8_t* out, const uint64_t* out_off,
+                                    const uint64_t* out_cap, sdz_inflate_record* rec, uint32_t n,
+                                    int32_t format, const uint8_t* dict, uint32_t dict_len,
+                                    void* stream);
+
+/* One Inflater on host buffers (what the N-API and ctypes facades call): create, then
+ * append(chunk) -> *out / *out_len (valid until the next call on this handle) and the
+ * record of the stream so far; the loop over out_full is done inside. */
+typedef struct sdz_inflater sdz_inflater;
+sdz_inflater* sdz_inflater_create(int32_t format, const uint8_t* dict, size_t dict_len);
+int sdz_inflater_append(sdz_inflater* z, const uint8_t* data, size_t len, const uint8_t** out,
+                        size_t* out_len, sdz_inflate_record* rec);
+void sdz_inflater_destroy(sdz_inflater* z);
 
 /* ---------------------------------------------------------------- deflate */
 

@@ -66,6 +66,9 @@ def lib():
             ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_size_t), ctypes.c_int32,
             ctypes.c_int32, u8p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_size_t,
             ctypes.POINTER(InflateResult)]
+        L.oracle_inflater_run_parts.restype = ctypes.c_int32
+        L.oracle_inflater_run_parts.argtypes = L.oracle_inflater_run.argtypes + [
+            ctypes.POINTER(ctypes.c_size_t), ctypes.POINTER(ctypes.c_int32)]
         L.oracle_inflate.restype = ctypes.c_int32
         L.oracle_inflate.argtypes = [u8p, ctypes.c_size_t, u8p, ctypes.c_size_t, ctypes.c_void_p,
                                      ctypes.c_size_t, ctypes.POINTER(InflateResult)]
@@ -124,6 +127,32 @@ def inflater_run(parts, raw=False, dictionary=None, out_cap=None):
     lib().oracle_inflater_run(arr, lens, n, 1 if raw else 0, d, len(d) if d else 0, out, cap,
                               ctypes.byref(res))
     return _result_dict(res, out.raw[:res.total_out])
+
+
+def inflater_parts(parts, raw=False, dictionary=None, out_cap=None):
+    """inflater_run, plus the output of each append() (list of bytes) and the index of the
+    append that threw (or None)."""
+    parts = [bytes(p) for p in parts]
+    n = len(parts)
+    arr = (ctypes.c_char_p * n)(*parts)
+    lens = (ctypes.c_size_t * n)(*[len(p) for p in parts])
+    total_in = sum(len(p) for p in parts)
+    cap = out_cap if out_cap is not None else max(1 << 16, total_in * 1100 + 65536)
+    out = ctypes.create_string_buffer(cap)
+    res = InflateResult()
+    pout = (ctypes.c_size_t * max(1, n))()
+    ep = ctypes.c_int32(-1)
+    d = bytes(dictionary) if dictionary is not None else None
+    lib().oracle_inflater_run_parts(arr, lens, n, 1 if raw else 0, d, len(d) if d else 0, out, cap,
+                                    ctypes.byref(res), pout, ctypes.byref(ep))
+    r = _result_dict(res, out.raw[:res.total_out])
+    pieces, o = [], 0
+    for k in range(n):
+        pieces.append(r["data"][o:o + pout[k]])
+        o += pout[k]
+    r["parts_out"] = pieces
+    r["error_part"] = None if ep.value < 0 else ep.value
+    return r
 
 
 def inflate(data, dictionary=None, out_cap=None):

@@ -1124,7 +1124,17 @@ typedef struct {
 int32_t oracle_inflater_run(const uint8_t* const* parts, const size_t* part_lens, int32_t nparts,
                             int32_t raw, const uint8_t* dict, size_t dict_len,
                             uint8_t* out, size_t out_cap, oracle_inflate_result* res) {
+    return oracle_inflater_run_parts(parts, part_lens, nparts, raw, dict, dict_len, out, out_cap, res,
+                                     NULL, NULL);
+}
+
+int32_t oracle_inflater_run_parts(const uint8_t* const* parts, const size_t* part_lens, int32_t nparts,
+                                  int32_t raw, const uint8_t* dict, size_t dict_len,
+                                  uint8_t* out, size_t out_cap, oracle_inflate_result* res,
+                                  size_t* part_out, int32_t* err_part) {
     memset(res, 0, sizeof *res);
+    if (err_part) *err_part = -1;
+    if (part_out) for (int32_t k = 0; k < nparts; k++) part_out[k] = 0;
     if (raw && dict) { res->error = ORA_E_BAD_ARG; return res->error; }
     inflater* I = (inflater*)calloc(1, sizeof(inflater));
     if (!I) { res->error = ORA_E_BAD_ARG; return res->error; }
@@ -1134,7 +1144,9 @@ int32_t oracle_inflater_run(const uint8_t* const* parts, const size_t* part_lens
     size_t out_len = 0;
     int32_t err_code = ORA_OK;
 
-    for (int pi = 0; pi < nparts && err_code == ORA_OK; pi++) {
+    int pi = 0;
+    for (; pi < nparts && err_code == ORA_OK; pi++) {
+        size_t out_before = out_len;
         const uint8_t* chunk = parts[pi];
         int64_t chunk_len = (int64_t)part_lens[pi];
         if (chunk_len == 0) continue;                           /* sd-inflate.ts:92-94 */
@@ -1177,6 +1189,8 @@ int32_t oracle_inflater_run(const uint8_t* const* parts, const size_t* part_lens
                 guard_last_avail = z->avail_in;
             }
         } while (z->avail_in > 0 || z->avail_out == 0);
+        if (part_out) part_out[pi] = out_len - out_before;
+        if (err_code != ORA_OK && err_part) *err_part = pi;
     }
 
     /* finish(): sd-inflate.ts:159-179 */

@@ -68,6 +68,13 @@ int32_t oracle_inflater_run(const uint8_t* const* parts, const size_t* part_lens
                             int32_t raw, const uint8_t* dict, size_t dict_len,
                             uint8_t* out, size_t out_cap, oracle_inflate_result* res);
 
+/* The same, also reporting each append()'s output length (part_out[nparts], may be
+ * NULL) and the index of the append that threw (*err_part, -1 if none; may be NULL). */
+int32_t oracle_inflater_run_parts(const uint8_t* const* parts, const size_t* part_lens, int32_t nparts,
+                                  int32_t raw, const uint8_t* dict, size_t dict_len,
+                                  uint8_t* out, size_t out_cap, oracle_inflate_result* res,
+                                  size_t* part_out, int32_t* err_part);
+
 /* inflate(data, dictionary) one-shot: auto-detect + throw mapping (sd-inflate.ts:189-228). */
 int32_t oracle_inflate(const uint8_t* in, size_t in_len, const uint8_t* dict, size_t dict_len,
                        uint8_t* out, size_t out_cap, oracle_inflate_result* res);

@@ -35,15 +35,25 @@ struct DSave {
     int32_t stored_ck, stored_size, mtime;
     uint32_t name_off, name_len, stored_left;
     int32_t dict_used, full;
-    uint32_t ntok, litw, nlit, pad;
+    uint32_t ntok, litw, nlit;
+    int32_t stall;                    // incremental mode: 1 out of input, 2 out of output room
     Tree LL, DD;
 };
 
 // per-stream resolve state (phase 2)
 struct RSave {
-    uint64_t pos;
-    uint32_t s1, s2, crc, snap1, snap2;
-    int32_t ck;
+    uint64_t pos;                     // this call: output bytes resolved so far
+    uint32_t s1, s2;                  // this call: sum b, sum i b (mod 65521) of its output
+    int32_t ck;                       // sticky watchdog flag
+    uint32_t hist;                    // incremental: window[] holds the 32 KiB before this call
+    // incremental mode: kept across calls
+    uint64_t total;                   // output bytes of the earlier calls
+    uint64_t in_base;                 // stream offset of this call's staged input byte 0
+    uint32_t a1, a2;                  // Inflater.checksum (adler32.ts state) after earlier calls
+    uint32_t crc;                     // Inflater.checksum (crc32, gzip) after earlier calls
+    uint32_t carry_len;               // input bytes carried into the next call
+    uint64_t abase;                   // output position where the current append() began
+    uint32_t a1s, a2s;                // the (exact) adler32 state there
 };
 
 }  // namespace sdz

@@ -90,6 +90,11 @@ struct Lane : Core {
     uint32_t name_off, name_len, stored_left;
     int dict_used;
     uint8_t* lens;                    // global scratch for code lengths
+    // end of input: one-shot streams end TRUNCATED; incremental ones (streaming) rewind to
+    // the start of the unit in progress (ubit) and stall until the next call
+    const uint8_t* inp;
+    uint64_t tbits, ubit;
+    int streaming, stall;
 };
 
 // ------------------------------------------------------------------ bit reader
@@ -431,6 +436,16 @@ __device__ __forceinline__ void lane_fail(Core& L, int status, int zmsg) {
     L.zmsg = zmsg;
     L.mode = LM_DONE;
 }
+// The unit that started at bit L.ubit (a header, block header, symbol, stored byte or
+// trailer) cannot finish: out of input (why 1) or of output room (why 2).  A one-shot
+// stream ends there; an incremental one (Inflater.append across calls) is repositioned at
+// the unit's start and waits for the next call -- the reference stops its output at the
+// same place, holding the unit's bits in its bit buffer (infcodes.ts:367-387 need rule).
+__device__ __forceinline__ void lane_stall(Lane& L, int why) {
+    if (!L.streaming) { lane_fail(L, why == 1 ? SDZ_TRUNCATED : SDZ_OUT_OVERFLOW, 0); return; }
+    br_init(L, L.inp, L.ubit, L.tbits);
+    L.stall = why;
+}
 
 // ------------------------------------------------------------------ block setup
 
@@ -581,14 +596,14 @@ __device__ __forceinline__ bool setup_dynamic(Lane& L, Tree& LL, Tree& DD, uint8
 __device__ __forceinline__ void block_step(Lane& L, Tree& LL, Tree& DD, uint8_t* region) {
     if (L.mode == LM_TYPE) {
         uint32_t t;
-        if (!br_get(L, 3, t)) { lane_fail(L, SDZ_TRUNCATED, 0); return; }
+        if (!br_get(L, 3, t)) { lane_stall(L, 1); return; }
         L.last = (int)(t & 1);
         uint32_t bt = t >> 1;
         if (bt == 0) {                                   // stored (infblocks.ts:184-196, 243-277)
             uint64_t cons = br_consumed(L);
             br_drop(L, (uint32_t)((8 - (cons & 7)) & 7));
             uint32_t lo, hi;
-            if (!br_get(L, 16, lo) || !br_get(L, 16, hi)) { lane_fail(L, SDZ_TRUNCATED, 0); return; }
+            if (!br_get(L, 16, lo) || !br_get(L, 16, hi)) { lane_stall(L, 1); return; }
             if ((~hi & 0xffffu) != lo) { lane_fail(L, SDZ_DATA_ERROR, ZM_STORED_LENS); return; }
             L.stored_left = lo;
             L.mode = lo ? LM_STORED : (L.last ? LM_TRAILER : LM_TYPE);
@@ -596,7 +611,11 @@ __device__ __forceinline__ void block_step(Lane& L, Tree& LL, Tree& DD, uint8_t*
             setup_fixed(L, LL, DD, region);
             L.mode = LM_CODES;
         } else if (bt == 2) {
-            if (!setup_dynamic(L, LL, DD, region)) { L.mode = LM_DONE; return; }
+            if (!setup_dynamic(L, LL, DD, region)) {
+                if (L.status == SDZ_TRUNCATED) { L.status = SDZ_OK; lane_stall(L, 1); }
+                else L.mode = LM_DONE;
+                return;
+            }
             L.mode = LM_CODES;
         } else {
             lane_fail(L, SDZ_DATA_ERROR, ZM_BLOCK_TYPE);
@@ -606,8 +625,9 @@ __device__ __forceinline__ void block_step(Lane& L, Tree& LL, Tree& DD, uint8_t*
     if (L.mode == LM_STORED) {                            // infblocks.ts:278-333, resumable
         while (L.stored_left && !L.full) {
             uint32_t b;
-            if (!br_get(L, 8, b)) { lane_fail(L, SDZ_TRUNCATED, 0); return; }
-            if (L.room == 0) { lane_fail(L, SDZ_OUT_OVERFLOW, 0); return; }
+            L.ubit = br_consumed(L);
+            if (!br_get(L, 8, b)) { lane_stall(L, 1); return; }
+            if (L.room == 0) { lane_stall(L, 2); return; }
             tok_lit(L, b);
             L.room--;
             L.stored_left--;
@@ -624,7 +644,7 @@ __device__ __forceinline__ void block_step(Lane& L, Tree& LL, Tree& DD, uint8_t*
             uint32_t v = 0;
             for (int k = 0; k < 4; ++k) {
                 uint32_t b;
-                if (!br_get(L, 8, b)) { lane_fail(L, SDZ_TRUNCATED, 0); return; }
+                if (!br_get(L, 8, b)) { lane_stall(L, 1); return; }
                 v = (v << 8) | b;
             }
             L.stored_ck = (int32_t)v;
@@ -632,13 +652,13 @@ __device__ __forceinline__ void block_step(Lane& L, Tree& LL, Tree& DD, uint8_t*
             uint32_t v = 0, z = 0;
             for (int k = 0; k < 4; ++k) {
                 uint32_t b;
-                if (!br_get(L, 8, b)) { lane_fail(L, SDZ_TRUNCATED, 0); return; }
+                if (!br_get(L, 8, b)) { lane_stall(L, 1); return; }
                 v = (v >> 8) | (b << 24);
             }
             L.stored_ck = (int32_t)v;
             for (int k = 0; k < 4; ++k) {
                 uint32_t b;
-                if (!br_get(L, 8, b)) { lane_fail(L, SDZ_TRUNCATED, 0); return; }
+                if (!br_get(L, 8, b)) { lane_stall(L, 1); return; }
                 z = (z >> 8) | (b << 24);
             }
             L.stored_size = (int32_t)z;
@@ -714,12 +734,12 @@ __device__ __forceinline__ void slow_step(Lane& L, const Tree& LL, const Tree& D
     bool bad = rc >= LL.lim[15];
     int32_t idx = bad ? (int32_t)(LL.pk[15] >> 16) - 32768 + (int32_t)rc : pk_rank(v, rc);
     int len = bad ? 15 : 15 - (int)(v & 15u);
-    if (br_avail(L) < TREE_NEED(LL, len, idx)) { lane_fail(L, SDZ_TRUNCATED, 0); return; }
+    if (br_avail(L) < TREE_NEED(LL, len, idx)) { lane_stall(L, 1); return; }
     if (bad) { lane_fail(L, SDZ_DATA_ERROR, ZM_INVALID_LITLEN); return; }
     uint32_t b = region[idx];
     L.bo += (uint32_t)len;
     if (idx < (int32_t)((v >> 4) & 511u)) {
-        if (L.room == 0) { lane_fail(L, SDZ_OUT_OVERFLOW, 0); return; }
+        if (L.room == 0) { lane_stall(L, 2); return; }
         L.room--;
         tok_lit(L, b);
         return;
@@ -728,7 +748,7 @@ __device__ __forceinline__ void slow_step(Lane& L, const Tree& LL, const Tree& D
     if (b > 29) { lane_fail(L, SDZ_DATA_ERROR, ZM_INVALID_LITLEN); return; }
     uint32_t e;
     uint32_t mlen = len_base(b, e);
-    if (br_avail(L) < (int)e) { lane_fail(L, SDZ_TRUNCATED, 0); return; }
+    if (br_avail(L) < (int)e) { lane_stall(L, 1); return; }
     mlen += (pw >> len) & ((1u << e) - 1u);
     L.bo += e;
     br_refill(L);
@@ -738,15 +758,15 @@ __device__ __forceinline__ void slow_step(Lane& L, const Tree& LL, const Tree& D
     bad = rc >= DD.lim[15];
     idx = bad ? (int32_t)(DD.pk[15] >> 16) - 32768 + (int32_t)rc : pk_rank(v, rc);
     len = bad ? 15 : 15 - (int)(v & 15u);
-    if (br_avail(L) < TREE_NEED(DD, len, idx)) { lane_fail(L, SDZ_TRUNCATED, 0); return; }
+    if (br_avail(L) < TREE_NEED(DD, len, idx)) { lane_stall(L, 1); return; }
     if (bad) { lane_fail(L, SDZ_DATA_ERROR, ZM_INVALID_DIST); return; }
     uint32_t ds = region[IL_DSYM + idx];
     L.bo += (uint32_t)len;
     uint32_t dist = dist_base(ds, e);
-    if (br_avail(L) < (int)e) { lane_fail(L, SDZ_TRUNCATED, 0); return; }
+    if (br_avail(L) < (int)e) { lane_stall(L, 1); return; }
     dist += (pw >> len) & ((1u << e) - 1u);
     L.bo += e;
-    if (L.room < mlen) { lane_fail(L, SDZ_OUT_OVERFLOW, 0); return; }
+    if (L.room < mlen) { lane_stall(L, 2); return; }
     L.room -= mlen;
     tok_match(L, mlen, dist);
 }
@@ -766,53 +786,53 @@ __device__ __forceinline__ void parse_container(Lane& L, int32_t format, int32_t
     if (raw) return;
     uint32_t b = 0, method = 0, flg = 0, v = 0;
     bool gz = false;
-    if (!br_get(L, 8, b)) { lane_fail(L, SDZ_TRUNCATED, 0); return; }
+    if (!br_get(L, 8, b)) { lane_stall(L, 1); return; }
     if (b == 0x1f) {
-        if (!br_get(L, 8, b)) { lane_fail(L, SDZ_TRUNCATED, 0); return; }
+        if (!br_get(L, 8, b)) { lane_stall(L, 1); return; }
         if (b != 0x8b) { lane_fail(L, SDZ_DATA_ERROR, ZM_INVALID_GZIP_ID); return; }
         gz = true;
-        if (!br_get(L, 8, method)) { lane_fail(L, SDZ_TRUNCATED, 0); return; }
+        if (!br_get(L, 8, method)) { lane_stall(L, 1); return; }
     } else {
         method = b;
     }
     if ((method & 0xf) != 8) { lane_fail(L, SDZ_DATA_ERROR, ZM_UNKNOWN_METHOD); return; }
     if ((method >> 4) + 8 > 15) { lane_fail(L, SDZ_DATA_ERROR, ZM_INVALID_WINDOW); return; }
-    if (!br_get(L, 8, flg)) { lane_fail(L, SDZ_TRUNCATED, 0); return; }
+    if (!br_get(L, 8, flg)) { lane_stall(L, 1); return; }
     if (gz) {
         L.container = SDZ_CONTAINER_GZIP;
         uint32_t mt = 0;
         for (int k = 0; k < 4; ++k) {
-            if (!br_get(L, 8, v)) { lane_fail(L, SDZ_TRUNCATED, 0); return; }
+            if (!br_get(L, 8, v)) { lane_stall(L, 1); return; }
             mt = (mt >> 8) | (v << 24);
         }
         L.mtime = (int32_t)mt;
         for (int k = 0; k < 2; ++k)
-            if (!br_get(L, 8, v)) { lane_fail(L, SDZ_TRUNCATED, 0); return; }
-        if (flg & 4) { lane_fail(L, SDZ_TRUNCATED, 0); return; }   // inflate.ts:333-346 (EXTRA0 never advances)
+            if (!br_get(L, 8, v)) { lane_stall(L, 1); return; }
+        if (flg & 4) { lane_fail(L, SDZ_TRUNCATED, 0); return; }   // inflate.ts:333-346 (EXTRA0 never advances): final
         if (flg & 8) {
             L.name_off = (uint32_t)(br_consumed(L) >> 3);
             for (;;) {
-                if (!br_get(L, 8, v)) { lane_fail(L, SDZ_TRUNCATED, 0); return; }
+                if (!br_get(L, 8, v)) { lane_stall(L, 1); return; }
                 if (v == 0) break;
                 L.name_len++;
             }
         }
         if (flg & 16) {
             for (;;) {
-                if (!br_get(L, 8, v)) { lane_fail(L, SDZ_TRUNCATED, 0); return; }
+                if (!br_get(L, 8, v)) { lane_stall(L, 1); return; }
                 if (v == 0) break;
             }
         }
         if (flg & 2)
             for (int k = 0; k < 2; ++k)
-                if (!br_get(L, 8, v)) { lane_fail(L, SDZ_TRUNCATED, 0); return; }
+                if (!br_get(L, 8, v)) { lane_stall(L, 1); return; }
     } else {
         L.container = SDZ_CONTAINER_ZLIB;
         if (((method << 8) + flg) % 31 != 0) { lane_fail(L, SDZ_DATA_ERROR, ZM_HEADER_CHECK); return; }
         if (flg & 0x20) {
             uint32_t id = 0;
             for (int k = 0; k < 4; ++k) {
-                if (!br_get(L, 8, v)) { lane_fail(L, SDZ_TRUNCATED, 0); return; }
+                if (!br_get(L, 8, v)) { lane_stall(L, 1); return; }
                 id = (id << 8) | v;
             }
             if (!has_dict) { lane_fail(L, SDZ_NEED_DICT, ZM_NEED_DICT); return; }
@@ -831,11 +851,12 @@ __device__ __forceinline__ void parse_container(Lane& L, int32_t format, int32_t
 // are its own, so the symbol loop keeps a small register footprint.
 __device__ __noinline__ void cold_run(DSave* S, const uint8_t* inp, uint64_t ilen, uint64_t cap,
                                       uint32_t* tb, uint32_t tcap, uint8_t* lens, int32_t format, int32_t has_dict,
-                                      int32_t dict_adler, uint32_t init) {
+                                      int32_t dict_adler, uint32_t init, uint32_t streaming) {
     Lane L;
     Tree LL, DD;
     uint8_t* region = lane_region();
     L.tb = tb; L.ts = lane_stage(); L.tcap = tcap; L.lens = lens;
+    L.inp = inp; L.tbits = ilen * 8; L.streaming = (int)streaming; L.stall = 0; L.ubit = 0;
     if (init) {
         L.mode = LM_TYPE; L.last = 0; L.status = SDZ_OK; L.zmsg = 0; L.container = SDZ_CONTAINER_RAW;
         L.fixed = 0; L.nl = L.nd = 0; L.stored_ck = 0; L.stored_size = 0; L.mtime = 0;
@@ -845,6 +866,7 @@ __device__ __noinline__ void cold_run(DSave* S, const uint8_t* inp, uint64_t ile
         L.pos0 = 0;
         LL.l = DD.l = 0; LL.g = DD.g = 0; LL.kmin = DD.kmin = 1; LL.left = DD.left = 0;
         parse_container(L, format, has_dict, dict_adler, ilen);
+        if (L.stall) L.mode = LM_INIT;                   // incremental: header not complete yet
     } else {
         L.mode = S->mode; L.last = S->last; L.status = S->status; L.zmsg = S->zmsg;
         L.container = S->container; L.fixed = S->fixed; L.nl = S->nl; L.nd = S->nd;
@@ -859,9 +881,10 @@ __device__ __noinline__ void cold_run(DSave* S, const uint8_t* inp, uint64_t ile
     uint64_t r = cap - L.pos0;
     L.room = L.room0 = (uint32_t)(r > 0x7fffffffull ? 0x7fffffffull : r);
     for (;;) {
-        if (L.full || L.mode == LM_DONE) break;
+        if (L.full || L.mode == LM_DONE || L.stall) break;
+        L.ubit = br_consumed(L);
         if (L.mode == LM_CODES) {
-            if (br_avail(L) >= 64) break;
+            if (br_avail(L) >= 64 && L.room >= 258) break;   // the hot loop's preconditions
             slow_step(L, LL, DD, region);
             if (L.ntok + 3 > L.tcap) L.full = true;
         } else {
@@ -876,6 +899,7 @@ __device__ __noinline__ void cold_run(DSave* S, const uint8_t* inp, uint64_t ile
     S->name_off = L.name_off; S->name_len = L.name_len; S->stored_left = L.stored_left;
     S->dict_used = L.dict_used;
     S->ntok = L.ntok; S->litw = L.litw; S->nlit = L.nlit; S->full = L.full ? 1 : 0;
+    S->stall = L.stall;
     S->LL = LL; S->DD = DD;
 }
 
@@ -898,8 +922,13 @@ __device__ __forceinline__ void hot_save(const Hot& H, DSave* S) {
     S->mode = H.mode; S->last = H.last; S->status = H.status; S->zmsg = H.zmsg;
     S->ntok = H.ntok; S->litw = H.litw; S->nlit = H.nlit; S->full = H.full ? 1 : 0;
 }
+// one symbol step reads at most 48 bits and writes at most 258 bytes; below either
+// bound the cold path's exact end-of-input / end-of-room handling takes over
 __device__ __forceinline__ bool hot_ready(const Hot& H) {
-    return H.mode == LM_CODES && !H.full && br_avail(H) >= 64;
+    return H.mode == LM_CODES && !H.full && br_avail(H) >= 64 && H.room >= 258;
+}
+__device__ __forceinline__ bool can_hot(const DSave* S, uint64_t tbits, uint64_t cap) {
+    return S->mode == LM_CODES && !S->full && !S->stall && tbits - S->bitpos >= 64 && cap - S->pos >= 258;
 }
 
 // one epoch of the symbol loop: every lane with `hot` set decodes until no more
@@ -942,21 +971,23 @@ __global__ __launch_bounds__(IL_THREADS, 1) void k_inflate_decode(InflateArgs A,
         inp = A.in + A.in_off[sid];
         ilen = A.in_len[sid];
         cap = A.out_cap[sid];
-        if (round == 0) {
+        // a call's first round starts a stream (one-shot, or an incremental stream whose
+        // header is still incomplete) or resumes it (later rounds; incremental calls)
+        const bool resume = round > 0 || (A.streaming && S->mode != LM_INIT);
+        if (round == 0 && (A.out_off[sid] & 7)) {
+            S->mode = LM_DONE; S->status = SDZ_BAD_RECORD; S->zmsg = 0; S->bitpos = 0; S->pos = 0;
+            S->container = SDZ_CONTAINER_RAW; S->stored_ck = 0; S->stored_size = 0; S->mtime = 0;
+            S->name_off = 0; S->name_len = 0; S->dict_used = 0; S->ntok = 0; S->litw = 0;
+            S->nlit = 0; S->full = 0; S->stall = 0;
+        } else if (!resume) {
             live = true;
-            if (A.out_off[sid] & 7) {
-                S->mode = LM_DONE; S->status = SDZ_BAD_RECORD; S->zmsg = 0; S->bitpos = 0; S->pos = 0;
-                S->container = SDZ_CONTAINER_RAW; S->stored_ck = 0; S->stored_size = 0; S->mtime = 0;
-                S->name_off = 0; S->name_len = 0; S->dict_used = 0; S->ntok = 0; S->litw = 0;
-                S->nlit = 0; S->full = 0;
-            } else {
-                cold_run(S, inp, ilen, cap, tb, A.round_tokens, lens, A.format,
-                         A.dict != nullptr, A.dict_adler, 1u);
-            }
-        } else if (S->mode != LM_DONE) {
+            cold_run(S, inp, ilen, cap, tb, A.round_tokens, lens, A.format,
+                     A.dict != nullptr, A.dict_adler, 1u, A.streaming);
+        } else if (S->mode != LM_DONE && !(round > 0 && S->stall)) {
             live = true;
             for (int k = 0; k < IL_REGION / 4; ++k) ((uint32_t*)region)[k] = ((const uint32_t*)S->region)[k];
             S->ntok = 0; S->full = 0;
+            if (round == 0) { S->pos = 0; S->stall = 0; }      // a new call: fresh output slot
         }
     }
     // epochs: lanes that need block-level work do it together (cold_run), then
@@ -964,13 +995,13 @@ __global__ __launch_bounds__(IL_THREADS, 1) void k_inflate_decode(InflateArgs A,
     // eighth of them has left the fast path; state is parked in DSave in between
     uint64_t tbits = ilen * 8;
     for (;;) {
-        bool hot = live && S->mode == LM_CODES && !S->full && tbits - S->bitpos >= 64;
-        bool cold = live && !S->full && S->mode != LM_DONE && !hot;
+        bool hot = live && can_hot(S, tbits, cap);
+        bool cold = live && !S->full && !S->stall && S->mode != LM_DONE && !hot;
         if (__ballot(cold)) {
             if (cold)
                 cold_run(S, inp, ilen, cap, tb, A.round_tokens, lens, A.format,
-                         A.dict != nullptr, A.dict_adler, 0u);
-            hot = live && S->mode == LM_CODES && !S->full && tbits - S->bitpos >= 64;
+                         A.dict != nullptr, A.dict_adler, S->mode == LM_INIT ? 1u : 0u, A.streaming);
+            hot = live && can_hot(S, tbits, cap);
         }
         uint64_t hm = __ballot(hot);
         if (hm == 0) break;
@@ -978,7 +1009,7 @@ __global__ __launch_bounds__(IL_THREADS, 1) void k_inflate_decode(InflateArgs A,
         hot_epoch(S, inp, ilen, cap, tb, A.round_tokens, hot, nhot - (nhot >= 16 ? nhot >> 3 : 1));
     }
 
-    bool more = live && S->mode != LM_DONE;
+    bool more = live && S->mode != LM_DONE && !S->stall;
     uint64_t mm = __ballot(more);                        // one counter update per wave
     if (mm && (threadIdx.x & 63u) == (uint32_t)__builtin_ctzll(mm)) atomicAdd(A.active, (uint32_t)__popcll(mm));
     if (!live) {
@@ -992,7 +1023,8 @@ __global__ __launch_bounds__(IL_THREADS, 1) void k_inflate_decode(InflateArgs A,
         S->ntok = H.ntok; S->litw = 0; S->nlit = 0;
         A.ntok[sid] = H.ntok;
     }
-    A.flags[sid] = S->mode == LM_DONE ? 1u : 0u;
+    // 0: more rounds; 1: finished this round; 3: stalled (incremental: done for this call)
+    A.flags[sid] = S->mode == LM_DONE ? 1u : S->stall ? 3u : 0u;
     if (S->mode != LM_DONE)
         for (int k = 0; k < IL_REGION / 4; ++k) ((uint32_t*)S->region)[k] = ((const uint32_t*)region)[k];
 }
@@ -1002,8 +1034,9 @@ uint32_t resolve_block_threads();
 uint32_t resolve_streams_per_block();
 void launch_inflate_finalize(const InflateArgs& a, hipStream_t s);
 
-uint64_t inflate_dsave_bytes() { return (sizeof(DSave) + 15) & ~(uint64_t)15; }
-uint64_t inflate_rsave_bytes() { return (sizeof(RSave) + 15) & ~(uint64_t)15; }
+// the state arrays are indexed as DSave* / RSave* arrays: the strides are the struct sizes
+uint64_t inflate_dsave_bytes() { return sizeof(DSave); }
+uint64_t inflate_rsave_bytes() { return sizeof(RSave); }
 
 // host driver: rounds of (decode, resolve) until no stream needs another round.
 // kernel_ms (optional, 3 entries) accumulates decode / resolve / finalize times.

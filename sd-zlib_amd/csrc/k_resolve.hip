@@ -93,18 +93,25 @@ __device__ __forceinline__ void lds_put(uint32_t* p, uint32_t v) {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
-// adler32.ts:34-105 over r bytes seeded with the chunk-start state (NMAX quirk)
-__device__ int32_t adler_quirk_tail(const uint8_t* p, uint32_t r, uint32_t s1, uint32_t s2in) {
+__device__ __forceinline__ uint32_t ridx64(int64_t p) {         // ring index of a (call-relative) position
+    int64_t x = p % RS_R;
+    return (uint32_t)(x < 0 ? x + RS_R : x);
+}
+
+// adler32.ts:34-105 over the r ring bytes from position p0, seeded with the chunk-start
+// state (NMAX quirk: sum2 += BASE instead of a reduction after each 5552-byte block)
+__device__ int32_t adler_quirk_ring(const uint8_t* ring, int64_t p0, uint32_t r, uint32_t s1, uint32_t s2in) {
     uint64_t a = s1, s2 = s2in;
-    uint32_t off = 0, len = r;
+    int64_t off = p0;
+    uint32_t len = r;
     while (len >= 5552) {
         len -= 5552;
-        for (int i = 0; i < 5552; ++i) { a += p[off++]; s2 += a; }
+        for (int i = 0; i < 5552; ++i) { a += ring[ridx64(off++)]; s2 += a; }
         a %= 65521u;
         s2 += 65521u;
     }
     if (len) {
-        while (len--) { a += p[off++]; s2 += a; }
+        while (len--) { a += ring[ridx64(off++)]; s2 += a; }
         a %= 65521u;
         s2 %= 65521u;
     }
@@ -359,9 +366,11 @@ __global__ __launch_bounds__(RS_THREADS) __attribute__((amdgpu_waves_per_eu(RS_W
     const uint32_t sid = blockIdx.x;
     if (sid >= A.n) return;
     const uint32_t flag = A.flags[sid];
-    if (flag == 2) return;
+    // incremental mode: a stream that finished in an earlier call still gets its record
+    const bool fin0 = A.streaming && round == 0 && flag == 2;
+    if (flag == 2 && !fin0) return;
     RSave* R = (RSave*)A.rsave + sid;
-    const DSave* S = (const DSave*)A.dsave + sid;
+    DSave* S = (DSave*)A.dsave + sid;
     const bool gz = S->container == SDZ_CONTAINER_GZIP;
     const uint64_t pos0 = round == 0 ? 0 : R->pos;
     uint8_t* out = A.out + A.out_off[sid];
@@ -370,12 +379,18 @@ __global__ __launch_bounds__(RS_THREADS) __attribute__((amdgpu_waves_per_eu(RS_W
     const int64_t dl = S->dict_used && A.dict ? (A.dict_len > 32767 ? 32767 : A.dict_len) : 0;
     const uint8_t* dict = dl ? A.dict + (A.dict_len - dl) : nullptr;
 
-    // the window: output bytes [pos0 - 32 KiB, pos0), the dictionary / zeros before 0
+    // the window: output bytes [pos0 - 32 KiB, pos0); before position 0 of this call, the
+    // window saved by the previous call (incremental mode), else the dictionary / zeros
     const uint32_t rp0 = (uint32_t)(pos0 % RS_R);
     const uint32_t pm0 = (uint32_t)(pos0 % 65521u);
-    if (pos0 == 0 && dl == 0) {
-        // a stream's first round without a dictionary: zeros, ring bytes [RS_R - RS_WIN, RS_R)
-        static_assert((RS_R - RS_WIN) % 16 == 0, "ring window start must be 16-aligned");
+    const uint8_t* hist = A.streaming && R->hist ? A.window + (uint64_t)sid * IS_WIN : nullptr;
+    static_assert((RS_R - RS_WIN) % 16 == 0 && IS_WIN == RS_WIN, "ring window start must be 16-aligned");
+    if (pos0 == 0 && hist) {
+        // ring bytes [RS_R - RS_WIN, RS_R) hold positions [-32 KiB, 0)
+        for (uint32_t k = tid; k < RS_WIN / 16; k += RS_THREADS)
+            ((uint4*)(ring + (RS_R - RS_WIN)))[k] = ((const uint4*)hist)[k];
+    } else if (pos0 == 0 && dl == 0) {
+        // a stream's first round without a dictionary: zeros
         for (uint32_t k = tid; k < RS_WIN / 16; k += RS_THREADS)
             ((uint4*)(ring + (RS_R - RS_WIN)))[k] = make_uint4(0, 0, 0, 0);
     } else {
@@ -383,6 +398,7 @@ __global__ __launch_bounds__(RS_THREADS) __attribute__((amdgpu_waves_per_eu(RS_W
             const int64_t p = (int64_t)pos0 - RS_WIN + k;
             uint32_t b = 0;
             if (p >= 0) b = round ? out[p] : 0u;
+            else if (hist) b = hist[RS_WIN + p];
             else if (p >= -dl) b = dict[dl + p];
             ring[ridx((int32_t)rp0 - RS_WIN + (int32_t)k)] = (uint8_t)b;
         }
@@ -608,51 +624,97 @@ __global__ __launch_bounds__(RS_THREADS) __attribute__((amdgpu_waves_per_eu(RS_W
     }
     __syncthreads();                                     // R->s1 / s2 were read above
     if (tid == 0) { R->pos = pos; R->s1 = S_all; R->s2 = T_all; R->ck = failed ? 1 : 0; }
-    if (flag != 1) return;
-    // Inflater chunk-wise checksum (16 KiB chunks, adler32.ts NMAX quirk): only a final
-    // chunk of 5552 or 11104 bytes differs from the plain adler32; then replay that
-    // chunk from the state at its start, S and T of the bytes before it
-    const uint32_t r = (uint32_t)(pos & 16383u);
-    const bool quirk = !gz && !failed && (r == 5552u || r == 11104u);
-    uint32_t snapS = S_all, snapT = T_all;
+    const bool fin = flag == 1 || flag == 3 || fin0;    // the stream's last round of this call
+    if (!fin) return;
+    const uint64_t bitpos = S->bitpos;
+    const uint64_t ilen = A.in_len[sid];
+    uint32_t carry_n = 0;
+    uint64_t keep_end = 0;
+    bool carry_over = false;
+    if (A.streaming && flag == 3) {
+        // stalled: keep the window (the 32 KiB before the next call's output) and the input
+        // from the unit in progress on (the bits the reference holds in its bit buffer)
+        uint8_t* win = A.window + (uint64_t)sid * IS_WIN;
+        const uint32_t wb = (uint32_t)((pos % RS_R + RS_R - RS_WIN) % RS_R);   // ring index of pos - 32 KiB
+        for (uint32_t k = tid; k < RS_WIN; k += RS_THREADS) win[k] = ring[(wb + k) % RS_R];
+        // out of input: all of it from the unit's first byte; out of room: only the carried
+        // bytes -- the caller passes its own unconsumed bytes again (from in_used on)
+        const uint64_t cb = bitpos >> 3;
+        const uint64_t nc = R->carry_len;
+        keep_end = S->stall == 2 ? (cb > nc ? cb : nc) : ilen;
+        carry_n = (uint32_t)(keep_end - cb);
+        carry_over = keep_end - cb > SDZ_INFLATE_CARRY;
+        if (!carry_over) {
+            const uint8_t* src = A.in + A.in_off[sid] + cb;
+            uint8_t* dst = A.carry + (uint64_t)sid * SDZ_INFLATE_CARRY;
+            for (uint32_t k = tid; k < carry_n; k += RS_THREADS) dst[k] = src[k];
+        }
+    }
+    // Inflater.checksum (sd-inflate.ts:136-146): adler32 over 16 KiB output chunks counted
+    // from the start of each append()'s output (abase), with the NMAX quirk (adler32.ts:67):
+    // a final chunk of 5552 or 11104 bytes leaves sum2 unreduced.  Every other chunk ends
+    // reduced, so the value is the plain adler32 state except after such a chunk, which is
+    // replayed from the state at its start -- recovered from the plain state at its end and
+    // its bytes (the last <= 11104 output bytes are in the ring).
+    const bool cont_next = A.streaming && flag == 3 && S->stall == 2;   // this append continues
+    const uint64_t T0 = A.streaming ? R->total : 0, T1 = T0 + pos;
+    const uint64_t abase = A.streaming ? R->abase : 0;
+    const uint32_t rr = (uint32_t)((T1 - abase) & 16383u);
+    const bool quirk = !gz && !failed && !cont_next && (rr == 5552u || rr == 11104u);
+    uint64_t qa = 0, qb = 0;                              // sum b_j, sum (rr - j) b_j of that chunk
     if (quirk) {
-        uint64_t a = 0, b = 0;
-        const uint64_t c = pos - r;
-        for (uint32_t k = tid; k < r; k += RS_THREADS) {
-            const uint32_t v = out[c + k];
-            a += v;
-            b += (uint64_t)((c + k) % 65521u) * v;
+        for (uint32_t k = tid; k < rr; k += RS_THREADS) {
+            const uint32_t v = ring[ridx64((int64_t)pos - rr + k)];
+            qa += v;
+            qb += (uint64_t)(rr - k) * v;
         }
 #pragma unroll
-        for (int o = 32; o > 0; o >>= 1) { a += __shfl_xor(a, o); b += __shfl_xor(b, o); }
-        if (lane == 0) { red[w][0] = a; red[w][1] = b; }
+        for (int o = 32; o > 0; o >>= 1) { qa += __shfl_xor(qa, o); qb += __shfl_xor(qb, o); }
+        if (lane == 0) { red[w][0] = qa; red[w][1] = qb; }
         __syncthreads();
-        uint64_t ta = 0, tb = 0;
+        qa = 0; qb = 0;
 #pragma unroll
-        for (int q = 0; q < RS_WAVES; ++q) { ta += red[q][0]; tb += red[q][1]; }
-        snapS = (uint32_t)((S_all + 65521u - mod65521(ta)) % 65521u);
-        snapT = (uint32_t)((T_all + 65521u - mod65521(tb)) % 65521u);
+        for (int q = 0; q < RS_WAVES; ++q) { qa += red[q][0]; qb += red[q][1]; }
     }
+    __syncthreads();                                      // window / carry copies done
     if (tid != 0) return;
+    if (carry_over) { S->mode = LM_DONE; S->status = SDZ_CARRY_OVERFLOW; S->zmsg = 0; }
     // final: record + verdicts (sd-inflate.ts:134-179); gzip's crc32 comes from k_inflate_finalize
     sdz_inflate_record Rc;
     Rc.status = failed ? SDZ_INTERNAL : S->status;
     Rc.zmsg = failed ? (int32_t)fail : S->zmsg;      // watchdog: site | position << 4
     Rc.out_len = pos;
-    uint64_t ib = S->bitpos;
-    uint64_t ilen = A.in_len[sid];
-    Rc.in_used = (ib + 7) >> 3;
-    if (Rc.in_used > ilen) Rc.in_used = ilen;
+    uint64_t used = (bitpos + 7) >> 3;
+    if (used > ilen) used = ilen;
+    // incremental: the stream offset up to which input is consumed or held by the device
+    Rc.in_used = A.streaming ? R->in_base + (flag == 3 && !carry_over ? keep_end : used) : used;
     Rc.stored_checksum = S->stored_ck;
-    bool have = pos > 0;                                  // Inflater.checksum stays undefined otherwise
+    const uint64_t total = T1;
+    bool have = total > 0;                                // Inflater.checksum stays undefined otherwise
     int32_t running = 0;
+    uint32_t a1 = A.streaming ? R->a1 : 1u, a2 = A.streaming ? R->a2 : 0u;   // state at T0 (exact)
     if (!gz) {
-        const uint64_t n = quirk ? pos - r : pos;
-        const uint32_t nm = mod65521(n), Sx = quirk ? snapS : S_all, Tx = quirk ? snapT : T_all;
-        const uint32_t a1 = (1u + Sx) % 65521u;
-        const uint32_t a2 = (uint32_t)(((uint64_t)nm + (uint64_t)nm * Sx + 65521ull * 65521ull - Tx) % 65521u);
-        if (quirk) running = adler_quirk_tail(out + (pos - r), r, a1, a2);
-        else running = (int32_t)(a1 | (a2 << 16));
+        if (pos) {                                        // no output keeps the exact (quirky) state
+            const uint32_t nm = mod65521(pos);
+            const uint32_t b1 = (uint32_t)(((uint64_t)a1 + S_all) % 65521u);
+            const uint32_t b2 = (uint32_t)(((uint64_t)a2 + (uint64_t)nm * a1 + (uint64_t)nm * S_all +
+                                            65521ull * 65521ull - T_all) % 65521u);
+            a1 = b1;
+            a2 = b2;
+        }
+        if (quirk) {
+            uint32_t s1s, s2s;                            // state at the final chunk's start
+            if (T1 - rr == abase) {
+                s1s = A.streaming ? R->a1s : 1u;
+                s2s = A.streaming ? R->a2s : 0u;
+            } else {
+                s1s = (uint32_t)((a1 + 65521u - mod65521(qa)) % 65521u);
+                s2s = (uint32_t)(((uint64_t)a2 + 65521ull * 65521ull - (uint64_t)rr * s1s - mod65521(qb)) % 65521u);
+            }
+            running = adler_quirk_ring(ring, (int64_t)pos - rr, rr, s1s, s2s);
+        } else {
+            running = (int32_t)(a1 | (a2 << 16));
+        }
     }
     Rc.running_checksum = have ? running : 0;
     Rc.stored_size = S->stored_size;
@@ -664,12 +726,26 @@ __global__ __launch_bounds__(RS_THREADS) __attribute__((amdgpu_waves_per_eu(RS_W
     Rc.complete = complete ? 1 : 0;
     uint8_t cv = S->stored_ck == 0 ? SDZ_UNCHECKED : ((have && S->stored_ck == running) ? SDZ_MATCH : SDZ_MISMATCH);
     uint8_t sv = S->stored_size == 0 ? SDZ_UNCHECKED
-               : ((int64_t)S->stored_size == (int64_t)pos ? SDZ_MATCH : SDZ_MISMATCH);
+               : ((int64_t)S->stored_size == (int64_t)total ? SDZ_MATCH : SDZ_MISMATCH);
     Rc.checksum_verdict = cv;
     Rc.size_verdict = sv;
     Rc.success = (complete && cv != SDZ_MISMATCH && sv != SDZ_MISMATCH) ? 1 : 0;
-    for (int k = 0; k < 11; ++k) Rc.reserved[k] = 0;
+    Rc.out_full = S->mode != LM_DONE && S->stall == 2 ? 1 : 0;
+    if (!complete && Rc.status == SDZ_OK) Rc.status = SDZ_TRUNCATED;   // incremental: needs more input
+    for (int k = 0; k < 10; ++k) Rc.reserved[k] = 0;
     A.rec[sid] = Rc;
+    if (A.streaming) {                                    // state for the next call
+        R->total = total;
+        if (!gz && have) { R->a1 = (uint32_t)running & 0xffffu; R->a2 = (uint32_t)running >> 16; }
+        if (flag == 3 && !carry_over) {
+            R->in_base += bitpos >> 3;
+            R->carry_len = carry_n;
+            R->hist = 1;
+            S->bitpos = bitpos & 7;
+        } else {
+            R->carry_len = 0;
+        }
+    }
 }
 
 // ------------------------------------------------------------------ gzip: crc32 + verdicts
@@ -685,9 +761,16 @@ __global__ __launch_bounds__(64) void k_inflate_finalize(InflateArgs A) {
     crc_tables_init(ct);
     __syncthreads();
     const uint64_t len = rec->out_len;
-    const uint32_t crc = crc32_wave(A.out + A.out_off[sid], len, ct);
+    uint32_t crc = crc32_wave(A.out + A.out_off[sid], len, ct);
     if (threadIdx.x != 0) return;
-    const bool have = len > 0;
+    RSave* R = (RSave*)A.rsave + sid;
+    bool have = len > 0;
+    if (A.streaming) {
+        // crc32(chunk, seed) chains: crc(A B) = crc(A) x^(8 |B|) + crc(B) mod P
+        crc = gf2_mulmod(gf2_xbytes(len, ct.x2n), R->crc) ^ crc;
+        R->crc = crc;
+        have = R->total > 0;
+    }
     const int32_t running = (int32_t)crc;
     rec->running_checksum = have ? running : 0;
     const uint8_t cv = rec->stored_checksum == 0 ? SDZ_UNCHECKED

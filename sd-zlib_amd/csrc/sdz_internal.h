@@ -16,6 +16,7 @@ enum ZMsg : int32_t {
 
 // bytes of per-stream global scratch used by the inflate kernel (code lengths)
 constexpr uint64_t kInflateScratchPerStream = 320;
+#define IS_WIN 32768u                 // incremental mode: window bytes per stream
 
 struct InflateArgs {
     const uint8_t* in;
@@ -40,11 +41,20 @@ struct InflateArgs {
     uint32_t* flags;             // n: 0 more rounds, 1 finished this round, 2 finished earlier
     uint32_t* active;            // 1 counter
     unsigned long long* dbg;     // phase cycle counters (SDZ_PHASE_TIMING), normally null
+    // incremental mode (sdz_inflate_append_batch_device): input may continue in a later
+    // call, so streams stall at the end of their input instead of ending TRUNCATED
+    uint32_t streaming;
+    uint8_t* window;             // n * 32 KiB: the 32 KiB before this call's output
+    uint8_t* carry;              // n * SDZ_INFLATE_CARRY: input carried to the next call
 };
 
 uint64_t inflate_dsave_bytes();  // per stream decode state
 uint64_t inflate_rsave_bytes();  // per stream resolve state
 int run_inflate_rounds(const InflateArgs& a, hipStream_t s, uint32_t* host_active, float* kernel_ms);
+// incremental mode: fresh state / stage carry + chunk contiguously (k_istream.hip)
+void launch_istate_reset(uint8_t* dsave, uint8_t* rsave, uint32_t n, hipStream_t s);
+void launch_istate_stage(const InflateArgs& a, const uint8_t* in, const uint64_t* in_off, const uint64_t* in_len,
+                         uint8_t* stage, uint64_t stride, uint64_t* st_off, uint64_t* st_len, hipStream_t s);
 
 struct DeflateArgs {
     const uint8_t* in;

@@ -98,6 +98,7 @@ struct Pool {
 };
 Pool g_inflate_scratch, g_deflate_state, g_tmp, g_stage;
 constexpr size_t kTmpFname = 256;     // g_tmp layout: [0, 256) small results, then the file name
+constexpr uint64_t kInflaterOutCap = 4ull << 20;   // sdz_inflater: output slot per device call
 
 // records the pool's event on every exit path once get() succeeded
 struct PoolUse {
@@ -250,23 +251,19 @@ float sdz_last_kernel_ms(void) {
 
 // ----------------------------------------------------------------- inflate
 
-int sdz_inflate_batch_device(const uint8_t* in, const uint64_t* in_off, const uint64_t* in_len,
-                             uint8_t* out, const uint64_t* out_off, const uint64_t* out_cap,
-                             sdz_inflate_record* rec, uint32_t n, int32_t format,
-                             const uint8_t* dict, uint32_t dict_len, void* stream) {
-    if (int rc = ensure_device()) return rc;
-    if (n == 0) return SDZ_API_OK;
-    if (!in || !in_off || !in_len || !out || !out_off || !out_cap || !rec)
-        return fail(SDZ_API_BAD_ARG, "sdz_inflate_batch_device: null pointer");
-    if (format < SDZ_FMT_AUTO || format > SDZ_FMT_CONTAINER)
-        return fail(SDZ_API_BAD_ARG, "sdz_inflate_batch_device: bad format");
-    hipStream_t s = (hipStream_t)stream;
-    std::lock_guard<std::mutex> lk(g_mu);
-    // per-stream slabs: code lengths | decode state | resolve state, then the token
-    // ring (round_tokens per stream, bounded to ~4 GiB in total), flags, counter
+}  // extern "C"
+
+namespace {
+
+// Scratch of one inflate call: per-stream code lengths, then (one-shot) decode and resolve
+// state, the token ring (round_tokens per stream; C2's streams finish in one round),
+// ntok / flags / the active counter, and `extra` bytes for the caller (incremental staging).
+// Fills the round machinery of `a`; returns the extra region or an error via rc.
+int inflate_scratch(InflateArgs& a, uint32_t n, bool own_state, size_t extra, hipStream_t s,
+                    PoolUse& use, uint8_t** extra_out) {
     const uint64_t dsb = inflate_dsave_bytes(), rsb = inflate_rsave_bytes();
     // tokens per stream per round: as many as a quarter of free HBM (at most 32 GiB) allows,
-    // up to 128 Ki (C2's streams then finish in one round); SDZ_ROUND_TOKENS overrides
+    // up to 128 Ki; SDZ_ROUND_TOKENS overrides
     size_t mem_free = 0, mem_total = 0;
     if (hipMemGetInfo(&mem_free, &mem_total) != hipSuccess) mem_free = 16ull << 30;
     uint64_t budget = std::min<uint64_t>(32ull << 30, mem_free / 4);
@@ -275,32 +272,25 @@ int sdz_inflate_batch_device(const uint8_t* in, const uint64_t* in_off, const ui
     uint32_t T = (uint32_t)std::min<uint64_t>(want, std::max<uint64_t>(1024, budget / (4ull * n)));
     T = std::max<uint32_t>(64, T & ~31u);
     const size_t off_ds = (size_t)n * kInflateScratchPerStream;
-    const size_t off_rs = off_ds + (size_t)n * dsb;
-    const size_t off_tk = (off_rs + (size_t)n * rsb + 255) & ~(size_t)255;
+    const size_t off_rs = off_ds + (own_state ? (size_t)n * dsb : 0);
+    const size_t off_tk = (off_rs + (own_state ? (size_t)n * rsb : 0) + 255) & ~(size_t)255;
     const size_t off_nt = off_tk + (size_t)n * T * 4;
-    size_t bytes = off_nt + (size_t)n * 8 + 256;
-    int32_t dict_adler = 1;
-    if (dict) {
-        if (int rc = device_checksum(dict, dict_len, 0, 1, &dict_adler, s)) return rc;
-    }
+    const size_t off_ex = (off_nt + (size_t)n * 8 + 256 + 255) & ~(size_t)255;
     void* scratch = nullptr;
-    PoolUse use(g_inflate_scratch, s);
-    if (int rc = use.get(bytes, &scratch)) return rc;
+    if (int rc = use.get(off_ex + extra, &scratch)) return rc;
     uint8_t* base = (uint8_t*)scratch;
-    InflateArgs a;
-    a.in = in; a.in_off = in_off; a.in_len = in_len;
-    a.out = out; a.out_off = out_off; a.out_cap = out_cap;
-    a.rec = rec;
     a.scratch = base;
-    a.dict = dict; a.dict_len = dict_len; a.dict_adler = dict_adler;
-    a.n = n; a.format = format;
-    a.dsave = base + off_ds;
-    a.rsave = base + off_rs;
+    if (own_state) { a.dsave = base + off_ds; a.rsave = base + off_rs; }
     a.tokens = (uint32_t*)(base + off_tk);
     a.round_tokens = T;
     a.ntok = (uint32_t*)(base + off_nt);
     a.flags = a.ntok + n;
     a.active = a.flags + n;
+    if (extra_out) *extra_out = base + off_ex;
+    return SDZ_API_OK;
+}
+
+int inflate_run(InflateArgs& a, hipStream_t s) {
     static thread_local uint32_t host_active = 0;
     a.dbg = nullptr;
     const bool phases = getenv("SDZ_PHASE_TIMING") != nullptr;   // development aid
@@ -323,6 +313,111 @@ int sdz_inflate_batch_device(const uint8_t* in, const uint64_t* in_off, const ui
     }
     HIPCHK(hipGetLastError());
     return SDZ_API_OK;
+}
+
+// incremental-mode state slab: DSave[n] | RSave[n] | window[n][32 KiB] | carry[n][CARRY]
+struct IStateLayout {
+    size_t ds, rs, win, carry, bytes;
+    explicit IStateLayout(uint32_t n) {
+        ds = 0;
+        rs = ((size_t)n * inflate_dsave_bytes() + 255) & ~(size_t)255;
+        win = (rs + (size_t)n * inflate_rsave_bytes() + 255) & ~(size_t)255;
+        carry = win + (size_t)n * IS_WIN;
+        bytes = carry + (size_t)n * SDZ_INFLATE_CARRY;
+    }
+};
+
+}  // namespace
+
+extern "C" {
+
+int sdz_inflate_batch_device(const uint8_t* in, const uint64_t* in_off, const uint64_t* in_len,
+                             uint8_t* out, const uint64_t* out_off, const uint64_t* out_cap,
+                             sdz_inflate_record* rec, uint32_t n, int32_t format,
+                             const uint8_t* dict, uint32_t dict_len, void* stream) {
+    if (int rc = ensure_device()) return rc;
+    if (n == 0) return SDZ_API_OK;
+    if (!in || !in_off || !in_len || !out || !out_off || !out_cap || !rec)
+        return fail(SDZ_API_BAD_ARG, "sdz_inflate_batch_device: null pointer");
+    if (format < SDZ_FMT_AUTO || format > SDZ_FMT_CONTAINER)
+        return fail(SDZ_API_BAD_ARG, "sdz_inflate_batch_device: bad format");
+    hipStream_t s = (hipStream_t)stream;
+    std::lock_guard<std::mutex> lk(g_mu);
+    int32_t dict_adler = 1;
+    if (dict) {
+        if (int rc = device_checksum(dict, dict_len, 0, 1, &dict_adler, s)) return rc;
+    }
+    InflateArgs a{};
+    PoolUse use(g_inflate_scratch, s);
+    if (int rc = inflate_scratch(a, n, true, 0, s, use, nullptr)) return rc;
+    a.in = in; a.in_off = in_off; a.in_len = in_len;
+    a.out = out; a.out_off = out_off; a.out_cap = out_cap;
+    a.rec = rec;
+    a.dict = dict; a.dict_len = dict_len; a.dict_adler = dict_adler;
+    a.n = n; a.format = format;
+    a.streaming = 0; a.window = nullptr; a.carry = nullptr;
+    return inflate_run(a, s);
+}
+
+uint64_t sdz_inflate_state_bytes(uint32_t n) { return IStateLayout(n).bytes; }
+
+int sdz_inflate_state_reset_device(void* state, uint32_t n, void* stream) {
+    if (int rc = ensure_device()) return rc;
+    if (n == 0) return SDZ_API_OK;
+    if (!state) return fail(SDZ_API_BAD_ARG, "sdz_inflate_state_reset_device: null state");
+    IStateLayout L(n);
+    launch_istate_reset((uint8_t*)state + L.ds, (uint8_t*)state + L.rs, n, (hipStream_t)stream);
+    HIPCHK(hipGetLastError());
+    return SDZ_API_OK;
+}
+
+int sdz_inflate_append_batch_device(void* state, const uint8_t* in, const uint64_t* in_off,
+                                    const uint64_t* in_len, uint8_t* out, const uint64_t* out_off,
+                                    const uint64_t* out_cap, sdz_inflate_record* rec, uint32_t n,
+                                    int32_t format, const uint8_t* dict, uint32_t dict_len,
+                                    void* stream) {
+    if (int rc = ensure_device()) return rc;
+    if (n == 0) return SDZ_API_OK;
+    if (!state || !in || !in_off || !in_len || !out || !out_off || !out_cap || !rec)
+        return fail(SDZ_API_BAD_ARG, "sdz_inflate_append_batch_device: null pointer");
+    if (format != SDZ_FMT_RAW && format != SDZ_FMT_CONTAINER)
+        return fail(SDZ_API_BAD_ARG, "sdz_inflate_append_batch_device: format must be RAW or CONTAINER");
+    hipStream_t s = (hipStream_t)stream;
+    std::lock_guard<std::mutex> lk(g_mu);
+    int32_t dict_adler = 1;
+    if (dict) {
+        if (int rc = device_checksum(dict, dict_len, 0, 1, &dict_adler, s)) return rc;
+    }
+    uint64_t mx = 0;
+    {
+        void* tmp = nullptr;
+        PoolUse tu(g_tmp, s);
+        if (int rc = tu.get(kTmpFname, &tmp)) return rc;
+        if (device_max_u64(in_len, n, (unsigned long long*)tmp, &mx, s))
+            return hip_fail(hipGetLastError(), "inflate append: input sizes");
+    }
+    // staging: carry ++ chunk per stream (+ 64 B of readable slack for the 16-byte loads)
+    const uint64_t stride = (SDZ_INFLATE_CARRY + mx + 64 + 255) & ~255ull;
+    IStateLayout SL(n);
+    InflateArgs a{};
+    a.dsave = (uint8_t*)state + SL.ds;
+    a.rsave = (uint8_t*)state + SL.rs;
+    a.window = (uint8_t*)state + SL.win;
+    a.carry = (uint8_t*)state + SL.carry;
+    a.streaming = 1;
+    a.n = n; a.format = format;
+    a.dict = dict; a.dict_len = dict_len; a.dict_adler = dict_adler;
+    PoolUse use(g_inflate_scratch, s);
+    uint8_t* ex = nullptr;
+    if (int rc = inflate_scratch(a, n, false, (size_t)n * stride + 16 * (size_t)n + 64, s, use, &ex)) return rc;
+    uint8_t* stage = ex;
+    uint64_t* st_off = (uint64_t*)(ex + (size_t)n * stride);
+    uint64_t* st_len = st_off + n;
+    launch_istate_stage(a, in, in_off, in_len, stage, stride, st_off, st_len, s);
+    a.in = stage; a.in_off = st_off; a.in_len = st_len;
+    a.out = out; a.out_off = out_off; a.out_cap = out_cap;
+    a.rec = rec;
+    return inflate_run(a, s);
 }
 
 // ----------------------------------------------------------------- deflate
@@ -523,6 +618,91 @@ int sdz_inflate_batch(const uint8_t* const* in, const size_t* in_len, uint8_t* c
     }
     return SDZ_API_OK;
 }
+
+// ----------------------------------------------------------------- one host Inflater
+
+}  // extern "C"
+
+struct sdz_inflater {
+    int32_t format = SDZ_FMT_CONTAINER;
+    uint8_t* d_state = nullptr;
+    uint8_t* d_dict = nullptr;
+    uint32_t dict_len = 0;
+    uint8_t* d_in = nullptr;
+    size_t in_cap = 0;
+    uint8_t* d_out = nullptr;
+    uint64_t* d_meta = nullptr;                   // in_off, in_len, out_off, out_cap
+    sdz_inflate_record* d_rec = nullptr;
+    std::vector<uint8_t> out;
+    uint64_t in_total = 0;                        // stream bytes passed before this append
+    ~sdz_inflater() {
+        for (void* p : { (void*)d_state, (void*)d_dict, (void*)d_in, (void*)d_out, (void*)d_meta, (void*)d_rec })
+            if (p) hipFree(p);
+    }
+};
+
+extern "C" {
+
+sdz_inflater* sdz_inflater_create(int32_t format, const uint8_t* dict, size_t dict_len) {
+    if (ensure_device()) return nullptr;
+    if (format != SDZ_FMT_RAW && format != SDZ_FMT_CONTAINER) {
+        fail(SDZ_API_BAD_ARG, "sdz_inflater_create: format must be RAW or CONTAINER");
+        return nullptr;
+    }
+    sdz_inflater* z = new sdz_inflater;
+    z->format = format;
+    hipError_t e = hipMalloc(&z->d_state, sdz_inflate_state_bytes(1));
+    if (e == hipSuccess) e = hipMalloc(&z->d_out, kInflaterOutCap + 64);
+    if (e == hipSuccess) e = hipMalloc(&z->d_meta, 4 * sizeof(uint64_t));
+    if (e == hipSuccess) e = hipMalloc(&z->d_rec, sizeof(sdz_inflate_record));
+    if (e == hipSuccess && dict) {
+        z->dict_len = (uint32_t)dict_len;
+        e = hipMalloc(&z->d_dict, dict_len + 64);
+        if (e == hipSuccess && dict_len) e = hipMemcpy(z->d_dict, dict, dict_len, hipMemcpyHostToDevice);
+    }
+    if (e != hipSuccess || sdz_inflate_state_reset_device(z->d_state, 1, nullptr) != SDZ_API_OK) {
+        if (e != hipSuccess) hip_fail(e, "sdz_inflater_create");
+        delete z;
+        return nullptr;
+    }
+    return z;
+}
+
+int sdz_inflater_append(sdz_inflater* z, const uint8_t* data, size_t len, const uint8_t** out,
+                        size_t* out_len, sdz_inflate_record* rec) {
+    if (!z || !out || !out_len || !rec || (!data && len)) return fail(SDZ_API_BAD_ARG, "sdz_inflater_append: null pointer");
+    z->out.clear();
+    if (len + 64 > z->in_cap) {
+        if (z->d_in) hipFree(z->d_in);
+        z->d_in = nullptr;
+        z->in_cap = std::max<size_t>(len + 64, 1 << 16);
+        HIPCHK(hipMalloc(&z->d_in, z->in_cap));
+    }
+    if (len) HIPCHK(hipMemcpy(z->d_in, data, len, hipMemcpyHostToDevice));
+    // more calls while the output slot fills up; each passes the chunk's bytes the device
+    // did not take (record in_used: stream offset of the first byte not consumed or held)
+    for (uint64_t from = 0;;) {
+        uint64_t meta[4] = { from, len - from, 0, kInflaterOutCap };
+        HIPCHK(hipMemcpy(z->d_meta, meta, sizeof meta, hipMemcpyHostToDevice));
+        int rc = sdz_inflate_append_batch_device(z->d_state, z->d_in, z->d_meta, z->d_meta + 1, z->d_out,
+                                                 z->d_meta + 2, z->d_meta + 3, z->d_rec, 1, z->format,
+                                                 z->d_dict, z->dict_len, nullptr);
+        if (rc) return rc;
+        HIPCHK(hipMemcpy(rec, z->d_rec, sizeof *rec, hipMemcpyDeviceToHost));
+        size_t o = z->out.size();
+        z->out.resize(o + rec->out_len);
+        if (rec->out_len) HIPCHK(hipMemcpy(z->out.data() + o, z->d_out, rec->out_len, hipMemcpyDeviceToHost));
+        const uint64_t sent_end = z->in_total + len;        // stream offset after this chunk
+        if (!rec->out_full) break;
+        from = len - (sent_end - rec->in_used);
+    }
+    z->in_total += len;
+    *out = z->out.data();
+    *out_len = z->out.size();
+    return SDZ_API_OK;
+}
+
+void sdz_inflater_destroy(sdz_inflater* z) { delete z; }
 
 int sdz_deflate_batch(const uint8_t* const* in, const size_t* in_len, uint8_t* const* out,
                       const size_t* out_cap, sdz_deflate_record* rec, uint32_t n, int32_t level,

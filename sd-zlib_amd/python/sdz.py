@@ -21,7 +21,8 @@ LIB_PATH = os.environ.get("SDZ_LIB") or os.path.join(os.path.dirname(_HERE), "li
 FMT_AUTO, FMT_RAW, FMT_CONTAINER = 0, 1, 2
 DEFLATE_FORMATS = {"raw": 0, "deflate": 1, "gzip": 2}
 STATUS = {0: "OK", 1: "DATA_ERROR", 2: "NEED_DICT", 3: "DICT_MISMATCH", 4: "TRUNCATED",
-          5: "OUT_OVERFLOW", 6: "TRAILING", 7: "TOO_SMALL", 8: "BAD_RECORD", 9: "INTERNAL"}
+          5: "OUT_OVERFLOW", 6: "TRAILING", 7: "TOO_SMALL", 8: "BAD_RECORD", 9: "INTERNAL",
+          10: "CARRY_OVERFLOW"}
 VERDICT = ("unchecked", "match", "mismatch")
 
 
@@ -37,7 +38,7 @@ class InflateRecord(ctypes.Structure):
         ("mtime", ctypes.c_int32), ("name_off", ctypes.c_uint32), ("name_len", ctypes.c_uint32),
         ("container", ctypes.c_uint8), ("complete", ctypes.c_uint8),
         ("checksum_verdict", ctypes.c_uint8), ("size_verdict", ctypes.c_uint8),
-        ("success", ctypes.c_uint8), ("reserved", ctypes.c_uint8 * 11),
+        ("success", ctypes.c_uint8), ("out_full", ctypes.c_uint8), ("reserved", ctypes.c_uint8 * 10),
     ]
 
 
@@ -59,6 +60,8 @@ EXPORTS = [
     "sdz_device_free", "sdz_copy_to_device", "sdz_copy_to_host", "sdz_memset_device",
     "sdz_copy_device_to_device",
     "sdz_sync", "sdz_stream_create", "sdz_stream_destroy", "sdz_set_timing", "sdz_last_kernel_ms", "sdz_last_kernel_breakdown",
+    "sdz_inflate_state_bytes", "sdz_inflate_state_reset_device", "sdz_inflate_append_batch_device",
+    "sdz_inflater_create", "sdz_inflater_append", "sdz_inflater_destroy",
 ]
 
 _lib = None
@@ -116,6 +119,18 @@ def lib():
     L.sdz_last_kernel_breakdown.argtypes = [ctypes.POINTER(ctypes.c_float)]
     L.sdz_last_kernel_breakdown.restype = ctypes.c_int
     L.sdz_set_device.argtypes = [ctypes.c_int]
+    L.sdz_inflate_state_bytes.argtypes = [u32]
+    L.sdz_inflate_state_bytes.restype = ctypes.c_uint64
+    L.sdz_inflate_state_reset_device.argtypes = [vp, u32, vp]
+    L.sdz_inflate_state_reset_device.restype = ctypes.c_int
+    L.sdz_inflate_append_batch_device.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, u32, i32, vp, u32, vp]
+    L.sdz_inflate_append_batch_device.restype = ctypes.c_int
+    L.sdz_inflater_create.argtypes = [i32, u8p, sz]
+    L.sdz_inflater_create.restype = vp
+    L.sdz_inflater_append.argtypes = [vp, u8p, sz, ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(sz),
+                                      ctypes.POINTER(InflateRecord)]
+    L.sdz_inflater_append.restype = ctypes.c_int
+    L.sdz_inflater_destroy.argtypes = [vp]
     _lib = L
     return L
 
@@ -236,6 +251,69 @@ def _u64_array(vals):
     return (ctypes.c_uint64 * len(vals))(*vals)
 
 
+class InflateStreams:
+    """n Inflaters on the device at once (sdz_inflate_append_batch_device): append() hands
+    every stream its next chunk (b"" for none) and an output slot of out_cap bytes, and
+    returns per-stream (record dict, output bytes)."""
+
+    def __init__(self, n, raw=False, dictionary=None):
+        L = lib()
+        self.n, self.fmt = n, FMT_RAW if raw else FMT_CONTAINER
+        self.state = DeviceBuffer(L.sdz_inflate_state_bytes(n))
+        _check(L.sdz_inflate_state_reset_device(self.state.ptr, n, None))
+        self.dict = None
+        if dictionary is not None:
+            self.dict = DeviceBuffer(len(dictionary) + 64)
+            self.dict.upload(bytes(dictionary))
+            self.dict_len = len(dictionary)
+        self.heads = [b""] * n
+        self.sent = [0] * n               # stream offset after the bytes passed so far
+
+    def append(self, chunks, out_cap=1 << 20):
+        """On out_full a stream holds back the chunk's bytes from in_used on: the result's
+        "unconsumed" gives them, to be passed again (before any new bytes) next call."""
+        L, n = lib(), self.n
+        chunks = [bytes(c) for c in chunks]
+        caps = [out_cap] * n if isinstance(out_cap, int) else list(out_cap)
+        in_off, o = [], 0
+        for c in chunks:
+            in_off.append(o)
+            o += (len(c) + 15) & ~15
+        d_in = DeviceBuffer(o + 128)
+        if o:
+            d_in.upload(b"".join(c + b"\0" * (((len(c) + 15) & ~15) - len(c)) for c in chunks))
+        out_off, q = [], 0
+        for c in caps:
+            out_off.append(q)
+            q += (c + 255) & ~255
+        d_out = DeviceBuffer(q + 64)
+        meta = in_off + [len(c) for c in chunks] + out_off + caps
+        d_meta = DeviceBuffer(8 * len(meta))
+        d_meta.upload(bytes(_u64_array(meta)))
+        d_rec = DeviceBuffer(ctypes.sizeof(InflateRecord) * n)
+        m = d_meta.ptr
+        _check(L.sdz_inflate_append_batch_device(
+            self.state.ptr, d_in.ptr, m, m + 8 * n, d_out.ptr, m + 16 * n, m + 24 * n, d_rec.ptr, n,
+            self.fmt, self.dict.ptr if self.dict else None, self.dict_len if self.dict else 0, None))
+        _check(L.sdz_sync(None))
+        recs = (InflateRecord * n).from_buffer_copy(d_rec.download(n * ctypes.sizeof(InflateRecord)))
+        res = []
+        for i in range(n):
+            if len(self.heads[i]) < 65536:
+                self.heads[i] += chunks[i][:65536 - len(self.heads[i])]
+            data = d_out.download(recs[i].out_len, out_off[i]) if recs[i].out_len else b""
+            r = _record_dict(recs[i], data, self.heads[i])
+            r["out_full"] = bool(recs[i].out_full)
+            end = self.sent[i] + len(chunks[i])
+            keep = end - recs[i].in_used if recs[i].out_full else 0
+            r["unconsumed"] = chunks[i][len(chunks[i]) - keep:] if keep else b""
+            self.sent[i] = end - keep
+            res.append(r)
+        for b in (d_in, d_out, d_meta, d_rec):
+            b.free()
+        return res
+
+
 # --------------------------------------------------------------------- reference API mirror
 
 def _u8(source, what="data must be an ArrayBuffer or buffer view"):
@@ -284,12 +362,17 @@ def _raise_for(r):
         raise SdzError("Custom dictionary is not valid for this data")
     if st == "TRAILING":
         raise SdzError("inflate error: trailing data after end of stream")
+    if st == "CARRY_OVERFLOW":
+        raise SdzError("inflate error: stream header larger than the incremental carry")
+    if st == "INTERNAL":
+        raise SdzError("inflate error: engine watchdog")
 
 
 class Inflater:
-    """sd-inflate.ts:54-180.  Streams are decoded one-shot on the GPU: append()
-    returns the stream's output (in 16 KiB chunks) once the accumulated input
-    holds a complete stream, [] before that; finish() reports the verdicts."""
+    """sd-inflate.ts:54-180.  Each append() runs the GPU decoder on the new bytes only:
+    the stream's decoder state, 32 KiB window, unfinished input unit and running checksum
+    stay on the device between calls (sdz_inflater_*), and append() returns the output the
+    reference's append() returns for the same input, in 16 KiB chunks (zstream.ts:11)."""
 
     def __init__(self, options=None):
         options = options or {}
@@ -305,32 +388,63 @@ class Inflater:
                 raise TypeError("options.dictionary must be undefined or a buffer or a buffer view")
             d = bytes(d)
         self._dict = d
-        self._input = b""
-        self._emitted = 0
-        self._last = None
+        self._h = None
+        self._rec = None
+        self._head = b""                 # the stream's first bytes, for the gzip FNAME
+        self._done = False
+        self._err = None
+
+    def _handle(self):
+        if self._h is None:
+            L = lib()
+            self._h = L.sdz_inflater_create(FMT_RAW if self._raw else FMT_CONTAINER, self._dict,
+                                            len(self._dict) if self._dict else 0)
+            if not self._h:
+                raise SdzError("libsdz: %s" % L.sdz_last_error().decode())
+        return self._h
 
     def append(self, data):
         chunk = _u8(data)
         if not chunk:
             return []
-        self._input += chunk
-        r = inflate_one(self._input, FMT_RAW if self._raw else FMT_CONTAINER, self._dict)
-        self._last = r
-        if r["status"] == "TRUNCATED":
-            return []
-        _raise_for(r)
-        out = r["data"][self._emitted:]
-        self._emitted = len(r["data"])
+        if self._err is not None:        # mode BAD: every later append throws again
+            raise self._err
+        if self._done:                   # sd-inflate.ts:130-132: nothing of this chunk consumed
+            raise SdzError("inflate error: bad input data")
+        if len(self._head) < 65536:
+            self._head += chunk[:65536 - len(self._head)]
+        rec = InflateRecord()
+        optr, olen = ctypes.c_void_p(), ctypes.c_size_t()
+        _check(lib().sdz_inflater_append(self._handle(), chunk, len(chunk), ctypes.byref(optr),
+                                         ctypes.byref(olen), ctypes.byref(rec)))
+        out = ctypes.string_at(optr, olen.value) if olen.value else b""
+        self._rec = rec
+        r = _record_dict(rec, out, self._head)
+        if r["status"] != "TRUNCATED":
+            self._done = True
+            try:
+                _raise_for(r)
+            except SdzError as e:
+                self._err = e
+                raise
         return _chunks(out)
 
     def finish(self):
-        r = self._last
-        if r is None:
+        if self._rec is None:
             return {"success": False, "complete": False, "checksum": "unchecked",
                     "fileSize": "unchecked", "fileName": "", "modDate": None}
+        r = _record_dict(self._rec, b"", self._head)
         return {"success": r["success"], "complete": r["complete"], "checksum": r["checksum"],
                 "fileSize": r["fileSize"], "fileName": r["fileName"],
                 "modDate": None if r["mtime"] == 0 else r["mtime"]}
+
+    def __del__(self):
+        try:
+            if self._h:
+                lib().sdz_inflater_destroy(self._h)
+                self._h = None
+        except Exception:
+            pass
 
 
 def inflate(data, dictionary=None):
