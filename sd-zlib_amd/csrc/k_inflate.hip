@@ -90,10 +90,9 @@ struct Lane : Core {
     uint32_t name_off, name_len, stored_left;
     int dict_used;
     uint8_t* lens;                    // global scratch for code lengths
-    // end of input: one-shot streams end TRUNCATED; incremental ones (streaming) rewind to
-    // the start of the unit in progress (ubit) and stall until the next call
-    const uint8_t* inp;
-    uint64_t tbits, ubit;
+    // end of input: one-shot streams end TRUNCATED; incremental ones (streaming) are parked
+    // at the start of the unit in progress (ubit) and stall until the next call
+    uint64_t ubit;
     int streaming, stall;
 };
 
@@ -438,12 +437,12 @@ __device__ __forceinline__ void lane_fail(Core& L, int status, int zmsg) {
 }
 // The unit that started at bit L.ubit (a header, block header, symbol, stored byte or
 // trailer) cannot finish: out of input (why 1) or of output room (why 2).  A one-shot
-// stream ends there; an incremental one (Inflater.append across calls) is repositioned at
+// stream ends there; an incremental one (Inflater.append across calls) is parked at
 // the unit's start and waits for the next call -- the reference stops its output at the
 // same place, holding the unit's bits in its bit buffer (infcodes.ts:367-387 need rule).
+// cold_run stops at once and parks the stream at L.ubit.
 __device__ __forceinline__ void lane_stall(Lane& L, int why) {
     if (!L.streaming) { lane_fail(L, why == 1 ? SDZ_TRUNCATED : SDZ_OUT_OVERFLOW, 0); return; }
-    br_init(L, L.inp, L.ubit, L.tbits);
     L.stall = why;
 }
 
@@ -625,7 +624,7 @@ __device__ __forceinline__ void block_step(Lane& L, Tree& LL, Tree& DD, uint8_t*
     if (L.mode == LM_STORED) {                            // infblocks.ts:278-333, resumable
         while (L.stored_left && !L.full) {
             uint32_t b;
-            L.ubit = br_consumed(L);
+            if (L.streaming) L.ubit = br_consumed(L);
             if (!br_get(L, 8, b)) { lane_stall(L, 1); return; }
             if (L.room == 0) { lane_stall(L, 2); return; }
             tok_lit(L, b);
@@ -849,14 +848,15 @@ __device__ __forceinline__ void parse_container(Lane& L, int32_t format, int32_t
 // parked in the stream's DSave.  Returns when the lane can use the fast path
 // again, has finished, or has filled its token ring.  Not inlined: its registers
 // are its own, so the symbol loop keeps a small register footprint.
+template <bool STREAM>
 __device__ __noinline__ void cold_run(DSave* S, const uint8_t* inp, uint64_t ilen, uint64_t cap,
                                       uint32_t* tb, uint32_t tcap, uint8_t* lens, int32_t format, int32_t has_dict,
-                                      int32_t dict_adler, uint32_t init, uint32_t streaming) {
+                                      int32_t dict_adler, uint32_t init) {
     Lane L;
     Tree LL, DD;
     uint8_t* region = lane_region();
     L.tb = tb; L.ts = lane_stage(); L.tcap = tcap; L.lens = lens;
-    L.inp = inp; L.tbits = ilen * 8; L.streaming = (int)streaming; L.stall = 0; L.ubit = 0;
+    L.streaming = STREAM; L.stall = 0; L.ubit = 0;
     if (init) {
         L.mode = LM_TYPE; L.last = 0; L.status = SDZ_OK; L.zmsg = 0; L.container = SDZ_CONTAINER_RAW;
         L.fixed = 0; L.nl = L.nd = 0; L.stored_ck = 0; L.stored_size = 0; L.mtime = 0;
@@ -882,9 +882,9 @@ __device__ __noinline__ void cold_run(DSave* S, const uint8_t* inp, uint64_t ile
     L.room = L.room0 = (uint32_t)(r > 0x7fffffffull ? 0x7fffffffull : r);
     for (;;) {
         if (L.full || L.mode == LM_DONE || L.stall) break;
-        L.ubit = br_consumed(L);
+        if (STREAM) L.ubit = br_consumed(L);
         if (L.mode == LM_CODES) {
-            if (br_avail(L) >= 64 && L.room >= 258) break;   // the hot loop's preconditions
+            if (br_avail(L) >= 64 && (!STREAM || L.room >= 258)) break;   // hot_ready's preconditions
             slow_step(L, LL, DD, region);
             if (L.ntok + 3 > L.tcap) L.full = true;
         } else {
@@ -892,7 +892,7 @@ __device__ __noinline__ void cold_run(DSave* S, const uint8_t* inp, uint64_t ile
             if (L.avail0 - L.avail > (1 << 28)) L.full = true;   // keeps the saturated counter exact
         }
     }
-    S->bitpos = br_consumed(L); S->pos = L.pos0 + (L.room0 - L.room);
+    S->bitpos = L.stall ? L.ubit : br_consumed(L); S->pos = L.pos0 + (L.room0 - L.room);
     S->mode = L.mode; S->last = L.last; S->status = L.status; S->zmsg = L.zmsg;
     S->container = L.container; S->fixed = L.fixed; S->nl = L.nl; S->nd = L.nd;
     S->stored_ck = L.stored_ck; S->stored_size = L.stored_size; S->mtime = L.mtime;
@@ -923,17 +923,24 @@ __device__ __forceinline__ void hot_save(const Hot& H, DSave* S) {
     S->ntok = H.ntok; S->litw = H.litw; S->nlit = H.nlit; S->full = H.full ? 1 : 0;
 }
 // one symbol step reads at most 48 bits and writes at most 258 bytes; below either
-// bound the cold path's exact end-of-input / end-of-room handling takes over
+// bound the cold path's exact end-of-input / end-of-room handling takes over.  The room
+// bound applies to incremental streams only (STREAM: 258 bytes), which must stop at a symbol's
+// start when out_cap is reached; a one-shot stream keeps the last symbols of
+// an exactly sized output slot in the hot loop, whose own room check ends it OUT_OVERFLOW.
+template <bool STREAM>
 __device__ __forceinline__ bool hot_ready(const Hot& H) {
-    return H.mode == LM_CODES && !H.full && br_avail(H) >= 64 && H.room >= 258;
+    return H.mode == LM_CODES && !H.full && br_avail(H) >= 64 && (!STREAM || H.room >= 258);
 }
+template <bool STREAM>
 __device__ __forceinline__ bool can_hot(const DSave* S, uint64_t tbits, uint64_t cap) {
-    return S->mode == LM_CODES && !S->full && !S->stall && tbits - S->bitpos >= 64 && cap - S->pos >= 258;
+    return S->mode == LM_CODES && !S->full && tbits - S->bitpos >= 64 &&
+           (!STREAM || (!S->stall && cap - S->pos >= 258));
 }
 
 // one epoch of the symbol loop: every lane with `hot` set decodes until no more
 // than `stop` lanes of the wave can continue.  Not inlined, so that its register
 // allocation is not shaped by the cold call in the caller's loop.
+template <bool STREAM>
 __device__ __noinline__ void hot_epoch(DSave* S, const uint8_t* inp, uint64_t ilen, uint64_t cap,
                                        uint32_t* tb, uint32_t tcap, bool hot, int stop) {
     Hot H;
@@ -946,13 +953,33 @@ __device__ __noinline__ void hot_epoch(DSave* S, const uint8_t* inp, uint64_t il
         if (hot) ring_step(H);
 #pragma unroll 1
         for (int rep = 0; rep < 4; ++rep) {
-            if (hot_ready(H)) {
+            if (hot_ready<STREAM>(H)) {
                 fast_step(H, LL, DD, region);
                 if (H.ntok + 3 > H.tcap) H.full = true;
             }
         }
-    } while (__popcll(__ballot(hot_ready(H))) > stop);
+    } while (__popcll(__ballot(hot_ready<STREAM>(H))) > stop);
     if (hot) hot_save(H, S);
+}
+
+template <bool STREAM>
+__device__ __forceinline__ void epochs(const InflateArgs& A, DSave* S, const uint8_t* inp, uint64_t ilen,
+                                       uint64_t cap, uint32_t* tb, uint8_t* lens, bool live) {
+    const uint64_t tbits = ilen * 8;
+    for (;;) {
+        bool hot = live && can_hot<STREAM>(S, tbits, cap);
+        bool cold = live && !S->full && S->mode != LM_DONE && !hot && (!STREAM || !S->stall);
+        if (__ballot(cold)) {
+            if (cold)
+                cold_run<STREAM>(S, inp, ilen, cap, tb, A.round_tokens, lens, A.format,
+                                 A.dict != nullptr, A.dict_adler, STREAM && S->mode == LM_INIT ? 1u : 0u);
+            hot = live && can_hot<STREAM>(S, tbits, cap);
+        }
+        uint64_t hm = __ballot(hot);
+        if (hm == 0) break;
+        int nhot = __popcll(hm);
+        hot_epoch<STREAM>(S, inp, ilen, cap, tb, A.round_tokens, hot, nhot - (nhot >= 16 ? nhot >> 3 : 1));
+    }
 }
 
 __global__ __launch_bounds__(IL_THREADS, 1) void k_inflate_decode(InflateArgs A, uint32_t round) {
@@ -981,8 +1008,10 @@ __global__ __launch_bounds__(IL_THREADS, 1) void k_inflate_decode(InflateArgs A,
             S->nlit = 0; S->full = 0; S->stall = 0;
         } else if (!resume) {
             live = true;
-            cold_run(S, inp, ilen, cap, tb, A.round_tokens, lens, A.format,
-                     A.dict != nullptr, A.dict_adler, 1u, A.streaming);
+            if (A.streaming) cold_run<true>(S, inp, ilen, cap, tb, A.round_tokens, lens, A.format,
+                                            A.dict != nullptr, A.dict_adler, 1u);
+            else cold_run<false>(S, inp, ilen, cap, tb, A.round_tokens, lens, A.format,
+                                 A.dict != nullptr, A.dict_adler, 1u);
         } else if (S->mode != LM_DONE && !(round > 0 && S->stall)) {
             live = true;
             for (int k = 0; k < IL_REGION / 4; ++k) ((uint32_t*)region)[k] = ((const uint32_t*)S->region)[k];
@@ -993,21 +1022,8 @@ __global__ __launch_bounds__(IL_THREADS, 1) void k_inflate_decode(InflateArgs A,
     // epochs: lanes that need block-level work do it together (cold_run), then
     // every lane that can decodes symbols with register-resident state until an
     // eighth of them has left the fast path; state is parked in DSave in between
-    uint64_t tbits = ilen * 8;
-    for (;;) {
-        bool hot = live && can_hot(S, tbits, cap);
-        bool cold = live && !S->full && !S->stall && S->mode != LM_DONE && !hot;
-        if (__ballot(cold)) {
-            if (cold)
-                cold_run(S, inp, ilen, cap, tb, A.round_tokens, lens, A.format,
-                         A.dict != nullptr, A.dict_adler, S->mode == LM_INIT ? 1u : 0u, A.streaming);
-            hot = live && can_hot(S, tbits, cap);
-        }
-        uint64_t hm = __ballot(hot);
-        if (hm == 0) break;
-        int nhot = __popcll(hm);
-        hot_epoch(S, inp, ilen, cap, tb, A.round_tokens, hot, nhot - (nhot >= 16 ? nhot >> 3 : 1));
-    }
+    if (A.streaming) epochs<true>(A, S, inp, ilen, cap, tb, lens, live);
+    else epochs<false>(A, S, inp, ilen, cap, tb, lens, live);
 
     bool more = live && S->mode != LM_DONE && !S->stall;
     uint64_t mm = __ballot(more);                        // one counter update per wave

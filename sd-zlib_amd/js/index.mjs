@@ -4,10 +4,12 @@
 // Same exports, argument validation, messages and auto-detection as the
 // reference (src/sd-inflate.ts, src/sd-deflate.ts, src/adler32.ts,
 // src/crc32.ts, src/common.ts); written for Node 12 (no ?. / ??).
-// Streams are decoded/encoded one-shot on the GPU: Inflater.append() returns
-// a stream's output (16 KiB chunks, zstream.ts:11) once the accumulated input
-// holds the complete stream; Deflater returns its whole output from finish().
-// Merged outputs are identical to the reference's.
+// Inflater.append() decodes each chunk on the GPU as it arrives: the stream's
+// decoder state, window, unfinished input and running checksum stay on the
+// device between appends (sdz_inflater_*), and append() returns the output the
+// reference's append() returns, in 16 KiB chunks (zstream.ts:11).  Deflater
+// compresses on the GPU at finish(); merged outputs are identical to the
+// reference's.
 import { createRequire } from "module";
 
 const require = createRequire(import.meta.url);
@@ -68,17 +70,6 @@ function chunks(data) {
 	return out;
 }
 
-function inflateOne(input, fmt, dict) {
-	let cap = Math.max(65536, input.length * 4);
-	for (;;) {
-		const r = addon.inflateBatch([input], fmt, [cap], dict || null)[0];
-		if (r.status !== "OUT_OVERFLOW") {
-			return r;
-		}
-		cap *= 4;
-	}
-}
-
 function throwFor(r) {
 	switch (r.status) {
 	case "DATA_ERROR": throw new Error("inflate error: " + r.zmsg);
@@ -86,6 +77,7 @@ function throwFor(r) {
 	case "DICT_MISMATCH": throw new Error("Custom dictionary is not valid for this data");
 	case "TRAILING": throw new Error("inflate error: trailing data after end of stream");
 	case "INTERNAL": throw new Error("inflate error: engine watchdog");
+	case "CARRY_OVERFLOW": throw new Error("inflate error: stream header larger than the incremental carry");
 	default: break;
 	}
 }
@@ -108,9 +100,12 @@ export class Inflater {
 			}
 			this.dict = u8ArrayFromBufferSource(dictionary);
 		}
-		this.pending = [];
-		this.emitted = 0;
+		this.handle = null;
+		this.head = [];          // the stream's first bytes (gzip FNAME)
+		this.headLen = 0;
 		this.last = undefined;
+		this.done = false;
+		this.error = null;
 	}
 
 	append(data) {
@@ -121,17 +116,32 @@ export class Inflater {
 		if (chunk.length === 0) {
 			return [];
 		}
-		this.pending.push(chunk);
-		const input = this.pending.length === 1 ? chunk : mergeBuffers(this.pending);
-		const r = inflateOne(input, this.raw ? FMT_RAW : FMT_CONTAINER, this.dict);
-		this.last = r;
-		if (r.status === "TRUNCATED") {
-			return [];
+		if (this.error) {
+			throw this.error;                        // mode BAD: every later append throws again
 		}
-		throwFor(r);
-		const out = r.data.subarray(this.emitted);
-		this.emitted = r.data.length;
-		return chunks(out);
+		if (this.done) {
+			throw new Error("inflate error: bad input data");   // sd-inflate.ts:130-132
+		}
+		if (this.handle === null) {
+			this.handle = addon.inflaterCreate(this.raw, this.dict || null);
+		}
+		if (this.headLen < 65536) {
+			const h = chunk.subarray(0, 65536 - this.headLen);
+			this.head.push(h);
+			this.headLen += h.length;
+		}
+		const r = addon.inflaterAppend(this.handle, chunk);
+		this.last = r;
+		if (r.status !== "TRUNCATED") {
+			this.done = true;
+			try {
+				throwFor(r);
+			} catch (e) {
+				this.error = e;
+				throw e;
+			}
+		}
+		return chunks(r.data);
 	}
 
 	finish() {
@@ -140,12 +150,19 @@ export class Inflater {
 			return { success: false, complete: false, checksum: "unchecked", fileSize: "unchecked",
 				fileName: "", modDate: undefined };
 		}
+		let fileName = "";
+		if (r.nameLen) {
+			const head = mergeBuffers(this.head);
+			for (let i = r.nameOff; i < r.nameOff + r.nameLen && i < head.length; i++) {
+				fileName += String.fromCharCode(head[i]);
+			}
+		}
 		return {
 			success: r.success,
 			complete: r.complete,
 			checksum: r.checksum,
 			fileSize: r.fileSize,
-			fileName: r.fileName,
+			fileName,
 			modDate: r.mtime === 0 ? undefined : new Date(r.mtime * 1000)
 		};
 	}

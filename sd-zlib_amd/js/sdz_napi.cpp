@@ -66,6 +66,7 @@ const char* status_name(int s) {
     case SDZ_TRAILING: return "TRAILING";
     case SDZ_INTERNAL: return "INTERNAL";
     case SDZ_TOO_SMALL: return "TOO_SMALL";
+    case SDZ_CARRY_OVERFLOW: return "CARRY_OVERFLOW";
     default: return "BAD_RECORD";
     }
 }
@@ -193,6 +194,75 @@ napi_value DeflateBatch(napi_env env, napi_callback_info info) {
     return arr;
 }
 
+// ---- one incremental Inflater (sdz_inflater_*): state stays on the device between appends
+
+void inflater_finalize(napi_env, void* data, void*) { sdz_inflater_destroy((sdz_inflater*)data); }
+
+// inflaterCreate(raw: boolean, dict: Uint8Array|null) -> handle
+napi_value InflaterCreate(napi_env env, napi_callback_info info) {
+    size_t argc = 2;
+    napi_value argv[2];
+    NAPI_OK(napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr));
+    bool raw = false;
+    NAPI_OK(napi_get_value_bool(env, argv[0], &raw));
+    const uint8_t* dict = nullptr;
+    size_t dict_len = 0;
+    napi_valuetype dt;
+    napi_typeof(env, argv[1], &dt);
+    if (dt != napi_null && dt != napi_undefined) get_bytes(env, argv[1], &dict, &dict_len);
+    sdz_inflater* z = sdz_inflater_create(raw ? SDZ_FMT_RAW : SDZ_FMT_CONTAINER, dict, dict_len);
+    if (!z) {
+        napi_throw_error(env, nullptr, (std::string("libsdz: ") + sdz_last_error()).c_str());
+        return nullptr;
+    }
+    napi_value h;
+    NAPI_OK(napi_create_external(env, z, inflater_finalize, nullptr, &h));
+    return h;
+}
+
+// inflaterAppend(handle, chunk: Uint8Array) -> { status, zmsg, complete, success, checksum,
+// fileSize, nameOff, nameLen, mtime, container, data }
+napi_value InflaterAppend(napi_env env, napi_callback_info info) {
+    size_t argc = 2;
+    napi_value argv[2];
+    NAPI_OK(napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr));
+    void* hp = nullptr;
+    NAPI_OK(napi_get_value_external(env, argv[0], &hp));
+    const uint8_t* in = nullptr;
+    size_t len = 0;
+    if (!get_bytes(env, argv[1], &in, &len)) {
+        napi_throw_type_error(env, nullptr, "data must be an ArrayBuffer or buffer view");
+        return nullptr;
+    }
+    const uint8_t* out = nullptr;
+    size_t out_len = 0;
+    sdz_inflate_record r;
+    if (sdz_inflater_append((sdz_inflater*)hp, in, len, &out, &out_len, &r)) {
+        napi_throw_error(env, nullptr, (std::string("libsdz: ") + sdz_last_error()).c_str());
+        return nullptr;
+    }
+    napi_value o, ab, ta;
+    NAPI_OK(napi_create_object(env, &o));
+    const char* sn = status_name(r.status);
+    set_str(env, o, "status", sn, strlen(sn));
+    const char* zm = sdz_zmsg(r.zmsg);
+    set_str(env, o, "zmsg", zm, strlen(zm));
+    set_bool(env, o, "complete", r.complete);
+    set_bool(env, o, "success", r.success);
+    set_str(env, o, "checksum", verdict(r.checksum_verdict), strlen(verdict(r.checksum_verdict)));
+    set_str(env, o, "fileSize", verdict(r.size_verdict), strlen(verdict(r.size_verdict)));
+    set_int(env, o, "nameOff", r.name_off);
+    set_int(env, o, "nameLen", r.name_len);
+    set_int(env, o, "mtime", r.mtime);
+    set_int(env, o, "container", r.container);
+    void* p = nullptr;
+    NAPI_OK(napi_create_arraybuffer(env, out_len ? out_len : 1, &p, &ab));
+    if (out_len) memcpy(p, out, out_len);
+    NAPI_OK(napi_create_typedarray(env, napi_uint8_array, out_len, ab, 0, &ta));
+    napi_set_named_property(env, o, "data", ta);
+    return o;
+}
+
 napi_value Checksum(napi_env env, napi_callback_info info, bool crc) {
     size_t argc = 2;
     napi_value argv[2];
@@ -231,6 +301,8 @@ napi_value Init(napi_env env, napi_value exports) {
         { "adler32", nullptr, Adler32, nullptr, nullptr, nullptr, napi_enumerable, nullptr },
         { "crc32", nullptr, Crc32, nullptr, nullptr, nullptr, napi_enumerable, nullptr },
         { "deviceCount", nullptr, DeviceCount, nullptr, nullptr, nullptr, napi_enumerable, nullptr },
+        { "inflaterCreate", nullptr, InflaterCreate, nullptr, nullptr, nullptr, napi_enumerable, nullptr },
+        { "inflaterAppend", nullptr, InflaterAppend, nullptr, nullptr, nullptr, napi_enumerable, nullptr },
     };
     napi_define_properties(env, exports, sizeof d / sizeof d[0], d);
     return exports;

@@ -119,18 +119,19 @@ def lib():
     L.sdz_last_kernel_breakdown.argtypes = [ctypes.POINTER(ctypes.c_float)]
     L.sdz_last_kernel_breakdown.restype = ctypes.c_int
     L.sdz_set_device.argtypes = [ctypes.c_int]
-    L.sdz_inflate_state_bytes.argtypes = [u32]
-    L.sdz_inflate_state_bytes.restype = ctypes.c_uint64
-    L.sdz_inflate_state_reset_device.argtypes = [vp, u32, vp]
-    L.sdz_inflate_state_reset_device.restype = ctypes.c_int
-    L.sdz_inflate_append_batch_device.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, u32, i32, vp, u32, vp]
-    L.sdz_inflate_append_batch_device.restype = ctypes.c_int
-    L.sdz_inflater_create.argtypes = [i32, u8p, sz]
-    L.sdz_inflater_create.restype = vp
-    L.sdz_inflater_append.argtypes = [vp, u8p, sz, ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(sz),
-                                      ctypes.POINTER(InflateRecord)]
-    L.sdz_inflater_append.restype = ctypes.c_int
-    L.sdz_inflater_destroy.argtypes = [vp]
+    if hasattr(L, "sdz_inflate_state_bytes"):       # (development variants built before it lack it)
+        L.sdz_inflate_state_bytes.argtypes = [u32]
+        L.sdz_inflate_state_bytes.restype = ctypes.c_uint64
+        L.sdz_inflate_state_reset_device.argtypes = [vp, u32, vp]
+        L.sdz_inflate_state_reset_device.restype = ctypes.c_int
+        L.sdz_inflate_append_batch_device.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, u32, i32, vp, u32, vp]
+        L.sdz_inflate_append_batch_device.restype = ctypes.c_int
+        L.sdz_inflater_create.argtypes = [i32, u8p, sz]
+        L.sdz_inflater_create.restype = vp
+        L.sdz_inflater_append.argtypes = [vp, u8p, sz, ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(sz),
+                                          ctypes.POINTER(InflateRecord)]
+        L.sdz_inflater_append.restype = ctypes.c_int
+        L.sdz_inflater_destroy.argtypes = [vp]
     _lib = L
     return L
 

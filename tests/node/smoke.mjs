@@ -33,6 +33,19 @@ check("inflate(simple.raw) auto-detect", eq(inflate(golden("simple.raw")), golde
 	check("Inflater two parts", eq(mergeBuffers(a.concat(b)), text) && inf.finish().success);
 }
 {
+	// every header, block header and symbol crossing appends: 1..5-byte pieces
+	const gz = golden("simple.gz");
+	const inf = new Inflater();
+	const parts = [];
+	for (let i = 0, k = 1; i < gz.length; i += k, k = k % 5 + 1) parts.push(...inf.append(gz.subarray(i, i + k)));
+	const res = inf.finish();
+	check("Inflater gzip in 1..5-byte pieces", eq(mergeBuffers(parts), golden("simple.txt")) && res.success &&
+		res.fileName === "simple.txt");
+	let msg = "";
+	try { inf.append(new Uint8Array([1, 2])); } catch (e) { msg = e.message; }
+	check("append after the end: bad input data", msg === "inflate error: bad input data");
+}
+{
 	const inf = new Inflater();
 	inf.append(golden("vertices.deflate"));
 	check("Inflater binary (vertices)", inf.finish().checksum === "match");

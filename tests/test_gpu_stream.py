@@ -223,3 +223,18 @@ def test_batched_streams_with_small_output_slots(paradise):
         assert last[i]["status"] == "OK" and last[i]["complete"]
         if not a10_split(refs[i]):                        # the reference's own verdict for these appends
             assert (last[i]["success"], last[i]["checksum"]) == (refs[i]["success"], refs[i]["checksum"]), i
+
+
+def test_node_facade_smoke():
+    """The drop-in ES module over the N-API addon (tests/node/smoke.mjs): the reference's
+    test/index.html cases, incremental appends included."""
+    import os
+    import shutil
+    import subprocess
+    node = shutil.which("node")
+    if node is None:
+        pytest.skip("node not installed")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([node, os.path.join(root, "tests", "node", "smoke.mjs")], capture_output=True,
+                       text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
