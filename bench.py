@@ -173,7 +173,7 @@ def inflate_step(sdz, b, split=None):
 def deflate_step(sdz, b, level, fmt):
     in_off, in_len, out_off, out_cap = b.ptrs()
     rc = sdz.lib().sdz_deflate_batch_device(b.d_in.ptr, in_off, in_len, b.d_out.ptr, out_off, out_cap,
-                                            b.d_rec.ptr, b.n, level, fmt, None, 0, 0, None)
+                                            b.d_rec.ptr, b.n, level, fmt, None, 0, 0, None, 0, None)
     if rc:
         raise RuntimeError(sdz.lib().sdz_last_error().decode())
     return sdz.lib().sdz_last_kernel_ms()

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define SDZ_ABI_VERSION 1
+#define SDZ_ABI_VERSION 2
 
 /* API return codes */
 enum {
@@ -172,16 +172,20 @@ void sdz_inflater_destroy(sdz_inflater* z);
  * bit-exact with the reference for the same input, level, format, file name and
  * MTIME (the reference stamps Math.floor(Date.now()/1000), sd-deflate.ts:140;
  * the caller passes it here).  fname: Latin-1 bytes already mapped as
- * sd-deflate.ts:125-130 does (NULL/0 = no FNAME).  Device pointers. */
+ * sd-deflate.ts:125-130 does (NULL/0 = no FNAME).  dict (may be NULL; format
+ * SDZ_DEFLATE_ZLIB only, as sd-deflate.ts:80-90 requires) is the preset dictionary of
+ * every stream: deflateSetDictionary (deflate.ts:1184-1216) and the 78 20 + DICTID
+ * header.  Device pointers (dict too). */
 int sdz_deflate_batch_device(const uint8_t* in, const uint64_t* in_off, const uint64_t* in_len,
                              uint8_t* out, const uint64_t* out_off, const uint64_t* out_cap,
                              sdz_deflate_record* rec, uint32_t n, int32_t level, int32_t format,
                              const uint8_t* fname, uint32_t fname_len, uint32_t mtime,
-                             void* stream);
+                             const uint8_t* dict, uint32_t dict_len, void* stream);
 
 int sdz_deflate_batch(const uint8_t* const* in, const size_t* in_len, uint8_t* const* out,
                       const size_t* out_cap, sdz_deflate_record* rec, uint32_t n, int32_t level,
-                      int32_t format, const uint8_t* fname, size_t fname_len, uint32_t mtime);
+                      int32_t format, const uint8_t* fname, size_t fname_len, uint32_t mtime,
+                      const uint8_t* dict, size_t dict_len);
 
 /* Worst-case compressed size for one stream (header + blocks + trailer). */
 uint64_t sdz_deflate_bound(uint64_t in_len, int32_t format, uint32_t fname_len);

@@ -704,6 +704,28 @@ __device__ __forceinline__ void deflate_slow(DS& s) {
     flush_block(s, true);
 }
 
+// deflate.ts:1184-1216 deflateSetDictionary: the dictionary's last <= MAX_DIST bytes become
+// the window's start, with their strings in the hash chains (shorter than MIN_MATCH: nothing)
+__device__ void set_dictionary(DS& s, const GLB uint8_t* dict, uint32_t dict_len) {
+    int length = (int)dict_len;
+    if (length < MIN_MATCH) return;
+    uint32_t index = 0;
+    if (length > MAX_DIST) {
+        length = MAX_DIST;
+        index = dict_len - (uint32_t)length;
+    }
+    for (int i = 0; i < length; i++) s.S->window[i] = dict[index + i];
+    s.strstart = length;
+    s.block_start = length;
+    s.ins_h = s.S->window[0];
+    s.ins_h = ((s.ins_h << HASH_SHIFT) ^ s.S->window[1]) & HASH_MASK;
+    for (int n = 0; n <= length - MIN_MATCH; n++) {
+        s.ins_h = ((s.ins_h << HASH_SHIFT) ^ s.S->window[n + (MIN_MATCH - 1)]) & HASH_MASK;
+        s.S->prev[n & W_MASK] = s.S->head[s.ins_h];
+        s.S->head[s.ins_h] = (uint16_t)n;
+    }
+}
+
 // adler32.ts:34-105 / crc32.ts:48-106 over the input (Deflater.append, sd-deflate.ts:185-190)
 __device__ int32_t input_checksum(const GLB uint8_t* p, uint64_t n, bool gzip, const uint32_t* crct) {
     if (gzip) {
@@ -788,15 +810,22 @@ __global__ __launch_bounds__(DF_THREADS) void k_deflate(DeflateArgs A) {
     s.heap_len = 0; s.heap_max = HEAP_SIZE;
     s.l_max_code = s.d_max_code = s.bl_max_code = 0;
     init_block(s);
+    if (A.dict) set_dictionary(s, (const GLB uint8_t*)A.dict, A.dict_len);   // sd-deflate.ts:80-90
 
     bool gzip = A.format == SDZ_DEFLATE_GZIP;
     DF_STAMP(s, 5);
     int32_t cks = input_checksum(s.in, s.in_len, gzip, crct);
     DF_STAMP(s, 0);
     // container header (sd-deflate.ts:98-152): written straight to the output slot
-    uint64_t hdr = A.format == SDZ_DEFLATE_ZLIB ? 2 : gzip ? 10 + (A.fname_len ? A.fname_len + 1 : 0) : 0;
+    // zlib: 78 01, or 78 20 + DICTID when the dictionary's adler32 is nonzero (sd-deflate.ts:98-115)
+    const bool dictid = A.format == SDZ_DEFLATE_ZLIB && A.dict && A.dict_adler != 0;
+    uint64_t hdr = A.format == SDZ_DEFLATE_ZLIB ? (dictid ? 6 : 2) : gzip ? 10 + (A.fname_len ? A.fname_len + 1 : 0) : 0;
     if (hdr > s.out_cap) { R.status = SDZ_OUT_OVERFLOW; A.rec[sid] = R; return; }
-    if (A.format == SDZ_DEFLATE_ZLIB) { s.out[0] = 0x78; s.out[1] = 0x01; }
+    if (dictid) {
+        const uint32_t d = (uint32_t)A.dict_adler;
+        s.out[0] = 0x78; s.out[1] = 0x20;
+        s.out[2] = (uint8_t)(d >> 24); s.out[3] = (uint8_t)(d >> 16); s.out[4] = (uint8_t)(d >> 8); s.out[5] = (uint8_t)d;
+    } else if (A.format == SDZ_DEFLATE_ZLIB) { s.out[0] = 0x78; s.out[1] = 0x01; }
     else if (gzip) {
         s.out[0] = 0x1f; s.out[1] = 0x8b; s.out[2] = 8; s.out[3] = A.fname_len ? 8 : 0;
         s.out[4] = (uint8_t)A.mtime; s.out[5] = (uint8_t)(A.mtime >> 8);

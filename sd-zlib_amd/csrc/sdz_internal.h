@@ -77,6 +77,9 @@ struct DeflateArgs {
     uint32_t rec_stride;
     int32_t* cks;                // n input checksums (record path)
     uint32_t fast;               // set by launch_deflate: k_deflate redoes flagged streams only
+    const uint8_t* dict;         // preset dictionary (deflateSetDictionary), may be null
+    uint32_t dict_len;
+    int32_t dict_adler;          // adler32.ts of the whole dictionary: the zlib header's DICTID
     unsigned long long* dbg;     // phase cycle counters (SDZ_PHASE_TIMING), normally null
 };
 

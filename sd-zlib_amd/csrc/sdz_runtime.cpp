@@ -426,7 +426,7 @@ uint64_t sdz_deflate_bound(uint64_t in_len, int32_t format, uint32_t fname_len) 
     // stored-block worst case (5 bytes per <= 16383-symbol block at most) + trees + container
     uint64_t blocks = in_len / 16000 + 2;
     uint64_t b = in_len + blocks * 5 + in_len / 8 + 1024;
-    if (format == SDZ_DEFLATE_ZLIB) b += 6;
+    if (format == SDZ_DEFLATE_ZLIB) b += 10;              // 78 20 + DICTID with a dictionary
     if (format == SDZ_DEFLATE_GZIP) b += 18 + fname_len + 1;
     return (b + 7) & ~7ull;
 }
@@ -435,7 +435,7 @@ int sdz_deflate_batch_device(const uint8_t* in, const uint64_t* in_off, const ui
                              uint8_t* out, const uint64_t* out_off, const uint64_t* out_cap,
                              sdz_deflate_record* rec, uint32_t n, int32_t level, int32_t format,
                              const uint8_t* fname, uint32_t fname_len, uint32_t mtime,
-                             void* stream) {
+                             const uint8_t* dict, uint32_t dict_len, void* stream) {
     if (int rc = ensure_device()) return rc;
     if (n == 0) return SDZ_API_OK;
     if (level < 1 || level > 9) return fail(SDZ_API_BAD_ARG, "level must be between 1 and 9, inclusive");
@@ -443,8 +443,14 @@ int sdz_deflate_batch_device(const uint8_t* in, const uint64_t* in_off, const ui
         return fail(SDZ_API_BAD_ARG, "container must be one of `raw`, `deflate`, `gzip`");
     if (!in || !in_off || !in_len || !out || !out_off || !out_cap || !rec)
         return fail(SDZ_API_BAD_ARG, "sdz_deflate_batch_device: null pointer");
+    if (dict && format != SDZ_DEFLATE_ZLIB)
+        return fail(SDZ_API_BAD_ARG, "Can only provide a dictionary for `deflate` containers.");
     hipStream_t s = (hipStream_t)stream;
     std::lock_guard<std::mutex> lk(g_mu);
+    int32_t dict_adler = 1;
+    if (dict) {
+        if (int rc = device_checksum(dict, dict_len, 0, 1, &dict_adler, s)) return rc;
+    }
     // per-stream state slabs: process in sub-batches so the slab pool stays bounded
     // one lane per stream: fill the chip (64 Ki lanes = one wave per SIMD) when a
     // quarter of free HBM holds the slabs, else as many as it does
@@ -457,7 +463,7 @@ int sdz_deflate_batch_device(const uint8_t* in, const uint64_t* in_off, const ui
     PoolUse tmp_use(g_tmp, s);
     if (int rc = tmp_use.get(kTmpFname + fname_len + 64, &tmp)) return rc;
     uint32_t stride = 0;
-    if (level >= 4) {
+    if (level >= 4 && !dict) {                    // a dictionary shifts the window: serial path
         uint64_t mx = 0;
         if (device_max_u64(in_len, n, (unsigned long long*)tmp, &mx, s))
             return hip_fail(hipGetLastError(), "deflate: input sizes");
@@ -493,6 +499,7 @@ int sdz_deflate_batch_device(const uint8_t* in, const uint64_t* in_off, const ui
         a.pv_buf = stride ? (uint16_t*)((uint8_t*)a.rec_buf + (size_t)chunk * stride * sizeof(uint64_t)) : nullptr;
         a.cks = stride ? (int32_t*)((uint8_t*)a.pv_buf + (size_t)chunk * stride * sizeof(uint16_t)) : nullptr;
         a.fast = 0;
+        a.dict = dict; a.dict_len = dict_len; a.dict_adler = dict_adler;
         a.fname = d_fname; a.fname_len = fname_len; a.mtime = mtime;
         a.n = m; a.level = level; a.format = format;
         launch_deflate(a, s);
@@ -706,9 +713,17 @@ void sdz_inflater_destroy(sdz_inflater* z) { delete z; }
 
 int sdz_deflate_batch(const uint8_t* const* in, const size_t* in_len, uint8_t* const* out,
                       const size_t* out_cap, sdz_deflate_record* rec, uint32_t n, int32_t level,
-                      int32_t format, const uint8_t* fname, size_t fname_len, uint32_t mtime) {
+                      int32_t format, const uint8_t* fname, size_t fname_len, uint32_t mtime,
+                      const uint8_t* dict, size_t dict_len) {
     if (int rc = ensure_device()) return rc;
     if (n == 0) return SDZ_API_OK;
+    uint8_t* d_dict = nullptr;
+    if (dict) {
+        HIPCHK(hipMalloc(&d_dict, dict_len + 64));
+        hipError_t e = hipMemcpy(d_dict, dict, dict_len, hipMemcpyHostToDevice);
+        if (e != hipSuccess) { hipFree(d_dict); return hip_fail(e, "hipMemcpy(dict)"); }
+    }
+    struct DictFree { uint8_t* p; ~DictFree() { if (p) hipFree(p); } } dict_free{ d_dict };
     std::vector<uint64_t> meta(4 * (size_t)n);
     uint64_t ti = 0, to = 0;
     for (uint32_t i = 0; i < n; ++i) {
@@ -727,7 +742,8 @@ int sdz_deflate_batch(const uint8_t* const* in, const size_t* in_len, uint8_t* c
     HIPCHK(hipMemcpy(hb.d_meta, meta.data(), meta.size() * sizeof(uint64_t), hipMemcpyHostToDevice));
     int rc = sdz_deflate_batch_device(hb.d_in, hb.d_meta, hb.d_meta + n, hb.d_out, hb.d_meta + 2 * (size_t)n,
                                       hb.d_meta + 3 * (size_t)n, (sdz_deflate_record*)hb.d_rec, n, level,
-                                      format, fname, (uint32_t)fname_len, mtime, nullptr);
+                                      format, fname, (uint32_t)fname_len, mtime, d_dict, (uint32_t)dict_len,
+                                      nullptr);
     if (rc) return rc;
     HIPCHK(hipDeviceSynchronize());
     std::vector<sdz_deflate_record> r(n);

@@ -222,7 +222,7 @@ export class Deflater {
 			if (!u8ArrayFromBufferSource(dictionary)) {
 				throw new TypeError("dictionary must be an ArrayBuffer or buffer view");
 			}
-			throw new Error("preset dictionaries are not yet on the GPU deflate path (SURVEY.md §8f row 3)");
+			this.dict = u8ArrayFromBufferSource(dictionary);
 		}
 		this.level = level;
 		this.format = format;
@@ -254,7 +254,7 @@ export class Deflater {
 		const input = this.parts.length === 1 ? this.parts[0] : mergeBuffers(this.parts);
 		const fmt = this.format === "raw" ? 0 : this.format === "deflate" ? 1 : 2;
 		const mtime = Math.floor(Date.now() / 1000);      // sd-deflate.ts:140
-		const r = addon.deflateBatch([input], this.level, fmt, this.fileName, mtime)[0];
+		const r = addon.deflateBatch([input], this.level, fmt, this.fileName, mtime, this.dict || null)[0];
 		if (r.status !== "OK") {
 			throw new Error("deflating: " + r.status);
 		}
@@ -285,7 +285,7 @@ export function deflateBatch(streams, options) {
 	const o = options || {};
 	const views = streams.map(s => u8ArrayFromBufferSource(s));
 	const fmt = o.format === "raw" ? 0 : o.format === "gzip" ? 2 : 1;
-	return addon.deflateBatch(views, o.level || 6, fmt, new Uint8Array(0), o.mtime || 0);
+	return addon.deflateBatch(views, o.level || 6, fmt, new Uint8Array(0), o.mtime || 0, null);
 }
 
 export function deviceCount() {

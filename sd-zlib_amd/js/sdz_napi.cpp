@@ -138,10 +138,11 @@ napi_value InflateBatch(napi_env env, napi_callback_info info) {
     return arr;
 }
 
-// deflateBatch(streams: Uint8Array[], level, format, fileNameLatin1: Uint8Array, mtime)
+// deflateBatch(streams: Uint8Array[], level, format, fileNameLatin1: Uint8Array, mtime,
+//              dict: Uint8Array|null)
 napi_value DeflateBatch(napi_env env, napi_callback_info info) {
-    size_t argc = 5;
-    napi_value argv[5];
+    size_t argc = 6;
+    napi_value argv[6];
     NAPI_OK(napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr));
     uint32_t n = 0;
     NAPI_OK(napi_get_array_length(env, argv[0], &n));
@@ -155,6 +156,13 @@ napi_value DeflateBatch(napi_env env, napi_callback_info info) {
     double dm = 0;
     NAPI_OK(napi_get_value_double(env, argv[4], &dm));
     mtime = (uint32_t)(int64_t)dm;
+    const uint8_t* dict = nullptr;
+    size_t dict_len = 0;
+    if (argc > 5) {
+        napi_valuetype dt;
+        napi_typeof(env, argv[5], &dt);
+        if (dt != napi_null && dt != napi_undefined) get_bytes(env, argv[5], &dict, &dict_len);
+    }
     std::vector<const uint8_t*> in(n);
     std::vector<size_t> in_len(n), cap(n);
     std::vector<uint8_t*> out(n);
@@ -173,7 +181,7 @@ napi_value DeflateBatch(napi_env env, napi_callback_info info) {
     }
     std::vector<sdz_deflate_record> rec(n);
     int rc = sdz_deflate_batch(in.data(), in_len.data(), out.data(), cap.data(), rec.data(), n, level, fmt,
-                               fname_len ? fname : nullptr, fname_len, mtime);
+                               fname_len ? fname : nullptr, fname_len, mtime, dict, dict_len);
     if (rc) {
         napi_throw_error(env, nullptr, (std::string("libsdz: ") + sdz_last_error()).c_str());
         return nullptr;

@@ -83,11 +83,11 @@ def lib():
                                     ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(sz),
                                     ctypes.POINTER(InflateRecord), u32, i32, u8p, sz]
     L.sdz_inflate_batch.restype = ctypes.c_int
-    L.sdz_deflate_batch_device.argtypes = [vp, vp, vp, vp, vp, vp, vp, u32, i32, i32, vp, u32, u32, vp]
+    L.sdz_deflate_batch_device.argtypes = [vp, vp, vp, vp, vp, vp, vp, u32, i32, i32, vp, u32, u32, vp, u32, vp]
     L.sdz_deflate_batch_device.restype = ctypes.c_int
     L.sdz_deflate_batch.argtypes = [ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(sz),
                                     ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(sz),
-                                    ctypes.POINTER(DeflateRecord), u32, i32, i32, u8p, sz, u32]
+                                    ctypes.POINTER(DeflateRecord), u32, i32, i32, u8p, sz, u32, u8p, sz]
     L.sdz_deflate_batch.restype = ctypes.c_int
     L.sdz_deflate_bound.argtypes = [ctypes.c_uint64, i32, u32]
     L.sdz_deflate_bound.restype = ctypes.c_uint64
@@ -197,7 +197,8 @@ def inflate_one(data, fmt=FMT_AUTO, dictionary=None):
         cap *= 4
 
 
-def deflate_batch(streams, level=6, format="deflate", file_name_latin1=b"", mtime=0, out_caps=None):
+def deflate_batch(streams, level=6, format="deflate", file_name_latin1=b"", mtime=0, out_caps=None,
+                  dictionary=None):
     L = lib()
     n = len(streams)
     streams = [bytes(s) for s in streams]
@@ -212,8 +213,9 @@ def deflate_batch(streams, level=6, format="deflate", file_name_latin1=b"", mtim
     caps = (ctypes.c_size_t * n)(*caps_l)
     recs = (DeflateRecord * n)()
     fn = bytes(file_name_latin1)
+    d = bytes(dictionary) if dictionary is not None else None
     _check(L.sdz_deflate_batch(ins, in_len, outs, caps, recs, n, level, fmt, fn or None, len(fn),
-                               mtime & 0xFFFFFFFF))
+                               mtime & 0xFFFFFFFF, d, len(d) if d is not None else 0))
     return [{"status": STATUS.get(recs[i].status, recs[i].status), "checksum": recs[i].checksum,
              "data": bufs[i].raw[:recs[i].out_len]} for i in range(n)]
 
@@ -490,10 +492,14 @@ class Deflater:
             raise ValueError("container must be one of `raw`, `deflate`, `gzip`")
         if file_name is not None and not isinstance(file_name, str):
             raise TypeError("fileName must be a string")
-        if options.get("dictionary") is not None:
+        d = options.get("dictionary")
+        if d is not None:
             if fmt != "deflate":
                 raise TypeError("Can only provide a dictionary for `deflate` containers.")
-            raise NotImplementedError("preset dictionaries on the GPU deflate path: SURVEY §8f row 3")
+            if not isinstance(d, (bytes, bytearray, memoryview)):
+                raise TypeError("dictionary must be an ArrayBuffer or buffer view")
+            d = bytes(d)
+        self._dict = d
         self._level, self._fmt = level, fmt
         self._name = _latin1(file_name or "")
         self._input = b""
@@ -512,7 +518,7 @@ class Deflater:
         if not self._appended:
             raise SdzError("Cannot call finish before at least 1 call to append")
         mtime = self.mtime if self.mtime is not None else int(math.floor(time.time()))
-        r = deflate_batch([self._input], self._level, self._fmt, self._name, mtime)[0]
+        r = deflate_batch([self._input], self._level, self._fmt, self._name, mtime, dictionary=self._dict)[0]
         if r["status"] != "OK":
             raise SdzError("deflating: " + r["status"])
         return _chunks(r["data"])

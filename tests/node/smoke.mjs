@@ -58,6 +58,15 @@ check("inflate(simple.raw) auto-detect", eq(inflate(golden("simple.raw")), golde
 	check("gzip round trip", eq(out, text) && inf.finish().fileName === "paradiselost.orig");
 }
 check("deflate L6 == reference fixture", eq(deflate(text, { level: 6 }), golden("paradiselost.deflate")));
+{
+	// test/index.html:173-208: a preset dictionary round trip ("deflate" container)
+	const words = new TextEncoder().encode("the of and to in that with his her for thou thy thee");
+	const src = text.subarray(2000, 30000);
+	const comp = deflate(src, { level: 6, dictionary: words });
+	const inf = new Inflater({ dictionary: words });
+	const out = mergeBuffers(inf.append(comp));
+	check("dictionary round trip", comp[0] === 0x78 && comp[1] === 0x20 && eq(out, src) && inf.finish().success);
+}
 check("adler32 KAT", adler32(golden("simple.txt")) === -1612443532);
 check("crc32 KAT", crc32(golden("simple.txt")) === 1488305224);
 let threw = "";

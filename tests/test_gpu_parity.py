@@ -487,7 +487,7 @@ def test_concurrent_streams_do_not_share_scratch(paradise):
             b = dfl[k]
             rc = L.sdz_deflate_batch_device(b.d_in.ptr, *b.ptrs()[:2], b.d_out.ptr, *b.ptrs()[2:],
                                             b.d_rec.ptr, b.n, 6 + 3 * k - 3 * k * rep, 1, None, 0, 0,
-                                            streams[k])
+                                            None, 0, streams[k])
             assert rc == 0, L.sdz_last_error()
         for k in range(2):
             b = inf[k]

@@ -182,12 +182,12 @@ def run_c5(scale, seed=0x5D5A1B1E):
     slots = Slots(pool, pick, [bound] * n)
     a, b, c, d = slots.ptrs()
     rc = L.sdz_deflate_batch_device(slots.d_in.ptr, a, b, slots.d_out.ptr, c, d, slots.d_rec.ptr, n, 9, 2,
-                                    None, 0, 0, None)
+                                    None, 0, 0, None, 0, None)
     assert rc == 0, L.sdz_last_error()
     L.sdz_sync(None)                                      # the warm-up is asynchronous
     t0 = time.perf_counter()
     rc = L.sdz_deflate_batch_device(slots.d_in.ptr, a, b, slots.d_out.ptr, c, d, slots.d_rec.ptr, n, 9, 2,
-                                    None, 0, 0, None)
+                                    None, 0, 0, None, 0, None)
     L.sdz_sync(None)
     dwall = (time.perf_counter() - t0) * 1e3
     assert rc == 0, L.sdz_last_error()
