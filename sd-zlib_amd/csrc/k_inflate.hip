@@ -848,25 +848,46 @@ __device__ __forceinline__ void parse_container(Lane& L, int32_t format, int32_t
 // parked in the stream's DSave.  Returns when the lane can use the fast path
 // again, has finished, or has filled its token ring.  Not inlined: its registers
 // are its own, so the symbol loop keeps a small register footprint.
-template <bool STREAM>
+// MODE: 0 one-shot; 1 incremental (Inflater.append across calls: stall at the end of the
+// input); 2 segment (block-parallel decode of a long stream, k_split.hip: start at a
+// candidate block start, stop at a block boundary that is a candidate, or at the trailer)
+struct SegStop {
+    uint64_t start;                   // the segment's start bit
+    const uint64_t* cand;             // its stream's sorted candidate block starts
+    uint32_t ncand;
+};
+__device__ __forceinline__ bool seg_is_cand(const SegStop& G, uint64_t bit) {
+    uint32_t lo = 0, hi = G.ncand;
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (G.cand[mid] < bit) lo = mid + 1; else hi = mid;
+    }
+    return lo < G.ncand && G.cand[lo] == bit;
+}
+
+template <int MODE>
 __device__ __noinline__ void cold_run(DSave* S, const uint8_t* inp, uint64_t ilen, uint64_t cap,
                                       uint32_t* tb, uint32_t tcap, uint8_t* lens, int32_t format, int32_t has_dict,
-                                      int32_t dict_adler, uint32_t init) {
+                                      int32_t dict_adler, uint32_t init, SegStop G) {
     Lane L;
     Tree LL, DD;
     uint8_t* region = lane_region();
     L.tb = tb; L.ts = lane_stage(); L.tcap = tcap; L.lens = lens;
-    L.streaming = STREAM; L.stall = 0; L.ubit = 0;
+    L.streaming = MODE == 1; L.stall = 0; L.ubit = 0;
     if (init) {
         L.mode = LM_TYPE; L.last = 0; L.status = SDZ_OK; L.zmsg = 0; L.container = SDZ_CONTAINER_RAW;
         L.fixed = 0; L.nl = L.nd = 0; L.stored_ck = 0; L.stored_size = 0; L.mtime = 0;
         L.name_off = 0; L.name_len = 0; L.stored_left = 0; L.dict_used = 0;
         L.ntok = 0; L.litw = 0; L.nlit = 0; L.full = false;
-        br_init(L, inp, 0, ilen * 8);
-        L.pos0 = 0;
         LL.l = DD.l = 0; LL.g = DD.g = 0; LL.kmin = DD.kmin = 1; LL.left = DD.left = 0;
-        parse_container(L, format, has_dict, dict_adler, ilen);
-        if (L.stall) L.mode = LM_INIT;                   // incremental: header not complete yet
+        L.pos0 = 0;
+        if (MODE == 2 && G.start) {
+            br_init(L, inp, G.start, ilen * 8);           // a candidate block start: raw blocks
+        } else {
+            br_init(L, inp, 0, ilen * 8);
+            parse_container(L, format, has_dict, dict_adler, ilen);
+            if (L.stall) L.mode = LM_INIT;               // incremental: header not complete yet
+        }
     } else {
         L.mode = S->mode; L.last = S->last; L.status = S->status; L.zmsg = S->zmsg;
         L.container = S->container; L.fixed = S->fixed; L.nl = S->nl; L.nd = S->nd;
@@ -882,9 +903,13 @@ __device__ __noinline__ void cold_run(DSave* S, const uint8_t* inp, uint64_t ile
     L.room = L.room0 = (uint32_t)(r > 0x7fffffffull ? 0x7fffffffull : r);
     for (;;) {
         if (L.full || L.mode == LM_DONE || L.stall) break;
-        if (STREAM) L.ubit = br_consumed(L);
+        if (MODE) L.ubit = br_consumed(L);
+        if (MODE == 2) {                                  // a segment ends at the trailer, or at a candidate
+            if (L.mode == LM_TRAILER) { L.stall = SEG_FINAL; break; }
+            if (L.mode == LM_TYPE && L.ubit != G.start && seg_is_cand(G, L.ubit)) { L.stall = SEG_HANDOVER; break; }
+        }
         if (L.mode == LM_CODES) {
-            if (br_avail(L) >= 64 && (!STREAM || L.room >= 258)) break;   // hot_ready's preconditions
+            if (br_avail(L) >= 64 && (MODE != 1 || L.room >= 258)) break;   // hot_ready's preconditions
             slow_step(L, LL, DD, region);
             if (L.ntok + 3 > L.tcap) L.full = true;
         } else {
@@ -924,17 +949,18 @@ __device__ __forceinline__ void hot_save(const Hot& H, DSave* S) {
 }
 // one symbol step reads at most 48 bits and writes at most 258 bytes; below either
 // bound the cold path's exact end-of-input / end-of-room handling takes over.  The room
-// bound applies to incremental streams only (STREAM: 258 bytes), which must stop at a symbol's
-// start when out_cap is reached; a one-shot stream keeps the last symbols of
-// an exactly sized output slot in the hot loop, whose own room check ends it OUT_OVERFLOW.
+// bound applies to incremental streams only (STREAM: 258 bytes), which must stop at a
+// symbol's start when out_cap is reached; a one-shot stream (or segment) keeps the last
+// symbols of an exactly sized output slot in the hot loop, whose own room check ends it
+// OUT_OVERFLOW.
 template <bool STREAM>
 __device__ __forceinline__ bool hot_ready(const Hot& H) {
     return H.mode == LM_CODES && !H.full && br_avail(H) >= 64 && (!STREAM || H.room >= 258);
 }
-template <bool STREAM>
+template <int MODE>
 __device__ __forceinline__ bool can_hot(const DSave* S, uint64_t tbits, uint64_t cap) {
-    return S->mode == LM_CODES && !S->full && tbits - S->bitpos >= 64 &&
-           (!STREAM || (!S->stall && cap - S->pos >= 258));
+    return S->mode == LM_CODES && !S->full && tbits - S->bitpos >= 64 && (MODE == 0 || !S->stall) &&
+           (MODE != 1 || cap - S->pos >= 258);
 }
 
 // one epoch of the symbol loop: every lane with `hot` set decodes until no more
@@ -962,56 +988,73 @@ __device__ __noinline__ void hot_epoch(DSave* S, const uint8_t* inp, uint64_t il
     if (hot) hot_save(H, S);
 }
 
-template <bool STREAM>
+template <int MODE>
 __device__ __forceinline__ void epochs(const InflateArgs& A, DSave* S, const uint8_t* inp, uint64_t ilen,
-                                       uint64_t cap, uint32_t* tb, uint8_t* lens, bool live) {
+                                       uint64_t cap, uint32_t* tb, uint32_t tcap, uint8_t* lens, bool live,
+                                       SegStop G) {
     const uint64_t tbits = ilen * 8;
     for (;;) {
-        bool hot = live && can_hot<STREAM>(S, tbits, cap);
-        bool cold = live && !S->full && S->mode != LM_DONE && !hot && (!STREAM || !S->stall);
+        bool hot = live && can_hot<MODE>(S, tbits, cap);
+        bool cold = live && !S->full && S->mode != LM_DONE && !hot && (MODE == 0 || !S->stall);
         if (__ballot(cold)) {
             if (cold)
-                cold_run<STREAM>(S, inp, ilen, cap, tb, A.round_tokens, lens, A.format,
-                                 A.dict != nullptr, A.dict_adler, STREAM && S->mode == LM_INIT ? 1u : 0u);
-            hot = live && can_hot<STREAM>(S, tbits, cap);
+                cold_run<MODE>(S, inp, ilen, cap, tb, tcap, lens, A.format, A.dict != nullptr, A.dict_adler,
+                               MODE == 1 && S->mode == LM_INIT ? 1u : 0u, G);
+            hot = live && can_hot<MODE>(S, tbits, cap);
         }
         uint64_t hm = __ballot(hot);
         if (hm == 0) break;
         int nhot = __popcll(hm);
-        hot_epoch<STREAM>(S, inp, ilen, cap, tb, A.round_tokens, hot, nhot - (nhot >= 16 ? nhot >> 3 : 1));
+        hot_epoch<MODE == 1>(S, inp, ilen, cap, tb, tcap, hot, nhot - (nhot >= 16 ? nhot >> 3 : 1));
     }
 }
 
+// One lane per stream; in segment mode (A.segmode, k_split.hip) one lane per segment of a
+// long stream, in one round, into the segment's own token buffer.  Streams whose tokens
+// the segments provide (A.split_state) are skipped: k_seg_feed fills their rounds.
 __global__ __launch_bounds__(IL_THREADS, 1) void k_inflate_decode(InflateArgs A, uint32_t round) {
     uint8_t* region = lane_region();
     uint32_t* ts = lane_stage();
     uint32_t gid = blockIdx.x * IL_THREADS + threadIdx.x;
     bool valid = gid < A.n;
     uint32_t sid = valid ? gid : 0u;
+    if (valid && A.split_state && A.split_state[sid]) valid = false;   // fed by k_seg_feed
+    const uint32_t xid = A.segmode ? A.seg[sid].stream : sid;           // the stream of the input
     DSave* S = (DSave*)A.dsave + sid;
-    uint32_t* tb = A.tokens + (uint64_t)sid * A.round_tokens;
+    uint32_t* tb = A.segmode ? A.segtok + A.seg[sid].tok : A.tokens + (uint64_t)sid * A.round_tokens;
+    const uint32_t tcap = A.segmode ? A.seg[sid].cap : A.round_tokens;
     uint8_t* lens = A.scratch + (uint64_t)sid * kInflateScratchPerStream;
+    SegStop G = { 0, nullptr, 0 };
+    if (A.segmode) {
+        const uint32_t k = A.seg[sid].split;
+        const uint32_t nc = A.spinfo[k].ncand;
+        G.start = A.seg[sid].bit;
+        G.cand = A.cand + (uint64_t)k * SP_CAND_MAX;
+        G.ncand = nc < SP_CAND_MAX ? nc : SP_CAND_MAX;
+    }
     const uint8_t* inp = A.in;
     uint64_t ilen = 0, cap = 0;
     bool live = false;
     if (valid) {
-        inp = A.in + A.in_off[sid];
-        ilen = A.in_len[sid];
-        cap = A.out_cap[sid];
+        inp = A.in + A.in_off[xid];
+        ilen = A.in_len[xid];
+        cap = A.out_cap[xid];
         // a call's first round starts a stream (one-shot, or an incremental stream whose
         // header is still incomplete) or resumes it (later rounds; incremental calls)
         const bool resume = round > 0 || (A.streaming && S->mode != LM_INIT);
-        if (round == 0 && (A.out_off[sid] & 7)) {
+        if (round == 0 && (A.out_off[xid] & 7)) {
             S->mode = LM_DONE; S->status = SDZ_BAD_RECORD; S->zmsg = 0; S->bitpos = 0; S->pos = 0;
             S->container = SDZ_CONTAINER_RAW; S->stored_ck = 0; S->stored_size = 0; S->mtime = 0;
             S->name_off = 0; S->name_len = 0; S->dict_used = 0; S->ntok = 0; S->litw = 0;
             S->nlit = 0; S->full = 0; S->stall = 0;
         } else if (!resume) {
             live = true;
-            if (A.streaming) cold_run<true>(S, inp, ilen, cap, tb, A.round_tokens, lens, A.format,
-                                            A.dict != nullptr, A.dict_adler, 1u);
-            else cold_run<false>(S, inp, ilen, cap, tb, A.round_tokens, lens, A.format,
-                                 A.dict != nullptr, A.dict_adler, 1u);
+            if (A.streaming) cold_run<1>(S, inp, ilen, cap, tb, tcap, lens, A.format,
+                                         A.dict != nullptr, A.dict_adler, 1u, G);
+            else if (A.segmode) cold_run<2>(S, inp, ilen, cap, tb, tcap, lens, A.format,
+                                            A.dict != nullptr, A.dict_adler, 1u, G);
+            else cold_run<0>(S, inp, ilen, cap, tb, tcap, lens, A.format,
+                             A.dict != nullptr, A.dict_adler, 1u, G);
         } else if (S->mode != LM_DONE && !(round > 0 && S->stall)) {
             live = true;
             for (int k = 0; k < IL_REGION / 4; ++k) ((uint32_t*)region)[k] = ((const uint32_t*)S->region)[k];
@@ -1022,8 +1065,9 @@ __global__ __launch_bounds__(IL_THREADS, 1) void k_inflate_decode(InflateArgs A,
     // epochs: lanes that need block-level work do it together (cold_run), then
     // every lane that can decodes symbols with register-resident state until an
     // eighth of them has left the fast path; state is parked in DSave in between
-    if (A.streaming) epochs<true>(A, S, inp, ilen, cap, tb, lens, live);
-    else epochs<false>(A, S, inp, ilen, cap, tb, lens, live);
+    if (A.streaming) epochs<1>(A, S, inp, ilen, cap, tb, tcap, lens, live, G);
+    else if (A.segmode) epochs<2>(A, S, inp, ilen, cap, tb, tcap, lens, live, G);
+    else epochs<0>(A, S, inp, ilen, cap, tb, tcap, lens, live, G);
 
     bool more = live && S->mode != LM_DONE && !S->stall;
     uint64_t mm = __ballot(more);                        // one counter update per wave
@@ -1039,10 +1083,15 @@ __global__ __launch_bounds__(IL_THREADS, 1) void k_inflate_decode(InflateArgs A,
         S->ntok = H.ntok; S->litw = 0; S->nlit = 0;
         A.ntok[sid] = H.ntok;
     }
-    // 0: more rounds; 1: finished this round; 3: stalled (incremental: done for this call)
+    // 0: more rounds; 1: finished this round; 3+: stalled (incremental: done for this call;
+    // segment: handed over or reached the trailer)
     A.flags[sid] = S->mode == LM_DONE ? 1u : S->stall ? 3u : 0u;
-    if (S->mode != LM_DONE)
+    if (S->mode != LM_DONE && !A.segmode)
         for (int k = 0; k < IL_REGION / 4; ++k) ((uint32_t*)S->region)[k] = ((const uint32_t*)region)[k];
+}
+
+void launch_seg_decode(const InflateArgs& a, hipStream_t s) {
+    hipLaunchKernelGGL(k_inflate_decode, dim3((a.n + IL_THREADS - 1) / IL_THREADS), dim3(IL_THREADS), 0, s, a, 0u);
 }
 
 __global__ void k_inflate_resolve(InflateArgs A, uint32_t round);
@@ -1070,6 +1119,7 @@ int run_inflate_rounds(const InflateArgs& a, hipStream_t s, uint32_t* host_activ
         if (hipMemsetAsync(a.active, 0, sizeof(uint32_t), s) != hipSuccess) { rc = -1; break; }
         if (kernel_ms) (void)hipEventRecord(ev[0], s);
         hipLaunchKernelGGL(k_inflate_decode, g1, dim3(IL_THREADS), 0, s, a, round);
+        if (a.split_plan) launch_seg_feed(a, round, s);  // the split streams' tokens (k_split.hip)
         if (kernel_ms) (void)hipEventRecord(ev[1], s);
         hipLaunchKernelGGL(k_inflate_resolve, g2, dim3(resolve_block_threads()), 0, s, a, round);
         if (kernel_ms) (void)hipEventRecord(ev[2], s);

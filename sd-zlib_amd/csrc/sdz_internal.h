@@ -3,6 +3,7 @@
 #include <stdint.h>
 #include <hip/hip_runtime.h>
 #include "sdz.h"
+#include "split.h"
 
 namespace sdz {
 
@@ -46,6 +47,14 @@ struct InflateArgs {
     uint32_t streaming;
     uint8_t* window;             // n * 32 KiB: the 32 KiB before this call's output
     uint8_t* carry;              // n * SDZ_INFLATE_CARRY: input carried to the next call
+    // block-parallel decode of long streams (k_split.hip, split.h)
+    const SplitPlan* split_plan; // host pointer: this call's split pre-pass, or null
+    const uint32_t* split_state; // per stream: 1 = its tokens are fed from the segments (no decode)
+    uint32_t segmode;            // 1: this decode launch runs segments, one lane per segment
+    const SegInfo* seg;          // segment mode: start bit, token buffer, stream per segment
+    const SplitInfo* spinfo;     // segment mode: the split streams (candidate counts)
+    const uint64_t* cand;        // segment mode: sorted candidates, SP_CAND_MAX per split stream
+    uint32_t* segtok;            // segment mode: the segment token pool
 };
 
 uint64_t inflate_dsave_bytes();  // per stream decode state
@@ -53,6 +62,13 @@ uint64_t inflate_rsave_bytes();  // per stream resolve state
 int run_inflate_rounds(const InflateArgs& a, hipStream_t s, uint32_t* host_active, float* kernel_ms);
 // incremental mode: fresh state / stage carry + chunk contiguously (k_istream.hip)
 void launch_istate_reset(uint8_t* dsave, uint8_t* rsave, uint32_t n, hipStream_t s);
+// block-parallel decode of long streams (k_split.hip)
+void launch_split_find(const uint8_t* in, const uint64_t* in_off, SplitInfo* sp, uint32_t nsplit, uint64_t* cand,
+                       uint64_t total_lanes, hipStream_t s);
+void launch_seg_decode(const InflateArgs& a, hipStream_t s);
+void launch_seg_chain(const InflateArgs& a, SplitInfo* sp, uint32_t nsplit, const SegInfo* seg, const uint64_t* cand,
+                      const void* segD, uint32_t* chain, uint64_t* chain_tok, uint32_t* split_state, hipStream_t s);
+void launch_seg_feed(const InflateArgs& a, uint32_t round, hipStream_t s);
 void launch_istate_stage(const InflateArgs& a, const uint8_t* in, const uint64_t* in_off, const uint64_t* in_len,
                          uint8_t* stage, uint64_t stride, uint64_t* st_off, uint64_t* st_len, hipStream_t s);
 

@@ -22,6 +22,7 @@ thread_local std::string g_err;
 thread_local float g_last_ms = 0.f;
 thread_local hipEvent_t g_ev0 = nullptr, g_ev1 = nullptr;
 thread_local bool g_ev_pending = false;
+thread_local float g_extra_ms = 0.f;    // GPU time of the last call outside g_ev0..g_ev1 (split pre-pass)
 int g_timing = 0;
 float g_breakdown[3] = { 0.f, 0.f, 0.f };   // decode / resolve / finalize of the last inflate
 std::mutex g_mu;
@@ -96,7 +97,7 @@ struct Pool {
         return SDZ_API_OK;
     }
 };
-Pool g_inflate_scratch, g_deflate_state, g_tmp, g_stage;
+Pool g_inflate_scratch, g_deflate_state, g_tmp, g_stage, g_split;
 constexpr size_t kTmpFname = 256;     // g_tmp layout: [0, 256) small results, then the file name
 constexpr uint64_t kInflaterOutCap = 4ull << 20;   // sdz_inflater: output slot per device call
 
@@ -116,6 +117,7 @@ struct PoolUse {
 
 void timing_begin(hipStream_t s) {
     if (!g_timing) return;
+    g_extra_ms = 0.f;
     if (!g_ev0) { hipEventCreate(&g_ev0); hipEventCreate(&g_ev1); }
     hipEventRecord(g_ev0, s);
 }
@@ -243,7 +245,7 @@ float sdz_last_kernel_ms(void) {
         hipEventSynchronize(g_ev1);
         float ms = 0.f;
         hipEventElapsedTime(&ms, g_ev0, g_ev1);
-        g_last_ms = ms;
+        g_last_ms = ms + g_extra_ms;
         g_ev_pending = false;
     }
     return g_last_ms;
@@ -290,7 +292,7 @@ int inflate_scratch(InflateArgs& a, uint32_t n, bool own_state, size_t extra, hi
     return SDZ_API_OK;
 }
 
-int inflate_run(InflateArgs& a, hipStream_t s) {
+int inflate_run(InflateArgs& a, hipStream_t s, bool timing_started = false) {
     static thread_local uint32_t host_active = 0;
     a.dbg = nullptr;
     const bool phases = getenv("SDZ_PHASE_TIMING") != nullptr;   // development aid
@@ -298,7 +300,7 @@ int inflate_run(InflateArgs& a, hipStream_t s) {
         HIPCHK(hipMalloc(&a.dbg, 64 * sizeof(unsigned long long)));
         HIPCHK(hipMemsetAsync(a.dbg, 0, 64 * sizeof(unsigned long long), s));
     }
-    timing_begin(s);
+    if (!timing_started) timing_begin(s);
     if (run_inflate_rounds(a, s, &host_active, g_timing ? g_breakdown : nullptr))
         return hip_fail(hipGetLastError(), "inflate rounds");
     timing_end(s);
@@ -312,6 +314,150 @@ int inflate_run(InflateArgs& a, hipStream_t s) {
         hipFree(a.dbg);
     }
     HIPCHK(hipGetLastError());
+    return SDZ_API_OK;
+}
+
+// Block-parallel decode of long streams (k_split.hip): when a batch holds streams much longer
+// than its median, their block starts are found, their blocks decoded as segments (one lane
+// each) and chained back in order, before the rounds; the rounds then feed their tokens to
+// the resolve phase.  Which streams: compressed size >= max(SDZ_SPLIT_MIN (64 KiB), twice the
+// batch's bytes per decoder lane (64 Ki lanes: one wave per SIMD)), so that no lane is left
+// with much more than an even share; a batch of equal streams (C2) is not split.
+// SDZ_SPLIT=0 turns it off.  Returns 0 with plan.nsplit == 0 when nothing is split.
+struct SplitHost {
+    SplitPlan plan{};
+    uint32_t* split_state = nullptr;
+};
+int inflate_split_plan(InflateArgs& a, hipStream_t s, PoolUse& use, SplitHost& H, float* ms) {
+    const uint32_t n = a.n;
+    if (const char* e = getenv("SDZ_SPLIT")) if (atoi(e) == 0) return SDZ_API_OK;
+    uint64_t split_min = 64 << 10;
+    if (const char* e = getenv("SDZ_SPLIT_MIN")) split_min = strtoull(e, nullptr, 10);
+    std::vector<uint64_t> len(n), off(n);
+    HIPCHK(hipMemcpyAsync(len.data(), a.in_len, n * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    uint64_t total = 0;
+    for (uint64_t x : len) total += x;
+    const uint64_t thr = std::max<uint64_t>(split_min, 2 * (total / 65536));
+    std::vector<SplitInfo> sp;
+    uint64_t lanes = 0;
+    for (uint32_t i = 0; i < n; ++i) {
+        if (len[i] < thr || len[i] > (1ull << 32)) continue;
+        SplitInfo x{};
+        x.sid = i;
+        x.nbits = len[i] * 8;
+        x.lane0 = lanes;
+        lanes += (x.nbits + 31) / 32;
+        sp.push_back(x);
+    }
+    if (sp.empty()) return SDZ_API_OK;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    if (ms) { (void)hipEventCreate(&e0); (void)hipEventCreate(&e1); (void)hipEventRecord(e0, s); }
+    const uint32_t ns = (uint32_t)sp.size();
+    // phase 1: candidates (their own allocation: freed at the end of this function)
+    uint8_t* d1 = nullptr;
+    const size_t cand_bytes = (size_t)ns * SP_CAND_MAX * sizeof(uint64_t);
+    HIPCHK(hipMalloc(&d1, ns * sizeof(SplitInfo) + cand_bytes));
+    struct Free { uint8_t* p; ~Free() { if (p) hipFree(p); } } free1{ d1 };
+    SplitInfo* d_sp1 = (SplitInfo*)d1;
+    uint64_t* d_cand1 = (uint64_t*)(d1 + ns * sizeof(SplitInfo));
+    HIPCHK(hipMemcpyAsync(d_sp1, sp.data(), ns * sizeof(SplitInfo), hipMemcpyHostToDevice, s));
+    launch_split_find(a.in, a.in_off, d_sp1, ns, d_cand1, lanes, s);
+    HIPCHK(hipGetLastError());
+    std::vector<uint64_t> cand((size_t)ns * SP_CAND_MAX);
+    HIPCHK(hipMemcpyAsync(sp.data(), d_sp1, ns * sizeof(SplitInfo), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(cand.data(), d_cand1, cand_bytes, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    // phase 2: segments -- the stream's start, then one per candidate; token capacity from
+    // the bits to the next candidate (1 token per 6 bits; a segment that fills up sends its
+    // stream to the serial path)
+    std::vector<SegInfo> seg;
+    uint64_t tok = 0;
+    uint32_t chain = 0;
+    for (uint32_t k = 0; k < ns; ++k) {
+        SplitInfo& x = sp[k];
+        const uint32_t nc = std::min<uint32_t>(x.ncand, SP_CAND_MAX);
+        const uint64_t* c = cand.data() + (size_t)k * SP_CAND_MAX;
+        x.skip0 = nc && c[0] == 0 ? 1 : 0;
+        x.seg0 = (uint32_t)seg.size();
+        x.chain0 = chain;
+        const bool use = x.ncand <= SP_CAND_MAX;
+        const uint32_t m = use ? 1 + nc - x.skip0 : 1;
+        x.nseg = m;
+        chain += m;
+        for (uint32_t j = 0; j < m; ++j) {
+            const uint64_t b = j == 0 ? 0 : c[j - 1 + x.skip0];
+            const uint64_t e = j + 1 < m ? c[j + x.skip0] : x.nbits;
+            SegInfo g{};
+            g.bit = b;
+            g.tok = tok;
+            g.cap = (uint32_t)std::min<uint64_t>(((e - b) / 6 + 1024 + 31) & ~31ull, 1u << 30);
+            g.split = k;
+            g.stream = x.sid;
+            tok += g.cap;
+            seg.push_back(g);
+        }
+    }
+    const uint32_t nseg = (uint32_t)seg.size();
+    const uint64_t dsb = inflate_dsave_bytes();
+    auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+    size_t o = 0;
+    const size_t o_sp = o; o = al(o + ns * sizeof(SplitInfo));
+    const size_t o_seg = o; o = al(o + nseg * sizeof(SegInfo));
+    const size_t o_cand = o; o = al(o + cand_bytes);
+    const size_t o_chain = o; o = al(o + chain * sizeof(uint32_t));
+    const size_t o_ctok = o; o = al(o + chain * sizeof(uint64_t));
+    const size_t o_state = o; o = al(o + n * sizeof(uint32_t));
+    const size_t o_segD = o; o = al(o + nseg * dsb);
+    const size_t o_lens = o; o = al(o + nseg * kInflateScratchPerStream);
+    const size_t o_nt = o; o = al(o + (2 * (size_t)nseg + 1) * sizeof(uint32_t));
+    const size_t o_tok = o; o = al(o + tok * sizeof(uint32_t));
+    void* base = nullptr;
+    if (int rc = use.get(o, &base)) return rc;
+    uint8_t* B = (uint8_t*)base;
+    H.plan.nsplit = ns;
+    H.plan.nseg = nseg;
+    H.plan.sp = (SplitInfo*)(B + o_sp);
+    H.plan.seg = (SegInfo*)(B + o_seg);
+    H.plan.cand = (uint64_t*)(B + o_cand);
+    H.plan.chain = (uint32_t*)(B + o_chain);
+    H.plan.chain_tok = (uint64_t*)(B + o_ctok);
+    H.plan.segtok = (uint32_t*)(B + o_tok);
+    H.split_state = (uint32_t*)(B + o_state);
+    HIPCHK(hipMemcpyAsync(H.plan.sp, sp.data(), ns * sizeof(SplitInfo), hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(H.plan.seg, seg.data(), nseg * sizeof(SegInfo), hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(H.plan.cand, d_cand1, cand_bytes, hipMemcpyDeviceToDevice, s));
+    HIPCHK(hipMemsetAsync(H.split_state, 0, n * sizeof(uint32_t), s));
+    // phase 3: every segment decoded, one lane each, in one round
+    InflateArgs g = a;
+    g.n = nseg;
+    g.dsave = B + o_segD;
+    g.scratch = B + o_lens;
+    g.ntok = (uint32_t*)(B + o_nt);
+    g.flags = g.ntok + nseg;
+    g.active = g.flags + nseg;
+    g.split_plan = nullptr;
+    g.split_state = nullptr;
+    g.segmode = 1;
+    g.seg = H.plan.seg;
+    g.spinfo = H.plan.sp;
+    g.cand = H.plan.cand;
+    g.segtok = H.plan.segtok;
+    launch_seg_decode(g, s);
+    // phase 4: chains, trailers; the chained streams' decode state for the rounds
+    launch_seg_chain(a, H.plan.sp, ns, H.plan.seg, H.plan.cand, g.dsave, H.plan.chain, H.plan.chain_tok,
+                     H.split_state, s);
+    HIPCHK(hipGetLastError());
+    if (ms) {
+        (void)hipEventRecord(e1, s);
+        (void)hipEventSynchronize(e1);
+        float t = 0.f;
+        (void)hipEventElapsedTime(&t, e0, e1);
+        *ms = t;
+        (void)hipEventDestroy(e0);
+        (void)hipEventDestroy(e1);
+    }
+    HIPCHK(hipStreamSynchronize(s));                     // phase 1's allocation is freed on return
     return SDZ_API_OK;
 }
 
@@ -356,7 +502,15 @@ int sdz_inflate_batch_device(const uint8_t* in, const uint64_t* in_off, const ui
     a.dict = dict; a.dict_len = dict_len; a.dict_adler = dict_adler;
     a.n = n; a.format = format;
     a.streaming = 0; a.window = nullptr; a.carry = nullptr;
-    return inflate_run(a, s);
+    a.split_plan = nullptr; a.split_state = nullptr; a.segmode = 0;
+    PoolUse split_use(g_split, s);
+    SplitHost sh;
+    float split_ms = 0.f;
+    if (int rc = inflate_split_plan(a, s, split_use, sh, g_timing ? &split_ms : nullptr)) return rc;
+    if (sh.plan.nsplit) { a.split_plan = &sh.plan; a.split_state = sh.split_state; }
+    int rc = inflate_run(a, s);
+    if (g_timing) { g_breakdown[0] += split_ms; g_extra_ms = split_ms; }   // the pre-pass counts as decode
+    return rc;
 }
 
 uint64_t sdz_inflate_state_bytes(uint32_t n) { return IStateLayout(n).bytes; }

@@ -120,6 +120,9 @@ def inflate(slots, fmt):
     L.sdz_sync(None)
     wall = (time.perf_counter() - t0) * 1e3
     assert rc == 0, L.sdz_last_error()
+    f3 = (ctypes.c_float * 3)()
+    L.sdz_last_kernel_breakdown(f3)
+    log("inflate: decode %.2f ms (split pre-pass included), resolve %.2f ms, finalize %.2f ms" % tuple(f3))
     return L.sdz_last_kernel_ms(), wall
 
 
