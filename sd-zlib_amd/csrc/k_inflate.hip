@@ -27,19 +27,29 @@
 
 namespace sdz {
 
-#define IL_THREADS 256
+// IL_STREAMS streams per workgroup, IL_WAVE_LANES of them per wave: with 32, a workgroup
+// has twice the waves, each with half its lanes active -- the same streams and LDS per CU,
+// two instruction streams per SIMD to hide each other's latency
+#ifndef IL_WAVE_LANES
+#define IL_WAVE_LANES 64
+#endif
+#define IL_STREAMS 256
+#define IL_THREADS (IL_STREAMS * 64 / IL_WAVE_LANES)
 #define IL_TSTAGE 32                  // tokens staged in LDS per stream (one 128 B line)
 #define IL_TSTRIDE 136                // LDS bytes per stream for the token stage (8-aligned)
 #define IL_BAD_IDX 300                // rank selected by codes past lim[15]
 
 // LDS: per-stream symbol tables, then per-stream token stages (file scope, so the
 // non-inlined hot and cold functions address it as LDS, not through flat pointers)
-__shared__ __attribute__((aligned(16))) uint8_t g_region[IL_THREADS * IL_REGION];
-__shared__ __attribute__((aligned(16))) uint32_t g_stage[IL_THREADS * (IL_TSTRIDE / 4)];
-__device__ __forceinline__ uint8_t* lane_region() { return g_region + threadIdx.x * IL_REGION; }
-__shared__ __attribute__((aligned(16))) uint32_t g_ring[IL_THREADS * 18];   // 64 B + 8 B pad per lane
-__device__ __forceinline__ uint32_t* lane_stage() { return g_stage + threadIdx.x * (IL_TSTRIDE / 4); }
-__device__ __forceinline__ uint32_t* lane_ring() { return g_ring + threadIdx.x * 18; }
+__device__ __forceinline__ uint32_t lane_slot() {   // this lane's stream slot in the workgroup
+    return IL_WAVE_LANES == 64 ? threadIdx.x : (threadIdx.x >> 6) * IL_WAVE_LANES + (threadIdx.x & (IL_WAVE_LANES - 1));
+}
+__shared__ __attribute__((aligned(16))) uint8_t g_region[IL_STREAMS * IL_REGION];
+__shared__ __attribute__((aligned(16))) uint32_t g_stage[IL_STREAMS * (IL_TSTRIDE / 4)];
+__device__ __forceinline__ uint8_t* lane_region() { return g_region + lane_slot() * IL_REGION; }
+__shared__ __attribute__((aligned(16))) uint32_t g_ring[IL_STREAMS * 18];   // 64 B + 8 B pad per lane
+__device__ __forceinline__ uint32_t* lane_stage() { return g_stage + lane_slot() * (IL_TSTRIDE / 4); }
+__device__ __forceinline__ uint32_t* lane_ring() { return g_ring + lane_slot() * 18; }
 
 __constant__ uint8_t c_border[19] = { 16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15 };
 
@@ -1015,8 +1025,8 @@ __device__ __forceinline__ void epochs(const InflateArgs& A, DSave* S, const uin
 __global__ __launch_bounds__(IL_THREADS, 1) void k_inflate_decode(InflateArgs A, uint32_t round) {
     uint8_t* region = lane_region();
     uint32_t* ts = lane_stage();
-    uint32_t gid = blockIdx.x * IL_THREADS + threadIdx.x;
-    bool valid = gid < A.n;
+    uint32_t gid = blockIdx.x * IL_STREAMS + lane_slot();
+    bool valid = gid < A.n && (threadIdx.x & 63u) < IL_WAVE_LANES;
     uint32_t sid = valid ? gid : 0u;
     if (valid && A.split_state && A.split_state[sid]) valid = false;   // fed by k_seg_feed
     const uint32_t xid = A.segmode ? A.seg[sid].stream : sid;           // the stream of the input
@@ -1091,7 +1101,7 @@ __global__ __launch_bounds__(IL_THREADS, 1) void k_inflate_decode(InflateArgs A,
 }
 
 void launch_seg_decode(const InflateArgs& a, hipStream_t s) {
-    hipLaunchKernelGGL(k_inflate_decode, dim3((a.n + IL_THREADS - 1) / IL_THREADS), dim3(IL_THREADS), 0, s, a, 0u);
+    hipLaunchKernelGGL(k_inflate_decode, dim3((a.n + IL_STREAMS - 1) / IL_STREAMS), dim3(IL_THREADS), 0, s, a, 0u);
 }
 
 __global__ void k_inflate_resolve(InflateArgs A, uint32_t round);
@@ -1108,7 +1118,7 @@ uint64_t inflate_rsave_bytes() { return sizeof(RSave); }
 int run_inflate_rounds(const InflateArgs& a, hipStream_t s, uint32_t* host_active, float* kernel_ms) {
     if (a.n == 0) return 0;
     uint32_t spb = resolve_streams_per_block();
-    dim3 g1((a.n + IL_THREADS - 1) / IL_THREADS), g2((a.n + spb - 1) / spb);
+    dim3 g1((a.n + IL_STREAMS - 1) / IL_STREAMS), g2((a.n + spb - 1) / spb);
     hipEvent_t ev[4] = { nullptr, nullptr, nullptr, nullptr };
     if (kernel_ms) {
         for (auto& e : ev) (void)hipEventCreate(&e);

@@ -233,6 +233,7 @@ export class Deflater {
 		});
 		this.fileName = new Uint8Array(name);
 		this.parts = [];
+		this.checksum = format === "gzip" ? 0 : 1;
 	}
 
 	append(data) {
@@ -243,6 +244,9 @@ export class Deflater {
 		if (!chunk.length) {
 			return [];
 		}
+		// sd-deflate.ts:185-190: the trailer's checksum runs chunk by chunk (adler32's NMAX
+		// quirk depends on where the appends split the input)
+		this.checksum = this.format === "gzip" ? crc32(chunk, this.checksum) : adler32(chunk, this.checksum);
 		this.parts.push(chunk);
 		return [];
 	}
@@ -257,6 +261,11 @@ export class Deflater {
 		const r = addon.deflateBatch([input], this.level, fmt, this.fileName, mtime, this.dict || null)[0];
 		if (r.status !== "OK") {
 			throw new Error("deflating: " + r.status);
+		}
+		if (this.format === "deflate") {                 // the append-chained adler32 (big-endian)
+			const n = r.data.length, c = this.checksum >>> 0;
+			r.data[n - 4] = c >>> 24; r.data[n - 3] = (c >>> 16) & 255;
+			r.data[n - 2] = (c >>> 8) & 255; r.data[n - 1] = c & 255;
 		}
 		return chunks(r.data);
 	}

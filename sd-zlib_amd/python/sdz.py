@@ -504,12 +504,19 @@ class Deflater:
         self._name = _latin1(file_name or "")
         self._input = b""
         self._appended = False
+        self._checksum = 0 if fmt == "gzip" else 1
         self.mtime = None
 
     def append(self, data):
         chunk = _u8(data)
         if not chunk:
             return []
+        # sd-deflate.ts:185-190: the trailer's checksum runs chunk by chunk, so adler32's NMAX
+        # quirk (adler32.ts:67) depends on where the appends split the input
+        if self._fmt == "gzip":
+            self._checksum = crc32(chunk, self._checksum)
+        else:
+            self._checksum = adler32(chunk, self._checksum)
         self._input += chunk
         self._appended = True
         return []
@@ -521,7 +528,10 @@ class Deflater:
         r = deflate_batch([self._input], self._level, self._fmt, self._name, mtime, dictionary=self._dict)[0]
         if r["status"] != "OK":
             raise SdzError("deflating: " + r["status"])
-        return _chunks(r["data"])
+        data = r["data"]
+        if self._fmt == "deflate":                      # the append-chained adler32 (big-endian)
+            data = data[:-4] + (self._checksum & 0xFFFFFFFF).to_bytes(4, "big")
+        return _chunks(data)
 
 
 def deflate(data, options=None):

@@ -46,3 +46,19 @@ def test_dictionary_batch_and_errors(paradise):
         sdz.Deflater({"format": "gzip", "dictionary": terms})
     with pytest.raises(sdz.SdzError, match="Can only provide a dictionary"):
         sdz.deflate_batch(srcs[:1], level=6, format="raw", dictionary=terms)
+
+
+def test_deflater_checksum_chains_per_append(paradise):
+    """sd-deflate.ts:185-190: Deflater.append() folds each chunk into the running checksum, so
+    an append of 5552 or 11104 bytes (adler32's NMAX quirk) changes the trailer; the merged
+    output must match the reference's for the same appends."""
+    for sizes in ([5552, 5552, 100], [11104, 7], [3000, 16384, 5552], [70000, 11104, 9]):
+        parts, o = [], 0
+        for z in sizes:
+            parts.append(paradise[o:o + z])
+            o += z
+        for fmt in ("deflate", "gzip", "raw"):
+            d = sdz.Deflater({"format": fmt, "level": 6})
+            d.mtime = 0
+            out = b"".join(b"".join(d.append(p)) for p in parts) + b"".join(d.finish())
+            assert out == O.deflater_run(parts, level=6, format=fmt, mtime=0), (sizes, fmt)
