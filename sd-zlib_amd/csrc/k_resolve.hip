@@ -26,6 +26,7 @@
 // Positions before the output start read the preset dictionary or zeros.
 #include "inflate_state.h"
 #include "crc32_dev.h"
+#include <algorithm>
 #include <type_traits>
 
 namespace sdz {
@@ -752,7 +753,37 @@ __global__ __launch_bounds__(RS_THREADS) __attribute__((amdgpu_waves_per_eu(RS_W
 
 // one wave per finished gzip stream: crc32 of its output (crc32_dev.h) and the checksum
 // verdicts that depend on it
-__global__ __launch_bounds__(64) void k_inflate_finalize(InflateArgs A) {
+// Long outputs are cut into chunks whose crc32 k_gzip_crc_parts computes one block each (4
+// waves, 64 lanes each over a quarter); k_inflate_finalize chains them in order with x^(8 n)
+// shifts (crc32 of a concatenation).  parts[sid * maxc + c]: chunk c of stream sid.
+__global__ __launch_bounds__(256) void k_gzip_crc_parts(InflateArgs A, uint64_t chunk, uint32_t maxc, uint32_t* parts) {
+    __shared__ CrcTables ct;
+    __shared__ uint32_t wc[4];
+    const uint32_t sid = blockIdx.y, c = blockIdx.x;
+    if (sid >= A.n) return;
+    const sdz_inflate_record* rec = A.rec + sid;
+    const uint64_t len = rec->out_len;
+    if (rec->container != SDZ_CONTAINER_GZIP || len <= chunk || (uint64_t)c * chunk >= len) return;
+    crc_tables_init(ct);
+    __syncthreads();
+    const uint64_t a = (uint64_t)c * chunk, n = len - a < chunk ? len - a : chunk;
+    const uint64_t q = ((n + 3) / 4 + 7) & ~7ull;        // a quarter per wave (8-byte multiples)
+    const uint32_t w = threadIdx.x >> 6;
+    const uint64_t b0 = (uint64_t)w * q < n ? (uint64_t)w * q : n, b1 = b0 + q < n ? b0 + q : n;
+    const uint32_t cr = crc32_wave(A.out + A.out_off[sid] + a + b0, b1 - b0, ct);
+    if ((threadIdx.x & 63u) == 0) wc[w] = cr;
+    __syncthreads();
+    if (threadIdx.x != 0) return;
+    uint32_t crc = 0;
+    for (uint32_t k = 0; k < 4; ++k) {
+        const uint64_t lo = (uint64_t)k * q < n ? (uint64_t)k * q : n, hi = lo + q < n ? lo + q : n;
+        crc = gf2_mulmod(gf2_xbytes(hi - lo, ct.x2n), crc) ^ wc[k];
+    }
+    parts[(uint64_t)sid * maxc + c] = crc;
+}
+
+__global__ __launch_bounds__(64) void k_inflate_finalize(InflateArgs A, uint64_t chunk, uint32_t maxc,
+                                                         const uint32_t* parts) {
     __shared__ CrcTables ct;
     const uint32_t sid = blockIdx.x;
     if (sid >= A.n) return;
@@ -761,8 +792,17 @@ __global__ __launch_bounds__(64) void k_inflate_finalize(InflateArgs A) {
     crc_tables_init(ct);
     __syncthreads();
     const uint64_t len = rec->out_len;
-    uint32_t crc = crc32_wave(A.out + A.out_off[sid], len, ct);
-    if (threadIdx.x != 0) return;
+    uint32_t crc = 0;
+    if (len <= chunk) {
+        crc = crc32_wave(A.out + A.out_off[sid], len, ct);
+        if (threadIdx.x != 0) return;
+    } else {
+        if (threadIdx.x != 0) return;
+        for (uint64_t a = 0, c = 0; a < len; a += chunk, ++c) {
+            const uint64_t n = len - a < chunk ? len - a : chunk;
+            crc = gf2_mulmod(gf2_xbytes(n, ct.x2n), crc) ^ parts[(uint64_t)sid * maxc + c];
+        }
+    }
     RSave* R = (RSave*)A.rsave + sid;
     bool have = len > 0;
     if (A.streaming) {
@@ -781,8 +821,26 @@ __global__ __launch_bounds__(64) void k_inflate_finalize(InflateArgs A) {
 
 uint32_t resolve_block_threads() { return RS_THREADS; }
 uint32_t resolve_streams_per_block() { return 1; }
+// parts: scratch for the chunk crcs (a.tokens: the token rings are free once the rounds are
+// done; >= 1024 entries per stream); chunks of >= 256 KiB, <= 1024 per stream and <= 4 Mi
+// blocks in all
 void launch_inflate_finalize(const InflateArgs& a, hipStream_t s) {
-    hipLaunchKernelGGL(k_inflate_finalize, dim3(a.n), dim3(64), 0, s, a);
+    uint64_t mx = 0;
+    uint64_t chunk = 256 << 10;
+    uint32_t maxc = 1;
+    unsigned long long* slot = (unsigned long long*)a.tokens;
+    uint32_t* parts = a.tokens + 64;
+    if (device_max_u64(a.out_cap, a.n, slot, &mx, s) == 0 && mx > chunk) {
+        uint64_t c = (mx + chunk - 1) / chunk;
+        const uint64_t lim = std::min<uint64_t>(1024, std::max<uint64_t>(1, (4ull << 20) / a.n));
+        if (c > lim) { c = lim; chunk = ((mx + c - 1) / c + 7) & ~7ull; }
+        maxc = (uint32_t)c;
+        if ((uint64_t)maxc * a.n + 64 <= (uint64_t)a.round_tokens * a.n)
+            hipLaunchKernelGGL(k_gzip_crc_parts, dim3(maxc, a.n), dim3(256), 0, s, a, chunk, maxc, parts);
+        else
+            chunk = ~0ull;                               // (no room: one wave per stream)
+    }
+    hipLaunchKernelGGL(k_inflate_finalize, dim3(a.n), dim3(64), 0, s, a, chunk, maxc, (const uint32_t*)parts);
 }
 
 }  // namespace sdz

@@ -35,27 +35,107 @@ __device__ __forceinline__ uint32_t sp_bits(const uint8_t* p, uint64_t pos, int 
     return (v >> (pos & 7)) & ((1u << n) - 1u);
 }
 
-// The deep test from the code-length code on (infblocks.ts:354-551 / inftree.ts:313-379 on a
-// strict reading: every code complete).  cl: the 19 code-length code lengths.  Literal/
-// length and distance lengths are summed into Kraft counters as they are decoded, so a
-// random bit string is usually rejected after a few lengths.
-__device__ __noinline__ bool sp_deep(const uint8_t* p, uint64_t nbits, uint64_t pos, int hlit, int hdist,
-                                     uint64_t cl) {
-    int cnt[8];
+// Pass 1 (k_split_filter): one lane tests 32 consecutive bit positions -- the block-type bits
+// of all 32 at once from a 64-bit window, then HLIT/HDIST and the Kraft sum of the code-length
+// code (its order does not matter for the sum) from registers.  About 0.1 % of positions pass
+// (measured on zlib output); they are appended, (position << 20 | split index), to a list.
+// Each block walks a contiguous range of lanes, so the split stream of a lane is found by
+// stepping forward, not by a search per lane.
+__global__ __launch_bounds__(256) void k_split_filter(const uint8_t* in, const uint64_t* in_off, const SplitInfo* sp,
+                                                      uint32_t nsplit, uint64_t total_lanes, uint64_t lanes_per_block,
+                                                      uint64_t* surv, uint32_t* nsurv, uint32_t cap) {
+    const uint64_t L0 = (uint64_t)blockIdx.x * lanes_per_block;
+    if (L0 >= total_lanes) return;
+    const uint64_t L1 = L0 + lanes_per_block < total_lanes ? L0 + lanes_per_block : total_lanes;
+    uint32_t lo = 0, hi = nsplit;                         // the split stream holding lane L0
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (sp[mid].lane0 <= L0) lo = mid; else hi = mid;
+    }
+    uint32_t k = lo;
+    for (uint64_t g = L0 + threadIdx.x; g < L1; g += 256) {
+        while (k + 1 < nsplit && sp[k + 1].lane0 <= g) ++k;
+        const SplitInfo& S = sp[k];
+        const uint64_t p0 = 32 * (g - S.lane0);
+        const uint64_t nbits = S.nbits;
+        const uint32_t* p32 = (const uint32_t*)(in + in_off[S.sid] + (p0 >> 3));   // 4-byte aligned
+        uint32_t w0 = p32[0], w1 = p32[1], w2 = p32[2], w3 = p32[3];   // 64 B of slack past every input
+        const uint64_t W = (uint64_t)w0 | ((uint64_t)w1 << 32);
+        uint32_t M = (uint32_t)((~W >> 1) & (W >> 2));        // BTYPE = 2 (bits 1, 2 = 0, 1)
+        uint64_t out[4];
+        uint32_t no = 0;
+        while (M) {
+            const uint32_t i = (uint32_t)__builtin_ctz(M);
+            M &= M - 1;
+            const uint32_t a = __builtin_amdgcn_alignbit(w1, w0, i);    // bits i .. i+31
+            const uint32_t b = __builtin_amdgcn_alignbit(w2, w1, i);    // bits i+32 .. i+63
+            const uint32_t c = __builtin_amdgcn_alignbit(w3, w2, i);    // bits i+64 .. i+95
+            const uint32_t hlit = (a >> 3) & 31u, hdist = (a >> 8) & 31u, hclen = (a >> 13) & 15u;
+            const uint64_t q = (((uint64_t)b << 32) | a) >> 17;          // fields 0..14 of the code-length code
+            const uint32_t r = (uint32_t)((((uint64_t)c << 32) | b) >> 30);   // fields 15..18
+            uint32_t kraft = 0;
 #pragma unroll
-    for (int k = 0; k < 8; ++k) cnt[k] = 0;
-    for (int s = 0; s < 19; ++s) cnt[(cl >> (3 * s)) & 7]++;
-    // canonical code-length code: first code and first index per length
-    int first[8], base[8];
-    uint8_t syms[19];
+            for (int f = 0; f < 19; ++f) {
+                const uint32_t len = f < 15 ? (uint32_t)(q >> (3 * f)) & 7u : (r >> (3 * (f - 15))) & 7u;
+                kraft += (f < (int)hclen + 4 && len) ? 128u >> len : 0u;
+            }
+            const bool pass = hlit <= 29 && hdist <= 29 && kraft == 128u && p0 + i + 17 + 57 <= nbits;
+            if (pass && no < 4) out[no++] = ((p0 + i) << 20) | k;
+        }
+        // append this lane's survivors (at most 4 of 32 positions: more is not a real stream)
+        const uint64_t bm = __ballot(no != 0);
+        if (bm) {
+            uint32_t tot = no;                             // wave prefix of the counts
+            uint32_t pre = 0;
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t v = __shfl_up(tot, o);
+                if ((threadIdx.x & 63u) >= (uint32_t)o) tot += v;
+            }
+            pre = tot - no;
+            const uint32_t wsum = __shfl(tot, 63);
+            uint32_t base = 0;
+            if ((threadIdx.x & 63u) == 63u) base = atomicAdd(nsurv, wsum);
+            base = __shfl(base, 63);
+            for (uint32_t j = 0; j < no; ++j)
+                if (base + pre + j < cap) surv[base + pre + j] = out[j];
+        }
+    }
+}
+
+// Pass 2 (k_split_deep): one lane per survivor decodes the code lengths (infblocks.ts:354-551 /
+// inftree.ts:313-379 on a strict reading: every code complete) with the code-length code in a
+// 128-entry LDS table, and keeps Kraft sums of the literal/length and distance lengths as it
+// goes, so a random bit string is rejected after a few lengths.  Survivors are candidates.
+__global__ __launch_bounds__(256) void k_split_deep(const uint8_t* in, const uint64_t* in_off, SplitInfo* sp,
+                                                    const uint64_t* surv, const uint32_t* nsurv, uint32_t cap,
+                                                    uint64_t* cand) {
+    __shared__ uint8_t lut[256][128];                     // 7 stream bits -> symbol << 3 | code length
+    const uint32_t t = blockIdx.x * 256 + threadIdx.x;
+    const uint32_t ns = *nsurv < cap ? *nsurv : cap;
+    if (t >= ns) return;
+    const uint64_t e = surv[t];
+    const uint32_t k = (uint32_t)(e & 0xfffffu);
+    uint64_t pos = e >> 20;
+    SplitInfo& S = sp[k];
+    const uint8_t* p = in + in_off[S.sid];
+    const uint64_t nbits = S.nbits;
+    const uint64_t h = sp_bits(p, pos, 17);
+    const int hlit = (int)((h >> 3) & 31u) + 257, hdist = (int)((h >> 8) & 31u) + 1, hclen = (int)(h >> 13) + 4;
+    pos += 17;
+    uint64_t cl = 0;                                      // the 19 lengths, 3 bits each, symbol order
+    for (int i = 0; i < hclen; ++i) { cl |= (uint64_t)sp_bits(p, pos, 3) << (3 * c_split_border[i]); pos += 3; }
+    uint8_t* T = lut[threadIdx.x];
     {
-        int code = 0, k = 0;
-        for (int l = 1; l < 8; ++l) {
-            first[l] = code;
-            base[l] = k;
-            for (int s = 0; s < 19; ++s)
-                if ((int)((cl >> (3 * s)) & 7) == l) syms[k++] = (uint8_t)s;
-            code = (code + cnt[l]) << 1;
+        int code = 0;
+        for (int l = 1; l < 8; ++l) {                     // canonical codes, MSB first in the stream
+            for (int sym = 0; sym < 19; ++sym) {
+                if ((int)((cl >> (3 * sym)) & 7u) != l) continue;
+                uint32_t rev = 0;
+                for (int j = 0; j < l; ++j) rev |= (uint32_t)((code >> (l - 1 - j)) & 1) << j;
+                for (uint32_t x = rev; x < 128u; x += 1u << l) T[x] = (uint8_t)(sym << 3 | l);
+                ++code;
+            }
+            code <<= 1;
         }
     }
     const int total = hlit + hdist;
@@ -63,91 +143,34 @@ __device__ __noinline__ bool sp_deep(const uint8_t* p, uint64_t nbits, uint64_t 
     uint32_t kl = 0, kd = 0;                              // Kraft sums in units of 2^-15
     bool eob = false;
     while (n < total) {
-        if (pos + 7 + 7 > nbits) return false;
+        if (pos + 14 > nbits) return;
         const uint32_t w = sp_bits(p, pos, 14);
-        int code = 0, sym = -1, l = 1;
-        for (; l < 8; ++l) {
-            code = (code << 1) | (int)((w >> (l - 1)) & 1u);
-            if (cnt[l] && code - first[l] < cnt[l]) { sym = syms[base[l] + code - first[l]]; break; }
-        }
-        if (sym < 0) return false;
+        const uint32_t v = T[w & 127u];
+        const int sym = (int)(v >> 3), l = (int)(v & 7u);
         pos += (uint64_t)l;
         int rep = 1, val = sym;
         if (sym >= 16) {
             const int eb = sym == 16 ? 2 : sym == 17 ? 3 : 7;
-            const int r = (int)((w >> l) & ((1u << eb) - 1u));
+            rep = (sym == 18 ? 11 : 3) + (int)((w >> l) & ((1u << eb) - 1u));
             pos += (uint64_t)eb;
-            rep = (sym == 16 ? 3 : sym == 17 ? 3 : 11) + r;
-            if (sym == 16 && n == 0) return false;
+            if (sym == 16 && n == 0) return;
             val = sym == 16 ? prev : 0;
-            if (n + rep > total) return false;
+            if (n + rep > total) return;
         }
         if (val) {
             const uint32_t u = 32768u >> val;
-            for (int r = 0; r < rep; ++r, ++n) {
-                if (n < hlit) { kl += u; if (n == 256) eob = true; }
-                else kd += u;
-            }
-            if (kl > 32768u || kd > 32768u) return false;
-        } else {
-            n += rep;
+            const int nl = n < hlit ? (hlit - n < rep ? hlit - n : rep) : 0;   // of them literal/length
+            kl += (uint32_t)nl * u;
+            kd += (uint32_t)(rep - nl) * u;
+            eob = eob || (n <= 256 && 256 < n + nl);
+            if (kl > 32768u || kd > 32768u) return;
         }
+        n += rep;
         prev = val;
     }
-    return eob && kl == 32768u && kd == 32768u;
-}
-
-// One lane tests 32 consecutive bit positions: the block-type bits of all 32 at once from a
-// 64-bit window, then the header fields and the code-length code's Kraft sum (from a
-// 160-bit window in registers) for the survivors, then the deep test for the rare rest.
-__global__ __launch_bounds__(256) void k_split_find(const uint8_t* in, const uint64_t* in_off, SplitInfo* sp,
-                                                    uint32_t nsplit, uint64_t* cand, uint64_t total_lanes) {
-    const uint64_t g = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-    if (g >= total_lanes) return;
-    uint32_t lo = 0, hi = nsplit;                         // the stream whose lane range holds g
-    while (hi - lo > 1) {
-        const uint32_t mid = (lo + hi) >> 1;
-        if (sp[mid].lane0 <= g) lo = mid; else hi = mid;
-    }
-    SplitInfo& S = sp[lo];
-    const uint64_t p0 = 32 * (g - S.lane0);
-    const uint64_t nbits = S.nbits;
-    if (p0 >= nbits) return;
-    const uint8_t* p = in + in_off[S.sid];
-    uint32_t w[5];
-    const uint32_t* p32 = (const uint32_t*)(p + (p0 >> 3));   // p0 is a multiple of 32: 4-byte aligned
-#pragma unroll
-    for (int k = 0; k < 5; ++k) w[k] = p32[k];                // 64 B of slack past every input
-    const uint64_t W = (uint64_t)w[0] | ((uint64_t)w[1] << 32);
-    uint32_t M = (uint32_t)((~W >> 1) & (W >> 2));            // BTYPE = 2 (bits 1, 2 = 0, 1)
-    while (M) {
-        const int i = __builtin_ctz(M);
-        M &= M - 1;
-        const uint64_t pos = p0 + (uint64_t)i;
-        if (pos + 17 + 57 > nbits) continue;
-        auto win = [&](int b) -> uint32_t {                  // 32 bits from bit b of the window
-            const int k = b >> 5, s = b & 31;
-            const uint32_t a = k == 0 ? w[0] : k == 1 ? w[1] : k == 2 ? w[2] : w[3];
-            const uint32_t c = k == 0 ? w[1] : k == 1 ? w[2] : k == 2 ? w[3] : w[4];
-            return s ? (a >> s) | (c << (32 - s)) : a;
-        };
-        const uint32_t h = win(i) & 0x1ffffu;
-        const int hlit = (int)((h >> 3) & 31u), hdist = (int)((h >> 8) & 31u), hclen = (int)(h >> 13) + 4;
-        if (hlit > 29 || hdist > 29) continue;
-        const uint32_t a = win(i + 17), b = win(i + 17 + 32);
-        const uint64_t bits = (uint64_t)a | ((uint64_t)b << 32);  // the code-length code lengths
-        uint64_t cl = 0;
-        uint32_t kraft = 0;
-        for (int k = 0; k < hclen; ++k) {
-            const uint32_t len = (uint32_t)(bits >> (3 * k)) & 7u;
-            cl |= (uint64_t)len << (3 * c_split_border[k]);
-            kraft += len ? 128u >> len : 0u;
-        }
-        if (kraft != 128u) continue;                      // complete code-length code
-        if (!sp_deep(p, nbits, pos + 17 + 3 * (uint64_t)hclen, hlit + 257, hdist + 1, cl)) continue;
-        const uint32_t k = atomicAdd(&S.ncand, 1u);
-        if (k < SP_CAND_MAX) cand[(uint64_t)lo * SP_CAND_MAX + k] = pos;
-    }
+    if (!(eob && kl == 32768u && kd == 32768u)) return;
+    const uint32_t j = atomicAdd(&S.ncand, 1u);
+    if (j < SP_CAND_MAX) cand[(uint64_t)k * SP_CAND_MAX + j] = e >> 20;
 }
 
 // bitonic sort of each stream's candidates in LDS (one workgroup per split stream)
@@ -270,13 +293,18 @@ __global__ __launch_bounds__(256) void k_seg_feed(InflateArgs A, const SplitInfo
     const uint32_t* ch = chain + S.chain0;
     const uint64_t* ct = chain_tok + S.chain0;
     uint32_t* dst = A.tokens + (uint64_t)sid * T;
-    for (uint64_t t = t0 + threadIdx.x; t < t1; t += 256) {
-        uint32_t lo = 0, hi = S.chain_len;               // the chain entry holding stream token t
-        while (hi - lo > 1) {
-            const uint32_t mid = (lo + hi) >> 1;
-            if (ct[mid] <= t) lo = mid; else hi = mid;
-        }
-        dst[t - t0] = segtok[seg[ch[lo]].tok + (t - ct[lo])];
+    uint32_t lo = 0, hi = S.chain_len;                   // the chain entry holding stream token t0
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (ct[mid] <= t0) lo = mid; else hi = mid;
+    }
+    // entry by entry, the whole block copies the entry's part of [t0, t1)
+    for (uint32_t c = lo; c < S.chain_len && ct[c] < t1; ++c) {
+        const uint64_t a = ct[c] > t0 ? ct[c] : t0;
+        const uint64_t b = c + 1 < S.chain_len && ct[c + 1] < t1 ? ct[c + 1] : t1;
+        const uint32_t* src = segtok + seg[ch[c]].tok + (a - ct[c]);
+        uint32_t* d = dst + (a - t0);
+        for (uint64_t t = threadIdx.x; t < b - a; t += 256) d[t] = src[t];
     }
     if (threadIdx.x == 0) {
         const bool last = t1 == S.ntok;
@@ -287,9 +315,12 @@ __global__ __launch_bounds__(256) void k_seg_feed(InflateArgs A, const SplitInfo
 }
 
 void launch_split_find(const uint8_t* in, const uint64_t* in_off, SplitInfo* sp, uint32_t nsplit, uint64_t* cand,
-                       uint64_t total_lanes, hipStream_t s) {
-    hipLaunchKernelGGL(k_split_find, dim3((uint32_t)((total_lanes + 255) / 256)), dim3(256), 0, s, in, in_off, sp,
-                       nsplit, cand, total_lanes);
+                       uint64_t total_lanes, uint64_t* surv, uint32_t* nsurv, uint32_t cap, hipStream_t s) {
+    const uint64_t blocks = 8192;                         // persistent: each block a contiguous lane range
+    const uint64_t per = ((total_lanes + blocks - 1) / blocks + 255) & ~255ull;
+    hipLaunchKernelGGL(k_split_filter, dim3((uint32_t)((total_lanes + per - 1) / per)), dim3(256), 0, s, in, in_off,
+                       sp, nsplit, total_lanes, per, surv, nsurv, cap);
+    hipLaunchKernelGGL(k_split_deep, dim3((cap + 255) / 256), dim3(256), 0, s, in, in_off, sp, surv, nsurv, cap, cand);
     hipLaunchKernelGGL(k_split_sort, dim3(nsplit), dim3(256), 0, s, sp, cand);
 }
 void launch_seg_chain(const InflateArgs& a, SplitInfo* sp, uint32_t nsplit, const SegInfo* seg, const uint64_t* cand,

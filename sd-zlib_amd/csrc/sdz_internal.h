@@ -64,7 +64,7 @@ int run_inflate_rounds(const InflateArgs& a, hipStream_t s, uint32_t* host_activ
 void launch_istate_reset(uint8_t* dsave, uint8_t* rsave, uint32_t n, hipStream_t s);
 // block-parallel decode of long streams (k_split.hip)
 void launch_split_find(const uint8_t* in, const uint64_t* in_off, SplitInfo* sp, uint32_t nsplit, uint64_t* cand,
-                       uint64_t total_lanes, hipStream_t s);
+                       uint64_t total_lanes, uint64_t* surv, uint32_t* nsurv, uint32_t cap, hipStream_t s);
 void launch_seg_decode(const InflateArgs& a, hipStream_t s);
 void launch_seg_chain(const InflateArgs& a, SplitInfo* sp, uint32_t nsplit, const SegInfo* seg, const uint64_t* cand,
                       const void* segD, uint32_t* chain, uint64_t* chain_tok, uint32_t* split_state, hipStream_t s);

@@ -355,14 +355,21 @@ int inflate_split_plan(InflateArgs& a, hipStream_t s, PoolUse& use, SplitHost& H
     if (ms) { (void)hipEventCreate(&e0); (void)hipEventCreate(&e1); (void)hipEventRecord(e0, s); }
     const uint32_t ns = (uint32_t)sp.size();
     // phase 1: candidates (their own allocation: freed at the end of this function)
+    // (filter survivors: ~0.1 % of positions on zlib output; room for 0.2 %, and a stream's
+    // candidates beyond that are only lost parallelism: its segments get longer)
     uint8_t* d1 = nullptr;
     const size_t cand_bytes = (size_t)ns * SP_CAND_MAX * sizeof(uint64_t);
-    HIPCHK(hipMalloc(&d1, ns * sizeof(SplitInfo) + cand_bytes));
+    const uint32_t scap = (uint32_t)std::min<uint64_t>(1u << 30, std::max<uint64_t>(4096, lanes * 32 / 512));
+    const size_t b1 = ns * sizeof(SplitInfo) + cand_bytes + (size_t)scap * sizeof(uint64_t) + 256;
+    HIPCHK(hipMalloc(&d1, b1));
     struct Free { uint8_t* p; ~Free() { if (p) hipFree(p); } } free1{ d1 };
     SplitInfo* d_sp1 = (SplitInfo*)d1;
     uint64_t* d_cand1 = (uint64_t*)(d1 + ns * sizeof(SplitInfo));
+    uint64_t* d_surv = d_cand1 + (size_t)ns * SP_CAND_MAX;
+    uint32_t* d_nsurv = (uint32_t*)(d_surv + scap);
     HIPCHK(hipMemcpyAsync(d_sp1, sp.data(), ns * sizeof(SplitInfo), hipMemcpyHostToDevice, s));
-    launch_split_find(a.in, a.in_off, d_sp1, ns, d_cand1, lanes, s);
+    HIPCHK(hipMemsetAsync(d_nsurv, 0, sizeof(uint32_t), s));
+    launch_split_find(a.in, a.in_off, d_sp1, ns, d_cand1, lanes, d_surv, d_nsurv, scap, s);
     HIPCHK(hipGetLastError());
     std::vector<uint64_t> cand((size_t)ns * SP_CAND_MAX);
     HIPCHK(hipMemcpyAsync(sp.data(), d_sp1, ns * sizeof(SplitInfo), hipMemcpyDeviceToHost, s));
