@@ -1028,7 +1028,10 @@ __global__ __launch_bounds__(IL_THREADS, 1) void k_inflate_decode(InflateArgs A,
     uint32_t gid = blockIdx.x * IL_STREAMS + lane_slot();
     bool valid = gid < A.n && (threadIdx.x & 63u) < IL_WAVE_LANES;
     uint32_t sid = valid ? gid : 0u;
-    if (valid && A.split_state && A.split_state[sid]) valid = false;   // fed by k_seg_feed
+    if (valid && A.split_state) {                        // split streams: see split.h
+        const uint32_t st = A.split_state[sid];
+        valid = A.fallback_pass ? st == SPS_FALLBACK : (st == 0 || st == SPS_FALLBACK);
+    }
     const uint32_t xid = A.segmode ? A.seg[sid].stream : sid;           // the stream of the input
     DSave* S = (DSave*)A.dsave + sid;
     uint32_t* tb = A.segmode ? A.segtok + A.seg[sid].tok : A.tokens + (uint64_t)sid * A.round_tokens;
@@ -1129,7 +1132,19 @@ int run_inflate_rounds(const InflateArgs& a, hipStream_t s, uint32_t* host_activ
         if (hipMemsetAsync(a.active, 0, sizeof(uint32_t), s) != hipSuccess) { rc = -1; break; }
         if (kernel_ms) (void)hipEventRecord(ev[0], s);
         hipLaunchKernelGGL(k_inflate_decode, g1, dim3(IL_THREADS), 0, s, a, round);
-        if (a.split_plan) launch_seg_feed(a, round, s);  // the split streams' tokens (k_split.hip)
+        if (a.split_plan) {                              // the split streams (k_split.hip)
+            if (round == 0) {
+                // segments decoded on the side stream meanwhile: chain them, decode the
+                // streams whose chain broke, serially from their start
+                const SplitPlan& P = *a.split_plan;
+                if (hipStreamWaitEvent(s, (hipEvent_t)P.ready, 0) != hipSuccess) { rc = -1; break; }
+                launch_seg_chain(a, P.sp, P.nsplit, P.seg, P.cand, P.segD, P.chain, P.chain_tok, a.split_state, s);
+                InflateArgs f = a;
+                f.fallback_pass = 1;
+                hipLaunchKernelGGL(k_inflate_decode, g1, dim3(IL_THREADS), 0, s, f, 0u);
+            }
+            launch_seg_feed(a, round, s);
+        }
         if (kernel_ms) (void)hipEventRecord(ev[1], s);
         hipLaunchKernelGGL(k_inflate_resolve, g2, dim3(resolve_block_threads()), 0, s, a, round);
         if (kernel_ms) (void)hipEventRecord(ev[2], s);

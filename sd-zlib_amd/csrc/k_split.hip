@@ -28,24 +28,45 @@ namespace sdz {
 
 __constant__ uint8_t c_split_border[19] = { 16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15 };
 
-// n <= 25 bits at bit position `pos` of p (byte loads: any alignment, reads <= 4 bytes on)
-__device__ __forceinline__ uint32_t sp_bits(const uint8_t* p, uint64_t pos, int n) {
-    const uint8_t* q = p + (pos >> 3);
-    const uint32_t v = (uint32_t)q[0] | ((uint32_t)q[1] << 8) | ((uint32_t)q[2] << 16) | ((uint32_t)q[3] << 24);
-    return (v >> (pos & 7)) & ((1u << n) - 1u);
+// little-endian u32 at byte q of an input of `len` bytes (q may be unaligned; bytes past the
+// end read as 0, so no lane reads past its stream's last byte)
+__device__ __forceinline__ uint32_t sp_u32(const uint8_t* p, uint64_t q, uint64_t len) {
+    if (q + 4 <= len) {
+        const uint8_t* r = p + q;
+        return (uint32_t)r[0] | ((uint32_t)r[1] << 8) | ((uint32_t)r[2] << 16) | ((uint32_t)r[3] << 24);
+    }
+    uint32_t v = 0;
+    for (uint32_t j = 0; j < 4; ++j) if (q + j < len) v |= (uint32_t)p[q + j] << (8 * j);
+    return v;
+}
+__device__ __forceinline__ uint32_t sp_u32a(const uint8_t* p, uint64_t q, uint64_t len) {   // q % 4 == 0
+    if (q + 4 <= len && (((uintptr_t)(p + q)) & 3) == 0) return *(const uint32_t*)(p + q);
+    return sp_u32(p, q, len);
 }
 
-// Pass 1 (k_split_filter): one lane tests 32 consecutive bit positions -- the block-type bits
-// of all 32 at once from a 64-bit window, then HLIT/HDIST and the Kraft sum of the code-length
-// code (its order does not matter for the sum) from registers.  About 0.1 % of positions pass
-// (measured on zlib output); they are appended, (position << 20 | split index), to a list.
+// Pass 1 (k_split_filter): one lane tests 32 consecutive bit positions.  Bit-sliced over the
+// 32 positions (one mask bit each): BTYPE = 2, HLIT <= 29, HDIST <= 29 and room for a header
+// (about 22 % pass); then, per remaining position, the Kraft sum of the code-length code's
+// first HCLEN + 4 lengths (their order does not matter for the sum) from a 4096-entry LDS
+// table of 4-length partial sums, 5 lookups.  About 0.1 % of positions pass (measured on zlib
+// output); they go, (position << 20 | split index), to the block's own survivor region.
 // Each block walks a contiguous range of lanes, so the split stream of a lane is found by
 // stepping forward, not by a search per lane.
 __global__ __launch_bounds__(256) void k_split_filter(const uint8_t* in, const uint64_t* in_off, const SplitInfo* sp,
                                                       uint32_t nsplit, uint64_t total_lanes, uint64_t lanes_per_block,
-                                                      uint64_t* surv, uint32_t* nsurv, uint32_t cap) {
+                                                      uint64_t* surv, uint32_t* nsurv, uint32_t bcap) {
+    __shared__ uint32_t cnt;
+    __shared__ uint8_t klut[4096];                        // 4 lengths (3 bits each) -> sum of 128 >> len (len > 0)
     const uint64_t L0 = (uint64_t)blockIdx.x * lanes_per_block;
     if (L0 >= total_lanes) return;
+    for (uint32_t x = threadIdx.x; x < 4096; x += 256) {
+        uint32_t k = 0;
+        for (int j = 0; j < 4; ++j) k += (128u >> ((x >> (3 * j)) & 7u)) & 127u;
+        klut[x] = (uint8_t)(k < 255 ? k : 255);
+    }
+    if (threadIdx.x == 0) cnt = 0;
+    __syncthreads();
+    surv += (uint64_t)blockIdx.x * bcap;                  // this block's own region: no global atomics
     const uint64_t L1 = L0 + lanes_per_block < total_lanes ? L0 + lanes_per_block : total_lanes;
     uint32_t lo = 0, hi = nsplit;                         // the split stream holding lane L0
     while (hi - lo > 1) {
@@ -57,11 +78,19 @@ __global__ __launch_bounds__(256) void k_split_filter(const uint8_t* in, const u
         while (k + 1 < nsplit && sp[k + 1].lane0 <= g) ++k;
         const SplitInfo& S = sp[k];
         const uint64_t p0 = 32 * (g - S.lane0);
-        const uint64_t nbits = S.nbits;
-        const uint32_t* p32 = (const uint32_t*)(in + in_off[S.sid] + (p0 >> 3));   // 4-byte aligned
-        uint32_t w0 = p32[0], w1 = p32[1], w2 = p32[2], w3 = p32[3];   // 64 B of slack past every input
+        const uint64_t nbits = S.nbits, nbytes = nbits >> 3;
+        const uint8_t* p = in + in_off[S.sid];
+        const uint64_t q = p0 >> 3;
+        const uint32_t w0 = sp_u32a(p, q, nbytes), w1 = sp_u32a(p, q + 4, nbytes);
+        const uint32_t w2 = sp_u32a(p, q + 8, nbytes), w3 = sp_u32a(p, q + 12, nbytes);
         const uint64_t W = (uint64_t)w0 | ((uint64_t)w1 << 32);
-        uint32_t M = (uint32_t)((~W >> 1) & (W >> 2));        // BTYPE = 2 (bits 1, 2 = 0, 1)
+#define SPB(d) ((uint32_t)(W >> (d)))
+        uint32_t M = ~SPB(1) & SPB(2)                                   // BTYPE = 2 (bits 1, 2 = 0, 1)
+                   & ~(SPB(4) & SPB(5) & SPB(6) & SPB(7))               // HLIT (bits 3-7) < 30
+                   & ~(SPB(9) & SPB(10) & SPB(11) & SPB(12));           // HDIST (bits 8-12) < 30
+#undef SPB
+        const uint64_t room = nbits >= p0 + 74 ? nbits - p0 - 74 + 1 : 0;   // header of 17 + 57 bits fits
+        M &= room >= 32 ? 0xffffffffu : (uint32_t)((1ull << room) - 1);
         uint64_t out[4];
         uint32_t no = 0;
         while (M) {
@@ -70,72 +99,103 @@ __global__ __launch_bounds__(256) void k_split_filter(const uint8_t* in, const u
             const uint32_t a = __builtin_amdgcn_alignbit(w1, w0, i);    // bits i .. i+31
             const uint32_t b = __builtin_amdgcn_alignbit(w2, w1, i);    // bits i+32 .. i+63
             const uint32_t c = __builtin_amdgcn_alignbit(w3, w2, i);    // bits i+64 .. i+95
-            const uint32_t hlit = (a >> 3) & 31u, hdist = (a >> 8) & 31u, hclen = (a >> 13) & 15u;
-            const uint64_t q = (((uint64_t)b << 32) | a) >> 17;          // fields 0..14 of the code-length code
-            const uint32_t r = (uint32_t)((((uint64_t)c << 32) | b) >> 30);   // fields 15..18
-            uint32_t kraft = 0;
-#pragma unroll
-            for (int f = 0; f < 19; ++f) {
-                const uint32_t len = f < 15 ? (uint32_t)(q >> (3 * f)) & 7u : (r >> (3 * (f - 15))) & 7u;
-                kraft += (f < (int)hclen + 4 && len) ? 128u >> len : 0u;
-            }
-            const bool pass = hlit <= 29 && hdist <= 29 && kraft == 128u && p0 + i + 17 + 57 <= nbits;
-            if (pass && no < 4) out[no++] = ((p0 + i) << 20) | k;
+            const uint32_t hclen = (a >> 13) & 15u;
+            uint64_t X = ((((uint64_t)b << 32) | a) >> 17) | ((uint64_t)c << 47);   // the 19 lengths' bits
+            X &= (1ull << (3 * hclen + 12)) - 1;                          // the HCLEN + 4 sent
+            const uint32_t kraft = (uint32_t)klut[X & 4095u] + klut[(X >> 12) & 4095u] + klut[(X >> 24) & 4095u] +
+                                   klut[(X >> 36) & 4095u] + klut[(X >> 48) & 4095u];
+            if (kraft == 128u && no < 4) out[no++] = ((p0 + i) << 20) | k;
         }
         // append this lane's survivors (at most 4 of 32 positions: more is not a real stream)
         const uint64_t bm = __ballot(no != 0);
         if (bm) {
             uint32_t tot = no;                             // wave prefix of the counts
-            uint32_t pre = 0;
             for (int o = 1; o < 64; o <<= 1) {
                 const uint32_t v = __shfl_up(tot, o);
                 if ((threadIdx.x & 63u) >= (uint32_t)o) tot += v;
             }
-            pre = tot - no;
+            const uint32_t pre = tot - no;
             const uint32_t wsum = __shfl(tot, 63);
             uint32_t base = 0;
-            if ((threadIdx.x & 63u) == 63u) base = atomicAdd(nsurv, wsum);
+            if ((threadIdx.x & 63u) == 63u) base = atomicAdd(&cnt, wsum);
             base = __shfl(base, 63);
             for (uint32_t j = 0; j < no; ++j)
-                if (base + pre + j < cap) surv[base + pre + j] = out[j];
+                if (base + pre + j < bcap) surv[base + pre + j] = out[j];
         }
     }
+    __syncthreads();
+    if (threadIdx.x == 0) nsurv[blockIdx.x] = cnt < bcap ? cnt : bcap;
 }
+
+// bit reader over one input for k_split_deep: 64-bit buffer, refilled a word at a time
+struct SpBits {
+    const uint8_t* p;
+    uint64_t len, next;                                   // next byte to load
+    uint64_t buf;
+    uint32_t nb;                                          // valid bits in buf
+    __device__ __forceinline__ void init(const uint8_t* p_, uint64_t len_, uint64_t pos) {
+        p = p_; len = len_;
+        const uint64_t q = pos >> 3;
+        buf = ((uint64_t)sp_u32(p, q, len) | ((uint64_t)sp_u32(p, q + 4, len) << 32)) >> (pos & 7);
+        nb = 64 - (uint32_t)(pos & 7);
+        next = q + 8;
+    }
+    __device__ __forceinline__ void fill() {              // nb >= 32 after
+        if (nb < 32) { buf |= (uint64_t)sp_u32(p, next, len) << nb; next += 4; nb += 32; }
+    }
+    __device__ __forceinline__ uint32_t peek(uint32_t n) const { return (uint32_t)buf & ((1u << n) - 1u); }
+    __device__ __forceinline__ void drop(uint32_t n) { buf >>= n; nb -= n; }
+};
 
 // Pass 2 (k_split_deep): one lane per survivor decodes the code lengths (infblocks.ts:354-551 /
 // inftree.ts:313-379 on a strict reading: every code complete) with the code-length code in a
 // 128-entry LDS table, and keeps Kraft sums of the literal/length and distance lengths as it
-// goes, so a random bit string is rejected after a few lengths.  Survivors are candidates.
+// goes, so a random bit string is rejected as soon as one is over-subscribed.  Survivors are
+// candidates.
 __global__ __launch_bounds__(256) void k_split_deep(const uint8_t* in, const uint64_t* in_off, SplitInfo* sp,
-                                                    const uint64_t* surv, const uint32_t* nsurv, uint32_t cap,
+                                                    const uint64_t* surv, const uint32_t* nsurv, uint32_t bcap,
                                                     uint64_t* cand) {
     __shared__ uint8_t lut[256][128];                     // 7 stream bits -> symbol << 3 | code length
-    const uint32_t t = blockIdx.x * 256 + threadIdx.x;
-    const uint32_t ns = *nsurv < cap ? *nsurv : cap;
-    if (t >= ns) return;
+    const uint64_t t = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    const uint32_t fb = (uint32_t)(t / bcap);             // the filter block whose region holds t
+    if (t - (uint64_t)fb * bcap >= nsurv[fb]) return;
     const uint64_t e = surv[t];
     const uint32_t k = (uint32_t)(e & 0xfffffu);
     uint64_t pos = e >> 20;
     SplitInfo& S = sp[k];
-    const uint8_t* p = in + in_off[S.sid];
     const uint64_t nbits = S.nbits;
-    const uint64_t h = sp_bits(p, pos, 17);
+    SpBits R;
+    R.init(in + in_off[S.sid], nbits >> 3, pos);
+    const uint32_t h = R.peek(17);
+    R.drop(17);
+    R.fill();
     const int hlit = (int)((h >> 3) & 31u) + 257, hdist = (int)((h >> 8) & 31u) + 1, hclen = (int)(h >> 13) + 4;
-    pos += 17;
+    pos += 17 + 3 * (uint64_t)hclen;
     uint64_t cl = 0;                                      // the 19 lengths, 3 bits each, symbol order
-    for (int i = 0; i < hclen; ++i) { cl |= (uint64_t)sp_bits(p, pos, 3) << (3 * c_split_border[i]); pos += 3; }
+    uint64_t bl = 0;                                      // lengths 1..7: their counts, 8 bits each
+    for (int i = 0; i < hclen; ++i) {
+        const uint32_t l = R.peek(3);
+        R.drop(3);
+        if (i == 9) R.fill();
+        cl |= (uint64_t)l << (3 * c_split_border[i]);
+        bl += l ? 1ull << (8 * l) : 0ull;
+    }
     uint8_t* T = lut[threadIdx.x];
     {
-        int code = 0;
-        for (int l = 1; l < 8; ++l) {                     // canonical codes, MSB first in the stream
-            for (int sym = 0; sym < 19; ++sym) {
-                if ((int)((cl >> (3 * sym)) & 7u) != l) continue;
-                uint32_t rev = 0;
-                for (int j = 0; j < l; ++j) rev |= (uint32_t)((code >> (l - 1 - j)) & 1) << j;
-                for (uint32_t x = rev; x < 128u; x += 1u << l) T[x] = (uint8_t)(sym << 3 | l);
-                ++code;
-            }
-            code <<= 1;
+        // canonical codes (inftree.ts: shorter first, then symbol order), MSB first in the stream
+        uint64_t nx = 0;                                  // first code of each length, 8 bits each
+        uint32_t code = 0;
+        for (int l = 1; l < 8; ++l) {
+            code = (code + (uint32_t)((bl >> (8 * (l - 1))) & 255u)) << 1;
+            nx |= (uint64_t)code << (8 * l);
+        }
+        for (int sym = 0; sym < 19; ++sym) {
+            const uint32_t l = (uint32_t)(cl >> (3 * sym)) & 7u;
+            if (!l) continue;
+            const uint32_t c = (uint32_t)(nx >> (8 * l)) & 255u;
+            nx += 1ull << (8 * l);
+            const uint32_t rev = __builtin_bitreverse32(c) >> (32 - l);
+            for (uint32_t x = rev; x < 128u; x += 1u << l) T[x] = (uint8_t)(sym << 3 | l);
         }
     }
     const int total = hlit + hdist;
@@ -144,19 +204,21 @@ __global__ __launch_bounds__(256) void k_split_deep(const uint8_t* in, const uin
     bool eob = false;
     while (n < total) {
         if (pos + 14 > nbits) return;
-        const uint32_t w = sp_bits(p, pos, 14);
+        R.fill();
+        const uint32_t w = R.peek(14);
         const uint32_t v = T[w & 127u];
         const int sym = (int)(v >> 3), l = (int)(v & 7u);
-        pos += (uint64_t)l;
-        int rep = 1, val = sym;
+        int rep = 1, val = sym, used = l;
         if (sym >= 16) {
             const int eb = sym == 16 ? 2 : sym == 17 ? 3 : 7;
             rep = (sym == 18 ? 11 : 3) + (int)((w >> l) & ((1u << eb) - 1u));
-            pos += (uint64_t)eb;
+            used += eb;
             if (sym == 16 && n == 0) return;
             val = sym == 16 ? prev : 0;
             if (n + rep > total) return;
         }
+        R.drop((uint32_t)used);
+        pos += (uint64_t)used;
         if (val) {
             const uint32_t u = 32768u >> val;
             const int nl = n < hlit ? (hlit - n < rep ? hlit - n : rep) : 0;   // of them literal/length
@@ -264,9 +326,10 @@ __global__ void k_seg_chain(InflateArgs A, SplitInfo* sp, uint32_t nsplit, const
         end += 8 * (uint64_t)tb;
         status = end < nbits ? SDZ_TRAILING : SDZ_OK;
     }
+    if (A.out_off[sid] & 7) ok = false;                  // (the serial path reports it)
     S.chain_len = ok ? len : 0;
     S.ntok = ok ? ntok : 0;
-    split_state[sid] = ok ? 1u : 0u;
+    split_state[sid] = ok ? SPS_FED : SPS_FALLBACK;
     if (!ok) return;
     O->mode = LM_DONE; O->status = status; O->zmsg = 0; O->stall = 0; O->full = 0;
     O->bitpos = end; O->pos = out;
@@ -283,7 +346,7 @@ __global__ __launch_bounds__(256) void k_seg_feed(InflateArgs A, const SplitInfo
                                                   uint32_t round) {
     const SplitInfo& S = sp[blockIdx.x];
     const uint32_t sid = S.sid;
-    if (!split_state[sid]) return;                       // serial path
+    if (split_state[sid] != SPS_FED) return;            // serial path
     const uint64_t T = A.round_tokens, t0 = (uint64_t)round * T;
     if (t0 > S.ntok || (t0 == S.ntok && round > 0)) {    // finished in an earlier round
         if (threadIdx.x == 0) { A.ntok[sid] = 0; A.flags[sid] = 2; }
@@ -316,11 +379,16 @@ __global__ __launch_bounds__(256) void k_seg_feed(InflateArgs A, const SplitInfo
 
 void launch_split_find(const uint8_t* in, const uint64_t* in_off, SplitInfo* sp, uint32_t nsplit, uint64_t* cand,
                        uint64_t total_lanes, uint64_t* surv, uint32_t* nsurv, uint32_t cap, hipStream_t s) {
-    const uint64_t blocks = 8192;                         // persistent: each block a contiguous lane range
+    // persistent: each block a contiguous lane range and its own survivor region (cap / 8192
+    // entries; nsurv: SPLIT_FILTER_BLOCKS counts, zeroed by the caller)
+    const uint64_t blocks = SPLIT_FILTER_BLOCKS;
     const uint64_t per = ((total_lanes + blocks - 1) / blocks + 255) & ~255ull;
+    const uint32_t bcap = cap / SPLIT_FILTER_BLOCKS;
     hipLaunchKernelGGL(k_split_filter, dim3((uint32_t)((total_lanes + per - 1) / per)), dim3(256), 0, s, in, in_off,
-                       sp, nsplit, total_lanes, per, surv, nsurv, cap);
-    hipLaunchKernelGGL(k_split_deep, dim3((cap + 255) / 256), dim3(256), 0, s, in, in_off, sp, surv, nsurv, cap, cand);
+                       sp, nsplit, total_lanes, per, surv, nsurv, bcap);
+    const uint64_t nt = (uint64_t)bcap * SPLIT_FILTER_BLOCKS;
+    hipLaunchKernelGGL(k_split_deep, dim3((uint32_t)((nt + 255) / 256)), dim3(256), 0, s, in, in_off, sp, surv, nsurv,
+                       bcap, cand);
     hipLaunchKernelGGL(k_split_sort, dim3(nsplit), dim3(256), 0, s, sp, cand);
 }
 void launch_seg_chain(const InflateArgs& a, SplitInfo* sp, uint32_t nsplit, const SegInfo* seg, const uint64_t* cand,

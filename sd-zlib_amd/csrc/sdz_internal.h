@@ -49,7 +49,8 @@ struct InflateArgs {
     uint8_t* carry;              // n * SDZ_INFLATE_CARRY: input carried to the next call
     // block-parallel decode of long streams (k_split.hip, split.h)
     const SplitPlan* split_plan; // host pointer: this call's split pre-pass, or null
-    const uint32_t* split_state; // per stream: 1 = its tokens are fed from the segments (no decode)
+    uint32_t* split_state;       // per stream SPS_* (split.h): whether the rounds decode it
+    uint32_t fallback_pass;      // 1: this round-0 decode runs the SPS_FALLBACK streams only
     uint32_t segmode;            // 1: this decode launch runs segments, one lane per segment
     const SegInfo* seg;          // segment mode: start bit, token buffer, stream per segment
     const SplitInfo* spinfo;     // segment mode: the split streams (candidate counts)

@@ -320,25 +320,44 @@ int inflate_run(InflateArgs& a, hipStream_t s, bool timing_started = false) {
 // Block-parallel decode of long streams (k_split.hip): when a batch holds streams much longer
 // than its median, their block starts are found, their blocks decoded as segments (one lane
 // each) and chained back in order, before the rounds; the rounds then feed their tokens to
-// the resolve phase.  Which streams: compressed size >= max(SDZ_SPLIT_MIN (64 KiB), twice the
-// batch's bytes per decoder lane (64 Ki lanes: one wave per SIMD)), so that no lane is left
-// with much more than an even share; a batch of equal streams (C2) is not split.
-// SDZ_SPLIT=0 turns it off.  Returns 0 with plan.nsplit == 0 when nothing is split.
+// the resolve phase.  Which streams: compressed size >= max(SDZ_SPLIT_MIN (16 KiB), share x
+// the batch's bytes per decoder lane (64 Ki lanes: one wave per SIMD)).  The segments decode
+// while the first round decodes the other streams, so the round takes about the longer of
+// the two; share = 0.5 for batches of < 32 Ki streams (lanes to spare: C4 at 1/8 is fastest
+// there, measured), 2 for larger ones (every lane busy: only outliers are worth the finder's
+// pass -- a batch of equal streams, C2, is not split).  SDZ_SPLIT_SHARE overrides the share,
+// SDZ_SPLIT=0 turns splitting off.  Returns 0 with plan.nsplit == 0 when nothing is split.
 struct SplitHost {
     SplitPlan plan{};
     uint32_t* split_state = nullptr;
 };
+// per device: the side stream the segments decode on (overlapping the first round's decode
+// of the other streams) and its completion event
+struct SideStream { hipStream_t s = nullptr; hipEvent_t ev = nullptr; };
+std::vector<SideStream> g_side;
+int side_stream(SideStream** out) {
+    int d = 0;
+    HIPCHK(hipGetDevice(&d));
+    if ((size_t)d >= g_side.size()) g_side.resize((size_t)d + 1);
+    SideStream& S = g_side[(size_t)d];
+    if (!S.s) HIPCHK(hipStreamCreateWithFlags(&S.s, hipStreamNonBlocking));
+    if (!S.ev) HIPCHK(hipEventCreateWithFlags(&S.ev, hipEventDisableTiming));
+    *out = &S;
+    return SDZ_API_OK;
+}
 int inflate_split_plan(InflateArgs& a, hipStream_t s, PoolUse& use, SplitHost& H, float* ms) {
     const uint32_t n = a.n;
     if (const char* e = getenv("SDZ_SPLIT")) if (atoi(e) == 0) return SDZ_API_OK;
-    uint64_t split_min = 64 << 10;
+    uint64_t split_min = 16 << 10;
     if (const char* e = getenv("SDZ_SPLIT_MIN")) split_min = strtoull(e, nullptr, 10);
     std::vector<uint64_t> len(n), off(n);
     HIPCHK(hipMemcpyAsync(len.data(), a.in_len, n * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
     uint64_t total = 0;
     for (uint64_t x : len) total += x;
-    const uint64_t thr = std::max<uint64_t>(split_min, 2 * (total / 65536));
+    double share = n < 32768 ? 0.5 : 2.0;
+    if (const char* e = getenv("SDZ_SPLIT_SHARE")) share = atof(e);
+    const uint64_t thr = std::max<uint64_t>(split_min, (uint64_t)(share * (double)(total / 65536)));
     std::vector<SplitInfo> sp;
     uint64_t lanes = 0;
     for (uint32_t i = 0; i < n; ++i) {
@@ -359,8 +378,10 @@ int inflate_split_plan(InflateArgs& a, hipStream_t s, PoolUse& use, SplitHost& H
     // candidates beyond that are only lost parallelism: its segments get longer)
     uint8_t* d1 = nullptr;
     const size_t cand_bytes = (size_t)ns * SP_CAND_MAX * sizeof(uint64_t);
-    const uint32_t scap = (uint32_t)std::min<uint64_t>(1u << 30, std::max<uint64_t>(4096, lanes * 32 / 512));
-    const size_t b1 = ns * sizeof(SplitInfo) + cand_bytes + (size_t)scap * sizeof(uint64_t) + 256;
+    const uint32_t scap = (uint32_t)std::min<uint64_t>(1u << 30, std::max<uint64_t>(SPLIT_FILTER_BLOCKS * 16,
+                                                                                 lanes * 32 / 512));
+    const size_t b1 = ns * sizeof(SplitInfo) + cand_bytes + (size_t)scap * sizeof(uint64_t) +
+                      SPLIT_FILTER_BLOCKS * sizeof(uint32_t);
     HIPCHK(hipMalloc(&d1, b1));
     struct Free { uint8_t* p; ~Free() { if (p) hipFree(p); } } free1{ d1 };
     SplitInfo* d_sp1 = (SplitInfo*)d1;
@@ -368,13 +389,24 @@ int inflate_split_plan(InflateArgs& a, hipStream_t s, PoolUse& use, SplitHost& H
     uint64_t* d_surv = d_cand1 + (size_t)ns * SP_CAND_MAX;
     uint32_t* d_nsurv = (uint32_t*)(d_surv + scap);
     HIPCHK(hipMemcpyAsync(d_sp1, sp.data(), ns * sizeof(SplitInfo), hipMemcpyHostToDevice, s));
-    HIPCHK(hipMemsetAsync(d_nsurv, 0, sizeof(uint32_t), s));
+    HIPCHK(hipMemsetAsync(d_nsurv, 0, SPLIT_FILTER_BLOCKS * sizeof(uint32_t), s));
     launch_split_find(a.in, a.in_off, d_sp1, ns, d_cand1, lanes, d_surv, d_nsurv, scap, s);
     HIPCHK(hipGetLastError());
     std::vector<uint64_t> cand((size_t)ns * SP_CAND_MAX);
     HIPCHK(hipMemcpyAsync(sp.data(), d_sp1, ns * sizeof(SplitInfo), hipMemcpyDeviceToHost, s));
     HIPCHK(hipMemcpyAsync(cand.data(), d_cand1, cand_bytes, hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
+    if (getenv("SDZ_SPLIT_DEBUG")) {
+        std::vector<uint32_t> nsv(SPLIT_FILTER_BLOCKS);
+        HIPCHK(hipMemcpy(nsv.data(), d_nsurv, nsv.size() * sizeof(uint32_t), hipMemcpyDeviceToHost));
+        uint64_t tsv = 0, tc = 0, over = 0, full = 0;
+        for (uint32_t x : nsv) { tsv += x; full += x == scap / SPLIT_FILTER_BLOCKS; }
+        for (const SplitInfo& x : sp) { tc += x.ncand; over += x.ncand > SP_CAND_MAX; }
+        fprintf(stderr, "sdz split: %u streams, %llu bits, %llu survivors (%llu full regions of %u), "
+                "%llu candidates, %llu streams over the cap\n", ns, (unsigned long long)(lanes * 32),
+                (unsigned long long)tsv, (unsigned long long)full, scap / SPLIT_FILTER_BLOCKS,
+                (unsigned long long)tc, (unsigned long long)over);
+    }
     // phase 2: segments -- the stream's start, then one per candidate; token capacity from
     // the bits to the next candidate (1 token per 6 bits; a segment that fills up sends its
     // stream to the serial path)
@@ -434,8 +466,19 @@ int inflate_split_plan(InflateArgs& a, hipStream_t s, PoolUse& use, SplitHost& H
     HIPCHK(hipMemcpyAsync(H.plan.sp, sp.data(), ns * sizeof(SplitInfo), hipMemcpyHostToDevice, s));
     HIPCHK(hipMemcpyAsync(H.plan.seg, seg.data(), nseg * sizeof(SegInfo), hipMemcpyHostToDevice, s));
     HIPCHK(hipMemcpyAsync(H.plan.cand, d_cand1, cand_bytes, hipMemcpyDeviceToDevice, s));
-    HIPCHK(hipMemsetAsync(H.split_state, 0, n * sizeof(uint32_t), s));
-    // phase 3: every segment decoded, one lane each, in one round
+    {
+        std::vector<uint32_t> st(n, 0u);
+        for (const SplitInfo& x : sp) st[x.sid] = SPS_PENDING;
+        HIPCHK(hipMemcpyAsync(H.split_state, st.data(), n * sizeof(uint32_t), hipMemcpyHostToDevice, s));
+        HIPCHK(hipStreamSynchronize(s));                 // (st is a local)
+    }
+    // phase 3: every segment decoded, one lane each, in one round, on the side stream: the
+    // first round's decode of the other streams runs meanwhile (run_inflate_rounds waits
+    // for plan.ready before chaining them)
+    SideStream* side = nullptr;
+    if (int rc = side_stream(&side)) return rc;
+    HIPCHK(hipEventRecord(side->ev, s));
+    HIPCHK(hipStreamWaitEvent(side->s, side->ev, 0));
     InflateArgs g = a;
     g.n = nseg;
     g.dsave = B + o_segD;
@@ -450,11 +493,11 @@ int inflate_split_plan(InflateArgs& a, hipStream_t s, PoolUse& use, SplitHost& H
     g.spinfo = H.plan.sp;
     g.cand = H.plan.cand;
     g.segtok = H.plan.segtok;
-    launch_seg_decode(g, s);
-    // phase 4: chains, trailers; the chained streams' decode state for the rounds
-    launch_seg_chain(a, H.plan.sp, ns, H.plan.seg, H.plan.cand, g.dsave, H.plan.chain, H.plan.chain_tok,
-                     H.split_state, s);
+    launch_seg_decode(g, side->s);
     HIPCHK(hipGetLastError());
+    HIPCHK(hipEventRecord(side->ev, side->s));
+    H.plan.segD = g.dsave;
+    H.plan.ready = (void*)side->ev;
     if (ms) {
         (void)hipEventRecord(e1, s);
         (void)hipEventSynchronize(e1);
@@ -516,6 +559,8 @@ int sdz_inflate_batch_device(const uint8_t* in, const uint64_t* in_off, const ui
     if (int rc = inflate_split_plan(a, s, split_use, sh, g_timing ? &split_ms : nullptr)) return rc;
     if (sh.plan.nsplit) { a.split_plan = &sh.plan; a.split_state = sh.split_state; }
     int rc = inflate_run(a, s);
+    // (every exit: the pools' next user waits for the side stream's segment decode too)
+    if (sh.plan.nsplit) (void)hipStreamWaitEvent(s, (hipEvent_t)sh.plan.ready, 0);
     if (g_timing) { g_breakdown[0] += split_ms; g_extra_ms = split_ms; }   // the pre-pass counts as decode
     return rc;
 }

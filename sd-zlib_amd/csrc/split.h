@@ -7,8 +7,15 @@
 namespace sdz {
 
 #define SP_CAND_MAX 4096              // candidate block starts kept per stream
+#define SPLIT_FILTER_BLOCKS 8192u    // k_split_filter's grid (one survivor region each)
 #define SEG_HANDOVER 3                // DSave.stall of a segment that reached a candidate block start
 #define SEG_FINAL 4                   // ... that reached the end of the last block (the trailer)
+// split_state per stream: 0 serial decode; 1 fed from its segments; 2 planned (segments still
+// decoding: skipped by the first round-0 decode); 3 planned, chain broken: decoded serially,
+// starting in a second round-0 decode pass
+#define SPS_FED 1u
+#define SPS_PENDING 2u
+#define SPS_FALLBACK 3u
 
 struct SplitInfo {                    // one per split stream
     uint32_t sid;                     // stream index in the batch
@@ -39,6 +46,8 @@ struct SplitPlan {                    // device pointers of one inflate call's s
     uint32_t* chain;
     uint64_t* chain_tok;
     uint32_t* segtok;
+    const void* segD;                 // the segments' decode states (their own DSave array)
+    void* ready;                      // hipEvent_t: the segment decode (side stream) is done
 };
 
 }  // namespace sdz
