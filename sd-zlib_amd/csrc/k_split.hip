@@ -48,7 +48,9 @@ __device__ __forceinline__ uint32_t sp_u32a(const uint8_t* p, uint64_t q, uint64
 // 32 positions (one mask bit each): BTYPE = 2, HLIT <= 29, HDIST <= 29 and room for a header
 // (about 22 % pass); then, per remaining position, the Kraft sum of the code-length code's
 // first HCLEN + 4 lengths (their order does not matter for the sum) from a 4096-entry LDS
-// table of 4-length partial sums, 5 lookups.  About 0.1 % of positions pass (measured on zlib
+// table of 4-length partial sums, 5 lookups.  (Bit-sliced Kraft tests mod 4 ahead of it, the
+// sums from 32-bit words with 6 lookups, and a table-free v_perm/v_sad sum were all slower:
+// the loop is VALU-bound, 9.0 ms on C4 at 1/8.)  About 0.1 % of positions pass (measured on zlib
 // output); they go, (position << 20 | split index), to the block's own survivor region.
 // Each block walks a contiguous range of lanes, so the split stream of a lane is found by
 // stepping forward, not by a search per lane.
@@ -73,16 +75,34 @@ __global__ __launch_bounds__(256) void k_split_filter(const uint8_t* in, const u
         const uint32_t mid = (lo + hi) >> 1;
         if (sp[mid].lane0 <= L0) lo = mid; else hi = mid;
     }
-    uint32_t k = lo;
+    // the lane's split stream, cached: a lane steps to the next stream only at its boundary,
+    // and the next lane group's 16 bytes are loaded while this one is tested
+    uint32_t sk = lo;
+    uint64_t slane0 = sp[sk].lane0, snbits = sp[sk].nbits;
+    uint64_t snxt = sk + 1 < nsplit ? sp[sk + 1].lane0 : ~0ull;
+    const uint8_t* sbase = in + in_off[sp[sk].sid];
+    uint32_t c0 = 0, c1 = 0, c2 = 0, c3 = 0;             // the words of the next lane group
+    uint64_t cp0 = 0, cnb = 0;
+    uint32_t ck = 0;
+    auto fetch = [&](uint64_t g) {
+        while (g >= snxt) {
+            ++sk;
+            slane0 = snxt;
+            snbits = sp[sk].nbits;
+            sbase = in + in_off[sp[sk].sid];
+            snxt = sk + 1 < nsplit ? sp[sk + 1].lane0 : ~0ull;
+        }
+        cp0 = 32 * (g - slane0); cnb = snbits; ck = sk;
+        const uint64_t q = cp0 >> 3, nbytes = snbits >> 3;
+        c0 = sp_u32a(sbase, q, nbytes); c1 = sp_u32a(sbase, q + 4, nbytes);
+        c2 = sp_u32a(sbase, q + 8, nbytes); c3 = sp_u32a(sbase, q + 12, nbytes);
+    };
+    if (L0 + threadIdx.x < L1) fetch(L0 + threadIdx.x);
     for (uint64_t g = L0 + threadIdx.x; g < L1; g += 256) {
-        while (k + 1 < nsplit && sp[k + 1].lane0 <= g) ++k;
-        const SplitInfo& S = sp[k];
-        const uint64_t p0 = 32 * (g - S.lane0);
-        const uint64_t nbits = S.nbits, nbytes = nbits >> 3;
-        const uint8_t* p = in + in_off[S.sid];
-        const uint64_t q = p0 >> 3;
-        const uint32_t w0 = sp_u32a(p, q, nbytes), w1 = sp_u32a(p, q + 4, nbytes);
-        const uint32_t w2 = sp_u32a(p, q + 8, nbytes), w3 = sp_u32a(p, q + 12, nbytes);
+        const uint32_t w0 = c0, w1 = c1, w2 = c2, w3 = c3;
+        const uint64_t p0 = cp0, nbits = cnb;
+        const uint32_t k = ck;
+        if (g + 256 < L1) fetch(g + 256);                 // (issued before this group's tests)
         const uint64_t W = (uint64_t)w0 | ((uint64_t)w1 << 32);
 #define SPB(d) ((uint32_t)(W >> (d)))
         uint32_t M = ~SPB(1) & SPB(2)                                   // BTYPE = 2 (bits 1, 2 = 0, 1)
@@ -147,92 +167,195 @@ struct SpBits {
     __device__ __forceinline__ void drop(uint32_t n) { buf >>= n; nb -= n; }
 };
 
-// Pass 2 (k_split_deep): one lane per survivor decodes the code lengths (infblocks.ts:354-551 /
+// Pass 2 (k_split_deep): survivors' code lengths decoded (infblocks.ts:354-551 /
 // inftree.ts:313-379 on a strict reading: every code complete) with the code-length code in a
-// 128-entry LDS table, and keeps Kraft sums of the literal/length and distance lengths as it
-// goes, so a random bit string is rejected as soon as one is over-subscribed.  Survivors are
-// candidates.
-__global__ __launch_bounds__(256) void k_split_deep(const uint8_t* in, const uint64_t* in_off, SplitInfo* sp,
-                                                    const uint64_t* surv, const uint32_t* nsurv, uint32_t bcap,
-                                                    uint64_t* cand) {
-    __shared__ uint8_t lut[256][128];                     // 7 stream bits -> symbol << 3 | code length
-    const uint64_t t = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-    const uint32_t fb = (uint32_t)(t / bcap);             // the filter block whose region holds t
-    if (t - (uint64_t)fb * bcap >= nsurv[fb]) return;
-    const uint64_t e = surv[t];
-    const uint32_t k = (uint32_t)(e & 0xfffffu);
-    uint64_t pos = e >> 20;
-    SplitInfo& S = sp[k];
-    const uint64_t nbits = S.nbits;
-    SpBits R;
-    R.init(in + in_off[S.sid], nbits >> 3, pos);
-    const uint32_t h = R.peek(17);
-    R.drop(17);
-    R.fill();
-    const int hlit = (int)((h >> 3) & 31u) + 257, hdist = (int)((h >> 8) & 31u) + 1, hclen = (int)(h >> 13) + 4;
-    pos += 17 + 3 * (uint64_t)hclen;
+// 128-entry LDS table per lane, and running Kraft sums of the literal/length and distance
+// lengths, so a random bit string is rejected as soon as one is over-subscribed.  Survivors
+// that pass are candidates.  A survivor takes 45 code-length symbols on average but up to
+// ~300 (zlib output), so lanes are persistent: one wave works through one filter block's
+// survivor region, and whenever 16 of its lanes are idle they take the next 16 survivors
+// together -- the wave's steps stay busy instead of waiting for its slowest survivor.
+// k_split_deep's bit reader: the survivor's first 64 bytes are staged in the lane's LDS slot
+// when it starts (one batch of loads for the lanes starting together), so a refill is an LDS
+// read; only a survivor that runs past them (~10 %) reads global memory again.
+struct SpBitsL {
+    const uint8_t* p;
+    uint32_t* W;                                          // the lane's 16 staged dwords
+    uint64_t len, q0;                                     // stream bytes; first staged byte
+    uint64_t buf;
+    uint32_t nb, next;                                    // valid bits in buf; next dword to load
+    __device__ __forceinline__ void init(const uint8_t* p_, uint32_t* W_, uint64_t len_, uint64_t pos) {
+        p = p_; W = W_; len = len_;
+        q0 = (pos >> 3) & ~3ull;
+        const uint8_t* r = p + q0;
+        if (q0 + 64 <= len && (((uintptr_t)r) & 15) == 0) {
+            const uint4* r4 = (const uint4*)r;
+            const uint4 a = r4[0], b = r4[1], c = r4[2], d = r4[3];
+            W[0] = a.x; W[1] = a.y; W[2] = a.z; W[3] = a.w; W[4] = b.x; W[5] = b.y; W[6] = b.z; W[7] = b.w;
+            W[8] = c.x; W[9] = c.y; W[10] = c.z; W[11] = c.w; W[12] = d.x; W[13] = d.y; W[14] = d.z; W[15] = d.w;
+        } else {
+            for (uint32_t j = 0; j < 16; ++j) W[j] = sp_u32(p, q0 + 4 * j, len);
+        }
+        const uint32_t sh = (uint32_t)(pos - 8 * q0);     // 0 .. 31
+        buf = ((uint64_t)W[0] | ((uint64_t)W[1] << 32)) >> sh;
+        nb = 64 - sh;
+        next = 2;
+    }
+    __device__ __forceinline__ void fill() {              // nb >= 32 after
+        if (nb < 32) {
+            const uint32_t d = next < 16 ? W[next] : sp_u32(p, q0 + 4 * (uint64_t)next, len);
+            buf |= (uint64_t)d << nb;
+            ++next;
+            nb += 32;
+        }
+    }
+    __device__ __forceinline__ uint32_t peek(uint32_t n) const { return (uint32_t)buf & ((1u << n) - 1u); }
+    __device__ __forceinline__ void drop(uint32_t n) { buf >>= n; nb -= n; }
+};
+
+// The code-length code is decoded table-free (a LUT per lane cost more to fill than the
+// ~45 symbols it serves: a fill loop's trip count differs per lane): 6 left-justified limits
+// give the code length of the next 7 bits read MSB-first, then rank = base[len] + code, and
+// the rank's symbol comes from the lane's 19 sorted symbols in LDS.
+struct DeepLane {
+    SpBitsL R;
+    uint64_t pos, nbits;
+    uint64_t base;                                        // per length 1..7: rank - code + 128, 8 bits each
+    uint32_t lim1, lim2, lim3, lim4, lim5, lim6;          // (first code + count) << (7 - len)
+    uint32_t k;                                           // split index
+    int n, prev, hlit, total;
+    uint32_t kl, kd;                                      // Kraft sums in units of 2^-15
+    bool eob;
+};
+
+__device__ __forceinline__ void deep_start(DeepLane& L, uint8_t* T, uint32_t* W, const uint8_t* in,
+                                           const uint64_t* in_off, const SplitInfo* sp, uint64_t e) {
+    L.k = (uint32_t)(e & 0xfffffu);
+    L.pos = e >> 20;
+    const SplitInfo& S = sp[L.k];
+    L.nbits = S.nbits;
+    L.R.init(in + in_off[S.sid], W, L.nbits >> 3, L.pos);
+    const uint32_t h = L.R.peek(17);
+    L.R.drop(17);
+    L.R.fill();
+    const int hclen = (int)(h >> 13) + 4;
+    L.hlit = (int)((h >> 3) & 31u) + 257;
+    L.total = L.hlit + (int)((h >> 8) & 31u) + 1;
+    L.pos += 17 + 3 * (uint64_t)hclen;
     uint64_t cl = 0;                                      // the 19 lengths, 3 bits each, symbol order
     uint64_t bl = 0;                                      // lengths 1..7: their counts, 8 bits each
-    for (int i = 0; i < hclen; ++i) {
-        const uint32_t l = R.peek(3);
-        R.drop(3);
-        if (i == 9) R.fill();
+    for (int i = 0; i < 19; ++i) {                        // (uniform trip count; fields past HCLEN + 4 are 0)
+        const uint32_t l = i < hclen ? L.R.peek(3) : 0u;
+        if (i < hclen) L.R.drop(3);
+        if (i == 9) L.R.fill();
         cl |= (uint64_t)l << (3 * c_split_border[i]);
         bl += l ? 1ull << (8 * l) : 0ull;
     }
-    uint8_t* T = lut[threadIdx.x];
-    {
-        // canonical codes (inftree.ts: shorter first, then symbol order), MSB first in the stream
-        uint64_t nx = 0;                                  // first code of each length, 8 bits each
-        uint32_t code = 0;
-        for (int l = 1; l < 8; ++l) {
-            code = (code + (uint32_t)((bl >> (8 * (l - 1))) & 255u)) << 1;
-            nx |= (uint64_t)code << (8 * l);
-        }
-        for (int sym = 0; sym < 19; ++sym) {
-            const uint32_t l = (uint32_t)(cl >> (3 * sym)) & 7u;
-            if (!l) continue;
-            const uint32_t c = (uint32_t)(nx >> (8 * l)) & 255u;
-            nx += 1ull << (8 * l);
-            const uint32_t rev = __builtin_bitreverse32(c) >> (32 - l);
-            for (uint32_t x = rev; x < 128u; x += 1u << l) T[x] = (uint8_t)(sym << 3 | l);
+    // canonical codes (inftree.ts: shorter first, then symbol order)
+    uint64_t nx = 0;                                      // next rank of each length, 8 bits each
+    uint32_t code = 0, off = 0, lim[7];
+    L.base = 0;
+#pragma unroll
+    for (int l = 1; l < 8; ++l) {
+        const uint32_t c = (uint32_t)(bl >> (8 * l)) & 255u;
+        code = (code + ((uint32_t)(bl >> (8 * (l - 1))) & 255u)) << 1;   // first code of length l
+        lim[l - 1] = (code + c) << (7 - l);
+        L.base |= (uint64_t)((off - code + 128u) & 255u) << (8 * l);
+        nx |= (uint64_t)off << (8 * l);
+        off += c;
+    }
+    L.lim1 = lim[0]; L.lim2 = lim[1]; L.lim3 = lim[2]; L.lim4 = lim[3]; L.lim5 = lim[4]; L.lim6 = lim[5];
+    for (int sym = 0; sym < 19; ++sym) {                  // the symbols in rank order
+        const uint32_t l = (uint32_t)(cl >> (3 * sym)) & 7u;
+        const uint32_t r = (uint32_t)(nx >> (8 * l)) & 255u;
+        if (l) T[r] = (uint8_t)sym;
+        nx += l ? 1ull << (8 * l) : 0ull;
+    }
+    L.n = 0; L.prev = 0; L.kl = 0; L.kd = 0; L.eob = false;
+}
+
+// one code-length symbol; 0: go on, 1: rejected, 2: complete and valid (a candidate)
+__device__ __forceinline__ int deep_step(DeepLane& L, const uint8_t* T) {
+    if (L.pos + 14 > L.nbits) return 1;
+    L.R.fill();
+    const uint32_t w = L.R.peek(14);
+    const uint32_t v = __builtin_bitreverse32(w) >> 25;  // the next 7 bits, first one most significant
+    const uint32_t l = 1u + (v >= L.lim1) + (v >= L.lim2) + (v >= L.lim3) + (v >= L.lim4) + (v >= L.lim5) +
+                       (v >= L.lim6);
+    const uint32_t rank = (uint32_t)((L.base >> (8 * l)) & 255u) - 128u + (v >> (7 - l));
+    const int sym = (int)T[rank];
+    int rep = 1, val = sym, used = (int)l;
+    if (sym >= 16) {
+        const int eb = sym == 16 ? 2 : sym == 17 ? 3 : 7;
+        rep = (sym == 18 ? 11 : 3) + (int)((w >> l) & ((1u << eb) - 1u));
+        used += eb;
+        if (sym == 16 && L.n == 0) return 1;
+        val = sym == 16 ? L.prev : 0;
+        if (L.n + rep > L.total) return 1;
+    }
+    L.R.drop((uint32_t)used);
+    L.pos += (uint64_t)used;
+    if (val) {
+        const uint32_t u = 32768u >> val;
+        const int nl = L.n < L.hlit ? (L.hlit - L.n < rep ? L.hlit - L.n : rep) : 0;   // of them literal/length
+        L.kl += (uint32_t)nl * u;
+        L.kd += (uint32_t)(rep - nl) * u;
+        L.eob = L.eob || (L.n <= 256 && 256 < L.n + nl);
+        if (L.kl > 32768u || L.kd > 32768u) return 1;
+    }
+    L.n += rep;
+    L.prev = val;
+    if (L.n < L.total) return 0;
+    return L.eob && L.kl == 32768u && L.kd == 32768u ? 2 : 1;
+}
+
+__global__ __launch_bounds__(256) void k_split_deep(const uint8_t* in, const uint64_t* in_off, SplitInfo* sp,
+                                                    const uint64_t* surv, const uint32_t* nsurv, uint32_t bcap,
+                                                    uint64_t* cand) {
+    // per lane, at odd dword strides (5 and 17: lanes' slots start in different banks)
+    __shared__ uint32_t syms[256 * 5];                    // the code-length code's symbols by rank (bytes)
+    __shared__ uint32_t win[256 * 17];                    // staged input, 64 B
+    uint8_t* T = (uint8_t*)(syms + threadIdx.x * 5);
+    uint32_t* W = win + threadIdx.x * 17;
+    const uint32_t wid = blockIdx.x * 4 + (threadIdx.x >> 6), nw = gridDim.x * 4;
+    for (uint32_t r = wid; r < SPLIT_FILTER_BLOCKS; r += nw) {
+        const uint32_t cnt = nsurv[r];
+        const uint64_t* S = surv + (uint64_t)r * bcap;
+        uint32_t next = 0;                                // next survivor to hand out (wave-uniform)
+        bool act = false;
+        uint64_t e = 0;
+        DeepLane L;
+        for (;;) {
+            const uint64_t idle = __ballot(!act);
+            const uint32_t nidle = (uint32_t)__popcll(idle);
+            if (next < cnt && nidle >= 16) {
+                if (!act) {
+                    const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(idle >> 32),
+                                                                    __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0u));
+                    if (next + rank < cnt) {
+                        e = S[next + rank];
+                        deep_start(L, T, W, in, in_off, sp, e);
+                        act = true;
+                    }
+                }
+                next += nidle;
+            }
+            if (!__ballot(act)) {
+                if (next >= cnt) break;
+                continue;
+            }
+            if (act) {
+                const int st = deep_step(L, T);
+                if (st) {
+                    act = false;
+                    if (st == 2) {
+                        const uint32_t j = atomicAdd(&sp[L.k].ncand, 1u);
+                        if (j < SP_CAND_MAX) cand[(uint64_t)L.k * SP_CAND_MAX + j] = e >> 20;
+                    }
+                }
+            }
         }
     }
-    const int total = hlit + hdist;
-    int n = 0, prev = 0;
-    uint32_t kl = 0, kd = 0;                              // Kraft sums in units of 2^-15
-    bool eob = false;
-    while (n < total) {
-        if (pos + 14 > nbits) return;
-        R.fill();
-        const uint32_t w = R.peek(14);
-        const uint32_t v = T[w & 127u];
-        const int sym = (int)(v >> 3), l = (int)(v & 7u);
-        int rep = 1, val = sym, used = l;
-        if (sym >= 16) {
-            const int eb = sym == 16 ? 2 : sym == 17 ? 3 : 7;
-            rep = (sym == 18 ? 11 : 3) + (int)((w >> l) & ((1u << eb) - 1u));
-            used += eb;
-            if (sym == 16 && n == 0) return;
-            val = sym == 16 ? prev : 0;
-            if (n + rep > total) return;
-        }
-        R.drop((uint32_t)used);
-        pos += (uint64_t)used;
-        if (val) {
-            const uint32_t u = 32768u >> val;
-            const int nl = n < hlit ? (hlit - n < rep ? hlit - n : rep) : 0;   // of them literal/length
-            kl += (uint32_t)nl * u;
-            kd += (uint32_t)(rep - nl) * u;
-            eob = eob || (n <= 256 && 256 < n + nl);
-            if (kl > 32768u || kd > 32768u) return;
-        }
-        n += rep;
-        prev = val;
-    }
-    if (!(eob && kl == 32768u && kd == 32768u)) return;
-    const uint32_t j = atomicAdd(&S.ncand, 1u);
-    if (j < SP_CAND_MAX) cand[(uint64_t)k * SP_CAND_MAX + j] = e >> 20;
 }
 
 // bitonic sort of each stream's candidates in LDS (one workgroup per split stream)
@@ -259,6 +382,35 @@ __global__ __launch_bounds__(256) void k_split_sort(SplitInfo* sp, uint64_t* can
         }
     }
     for (uint32_t k = threadIdx.x; k < n; k += 256) c[k] = v[k];
+}
+
+// the candidates of the streams that split (ncand <= SP_CAND_MAX), packed in stream order for
+// the host's segment plan: one block scans the counts, then one block per stream copies
+__global__ __launch_bounds__(1024) void k_split_pack_scan(SplitInfo* sp, uint32_t nsplit, uint32_t* total) {
+    __shared__ uint32_t part[1024];
+    uint32_t base = 0;
+    for (uint32_t k0 = 0; k0 < nsplit; k0 += 1024) {
+        const uint32_t k = k0 + threadIdx.x;
+        const uint32_t c = k < nsplit && sp[k].ncand <= SP_CAND_MAX ? sp[k].ncand : 0u;
+        part[threadIdx.x] = c;
+        __syncthreads();
+        for (uint32_t o = 1; o < 1024; o <<= 1) {         // inclusive scan
+            const uint32_t v = threadIdx.x >= o ? part[threadIdx.x - o] : 0u;
+            __syncthreads();
+            part[threadIdx.x] += v;
+            __syncthreads();
+        }
+        if (k < nsplit) sp[k].cand0 = base + part[threadIdx.x] - c;
+        base += part[1023];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) *total = base;
+}
+__global__ __launch_bounds__(256) void k_split_pack(const SplitInfo* sp, const uint64_t* cand, uint64_t* packed) {
+    const SplitInfo& S = sp[blockIdx.x];
+    if (S.ncand > SP_CAND_MAX) return;
+    const uint64_t* c = cand + (uint64_t)blockIdx.x * SP_CAND_MAX;
+    for (uint32_t k = threadIdx.x; k < S.ncand; k += 256) packed[S.cand0 + k] = c[k];
 }
 
 __device__ __forceinline__ int64_t sp_find(const uint64_t* c, uint32_t n, uint64_t bit) {   // index of bit, or -1
@@ -377,6 +529,11 @@ __global__ __launch_bounds__(256) void k_seg_feed(InflateArgs A, const SplitInfo
     }
 }
 
+void launch_split_pack(SplitInfo* sp, uint32_t nsplit, const uint64_t* cand, uint64_t* packed, uint32_t* total,
+                       hipStream_t s) {
+    hipLaunchKernelGGL(k_split_pack_scan, dim3(1), dim3(1024), 0, s, sp, nsplit, total);
+    hipLaunchKernelGGL(k_split_pack, dim3(nsplit), dim3(256), 0, s, sp, cand, packed);
+}
 void launch_split_find(const uint8_t* in, const uint64_t* in_off, SplitInfo* sp, uint32_t nsplit, uint64_t* cand,
                        uint64_t total_lanes, uint64_t* surv, uint32_t* nsurv, uint32_t cap, hipStream_t s) {
     // persistent: each block a contiguous lane range and its own survivor region (cap / 8192
@@ -386,9 +543,8 @@ void launch_split_find(const uint8_t* in, const uint64_t* in_off, SplitInfo* sp,
     const uint32_t bcap = cap / SPLIT_FILTER_BLOCKS;
     hipLaunchKernelGGL(k_split_filter, dim3((uint32_t)((total_lanes + per - 1) / per)), dim3(256), 0, s, in, in_off,
                        sp, nsplit, total_lanes, per, surv, nsurv, bcap);
-    const uint64_t nt = (uint64_t)bcap * SPLIT_FILTER_BLOCKS;
-    hipLaunchKernelGGL(k_split_deep, dim3((uint32_t)((nt + 255) / 256)), dim3(256), 0, s, in, in_off, sp, surv, nsurv,
-                       bcap, cand);
+    hipLaunchKernelGGL(k_split_deep, dim3(SPLIT_FILTER_BLOCKS / 4), dim3(256), 0, s, in, in_off, sp, surv, nsurv,
+                       bcap, cand);                       // one wave per survivor region
     hipLaunchKernelGGL(k_split_sort, dim3(nsplit), dim3(256), 0, s, sp, cand);
 }
 void launch_seg_chain(const InflateArgs& a, SplitInfo* sp, uint32_t nsplit, const SegInfo* seg, const uint64_t* cand,

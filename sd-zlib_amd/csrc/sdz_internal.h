@@ -66,6 +66,9 @@ void launch_istate_reset(uint8_t* dsave, uint8_t* rsave, uint32_t n, hipStream_t
 // block-parallel decode of long streams (k_split.hip)
 void launch_split_find(const uint8_t* in, const uint64_t* in_off, SplitInfo* sp, uint32_t nsplit, uint64_t* cand,
                        uint64_t total_lanes, uint64_t* surv, uint32_t* nsurv, uint32_t cap, hipStream_t s);
+// candidates of the split streams packed in stream order (SplitInfo.cand0), count in *total
+void launch_split_pack(SplitInfo* sp, uint32_t nsplit, const uint64_t* cand, uint64_t* packed, uint32_t* total,
+                       hipStream_t s);
 void launch_seg_decode(const InflateArgs& a, hipStream_t s);
 void launch_seg_chain(const InflateArgs& a, SplitInfo* sp, uint32_t nsplit, const SegInfo* seg, const uint64_t* cand,
                       const void* segD, uint32_t* chain, uint64_t* chain_tok, uint32_t* split_state, hipStream_t s);

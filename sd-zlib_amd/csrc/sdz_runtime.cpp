@@ -97,7 +97,7 @@ struct Pool {
         return SDZ_API_OK;
     }
 };
-Pool g_inflate_scratch, g_deflate_state, g_tmp, g_stage, g_split;
+Pool g_inflate_scratch, g_deflate_state, g_tmp, g_stage, g_split, g_find;
 constexpr size_t kTmpFname = 256;     // g_tmp layout: [0, 256) small results, then the file name
 constexpr uint64_t kInflaterOutCap = 4ull << 20;   // sdz_inflater: output slot per device call
 
@@ -320,13 +320,10 @@ int inflate_run(InflateArgs& a, hipStream_t s, bool timing_started = false) {
 // Block-parallel decode of long streams (k_split.hip): when a batch holds streams much longer
 // than its median, their block starts are found, their blocks decoded as segments (one lane
 // each) and chained back in order, before the rounds; the rounds then feed their tokens to
-// the resolve phase.  Which streams: compressed size >= max(SDZ_SPLIT_MIN (16 KiB), share x
-// the batch's bytes per decoder lane (64 Ki lanes: one wave per SIMD)).  The segments decode
-// while the first round decodes the other streams, so the round takes about the longer of
-// the two; share = 0.5 for batches of < 32 Ki streams (lanes to spare: C4 at 1/8 is fastest
-// there, measured), 2 for larger ones (every lane busy: only outliers are worth the finder's
-// pass -- a batch of equal streams, C2, is not split).  SDZ_SPLIT_SHARE overrides the share,
-// SDZ_SPLIT=0 turns splitting off.  Returns 0 with plan.nsplit == 0 when nothing is split.
+// the resolve phase.  Which streams: those of compressed size >= a threshold t (>= 16 KiB,
+// SDZ_SPLIT_MIN) chosen by split_threshold's cost model; SDZ_SPLIT_SHARE=x forces t = x times
+// the batch's bytes per decoder lane, SDZ_SPLIT=0 turns splitting off.  Returns 0 with
+// plan.nsplit == 0 when nothing is split.
 struct SplitHost {
     SplitPlan plan{};
     uint32_t* split_state = nullptr;
@@ -345,19 +342,54 @@ int side_stream(SideStream** out) {
     *out = &S;
     return SDZ_API_OK;
 }
+// The first round's decode takes about
+//   finder(split bytes) + max(longest unsplit stream / lane rate, longest segment / lane rate,
+//                             all bytes / full-chip rate)
+// (the segments decode while the unsplit streams do; a lane decodes its stream serially, and
+// at 64 Ki busy lanes the chip is at its aggregate rate).  The rates are measured figures:
+// ~2.5 MB/s of input per lane, ~220 GB/s of input for the chip (C2), ~130 GB/s for the
+// finder (C4); segments are blocks (~30 KB on zlib output; 32 KB fitted to C4's measured
+// optimum).  The threshold minimising this
+// over the batch's own sizes is taken (none when splitting does not pay: a batch of equal
+// streams, C2).
+uint64_t split_threshold(std::vector<uint64_t> len, uint64_t split_min) {
+    const double r_lane = 2.5e6, r_chip = 220e9, r_find = 130e9, seg_max = 32768;
+    std::sort(len.begin(), len.end());
+    uint64_t total = 0;
+    for (uint64_t x : len) total += x;
+    const double floor_t = (double)total / r_chip;
+    const size_t n = len.size();
+    double best = std::max((double)len[n - 1] / r_lane, floor_t);   // nothing split
+    uint64_t thr = ~0ull;
+    double suffix = 0;
+    for (size_t k = n; k-- > 0;) {                       // split streams k .. n-1 (t = len[k])
+        suffix += (double)len[k];
+        if (len[k] < split_min) break;
+        if (k + 1 < n && len[k] == len[k + 1]) continue;  // (equal sizes split together)
+        const double unsplit = k ? (double)len[k - 1] / r_lane : 0.0;
+        const double t = suffix / r_find + std::max(std::max(unsplit, seg_max / r_lane), floor_t);
+        if (t < best) { best = t; thr = len[k]; }
+    }
+    return thr;
+}
+
 int inflate_split_plan(InflateArgs& a, hipStream_t s, PoolUse& use, SplitHost& H, float* ms) {
     const uint32_t n = a.n;
     if (const char* e = getenv("SDZ_SPLIT")) if (atoi(e) == 0) return SDZ_API_OK;
     uint64_t split_min = 16 << 10;
     if (const char* e = getenv("SDZ_SPLIT_MIN")) split_min = strtoull(e, nullptr, 10);
-    std::vector<uint64_t> len(n), off(n);
+    std::vector<uint64_t> len(n);
     HIPCHK(hipMemcpyAsync(len.data(), a.in_len, n * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
-    uint64_t total = 0;
-    for (uint64_t x : len) total += x;
-    double share = n < 32768 ? 0.5 : 2.0;
-    if (const char* e = getenv("SDZ_SPLIT_SHARE")) share = atof(e);
-    const uint64_t thr = std::max<uint64_t>(split_min, (uint64_t)(share * (double)(total / 65536)));
+    uint64_t thr = 0;
+    if (const char* e = getenv("SDZ_SPLIT_SHARE")) {
+        uint64_t total = 0;
+        for (uint64_t x : len) total += x;
+        thr = std::max<uint64_t>(split_min, (uint64_t)(atof(e) * (double)(total / 65536)));
+    } else {
+        thr = split_threshold(len, split_min);
+    }
+    if (getenv("SDZ_SPLIT_DEBUG")) fprintf(stderr, "sdz split: threshold %llu\n", (unsigned long long)thr);
     std::vector<SplitInfo> sp;
     uint64_t lanes = 0;
     for (uint32_t i = 0; i < n; ++i) {
@@ -373,29 +405,38 @@ int inflate_split_plan(InflateArgs& a, hipStream_t s, PoolUse& use, SplitHost& H
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (ms) { (void)hipEventCreate(&e0); (void)hipEventCreate(&e1); (void)hipEventRecord(e0, s); }
     const uint32_t ns = (uint32_t)sp.size();
-    // phase 1: candidates (their own allocation: freed at the end of this function)
+    // phase 1: candidates, in their own pool (this call's only), then packed for the host
     // (filter survivors: ~0.1 % of positions on zlib output; room for 0.2 %, and a stream's
     // candidates beyond that are only lost parallelism: its segments get longer)
-    uint8_t* d1 = nullptr;
     const size_t cand_bytes = (size_t)ns * SP_CAND_MAX * sizeof(uint64_t);
     const uint32_t scap = (uint32_t)std::min<uint64_t>(1u << 30, std::max<uint64_t>(SPLIT_FILTER_BLOCKS * 16,
                                                                                  lanes * 32 / 512));
     const size_t b1 = ns * sizeof(SplitInfo) + cand_bytes + (size_t)scap * sizeof(uint64_t) +
-                      SPLIT_FILTER_BLOCKS * sizeof(uint32_t);
-    HIPCHK(hipMalloc(&d1, b1));
-    struct Free { uint8_t* p; ~Free() { if (p) hipFree(p); } } free1{ d1 };
+                      SPLIT_FILTER_BLOCKS * sizeof(uint32_t) + 256;
+    PoolUse find_use(g_find, s);
+    void* p1 = nullptr;
+    if (int rc = find_use.get(b1, &p1)) return rc;
+    uint8_t* d1 = (uint8_t*)p1;
     SplitInfo* d_sp1 = (SplitInfo*)d1;
     uint64_t* d_cand1 = (uint64_t*)(d1 + ns * sizeof(SplitInfo));
     uint64_t* d_surv = d_cand1 + (size_t)ns * SP_CAND_MAX;
     uint32_t* d_nsurv = (uint32_t*)(d_surv + scap);
+    uint32_t* d_npacked = d_nsurv + SPLIT_FILTER_BLOCKS;
     HIPCHK(hipMemcpyAsync(d_sp1, sp.data(), ns * sizeof(SplitInfo), hipMemcpyHostToDevice, s));
     HIPCHK(hipMemsetAsync(d_nsurv, 0, SPLIT_FILTER_BLOCKS * sizeof(uint32_t), s));
     launch_split_find(a.in, a.in_off, d_sp1, ns, d_cand1, lanes, d_surv, d_nsurv, scap, s);
+    // (every candidate was a survivor: the survivor list's room holds the packed candidates)
+    launch_split_pack(d_sp1, ns, d_cand1, d_surv, d_npacked, s);
     HIPCHK(hipGetLastError());
-    std::vector<uint64_t> cand((size_t)ns * SP_CAND_MAX);
+    uint32_t npacked = 0;
     HIPCHK(hipMemcpyAsync(sp.data(), d_sp1, ns * sizeof(SplitInfo), hipMemcpyDeviceToHost, s));
-    HIPCHK(hipMemcpyAsync(cand.data(), d_cand1, cand_bytes, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(&npacked, d_npacked, sizeof npacked, hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
+    std::vector<uint64_t> packed(npacked);
+    if (npacked) {
+        HIPCHK(hipMemcpyAsync(packed.data(), d_surv, npacked * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+    }
     if (getenv("SDZ_SPLIT_DEBUG")) {
         std::vector<uint32_t> nsv(SPLIT_FILTER_BLOCKS);
         HIPCHK(hipMemcpy(nsv.data(), d_nsurv, nsv.size() * sizeof(uint32_t), hipMemcpyDeviceToHost));
@@ -416,7 +457,7 @@ int inflate_split_plan(InflateArgs& a, hipStream_t s, PoolUse& use, SplitHost& H
     for (uint32_t k = 0; k < ns; ++k) {
         SplitInfo& x = sp[k];
         const uint32_t nc = std::min<uint32_t>(x.ncand, SP_CAND_MAX);
-        const uint64_t* c = cand.data() + (size_t)k * SP_CAND_MAX;
+        const uint64_t* c = packed.data() + x.cand0;
         x.skip0 = nc && c[0] == 0 ? 1 : 0;
         x.seg0 = (uint32_t)seg.size();
         x.chain0 = chain;
@@ -507,7 +548,7 @@ int inflate_split_plan(InflateArgs& a, hipStream_t s, PoolUse& use, SplitHost& H
         (void)hipEventDestroy(e0);
         (void)hipEventDestroy(e1);
     }
-    HIPCHK(hipStreamSynchronize(s));                     // phase 1's allocation is freed on return
+    HIPCHK(hipStreamSynchronize(s));                     // (the host vectors above are copy sources)
     return SDZ_API_OK;
 }
 

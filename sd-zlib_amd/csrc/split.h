@@ -25,7 +25,8 @@ struct SplitInfo {                    // one per split stream
     uint32_t seg0, nseg;              // its segments: seg0 starts at bit 0, then one per candidate
     uint32_t skip0;                   // 1 when candidate 0 is bit 0 (covered by seg0, no own segment)
     uint32_t chain0;                  // offset of its chain arrays (nseg entries)
-    uint32_t chain_len, pad;
+    uint32_t chain_len;
+    uint32_t cand0;                   // offset of its candidates in the packed list (host copy)
     uint64_t ntok;                    // tokens of the chained stream
 };
 
