@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define SDZ_ABI_VERSION 2
+#define SDZ_ABI_VERSION 3
 
 /* API return codes */
 enum {
@@ -186,6 +186,40 @@ int sdz_deflate_batch(const uint8_t* const* in, const size_t* in_len, uint8_t* c
                       const size_t* out_cap, sdz_deflate_record* rec, uint32_t n, int32_t level,
                       int32_t format, const uint8_t* fname, size_t fname_len, uint32_t mtime,
                       const uint8_t* dict, size_t dict_len);
+
+/* ------------------------------------------------- incremental deflate */
+
+/* Deflater.append(chunk) / finish() across calls, as many Deflaters at once
+ * (sd-deflate.ts:51-254 over deflate.ts:1218-1327 with NO_FLUSH / FINISH).  A state slab
+ * (sdz_deflate_state_bytes) holds each stream's compressor between calls: window, hash
+ * chains, the block being built, the bit buffer, the running input checksum.  Each call
+ * hands every stream its next chunk (in_len[i] may be 0) with finish = 0, or ends every
+ * stream with finish = 1 (a chunk given with finish is compressed first).  A stream's output
+ * for the call -- what the reference's append()/finish() returns, concatenated: the header
+ * on the first non-empty append, the blocks flushed meanwhile, the trailer at finish -- goes
+ * to out[out_off[i] ..]; out_cap[i] >= sdz_deflate_append_bound(in_len[i], ...) always
+ * suffices.  rec: status (SDZ_DATA_ERROR for finish before any append and for an append
+ * after finish, which the reference throws on), out_len of this call, the running checksum.
+ * level, format, fname, mtime and dict must be the same on every call of a stream.  The
+ * concatenated output equals sdz_deflate_batch_device's on the concatenated input. */
+uint64_t sdz_deflate_state_bytes(uint32_t n);
+uint64_t sdz_deflate_append_bound(uint64_t in_len, int32_t format, uint32_t fname_len);
+int sdz_deflate_state_reset_device(void* state, uint32_t n, void* stream);
+int sdz_deflate_append_batch_device(void* state, const uint8_t* in, const uint64_t* in_off,
+                                    const uint64_t* in_len, uint8_t* out, const uint64_t* out_off,
+                                    const uint64_t* out_cap, sdz_deflate_record* rec, uint32_t n,
+                                    int32_t level, int32_t format, const uint8_t* fname,
+                                    uint32_t fname_len, uint32_t mtime, const uint8_t* dict,
+                                    uint32_t dict_len, int32_t finish, void* stream);
+
+/* One Deflater on host buffers: create, then append(chunk, finish 0) / append(chunk or
+ * NULL, finish 1) -> *out / *out_len (valid until the next call on this handle). */
+typedef struct sdz_deflater sdz_deflater;
+sdz_deflater* sdz_deflater_create(int32_t level, int32_t format, const uint8_t* fname, size_t fname_len,
+                                  uint32_t mtime, const uint8_t* dict, size_t dict_len);
+int sdz_deflater_append(sdz_deflater* z, const uint8_t* data, size_t len, int32_t finish,
+                        const uint8_t** out, size_t* out_len, sdz_deflate_record* rec);
+void sdz_deflater_destroy(sdz_deflater* z);
 
 /* Worst-case compressed size for one stream (header + blocks + trailer). */
 uint64_t sdz_deflate_bound(uint64_t in_len, int32_t format, uint32_t fname_len);

@@ -78,6 +78,8 @@ def lib():
             ctypes.c_int32, ctypes.c_int32, u8p, ctypes.c_size_t, ctypes.c_int32, u8p,
             ctypes.c_size_t, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_size_t,
             ctypes.POINTER(ctypes.c_size_t)]
+        L.oracle_deflater_run_parts.restype = ctypes.c_int32
+        L.oracle_deflater_run_parts.argtypes = L.oracle_deflater_run.argtypes + [ctypes.POINTER(ctypes.c_size_t)]
         L.oracle_fixed_table_entry.restype = ctypes.c_int32
         L.oracle_fixed_table_entry.argtypes = [ctypes.c_int, ctypes.c_int]
         L.oracle_tree_table.restype = ctypes.c_int32
@@ -187,6 +189,32 @@ def deflater_run(parts, level=6, format="deflate", dictionary=None, file_name=No
     if err:
         raise RuntimeError("oracle deflate error %d: %s" % (err, ERRORS.get(err)))
     return out.raw[:out_len.value]
+
+
+def deflater_parts(parts, level=6, format="deflate", dictionary=None, file_name=None, mtime=0):
+    """The reference Deflater's per-call outputs: [append(p) for p in parts] + [finish()],
+    each the concatenation of the Uint8Arrays that call returns (sd-deflate.ts:173-253)."""
+    parts = [bytes(p) for p in parts]
+    n = len(parts)
+    arr = (ctypes.c_char_p * n)(*parts)
+    lens = (ctypes.c_size_t * n)(*[len(p) for p in parts])
+    total = sum(len(p) for p in parts)
+    cap = total + total // 8 + 4096
+    out = ctypes.create_string_buffer(cap)
+    out_len = ctypes.c_size_t(0)
+    ends = (ctypes.c_size_t * (n + 1))()
+    d = bytes(dictionary) if dictionary is not None else None
+    fn = latin1_filename(file_name) if file_name else b""
+    err = lib().oracle_deflater_run_parts(arr, lens, n, level, FORMAT[format], d, len(d) if d else 0,
+                                          1 if d is not None else 0, fn, len(fn), mtime & 0xFFFFFFFF,
+                                          out, cap, ctypes.byref(out_len), ends)
+    if err:
+        raise RuntimeError("oracle deflate error %d: %s" % (err, ERRORS.get(err)))
+    raw, res, prev = out.raw, [], 0
+    for k in range(n + 1):
+        res.append(raw[prev:ends[k]])
+        prev = ends[k]
+    return res
 
 
 def deflate(data, level=6, format="deflate", dictionary=None, file_name=None, mtime=0):

@@ -2065,11 +2065,14 @@ static void emit(deflate_state* s, const uint8_t* b, size_t n) {
     s->out_len += n;
 }
 
-/* sd-deflate.ts:51-254 Deflater + 263-274 deflate() */
-int32_t oracle_deflater_run(const uint8_t* const* parts, const size_t* part_lens, int32_t nparts,
-                            int32_t level, int32_t format, const uint8_t* dict, size_t dict_len,
-                            int32_t has_dict, const uint8_t* fname, size_t fname_len,
-                            uint32_t mtime, uint8_t* out, size_t out_cap, size_t* out_len) {
+/* sd-deflate.ts:51-254 Deflater + 263-274 deflate().  part_end (may be NULL; nparts + 1
+ * entries): the output length after each append() and after finish() -- where the
+ * reference's per-call outputs end in the concatenation. */
+int32_t oracle_deflater_run_parts(const uint8_t* const* parts, const size_t* part_lens, int32_t nparts,
+                                  int32_t level, int32_t format, const uint8_t* dict, size_t dict_len,
+                                  int32_t has_dict, const uint8_t* fname, size_t fname_len,
+                                  uint32_t mtime, uint8_t* out, size_t out_cap, size_t* out_len,
+                                  size_t* part_end) {
     *out_len = 0;
     if (level < 1 || level > 9 || format < 0 || format > 2) return ORA_E_BAD_ARG;
     if (has_dict && format != 1) return ORA_E_BAD_ARG;
@@ -2087,7 +2090,7 @@ int32_t oracle_deflater_run(const uint8_t* const* parts, const size_t* part_lens
     for (int pi = 0; pi < nparts; pi++) {
         const uint8_t* chunk = parts[pi];
         size_t clen = part_lens[pi];
-        if (clen == 0) continue;                                  /* sd-deflate.ts:180-182 */
+        if (clen == 0) { if (part_end) part_end[pi] = s->out_len; continue; }                                  /* sd-deflate.ts:180-182 */
         if (format != 2) checksum = oracle_adler32(chunk, clen, checksum);
         else checksum = oracle_crc32(chunk, clen, checksum);
         orig_size += (uint32_t)clen;
@@ -2114,6 +2117,7 @@ int32_t oracle_deflater_run(const uint8_t* const* parts, const size_t* part_lens
         do {
             deflate_call(s, NO_FLUSH);
         } while (s->avail_in > 0);
+        if (part_end) part_end[pi] = s->out_len;
     }
     if (s->status == DS_INIT) { free(s); return ORA_E_FINISH_BEFORE_APPEND; }
     deflate_call(s, FINISH);
@@ -2130,8 +2134,17 @@ int32_t oracle_deflater_run(const uint8_t* const* parts, const size_t* part_lens
     }
     int ovf = s->overflow;
     *out_len = s->out_len;
+    if (part_end) part_end[nparts] = s->out_len;
     free(s);
     if (ovf == 2) return ORA_E_OUT_CAP;
     if (ovf) return ORA_E_PENDING_OVERFLOW;
     return ORA_OK;
+}
+
+int32_t oracle_deflater_run(const uint8_t* const* parts, const size_t* part_lens, int32_t nparts,
+                            int32_t level, int32_t format, const uint8_t* dict, size_t dict_len,
+                            int32_t has_dict, const uint8_t* fname, size_t fname_len,
+                            uint32_t mtime, uint8_t* out, size_t out_cap, size_t* out_len) {
+    return oracle_deflater_run_parts(parts, part_lens, nparts, level, format, dict, dict_len, has_dict, fname,
+                                     fname_len, mtime, out, out_cap, out_len, NULL);
 }

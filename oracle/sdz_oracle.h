@@ -90,6 +90,13 @@ int32_t oracle_deflater_run(const uint8_t* const* parts, const size_t* part_lens
                             int32_t level, int32_t format, const uint8_t* dict, size_t dict_len,
                             int32_t has_dict, const uint8_t* fname, size_t fname_len,
                             uint32_t mtime, uint8_t* out, size_t out_cap, size_t* out_len);
+/* the same; part_end (nparts + 1 entries): output length after each append() and after
+ * finish(), i.e. where the reference's per-call outputs end (sd-deflate.ts:173-253) */
+int32_t oracle_deflater_run_parts(const uint8_t* const* parts, const size_t* part_lens, int32_t nparts,
+                                  int32_t level, int32_t format, const uint8_t* dict, size_t dict_len,
+                                  int32_t has_dict, const uint8_t* fname, size_t fname_len,
+                                  uint32_t mtime, uint8_t* out, size_t out_cap, size_t* out_len,
+                                  size_t* part_end);
 
 #ifdef __cplusplus
 }

@@ -42,6 +42,16 @@ typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 #define HEAP_SIZE (2 * L_CODES + 1)
 #define END_BLOCK 256
 
+// the scalar state of a Deflater between appends (sdz_deflate_append_batch_device)
+struct DfScal {
+    int32_t status;                 // 0 INIT (nothing appended), 1 BUSY, 2 FINISH (deflate.ts DeflateState)
+    int32_t checksum;               // running adler32 / crc32 of the input (sd-deflate.ts:185-190)
+    uint32_t orig;                  // input bytes so far, mod 2^32 (sd-deflate.ts:191)
+    int32_t pending, ins_h, block_start, match_length, match_available, strstart, match_start, lookahead,
+        prev_length, last_lit, matches, opt_len, static_len, bi_valid;
+    uint32_t bi_buf;
+};
+
 struct DSlab {                      // per-stream HBM state
     uint8_t window[WINDOW_SIZE];
     uint8_t pending[PENDING_SIZE];
@@ -54,6 +64,7 @@ struct DSlab {                      // per-stream HBM state
     uint16_t heap[2 * L_CODES + 1];
     uint16_t bl_count[16];
     uint16_t next_code[16];
+    DfScal sc;                      // incremental Deflater only
 };
 
 #define SLAB_BYTES ((sizeof(DSlab) + 255) & ~(uint64_t)255)
@@ -622,12 +633,17 @@ __device__ __forceinline__ int insert_string(DS& s) {
     return hh;
 }
 
-// deflate.ts:953-1049 (levels 1-3), run to FINISH
-__device__ __forceinline__ void deflate_fast(DS& s) {
+// deflate.ts:953-1049 (levels 1-3).  One-shot (STREAM false): the whole input, to FINISH.
+// STREAM: an append's chunk; without `finish` the loop stops where the reference's
+// deflate(NO_FLUSH) returns NeedMore (lookahead < MIN_LOOKAHEAD after fill_window, deflate.ts
+// 968-975), returning false.
+template <bool STREAM>
+__device__ __forceinline__ bool deflate_fast(DS& s, bool finish = true) {
     int hash_head = 0;
     for (;;) {
         if (s.lookahead < MIN_LOOKAHEAD) {
             fill_window(s);
+            if (STREAM && s.lookahead < MIN_LOOKAHEAD && !finish) return false;
             if (s.lookahead == 0) break;
         }
         if (s.lookahead >= MIN_MATCH) hash_head = insert_string(s);
@@ -655,14 +671,17 @@ __device__ __forceinline__ void deflate_fast(DS& s) {
         if (bflush) flush_block(s, false);
     }
     flush_block(s, true);
+    return true;
 }
 
-// deflate.ts:1054-1182 (levels 4-9), run to FINISH
-__device__ __forceinline__ void deflate_slow(DS& s) {
+// deflate.ts:1054-1182 (levels 4-9); STREAM and finish as deflate_fast
+template <bool STREAM>
+__device__ __forceinline__ bool deflate_slow(DS& s, bool finish = true) {
     int hash_head = 0;
     for (;;) {
         if (s.lookahead < MIN_LOOKAHEAD) {
             fill_window(s);
+            if (STREAM && s.lookahead < MIN_LOOKAHEAD && !finish) return false;
             if (s.lookahead == 0) break;
         }
         if (s.lookahead >= MIN_MATCH) hash_head = insert_string(s);
@@ -702,6 +721,7 @@ __device__ __forceinline__ void deflate_slow(DS& s) {
         s.match_available = 0;
     }
     flush_block(s, true);
+    return true;
 }
 
 // deflate.ts:1184-1216 deflateSetDictionary: the dictionary's last <= MAX_DIST bytes become
@@ -836,8 +856,8 @@ __global__ __launch_bounds__(DF_THREADS) void k_deflate(DeflateArgs A) {
     }
     s.out_len = hdr;
 
-    if (c_config[A.level][4]) deflate_fast(s);
-    else deflate_slow(s);
+    if (c_config[A.level][4]) deflate_fast<false>(s);
+    else deflate_slow<false>(s);
 
     // trailer (sd-deflate.ts:154-165)
     uint64_t tl = A.format == SDZ_DEFLATE_ZLIB ? 4 : gzip ? 8 : 0;
@@ -863,6 +883,173 @@ __global__ __launch_bounds__(DF_THREADS) void k_deflate(DeflateArgs A) {
     A.rec[sid] = R;
 }
 
+// ------------------------------------------------------------------ incremental Deflater
+
+// adler32(chunk, seed) / crc32(chunk, seed) (adler32.ts:34-105 with the NMAX grid from the
+// chunk's start, crc32.ts:48-106): the running checksum of Deflater.append
+__device__ int32_t chunk_checksum(const GLB uint8_t* p, uint64_t n, bool gzip, const uint32_t* crct, int32_t seed) {
+    if (gzip) {
+        uint32_t c = ~(uint32_t)seed;
+        for (uint64_t i = 0; i < n; i++) c = crct[(c ^ p[i]) & 255] ^ (c >> 8);
+        return (int32_t)~c;
+    }
+    uint64_t a = (uint32_t)seed & 0xffffu, s2 = ((uint32_t)seed >> 16) & 0xffffu, len = n, off = 0;
+    while (len >= 5552) {
+        len -= 5552;
+        for (int i = 0; i < 5552; i++) { a += p[off++]; s2 += a; }
+        a %= 65521u;
+        s2 += 65521u;
+    }
+    if (len) {
+        while (len--) { a += p[off++]; s2 += a; }
+        a %= 65521u;
+        s2 %= 65521u;
+    }
+    return (int32_t)((uint32_t)a | ((uint32_t)s2 << 16));
+}
+
+__global__ void k_deflate_reset(uint8_t* state, uint32_t n) {
+    const uint32_t sid = blockIdx.x * blockDim.x + threadIdx.x;
+    if (sid < n) ((GLB DSlab*)(state + (uint64_t)sid * SLAB_BYTES))->sc.status = 0;
+}
+
+// One Deflater.append(chunk) (finish = 0) or finish() (finish = 1) per stream, the stream's
+// whole state in its slab between calls (sd-deflate.ts:173-253 over deflate.ts:1218-1327 with
+// NO_FLUSH / FINISH).  The output of a call is what the reference's append()/finish() returns,
+// concatenated: the header on the first non-empty append, the blocks flushed during the call
+// (flush_block_only -> flush_pending), and the trailer at finish.  A record's out_len is this
+// call's output; its checksum the running one.  finish() before any append and an append after
+// finish() report SDZ_DATA_ERROR (the reference throws, sd-deflate.ts:232-234, 211-214).
+__global__ __launch_bounds__(DF_THREADS) void k_deflate_stream(DeflateArgs A, uint32_t finish) {
+    __shared__ uint32_t crct[256];
+    for (int n = threadIdx.x; n < 256; n += DF_THREADS) {
+        uint32_t c = (uint32_t)n;
+        for (int k = 0; k < 8; ++k) c = (c & 1) ? 0xedb88320u ^ (c >> 1) : c >> 1;
+        crct[n] = c;
+    }
+    __syncthreads();
+    const uint32_t sid = blockIdx.x * DF_THREADS + threadIdx.x;
+    if (sid >= A.n) return;
+    DS s;
+#ifdef SDZ_TIMING
+    s.timed = false;
+#endif
+    s.S = (GLB DSlab*)(A.state + (uint64_t)sid * SLAB_BYTES);
+    s.T = (const GLB DTables*)&g_dt;
+    s.in = (const GLB uint8_t*)(A.in + A.in_off[sid]);
+    s.in_len = A.in_len[sid];
+    s.in_pos = 0;
+    s.out = (GLB uint8_t*)(A.out + A.out_off[sid]);
+    s.out_cap = A.out_cap[sid];
+    s.out_len = 0;
+    s.err = 0;
+    GLB DfScal& C = s.S->sc;
+    const bool gzip = A.format == SDZ_DEFLATE_GZIP;
+    sdz_deflate_record R;
+    R.status = SDZ_OK; R.out_len = 0; R.reserved = 0;
+    const int32_t st = C.status;
+    R.checksum = st ? C.checksum : 0;
+    if ((finish && st == 0) || (!finish && st == 2 && s.in_len)) {
+        R.status = SDZ_DATA_ERROR;
+        A.rec[sid] = R;
+        return;
+    }
+    if (!finish && s.in_len == 0) { A.rec[sid] = R; return; }   // sd-deflate.ts:180-182: nothing
+    s.level = A.level;
+    s.good_match = c_config[A.level][0];
+    s.max_lazy = c_config[A.level][1];
+    s.nice_match = c_config[A.level][2];
+    s.max_chain = c_config[A.level][3];
+    s.heap_len = 0; s.heap_max = HEAP_SIZE;
+    s.l_max_code = s.d_max_code = s.bl_max_code = 0;
+    if (st == 0) {
+        // Deflate constructor (deflate.ts:196-220) + deflateSetDictionary, as k_deflate
+        const u32x4 z = {0u, 0u, 0u, 0u};
+        GLB u32x4* w4 = (GLB u32x4*)s.S->window;
+        for (int i = 0; i < WINDOW_SIZE / 16; i++) w4[i] = z;
+        GLB u32x4* h4 = (GLB u32x4*)s.S->head;
+        for (int i = 0; i < HASH_SIZE * 2 / 16; i++) h4[i] = z;
+        GLB u32x4* p4 = (GLB u32x4*)s.S->prev;
+        for (int i = 0; i < W_SIZE * 2 / 16; i++) p4[i] = z;
+        for (int i = 0; i < HEAP_SIZE * 2; i++) s.S->ltree[i] = 0;
+        for (int i = 0; i < (2 * D_CODES + 1) * 2; i++) s.S->dtree[i] = 0;
+        for (int i = 0; i < (2 * BL_CODES + 1) * 2; i++) s.S->bltree[i] = 0;
+        s.pending = 0;
+        s.ins_h = 0; s.block_start = 0; s.match_length = MIN_MATCH - 1; s.match_available = 0;
+        s.strstart = 0; s.match_start = 0; s.lookahead = 0; s.prev_length = MIN_MATCH - 1;
+        s.bi_buf = 0; s.bi_valid = 0;
+        init_block(s);
+        if (A.dict) set_dictionary(s, (const GLB uint8_t*)A.dict, A.dict_len);
+        C.checksum = gzip ? 0 : 1;
+        C.orig = 0;
+        // container header (sd-deflate.ts:98-152), on the first append
+        const bool dictid = A.format == SDZ_DEFLATE_ZLIB && A.dict && A.dict_adler != 0;
+        const uint64_t hdr = A.format == SDZ_DEFLATE_ZLIB ? (dictid ? 6 : 2)
+                           : gzip ? 10 + (A.fname_len ? A.fname_len + 1 : 0) : 0;
+        if (hdr > s.out_cap) { R.status = SDZ_OUT_OVERFLOW; A.rec[sid] = R; return; }
+        if (dictid) {
+            const uint32_t d = (uint32_t)A.dict_adler;
+            s.out[0] = 0x78; s.out[1] = 0x20;
+            s.out[2] = (uint8_t)(d >> 24); s.out[3] = (uint8_t)(d >> 16); s.out[4] = (uint8_t)(d >> 8); s.out[5] = (uint8_t)d;
+        } else if (A.format == SDZ_DEFLATE_ZLIB) { s.out[0] = 0x78; s.out[1] = 0x01; }
+        else if (gzip) {
+            s.out[0] = 0x1f; s.out[1] = 0x8b; s.out[2] = 8; s.out[3] = A.fname_len ? 8 : 0;
+            s.out[4] = (uint8_t)A.mtime; s.out[5] = (uint8_t)(A.mtime >> 8);
+            s.out[6] = (uint8_t)(A.mtime >> 16); s.out[7] = (uint8_t)(A.mtime >> 24);
+            s.out[8] = 0; s.out[9] = 0xff;
+            for (uint32_t i = 0; i < A.fname_len; i++) s.out[10 + i] = A.fname[i];
+            if (A.fname_len) s.out[10 + A.fname_len] = 0;
+        }
+        s.out_len = hdr;
+    } else {
+        s.pending = C.pending; s.ins_h = C.ins_h; s.block_start = C.block_start; s.match_length = C.match_length;
+        s.match_available = C.match_available; s.strstart = C.strstart; s.match_start = C.match_start;
+        s.lookahead = C.lookahead; s.prev_length = C.prev_length; s.last_lit = C.last_lit; s.matches = C.matches;
+        s.opt_len = C.opt_len; s.static_len = C.static_len; s.bi_buf = C.bi_buf; s.bi_valid = C.bi_valid;
+    }
+    if (s.in_len) {
+        C.checksum = chunk_checksum(s.in, s.in_len, gzip, crct, C.checksum);
+        C.orig += (uint32_t)s.in_len;
+    }
+    // deflate.ts:1290: a call runs the compressor when there is input, lookahead, or a first
+    // FINISH; a repeated finish() only adds the trailer again (as the reference does)
+    if (st != 2) {
+        if (c_config[A.level][4]) deflate_fast<true>(s, finish != 0);
+        else deflate_slow<true>(s, finish != 0);
+    }
+    if (finish) {
+        const uint64_t tl = A.format == SDZ_DEFLATE_ZLIB ? 4 : gzip ? 8 : 0;
+        const uint32_t c = (uint32_t)C.checksum, z = C.orig;
+        if (s.out_len + tl > s.out_cap) s.err |= 2;
+        else if (A.format == SDZ_DEFLATE_ZLIB) {
+            s.out[s.out_len] = (uint8_t)(c >> 24); s.out[s.out_len + 1] = (uint8_t)(c >> 16);
+            s.out[s.out_len + 2] = (uint8_t)(c >> 8); s.out[s.out_len + 3] = (uint8_t)c;
+            s.out_len += 4;
+        } else if (gzip) {
+            for (int k = 0; k < 4; k++) s.out[s.out_len + k] = (uint8_t)(c >> (8 * k));
+            for (int k = 0; k < 4; k++) s.out[s.out_len + 4 + k] = (uint8_t)(z >> (8 * k));
+            s.out_len += 8;
+        }
+    }
+    C.status = finish ? 2 : 1;
+    C.pending = s.pending; C.ins_h = s.ins_h; C.block_start = s.block_start; C.match_length = s.match_length;
+    C.match_available = s.match_available; C.strstart = s.strstart; C.match_start = s.match_start;
+    C.lookahead = s.lookahead; C.prev_length = s.prev_length; C.last_lit = s.last_lit; C.matches = s.matches;
+    C.opt_len = s.opt_len; C.static_len = s.static_len; C.bi_buf = s.bi_buf; C.bi_valid = s.bi_valid;
+    R.status = (s.err & 2) ? SDZ_OUT_OVERFLOW : (s.err & 1) ? SDZ_DATA_ERROR : SDZ_OK;
+    R.checksum = C.checksum;
+    R.out_len = s.out_len;
+    A.rec[sid] = R;
+}
+
+void launch_deflate_reset(uint8_t* state, uint32_t n, hipStream_t s) {
+    if (n) hipLaunchKernelGGL(k_deflate_reset, dim3((n + 255) / 256), dim3(256), 0, s, state, n);
+}
+void launch_deflate_stream(const DeflateArgs& a, uint32_t finish, hipStream_t s) {
+    if (!a.n) return;
+    hipLaunchKernelGGL(k_deflate_tables, dim3(1), dim3(1), 0, s);
+    hipLaunchKernelGGL(k_deflate_stream, dim3((a.n + DF_THREADS - 1) / DF_THREADS), dim3(DF_THREADS), 0, s, a, finish);
+}
 
 // ------------------------------------------------------------------ record path kernels
 

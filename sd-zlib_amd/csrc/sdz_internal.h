@@ -105,6 +105,9 @@ struct DeflateArgs {
 
 uint64_t deflate_state_bytes();
 void launch_deflate(const DeflateArgs& a, hipStream_t s);
+// incremental Deflater (k_deflate_stream): fresh state; one append (finish 0) / finish (1)
+void launch_deflate_reset(uint8_t* state, uint32_t n, hipStream_t s);
+void launch_deflate_stream(const DeflateArgs& a, uint32_t finish, hipStream_t s);
 constexpr uint32_t kDeflateRecMax = 65536;   // longest input on the record path
 // max of n device-resident u64 values (blocking; for scratch sizing); d_slot: 8 device bytes
 int device_max_u64(const uint64_t* v, uint32_t n, unsigned long long* d_slot, uint64_t* out, hipStream_t s);

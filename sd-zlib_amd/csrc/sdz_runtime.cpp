@@ -873,6 +873,70 @@ int sdz_inflate_batch(const uint8_t* const* in, const size_t* in_len, uint8_t* c
     return SDZ_API_OK;
 }
 
+// ------------------------------------------------------------ incremental deflate
+
+uint64_t sdz_deflate_state_bytes(uint32_t n) { return (uint64_t)n * deflate_state_bytes(); }
+
+uint64_t sdz_deflate_append_bound(uint64_t in_len, int32_t format, uint32_t fname_len) {
+    // blocks flushed by one call: this call's input at <= 31 bits per 3-byte match / 9 bits per
+    // literal (static trees; dynamic and stored are only chosen when smaller), plus the block
+    // pending from earlier calls (<= 16,383 symbols), header and trailer
+    return in_len + in_len / 3 + (128u << 10) + 64 + (format == SDZ_DEFLATE_GZIP ? fname_len + 1 : 0);
+}
+
+int sdz_deflate_state_reset_device(void* state, uint32_t n, void* stream) {
+    if (int rc = ensure_device()) return rc;
+    if (n == 0) return SDZ_API_OK;
+    if (!state) return fail(SDZ_API_BAD_ARG, "sdz_deflate_state_reset_device: null state");
+    launch_deflate_reset((uint8_t*)state, n, (hipStream_t)stream);
+    HIPCHK(hipGetLastError());
+    return SDZ_API_OK;
+}
+
+int sdz_deflate_append_batch_device(void* state, const uint8_t* in, const uint64_t* in_off,
+                                    const uint64_t* in_len, uint8_t* out, const uint64_t* out_off,
+                                    const uint64_t* out_cap, sdz_deflate_record* rec, uint32_t n,
+                                    int32_t level, int32_t format, const uint8_t* fname,
+                                    uint32_t fname_len, uint32_t mtime, const uint8_t* dict,
+                                    uint32_t dict_len, int32_t finish, void* stream) {
+    if (int rc = ensure_device()) return rc;
+    if (n == 0) return SDZ_API_OK;
+    if (level < 1 || level > 9) return fail(SDZ_API_BAD_ARG, "level must be between 1 and 9, inclusive");
+    if (format < SDZ_DEFLATE_RAW || format > SDZ_DEFLATE_GZIP)
+        return fail(SDZ_API_BAD_ARG, "container must be one of `raw`, `deflate`, `gzip`");
+    if (!state || !in || !in_off || !in_len || !out || !out_off || !out_cap || !rec)
+        return fail(SDZ_API_BAD_ARG, "sdz_deflate_append_batch_device: null pointer");
+    if (dict && format != SDZ_DEFLATE_ZLIB)
+        return fail(SDZ_API_BAD_ARG, "Can only provide a dictionary for `deflate` containers.");
+    hipStream_t s = (hipStream_t)stream;
+    std::lock_guard<std::mutex> lk(g_mu);
+    int32_t dict_adler = 1;
+    if (dict) {
+        if (int rc = device_checksum(dict, dict_len, 0, 1, &dict_adler, s)) return rc;
+    }
+    void* tmp = nullptr;
+    PoolUse tmp_use(g_tmp, s);
+    if (int rc = tmp_use.get(kTmpFname + fname_len + 64, &tmp)) return rc;
+    uint8_t* d_fname = nullptr;
+    if (fname_len) {
+        d_fname = (uint8_t*)tmp + kTmpFname;
+        HIPCHK(hipMemcpyAsync(d_fname, fname, fname_len, hipMemcpyHostToDevice, s));
+    }
+    DeflateArgs a{};
+    a.in = in; a.in_off = in_off; a.in_len = in_len;
+    a.out = out; a.out_off = out_off; a.out_cap = out_cap;
+    a.rec = rec; a.state = (uint8_t*)state;
+    a.dict = dict; a.dict_len = dict_len; a.dict_adler = dict_adler;
+    a.fname = d_fname; a.fname_len = fname_len; a.mtime = mtime;
+    a.n = n; a.level = level; a.format = format;
+    timing_begin(s);
+    launch_deflate_stream(a, finish ? 1u : 0u, s);
+    timing_end(s);
+    HIPCHK(hipGetLastError());
+    if (fname_len) HIPCHK(hipStreamSynchronize(s));     // (the host file name was a copy source)
+    return SDZ_API_OK;
+}
+
 // ----------------------------------------------------------------- one host Inflater
 
 }  // extern "C"
@@ -957,6 +1021,96 @@ int sdz_inflater_append(sdz_inflater* z, const uint8_t* data, size_t len, const 
 }
 
 void sdz_inflater_destroy(sdz_inflater* z) { delete z; }
+
+}  // extern "C"
+
+struct sdz_deflater {
+    int32_t level = 6, format = SDZ_DEFLATE_ZLIB;
+    std::vector<uint8_t> fname;
+    uint32_t mtime = 0;
+    uint8_t* d_state = nullptr;
+    uint8_t* d_dict = nullptr;
+    uint32_t dict_len = 0;
+    uint8_t* d_in = nullptr;
+    size_t in_cap = 0;
+    uint8_t* d_out = nullptr;
+    size_t out_cap = 0;
+    uint64_t* d_meta = nullptr;                   // in_off, in_len, out_off, out_cap
+    sdz_deflate_record* d_rec = nullptr;
+    std::vector<uint8_t> out;
+    ~sdz_deflater() {
+        for (void* p : { (void*)d_state, (void*)d_dict, (void*)d_in, (void*)d_out, (void*)d_meta, (void*)d_rec })
+            if (p) hipFree(p);
+    }
+};
+
+extern "C" {
+
+sdz_deflater* sdz_deflater_create(int32_t level, int32_t format, const uint8_t* fname, size_t fname_len,
+                                  uint32_t mtime, const uint8_t* dict, size_t dict_len) {
+    if (ensure_device()) return nullptr;
+    if (level < 1 || level > 9) { fail(SDZ_API_BAD_ARG, "level must be between 1 and 9, inclusive"); return nullptr; }
+    if (format < SDZ_DEFLATE_RAW || format > SDZ_DEFLATE_GZIP) {
+        fail(SDZ_API_BAD_ARG, "container must be one of `raw`, `deflate`, `gzip`");
+        return nullptr;
+    }
+    if (dict && format != SDZ_DEFLATE_ZLIB) {
+        fail(SDZ_API_BAD_ARG, "Can only provide a dictionary for `deflate` containers.");
+        return nullptr;
+    }
+    sdz_deflater* z = new sdz_deflater;
+    z->level = level; z->format = format; z->mtime = mtime;
+    if (fname && fname_len) z->fname.assign(fname, fname + fname_len);
+    hipError_t e = hipMalloc(&z->d_state, sdz_deflate_state_bytes(1));
+    if (e == hipSuccess) e = hipMalloc(&z->d_meta, 4 * sizeof(uint64_t));
+    if (e == hipSuccess) e = hipMalloc(&z->d_rec, sizeof(sdz_deflate_record));
+    if (e == hipSuccess && dict) {
+        z->dict_len = (uint32_t)dict_len;
+        e = hipMalloc(&z->d_dict, dict_len + 64);
+        if (e == hipSuccess && dict_len) e = hipMemcpy(z->d_dict, dict, dict_len, hipMemcpyHostToDevice);
+    }
+    if (e != hipSuccess || sdz_deflate_state_reset_device(z->d_state, 1, nullptr) != SDZ_API_OK) {
+        if (e != hipSuccess) hip_fail(e, "sdz_deflater_create");
+        delete z;
+        return nullptr;
+    }
+    return z;
+}
+
+int sdz_deflater_append(sdz_deflater* z, const uint8_t* data, size_t len, int32_t finish,
+                        const uint8_t** out, size_t* out_len, sdz_deflate_record* rec) {
+    if (!z || !out || !out_len || !rec || (!data && len)) return fail(SDZ_API_BAD_ARG, "sdz_deflater_append: null pointer");
+    z->out.clear();
+    if (len + 64 > z->in_cap) {
+        if (z->d_in) hipFree(z->d_in);
+        z->d_in = nullptr;
+        z->in_cap = std::max<size_t>(len + 64, 1 << 16);
+        HIPCHK(hipMalloc(&z->d_in, z->in_cap));
+    }
+    const uint64_t cap = sdz_deflate_append_bound(len, z->format, (uint32_t)z->fname.size());
+    if (cap > z->out_cap) {
+        if (z->d_out) hipFree(z->d_out);
+        z->d_out = nullptr;
+        z->out_cap = cap;
+        HIPCHK(hipMalloc(&z->d_out, z->out_cap));
+    }
+    if (len) HIPCHK(hipMemcpy(z->d_in, data, len, hipMemcpyHostToDevice));
+    uint64_t meta[4] = { 0, len, 0, cap };
+    HIPCHK(hipMemcpy(z->d_meta, meta, sizeof meta, hipMemcpyHostToDevice));
+    int rc = sdz_deflate_append_batch_device(z->d_state, z->d_in, z->d_meta, z->d_meta + 1, z->d_out, z->d_meta + 2,
+                                             z->d_meta + 3, z->d_rec, 1, z->level, z->format,
+                                             z->fname.empty() ? nullptr : z->fname.data(), (uint32_t)z->fname.size(),
+                                             z->mtime, z->d_dict, z->dict_len, finish, nullptr);
+    if (rc) return rc;
+    HIPCHK(hipMemcpy(rec, z->d_rec, sizeof *rec, hipMemcpyDeviceToHost));
+    z->out.resize(rec->out_len);
+    if (rec->out_len) HIPCHK(hipMemcpy(z->out.data(), z->d_out, rec->out_len, hipMemcpyDeviceToHost));
+    *out = z->out.data();
+    *out_len = z->out.size();
+    return SDZ_API_OK;
+}
+
+void sdz_deflater_destroy(sdz_deflater* z) { delete z; }
 
 int sdz_deflate_batch(const uint8_t* const* in, const size_t* in_len, uint8_t* const* out,
                       const size_t* out_cap, sdz_deflate_record* rec, uint32_t n, int32_t level,

@@ -232,8 +232,22 @@ export class Deflater {
 			return cc > 0xff ? 95 : cc;
 		});
 		this.fileName = new Uint8Array(name);
-		this.parts = [];
-		this.checksum = format === "gzip" ? 0 : 1;
+		this.handle = null;
+		this.mtime = undefined;     // gzip MTIME override (tests); default Date.now() at the first append
+	}
+
+	// the compressor lives on the device from the first append on (sdz_deflater_*)
+	call(chunk, finish) {
+		if (this.handle === null) {
+			const fmt = this.format === "raw" ? 0 : this.format === "deflate" ? 1 : 2;
+			const mtime = this.mtime !== undefined ? this.mtime : Math.floor(Date.now() / 1000);   // sd-deflate.ts:140
+			this.handle = addon.deflaterCreate(this.level, fmt, this.fileName, mtime >>> 0, this.dict || null);
+		}
+		const r = addon.deflaterAppend(this.handle, chunk, finish);
+		if (r.status !== "OK") {
+			throw new Error("deflating: " + r.status);
+		}
+		return chunks(r.data);
 	}
 
 	append(data) {
@@ -244,30 +258,14 @@ export class Deflater {
 		if (!chunk.length) {
 			return [];
 		}
-		// sd-deflate.ts:185-190: the trailer's checksum runs chunk by chunk (adler32's NMAX
-		// quirk depends on where the appends split the input)
-		this.checksum = this.format === "gzip" ? crc32(chunk, this.checksum) : adler32(chunk, this.checksum);
-		this.parts.push(chunk);
-		return [];
+		return this.call(chunk, false);
 	}
 
 	finish() {
-		if (this.parts.length === 0) {
+		if (this.handle === null) {
 			throw new Error("Cannot call finish before at least 1 call to append");
 		}
-		const input = this.parts.length === 1 ? this.parts[0] : mergeBuffers(this.parts);
-		const fmt = this.format === "raw" ? 0 : this.format === "deflate" ? 1 : 2;
-		const mtime = Math.floor(Date.now() / 1000);      // sd-deflate.ts:140
-		const r = addon.deflateBatch([input], this.level, fmt, this.fileName, mtime, this.dict || null)[0];
-		if (r.status !== "OK") {
-			throw new Error("deflating: " + r.status);
-		}
-		if (this.format === "deflate") {                 // the append-chained adler32 (big-endian)
-			const n = r.data.length, c = this.checksum >>> 0;
-			r.data[n - 4] = c >>> 24; r.data[n - 3] = (c >>> 16) & 255;
-			r.data[n - 2] = (c >>> 8) & 255; r.data[n - 1] = c & 255;
-		}
-		return chunks(r.data);
+		return this.call(new Uint8Array(0), true);
 	}
 }
 
@@ -277,10 +275,19 @@ export function deflate(data, options) {
 	if (!(input instanceof Uint8Array)) {
 		throw new TypeError("data must be an ArrayBuffer or buffer view");
 	}
-	const deflater = new Deflater(options);
-	const buffers = deflater.append(data);
-	buffers.push(...deflater.finish());
-	return mergeBuffers(buffers);
+	// Deflater(options).append(data) + finish(), merged: one call of the batched compressor
+	// (its record path for levels 4-9) gives the same bytes
+	const d = new Deflater(options);
+	if (!input.length) {
+		throw new Error("Cannot call finish before at least 1 call to append");
+	}
+	const fmt = d.format === "raw" ? 0 : d.format === "deflate" ? 1 : 2;
+	const mtime = Math.floor(Date.now() / 1000);      // sd-deflate.ts:140
+	const r = addon.deflateBatch([input], d.level, fmt, d.fileName, mtime, d.dict || null)[0];
+	if (r.status !== "OK") {
+		throw new Error("deflating: " + r.status);
+	}
+	return r.data;
 }
 
 // batched entry points (the GPU's native shape; not in the reference API)

@@ -271,6 +271,75 @@ napi_value InflaterAppend(napi_env env, napi_callback_info info) {
     return o;
 }
 
+// ---- one incremental Deflater (sdz_deflater_*): compressor state stays on the device
+
+void deflater_finalize(napi_env, void* data, void*) { sdz_deflater_destroy((sdz_deflater*)data); }
+
+// deflaterCreate(level, format (0 raw, 1 deflate, 2 gzip), fileNameLatin1: Uint8Array, mtime,
+// dict: Uint8Array|null) -> handle
+napi_value DeflaterCreate(napi_env env, napi_callback_info info) {
+    size_t argc = 5;
+    napi_value argv[5];
+    NAPI_OK(napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr));
+    int32_t level = 6, fmt = 1;
+    uint32_t mtime = 0;
+    NAPI_OK(napi_get_value_int32(env, argv[0], &level));
+    NAPI_OK(napi_get_value_int32(env, argv[1], &fmt));
+    const uint8_t* fname = nullptr;
+    size_t fname_len = 0;
+    get_bytes(env, argv[2], &fname, &fname_len);
+    NAPI_OK(napi_get_value_uint32(env, argv[3], &mtime));
+    const uint8_t* dict = nullptr;
+    size_t dict_len = 0;
+    napi_valuetype dt;
+    napi_typeof(env, argv[4], &dt);
+    if (dt != napi_null && dt != napi_undefined) get_bytes(env, argv[4], &dict, &dict_len);
+    sdz_deflater* z = sdz_deflater_create(level, fmt, fname, fname_len, mtime,
+                                          dt != napi_null && dt != napi_undefined ? (dict ? dict : (const uint8_t*)"") : nullptr,
+                                          dict_len);
+    if (!z) {
+        napi_throw_error(env, nullptr, (std::string("libsdz: ") + sdz_last_error()).c_str());
+        return nullptr;
+    }
+    napi_value h;
+    NAPI_OK(napi_create_external(env, z, deflater_finalize, nullptr, &h));
+    return h;
+}
+
+// deflaterAppend(handle, chunk: Uint8Array, finish: boolean) -> { status, data }
+napi_value DeflaterAppend(napi_env env, napi_callback_info info) {
+    size_t argc = 3;
+    napi_value argv[3];
+    NAPI_OK(napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr));
+    void* hp = nullptr;
+    NAPI_OK(napi_get_value_external(env, argv[0], &hp));
+    const uint8_t* in = nullptr;
+    size_t len = 0;
+    if (!get_bytes(env, argv[1], &in, &len)) {
+        napi_throw_type_error(env, nullptr, "data must be an ArrayBuffer or buffer view");
+        return nullptr;
+    }
+    bool finish = false;
+    NAPI_OK(napi_get_value_bool(env, argv[2], &finish));
+    const uint8_t* out = nullptr;
+    size_t out_len = 0;
+    sdz_deflate_record r;
+    if (sdz_deflater_append((sdz_deflater*)hp, in, len, finish ? 1 : 0, &out, &out_len, &r)) {
+        napi_throw_error(env, nullptr, (std::string("libsdz: ") + sdz_last_error()).c_str());
+        return nullptr;
+    }
+    napi_value o, ab, ta;
+    NAPI_OK(napi_create_object(env, &o));
+    const char* sn = status_name(r.status);
+    set_str(env, o, "status", sn, strlen(sn));
+    void* p = nullptr;
+    NAPI_OK(napi_create_arraybuffer(env, out_len ? out_len : 1, &p, &ab));
+    if (out_len) memcpy(p, out, out_len);
+    NAPI_OK(napi_create_typedarray(env, napi_uint8_array, out_len, ab, 0, &ta));
+    napi_set_named_property(env, o, "data", ta);
+    return o;
+}
+
 napi_value Checksum(napi_env env, napi_callback_info info, bool crc) {
     size_t argc = 2;
     napi_value argv[2];
@@ -311,6 +380,8 @@ napi_value Init(napi_env env, napi_value exports) {
         { "deviceCount", nullptr, DeviceCount, nullptr, nullptr, nullptr, napi_enumerable, nullptr },
         { "inflaterCreate", nullptr, InflaterCreate, nullptr, nullptr, nullptr, napi_enumerable, nullptr },
         { "inflaterAppend", nullptr, InflaterAppend, nullptr, nullptr, nullptr, napi_enumerable, nullptr },
+        { "deflaterCreate", nullptr, DeflaterCreate, nullptr, nullptr, nullptr, napi_enumerable, nullptr },
+        { "deflaterAppend", nullptr, DeflaterAppend, nullptr, nullptr, nullptr, napi_enumerable, nullptr },
     };
     napi_define_properties(env, exports, sizeof d / sizeof d[0], d);
     return exports;

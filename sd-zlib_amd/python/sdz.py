@@ -62,6 +62,8 @@ EXPORTS = [
     "sdz_sync", "sdz_stream_create", "sdz_stream_destroy", "sdz_set_timing", "sdz_last_kernel_ms", "sdz_last_kernel_breakdown",
     "sdz_inflate_state_bytes", "sdz_inflate_state_reset_device", "sdz_inflate_append_batch_device",
     "sdz_inflater_create", "sdz_inflater_append", "sdz_inflater_destroy",
+    "sdz_deflate_state_bytes", "sdz_deflate_append_bound", "sdz_deflate_state_reset_device",
+    "sdz_deflate_append_batch_device", "sdz_deflater_create", "sdz_deflater_append", "sdz_deflater_destroy",
 ]
 
 _lib = None
@@ -132,6 +134,22 @@ def lib():
                                           ctypes.POINTER(InflateRecord)]
         L.sdz_inflater_append.restype = ctypes.c_int
         L.sdz_inflater_destroy.argtypes = [vp]
+    if hasattr(L, "sdz_deflater_create"):
+        L.sdz_deflate_state_bytes.argtypes = [u32]
+        L.sdz_deflate_state_bytes.restype = ctypes.c_uint64
+        L.sdz_deflate_append_bound.argtypes = [ctypes.c_uint64, i32, u32]
+        L.sdz_deflate_append_bound.restype = ctypes.c_uint64
+        L.sdz_deflate_state_reset_device.argtypes = [vp, u32, vp]
+        L.sdz_deflate_state_reset_device.restype = ctypes.c_int
+        L.sdz_deflate_append_batch_device.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, u32, i32, i32, vp, u32, u32,
+                                                      vp, u32, i32, vp]
+        L.sdz_deflate_append_batch_device.restype = ctypes.c_int
+        L.sdz_deflater_create.argtypes = [i32, i32, u8p, sz, u32, u8p, sz]
+        L.sdz_deflater_create.restype = vp
+        L.sdz_deflater_append.argtypes = [vp, u8p, sz, i32, ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(sz),
+                                          ctypes.POINTER(DeflateRecord)]
+        L.sdz_deflater_append.restype = ctypes.c_int
+        L.sdz_deflater_destroy.argtypes = [vp]
     _lib = L
     return L
 
@@ -252,6 +270,63 @@ class DeviceBuffer:
 
 def _u64_array(vals):
     return (ctypes.c_uint64 * len(vals))(*vals)
+
+
+class DeflateStreams:
+    """n Deflaters on the device at once (sdz_deflate_append_batch_device): append() hands
+    every stream its next chunk (b"" for none); finish() ends them all (with a last chunk
+    each, optionally).  Both return per stream (status name, output bytes of the call)."""
+
+    def __init__(self, n, level=6, format="deflate", file_name_latin1=b"", mtime=0, dictionary=None):
+        L = lib()
+        self.n, self.level, self.fmt = n, level, DEFLATE_FORMATS[format]
+        self.fname, self.mtime = bytes(file_name_latin1), mtime
+        self.state = DeviceBuffer(L.sdz_deflate_state_bytes(n))
+        _check(L.sdz_deflate_state_reset_device(self.state.ptr, n, None))
+        self.dict, self.dict_len = None, 0
+        if dictionary is not None:
+            self.dict = DeviceBuffer(len(dictionary) + 64)
+            self.dict.upload(bytes(dictionary))
+            self.dict_len = len(dictionary)
+
+    def _call(self, chunks, finish):
+        L, n = lib(), self.n
+        chunks = [bytes(c) for c in chunks]
+        in_off, o = [], 0
+        for c in chunks:
+            in_off.append(o)
+            o += (len(c) + 15) & ~15
+        d_in = DeviceBuffer(o + 128)
+        if o:
+            d_in.upload(b"".join(c + b"\0" * (((len(c) + 15) & ~15) - len(c)) for c in chunks))
+        caps = [int(L.sdz_deflate_append_bound(len(c), self.fmt, len(self.fname))) for c in chunks]
+        out_off, q = [], 0
+        for c in caps:
+            out_off.append(q)
+            q += (c + 255) & ~255
+        d_out = DeviceBuffer(q + 64)
+        meta = in_off + [len(c) for c in chunks] + out_off + caps
+        d_meta = DeviceBuffer(8 * len(meta))
+        d_meta.upload(bytes(_u64_array(meta)))
+        d_rec = DeviceBuffer(ctypes.sizeof(DeflateRecord) * n)
+        m = d_meta.ptr
+        _check(L.sdz_deflate_append_batch_device(
+            self.state.ptr, d_in.ptr, m, m + 8 * n, d_out.ptr, m + 16 * n, m + 24 * n, d_rec.ptr, n,
+            self.level, self.fmt, self.fname or None, len(self.fname), self.mtime & 0xFFFFFFFF,
+            self.dict.ptr if self.dict else None, self.dict_len, 1 if finish else 0, None))
+        _check(L.sdz_sync(None))
+        recs = (DeflateRecord * n).from_buffer_copy(d_rec.download(n * ctypes.sizeof(DeflateRecord)))
+        res = [(STATUS.get(r.status, str(r.status)), d_out.download(r.out_len, out_off[i]) if r.out_len else b"")
+               for i, r in enumerate(recs)]
+        for b in (d_in, d_out, d_meta, d_rec):
+            b.free()
+        return res
+
+    def append(self, chunks):
+        return self._call(chunks, False)
+
+    def finish(self, chunks=None):
+        return self._call(chunks if chunks is not None else [b""] * self.n, True)
 
 
 class InflateStreams:
@@ -478,8 +553,10 @@ def _latin1(name):
 
 
 class Deflater:
-    """sd-deflate.ts:51-254.  append() buffers, finish() compresses the whole input
-    on the GPU; the merged output is identical to the reference's."""
+    """sd-deflate.ts:51-254.  Each append() runs the GPU compressor on the new bytes only: the
+    stream's window, hash chains, pending block, bit buffer and running checksum stay on the
+    device between calls (sdz_deflater_*), and append()/finish() return what the reference's
+    return for the same calls, in 16 KiB chunks (zstream.ts:11)."""
 
     def __init__(self, options=None):
         options = options or {}
@@ -502,42 +579,62 @@ class Deflater:
         self._dict = d
         self._level, self._fmt = level, fmt
         self._name = _latin1(file_name or "")
-        self._input = b""
-        self._appended = False
-        self._checksum = 0 if fmt == "gzip" else 1
-        self.mtime = None
+        self._h = None
+        self.mtime = None                # gzip MTIME: None = Math.floor(Date.now()/1000) at the first append
+
+    def _handle(self):
+        if self._h is None:
+            L = lib()
+            mtime = self.mtime if self.mtime is not None else int(math.floor(time.time()))
+            self._h = L.sdz_deflater_create(self._level, DEFLATE_FORMATS[self._fmt], self._name, len(self._name),
+                                            mtime & 0xFFFFFFFF, self._dict, len(self._dict) if self._dict else 0)
+            if not self._h:
+                raise SdzError("libsdz: %s" % L.sdz_last_error().decode())
+        return self._h
+
+    def _call(self, chunk, finish):
+        rec = DeflateRecord()
+        optr, olen = ctypes.c_void_p(), ctypes.c_size_t()
+        _check(lib().sdz_deflater_append(self._handle(), chunk, len(chunk), 1 if finish else 0,
+                                         ctypes.byref(optr), ctypes.byref(olen), ctypes.byref(rec)))
+        return rec, (ctypes.string_at(optr, olen.value) if olen.value else b"")
 
     def append(self, data):
         chunk = _u8(data)
         if not chunk:
-            return []
-        # sd-deflate.ts:185-190: the trailer's checksum runs chunk by chunk, so adler32's NMAX
-        # quirk (adler32.ts:67) depends on where the appends split the input
-        if self._fmt == "gzip":
-            self._checksum = crc32(chunk, self._checksum)
-        else:
-            self._checksum = adler32(chunk, self._checksum)
-        self._input += chunk
-        self._appended = True
-        return []
+            return []                    # sd-deflate.ts:180-182
+        rec, out = self._call(chunk, False)
+        if rec.status != 0:
+            raise SdzError("deflating: " + STATUS.get(rec.status, str(rec.status)))
+        return _chunks(out)
 
     def finish(self):
-        if not self._appended:
+        if self._h is None:
             raise SdzError("Cannot call finish before at least 1 call to append")
-        mtime = self.mtime if self.mtime is not None else int(math.floor(time.time()))
-        r = deflate_batch([self._input], self._level, self._fmt, self._name, mtime, dictionary=self._dict)[0]
-        if r["status"] != "OK":
-            raise SdzError("deflating: " + r["status"])
-        data = r["data"]
-        if self._fmt == "deflate":                      # the append-chained adler32 (big-endian)
-            data = data[:-4] + (self._checksum & 0xFFFFFFFF).to_bytes(4, "big")
-        return _chunks(data)
+        rec, out = self._call(b"", True)
+        if rec.status != 0:
+            raise SdzError("deflating: " + STATUS.get(rec.status, str(rec.status)))
+        return _chunks(out)
+
+    def __del__(self):
+        try:
+            if self._h:
+                lib().sdz_deflater_destroy(self._h)
+                self._h = None
+        except Exception:
+            pass
 
 
 def deflate(data, options=None):
-    """sd-deflate.ts:263-274"""
-    _u8(data)
-    d = Deflater(options)
-    bufs = d.append(data)
-    bufs += d.finish()
-    return mergeBuffers(bufs)
+    """sd-deflate.ts:263-274: Deflater(options).append(data) + finish(), merged.  One call of
+    the batched compressor (its record path for levels 4-9), whose output equals the
+    Deflater's for the same input."""
+    inp = _u8(data)
+    d = Deflater(options)                # the options' checks
+    if not inp:
+        raise SdzError("Cannot call finish before at least 1 call to append")
+    mtime = d.mtime if d.mtime is not None else int(math.floor(time.time()))
+    r = deflate_batch([inp], d._level, d._fmt, d._name, mtime, dictionary=d._dict)[0]
+    if r["status"] != "OK":
+        raise SdzError("deflating: " + r["status"])
+    return r["data"]

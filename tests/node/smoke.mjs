@@ -59,6 +59,19 @@ check("inflate(simple.raw) auto-detect", eq(inflate(golden("simple.raw")), golde
 }
 check("deflate L6 == reference fixture", eq(deflate(text, { level: 6 }), golden("paradiselost.deflate")));
 {
+	// Deflater.append in pieces: output arrives per append (complete blocks), and the merged
+	// stream is the reference's
+	const d = new Deflater({ level: 6 });
+	const outs = [];
+	for (let i = 0, k = 1; i < text.length; i += k, k = k * 3 % 70001 + 1) outs.push(...d.append(text.subarray(i, i + k)));
+	const early = mergeBuffers(outs).length;
+	outs.push(...d.finish());
+	check("Deflater in pieces == reference fixture", eq(mergeBuffers(outs), golden("paradiselost.deflate")) && early > 100000);
+	let m = "";
+	try { new Deflater().finish(); } catch (e) { m = e.message; }
+	check("finish before append", m === "Cannot call finish before at least 1 call to append");
+}
+{
 	// test/index.html:173-208: a preset dictionary round trip ("deflate" container)
 	const words = new TextEncoder().encode("the of and to in that with his her for thou thy thee");
 	const src = text.subarray(2000, 30000);
