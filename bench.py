@@ -14,6 +14,7 @@ own Node path cannot be run) and a deflate leg (configs[2]).
 """
 import argparse
 import ctypes
+import glob
 import json
 import os
 import sys
@@ -384,8 +385,10 @@ def main():
                          "in %.1f s; per core: %d in %.1f s on 1 thread" % (cnt, threads, dt, c1, d1)}
 
     traffic = None
-    pmc = os.path.join(ROOT, "profiles", "r01_inflate_pmc.json")
-    if os.path.exists(pmc) and n == 65536:
+    # the latest round's PMC traffic summary (tools/round_measure.sh writes profiles/rNN_inflate_pmc.json)
+    pmcs = sorted(glob.glob(os.path.join(ROOT, "profiles", "r[0-9][0-9]_inflate_pmc.json")))
+    pmc = pmcs[-1] if pmcs else ""
+    if pmc and os.path.exists(pmc) and n == 65536:
         try:
             traffic = json.load(open(pmc)).get("hbm_bytes_per_launch")
         except Exception:
