@@ -221,6 +221,20 @@ int sdz_deflater_append(sdz_deflater* z, const uint8_t* data, size_t len, int32_
                         const uint8_t** out, size_t* out_len, sdz_deflate_record* rec);
 void sdz_deflater_destroy(sdz_deflater* z);
 
+/* ------------------------------------------- fast deflate (NOT bit-exact) */
+
+/* The opt-in fast compressor: valid raw / zlib / gzip streams -- the
+ * container as sd-deflate.ts:98-165 writes it, any inflater reads them, adler32 / crc32 of
+ * the input in the trailer -- but not the reference's bytes: each 16 KiB tile of a stream
+ * is compressed on its own (greedy parse, one dynamic-Huffman or stored block per tile,
+ * byte-aligned by an empty stored block).  Not a drop-in for deflate(); for callers that
+ * only need a valid stream fast.  out_cap[i] >= sdz_deflate_fast_bound(in_len[i], ...). */
+uint64_t sdz_deflate_fast_bound(uint64_t in_len, int32_t format, uint32_t fname_len);
+int sdz_deflate_fast_batch_device(const uint8_t* in, const uint64_t* in_off, const uint64_t* in_len,
+                                  uint8_t* out, const uint64_t* out_off, const uint64_t* out_cap,
+                                  sdz_deflate_record* rec, uint32_t n, int32_t format,
+                                  const uint8_t* fname, uint32_t fname_len, uint32_t mtime, void* stream);
+
 /* Worst-case compressed size for one stream (header + blocks + trailer). */
 uint64_t sdz_deflate_bound(uint64_t in_len, int32_t format, uint32_t fname_len);
 

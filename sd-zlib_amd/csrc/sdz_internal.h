@@ -105,6 +105,13 @@ struct DeflateArgs {
 
 uint64_t deflate_state_bytes();
 void launch_deflate(const DeflateArgs& a, hipStream_t s);
+// the fast (not bit-exact) compressor (k_deflate_fast.hip): 16 KiB tiles, one block each
+#define FT_TILE_BYTES 8192u
+#define FT_TILE_OUT 8256u                 // a tile's output slot (<= tile + 10 bytes)
+void launch_fast_tiles(const uint8_t* in, const uint64_t* in_off, const uint64_t* in_len, const uint32_t* tile_stream,
+                       const uint32_t* tile_idx, uint32_t ntiles, uint8_t* tile_out, uint32_t* tile_len, hipStream_t s);
+void launch_fast_concat(const DeflateArgs& a, const uint32_t* tile0, const uint8_t* tile_out, const uint32_t* tile_len,
+                        const int32_t* cks, hipStream_t s);
 // incremental Deflater (k_deflate_stream): fresh state; one append (finish 0) / finish (1)
 void launch_deflate_reset(uint8_t* state, uint32_t n, hipStream_t s);
 void launch_deflate_stream(const DeflateArgs& a, uint32_t finish, hipStream_t s);

@@ -937,6 +937,72 @@ int sdz_deflate_append_batch_device(void* state, const uint8_t* in, const uint64
     return SDZ_API_OK;
 }
 
+// ---------------------------------------------------------- fast (not bit-exact) deflate
+
+uint64_t sdz_deflate_fast_bound(uint64_t in_len, int32_t format, uint32_t fname_len) {
+    const uint64_t tiles = (in_len + FT_TILE_BYTES - 1) / FT_TILE_BYTES;
+    return tiles * (FT_TILE_BYTES + 10) + 18 + fname_len + 1;
+}
+
+int sdz_deflate_fast_batch_device(const uint8_t* in, const uint64_t* in_off, const uint64_t* in_len,
+                                  uint8_t* out, const uint64_t* out_off, const uint64_t* out_cap,
+                                  sdz_deflate_record* rec, uint32_t n, int32_t format,
+                                  const uint8_t* fname, uint32_t fname_len, uint32_t mtime, void* stream) {
+    if (int rc = ensure_device()) return rc;
+    if (n == 0) return SDZ_API_OK;
+    if (format < SDZ_DEFLATE_RAW || format > SDZ_DEFLATE_GZIP)
+        return fail(SDZ_API_BAD_ARG, "container must be one of `raw`, `deflate`, `gzip`");
+    if (!in || !in_off || !in_len || !out || !out_off || !out_cap || !rec)
+        return fail(SDZ_API_BAD_ARG, "sdz_deflate_fast_batch_device: null pointer");
+    hipStream_t s = (hipStream_t)stream;
+    std::lock_guard<std::mutex> lk(g_mu);
+    // the tiles: which stream, which of its tiles (host plan from the input sizes)
+    std::vector<uint64_t> len(n);
+    HIPCHK(hipMemcpyAsync(len.data(), in_len, n * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    std::vector<uint32_t> tile0(n), ts, ti;
+    for (uint32_t i = 0; i < n; ++i) {
+        tile0[i] = (uint32_t)ts.size();
+        const uint64_t nt = (len[i] + FT_TILE_BYTES - 1) / FT_TILE_BYTES;
+        for (uint64_t k = 0; k < nt; ++k) { ts.push_back(i); ti.push_back((uint32_t)k); }
+    }
+    const uint32_t ntiles = (uint32_t)ts.size();
+    auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+    size_t o = 0;
+    const size_t o_tout = o; o = al(o + (size_t)ntiles * FT_TILE_OUT);
+    const size_t o_tlen = o; o = al(o + (size_t)ntiles * 4);
+    const size_t o_ts = o; o = al(o + (size_t)ntiles * 4);
+    const size_t o_ti = o; o = al(o + (size_t)ntiles * 4);
+    const size_t o_t0 = o; o = al(o + (size_t)n * 4);
+    const size_t o_ck = o; o = al(o + (size_t)n * 4);
+    void* base = nullptr;
+    PoolUse use(g_deflate_state, s);
+    if (int rc = use.get(o + fname_len + 64, &base)) return rc;
+    uint8_t* B = (uint8_t*)base;
+    uint8_t* d_fname = fname_len ? B + o : nullptr;
+    if (ntiles) {
+        HIPCHK(hipMemcpyAsync(B + o_ts, ts.data(), ntiles * 4, hipMemcpyHostToDevice, s));
+        HIPCHK(hipMemcpyAsync(B + o_ti, ti.data(), ntiles * 4, hipMemcpyHostToDevice, s));
+    }
+    HIPCHK(hipMemcpyAsync(B + o_t0, tile0.data(), n * 4, hipMemcpyHostToDevice, s));
+    if (fname_len) HIPCHK(hipMemcpyAsync(d_fname, fname, fname_len, hipMemcpyHostToDevice, s));
+    DeflateArgs a{};
+    a.in = in; a.in_off = in_off; a.in_len = in_len;
+    a.out = out; a.out_off = out_off; a.out_cap = out_cap;
+    a.rec = rec; a.n = n; a.level = 6; a.format = format;
+    a.fname = d_fname; a.fname_len = fname_len; a.mtime = mtime;
+    timing_begin(s);
+    launch_checksum(in, in_off, in_len, nullptr, (int32_t*)(B + o_ck), n, format == SDZ_DEFLATE_GZIP ? 1 : 0, s);
+    launch_fast_tiles(in, in_off, in_len, (const uint32_t*)(B + o_ts), (const uint32_t*)(B + o_ti), ntiles,
+                      B + o_tout, (uint32_t*)(B + o_tlen), s);
+    launch_fast_concat(a, (const uint32_t*)(B + o_t0), B + o_tout, (const uint32_t*)(B + o_tlen),
+                       (const int32_t*)(B + o_ck), s);
+    timing_end(s);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(s));                     // (the host plan vectors are copy sources)
+    return SDZ_API_OK;
+}
+
 // ----------------------------------------------------------------- one host Inflater
 
 }  // extern "C"

@@ -64,6 +64,7 @@ EXPORTS = [
     "sdz_inflater_create", "sdz_inflater_append", "sdz_inflater_destroy",
     "sdz_deflate_state_bytes", "sdz_deflate_append_bound", "sdz_deflate_state_reset_device",
     "sdz_deflate_append_batch_device", "sdz_deflater_create", "sdz_deflater_append", "sdz_deflater_destroy",
+    "sdz_deflate_fast_bound", "sdz_deflate_fast_batch_device",
 ]
 
 _lib = None
@@ -150,6 +151,11 @@ def lib():
                                           ctypes.POINTER(DeflateRecord)]
         L.sdz_deflater_append.restype = ctypes.c_int
         L.sdz_deflater_destroy.argtypes = [vp]
+    if hasattr(L, "sdz_deflate_fast_batch_device"):
+        L.sdz_deflate_fast_bound.argtypes = [ctypes.c_uint64, i32, u32]
+        L.sdz_deflate_fast_bound.restype = ctypes.c_uint64
+        L.sdz_deflate_fast_batch_device.argtypes = [vp, vp, vp, vp, vp, vp, vp, u32, i32, vp, u32, u32, vp]
+        L.sdz_deflate_fast_batch_device.restype = ctypes.c_int
     _lib = L
     return L
 
@@ -236,6 +242,42 @@ def deflate_batch(streams, level=6, format="deflate", file_name_latin1=b"", mtim
                                mtime & 0xFFFFFFFF, d, len(d) if d is not None else 0))
     return [{"status": STATUS.get(recs[i].status, recs[i].status), "checksum": recs[i].checksum,
              "data": bufs[i].raw[:recs[i].out_len]} for i in range(n)]
+
+
+def deflate_fast_batch(streams, format="deflate", file_name_latin1=b"", mtime=0):
+    """The opt-in fast compressor (sdz_deflate_fast_batch_device): valid streams, not the
+    reference's bytes.  Returns per stream {status, checksum, data}."""
+    L = lib()
+    n = len(streams)
+    streams = [bytes(s) for s in streams]
+    fmt = DEFLATE_FORMATS[format]
+    fn = bytes(file_name_latin1)
+    in_off, o = [], 0
+    for s in streams:
+        in_off.append(o)
+        o += (len(s) + 15) & ~15
+    caps = [int(L.sdz_deflate_fast_bound(len(s), fmt, len(fn))) for s in streams]
+    out_off, q = [], 0
+    for c in caps:
+        out_off.append(q)
+        q += (c + 255) & ~255
+    d_in, d_out = DeviceBuffer(o + 128), DeviceBuffer(q + 64)
+    if o:
+        d_in.upload(b"".join(s + b"\0" * (((len(s) + 15) & ~15) - len(s)) for s in streams))
+    meta = in_off + [len(s) for s in streams] + out_off + caps
+    d_meta = DeviceBuffer(8 * len(meta))
+    d_meta.upload(bytes(_u64_array(meta)))
+    d_rec = DeviceBuffer(ctypes.sizeof(DeflateRecord) * n)
+    m = d_meta.ptr
+    _check(L.sdz_deflate_fast_batch_device(d_in.ptr, m, m + 8 * n, d_out.ptr, m + 16 * n, m + 24 * n, d_rec.ptr, n,
+                                           fmt, fn or None, len(fn), mtime & 0xFFFFFFFF, None))
+    _check(L.sdz_sync(None))
+    recs = (DeflateRecord * n).from_buffer_copy(d_rec.download(n * ctypes.sizeof(DeflateRecord)))
+    res = [{"status": STATUS.get(r.status, r.status), "checksum": r.checksum,
+            "data": d_out.download(r.out_len, out_off[i]) if r.out_len else b""} for i, r in enumerate(recs)]
+    for b in (d_in, d_out, d_meta, d_rec):
+        b.free()
+    return res
 
 
 # --------------------------------------------------------------------- device-resident

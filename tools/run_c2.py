@@ -17,7 +17,7 @@ from bench import DeviceBatch, inflate_step, deflate_step, slice_offsets, fill_s
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--mode", default="inflate", choices=["inflate", "deflate", "distinct"])
+    ap.add_argument("--mode", default="inflate", choices=["inflate", "deflate", "distinct", "fast"])
     ap.add_argument("--same", action="store_true", help="deflate: one slice in every stream")
     ap.add_argument("--steps", type=int, default=2)
     ap.add_argument("--streams", type=int, default=65536)
@@ -49,6 +49,30 @@ def main():
         print("distinct inflate: kernel %.3f ms %s, %.1f GB/s out, parity %s"
               % (r["roofline"]["kernel_ms"], r["roofline"]["kernels_ms"],
                  r["config"]["bytes_out_per_gpu"] / r["roofline"]["kernel_ms"] / 1e6, r["parity"]), flush=True)
+    elif args.mode == "fast":
+        # the opt-in fast compressor on the C3 layout; validity checked with Python's zlib
+        import ctypes
+        import zlib
+        offs = slice_offsets(args.streams, len(text) - 65536)
+        b = DeviceBatch(sdz, text[:65536], args.streams, int(L.sdz_deflate_fast_bound(65536, 1, 0)))
+        fill_slices(sdz, b, text, offs, 65536)
+        for i in range(args.steps):
+            in_off, in_len, out_off, out_cap = b.ptrs()
+            rc = L.sdz_deflate_fast_batch_device(b.d_in.ptr, in_off, in_len, b.d_out.ptr, out_off, out_cap,
+                                                 b.d_rec.ptr, b.n, 1, None, 0, 0, None)
+            if rc:
+                raise RuntimeError(L.sdz_last_error().decode())
+            ms = L.sdz_last_kernel_ms()
+            recs = (sdz.DeflateRecord * args.streams).from_buffer_copy(
+                b.d_rec.download(args.streams * ctypes.sizeof(sdz.DeflateRecord)))
+            tot = sum(r.out_len for r in recs)
+            ok = all(r.status == 0 for r in recs)
+            for k in range(0, args.streams, max(1, args.streams // 64)):
+                data = b.d_out.download(recs[k].out_len, k * b.out_stride)
+                ok = ok and zlib.decompress(data) == text[offs[k]:offs[k] + 65536]
+            print("fast deflate step %d: kernel %.3f ms, %.2f GB/s in, %.2f GB/s out, ratio %.3f, valid %s"
+                  % (i, ms, 65536 * args.streams / ms / 1e6, tot / ms / 1e6, tot / (65536 * args.streams), ok),
+                  flush=True)
     else:
         # the bench's C3 layout: distinct slices of paradiselost.txt at xorshift64 offsets
         # (identical streams would run the serial parse without any lane divergence)
