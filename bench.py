@@ -180,6 +180,43 @@ def deflate_step(sdz, b, level, fmt):
     return sdz.lib().sdz_last_kernel_ms()
 
 
+def deflate_fast_leg(sdz, L, text, offs, slice_len, nd, steps, barrier, allmax, world, rank):
+    """The opt-in fast compressor (not bit-exact) on the C3 slices: valid
+    zlib streams (checked with Python's zlib on a sample), throughput and ratio."""
+    import zlib
+    bf = DeviceBatch(sdz, text[:slice_len], nd, int(L.sdz_deflate_fast_bound(slice_len, 1, 0)))
+    fill_slices(sdz, bf, text, offs, slice_len)
+
+    def step():
+        in_off, in_len, out_off, out_cap = bf.ptrs()
+        if L.sdz_deflate_fast_batch_device(bf.d_in.ptr, in_off, in_len, bf.d_out.ptr, out_off, out_cap,
+                                           bf.d_rec.ptr, nd, 1, None, 0, 0, None):
+            raise RuntimeError(L.sdz_last_error().decode())
+        return L.sdz_last_kernel_ms()
+    step()
+    L.sdz_sync(None)
+    barrier()
+    t0 = time.perf_counter()
+    ks = [step() for _ in range(steps)]
+    L.sdz_sync(None)
+    barrier()
+    wall = allmax(time.perf_counter() - t0) / steps
+    rec = (sdz.DeflateRecord * nd).from_buffer_copy(bf.d_rec.download(nd * ctypes.sizeof(sdz.DeflateRecord)))
+    total = sum(r.out_len for r in rec)
+    ok = all(r.status == 0 for r in rec)
+    if rank == 0:
+        for j in sorted({0, 1, nd // 3, nd // 2, nd - 1}):
+            ok = ok and zlib.decompress(bf.d_out.download(rec[j].out_len, j * bf.out_stride)) == \
+                text[offs[j]:offs[j] + slice_len]
+    bf.free()
+    return {"value": round(world * total / wall / 1e6, 2), "unit": "compressed MB/s",
+            "input_MBps": round(world * nd * slice_len / wall / 1e6, 2), "ratio": round(total / (nd * slice_len), 4),
+            "kernel_ms": round(sum(ks) / len(ks), 3), "ms_per_step": round(1000 * wall, 3),
+            "config": {"workload": "C3 slices, opt-in fast compressor (8 KiB tiles, greedy parse; NOT bit-exact)",
+                       "streams_per_gpu": nd, "slice_bytes": slice_len},
+            "valid": bool(ok), "bit_exact": False}
+
+
 def cpu_baseline_inflate(comp, seconds, threads):
     """Oracle (CPU restatement of the reference) inflating the same stream on host cores."""
     import oracle as O
@@ -216,6 +253,8 @@ def main():
     ap.add_argument("--deflate-streams", type=int, default=65536,
                     help="streams for the deflate leg (64 KiB slices, L6); 0 disables")
     ap.add_argument("--deflate-steps", type=int, default=1)
+    ap.add_argument("--fast-steps", type=int, default=2,
+                    help="steps of the opt-in fast (not bit-exact) compressor leg on the C3 slices (0: skip)")
     ap.add_argument("--distinct-steps", type=int, default=3,
                     help="steps of the distinct-stream inflate leg (the deflate leg's outputs); 0 disables")
     ap.add_argument("--copy-gib", type=float, default=4.0, help="device copy peak probe size; 0 disables")
@@ -337,6 +376,7 @@ def main():
     # the distinct-stream inflate leg (the north star's 64 Ki x 64 KiB dynamic-Huffman target)
     deflate = None
     distinct = None
+    fast = None
     if args.deflate_streams > 0:
         nd = args.deflate_streams
         slice_len = 65536
@@ -372,6 +412,8 @@ def main():
             distinct = inflate_distinct(sdz, L, bd, drec, text, offs, slice_len, args.distinct_steps,
                                         barrier, allmax, world)
         bd.free()
+        if args.fast_steps > 0 and hasattr(L, "sdz_deflate_fast_batch_device"):
+            fast = deflate_fast_leg(sdz, L, text, offs, slice_len, nd, args.fast_steps, barrier, allmax, world, rank)
 
     cpu = None
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
@@ -421,6 +463,7 @@ def main():
         "parity": bool(okall),
         "gather_ms": None if gather_ms is None else round(gather_ms, 3),
         "deflate": deflate,
+        "deflate_fast": fast,
         "inflate_distinct": distinct,
     }
     if rank == 0:

@@ -67,8 +67,8 @@ struct FtShared {
     uint32_t freq[286 + 30 + 19];
     uint16_t code[286 + 30 + 19];                         // bit-reversed canonical codes
     uint8_t clen[286 + 30 + 19];
-    uint32_t sortk[512];                                  // Huffman: (freq << 9 | sym) ascending, lit/len
-    uint32_t sortd[32];                                   // ... distance
+    uint32_t sortd[32];                                   // the code-length code: (freq << 9 | sym) ascending
+    uint32_t rstart[10];                                  // run starts of the code-length sequence
     uint32_t hq[320];                                     // two-queue Huffman: internal node weights
     uint16_t hpar[2 * 286];                               // parent links (leaf i, node 286 + j)
     uint8_t hdep[286], hndep[286];
@@ -78,7 +78,7 @@ struct FtShared {
     uint16_t newend[FT_THREADS];                          // end of the chain its word holds now
     uint16_t ent[FT_THREADS];                             // the entry that chain was parsed from
     uint32_t mism[FT_THREADS / 32];                       // segments whose chain may not be the true one
-    uint32_t bl[16];
+    uint32_t bl[16], blf[16];                             // code lengths: first / final counts per length
     uint32_t misc[12];                                    // 0 nrle, 1 header bits, 2 hlit, 3 hdist, 4 hclen, 5 stored?,
                                                           // 6 end bits, 7 bytes, 8 lit/len count, 9 matches, 10 data bits
 };
@@ -102,29 +102,6 @@ __device__ __forceinline__ uint32_t ft_match(const FtShared& S, uint32_t p, uint
     }
     if (l > lim) l = lim;
     return l >= 4 ? l : 0;
-}
-
-// All threads: the used symbols of freq[f0 .. f0 + ns) as (freq << 9 | sym), sorted ascending
-// into key[0 .. m) (bitonic, np = a power of two >= ns); returns m.
-__device__ uint32_t ft_sort(FtShared& S, uint32_t f0, uint32_t ns, uint32_t* key, uint32_t np) {
-    for (uint32_t k = threadIdx.x; k < np; k += FT_THREADS)
-        key[k] = k < ns && S.freq[f0 + k] ? (S.freq[f0 + k] << 9) | k : 0xffffffffu;
-    __syncthreads();
-    for (uint32_t size = 2; size <= np; size <<= 1)
-        for (uint32_t stride = size >> 1; stride > 0; stride >>= 1) {
-            for (uint32_t k = threadIdx.x; k < np; k += FT_THREADS) {
-                const uint32_t j = k ^ stride;
-                if (j > k) {
-                    const bool up = (k & size) == 0;
-                    const uint32_t x = key[k], y = key[j];
-                    if ((x > y) == up) { key[k] = y; key[j] = x; }
-                }
-            }
-            __syncthreads();
-        }
-    uint32_t m = 0;                                      // (every thread counts the same)
-    for (uint32_t k = 0; k < ns; ++k) m += key[k] != 0xffffffffu;
-    return m;
 }
 
 // One thread: Huffman code lengths, at most maxbits, for the m used symbols key[0 .. m)
@@ -175,40 +152,89 @@ __device__ void ft_lengths(FtShared& S, const uint32_t* key, uint32_t m, uint32_
     for (uint32_t i = 0; i < m; ++i) S.clen[f0 + (key[i] & 511u)] = S.hdep[i];
 }
 
-// All threads: literal/length or distance code lengths for the m used symbols key[0 .. m)
-// (ascending frequency, F = their total): l = ceil(log2(F / f)) keeps the Kraft sum <= 1
-// (2^-l <= f / F) and is <= 15 for F <= 2^15; the gap to exactly 1 -- a multiple of the
-// longest class's 2^-l -- is filled by moving symbols one class shorter, the shortest
-// classes first (largest steps), repeated until it closes; then the least frequent symbols
-// take the longest lengths.  Within a few percent of Huffman, and no serial tree walk.
-__device__ void ft_lengths_par(FtShared& S, const uint32_t* key, uint32_t m, uint32_t f0, uint32_t ns, uint32_t F) {
+// All threads: literal/length or distance code lengths for the used symbols of
+// freq[f0 .. f0 + ns) (F = their total), no sort: l = ceil(log2(F / f)) keeps the Kraft sum
+// <= 1 (2^-l <= f / F) and is <= 15 for F <= 2^15; the gap to exactly 1 -- a multiple of the
+// longest class's 2^-l -- is closed by moving symbols one class shorter, the shortest classes
+// first (largest steps), in closed form per class and pass.  Final lengths go out in order of
+// (first length, symbol): the first bl[1] symbols get 1 bit, and so on -- monotone in the
+// frequency up to ties within a class.  Within a few percent of Huffman.
+__device__ void ft_lengths_par(FtShared& S, uint32_t f0, uint32_t ns, uint32_t F) {
     const uint32_t tid = threadIdx.x;
-    for (uint32_t s = tid; s < ns; s += FT_THREADS) S.clen[f0 + s] = 0;
-    if (tid < 16) S.bl[tid] = 0;
+    if (tid < 16) S.bl[tid] = 0;                         // bl[0]: used symbols
     __syncthreads();
-    if (m >= 2)
-        for (uint32_t i = tid; i < m; i += FT_THREADS) {
-            const uint32_t f = key[i] >> 9, q = (F + f - 1) / f;
-            const uint32_t l = q <= 1 ? 1u : (32u - __builtin_clz(q - 1)) < 15u ? 32u - __builtin_clz(q - 1) : 15u;
+    for (uint32_t s = tid; s < ns; s += FT_THREADS) {
+        const uint32_t f = S.freq[f0 + s];
+        uint32_t l = 0;
+        if (f) {
+            const uint32_t q = (F + f - 1) / f;
+            l = q <= 1 ? 1u : 32u - __builtin_clz(q - 1);
+            l = l < 15u ? l : 15u;
             atomicAdd(&S.bl[l], 1u);
+            atomicAdd(&S.bl[0], 1u);
         }
-    __syncthreads();
-    if (tid == 0 && m >= 2) {
-        uint32_t K = 0;
-        for (uint32_t l = 1; l < 16; ++l) K += S.bl[l] << (15 - l);
-        uint32_t G = K < 32768u ? 32768u - K : 0u;
-        while (G)
-            for (uint32_t l = 2; l < 16 && G; ++l)
-                while (S.bl[l] && (1u << (15 - l)) <= G) { S.bl[l]--; S.bl[l - 1]++; G -= 1u << (15 - l); }
+        S.clen[f0 + s] = (uint8_t)l;                     // the first length
     }
     __syncthreads();
-    if (m >= 2)
-        for (uint32_t i = tid; i < m; i += FT_THREADS) {
-            uint32_t acc = 0, l = 15;
-            for (; l >= 1; --l) { acc += S.bl[l]; if (i < acc) break; }
-            S.clen[f0 + (key[i] & 511u)] = (uint8_t)l;
+    const uint32_t m = S.bl[0];
+    if (m <= 1) {                                        // one code (or none): two codes of length 1
+        if (tid == 0) {
+            uint32_t s1 = 0;
+            for (uint32_t s = 0; s < ns; ++s) if (S.clen[f0 + s]) s1 = s;
+            for (uint32_t s = 0; s < ns; ++s) S.clen[f0 + s] = 0;
+            S.clen[f0 + s1] = 1;
+            S.clen[f0 + (s1 ? 0 : 1)] = 1;
         }
-    else if (m == 1 && tid == 0) S.clen[f0 + (key[0] & 511u)] = 1;
+        __syncthreads();
+        return;
+    }
+    if (tid == 0) {
+        uint32_t b[16], K = 0;
+#pragma unroll
+        for (int l = 1; l < 16; ++l) { b[l] = S.bl[l]; K += b[l] << (15 - l); }
+        uint32_t G = K < 32768u ? 32768u - K : 0u;
+        while (G) {
+#pragma unroll
+            for (int l = 2; l < 16; ++l) {
+                const uint32_t step = 1u << (15 - l), k = b[l] < G / step ? b[l] : G / step;
+                b[l] -= k; b[l - 1] += k; G -= k * step;
+            }
+        }
+#pragma unroll
+        for (int l = 1; l < 16; ++l) S.blf[l] = b[l];    // final counts
+    }
+    __syncthreads();
+    if (tid < 64) {                                      // ranks by (first length, symbol); wave 0
+        const uint32_t lane = tid;
+        const uint64_t lt = (1ull << lane) - 1ull;
+        uint32_t off[16], cum[16];
+        uint32_t acc = 0, accf = 0;
+#pragma unroll
+        for (int l = 1; l < 16; ++l) { off[l] = acc; acc += S.bl[l]; accf += S.blf[l]; cum[l] = accf; }
+        uint32_t fin[5];
+#pragma unroll
+        for (uint32_t ci = 0; ci < 5; ++ci) {
+            const uint32_t c = 64 * ci;
+            const uint32_t l0 = c + lane < ns ? S.clen[f0 + c + lane] : 0u;
+            uint32_t r = 0;
+#pragma unroll
+            for (int L = 1; L < 16; ++L) {
+                const uint64_t mk = __ballot(l0 == (uint32_t)L);
+                if (l0 == (uint32_t)L) r = off[L] + (uint32_t)__popcll(mk & lt);
+                off[L] += (uint32_t)__popcll(mk);
+            }
+            uint32_t lf = 0;
+            if (l0) {
+                lf = 15;
+#pragma unroll
+                for (int L = 15; L >= 1; --L) if (r < cum[L]) lf = (uint32_t)L;
+            }
+            fin[ci] = lf;
+        }
+#pragma unroll
+        for (uint32_t ci = 0; ci < 5; ++ci)               // (all first lengths were read before)
+            if (64 * ci + lane < ns) S.clen[f0 + 64 * ci + lane] = (uint8_t)fin[ci];
+    }
     __syncthreads();
 }
 
@@ -246,6 +272,46 @@ __device__ void ft_codes_wave(FtShared& S, uint32_t f0, uint32_t ns) {
     }
 }
 
+// All threads: exclusive prefix sum of v over the block; *total = the sum
+__device__ __forceinline__ uint32_t ft_scan(FtShared& S, uint32_t v, uint32_t* total) {
+    const uint32_t tid = threadIdx.x;
+    uint32_t incl = v;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t x = __shfl_up(incl, d);
+        if ((tid & 63u) >= (uint32_t)d) incl += x;
+    }
+    __syncthreads();                                     // (segbits reuse)
+    if ((tid & 63u) == 63u) S.segbits[tid >> 6] = incl;
+    __syncthreads();
+    uint32_t base = 0, tot = 0;
+#pragma unroll
+    for (uint32_t w = 0; w < FT_THREADS / 64; ++w) {
+        const uint32_t x = S.segbits[w];
+        base += w < (tid >> 6) ? x : 0u;
+        tot += x;
+    }
+    *total = tot;
+    return base + incl - v;
+}
+
+// a run of r equal code lengths v as send_tree codes them (deflate.ts:378-429): the symbol
+// count, and (with out) the symbols (sym | extra << 5)
+__device__ __forceinline__ uint32_t ft_run(uint32_t v, uint32_t r, uint16_t* out) {
+    uint32_t c = 0, left = r;
+    if (v == 0) {
+        while (left >= 11) { const uint32_t k = left < 138 ? left : 138; if (out) out[c] = (uint16_t)(18 | ((k - 11) << 5)); ++c; left -= k; }
+        if (left >= 3) { if (out) out[c] = (uint16_t)(17 | ((left - 3) << 5)); ++c; left = 0; }
+    } else {
+        if (out) out[c] = (uint16_t)v;
+        ++c;
+        --left;
+        while (left >= 3) { const uint32_t k = left < 6 ? left : 6; if (out) out[c] = (uint16_t)(16 | ((k - 3) << 5)); ++c; left -= k; }
+    }
+    while (left) { if (out) out[c] = (uint16_t)v; ++c; --left; }
+    return c;
+}
+
 // clear the token-start bits of positions [a, b)
 __device__ __forceinline__ void ft_clear(FtShared& S, uint32_t a, uint32_t b) {
     while (a < b) {
@@ -267,6 +333,12 @@ __device__ __forceinline__ void ft_put(FtShared& S, uint32_t o, uint32_t v, uint
 
 // one tile: A.in stream tile_stream[t], its tile tile_idx[t]; output bytes to
 // tile_out + t * FT_TILE_OUT, length to tile_len[t]
+#ifdef FT_TIMING                                         // development aid: phase clocks of tile 0
+#define FT_STAMP(k) do { if (t == 0) { __syncthreads(); if (tid == 0) { const unsigned long long c_ = clock64(); \
+    ftc[k] = c_ - ftl; ftl = c_; } } } while (0)
+#else
+#define FT_STAMP(k) do {} while (0)
+#endif
 __global__ __launch_bounds__(FT_THREADS) void k_fast_tiles(const uint8_t* in, const uint64_t* in_off,
                                                            const uint64_t* in_len, const uint32_t* tile_stream,
                                                            const uint32_t* tile_idx, uint32_t ntiles,
@@ -274,6 +346,9 @@ __global__ __launch_bounds__(FT_THREADS) void k_fast_tiles(const uint8_t* in, co
     __shared__ FtShared S;
     const uint32_t t = blockIdx.x, tid = threadIdx.x;
     if (t >= ntiles) return;
+#ifdef FT_TIMING
+    unsigned long long ftc[12] = {0}, ftl = clock64();
+#endif
     const uint32_t sid = tile_stream[t];
     const uint64_t len = in_len[sid];
     const uint64_t t0 = (uint64_t)tile_idx[t] * FT_TILE;
@@ -292,6 +367,7 @@ __global__ __launch_bounds__(FT_THREADS) void k_fast_tiles(const uint8_t* in, co
     for (uint32_t k = tid; k < FT_TILE / 32; k += FT_THREADS) S.tbits[k] = 0;
     for (uint32_t k = tid; k < 286 + 30 + 19; k += FT_THREADS) S.freq[k] = 0;
     __syncthreads();
+    FT_STAMP(0);
     // 1. candidates, 256 positions at a time
     for (uint32_t c = 0; c < n; c += FT_THREADS) {
         const uint32_t p = c + tid;
@@ -302,6 +378,7 @@ __global__ __launch_bounds__(FT_THREADS) void k_fast_tiles(const uint8_t* in, co
         if (ok) atomicMax(&S.ht[h], p + 1);
         __syncthreads();
     }
+    FT_STAMP(1);
     // 2. speculative greedy parse of each segment from its start
     {
         const uint32_t s0 = tid * FT_SEG;
@@ -315,6 +392,7 @@ __global__ __launch_bounds__(FT_THREADS) void k_fast_tiles(const uint8_t* in, co
         S.segend[tid] = p;
     }
     __syncthreads();
+    FT_STAMP(2);
     // the true parse across segment boundaries.  A segment is one token-start word (32
     // positions).  In parallel, each segment re-parses from where its predecessor's
     // speculative parse ended (the true entry whenever the predecessor's own parse met its
@@ -410,12 +488,13 @@ __global__ __launch_bounds__(FT_THREADS) void k_fast_tiles(const uint8_t* in, co
     for (uint32_t k = tid; k < FT_OUT_WORDS; k += FT_THREADS) S.out[k] = 0;   // (the hash table is done)
     if (tid < 12) S.misc[tid] = 0;
     __syncthreads();
+    FT_STAMP(3);
     // 3. frequencies
     {
         const uint32_t s0 = tid * FT_SEG;
         uint32_t nt = 0, nm = 0;
-        for (uint32_t p = s0; p < s0 + FT_SEG && p < n; ++p) {
-            if (!ft_bit(S, p)) continue;
+        for (uint32_t tw = s0 < n ? S.tbits[tid] : 0u; tw; tw &= tw - 1) {   // the segment's token starts
+            const uint32_t p = s0 + __builtin_ctz(tw);
             ++nt;
             const uint32_t ml = S.mlen[p];
             if (ml == 0) atomicAdd(&S.freq[ft_byte(S, p)], 1u);
@@ -431,17 +510,10 @@ __global__ __launch_bounds__(FT_THREADS) void k_fast_tiles(const uint8_t* in, co
     }
     if (tid == 0) S.freq[256] = 1;                       // end of block
     __syncthreads();
-    const uint32_t ml_ll = ft_sort(S, 0, 286, S.sortk, 512);
-    const uint32_t ml_d = ft_sort(S, 286, 30, S.sortd, 32);
-    ft_lengths_par(S, S.sortk, ml_ll, 0, 286, S.misc[8] + 1);
-    if (ml_d >= 2) ft_lengths_par(S, S.sortd, ml_d, 286, 30, S.misc[9]);
-    else if (tid == 0) {                                 // none or one distance: two codes of length 1
-        const uint32_t d0 = ml_d ? S.sortd[0] & 511u : 0u;
-        for (uint32_t s = 0; s < 30; ++s) S.clen[286 + s] = 0;
-        S.clen[286 + d0] = 1;
-        S.clen[286 + (d0 ? 0 : 1)] = 1;
-    }
-    __syncthreads();
+    FT_STAMP(4);
+    ft_lengths_par(S, 0, 286, S.misc[8] + 1);
+    ft_lengths_par(S, 286, 30, S.misc[9] ? S.misc[9] : 1);
+    FT_STAMP(5);
     // the data bits (the symbols with their extra bits), in parallel
     for (uint32_t sy = tid; sy < 316; sy += FT_THREADS) {
         const uint32_t f = S.freq[sy];
@@ -451,92 +523,129 @@ __global__ __launch_bounds__(FT_THREADS) void k_fast_tiles(const uint8_t* in, co
         else eb = sy - 286 < 4 ? 0 : (sy - 286) / 2 - 1;
         atomicAdd(&S.misc[10], f * (S.clen[sy] + eb));
     }
-    if (tid == 0) {
-        uint32_t hlit = 286, hdist = 30;
-        while (hlit > 257 && !S.clen[hlit - 1]) --hlit;
-        while (hdist > 1 && !S.clen[286 + hdist - 1]) --hdist;
-        // the code-length sequence, run-length coded (deflate.ts:378-429 send_tree's rules)
-        uint32_t nr = 0;
-        const uint32_t tot = hlit + hdist;
-        auto L = [&](uint32_t i) -> uint32_t { return i < hlit ? S.clen[i] : S.clen[286 + i - hlit]; };
-        for (uint32_t i = 0; i < tot;) {
-            const uint32_t v = L(i);
-            uint32_t r = 1;
-            while (i + r < tot && L(i + r) == v) ++r;
-            uint32_t left = r;
-            if (v == 0) {
-                while (left >= 11) { const uint32_t k = left < 138 ? left : 138; S.rle[nr++] = (uint16_t)(18 | ((k - 11) << 5)); left -= k; }
-                if (left >= 3) { S.rle[nr++] = (uint16_t)(17 | ((left - 3) << 5)); left = 0; }
-                while (left) { S.rle[nr++] = 0; --left; }
-            } else {
-                S.rle[nr++] = (uint16_t)v;
-                --left;
-                while (left >= 3) { const uint32_t k = left < 6 ? left : 6; S.rle[nr++] = (uint16_t)(16 | ((k - 3) << 5)); left -= k; }
-                while (left) { S.rle[nr++] = (uint16_t)v; --left; }
+    // HLIT / HDIST: the last used code of each set
+    if (tid < 2) S.misc[2 + tid] = 0;
+    __syncthreads();
+    for (uint32_t sy = tid; sy < 316; sy += FT_THREADS)
+        if (S.clen[sy]) atomicMax(&S.misc[sy < 286 ? 2 : 3], sy < 286 ? sy + 1 : sy - 285);
+    for (uint32_t k = tid; k < 19; k += FT_THREADS) S.freq[316 + k] = 0;
+    if (tid < 10) S.rstart[tid] = 0;
+    __syncthreads();
+    const uint32_t hlit = S.misc[2] > 257 ? S.misc[2] : 257, hdist = S.misc[3] > 1 ? S.misc[3] : 1;
+    const uint32_t tot = hlit + hdist;
+    auto cl = [&](uint32_t i) -> uint32_t { return i < hlit ? S.clen[i] : S.clen[286 + i - hlit]; };
+    // the code-length sequence, run-length coded: runs start where a length changes; each
+    // run's symbols go to a prefix-summed place (two positions per thread)
+    uint32_t rv[2] = {0, 0}, rr[2] = {0, 0}, rc[2] = {0, 0};
+    bool st[2] = {false, false};
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        const uint32_t i = 2 * tid + j;
+        st[j] = i < tot && (i == 0 || cl(i) != cl(i - 1));
+        if (st[j]) atomicOr(&S.rstart[i >> 5], 1u << (i & 31u));
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        if (!st[j]) continue;
+        const uint32_t i = 2 * tid + j;
+        uint32_t nx = tot;                               // the next run's start
+        for (uint32_t w = (i + 1) >> 5; w < 10 && (w << 5) < tot; ++w) {
+            const uint32_t mk = S.rstart[w] & (w == ((i + 1) >> 5) ? ~0u << ((i + 1) & 31u) : ~0u);
+            if (mk) { nx = (w << 5) + __builtin_ctz(mk); break; }
+        }
+        const uint32_t v = cl(i), r = (nx < tot ? nx : tot) - i;
+        rv[j] = v; rr[j] = r; rc[j] = ft_run(v, r, nullptr);
+    }
+    uint32_t nr;
+    const uint32_t rbase = ft_scan(S, rc[0] + rc[1], &nr);
+    if (rc[0]) ft_run(rv[0], rr[0], S.rle + rbase);
+    if (rc[1]) ft_run(rv[1], rr[1], S.rle + rbase + rc[0]);
+    __syncthreads();
+    for (uint32_t k = tid; k < nr; k += FT_THREADS) atomicAdd(&S.freq[316 + (S.rle[k] & 31u)], 1u);
+    __syncthreads();
+    if (tid < 19) {                                      // the code-length code's used symbols, ranked
+        const uint32_t f = S.freq[316 + tid];
+        if (f) {
+            const uint32_t v = (f << 9) | tid;
+            uint32_t rk = 0;
+            for (uint32_t k = 0; k < 19; ++k) {
+                const uint32_t g = S.freq[316 + k];
+                rk += g && ((g << 9) | k) < v;
             }
-            i += r;
+            S.sortd[rk] = v;
         }
-        for (uint32_t k = 0; k < 19; ++k) S.freq[316 + k] = 0;
-        for (uint32_t k = 0; k < nr; ++k) S.freq[316 + (S.rle[k] & 31u)]++;
-        uint32_t mb = 0;                                 // 19 keys: insertion sort
-        for (uint32_t k = 0; k < 19; ++k) {
-            if (!S.freq[316 + k]) continue;
-            const uint32_t v = (S.freq[316 + k] << 9) | k;
-            uint32_t j = mb++;
-            while (j > 0 && S.sortd[j - 1] > v) { S.sortd[j] = S.sortd[j - 1]; --j; }
-            S.sortd[j] = v;
-        }
+    }
+    __syncthreads();
+    if (tid == 0) {                                      // the code-length code (19 symbols, <= 7 bits)
+        uint32_t mb = 0;
+        for (uint32_t k = 0; k < 19; ++k) mb += S.freq[316 + k] != 0;
         ft_lengths(S, S.sortd, mb, 316, 19, 7);
         uint32_t nb = 0, b0 = 0;
         for (uint32_t sy = 0; sy < 19; ++sy) if (S.clen[316 + sy]) { ++nb; b0 = sy; }
         if (nb == 1) S.clen[316 + (b0 ? 0 : 1)] = 1;     // (complete: two codes of length 1)
         uint32_t hclen = 19;
         while (hclen > 4 && !S.clen[316 + c_ft_border[hclen - 1]]) --hclen;
-        S.misc[0] = nr; S.misc[2] = hlit; S.misc[3] = hdist; S.misc[4] = hclen;
+        S.misc[0] = nr; S.misc[4] = hclen;
     }
     __syncthreads();
+    FT_STAMP(6);
     if (tid < 64) {
         ft_codes_wave(S, 0, 286);
         ft_codes_wave(S, 286, 30);
         ft_codes_wave(S, 316, 19);
     }
     __syncthreads();
-    if (tid == 0) {
-        const uint32_t nr = S.misc[0], hlit = S.misc[2], hdist = S.misc[3], hclen = S.misc[4];
-        // sizes: the dynamic block against a stored one
-        uint64_t bits = 3 + 14 + 3 * hclen + (uint64_t)S.misc[10];
-        for (uint32_t k = 0; k < nr; ++k) {
+    // the block header: 17 fixed bits, HCLEN + 4 3-bit lengths, then the run-length symbols at
+    // prefix-summed offsets (two per thread)
+    const uint32_t hclen = S.misc[4];
+    const uint32_t h0 = 17 + 3 * hclen;
+    uint32_t hb[2] = {0, 0};
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        const uint32_t k = 2 * tid + j;
+        if (k < nr) {
             const uint32_t sy = S.rle[k] & 31u;
-            bits += S.clen[316 + sy] + (sy == 16 ? 2 : sy == 17 ? 3 : sy == 18 ? 7 : 0);
+            hb[j] = S.clen[316 + sy] + (sy == 16 ? 2 : sy == 17 ? 3 : sy == 18 ? 7 : 0);
         }
-        const bool stored = bits + 7 >= 8ull * (n + 5);
-        S.misc[5] = stored;
-        // the block header
-        uint32_t o = 0;
-        if (!stored) {
+    }
+    uint32_t hbits;
+    const uint32_t hbase = ft_scan(S, hb[0] + hb[1], &hbits);
+    const uint64_t bits = (uint64_t)h0 + hbits + S.misc[10];
+    const bool stored_blk = bits + 7 >= 8ull * (n + 5);
+    if (!stored_blk) {
+        if (tid == 0) {
+            uint32_t o = 0;
             ft_put(S, o, last ? 5u : 4u, 3); o += 3;      // BFINAL, BTYPE = 2
             ft_put(S, o, hlit - 257, 5); o += 5;
             ft_put(S, o, hdist - 1, 5); o += 5;
             ft_put(S, o, hclen - 4, 4); o += 4;
             for (uint32_t k = 0; k < hclen; ++k) { ft_put(S, o, S.clen[316 + c_ft_border[k]], 3); o += 3; }
-            for (uint32_t k = 0; k < nr; ++k) {
+        }
+        uint32_t o = h0 + hbase;
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const uint32_t k = 2 * tid + j;
+            if (k < nr) {
                 const uint32_t sy = S.rle[k] & 31u, ex = S.rle[k] >> 5;
-                ft_put(S, o, S.code[316 + sy], S.clen[316 + sy]); o += S.clen[316 + sy];
+                ft_put(S, o, S.code[316 + sy], S.clen[316 + sy]);
                 const uint32_t eb = sy == 16 ? 2 : sy == 17 ? 3 : sy == 18 ? 7 : 0;
-                ft_put(S, o, ex, eb); o += eb;
+                ft_put(S, o + S.clen[316 + sy], ex, eb);
+                o += hb[j];
             }
         }
-        S.misc[1] = o;
     }
+    if (tid == 0) { S.misc[5] = stored_blk; S.misc[1] = h0 + hbits; }
     __syncthreads();
+    FT_STAMP(7);
     const bool stored = S.misc[5] != 0;
     uint32_t total_bytes;
     if (!stored) {
         // 4. each thread's bits, a block scan, then the tokens at their offsets
         const uint32_t s0 = tid * FT_SEG;
         uint32_t mine = 0;
-        for (uint32_t p = s0; p < s0 + FT_SEG && p < n; ++p) {
-            if (!ft_bit(S, p)) continue;
+        for (uint32_t tw = s0 < n ? S.tbits[tid] : 0u; tw; tw &= tw - 1) {   // the segment's token starts
+            const uint32_t p = s0 + __builtin_ctz(tw);
             const uint32_t ml = S.mlen[p];
             if (ml == 0) { mine += S.clen[ft_byte(S, p)]; continue; }
             uint32_t eb, ev, db, dv;
@@ -556,22 +665,37 @@ __global__ __launch_bounds__(FT_THREADS) void k_fast_tiles(const uint8_t* in, co
         for (uint32_t w = 0; w < (tid >> 6); ++w) base += S.segbits[w];
         if (tid == FT_THREADS - 1) S.misc[6] = base + incl;   // end of the data bits
         __syncthreads();
-        uint32_t o = base + incl - mine;
-        for (uint32_t p = s0; p < s0 + FT_SEG && p < n; ++p) {
-            if (!ft_bit(S, p)) continue;
+        // this thread's bits [o, o + mine): gathered in a register, whole words stored; the
+        // first and last words are shared with the neighbours (atomic OR)
+        const uint32_t o0 = base + incl - mine;
+        uint32_t w = o0 >> 5, na = o0 & 31u;
+        uint64_t acc = 0;
+        bool first = true;
+        auto put = [&](uint32_t v, uint32_t nb) {
+            acc |= (uint64_t)v << na;
+            na += nb;
+            if (na >= 32) {
+                if (first) { atomicOr(&S.out[w], (uint32_t)acc); first = false; }
+                else S.out[w] = (uint32_t)acc;
+                ++w;
+                acc >>= 32;
+                na -= 32;
+            }
+        };
+        for (uint32_t tw = s0 < n ? S.tbits[tid] : 0u; tw; tw &= tw - 1) {   // the segment's token starts
+            const uint32_t p = s0 + __builtin_ctz(tw);
             const uint32_t ml = S.mlen[p];
             if (ml == 0) {
                 const uint32_t b = ft_byte(S, p);
-                ft_put(S, o, S.code[b], S.clen[b]); o += S.clen[b];
+                put(S.code[b], S.clen[b]);
                 continue;
             }
             uint32_t eb, ev, db, dv;
             const uint32_t lc = ft_lcode(ml + 3u, eb, ev), dc = ft_dcode(p - S.cand[p], db, dv);
-            ft_put(S, o, S.code[lc], S.clen[lc]); o += S.clen[lc];
-            ft_put(S, o, ev, eb); o += eb;
-            ft_put(S, o, S.code[286 + dc], S.clen[286 + dc]); o += S.clen[286 + dc];
-            ft_put(S, o, dv, db); o += db;
+            put(S.code[lc] | (ev << S.clen[lc]), S.clen[lc] + eb);                  // <= 20 bits
+            put(S.code[286 + dc] | (dv << S.clen[286 + dc]), S.clen[286 + dc] + db);  // <= 28 bits
         }
+        if (na) atomicOr(&S.out[w], (uint32_t)acc);
         __syncthreads();
         if (tid == 0) {
             uint32_t e = S.misc[6];
@@ -599,10 +723,17 @@ __global__ __launch_bounds__(FT_THREADS) void k_fast_tiles(const uint8_t* in, co
         for (uint32_t k = tid; k < n; k += FT_THREADS) o8[5 + k] = (uint8_t)ft_byte(S, k);
         __syncthreads();
     }
+    FT_STAMP(8);
     uint8_t* dst = tile_out + (uint64_t)t * FT_TILE_OUT;
     const uint8_t* o8 = (const uint8_t*)S.out;
     for (uint32_t k = tid; k < total_bytes; k += FT_THREADS) dst[k] = o8[k];
     if (tid == 0) tile_len[t] = total_bytes;
+#ifdef FT_TIMING
+    FT_STAMP(9);
+    if (t == 0 && tid == 0)
+        printf("ft phases: load %llu cand %llu parse %llu fix %llu freq %llu lens %llu rle %llu codes+hdr %llu enc %llu out %llu\n",
+               ftc[0], ftc[1], ftc[2], ftc[3], ftc[4], ftc[5], ftc[6], ftc[7], ftc[8], ftc[9]);
+#endif
 }
 
 // per stream: header (sd-deflate.ts:98-152), the tiles' bytes in order, trailer (154-165)
