@@ -201,3 +201,24 @@ def test_stored_block_defect_a9():
     comp = c.compress(small) + c.flush()
     r = O.inflater_run([comp])
     assert r["success"] and r["data"] == small
+
+
+def test_deflater_per_call_outputs(paradise):
+    """oracle_deflater_run_parts: the per-call outputs of the reference Deflater concatenate to
+    the one-shot stream, empty appends return nothing, and the first append carries the
+    header (the GPU incremental Deflater is checked against these, tests/test_gpu_deflate_stream.py)."""
+    rng = random.Random(12)
+    for fmt in ("deflate", "gzip", "raw"):
+        for level in (1, 6, 9):
+            cuts = sorted(rng.sample(range(1, len(paradise)), 9))
+            parts = [paradise[a:b] for a, b in zip([0] + cuts, cuts + [len(paradise)])]
+            parts.insert(2, b"")
+            outs = O.deflater_parts(parts, level=level, format=fmt, mtime=3)
+            assert len(outs) == len(parts) + 1
+            assert b"".join(outs) == O.deflate(paradise, level=level, format=fmt, mtime=3)
+            assert outs[2] == b""
+            if fmt == "deflate":
+                assert outs[0][:2] == b"\x78\x01"
+            if fmt == "gzip":
+                assert outs[0][:2] == b"\x1f\x8b"
+            assert zlib.decompress(b"".join(outs), {"deflate": 15, "gzip": 31, "raw": -15}[fmt]) == paradise
