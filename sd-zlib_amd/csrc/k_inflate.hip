@@ -1122,7 +1122,8 @@ uint64_t inflate_rsave_bytes() { return sizeof(RSave); }
 
 // host driver: rounds of (decode, resolve) until no stream needs another round.
 // kernel_ms (optional, 3 entries) accumulates decode / resolve / finalize times.
-int run_inflate_rounds(const InflateArgs& a, hipStream_t s, uint32_t* host_active, float* kernel_ms) {
+int run_inflate_rounds(const InflateArgs& a, hipStream_t s, uint32_t* host_active, float* kernel_ms,
+                       int (*hook)(void*), void* hook_ctx) {
     if (a.n == 0) return 0;
     uint32_t spb = resolve_streams_per_block();
     dim3 g1((a.n + IL_STREAMS - 1) / IL_STREAMS), g2((a.n + spb - 1) / spb);
@@ -1136,6 +1137,9 @@ int run_inflate_rounds(const InflateArgs& a, hipStream_t s, uint32_t* host_activ
         if (hipMemsetAsync(a.active, 0, sizeof(uint32_t), s) != hipSuccess) { rc = -1; break; }
         if (kernel_ms) (void)hipEventRecord(ev[0], s);
         hipLaunchKernelGGL(k_inflate_decode, g1, dim3(IL_THREADS), 0, s, a, round);
+        if (round == 0 && hook) {
+            if (int hr = hook(hook_ctx)) { rc = hr; break; }
+        }
         if (a.split_plan) {                              // the split streams (k_split.hip)
             if (round == 0) {
                 // segments decoded on the side stream meanwhile: chain them, decode the

@@ -60,7 +60,10 @@ struct InflateArgs {
 
 uint64_t inflate_dsave_bytes();  // per stream decode state
 uint64_t inflate_rsave_bytes();  // per stream resolve state
-int run_inflate_rounds(const InflateArgs& a, hipStream_t s, uint32_t* host_active, float* kernel_ms);
+// hook (optional): called once on the host right after the first round's decode is queued
+// (the split pre-pass's second half); a nonzero return ends the rounds with that code
+int run_inflate_rounds(const InflateArgs& a, hipStream_t s, uint32_t* host_active, float* kernel_ms,
+                       int (*hook)(void*) = nullptr, void* hook_ctx = nullptr);
 // incremental mode: fresh state / stage carry + chunk contiguously (k_istream.hip)
 void launch_istate_reset(uint8_t* dsave, uint8_t* rsave, uint32_t n, hipStream_t s);
 // block-parallel decode of long streams (k_split.hip)

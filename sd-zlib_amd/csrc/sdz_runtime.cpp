@@ -292,7 +292,8 @@ int inflate_scratch(InflateArgs& a, uint32_t n, bool own_state, size_t extra, hi
     return SDZ_API_OK;
 }
 
-int inflate_run(InflateArgs& a, hipStream_t s, bool timing_started = false) {
+int inflate_run(InflateArgs& a, hipStream_t s, bool timing_started = false, int (*hook)(void*) = nullptr,
+                void* hook_ctx = nullptr) {
     static thread_local uint32_t host_active = 0;
     a.dbg = nullptr;
     const bool phases = getenv("SDZ_PHASE_TIMING") != nullptr;   // development aid
@@ -301,8 +302,8 @@ int inflate_run(InflateArgs& a, hipStream_t s, bool timing_started = false) {
         HIPCHK(hipMemsetAsync(a.dbg, 0, 64 * sizeof(unsigned long long), s));
     }
     if (!timing_started) timing_begin(s);
-    if (run_inflate_rounds(a, s, &host_active, g_timing ? g_breakdown : nullptr))
-        return hip_fail(hipGetLastError(), "inflate rounds");
+    if (int rc = run_inflate_rounds(a, s, &host_active, g_timing ? g_breakdown : nullptr, hook, hook_ctx))
+        return rc > 0 ? rc : hip_fail(hipGetLastError(), "inflate rounds");
     timing_end(s);
     if (phases) {
         unsigned long long h[64];
@@ -324,10 +325,6 @@ int inflate_run(InflateArgs& a, hipStream_t s, bool timing_started = false) {
 // SDZ_SPLIT_MIN) chosen by split_threshold's cost model; SDZ_SPLIT_SHARE=x forces t = x times
 // the batch's bytes per decoder lane, SDZ_SPLIT=0 turns splitting off.  Returns 0 with
 // plan.nsplit == 0 when nothing is split.
-struct SplitHost {
-    SplitPlan plan{};
-    uint32_t* split_state = nullptr;
-};
 // per device: the side stream the segments decode on (overlapping the first round's decode
 // of the other streams) and its completion event
 struct SideStream { hipStream_t s = nullptr; hipEvent_t ev = nullptr; };
@@ -373,7 +370,28 @@ uint64_t split_threshold(std::vector<uint64_t> len, uint64_t split_min) {
     return thr;
 }
 
-int inflate_split_plan(InflateArgs& a, hipStream_t s, PoolUse& use, SplitHost& H, float* ms) {
+// What the split pre-pass keeps between its two halves (inflate_split_start before the
+// first round, inflate_split_finish from inside it, run_inflate_rounds' hook).
+struct SplitHost {
+    SplitPlan plan{};
+    uint32_t* split_state = nullptr;
+    InflateArgs a{};                                     // the call's arguments (input, scratch)
+    hipStream_t s = nullptr;
+    SideStream* side = nullptr;
+    std::vector<SplitInfo> sp;
+    uint64_t lanes = 0;
+    uint32_t ns = 0, scap = 0;
+    size_t cand_bytes = 0;
+    SplitInfo* d_sp1 = nullptr;
+    uint64_t *d_cand1 = nullptr, *d_surv = nullptr;
+    uint32_t *d_nsurv = nullptr, *d_npacked = nullptr;
+    PoolUse* seg_use = nullptr;                          // the segments' pool (used on the side stream)
+};
+
+// Half 1, before the first round: which streams split (their split_state PENDING, so the
+// first round's decode skips them), and the finder launched on the side stream -- it runs
+// while the first round decodes the other streams.  SDZ_SPLIT=0 turns splitting off.
+int inflate_split_start(const InflateArgs& a, hipStream_t s, PoolUse& find_use, SplitHost& H) {
     const uint32_t n = a.n;
     if (const char* e = getenv("SDZ_SPLIT")) if (atoi(e) == 0) return SDZ_API_OK;
     uint64_t split_min = 16 << 10;
@@ -390,72 +408,93 @@ int inflate_split_plan(InflateArgs& a, hipStream_t s, PoolUse& use, SplitHost& H
         thr = split_threshold(len, split_min);
     }
     if (getenv("SDZ_SPLIT_DEBUG")) fprintf(stderr, "sdz split: threshold %llu\n", (unsigned long long)thr);
-    std::vector<SplitInfo> sp;
-    uint64_t lanes = 0;
+    H.sp.clear();
+    H.lanes = 0;
     for (uint32_t i = 0; i < n; ++i) {
         if (len[i] < thr || len[i] > (1ull << 32)) continue;
         SplitInfo x{};
         x.sid = i;
         x.nbits = len[i] * 8;
-        x.lane0 = lanes;
-        lanes += (x.nbits + 31) / 32;
-        sp.push_back(x);
+        x.lane0 = H.lanes;
+        H.lanes += (x.nbits + 31) / 32;
+        H.sp.push_back(x);
     }
-    if (sp.empty()) return SDZ_API_OK;
-    hipEvent_t e0 = nullptr, e1 = nullptr;
-    if (ms) { (void)hipEventCreate(&e0); (void)hipEventCreate(&e1); (void)hipEventRecord(e0, s); }
-    const uint32_t ns = (uint32_t)sp.size();
-    // phase 1: candidates, in their own pool (this call's only), then packed for the host
-    // (filter survivors: ~0.1 % of positions on zlib output; room for 0.2 %, and a stream's
-    // candidates beyond that are only lost parallelism: its segments get longer)
-    const size_t cand_bytes = (size_t)ns * SP_CAND_MAX * sizeof(uint64_t);
-    const uint32_t scap = (uint32_t)std::min<uint64_t>(1u << 30, std::max<uint64_t>(SPLIT_FILTER_BLOCKS * 16,
-                                                                                 lanes * 32 / 512));
-    const size_t b1 = ns * sizeof(SplitInfo) + cand_bytes + (size_t)scap * sizeof(uint64_t) +
-                      SPLIT_FILTER_BLOCKS * sizeof(uint32_t) + 256;
-    PoolUse find_use(g_find, s);
+    if (H.sp.empty()) return SDZ_API_OK;
+    const uint32_t ns = (uint32_t)H.sp.size();
+    H.ns = ns;
+    H.a = a;
+    H.s = s;
+    // the finder's scratch (filter survivors: ~0.1 % of positions on zlib output; room for
+    // 0.2 %, and a stream's candidates beyond that are only lost parallelism) and the
+    // per-stream split_state
+    H.cand_bytes = (size_t)ns * SP_CAND_MAX * sizeof(uint64_t);
+    H.scap = (uint32_t)std::min<uint64_t>(1u << 30, std::max<uint64_t>(SPLIT_FILTER_BLOCKS * 16, H.lanes * 32 / 512));
+    const size_t b1 = ns * sizeof(SplitInfo) + H.cand_bytes + (size_t)H.scap * sizeof(uint64_t) +
+                      SPLIT_FILTER_BLOCKS * sizeof(uint32_t) + 256 + (size_t)n * sizeof(uint32_t);
     void* p1 = nullptr;
     if (int rc = find_use.get(b1, &p1)) return rc;
     uint8_t* d1 = (uint8_t*)p1;
-    SplitInfo* d_sp1 = (SplitInfo*)d1;
-    uint64_t* d_cand1 = (uint64_t*)(d1 + ns * sizeof(SplitInfo));
-    uint64_t* d_surv = d_cand1 + (size_t)ns * SP_CAND_MAX;
-    uint32_t* d_nsurv = (uint32_t*)(d_surv + scap);
-    uint32_t* d_npacked = d_nsurv + SPLIT_FILTER_BLOCKS;
-    HIPCHK(hipMemcpyAsync(d_sp1, sp.data(), ns * sizeof(SplitInfo), hipMemcpyHostToDevice, s));
-    HIPCHK(hipMemsetAsync(d_nsurv, 0, SPLIT_FILTER_BLOCKS * sizeof(uint32_t), s));
-    launch_split_find(a.in, a.in_off, d_sp1, ns, d_cand1, lanes, d_surv, d_nsurv, scap, s);
+    H.d_sp1 = (SplitInfo*)d1;
+    H.d_cand1 = (uint64_t*)(d1 + ns * sizeof(SplitInfo));
+    H.d_surv = H.d_cand1 + (size_t)ns * SP_CAND_MAX;
+    H.d_nsurv = (uint32_t*)(H.d_surv + H.scap);
+    H.d_npacked = H.d_nsurv + SPLIT_FILTER_BLOCKS;
+    H.split_state = H.d_npacked + 64;
+    {
+        std::vector<uint32_t> st(n, 0u);
+        for (const SplitInfo& x : H.sp) st[x.sid] = SPS_PENDING;
+        HIPCHK(hipMemcpyAsync(H.split_state, st.data(), n * sizeof(uint32_t), hipMemcpyHostToDevice, s));
+        HIPCHK(hipMemcpyAsync(H.d_sp1, H.sp.data(), ns * sizeof(SplitInfo), hipMemcpyHostToDevice, s));
+        HIPCHK(hipMemsetAsync(H.d_nsurv, 0, SPLIT_FILTER_BLOCKS * sizeof(uint32_t), s));
+        HIPCHK(hipStreamSynchronize(s));                 // (host vectors are copy sources)
+    }
+    if (int rc = side_stream(&H.side)) return rc;
+    HIPCHK(hipEventRecord(H.side->ev, s));               // (the side stream sees the copies above)
+    HIPCHK(hipStreamWaitEvent(H.side->s, H.side->ev, 0));
+    launch_split_find(a.in, a.in_off, H.d_sp1, ns, H.d_cand1, H.lanes, H.d_surv, H.d_nsurv, H.scap, H.side->s);
     // (every candidate was a survivor: the survivor list's room holds the packed candidates)
-    launch_split_pack(d_sp1, ns, d_cand1, d_surv, d_npacked, s);
+    launch_split_pack(H.d_sp1, ns, H.d_cand1, H.d_surv, H.d_npacked, H.side->s);
     HIPCHK(hipGetLastError());
+    H.plan.nsplit = ns;
+    return SDZ_API_OK;
+}
+
+// Half 2, from run_inflate_rounds right after the first round's decode is queued: the
+// candidates come back (the host waits on the side stream only), the segments are planned
+// -- the stream's start, then one per candidate; token capacity from the bits to the next
+// candidate (1 token per 6 bits; a segment that fills up sends its stream to the serial
+// path) -- and decoded on the side stream, one lane each, in one round; plan.ready marks
+// their end (run_inflate_rounds waits for it before chaining).
+int inflate_split_finish(void* ctx) {
+    SplitHost& H = *(SplitHost*)ctx;
+    const uint32_t ns = H.ns;
+    hipStream_t ss = H.side->s;
     uint32_t npacked = 0;
-    HIPCHK(hipMemcpyAsync(sp.data(), d_sp1, ns * sizeof(SplitInfo), hipMemcpyDeviceToHost, s));
-    HIPCHK(hipMemcpyAsync(&npacked, d_npacked, sizeof npacked, hipMemcpyDeviceToHost, s));
-    HIPCHK(hipStreamSynchronize(s));
+    HIPCHK(hipMemcpyAsync(H.sp.data(), H.d_sp1, ns * sizeof(SplitInfo), hipMemcpyDeviceToHost, ss));
+    HIPCHK(hipMemcpyAsync(&npacked, H.d_npacked, sizeof npacked, hipMemcpyDeviceToHost, ss));
+    HIPCHK(hipStreamSynchronize(ss));
     std::vector<uint64_t> packed(npacked);
     if (npacked) {
-        HIPCHK(hipMemcpyAsync(packed.data(), d_surv, npacked * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
-        HIPCHK(hipStreamSynchronize(s));
+        HIPCHK(hipMemcpyAsync(packed.data(), H.d_surv, npacked * sizeof(uint64_t), hipMemcpyDeviceToHost, ss));
+        HIPCHK(hipStreamSynchronize(ss));
     }
     if (getenv("SDZ_SPLIT_DEBUG")) {
         std::vector<uint32_t> nsv(SPLIT_FILTER_BLOCKS);
-        HIPCHK(hipMemcpy(nsv.data(), d_nsurv, nsv.size() * sizeof(uint32_t), hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpyAsync(nsv.data(), H.d_nsurv, nsv.size() * sizeof(uint32_t), hipMemcpyDeviceToHost, ss));
+        HIPCHK(hipStreamSynchronize(ss));
         uint64_t tsv = 0, tc = 0, over = 0, full = 0;
-        for (uint32_t x : nsv) { tsv += x; full += x == scap / SPLIT_FILTER_BLOCKS; }
-        for (const SplitInfo& x : sp) { tc += x.ncand; over += x.ncand > SP_CAND_MAX; }
+        for (uint32_t x : nsv) { tsv += x; full += x == H.scap / SPLIT_FILTER_BLOCKS; }
+        for (const SplitInfo& x : H.sp) { tc += x.ncand; over += x.ncand > SP_CAND_MAX; }
         fprintf(stderr, "sdz split: %u streams, %llu bits, %llu survivors (%llu full regions of %u), "
-                "%llu candidates, %llu streams over the cap\n", ns, (unsigned long long)(lanes * 32),
-                (unsigned long long)tsv, (unsigned long long)full, scap / SPLIT_FILTER_BLOCKS,
+                "%llu candidates, %llu streams over the cap\n", ns, (unsigned long long)(H.lanes * 32),
+                (unsigned long long)tsv, (unsigned long long)full, H.scap / SPLIT_FILTER_BLOCKS,
                 (unsigned long long)tc, (unsigned long long)over);
     }
-    // phase 2: segments -- the stream's start, then one per candidate; token capacity from
-    // the bits to the next candidate (1 token per 6 bits; a segment that fills up sends its
-    // stream to the serial path)
     std::vector<SegInfo> seg;
     uint64_t tok = 0;
     uint32_t chain = 0;
     for (uint32_t k = 0; k < ns; ++k) {
-        SplitInfo& x = sp[k];
+        SplitInfo& x = H.sp[k];
         const uint32_t nc = std::min<uint32_t>(x.ncand, SP_CAND_MAX);
         const uint64_t* c = packed.data() + x.cand0;
         x.skip0 = nc && c[0] == 0 ? 1 : 0;
@@ -484,18 +523,16 @@ int inflate_split_plan(InflateArgs& a, hipStream_t s, PoolUse& use, SplitHost& H
     size_t o = 0;
     const size_t o_sp = o; o = al(o + ns * sizeof(SplitInfo));
     const size_t o_seg = o; o = al(o + nseg * sizeof(SegInfo));
-    const size_t o_cand = o; o = al(o + cand_bytes);
+    const size_t o_cand = o; o = al(o + H.cand_bytes);
     const size_t o_chain = o; o = al(o + chain * sizeof(uint32_t));
     const size_t o_ctok = o; o = al(o + chain * sizeof(uint64_t));
-    const size_t o_state = o; o = al(o + n * sizeof(uint32_t));
     const size_t o_segD = o; o = al(o + nseg * dsb);
     const size_t o_lens = o; o = al(o + nseg * kInflateScratchPerStream);
     const size_t o_nt = o; o = al(o + (2 * (size_t)nseg + 1) * sizeof(uint32_t));
     const size_t o_tok = o; o = al(o + tok * sizeof(uint32_t));
     void* base = nullptr;
-    if (int rc = use.get(o, &base)) return rc;
+    if (int rc = H.seg_use->get(o, &base)) return rc;   // (ordered on the side stream)
     uint8_t* B = (uint8_t*)base;
-    H.plan.nsplit = ns;
     H.plan.nseg = nseg;
     H.plan.sp = (SplitInfo*)(B + o_sp);
     H.plan.seg = (SegInfo*)(B + o_seg);
@@ -503,24 +540,11 @@ int inflate_split_plan(InflateArgs& a, hipStream_t s, PoolUse& use, SplitHost& H
     H.plan.chain = (uint32_t*)(B + o_chain);
     H.plan.chain_tok = (uint64_t*)(B + o_ctok);
     H.plan.segtok = (uint32_t*)(B + o_tok);
-    H.split_state = (uint32_t*)(B + o_state);
-    HIPCHK(hipMemcpyAsync(H.plan.sp, sp.data(), ns * sizeof(SplitInfo), hipMemcpyHostToDevice, s));
-    HIPCHK(hipMemcpyAsync(H.plan.seg, seg.data(), nseg * sizeof(SegInfo), hipMemcpyHostToDevice, s));
-    HIPCHK(hipMemcpyAsync(H.plan.cand, d_cand1, cand_bytes, hipMemcpyDeviceToDevice, s));
-    {
-        std::vector<uint32_t> st(n, 0u);
-        for (const SplitInfo& x : sp) st[x.sid] = SPS_PENDING;
-        HIPCHK(hipMemcpyAsync(H.split_state, st.data(), n * sizeof(uint32_t), hipMemcpyHostToDevice, s));
-        HIPCHK(hipStreamSynchronize(s));                 // (st is a local)
-    }
-    // phase 3: every segment decoded, one lane each, in one round, on the side stream: the
-    // first round's decode of the other streams runs meanwhile (run_inflate_rounds waits
-    // for plan.ready before chaining them)
-    SideStream* side = nullptr;
-    if (int rc = side_stream(&side)) return rc;
-    HIPCHK(hipEventRecord(side->ev, s));
-    HIPCHK(hipStreamWaitEvent(side->s, side->ev, 0));
-    InflateArgs g = a;
+    HIPCHK(hipMemcpyAsync(H.plan.sp, H.sp.data(), ns * sizeof(SplitInfo), hipMemcpyHostToDevice, ss));
+    HIPCHK(hipMemcpyAsync(H.plan.seg, seg.data(), nseg * sizeof(SegInfo), hipMemcpyHostToDevice, ss));
+    HIPCHK(hipMemcpyAsync(H.plan.cand, H.d_cand1, H.cand_bytes, hipMemcpyDeviceToDevice, ss));
+    HIPCHK(hipStreamSynchronize(ss));                    // (host vectors are copy sources)
+    InflateArgs g = H.a;
     g.n = nseg;
     g.dsave = B + o_segD;
     g.scratch = B + o_lens;
@@ -534,21 +558,11 @@ int inflate_split_plan(InflateArgs& a, hipStream_t s, PoolUse& use, SplitHost& H
     g.spinfo = H.plan.sp;
     g.cand = H.plan.cand;
     g.segtok = H.plan.segtok;
-    launch_seg_decode(g, side->s);
+    launch_seg_decode(g, ss);
     HIPCHK(hipGetLastError());
-    HIPCHK(hipEventRecord(side->ev, side->s));
+    HIPCHK(hipEventRecord(H.side->ev, ss));
     H.plan.segD = g.dsave;
-    H.plan.ready = (void*)side->ev;
-    if (ms) {
-        (void)hipEventRecord(e1, s);
-        (void)hipEventSynchronize(e1);
-        float t = 0.f;
-        (void)hipEventElapsedTime(&t, e0, e1);
-        *ms = t;
-        (void)hipEventDestroy(e0);
-        (void)hipEventDestroy(e1);
-    }
-    HIPCHK(hipStreamSynchronize(s));                     // (the host vectors above are copy sources)
+    H.plan.ready = (void*)H.side->ev;
     return SDZ_API_OK;
 }
 
@@ -594,15 +608,22 @@ int sdz_inflate_batch_device(const uint8_t* in, const uint64_t* in_off, const ui
     a.n = n; a.format = format;
     a.streaming = 0; a.window = nullptr; a.carry = nullptr;
     a.split_plan = nullptr; a.split_state = nullptr; a.segmode = 0;
-    PoolUse split_use(g_split, s);
+    PoolUse find_use(g_find, s);
     SplitHost sh;
-    float split_ms = 0.f;
-    if (int rc = inflate_split_plan(a, s, split_use, sh, g_timing ? &split_ms : nullptr)) return rc;
+    if (int rc = inflate_split_start(a, s, find_use, sh)) return rc;
+    // the segments' pool is used on the side stream (its reuse waits there)
+    PoolUse split_use(g_split, sh.side ? sh.side->s : s);
+    sh.seg_use = &split_use;
     if (sh.plan.nsplit) { a.split_plan = &sh.plan; a.split_state = sh.split_state; }
-    int rc = inflate_run(a, s);
-    // (every exit: the pools' next user waits for the side stream's segment decode too)
-    if (sh.plan.nsplit) (void)hipStreamWaitEvent(s, (hipEvent_t)sh.plan.ready, 0);
-    if (g_timing) { g_breakdown[0] += split_ms; g_extra_ms = split_ms; }   // the pre-pass counts as decode
+    int rc = inflate_run(a, s, false, sh.plan.nsplit ? inflate_split_finish : nullptr, &sh);
+    if (sh.plan.nsplit) {
+        // every exit: the main stream waits for the side stream's work, and the side stream
+        // (where the segments' pool is released) for the main stream's rounds
+        (void)hipEventRecord(sh.side->ev, sh.side->s);
+        (void)hipStreamWaitEvent(s, sh.side->ev, 0);
+        (void)hipEventRecord(sh.side->ev, s);
+        (void)hipStreamWaitEvent(sh.side->s, sh.side->ev, 0);
+    }
     return rc;
 }
 
