@@ -1007,6 +1007,12 @@ __device__ __forceinline__ void epochs(const InflateArgs& A, DSave* S, const uin
                                        uint64_t cap, uint32_t* tb, uint32_t tcap, uint8_t* lens, bool live,
                                        SegStop G) {
     const uint64_t tbits = ilen * 8;
+#ifdef SDZ_TIMING
+    // development: wave clocks of the cold (block-level) and hot (symbol) parts, waves of the
+    // first 8 workgroups (dbg[8..11]: cold cycles, hot cycles, cold runs, hot epochs)
+    const bool timed = A.dbg && blockIdx.x < 8 && (threadIdx.x & 63u) == 0;
+    unsigned long long tc = 0, th = 0, nc = 0, nh = 0, t0 = timed ? clock64() : 0;
+#endif
     for (;;) {
         bool hot = live && can_hot<MODE>(S, tbits, cap);
         bool cold = live && !S->full && S->mode != LM_DONE && !hot && (MODE == 0 || !S->stall);
@@ -1015,12 +1021,21 @@ __device__ __forceinline__ void epochs(const InflateArgs& A, DSave* S, const uin
                 cold_run<MODE>(S, inp, ilen, cap, tb, tcap, lens, A.format, A.dict != nullptr, A.dict_adler,
                                MODE == 1 && S->mode == LM_INIT ? 1u : 0u, G);
             hot = live && can_hot<MODE>(S, tbits, cap);
+#ifdef SDZ_TIMING
+            if (timed) { const unsigned long long t = clock64(); tc += t - t0; t0 = t; ++nc; }
+#endif
         }
         uint64_t hm = __ballot(hot);
         if (hm == 0) break;
         int nhot = __popcll(hm);
         hot_epoch<MODE == 1>(S, inp, ilen, cap, tb, tcap, hot, nhot - (nhot >= 16 ? nhot >> IL_STOP_SHIFT : 1));
+#ifdef SDZ_TIMING
+        if (timed) { const unsigned long long t = clock64(); th += t - t0; t0 = t; ++nh; }
+#endif
     }
+#ifdef SDZ_TIMING
+    if (timed) { atomicAdd(&A.dbg[8], tc); atomicAdd(&A.dbg[9], th); atomicAdd(&A.dbg[10], nc); atomicAdd(&A.dbg[11], nh); }
+#endif
 }
 
 // One lane per stream; in segment mode (A.segmode, k_split.hip) one lane per segment of a

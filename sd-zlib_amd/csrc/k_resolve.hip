@@ -394,6 +394,15 @@ __global__ __launch_bounds__(RS_THREADS) __attribute__((amdgpu_waves_per_eu(RS_W
         // a stream's first round without a dictionary: zeros
         for (uint32_t k = tid; k < RS_WIN / 16; k += RS_THREADS)
             ((uint4*)(ring + (RS_R - RS_WIN)))[k] = make_uint4(0, 0, 0, 0);
+    } else if (round && pos0 >= RS_WIN) {
+        // a later round: the 32 KiB before pos0 from the output, 4 loads in flight per thread
+        for (uint32_t k = 4 * tid; k < RS_WIN; k += 4 * RS_THREADS) {
+            const uint8_t* q = out + pos0 - RS_WIN + k;
+            const uint32_t b0 = q[0], b1 = q[1], b2 = q[2], b3 = q[3];
+            const int32_t r = (int32_t)rp0 - RS_WIN + (int32_t)k;
+            ring[ridx(r)] = (uint8_t)b0; ring[ridx(r + 1)] = (uint8_t)b1;
+            ring[ridx(r + 2)] = (uint8_t)b2; ring[ridx(r + 3)] = (uint8_t)b3;
+        }
     } else {
         for (uint32_t k = tid; k < RS_WIN; k += RS_THREADS) {
             const int64_t p = (int64_t)pos0 - RS_WIN + k;
