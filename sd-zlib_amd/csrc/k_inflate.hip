@@ -24,6 +24,7 @@
 // input (infcodes.ts:368-387), huft_build's MANY=1400 table budget, incomplete
 // single-code trees, the gzip FEXTRA mode that never advances (inflate.ts:343-345).
 #include "inflate_state.h"
+#include <type_traits>
 
 namespace sdz {
 
@@ -40,6 +41,9 @@ namespace sdz {
 #endif
 #define IL_THREADS (IL_STREAMS * 64 / IL_WAVE_LANES)
 #define IL_TSTAGE 32                  // tokens staged in LDS per stream (one 128 B line)
+#ifndef IL_UNIFORM_FLUSH
+#define IL_UNIFORM_FLUSH 1            // the symbol loop writes staged tokens at its ring step
+#endif
 #define IL_TSTRIDE 136                // LDS bytes per stream for the token stage (8-aligned)
 #define IL_BAD_IDX 300                // rank selected by codes past lim[15]
 
@@ -92,6 +96,7 @@ struct Hot : Core {
     uint32_t rpos, wpos;              // ring bytes consumed / committed (mod 2^32)
     uint4 s0, s1;                     // loads in flight, committed at the next group
     uint32_t ns;
+    uint32_t nfl;                     // tokens in HBM (IL_UNIFORM_FLUSH: a multiple of 16)
     g_uint4* vp;                      // next 16 input bytes to load
     g_uint4* vend;                    // first 16-byte chunk past the input
     uint32_t* ring;
@@ -159,6 +164,7 @@ __device__ __forceinline__ void br_refill(Hot& L) {
     L.bo &= 31u;
     L.nx = L.ring[(L.rpos >> 2) & 15u];
 }
+__device__ __forceinline__ void tok_flush_hot(Hot& L);
 // the wave-uniform ring step (see struct Hot); keeps >= 24 bytes in the ring,
 // enough for the 4 iterations of up to 48 bits each that follow
 __device__ __forceinline__ void ring_step(Hot& L) {
@@ -175,6 +181,7 @@ __device__ __forceinline__ void ring_step(Hot& L) {
         }
         L.ns = 0;
     }
+    tok_flush_hot(L);
     uint32_t lvl = L.wpos - L.rpos;
     if (lvl <= 48 && L.vp < L.vend) {
         L.s0 = *L.vp++;
@@ -417,26 +424,53 @@ __device__ __forceinline__ void tok_flush_stage(Core& L) {
 #pragma unroll
     for (int k = 0; k < IL_TSTAGE / 4; ++k) d[k] = make_uint4(v[2 * k].x, v[2 * k].y, v[2 * k + 1].x, v[2 * k + 1].y);
 }
-__device__ __forceinline__ void tok_push(Core& L, uint32_t t) {
+// The stage is a ring of the last 32 tokens.  The cold code flushes each 32-token line as it
+// fills; the symbol loop (IL_UNIFORM_FLUSH) only stages, and writes 16-token chunks at its
+// wave-uniform ring step (tok_flush_hot): a push site then has no flush branch, which some
+// lane of a wave of distinct streams took at nearly every step.
+template <class C>
+__device__ __forceinline__ void tok_push(C& L, uint32_t t) {
     uint32_t k = L.ntok & (IL_TSTAGE - 1);
     L.ts[k] = t;
     L.ntok++;
-    if (k == IL_TSTAGE - 1) tok_flush_stage(L);
+    if constexpr (!(IL_UNIFORM_FLUSH && std::is_same<C, Hot>::value))
+        if (k == IL_TSTAGE - 1) tok_flush_stage(L);
 }
-__device__ __forceinline__ void tok_flush_lits(Core& L) {
+template <class C>
+__device__ __forceinline__ void tok_flush_lits(C& L) {
     if (L.nlit) {
         tok_push(L, ((L.nlit - 1u) << 24) | L.litw);
         L.nlit = 0;
         L.litw = 0;
     }
 }
-__device__ __forceinline__ void tok_lit(Core& L, uint32_t b) {
+template <class C>
+__device__ __forceinline__ void tok_lit(C& L, uint32_t b) {
     L.litw |= b << (8 * L.nlit);
     if (++L.nlit == 3) tok_flush_lits(L);
 }
-__device__ __forceinline__ void tok_match(Core& L, uint32_t len, uint32_t dist) {
+template <class C>
+__device__ __forceinline__ void tok_match(C& L, uint32_t len, uint32_t dist) {
     tok_flush_lits(L);
     tok_push(L, 0x80000000u | ((len - 3u) << 16) | (dist - 1u));
+}
+// symbol loop: the next 16 staged tokens to HBM once there are (at most 2 tokens per step,
+// 4 steps between calls: at most 23 unwritten, within the 32-token ring)
+__device__ __forceinline__ void tok_flush_hot(Hot& L) {
+    if (!IL_UNIFORM_FLUSH) return;
+    const bool f = L.ntok - L.nfl >= 16u;
+    if (__ballot(f)) {
+        if (f) {
+            const uint2* st = (const uint2*)(L.ts + (L.nfl & (IL_TSTAGE - 1)));
+            GLB uint4* d = (GLB uint4*)(L.tb + L.nfl);
+            uint2 v[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) v[k] = st[k];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) d[k] = make_uint4(v[2 * k].x, v[2 * k].y, v[2 * k + 1].x, v[2 * k + 1].y);
+            L.nfl += 16u;
+        }
+    }
 }
 __device__ __forceinline__ void tok_finish(Core& L) {
     tok_flush_lits(L);
@@ -953,6 +987,7 @@ __device__ __forceinline__ void hot_load(Hot& H, HTree& LL, HTree& DD, const DSa
     H.room = H.room0 = (uint32_t)(r > 0x7fffffffull ? 0x7fffffffull : r);
     H.mode = S->mode; H.last = S->last; H.status = S->status; H.zmsg = S->zmsg;
     H.ntok = S->ntok; H.litw = S->litw; H.nlit = S->nlit; H.full = S->full != 0;
+    H.nfl = H.ntok & ~(IL_TSTAGE - 1u);                   // (the stage holds the open line)
     LL = (const HTree&)S->LL;
     DD = (const HTree&)S->DD;
 }
@@ -986,7 +1021,7 @@ __device__ __noinline__ void hot_epoch(DSave* S, const uint8_t* inp, uint64_t il
     Hot H;
     HTree LL, DD;
     const uint8_t* region = lane_region();
-    H.mode = LM_DONE; H.full = true; H.ntok = 0; H.tcap = tcap; H.tb = tb; H.ts = lane_stage();
+    H.mode = LM_DONE; H.full = true; H.ntok = 0; H.nfl = 0; H.tcap = tcap; H.tb = tb; H.ts = lane_stage();
     H.avail = 0; H.bo = 0;
     if (hot) hot_load(H, LL, DD, S, inp, ilen, cap);
     do {
@@ -999,6 +1034,9 @@ __device__ __noinline__ void hot_epoch(DSave* S, const uint8_t* inp, uint64_t il
             }
         }
     } while (__popcll(__ballot(hot_ready<STREAM>(H))) > stop);
+    // back to the cold code's invariant: everything below the open 32-token line in HBM
+    // (nfl >= ntok - 15 after this, and a multiple of 16)
+    tok_flush_hot(H);
     if (hot) hot_save(H, S);
 }
 
