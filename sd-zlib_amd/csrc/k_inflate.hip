@@ -444,15 +444,37 @@ __device__ __forceinline__ void tok_flush_lits(C& L) {
         L.litw = 0;
     }
 }
+#ifndef IL_BF_TOKENS
+#define IL_BF_TOKENS 1
+#endif
 template <class C>
 __device__ __forceinline__ void tok_lit(C& L, uint32_t b) {
     L.litw |= b << (8 * L.nlit);
-    if (++L.nlit == 3) tok_flush_lits(L);
+    if constexpr (IL_BF_TOKENS && IL_UNIFORM_FLUSH && std::is_same<C, Hot>::value) {
+        // symbol loop: no branch -- a store that does not push goes to the stage's spare slot
+        const bool full = ++L.nlit == 3;
+        L.ts[full ? (L.ntok & (IL_TSTAGE - 1)) : IL_TSTAGE] = (2u << 24) | L.litw;
+        L.ntok += full ? 1u : 0u;
+        L.litw = full ? 0u : L.litw;
+        L.nlit = full ? 0u : L.nlit;
+    } else {
+        if (++L.nlit == 3) tok_flush_lits(L);
+    }
 }
 template <class C>
 __device__ __forceinline__ void tok_match(C& L, uint32_t len, uint32_t dist) {
-    tok_flush_lits(L);
-    tok_push(L, 0x80000000u | ((len - 3u) << 16) | (dist - 1u));
+    if constexpr (IL_BF_TOKENS && IL_UNIFORM_FLUSH && std::is_same<C, Hot>::value) {
+        const bool hl = L.nlit != 0;
+        L.ts[hl ? (L.ntok & (IL_TSTAGE - 1)) : IL_TSTAGE] = ((L.nlit - 1u) << 24) | L.litw;
+        L.ntok += hl ? 1u : 0u;
+        L.ts[L.ntok & (IL_TSTAGE - 1)] = 0x80000000u | ((len - 3u) << 16) | (dist - 1u);
+        L.ntok++;
+        L.nlit = 0;
+        L.litw = 0;
+    } else {
+        tok_flush_lits(L);
+        tok_push(L, 0x80000000u | ((len - 3u) << 16) | (dist - 1u));
+    }
 }
 // symbol loop: the next 16 staged tokens to HBM once there are (at most 2 tokens per step,
 // 4 steps between calls: at most 23 unwritten, within the 32-token ring)
