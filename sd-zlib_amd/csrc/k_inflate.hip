@@ -739,10 +739,13 @@ __device__ __forceinline__ void block_step(Lane& L, Tree& LL, Tree& DD, uint8_t*
 }
 
 // length symbol (1..29 = sym - 256) -> base length and extra bits (infcodes.ts:27-35)
+// (selects only: a nested conditional here compiled to an exec-mask branch)
 __device__ __forceinline__ uint32_t len_base(uint32_t li, uint32_t& e) {
-    uint32_t k = li - 1u;                                 // 0..28
-    e = (k < 8u || k == 28u) ? 0u : (k - 4u) >> 2;
-    return k < 8u ? k + 3u : k == 28u ? 258u : ((4u + (k & 3u)) << e) + 3u;
+    const uint32_t k = li - 1u;                           // 0..28
+    e = k - 8u < 20u ? (k - 4u) >> 2 : 0u;                // 8..27: 1..5
+    const uint32_t sh = ((4u + (k & 3u)) << e) + 3u;      // (k = 4..7, e = 0: k + 3)
+    const uint32_t b = k < 4u ? k + 3u : sh;
+    return k == 28u ? 258u : b;
 }
 // distance symbol 0..29 -> base distance and extra bits (infcodes.ts:37-46)
 __device__ __forceinline__ uint32_t dist_base(uint32_t ds, uint32_t& e) {
@@ -1023,7 +1026,9 @@ __device__ __forceinline__ void hot_save(const Hot& H, DSave* S) {
 // bound applies to incremental streams only (STREAM: 258 bytes), which must stop at a
 // symbol's start when out_cap is reached; a one-shot stream (or segment) keeps the last
 // symbols of an exactly sized output slot in the hot loop, whose own room check ends it
-// OUT_OVERFLOW.
+// OUT_OVERFLOW.  (Leaving those symbols to the cold code too, so that the loop needs no room
+// checks, was measured: the extra cold epoch at every stream's end cost 3 ms of the
+// distinct streams' 14.)
 template <bool STREAM>
 __device__ __forceinline__ bool hot_ready(const Hot& H) {
     return H.mode == LM_CODES && !H.full && br_avail(H) >= 64 && (!STREAM || H.room >= 258);

@@ -510,3 +510,26 @@ def test_concurrent_streams_do_not_share_scratch(paradise):
                 assert b.output(i, recs[i].out_len) == exp_inf[k][i]
     for s in streams:
         assert L.sdz_stream_destroy(s) == 0
+
+
+def test_output_slot_edges():
+    """Output slots at and just below the decoded size: a slot too small ends OUT_OVERFLOW at
+    the first symbol that does not fit (whole symbols only: the record's bytes are a prefix
+    of the data, within one match of the slot's end); an exact slot succeeds."""
+    rng = random.Random(21)
+    plain = [text_corpus(rng, rng.randint(3000, 40000)) for _ in range(12)]
+    streams, caps, want = [], [], []
+    for p in plain:
+        s = zlib.compress(p, 6)
+        for k in (0, 1, 2, 3, 100, 257, 258, 259, 1000):
+            streams.append(s)
+            caps.append(len(p) - k)
+            want.append(p)
+    gpu = sdz.inflate_batch(streams, caps, sdz.FMT_AUTO)
+    for g, cap, p in zip(gpu, caps, want):
+        if cap == len(p):
+            assert g["success"] and g["data"] == p
+        else:
+            assert g["status"] == "OUT_OVERFLOW" and not g["success"], g["status"]
+            n = g["out_len"]
+            assert cap - 258 < n <= cap and g["data"][:n] == p[:n]
