@@ -217,6 +217,76 @@ def deflate_fast_leg(sdz, L, text, offs, slice_len, nd, steps, barrier, allmax, 
             "valid": bool(ok), "bit_exact": False}
 
 
+def mixed_leg(sdz, L, steps, scale, barrier, allmax, world, rank):
+    """BASELINE configs[3] (C4) shape across the ranks: 262,144 streams of 4 KiB - 16 MiB
+    (log-uniform, raw/zlib/gzip, compressible text) LPT-sharded over the node's 8 GPUs
+    (sdz_dist.lpt_shard); rank r decodes every `scale`-th stream of shard r (weak scaling:
+    at 8 ranks, 1/scale of the node's batch).  Streams are device copies of a pool of 36
+    distinct payloads (12 size buckets x 3 formats), as in tools/run_configs.py."""
+    import importlib.util
+    import math
+    import random
+    import sdz_dist
+    spec = importlib.util.spec_from_file_location("run_configs", os.path.join(ROOT, "tools", "run_configs.py"))
+    rc = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(rc)
+    lo, hi = math.log(4096), math.log(16 << 20)
+    edges = [int(math.exp(lo + (hi - lo) * (k + 0.5) / 12)) for k in range(12)]
+    rng = random.Random(0x5D5A1B1E)
+    step = (hi - lo) / 12                                  # a size's bucket: the nearest edge (log scale)
+    bucket = [min(11, int((rng.uniform(lo, hi) - lo) / step)) for _ in range(262144)]
+    shards = sdz_dist.lpt_shard([edges[k] for k in bucket], 8)
+    prng = random.Random(0x5D5A1B1F)
+    pool, plain = [], []
+    for k, sz in enumerate(edges):                         # pool index 3 k + format
+        for fmt in range(3):
+            data = rc.text(prng, sz)
+            plain.append(data)
+            pool.append(rc.compress(data, fmt))
+    picks = [[3 * bucket[i] + i % 3 for i in shards[r % 8][::scale]] for r in range(world)]
+    pick = picks[rank]
+    caps = [len(plain[j]) + 64 for j in pick]
+    slots = rc.Slots(pool, pick, caps)
+
+    def step():
+        a, b, c, d = slots.ptrs()
+        if L.sdz_inflate_batch_device(slots.d_in.ptr, a, b, slots.d_out.ptr, c, d, slots.d_rec.ptr, slots.n,
+                                      sdz.FMT_AUTO, None, 0, None):
+            raise RuntimeError(L.sdz_last_error().decode())
+        return L.sdz_last_kernel_ms()
+    step()
+    L.sdz_sync(None)
+    barrier()
+    t0 = time.perf_counter()
+    ks = [step() for _ in range(steps)]
+    L.sdz_sync(None)
+    barrier()
+    wall = allmax(time.perf_counter() - t0) / steps
+    recs = slots.records(sdz.InflateRecord)
+    ok = all(recs[i].status == 0 and recs[i].success and recs[i].out_len == len(plain[j]) and
+             (recs[i].checksum_verdict == 1 or j % 3 == 0) for i, j in enumerate(pick))
+    seen = set()
+    for i, j in enumerate(pick):                          # one stream per pool payload byte-compared
+        if j not in seen:
+            seen.add(j)
+            ok = ok and slots.d_out.download(len(plain[j]), slots.out_off[i]) == plain[j]
+    in_bytes = slots.in_bytes
+    slots.free()
+    ok = allmax(0.0 if ok else 1.0) == 0.0
+    total_out = sum(len(plain[j]) for pk in picks for j in pk)
+    total_in = sum(len(pool[j]) for pk in picks for j in pk)
+    kms = sum(ks) / len(ks)
+    return {"value": round(total_out / wall / 1e6, 2), "unit": "MB/s", "ms_per_step": round(1000 * wall, 3),
+            "kernel_ms": round(kms, 3),
+            "roofline": {"bound": "hbm", "achieved": round((in_bytes + sum(len(plain[j]) for j in pick)) / kms / 1e6, 2),
+                         "peak": 8000.0, "unit": "GB/s"},
+            "config": {"workload": "C4 shape: 262,144 streams of 4 KiB-16 MiB (raw/zlib/gzip) LPT-sharded over 8 "
+                                   "GPUs; each rank decodes every %dth stream of its shard" % scale,
+                       "streams_per_gpu": len(pick), "bytes_out_all_ranks": total_out, "bytes_in_all_ranks": total_in,
+                       "largest_stream_out": max(len(plain[j]) for j in pick)},
+            "parity": bool(ok)}
+
+
 def cpu_baseline_inflate(comp, seconds, threads):
     """Oracle (CPU restatement of the reference) inflating the same stream on host cores."""
     import oracle as O
@@ -257,6 +327,10 @@ def main():
                     help="steps of the opt-in fast (not bit-exact) compressor leg on the C3 slices (0: skip)")
     ap.add_argument("--distinct-steps", type=int, default=3,
                     help="steps of the distinct-stream inflate leg (the deflate leg's outputs); 0 disables")
+    ap.add_argument("--mixed-steps", type=int, default=2,
+                    help="steps of the C4-shaped mixed-size leg (LPT shards of 262,144 streams; 0: skip)")
+    ap.add_argument("--mixed-scale", type=int, default=8,
+                    help="the mixed leg decodes every Nth stream of the rank's LPT shard (1: the full shard)")
     ap.add_argument("--copy-gib", type=float, default=4.0, help="device copy peak probe size; 0 disables")
     ap.add_argument("--host-streams", type=int, default=0,
                     help="streams for the host-buffer (PCIe-inclusive) inflate probe, e.g. 2048; off by "
@@ -415,6 +489,10 @@ def main():
         if args.fast_steps > 0 and hasattr(L, "sdz_deflate_fast_batch_device"):
             fast = deflate_fast_leg(sdz, L, text, offs, slice_len, nd, args.fast_steps, barrier, allmax, world, rank)
 
+    mixed = None
+    if args.mixed_steps > 0:
+        mixed = mixed_leg(sdz, L, args.mixed_steps, args.mixed_scale, barrier, allmax, world, rank)
+
     cpu = None
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
         threads = max(1, min(16, os.cpu_count() or 1))
@@ -465,6 +543,7 @@ def main():
         "deflate": deflate,
         "deflate_fast": fast,
         "inflate_distinct": distinct,
+        "mixed": mixed,
     }
     if rank == 0:
         print(json.dumps(line), flush=True)
