@@ -1867,18 +1867,34 @@ int device_max_u64(const uint64_t* v, uint32_t n, unsigned long long* d_slot, ui
 
 static bool c_config_host_fast(int level) { return level >= 1 && level <= 3; }
 
-void launch_deflate(const DeflateArgs& a, hipStream_t st) {
+// side/ev (optional): a second stream and an event for it.  k_dfl_tail and the input checksum
+// depend only on the chain links (and the input), not on k_dfl_match: they run on the side
+// stream beside it -- latency-bound walks that fit next to match's one workgroup per CU --
+// and the parse waits for both.
+void launch_deflate(const DeflateArgs& a, hipStream_t st, hipStream_t side, hipEvent_t ev) {
     if (a.n == 0) return;
     dim3 grid((a.n + DF_THREADS - 1) / DF_THREADS);
     hipLaunchKernelGGL(k_deflate_tables, dim3(1), dim3(1), 0, st);
     if (a.rec_buf && !c_config_host_fast(a.level)) {
         const uint32_t nseg = (a.rec_stride + PM_SEG - 1) / PM_SEG;
+        const int ck_kind = a.format == SDZ_DEFLATE_GZIP ? 1 : 0;
         hipLaunchKernelGGL(k_dfl_chain, dim3((a.n + CH_WAVES - 1) / CH_WAVES), dim3(64 * CH_WAVES), 0, st, a);
+        const bool fork = side && ev && hipEventRecord(ev, st) == hipSuccess &&
+                          hipStreamWaitEvent(side, ev, 0) == hipSuccess;
+        if (fork) {
+            hipLaunchKernelGGL(k_dfl_tail, dim3(a.n), dim3(256), 0, side, a);
+            launch_checksum(a.in, a.in_off, a.in_len, nullptr, a.cks, a.n, ck_kind, side);
+            (void)hipEventRecord(ev, side);
+        }
         hipLaunchKernelGGL(k_dfl_match, dim3(a.n * nseg), dim3(PM_THREADS), 0, st, a, nseg);
-        hipLaunchKernelGGL(k_dfl_tail, dim3(a.n), dim3(256), 0, st, a);
+        if (fork) {
+            (void)hipStreamWaitEvent(st, ev, 0);
+        } else {
+            hipLaunchKernelGGL(k_dfl_tail, dim3(a.n), dim3(256), 0, st, a);
+            launch_checksum(a.in, a.in_off, a.in_len, nullptr, a.cks, a.n, ck_kind, st);
+        }
         hipLaunchKernelGGL(k_dfl_parse, grid, dim3(64), 0, st, a);
         hipLaunchKernelGGL(k_dfl_trees, dim3(a.n), dim3(64), 0, st, a);
-        launch_checksum(a.in, a.in_off, a.in_len, nullptr, a.cks, a.n, a.format == SDZ_DEFLATE_GZIP ? 1 : 0, st);
         hipLaunchKernelGGL(k_dfl_encode, dim3(a.n), dim3(EN_THREADS), 0, st, a);
         DeflateArgs f = a;
         f.fast = 1;                                          // streams the record path handed back

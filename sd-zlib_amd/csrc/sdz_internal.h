@@ -107,7 +107,7 @@ struct DeflateArgs {
 };
 
 uint64_t deflate_state_bytes();
-void launch_deflate(const DeflateArgs& a, hipStream_t s);
+void launch_deflate(const DeflateArgs& a, hipStream_t s, hipStream_t side = nullptr, hipEvent_t ev = nullptr);
 // the fast (not bit-exact) compressor (k_deflate_fast.hip): 16 KiB tiles, one block each
 #define FT_TILE_BYTES 8192u
 #define FT_TILE_OUT 8256u                 // a tile's output slot (<= tile + 10 bytes)

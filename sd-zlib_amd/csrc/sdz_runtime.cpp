@@ -754,6 +754,8 @@ int sdz_deflate_batch_device(const uint8_t* in, const uint64_t* in_off, const ui
         HIPCHK(hipMalloc(&dbg, 64 * sizeof(unsigned long long)));
         HIPCHK(hipMemsetAsync(dbg, 0, 64 * sizeof(unsigned long long), s));
     }
+    SideStream* side = nullptr;                   // the record path's tail + checksum run there
+    if (stride && side_stream(&side) != SDZ_API_OK) side = nullptr;
     timing_begin(s);
     for (uint32_t b = 0; b < n; b += chunk) {
         DeflateArgs a;
@@ -770,7 +772,7 @@ int sdz_deflate_batch_device(const uint8_t* in, const uint64_t* in_off, const ui
         a.dict = dict; a.dict_len = dict_len; a.dict_adler = dict_adler;
         a.fname = d_fname; a.fname_len = fname_len; a.mtime = mtime;
         a.n = m; a.level = level; a.format = format;
-        launch_deflate(a, s);
+        launch_deflate(a, s, side ? side->s : nullptr, side ? side->ev : nullptr);
     }
     timing_end(s);
     if (phases) {
