@@ -1429,12 +1429,7 @@ __global__ __launch_bounds__(256) void k_dfl_tail(DeflateArgs A) {
 // Symbols go to the stream's symbol buffer -- the front of its record buffer: symbol k is
 // written after record k/2 has been read -- as lc | dist << 8 (dist 0: literal lc).
 __global__ __launch_bounds__(64) void k_dfl_parse(DeflateArgs A) {
-    __shared__ uint32_t dfq[D_CODES][64];                   // dist-code counts of the open block
-    __shared__ uint8_t dcode[512];
     const uint32_t lane = threadIdx.x, sid = blockIdx.x * 64 + lane;
-    for (int i = (int)lane; i < 512; i += 64) dcode[i] = g_dt.dist_code[i];
-    for (int c = 0; c < D_CODES; ++c) dfq[c][lane] = 0;
-    __syncthreads();
     if (sid >= A.n) return;
     GLB DSlab* S = (GLB DSlab*)(A.state + (uint64_t)sid * SLAB_BYTES);
     GLB FStream* F = (GLB FStream*)S->window;
@@ -1448,18 +1443,21 @@ __global__ __launch_bounds__(64) void k_dfl_parse(DeflateArgs A) {
     int strstart = 0, lookahead = n, match_length = MIN_MATCH - 1, match_start = 0, match_available = 0;
     int block_start = 0, off = 0;
     uint32_t last_lit = 0, matches = 0, lx = 0, nblk = 0, sym0 = 0;
+    // TRUNCATE_BLOCK's estimate needs only sum over the block's matches of 5 + extra bits of
+    // the distance code (deflate.ts:503-506), kept as a running sum: extra bits of distance
+    // d + 1 are 0 for d < 4, else floor(log2 d) - 1 (no dist_code table, no per-code counts)
+    uint32_t dxb = 0;
     auto tally = [&](int dist, int lc) -> bool {             // _tr_tally, deflate.ts:488-524
         sym[lx++] = (uint32_t)lc | ((uint32_t)dist << 8);
         last_lit++;
         if (dist) {
             matches++;
-            const int d = dist - 1;
-            dfq[d < 256 ? dcode[d] : dcode[256 + (d >> 7)]][lane]++;
+            const uint32_t d = (uint32_t)(dist - 1);
+            dxb += 5u + (d < 4u ? 0u : 30u - (uint32_t)__builtin_clz(d));
         }
         if ((last_lit & 0x1fff) == 0 && level > 2) {         // TRUNCATE_BLOCK
-            uint32_t out_length = last_lit * 8;
+            uint32_t out_length = last_lit * 8 + dxb;
             const int in_length = strstart - block_start;
-            for (int dc = 0; dc < D_CODES; dc++) out_length += dfq[dc][lane] * (5 + c_extra_dbits[dc]);
             out_length >>= 3;
             if (matches < last_lit / 2 && (int)out_length < in_length / 2) return true;
         }
@@ -1472,8 +1470,7 @@ __global__ __launch_bounds__(64) void k_dfl_parse(DeflateArgs A) {
             B->block_start = block_start; B->strstart = strstart; B->off = off; B->eof = eof;
         }
         nblk++;
-        sym0 = lx; last_lit = 0; matches = 0;
-        for (int c = 0; c < D_CODES; ++c) dfq[c][lane] = 0;
+        sym0 = lx; last_lit = 0; matches = 0; dxb = 0;
         block_start = strstart;
     };
     for (;;) {
@@ -1867,10 +1864,11 @@ int device_max_u64(const uint64_t* v, uint32_t n, unsigned long long* d_slot, ui
 
 static bool c_config_host_fast(int level) { return level >= 1 && level <= 3; }
 
-// side/ev (optional): a second stream and an event for it.  k_dfl_tail and the input checksum
-// depend only on the chain links (and the input), not on k_dfl_match: they run on the side
-// stream beside it -- latency-bound walks that fit next to match's one workgroup per CU --
-// and the parse waits for both.
+// side/ev (optional): a second stream and an event for it.  The input checksum depends on
+// nothing else: it runs on the side stream beside the parse and the trees, which are
+// latency-bound (one lane per stream) and leave the CUs nearly idle; the encoder waits for
+// it.  (k_dfl_tail beside k_dfl_match, the other candidate, slowed match by more than the
+// tail's own 14 ms: C3 413 -> 438 ms of match.)
 void launch_deflate(const DeflateArgs& a, hipStream_t st, hipStream_t side, hipEvent_t ev) {
     if (a.n == 0) return;
     dim3 grid((a.n + DF_THREADS - 1) / DF_THREADS);
@@ -1879,22 +1877,18 @@ void launch_deflate(const DeflateArgs& a, hipStream_t st, hipStream_t side, hipE
         const uint32_t nseg = (a.rec_stride + PM_SEG - 1) / PM_SEG;
         const int ck_kind = a.format == SDZ_DEFLATE_GZIP ? 1 : 0;
         hipLaunchKernelGGL(k_dfl_chain, dim3((a.n + CH_WAVES - 1) / CH_WAVES), dim3(64 * CH_WAVES), 0, st, a);
+        hipLaunchKernelGGL(k_dfl_match, dim3(a.n * nseg), dim3(PM_THREADS), 0, st, a, nseg);
+        hipLaunchKernelGGL(k_dfl_tail, dim3(a.n), dim3(256), 0, st, a);
         const bool fork = side && ev && hipEventRecord(ev, st) == hipSuccess &&
                           hipStreamWaitEvent(side, ev, 0) == hipSuccess;
         if (fork) {
-            hipLaunchKernelGGL(k_dfl_tail, dim3(a.n), dim3(256), 0, side, a);
             launch_checksum(a.in, a.in_off, a.in_len, nullptr, a.cks, a.n, ck_kind, side);
             (void)hipEventRecord(ev, side);
         }
-        hipLaunchKernelGGL(k_dfl_match, dim3(a.n * nseg), dim3(PM_THREADS), 0, st, a, nseg);
-        if (fork) {
-            (void)hipStreamWaitEvent(st, ev, 0);
-        } else {
-            hipLaunchKernelGGL(k_dfl_tail, dim3(a.n), dim3(256), 0, st, a);
-            launch_checksum(a.in, a.in_off, a.in_len, nullptr, a.cks, a.n, ck_kind, st);
-        }
         hipLaunchKernelGGL(k_dfl_parse, grid, dim3(64), 0, st, a);
         hipLaunchKernelGGL(k_dfl_trees, dim3(a.n), dim3(64), 0, st, a);
+        if (fork) (void)hipStreamWaitEvent(st, ev, 0);
+        else launch_checksum(a.in, a.in_off, a.in_len, nullptr, a.cks, a.n, ck_kind, st);
         hipLaunchKernelGGL(k_dfl_encode, dim3(a.n), dim3(EN_THREADS), 0, st, a);
         DeflateArgs f = a;
         f.fast = 1;                                          // streams the record path handed back
