@@ -39,6 +39,9 @@ namespace sdz {
 #define RS_WIN 32768
 #define RS_R 36352                    // ring bytes: 32 KiB window + bytes in flight
 #define RS_SLACK (RS_R - RS_WIN)
+#ifndef RS_WPE
+#define RS_WPE RS_WAVES               // waves per SIMD the register budget is sized for
+#endif
 #ifndef RS_NAP
 #define RS_NAP 8                      // s_sleep units (64 clocks) between polls
 #endif
@@ -356,7 +359,7 @@ __device__ __forceinline__ void publish_wf(uint32_t* wf, uint32_t v1) {
     if ((threadIdx.x & 63u) == 0) lds_put(wf, v1);
 }
 
-__global__ __launch_bounds__(RS_THREADS) __attribute__((amdgpu_waves_per_eu(RS_WAVES, RS_WAVES))) void k_inflate_resolve(InflateArgs A, uint32_t round) {
+__global__ __launch_bounds__(RS_THREADS) __attribute__((amdgpu_waves_per_eu(RS_WPE, RS_WPE))) void k_inflate_resolve(InflateArgs A, uint32_t round) {
     __shared__ __attribute__((aligned(16))) uint8_t ring[RS_R + 256];   // + per-lane dummies
     __shared__ uint64_t chain;                           // (tag of the last started group) << 32 | its end
     __shared__ uint32_t wf, wwb, fail, edone;            // frontiers: final bytes, written-back bytes; emitters done
