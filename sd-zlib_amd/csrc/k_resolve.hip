@@ -277,7 +277,8 @@ __device__ __forceinline__ void emit_msk(uint8_t* ring, uint8_t* fmap, bool act,
     uint32_t* fmap32 = (uint32_t*)fmap;
     const uint32_t dumi = RS_R / 4 + (threadIdx.x & 31u);   // reads run RS_MW dwords on
     const bool lit = (t >> 31) == 0;
-    const bool slow = act && (d + len > RS_R || (!lit && (s + len > RS_R || s < 4u)) || mp + len > RS_BM);
+    // (a token across the map's end stays here: its map dwords wrap, with the next lap's byte)
+    const bool slow = act && (d + len > RS_R || (!lit && (s + len > RS_R || s < 4u)));
     const bool gen = act && (slow || (!lit && dist < len));  // periods and self-overlapping copies too
     if (__ballot(gen)) emit_tokens(ring, fmap, gen, t, d, s, len, dist, mp, lb);
     const bool one = act && !gen;
@@ -301,7 +302,9 @@ __device__ __forceinline__ void emit_msk(uint8_t* ring, uint8_t* fmap, bool act,
         const uint32_t h = hb >= 4 ? 0xffffffffu : hb <= 0 ? 0u : (1u << (8 * hb)) - 1u;
         const uint32_t mk = j == 0 ? h & lom : h;
         lds_mskor_at<j>(ring32, D0, mk, __builtin_amdgcn_alignbyte(x[j + 1], x[j], kk));
-        lds_mskor_at<j>(fmap32, M0, mk, lw);
+        const uint32_t mi = M0 + (uint32_t)j;                // map dword, wrapped (dword-aligned end)
+        const bool wr = mi >= RS_BM / 4u;
+        lds_mskor_at<0>(fmap32, wr ? mi - RS_BM / 4u : mi, mk, wr ? lap_next(lb) * 0x01010101u : lw);
     });
     // later steps of copies longer than 4 RS_MW - 3 bytes
     for (uint32_t w0 = RS_MW; __ballot(e > 4u * w0); w0 += RS_MW) {
@@ -313,7 +316,9 @@ __device__ __forceinline__ void emit_msk(uint8_t* ring, uint8_t* fmap, bool act,
             const int32_t hb = (int32_t)e - 4 * (int32_t)(w0 + j);
             const uint32_t mw = !on || hb <= 0 ? 0u : hb >= 4 ? 0xffffffffu : (1u << (8 * hb)) - 1u;
             lds_mskor_at<0>(ring32, D0 + w0 + (uint32_t)j, mw, __builtin_amdgcn_alignbyte(x[j + 1], x[j], k));
-            lds_mskor_at<0>(fmap32, M0 + w0 + (uint32_t)j, mw, lw);
+            const uint32_t mi = M0 + w0 + (uint32_t)j;
+            const bool wr = mi >= RS_BM / 4u;
+            lds_mskor_at<0>(fmap32, wr ? mi - RS_BM / 4u : mi, mw, wr ? lap_next(lb) * 0x01010101u : lw);
         }
     }
 }
