@@ -267,7 +267,7 @@ __device__ __forceinline__ void lds_mskor_at(uint32_t* base32, uint32_t i, uint3
 // d -- RS_MW dwords per step (tokens up to 4 RS_MW - 3 bytes take one step), each followed
 // by the same mask on the finality map (map index = ring index mod 4).  Masked writes
 // outside a token are no-ops.  Copies that overlap themselves (periods included), and
-// tokens across the ring's or map's end, go through emit_tokens.
+// tokens across the ring's end, go through emit_tokens (across the map's end: wrapped here).
 #ifndef RS_MW
 #define RS_MW 2
 #endif
