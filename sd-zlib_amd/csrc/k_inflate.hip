@@ -444,6 +444,9 @@ __device__ __forceinline__ void tok_flush_lits(C& L) {
         L.litw = 0;
     }
 }
+#ifndef IL_FULL_AT_RING
+#define IL_FULL_AT_RING 1                 // token room checked at the ring step (C2 decode -2 %, distinct -3 %)
+#endif
 #ifndef IL_BF_TOKENS
 #define IL_BF_TOKENS 1
 #endif
@@ -1053,11 +1056,20 @@ __device__ __noinline__ void hot_epoch(DSave* S, const uint8_t* inp, uint64_t il
     if (hot) hot_load(H, LL, DD, S, inp, ilen, cap);
     do {
         if (hot) ring_step(H);
-#pragma unroll 1
+#if IL_FULL_AT_RING
+        // token room checked once per 4 steps: at most 2 tokens per step
+        if (H.ntok + 3u + 8u > H.tcap) H.full = true;
+#endif
+#ifndef IL_REP_UNROLL
+#define IL_REP_UNROLL 4                   // the 4 steps between ring steps, unrolled (C2 decode -3 %)
+#endif
+#pragma unroll IL_REP_UNROLL
         for (int rep = 0; rep < 4; ++rep) {
             if (hot_ready<STREAM>(H)) {
                 fast_step(H, LL, DD, region);
+#if !IL_FULL_AT_RING
                 if (H.ntok + 3 > H.tcap) H.full = true;
+#endif
             }
         }
     } while (__popcll(__ballot(hot_ready<STREAM>(H))) > stop);
