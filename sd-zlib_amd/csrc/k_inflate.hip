@@ -256,8 +256,46 @@ __device__ __forceinline__ uint32_t tsel(const HTree& T, uint32_t rc) {
     uint32_t c1 = bfi(g4, b5, b1), c9 = bfi(g12, b13, b9);
     return bfi(g8, c9, c1);
 }
+#ifndef IL_BSEARCH
+#define IL_BSEARCH 1                      // binary-search tree select (C2 decode -3 %)
+#endif
+#if IL_BSEARCH
+// the same word by a 4-step binary search over the (non-decreasing) limits: c = #{k : rc >=
+// lim[k]} bit by bit, with the pk select tree cut by the top bit first so that only its last
+// level waits for the last compare (34 VALU against 45)
+__device__ __forceinline__ uint32_t ge_mask_m1(uint32_t rc, uint32_t limm1) {   // rc >= limm1 + 1
+    uint32_t m;
+    asm("v_sub_u32 %0, %1, %2\n\tv_ashrrev_i32 %0, 31, %0" : "=&v"(m) : "v"(limm1), "v"(rc));
+    return m;
+}
+// M1: the tree's limits are stored minus one (the hot loop's register copy, hot_epoch)
+template <bool M1 = false>
+__device__ __forceinline__ uint32_t tsel_bs(const HTree& T, uint32_t rc) {
+    auto ge = [&](uint32_t x) { return M1 ? ge_mask_m1(rc, x) : ge_mask(rc, x); };
+    const uint32_t m1 = ge(T.lim[8]);
+    // pk[1 + c]: level 1 by m1 (c >= 8)
+    const uint32_t p1 = bfi(m1, T.pk[9], T.pk[1]), p2 = bfi(m1, T.pk[10], T.pk[2]);
+    const uint32_t p3 = bfi(m1, T.pk[11], T.pk[3]), p4 = bfi(m1, T.pk[12], T.pk[4]);
+    const uint32_t p5 = bfi(m1, T.pk[13], T.pk[5]), p6 = bfi(m1, T.pk[14], T.pk[6]);
+    const uint32_t p7 = bfi(m1, T.pk[15], T.pk[7]), p8 = bfi(m1, T.pk[16], T.pk[8]);
+    const uint32_t l1 = bfi(m1, T.lim[9], T.lim[1]), l3 = bfi(m1, T.lim[11], T.lim[3]);
+    const uint32_t l5 = bfi(m1, T.lim[13], T.lim[5]), l7 = bfi(m1, T.lim[15], T.lim[7]);
+    const uint32_t l2 = bfi(m1, T.lim[10], T.lim[2]), l6 = bfi(m1, T.lim[14], T.lim[6]);
+    const uint32_t m2 = ge(bfi(m1, T.lim[12], T.lim[4]));
+    const uint32_t q1 = bfi(m2, p5, p1), q2 = bfi(m2, p6, p2), q3 = bfi(m2, p7, p3), q4 = bfi(m2, p8, p4);
+    const uint32_t k1 = bfi(m2, l5, l1), k3 = bfi(m2, l7, l3);
+    const uint32_t m3 = ge(bfi(m2, l6, l2));
+    const uint32_t r1 = bfi(m3, q3, q1), r2 = bfi(m3, q4, q2);
+    const uint32_t m4 = ge(bfi(m3, k3, k1));
+    return bfi(m4, r2, r1);
+}
+#define tsel tsel_bs<false>
+#define tsel_hot tsel_bs<true>
+#else
+#define tsel_hot tsel
+#endif
 __device__ __forceinline__ int32_t pk_rank(uint32_t v, uint32_t rc) {
-    return (int32_t)(v >> 16) + (int32_t)(rc >> (v & 15u)) - 32768;
+    return (int32_t)(v >> 16) + (int32_t)(rc >> (v & 31u)) - 32768;   // bit 4 is 0: v_lshrrev's own mask
 }
 
 // inftree.ts:212-296 table allocation replayed over counts only (c[g] already holds
@@ -335,7 +373,7 @@ __device__ __forceinline__ void finish_tree(Tree& T, const uint32_t (&hs)[5]) {
         T.lim[L] = (code + cl) << (15 - L);
         int32_t off = idx - (int32_t)code;
         uint32_t h = LIT ? cnt_get(hs, L) : 511u;
-        T.pk[L] = ((uint32_t)(off + 32768) << 16) | (h << 4) | (uint32_t)(15 - L);
+        T.pk[L] = ((uint32_t)(off + 32768) << 16) | (h << 5) | (uint32_t)(15 - L);
         idx += (int32_t)cl;
         code = (code + cl) << 1;
     }
@@ -762,12 +800,12 @@ __device__ __forceinline__ void fast_step(Hot& L, const HTree& LL, const HTree& 
     br_refill(L);
     uint32_t pw = br_peek32(L);
     uint32_t rc = __builtin_bitreverse32(pw) >> 17;
-    uint32_t v = tsel(LL, rc);
+    uint32_t v = tsel_hot(LL, rc);
     int32_t idx = pk_rank(v, rc);
     uint32_t len = 15u - (v & 15u);
     uint32_t b = region[idx];
     L.bo += len;
-    if (idx < (int32_t)((v >> 4) & 511u)) {               // literal
+    if (idx < (int32_t)((v >> 5) & 511u)) {               // literal
         if (L.room == 0) { lane_fail(L, SDZ_OUT_OVERFLOW, 0); return; }
         L.room--;
         tok_lit(L, b);
@@ -785,11 +823,11 @@ __device__ __forceinline__ void fast_step(Hot& L, const HTree& LL, const HTree& 
     br_refill(L);
     pw = br_peek32(L);
     rc = __builtin_bitreverse32(pw) >> 17;
-    v = tsel(DD, rc);
+    v = tsel_hot(DD, rc);
     idx = pk_rank(v, rc);
     len = 15u - (v & 15u);
     uint32_t ds = region[IL_DSYM + idx];
-    if (idx >= (int32_t)((v >> 4) & 511u)) { lane_fail(L, SDZ_DATA_ERROR, ZM_INVALID_DIST); return; }
+    if (idx >= (int32_t)((v >> 5) & 511u)) { lane_fail(L, SDZ_DATA_ERROR, ZM_INVALID_DIST); return; }
     uint32_t dist = dist_base(ds, e);
     dist += (pw >> len) & ((1u << e) - 1u);
     L.bo += len + e;
@@ -813,7 +851,7 @@ __device__ __forceinline__ void slow_step(Lane& L, const Tree& LL, const Tree& D
     if (bad) { lane_fail(L, SDZ_DATA_ERROR, ZM_INVALID_LITLEN); return; }
     uint32_t b = region[idx];
     L.bo += (uint32_t)len;
-    if (idx < (int32_t)((v >> 4) & 511u)) {
+    if (idx < (int32_t)((v >> 5) & 511u)) {
         if (L.room == 0) { lane_stall(L, 2); return; }
         L.room--;
         tok_lit(L, b);
@@ -1054,6 +1092,10 @@ __device__ __noinline__ void hot_epoch(DSave* S, const uint8_t* inp, uint64_t il
     H.mode = LM_DONE; H.full = true; H.ntok = 0; H.nfl = 0; H.tcap = tcap; H.tb = tb; H.ts = lane_stage();
     H.avail = 0; H.bo = 0;
     if (hot) hot_load(H, LL, DD, S, inp, ilen, cap);
+#if IL_BSEARCH
+#pragma unroll
+    for (int k = 1; k <= 15; ++k) { LL.lim[k] -= 1u; DD.lim[k] -= 1u; }   // tsel_hot's form
+#endif
     do {
         if (hot) ring_step(H);
 #if IL_FULL_AT_RING
