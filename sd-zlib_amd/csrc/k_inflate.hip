@@ -46,6 +46,9 @@ namespace sdz {
 #endif
 #define IL_TSTRIDE 136                // LDS bytes per stream for the token stage (8-aligned)
 #define IL_BAD_IDX 300                // rank selected by codes past lim[15]
+#ifndef IL_PEEK_PAR
+#define IL_PEEK_PAR 0                 // peek from the pre-refill words beside the refill's compare
+#endif
 
 // LDS: per-stream symbol tables, then per-stream token stages (file scope, so the
 // non-inlined hot and cold functions address it as LDS, not through flat pointers)
@@ -163,6 +166,20 @@ __device__ __forceinline__ void br_refill(Hot& L) {
     L.avail -= c ? 32 : 0;
     L.bo &= 31u;
     L.nx = L.ring[(L.rpos >> 2) & 15u];
+}
+// the refill and the peek after it, with the peek taken from the pre-refill words in parallel
+// with the refill's compare (one dependent operation less on the bit position's chain)
+__device__ __forceinline__ uint32_t br_refill_peek(Hot& L) {
+#if IL_PEEK_PAR
+    const bool c = L.bo >= 32;
+    const uint32_t pa = __builtin_amdgcn_alignbit(L.w1, L.w0, L.bo);   // alignbit uses bo & 31
+    const uint32_t pb = __builtin_amdgcn_alignbit(L.w2, L.w1, L.bo);
+    br_refill(L);
+    return c ? pb : pa;
+#else
+    br_refill(L);
+    return br_peek32(L);
+#endif
 }
 __device__ __forceinline__ void tok_flush_hot(Hot& L);
 // the wave-uniform ring step (see struct Hot); keeps >= 24 bytes in the ring,
@@ -797,8 +814,7 @@ __device__ __forceinline__ uint32_t dist_base(uint32_t ds, uint32_t& e) {
 // decode one literal/length symbol (+ its distance): the fast path, taken while at
 // least 64 input bits remain (one step reads at most 48)
 __device__ __forceinline__ void fast_step(Hot& L, const HTree& LL, const HTree& DD, const uint8_t* region) {
-    br_refill(L);
-    uint32_t pw = br_peek32(L);
+    uint32_t pw = br_refill_peek(L);
     uint32_t rc = __builtin_bitreverse32(pw) >> 17;
     uint32_t v = tsel_hot(LL, rc);
     int32_t idx = pk_rank(v, rc);
@@ -820,8 +836,7 @@ __device__ __forceinline__ void fast_step(Hot& L, const HTree& LL, const HTree& 
     uint32_t mlen = len_base(b, e);
     mlen += (pw >> len) & ((1u << e) - 1u);
     L.bo += e;
-    br_refill(L);
-    pw = br_peek32(L);
+    pw = br_refill_peek(L);
     rc = __builtin_bitreverse32(pw) >> 17;
     v = tsel_hot(DD, rc);
     idx = pk_rank(v, rc);
