@@ -10,7 +10,9 @@
  *
  * Pinned by tests/test_oracle.py against the reference's fixtures.
  */
+#define _POSIX_C_SOURCE 200809L
 #include "sdz_oracle.h"
+#include <pthread.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -42,17 +44,17 @@ int32_t oracle_adler32(const uint8_t* buf, size_t len, int32_t seed) {
 }
 
 static uint32_t crc_table0[256];
-static int crc_ready = 0;
-/* crc32.ts:179-214 (only table 0 is needed: slicing-by-4 is a pure speed-up). */
-static void crc_init(void) {
-    if (crc_ready) return;
+/* crc32.ts:179-214 (only table 0 is needed: slicing-by-4 is a pure speed-up).  The tables
+ * are built once (pthread_once): the CPU baseline calls the oracle from many threads. */
+static void crc_init_once(void) {
     for (uint32_t n = 0; n < 256; n++) {
         uint32_t c = n;
         for (int k = 0; k < 8; k++) c = (c & 1) ? 0xedb88320u ^ (c >> 1) : c >> 1;
         crc_table0[n] = c;
     }
-    crc_ready = 1;
 }
+static pthread_once_t crc_once = PTHREAD_ONCE_INIT;
+static void crc_init(void) { pthread_once(&crc_once, crc_init_once); }
 
 /* crc32.ts:48-106: c = ~seed; reflected byte loop; return ~c as int32 */
 int32_t oracle_crc32(const uint8_t* buf, size_t len, int32_t seed) {
@@ -319,9 +321,7 @@ static int inflate_trees_dynamic(int nl, int nd, const uint8_t* cl, int* bl, int
  * fixed code (zlib 1.1.3 inffixed.h); regenerated here, spot-checked in tests. */
 static int32_t fixed_tl[512 * 3];
 static int32_t fixed_td[32 * 3];
-static int fixed_ready = 0;
-static void fixed_init(void) {
-    if (fixed_ready) return;
+static void fixed_init_once(void) {
     uint8_t lens[288];
     huft_work W;
     int t, m;
@@ -334,8 +334,9 @@ static void fixed_init(void) {
     for (int i = 0; i < 30; i++) lens[i] = 5;
     init_work(&W); W.hn = 0; m = 5;
     huft_build(lens, 0, 30, 0, cpdist, cpdext, &t, &m, fixed_td, &W);
-    fixed_ready = 1;
 }
+static pthread_once_t fixed_once = PTHREAD_ONCE_INIT;
+static void fixed_init(void) { pthread_once(&fixed_once, fixed_init_once); }
 
 /* exported for the fixed-table spot check in tests */
 int32_t oracle_fixed_table_entry(int which, int idx) {
@@ -1263,15 +1264,13 @@ static const int extra_blbits[BL_CODES] = { 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 
 static const int bl_order[BL_CODES] = { 16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15 };
 static uint16_t static_ltree[(L_CODES + 2) * 2];
 static uint16_t static_dtree[D_CODES * 2];
-static int trees_ready = 0;
 
 static int bi_reverse(int code, int len);
 
 /* deftree.ts:25-38, 269-298, 319-337: the code tables are zlib's trees.h; they are
  * derived here from extra_lbits/extra_dbits exactly as zlib's tr_static_init does,
  * and spot-checked against the reference's literals in tests. */
-static void trees_init(void) {
-    if (trees_ready) return;
+static void trees_init_once(void) {
     int length = 0, code, n, dist;
     for (code = 0; code < LENGTH_CODES - 1; code++) {
         base_length[code] = length;
@@ -1307,8 +1306,9 @@ static void trees_init(void) {
         static_dtree[n * 2 + 1] = 5;
         static_dtree[n * 2] = (uint16_t)bi_reverse(n, 5);
     }
-    trees_ready = 1;
 }
+static pthread_once_t trees_once = PTHREAD_ONCE_INIT;
+static void trees_init(void) { pthread_once(&trees_once, trees_init_once); }
 
 /* exported for the table spot checks in tests */
 int32_t oracle_tree_table(int which, int idx) {
