@@ -4,9 +4,10 @@
 A step = one pass of the hot path over one batch: 65,536 device-resident copies
 of the reference fixture paradiselost.deflate (193,730 B -> 471,162 B each) are
 inflated by the HIP kernel into their own output slots, checksums fused.  With
---gpus N (torchrun, one rank per GPU, RCCL) every rank inflates its own 64 Ki
-streams (weak scaling, no data-path collective); per-stream result records are
-all-gathered over RCCL after the timed region (reported as gather_ms).
+--gpus N (torchrun, one rank per GPU) every rank inflates its own 64 Ki streams
+(weak scaling, no data-path collective); the per-stream result records are
+all-gathered over RCCL inside libsdz after the timed region (gather_ms), and the
+step barrier / max-over-ranks timing run over the same communicator.
 
 Also reported: the kernel's HBM roofline fraction (HIP events on the launch
 stream), the CPU baseline (oracle restatement on host cores; the reference's
@@ -88,14 +89,20 @@ def slice_offsets(n, span, seed=0x5D5A1B1E):
 
 
 def fill_slices(sdz, b, text, offs, slice_len):
-    """Stream j of batch b <- text[offs[j] : offs[j] + slice_len], copied on the device."""
+    """Stream j of batch b <- text[offs[j] : offs[j] + slice_len]: ONE k_gather launch
+    (sdz_gather_device), not one copy dispatch per stream."""
     L = sdz.lib()
+    n = len(offs)
     src = sdz.DeviceBuffer(len(text) + 64)
     src.upload(text)
-    for j, o in enumerate(offs):
-        rc = L.sdz_copy_device_to_device(b.d_in.ptr + j * b.in_stride, src.ptr + o, slice_len)
-        assert rc == 0, L.sdz_last_error()
+    meta = [j * b.in_stride for j in range(n)] + list(offs) + [slice_len] * n
+    d_meta = sdz.DeviceBuffer(8 * len(meta))
+    d_meta.upload(bytes((ctypes.c_uint64 * len(meta))(*meta)))
+    m = d_meta.ptr
+    assert L.sdz_gather_device(b.d_in.ptr, m, src.ptr, m + 8 * n, m + 16 * n, n, None) == 0, L.sdz_last_error()
+    assert L.sdz_sync(None) == 0
     src.free()
+    d_meta.free()
 
 
 def inflate_distinct(sdz, L, bd, drec, text, offs, slice_len, steps, barrier, allmax, world):
@@ -138,6 +145,8 @@ def inflate_distinct(sdz, L, bd, drec, text, offs, slice_len, steps, barrier, al
     for j in sorted({0, n // 2, n - 1}):
         ok = ok and d_out.download(slice_len, j * round_up(slice_len, 256)) == text[offs[j]:offs[j] + slice_len]
     ok = allmax(0.0 if ok else 1.0) == 0.0
+    # a sample of the compressed streams for the CPU baseline (the oracle inflating them)
+    sample = [bd.d_out.download(in_len[j], j * bd.out_stride) for j in range(0, n, max(1, n // 256))]
     for x in (d_meta, d_out, d_rec):
         x.free()
     kernel_ms = sum(kms) / len(kms)
@@ -154,7 +163,7 @@ def inflate_distinct(sdz, L, bd, drec, text, offs, slice_len, steps, barrier, al
                                     "k_inflate_resolve": round(sum(x[1] for x in split) / len(split), 3),
                                     "k_inflate_finalize": round(sum(x[2] for x in split) / len(split), 3)}},
         "parity": bool(ok),
-    }
+    }, sample
 
 
 def inflate_step(sdz, b, split=None):
@@ -287,21 +296,18 @@ def mixed_leg(sdz, L, steps, scale, barrier, allmax, world, rank):
             "parity": bool(ok)}
 
 
-def cpu_baseline_inflate(comp, seconds, threads):
-    """Oracle (CPU restatement of the reference) inflating the same stream on host cores."""
-    import oracle as O
-    L = O.lib()
-    out_cap = 600000
-    counts = [0] * threads
+def cpu_run(work_one, seconds, threads):
+    """Run work_one(i) -> bytes counted, on `threads` host threads for `seconds` (the oracle
+    releases the GIL inside its C calls).  Returns (units, bytes, elapsed s)."""
+    counts, nbytes = [0] * threads, [0] * threads
     stop = time.perf_counter() + seconds
 
     def work(t):
-        buf = ctypes.create_string_buffer(out_cap)
-        res = O.InflateResult()
+        i = t
         while time.perf_counter() < stop:
-            L.oracle_inflate(comp, len(comp), None, 0, buf, out_cap, ctypes.byref(res))
-            assert res.success
+            nbytes[t] += work_one(i)
             counts[t] += 1
+            i += threads
 
     t0 = time.perf_counter()
     ths = [threading.Thread(target=work, args=(i,)) for i in range(threads)]
@@ -309,8 +315,124 @@ def cpu_baseline_inflate(comp, seconds, threads):
         th.start()
     for th in ths:
         th.join()
-    dt = time.perf_counter() - t0
-    return sum(counts), dt
+    return sum(counts), sum(nbytes), time.perf_counter() - t0
+
+
+def cpu_inflater(comps, out_cap):
+    """work_one for cpu_run: the oracle (C restatement of the reference) inflating comps[i]"""
+    import oracle as O
+    L = O.lib()
+    local = threading.local()
+
+    def one(i):
+        if not hasattr(local, "buf"):
+            local.buf = ctypes.create_string_buffer(out_cap)
+            local.res = O.InflateResult()
+        c = comps[i % len(comps)]
+        L.oracle_inflate(c, len(c), None, 0, local.buf, out_cap, ctypes.byref(local.res))
+        assert local.res.success
+        return local.res.total_out
+    return one
+
+
+def cpu_deflater(srcs, level):
+    """work_one for cpu_run: the oracle's deflate(src, {level}) ("deflate" container);
+    counts compressed bytes"""
+    import oracle as O
+    L = O.lib()
+    local = threading.local()
+
+    def one(i):
+        src = srcs[i % len(srcs)]
+        if not hasattr(local, "buf"):
+            local.cap = len(src) + len(src) // 8 + 4096
+            local.buf = ctypes.create_string_buffer(local.cap)
+            local.olen = ctypes.c_size_t(0)
+        parts = (ctypes.c_char_p * 1)(src)
+        lens = (ctypes.c_size_t * 1)(len(src))
+        err = L.oracle_deflater_run(parts, lens, 1, level, 1, None, 0, 0, None, 0, 0, local.buf, local.cap,
+                                    ctypes.byref(local.olen))
+        assert err == 0
+        return local.olen.value
+    return one
+
+
+def cpu_baseline(work_one, seconds, unit_bytes_fn, sample):
+    """all-threads and one-thread runs of the same work; value in MB/s of unit_bytes_fn"""
+    threads = max(1, min(16, os.cpu_count() or 1))
+    cnt, nb, dt = cpu_run(work_one, seconds, threads)
+    c1, nb1, d1 = cpu_run(work_one, max(0.5, seconds / 2), 1)
+    return {"value": round(unit_bytes_fn(cnt, nb) / dt / 1e6, 2), "unit": "MB/s", "cores": threads, "kind": "port",
+            "per_core_MBps": round(unit_bytes_fn(c1, nb1) / d1 / 1e6, 2),
+            "sample": "%s: %d units on %d threads in %.1f s; per core: %d in %.1f s on 1 thread"
+                      % (sample, cnt, threads, dt, c1, d1)}
+
+
+def facade_latency(sdz, reps=40):
+    """BASELINE configs[0] (C1) through the drop-in's host path: inflate(simple.deflate) and
+    deflate(simple.txt) one call at a time (staging pools, no per-call allocation); median
+    microseconds per call.  Also deflate(paradiselost.txt) at L1/L6/L9 (test/perf.html's
+    case), checked against the reference fixture (L6) and the published size table."""
+    golden = os.path.join(ROOT, "tests", "golden")
+    simple_c = open(os.path.join(golden, "simple.deflate"), "rb").read()
+    simple_t = open(os.path.join(golden, "simple.txt"), "rb").read()
+    text = open(os.path.join(golden, "paradiselost.txt"), "rb").read()
+    comp = open(os.path.join(golden, "paradiselost.deflate"), "rb").read()
+
+    def med(f, k=reps):
+        f()
+        ts = []
+        for _ in range(k):
+            t0 = time.perf_counter()
+            f()
+            ts.append(time.perf_counter() - t0)
+        ts.sort()
+        return ts[len(ts) // 2]
+    ok = sdz.inflate(simple_c) == simple_t and sdz.deflate(simple_t, {"level": 6}) == simple_c
+    res = {"inflate_simple_us": round(1e6 * med(lambda: sdz.inflate(simple_c)), 1),
+           "deflate_simple_us": round(1e6 * med(lambda: sdz.deflate(simple_t, {"level": 6})), 1),
+           "inflate_paradiselost_ms": round(1e3 * med(lambda: sdz.inflate(comp)), 3)}
+    sizes = {1: 226188, 6: 193730, 9: 193162}           # test/perf.html:63-69
+    for lv in (1, 6, 9):
+        out = sdz.deflate(text, {"level": lv})
+        ok = ok and len(out) == sizes[lv] and (lv != 6 or out == comp)
+        res["deflate_paradiselost_L%d_ms" % lv] = round(1e3 * med(lambda: sdz.deflate(text, {"level": lv}), 5), 3)
+    res["parity"] = bool(ok)
+    res["note"] = ("drop-in facade (Python mirror of sd-inflate.ts / sd-deflate.ts) over the host-buffer C ABI; "
+                   "reference browser times for deflate(paradiselost.txt): L1 15-22 ms, L6 39-48 ms, L9 49-57 ms "
+                   "(test/perf.html:63-69)")
+    return res
+
+
+class Ranks:
+    """One process per GPU (torchrun env).  The collectives run over RCCL inside libsdz
+    (sdz_comm_*): the step barrier, max-over-ranks timing and the record all-gather.  The
+    only other channel is gloo on the CPU, used once to hand rank 0's RCCL id to the others."""
+
+    def __init__(self, sdz):
+        self.rank = int(os.environ.get("RANK", "0"))
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.local = int(os.environ.get("LOCAL_RANK", "0"))
+        self.comm = None
+        if self.world > 1:
+            import torch.distributed as dist
+            dist.init_process_group("gloo")
+            box = [sdz.Comm.unique_id() if self.rank == 0 else None]
+            dist.broadcast_object_list(box, src=0)
+            self.comm = sdz.Comm(box[0], self.world, self.rank)
+            self.dist = dist
+
+    def barrier(self):
+        if self.comm:
+            self.comm.max(0.0)
+
+    def allmax(self, x):
+        return self.comm.max(x) if self.comm else x
+
+    def close(self):
+        if self.comm:
+            self.comm.close()
+            self.dist.destroy_process_group()
 
 
 def main():
@@ -335,32 +457,18 @@ def main():
     ap.add_argument("--host-streams", type=int, default=0,
                     help="streams for the host-buffer (PCIe-inclusive) inflate probe, e.g. 2048; off by "
                          "default so that the rocprofv3 stats of the default command hold C2 launches only")
+    ap.add_argument("--latency", type=int, default=1, help="C1-style single-call latency of the facade (0: skip)")
     args = ap.parse_args()
 
-    import torch
-    import torch.distributed as dist
-    rank = int(os.environ.get("RANK", "0"))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
     import sdz
     L = sdz.lib()
     if sdz.device_count() < 1:
         raise SystemExit("bench.py: no GPU visible")
-    torch.cuda.set_device(local)
+    local = int(os.environ.get("LOCAL_RANK", "0"))
     assert L.sdz_set_device(local) == 0
-    if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-
-    def barrier():
-        if world > 1:
-            dist.barrier()
-
-    def allmax(x):
-        if world == 1:
-            return x
-        t = torch.tensor([x], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        return float(t.item())
+    R = Ranks(sdz)
+    rank, world = R.rank, R.world
+    barrier, allmax = R.barrier, R.allmax
 
     golden = os.path.join(ROOT, "tests", "golden")
     comp = open(os.path.join(golden, "paradiselost.deflate"), "rb").read()
@@ -389,19 +497,17 @@ def main():
     ok = all(r.status == 0 and r.success and r.out_len == len(text) and r.checksum_verdict == 1 for r in recs)
     for i in sorted({0, n // 3, n - 1}):
         ok = ok and b.d_out.download(len(text), i * b.out_stride) == text
-    # ---- RCCL gather of per-stream result records (outside the timed region)
+    # ---- RCCL all-gather of the per-stream result records (libsdz; outside the timed region)
     gather_ms = None
     if world > 1:
         import sdz_dist
         shards = [list(range(r * n, (r + 1) * n)) for r in range(world)]   # weak scaling: n per rank
-        torch.cuda.synchronize()
         g0 = time.perf_counter()
-        allrec = sdz_dist.gather_records(bytes(recs), b.rec_size, shards, rank, device="cuda")
-        torch.cuda.synchronize()
+        allrec = sdz_dist.gather_records_comm(R.comm, bytes(recs), b.rec_size, shards)
         gather_ms = 1000.0 * (time.perf_counter() - g0)
-        if rank == 0:
-            ok = ok and all(sdz.InflateRecord.from_buffer_copy(r).status == 0 and
-                            sdz.InflateRecord.from_buffer_copy(r).success for r in allrec)
+        ok = ok and len(allrec) == world * n and all(
+            sdz.InflateRecord.from_buffer_copy(r).status == 0 and sdz.InflateRecord.from_buffer_copy(r).success
+            for r in allrec)
     okall = allmax(0.0 if ok else 1.0) == 0.0
     bytes_in, bytes_out = len(comp) * n, len(text) * n
     b.free()
@@ -409,6 +515,8 @@ def main():
     # ---- measured device copy peak (report against it in the same run)
     copy_gbs = None
     if args.copy_gib > 0:
+        import torch                                      # (plumbing: a device copy)
+        torch.cuda.set_device(local)
         nb = int(args.copy_gib * (1 << 30))
         src = torch.empty(nb, dtype=torch.uint8, device="cuda")
         dst = torch.empty_like(src)
@@ -473,18 +581,45 @@ def main():
             for j in sorted({0, 1, nd // 2, nd - 1}):
                 got = bd.d_out.download(drec[j].out_len, j * bd.out_stride)
                 dok = dok and got == O.deflate(text[offs[j]:offs[j] + slice_len], level=6)
+        dkms = sum(dk) / len(dk)
+        dalg = nd * slice_len + comp_total                  # uncompressed in + compressed out
+        dachieved = dalg / (dkms / 1000.0) / 1e9
+        dtraffic = None
+        dpmcs = sorted(glob.glob(os.path.join(ROOT, "profiles", "r[0-9][0-9]_deflate_pmc.json")))
+        if dpmcs and nd == 65536:
+            try:
+                dtraffic = json.load(open(dpmcs[-1])).get("hbm_bytes_per_launch")
+            except Exception:
+                dtraffic = None
         deflate = {
             "value": round(world * comp_total / dwall / 1e6, 2), "unit": "compressed MB/s",
             "input_MBps": round(world * nd * slice_len / dwall / 1e6, 2),
-            "kernel_ms": round(sum(dk) / len(dk), 3), "ms_per_step": round(1000 * dwall, 3),
+            "kernel_ms": round(dkms, 3), "ms_per_step": round(1000 * dwall, 3),
             "config": {"workload": "C3 deflate level=6 format=deflate", "streams_per_gpu": nd,
                        "slice_bytes": slice_len,
                        "data": "%d distinct paradiselost.txt slices at xorshift64 offsets (enwik8 absent offline)" % nd},
+            "roofline": {"bound": "hbm", "achieved": round(dachieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(dachieved / HBM_PEAK_GBS, 5), "traffic": dtraffic,
+                         "algorithmic_bytes_per_launch": dalg,
+                         "launch": "one sdz_deflate_batch_device call: k_dfl_chain/match/tail/parse/trees/encode "
+                                   "(+ checksum), HIP events on the launch stream"},
             "parity": bool(dok),
         }
+        if rank == 0 and world == 1 and args.cpu_seconds > 0:
+            srcs = [text[offs[j]:offs[j] + slice_len] for j in range(0, nd, max(1, nd // 64))]
+            deflate["cpu_baseline"] = cpu_baseline(
+                cpu_deflater(srcs, 6), args.cpu_seconds, lambda c, nb: nb,
+                "oracle C restatement deflate(L6, \"deflate\") of %d of the leg's 64 KiB slices, compressed MB/s"
+                % len(srcs))
+            deflate["cpu_baseline"]["input_MBps"] = None
         if args.distinct_steps > 0:
-            distinct = inflate_distinct(sdz, L, bd, drec, text, offs, slice_len, args.distinct_steps,
-                                        barrier, allmax, world)
+            distinct, dsample = inflate_distinct(sdz, L, bd, drec, text, offs, slice_len, args.distinct_steps,
+                                                 barrier, allmax, world)
+            if rank == 0 and world == 1 and args.cpu_seconds > 0:
+                distinct["cpu_baseline"] = cpu_baseline(
+                    cpu_inflater(dsample, slice_len + 64), args.cpu_seconds, lambda c, nb: nb,
+                    "oracle C restatement inflating %d of the leg's distinct 64 KiB streams, uncompressed MB/s"
+                    % len(dsample))
         bd.free()
         if args.fast_steps > 0 and hasattr(L, "sdz_deflate_fast_batch_device"):
             fast = deflate_fast_leg(sdz, L, text, offs, slice_len, nd, args.fast_steps, barrier, allmax, world, rank)
@@ -493,16 +628,14 @@ def main():
     if args.mixed_steps > 0:
         mixed = mixed_leg(sdz, L, args.mixed_steps, args.mixed_scale, barrier, allmax, world, rank)
 
+    latency = None
+    if rank == 0 and args.latency > 0:
+        latency = facade_latency(sdz)
+
     cpu = None
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
-        threads = max(1, min(16, os.cpu_count() or 1))
-        cnt, dt = cpu_baseline_inflate(comp, args.cpu_seconds, threads)
-        c1, d1 = cpu_baseline_inflate(comp, max(0.5, args.cpu_seconds / 2), 1)
-        cpu = {"value": round(cnt * len(text) / dt / 1e6, 2), "unit": "MB/s", "cores": threads,
-               "kind": "port",
-               "per_core_MBps": round(c1 * len(text) / d1 / 1e6, 2),
-               "sample": "%d x paradiselost.deflate inflated by the oracle C restatement on %d threads "
-                         "in %.1f s; per core: %d in %.1f s on 1 thread" % (cnt, threads, dt, c1, d1)}
+        cpu = cpu_baseline(cpu_inflater([comp], len(text) + 64), args.cpu_seconds, lambda c, nb: nb,
+                           "paradiselost.deflate inflated by the oracle C restatement, uncompressed MB/s")
 
     traffic = None
     # the latest round's PMC traffic summary (tools/round_measure.sh writes profiles/rNN_inflate_pmc.json)
@@ -525,7 +658,8 @@ def main():
         "data": "synthetic: 65536 device copies/GPU of reference fixture paradiselost.deflate",
         "config": {"workload": "C2 batched inflate: paradiselost.deflate x %d per GPU (zlib, dynamic Huffman)" % n,
                    "streams_per_gpu": n, "bytes_in_per_gpu": bytes_in, "bytes_out_per_gpu": bytes_out,
-                   "parallelism": "dp%d (independent streams, no data-path collective)" % world},
+                   "parallelism": "dp%d (independent streams, no data-path collective; records all-gathered "
+                                  "over RCCL inside libsdz)" % world},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
                      "kernel_ms": round(kernel_ms, 3),
@@ -544,11 +678,11 @@ def main():
         "deflate_fast": fast,
         "inflate_distinct": distinct,
         "mixed": mixed,
+        "facade_latency": latency,
     }
     if rank == 0:
         print(json.dumps(line), flush=True)
-    if world > 1:
-        dist.destroy_process_group()
+    R.close()
 
 
 if __name__ == "__main__":

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define SDZ_ABI_VERSION 3
+#define SDZ_ABI_VERSION 4
 
 /* API return codes */
 enum {
@@ -225,7 +225,7 @@ void sdz_deflater_destroy(sdz_deflater* z);
 
 /* The opt-in fast compressor: valid raw / zlib / gzip streams -- the
  * container as sd-deflate.ts:98-165 writes it, any inflater reads them, adler32 / crc32 of
- * the input in the trailer -- but not the reference's bytes: each 16 KiB tile of a stream
+ * the input in the trailer -- but not the reference's bytes: each 8 KiB tile of a stream
  * is compressed on its own (greedy parse, one dynamic-Huffman or stored block per tile,
  * byte-aligned by an empty stored block).  Not a drop-in for deflate(); for callers that
  * only need a valid stream fast.  out_cap[i] >= sdz_deflate_fast_bound(in_len[i], ...). */
@@ -257,6 +257,59 @@ int sdz_adler32_batch_device(const uint8_t* in, const uint64_t* in_off, const ui
 int sdz_crc32_batch_device(const uint8_t* in, const uint64_t* in_off, const uint64_t* in_len,
                            const int32_t* seed, int32_t* result, uint32_t n, void* stream);
 
+/* ------------------------------------------------------ multi-GPU */
+
+/* The reference is single-threaded and has no batch API; these entry points run the batched
+ * engine over several GPUs of one node.  Streams are independent, so a batch is cut into
+ * shards by LPT (largest stream first, onto the shard with the fewest bytes so far), one
+ * shard per entry of `devices`; one host thread per shard runs the single-device path on its
+ * GPU (hipSetDevice), and the fixed-size per-stream records are all-gathered over RCCL
+ * (ncclAllGather over xGMI) -- the only collective, after the codec kernels.  A device listed
+ * twice (N logical shards on one GPU, for tests) uses a loopback gather instead (RCCL allows
+ * one rank per device).  Outputs return to the caller's host buffers from each shard's GPU.
+ * Records come back in the caller's stream order. */
+#define SDZ_MAX_SHARDS 16
+
+/* owner[i] = shard of stream i (LPT over sizes; ties by index: deterministic) */
+int sdz_lpt_shard(const uint64_t* sizes, uint32_t n, uint32_t nshards, uint32_t* owner);
+
+typedef struct sdz_multi_stats {
+    double wall_ms;                        /* the whole call (host clock) */
+    double compute_ms;                     /* slowest shard: staging + kernels + outputs back */
+    double gather_ms;                      /* record all-gather (RCCL or loopback) + records to host */
+    float kernel_ms[SDZ_MAX_SHARDS];       /* per shard: codec kernels (HIP events) */
+    uint64_t bytes_in[SDZ_MAX_SHARDS];     /* per shard: input and output bytes */
+    uint64_t bytes_out[SDZ_MAX_SHARDS];
+    uint32_t streams[SDZ_MAX_SHARDS];
+    int32_t nshards;
+    int32_t collective;                    /* 1: RCCL ncclAllGather, 0: loopback gather */
+} sdz_multi_stats;
+
+/* sdz_inflate_batch / sdz_deflate_batch over ndev shards (devices[k] = HIP device of shard k,
+ * ndev <= SDZ_MAX_SHARDS).  stats may be NULL. */
+int sdz_inflate_batch_multi(const uint8_t* const* in, const size_t* in_len, uint8_t* const* out,
+                            const size_t* out_cap, sdz_inflate_record* rec, uint32_t n, int32_t format,
+                            const uint8_t* dict, size_t dict_len, const int32_t* devices, int32_t ndev,
+                            sdz_multi_stats* stats);
+int sdz_deflate_batch_multi(const uint8_t* const* in, const size_t* in_len, uint8_t* const* out,
+                            const size_t* out_cap, sdz_deflate_record* rec, uint32_t n, int32_t level,
+                            int32_t format, const uint8_t* fname, size_t fname_len, uint32_t mtime,
+                            const uint8_t* dict, size_t dict_len, const int32_t* devices, int32_t ndev,
+                            sdz_multi_stats* stats);
+
+/* One process per GPU (torchrun-style launchers): a communicator over RCCL for the record
+ * gather and the step barrier.  Rank 0 makes the id (sdz_comm_unique_id), every rank gets it
+ * by the caller's own means, then each calls sdz_comm_init_rank on its current device. */
+#define SDZ_COMM_ID_BYTES 128
+typedef struct sdz_comm sdz_comm;
+int sdz_comm_unique_id(uint8_t* id /* SDZ_COMM_ID_BYTES */);
+sdz_comm* sdz_comm_init_rank(const uint8_t* id, int32_t nranks, int32_t rank);
+/* recv (device) <- every rank's `bytes` of send (device), rank order; blocking */
+int sdz_comm_allgather_device(sdz_comm* c, const void* send, void* recv, uint64_t bytes);
+/* *v <- max over ranks (host value; a barrier for step timing) */
+int sdz_comm_allreduce_max(sdz_comm* c, double* v);
+int sdz_comm_destroy(sdz_comm* c);
+
 /* ----------------------------------------------------------------- misc */
 
 const char* sdz_zmsg(int32_t code);       /* z.msg text for a record's zmsg */
@@ -272,6 +325,10 @@ int sdz_copy_to_device(void* dst, const void* src, uint64_t bytes);
 int sdz_copy_to_host(void* dst, const void* src, uint64_t bytes);
 int sdz_memset_device(void* dst, int value, uint64_t bytes);
 int sdz_copy_device_to_device(void* dst, const void* src, uint64_t bytes);
+/* n spans in one launch: dst[dst_off[i] ..] <- src[src_off[i] .. + len[i]) (device pointers,
+ * asynchronous on stream; spans must not overlap).  Stages batches for the *_device calls. */
+int sdz_gather_device(uint8_t* dst, const uint64_t* dst_off, const uint8_t* src, const uint64_t* src_off,
+                      const uint64_t* len, uint32_t n, void* stream);
 int sdz_sync(void* stream);
 /* a non-blocking hipStream_t (as void*) for the *_device calls; NULL on failure */
 void* sdz_stream_create(void);

@@ -69,6 +69,10 @@ def lib():
         L.oracle_inflater_run_parts.restype = ctypes.c_int32
         L.oracle_inflater_run_parts.argtypes = L.oracle_inflater_run.argtypes + [
             ctypes.POINTER(ctypes.c_size_t), ctypes.POINTER(ctypes.c_int32)]
+        L.oracle_inflater_run_chunks.restype = ctypes.c_int32
+        L.oracle_inflater_run_chunks.argtypes = L.oracle_inflater_run_parts.argtypes + [
+            ctypes.POINTER(ctypes.c_size_t), ctypes.POINTER(ctypes.c_int32), ctypes.c_size_t,
+            ctypes.POINTER(ctypes.c_size_t)]
         L.oracle_inflate.restype = ctypes.c_int32
         L.oracle_inflate.argtypes = [u8p, ctypes.c_size_t, u8p, ctypes.c_size_t, ctypes.c_void_p,
                                      ctypes.c_size_t, ctypes.POINTER(InflateResult)]
@@ -131,6 +135,32 @@ def inflater_run(parts, raw=False, dictionary=None, out_cap=None):
     return _result_dict(res, out.raw[:res.total_out])
 
 
+def inflater_chunks(parts, raw=False, dictionary=None, out_cap=None):
+    """The arrays each append() returns, as the reference builds them (sd-inflate.ts:101-150):
+    a list per append of the pushed Uint8Array lengths.  Also returns the result dict."""
+    parts = [bytes(p) for p in parts]
+    n = len(parts)
+    arr = (ctypes.c_char_p * n)(*parts)
+    lens = (ctypes.c_size_t * n)(*[len(p) for p in parts])
+    total_in = sum(len(p) for p in parts)
+    cap = out_cap if out_cap is not None else max(1 << 16, total_in * 1100 + 65536)
+    out = ctypes.create_string_buffer(cap)
+    res = InflateResult()
+    pout = (ctypes.c_size_t * max(1, n))()
+    ep = ctypes.c_int32(-1)
+    ccap = cap // 16384 + 4 * n + 16
+    clen = (ctypes.c_size_t * ccap)()
+    cpart = (ctypes.c_int32 * ccap)()
+    nch = ctypes.c_size_t(0)
+    d = bytes(dictionary) if dictionary is not None else None
+    lib().oracle_inflater_run_chunks(arr, lens, n, 1 if raw else 0, d, len(d) if d else 0, out, cap,
+                                     ctypes.byref(res), pout, ctypes.byref(ep), clen, cpart, ccap, ctypes.byref(nch))
+    per = [[] for _ in range(n)]
+    for k in range(min(nch.value, ccap)):
+        per[cpart[k]].append(clen[k])
+    return per, _result_dict(res, out.raw[:res.total_out])
+
+
 def inflater_parts(parts, raw=False, dictionary=None, out_cap=None):
     """inflater_run, plus the output of each append() (list of bytes) and the index of the
     append that threw (or None)."""
@@ -178,11 +208,11 @@ def deflater_run(parts, level=6, format="deflate", dictionary=None, file_name=No
     arr = (ctypes.c_char_p * n)(*parts)
     lens = (ctypes.c_size_t * n)(*[len(p) for p in parts])
     total = sum(len(p) for p in parts)
-    cap = total + total // 8 + 4096
+    fn = latin1_filename(file_name) if file_name else b""
+    cap = total + total // 8 + 4096 + len(fn)
     out = ctypes.create_string_buffer(cap)
     out_len = ctypes.c_size_t(0)
     d = bytes(dictionary) if dictionary is not None else None
-    fn = latin1_filename(file_name) if file_name else b""
     err = lib().oracle_deflater_run(arr, lens, n, level, FORMAT[format], d, len(d) if d else 0,
                                     1 if d is not None else 0, fn, len(fn), mtime & 0xFFFFFFFF,
                                     out, cap, ctypes.byref(out_len))
@@ -199,12 +229,12 @@ def deflater_parts(parts, level=6, format="deflate", dictionary=None, file_name=
     arr = (ctypes.c_char_p * n)(*parts)
     lens = (ctypes.c_size_t * n)(*[len(p) for p in parts])
     total = sum(len(p) for p in parts)
-    cap = total + total // 8 + 4096
+    fn = latin1_filename(file_name) if file_name else b""
+    cap = total + total // 8 + 4096 + len(fn)
     out = ctypes.create_string_buffer(cap)
     out_len = ctypes.c_size_t(0)
     ends = (ctypes.c_size_t * (n + 1))()
     d = bytes(dictionary) if dictionary is not None else None
-    fn = latin1_filename(file_name) if file_name else b""
     err = lib().oracle_deflater_run_parts(arr, lens, n, level, FORMAT[format], d, len(d) if d else 0,
                                           1 if d is not None else 0, fn, len(fn), mtime & 0xFFFFFFFF,
                                           out, cap, ctypes.byref(out_len), ends)

@@ -1133,7 +1133,17 @@ int32_t oracle_inflater_run_parts(const uint8_t* const* parts, const size_t* par
                                   int32_t raw, const uint8_t* dict, size_t dict_len,
                                   uint8_t* out, size_t out_cap, oracle_inflate_result* res,
                                   size_t* part_out, int32_t* err_part) {
+    return oracle_inflater_run_chunks(parts, part_lens, nparts, raw, dict, dict_len, out, out_cap, res,
+                                      part_out, err_part, NULL, NULL, 0, NULL);
+}
+
+int32_t oracle_inflater_run_chunks(const uint8_t* const* parts, const size_t* part_lens, int32_t nparts,
+                                   int32_t raw, const uint8_t* dict, size_t dict_len,
+                                   uint8_t* out, size_t out_cap, oracle_inflate_result* res,
+                                   size_t* part_out, int32_t* err_part,
+                                   size_t* chunk_sz, int32_t* chunk_part, size_t chunk_cap, size_t* nchunks) {
     memset(res, 0, sizeof *res);
+    if (nchunks) *nchunks = 0;
     if (err_part) *err_part = -1;
     if (part_out) for (int32_t k = 0; k < nparts; k++) part_out[k] = 0;
     if (raw && dict) { res->error = ORA_E_BAD_ARG; return res->error; }
@@ -1183,6 +1193,9 @@ int32_t oracle_inflater_run_parts(const uint8_t* const* parts, const size_t* par
                 if (out_len + cl > out_cap) { err_code = ORA_E_OUT_CAP; break; }
                 memcpy(out + out_len, z->next_out, cl);
                 out_len += cl;
+                /* the Uint8Array this iteration pushes (sd-inflate.ts:134) */
+                if (nchunks && *nchunks < chunk_cap) { chunk_sz[*nchunks] = cl; chunk_part[*nchunks] = pi; }
+                if (nchunks) (*nchunks)++;
             }
             /* DONE keeps returning STREAM_END without consuming input */
             if (zerr == Z_STREAM_END && z->next_out_index == 0 && z->avail_in > 0) {

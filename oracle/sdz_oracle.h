@@ -75,6 +75,15 @@ int32_t oracle_inflater_run_parts(const uint8_t* const* parts, const size_t* par
                                   uint8_t* out, size_t out_cap, oracle_inflate_result* res,
                                   size_t* part_out, int32_t* err_part);
 
+/* The same, also reporting the arrays append() returns: the length of each Uint8Array the
+ * reference pushes (sd-inflate.ts:101-150, one per 16 KiB ZStream pass that produced output)
+ * and the append it belongs to; *nchunks counts them all (entries past chunk_cap dropped). */
+int32_t oracle_inflater_run_chunks(const uint8_t* const* parts, const size_t* part_lens, int32_t nparts,
+                                   int32_t raw, const uint8_t* dict, size_t dict_len,
+                                   uint8_t* out, size_t out_cap, oracle_inflate_result* res,
+                                   size_t* part_out, int32_t* err_part,
+                                   size_t* chunk_sz, int32_t* chunk_part, size_t chunk_cap, size_t* nchunks);
+
 /* inflate(data, dictionary) one-shot: auto-detect + throw mapping (sd-inflate.ts:189-228). */
 int32_t oracle_inflate(const uint8_t* in, size_t in_len, const uint8_t* dict, size_t dict_len,
                        uint8_t* out, size_t out_cap, oracle_inflate_result* res);

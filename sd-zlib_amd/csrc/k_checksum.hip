@@ -14,15 +14,14 @@ namespace sdz {
 
 #define CK_THREADS 64
 
-__global__ __launch_bounds__(CK_THREADS) void k_checksum(const uint8_t* in, const uint64_t* in_off,
-                                                         const uint64_t* in_len, const int32_t* seed,
-                                                         int32_t* result, uint32_t n, int kind) {
+// block sid = blockIdx.x of a batch (in_off / in_len / seed / result indexed by it)
+__device__ __forceinline__ void k_checksum_body(const uint8_t* in, const uint64_t* in_off, const uint64_t* in_len,
+                                                const int32_t* seed, int32_t* result, int kind) {
     __shared__ CrcTables ct;
     uint32_t lane = threadIdx.x;
     if (kind != 0) crc_tables_init(ct);
     __syncthreads();
     uint32_t sid = blockIdx.x;
-    if (sid >= n) return;
     const uint8_t* p = in + in_off[sid];
     uint64_t len = in_len[sid];
     uint32_t sd = (uint32_t)(seed ? seed[sid] : (kind == 0 ? 1 : 0));
@@ -54,6 +53,29 @@ __global__ __launch_bounds__(CK_THREADS) void k_checksum(const uint8_t* in, cons
         const uint32_t crc = crc32_wave(p, len, ct);
         if (lane == 0) result[sid] = (int32_t)(gf2_mulmod(gf2_xbytes(len, ct.x2n), sd) ^ crc);
     }
+}
+
+__global__ __launch_bounds__(CK_THREADS) void k_checksum(const uint8_t* in, const uint64_t* in_off,
+                                                         const uint64_t* in_len, const int32_t* seed,
+                                                         int32_t* result, uint32_t n, int kind) {
+    if (blockIdx.x >= n) return;                         // (block-uniform: before any barrier)
+    k_checksum_body(in, in_off, in_len, seed, result, kind);
+}
+
+// one buffer, arguments by value: the DICTID of a preset dictionary, computed on the call's
+// stream so that no entry point waits for it on the host
+__global__ __launch_bounds__(CK_THREADS) void k_checksum_one(const uint8_t* in, uint64_t len, int32_t seed,
+                                                             int32_t* result, int kind) {
+    __shared__ uint64_t off_len[2];
+    __shared__ int32_t sd;
+    if (threadIdx.x == 0) { off_len[0] = 0; off_len[1] = len; sd = seed; }
+    __syncthreads();
+    // (the batched kernel's body, one buffer: it reads in_off / in_len / seed through pointers)
+    k_checksum_body(in, off_len, off_len + 1, &sd, result, kind);
+}
+
+void launch_checksum_one(const uint8_t* in, uint64_t len, int kind, int32_t seed, int32_t* result, hipStream_t s) {
+    hipLaunchKernelGGL(k_checksum_one, dim3(1), dim3(CK_THREADS), 0, s, in, len, seed, result, kind);
 }
 
 void launch_checksum(const uint8_t* in, const uint64_t* in_off, const uint64_t* in_len,

@@ -69,34 +69,36 @@ struct DSlab {                      // per-stream HBM state
 
 #define SLAB_BYTES ((sizeof(DSlab) + 255) & ~(uint64_t)255)
 
-// record path (levels 4-9, inputs <= 64 KiB): the stream's bookkeeping lives in its slab,
-// FStream over the window area and per-block code tables over the pending area.
+// record path (levels 4-9, inputs up to kDeflateRecMax): per stream a FStream header in its
+// slab, and per block a slot (FBlock + code table + header words) in the block area; records,
+// links and symbols in the record buffers (positions from rp0[k]).
 #define PM_TAIL (MAX_MATCH + MIN_MATCH + 1)       // last positions: searched by k_dfl_tail
-#define FB_MAXB 16                                  // blocks per stream (<= 9 for 64 KiB)
 #define FB_TAB_BYTES 2048                           // per block: codes + header words
 #define FB_HDR_OFF 1280                             // header words within a block's table
 #define FB_HDR_WORDS 176
+#define FB_SLOT (64 + FB_TAB_BYTES)                 // FBlock, then the table
 struct FBlock {
     uint32_t sym0, nsym;            // the block's symbols in the stream's symbol buffer
-    int32_t block_start, strstart;  // reference coordinates at the flush (rebased after the slide)
-    int32_t off;                    // original position of window index 0 at the flush
+    int32_t block_start, strstart;  // reference (window) coordinates at the flush
+    int64_t off;                    // original position of window index 0 at the flush
     uint32_t eof;
     uint32_t type;                  // k_dfl_trees: 0 stored, 1 static, 2 dynamic
     uint32_t hbits;                 // header bits (3 block-type bits + dynamic tree description)
     uint32_t dbits;                 // symbol bits incl. END_BLOCK (static / dynamic)
     uint32_t stored_len;
+    uint32_t carry;                 // k_dfl_encode: bi_valid at the block's start
+    uint64_t bstart;                // k_dfl_encode: the block's first bit in the output slot
 };
 struct FStream {
     uint32_t nblk;
     uint32_t flag;                  // nonzero: the stream is redone by the serial kernel
     uint32_t pad[2];
-    FBlock blk[FB_MAXB];
 };
-static_assert(sizeof(FStream) <= WINDOW_SIZE, "FStream fits the window area");
-static_assert(FB_MAXB * FB_TAB_BYTES <= PENDING_SIZE, "block tables fit the pending area");
+static_assert(sizeof(FBlock) <= 64, "FBlock fits its slot head");
 static_assert(FB_HDR_OFF >= (L_CODES + D_CODES) * 4 && FB_HDR_OFF + FB_HDR_WORDS * 4 <= FB_TAB_BYTES, "table layout");
 
 uint64_t deflate_state_bytes() { return SLAB_BYTES; }
+uint64_t deflate_rec_blocks(uint64_t len) { return len / 8192 + 2; }   // a non-final block covers >= 8192 symbols
 
 // tables shared by all streams (deftree.ts:25-38, 269-298, 319-337)
 struct DTables {
@@ -838,11 +840,11 @@ __global__ __launch_bounds__(DF_THREADS) void k_deflate(DeflateArgs A) {
     DF_STAMP(s, 0);
     // container header (sd-deflate.ts:98-152): written straight to the output slot
     // zlib: 78 01, or 78 20 + DICTID when the dictionary's adler32 is nonzero (sd-deflate.ts:98-115)
-    const bool dictid = A.format == SDZ_DEFLATE_ZLIB && A.dict && A.dict_adler != 0;
+    const bool dictid = A.format == SDZ_DEFLATE_ZLIB && A.dict && dict_id_of(A.dict_adler, A.dict_adler_dev) != 0;
     uint64_t hdr = A.format == SDZ_DEFLATE_ZLIB ? (dictid ? 6 : 2) : gzip ? 10 + (A.fname_len ? A.fname_len + 1 : 0) : 0;
     if (hdr > s.out_cap) { R.status = SDZ_OUT_OVERFLOW; A.rec[sid] = R; return; }
     if (dictid) {
-        const uint32_t d = (uint32_t)A.dict_adler;
+        const uint32_t d = (uint32_t)dict_id_of(A.dict_adler, A.dict_adler_dev);
         s.out[0] = 0x78; s.out[1] = 0x20;
         s.out[2] = (uint8_t)(d >> 24); s.out[3] = (uint8_t)(d >> 16); s.out[4] = (uint8_t)(d >> 8); s.out[5] = (uint8_t)d;
     } else if (A.format == SDZ_DEFLATE_ZLIB) { s.out[0] = 0x78; s.out[1] = 0x01; }
@@ -983,12 +985,12 @@ __global__ __launch_bounds__(DF_THREADS) void k_deflate_stream(DeflateArgs A, ui
         C.checksum = gzip ? 0 : 1;
         C.orig = 0;
         // container header (sd-deflate.ts:98-152), on the first append
-        const bool dictid = A.format == SDZ_DEFLATE_ZLIB && A.dict && A.dict_adler != 0;
+        const bool dictid = A.format == SDZ_DEFLATE_ZLIB && A.dict && dict_id_of(A.dict_adler, A.dict_adler_dev) != 0;
         const uint64_t hdr = A.format == SDZ_DEFLATE_ZLIB ? (dictid ? 6 : 2)
                            : gzip ? 10 + (A.fname_len ? A.fname_len + 1 : 0) : 0;
         if (hdr > s.out_cap) { R.status = SDZ_OUT_OVERFLOW; A.rec[sid] = R; return; }
         if (dictid) {
-            const uint32_t d = (uint32_t)A.dict_adler;
+            const uint32_t d = (uint32_t)dict_id_of(A.dict_adler, A.dict_adler_dev);
             s.out[0] = 0x78; s.out[1] = 0x20;
             s.out[2] = (uint8_t)(d >> 24); s.out[3] = (uint8_t)(d >> 16); s.out[4] = (uint8_t)(d >> 8); s.out[5] = (uint8_t)d;
         } else if (A.format == SDZ_DEFLATE_ZLIB) { s.out[0] = 0x78; s.out[1] = 0x01; }
@@ -1053,13 +1055,25 @@ void launch_deflate_stream(const DeflateArgs& a, uint32_t finish, hipStream_t s)
 
 // ------------------------------------------------------------------ record path kernels
 
-// k_dfl_chain: one wave per stream walks its positions in order, 1024 at a time: each lane
+// k_dfl_chain: one wave per chain unit walks its positions in order, 1024 at a time: each lane
 // hashes 16 consecutive positions from registers (the next chunk's bytes are already in
 // flight) into LDS, then 16 rounds of 64 positions swap themselves into the LDS head table.
 // Same-address lanes of one ds_wrxchg are served in lane order (tools/ubench/
 // lds_xchg_order.hip), so a lane receives the position of the previous lane with the same
-// hash, or the head: exactly insert_string's sequence.
+// hash, or the head: exactly insert_string's sequence (deflate_slow inserts every position
+// with lookahead >= MIN_MATCH, deflate.ts:1079-1085, 1124-1131).
+// Units: unit 0 of a stream covers positions [0, 64 Ki); unit j >= 1 covers
+// [64 Ki + (j - 1) 32 Ki, + 32 Ki) after hashing the 32 Ki before it (history: heads only), so
+// every unit's positions fit 16 bits relative to its history start h0 (0 = none: position h0
+// itself is never within MAX_DIST of a unit position, and position 0 is never matched, as
+// the reference's hash_head == 0 test, deflate.ts:1092).  The link stored for position P is
+// the distance to the previous same-hash position, 0 if none or farther than 32767 (beyond
+// MAX_DIST: every walk stops there, as the reference's does at `limit`, deflate.ts:941).
 #define CH_CHUNK 1024
+#define CH_UNIT 32768
+uint32_t deflate_chain_units(uint64_t len) {
+    return len <= 65536 ? 1u : 1u + (uint32_t)((len - 65536 + CH_UNIT - 1) / CH_UNIT);
+}
 __device__ __forceinline__ void ch_load(const GLB uint8_t* in, uint32_t n, uint32_t at, uint32_t (&w)[5]) {
     if (at + 20 <= n) {
         for (int i = 0; i < 5; ++i) __builtin_memcpy(&w[i], (const uint8_t*)(in + at + 4 * i), 4);
@@ -1074,10 +1088,10 @@ __device__ __forceinline__ void ch_load(const GLB uint8_t* in, uint32_t n, uint3
         }
     }
 }
-// Two streams share one block and one head table: wave w keeps its heads in half w of each
-// dword (positions < 2^16) and swaps them in with ds_mskor_rtn_b32, a masked exchange that,
-// like ds_wrxchg, serves same-address lanes in lane order.  That is two waves per CU where one
-// stream's 128 KiB table allowed one.  Each wave only syncs with itself.
+// Two units share one block and one head table: wave w keeps its heads in half w of each
+// dword and swaps them in with ds_mskor_rtn_b32, a masked exchange that, like ds_wrxchg,
+// serves same-address lanes in lane order.  That is two waves per CU where one unit's
+// 128 KiB table allowed one.  Each wave only syncs with itself.
 #define CH_WAVES 2
 __device__ __forceinline__ uint32_t lds_mskor_rtn(uint32_t* p, uint32_t mask, uint32_t v) {
     uint32_t r;
@@ -1089,22 +1103,27 @@ __global__ __launch_bounds__(64 * CH_WAVES) void k_dfl_chain(DeflateArgs A) {
     __shared__ __attribute__((aligned(16))) uint32_t head[HASH_SIZE];   // 128 KiB, a 16-bit half per wave
     __shared__ uint16_t hsw[CH_WAVES][CH_CHUNK];
     const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
-    const uint32_t sid = blockIdx.x * CH_WAVES + wv;
+    const uint32_t u = blockIdx.x * CH_WAVES + wv;
     for (uint32_t i = threadIdx.x; i < HASH_SIZE / 4; i += 64 * CH_WAVES) ((uint4*)head)[i] = make_uint4(0, 0, 0, 0);
     __syncthreads();
-    if (sid >= A.n) return;
-    const uint64_t in_len = A.in_len[sid];
-    if (in_len > A.rec_stride) return;
-    const GLB uint8_t* in = (const GLB uint8_t*)(A.in + A.in_off[sid]);
-    GLB uint16_t* pv = (GLB uint16_t*)A.pv_buf + (uint64_t)sid * A.rec_stride;
+    if (u >= A.ncunit) return;
+    const uint32_t k = A.cunit[u] >> kRecUnitShift, j = A.cunit[u] & ((1u << kRecUnitShift) - 1);
+    const uint64_t in_len = A.in_len[k];
+    const uint64_t rp = A.rp0[k];
+    if (rp == ~0ull) return;
+    const GLB uint8_t* in = (const GLB uint8_t*)(A.in + A.in_off[k]);
+    GLB uint16_t* pv = (GLB uint16_t*)A.pv_buf + rp;
     uint16_t* hs = hsw[wv];
     const uint32_t sh = 16u * wv, msk = 0xffffu << sh;
     const uint32_t n = (uint32_t)in_len;
+    const uint32_t a = j == 0 ? 0u : 65536u + (j - 1) * CH_UNIT;
+    const uint32_t e = j == 0 ? (n < 65536u ? n : 65536u) : (n - a < CH_UNIT ? n : a + CH_UNIT);
+    const uint32_t h0 = j == 0 ? 0u : a - 32768u;
     uint32_t w[5];
-    ch_load(in, n, 16 * lane, w);
-    for (uint32_t base = 0; base < n; base += CH_CHUNK) {
+    ch_load(in, n, h0 + 16 * lane, w);
+    for (uint32_t base = h0; base < e; base += CH_CHUNK) {
         uint32_t wn[5];
-        if (base + CH_CHUNK < n) ch_load(in, n, base + CH_CHUNK + 16 * lane, wn);
+        if (base + CH_CHUNK < e) ch_load(in, n, base + CH_CHUNK + 16 * lane, wn);
         for (int q = 0; q < 16; q += 2) {                // hashes of positions base + 16 lane + q
             uint32_t h2 = 0;
             for (int r = 0; r < 2; ++r) {
@@ -1123,17 +1142,22 @@ __global__ __launch_bounds__(64 * CH_WAVES) void k_dfl_chain(DeflateArgs A) {
         // order, so position order holds), then the stores: a few LDS round trips per chunk
         uint32_t hv[CH_CHUNK / 64], old[CH_CHUNK / 64];
 #pragma unroll
-        for (uint32_t j = 0; j < CH_CHUNK / 64; ++j) hv[j] = hs[64 * j + lane];
+        for (uint32_t t = 0; t < CH_CHUNK / 64; ++t) hv[t] = hs[64 * t + lane];
 #pragma unroll
-        for (uint32_t j = 0; j < CH_CHUNK / 64; ++j) {
-            const uint32_t p = base + 64 * j + lane;
-            old[j] = 0;
-            if (p + 2 < n) old[j] = lds_mskor_rtn(&head[hv[j]], msk, p << sh);   // insert_string runs while lookahead >= 3
+        for (uint32_t t = 0; t < CH_CHUNK / 64; ++t) {
+            const uint32_t p = base + 64 * t + lane;
+            old[t] = 0;
+            // insert_string runs while lookahead >= 3
+            if (p < e && p + 2 < n) old[t] = lds_mskor_rtn(&head[hv[t]], msk, (p - h0) << sh);
         }
 #pragma unroll
-        for (uint32_t j = 0; j < CH_CHUNK / 64; ++j) {
-            const uint32_t p = base + 64 * j + lane;
-            if (p < n) pv[p] = (uint16_t)(old[j] >> sh);
+        for (uint32_t t = 0; t < CH_CHUNK / 64; ++t) {
+            const uint32_t p = base + 64 * t + lane;
+            if (p >= a && p < e) {
+                const uint32_t q = (old[t] >> sh) & 0xffffu;          // relative to h0; 0 = none
+                const uint32_t d = q ? p - (q + h0) : 0u;
+                pv[p] = (uint16_t)(d <= 32767u ? d : 0u);
+            }
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
@@ -1170,15 +1194,21 @@ __device__ __forceinline__ uint32_t pm_w4(const uint8_t* w, uint32_t x) {   // 4
     const uint32_t* w32 = (const uint32_t*)w;
     return __builtin_amdgcn_alignbyte(w32[(x >> 2) + 1], w32[x >> 2], x & 3u);
 }
-__global__ __launch_bounds__(PM_THREADS) void k_dfl_match(DeflateArgs A, uint32_t nseg) {
+uint32_t deflate_match_segs(uint64_t len) {
+    const uint64_t tail = len > PM_TAIL ? len - PM_TAIL : 0;
+    return (uint32_t)((tail + PM_SEG - 1) / PM_SEG);
+}
+__global__ __launch_bounds__(PM_THREADS) void k_dfl_match(DeflateArgs A) {
     __shared__ __attribute__((aligned(16))) uint8_t win[(PM_WINB + 15) & ~15];
     __shared__ __attribute__((aligned(16))) uint16_t pvl[PM_PV];
     __shared__ int pm_next;                                 // first position not yet handed to a wave
-    const uint32_t sid = blockIdx.x / nseg, seg = blockIdx.x % nseg, tid = threadIdx.x;
+    const uint32_t tid = threadIdx.x;
     const uint32_t lane = tid & 63u, wv = tid >> 6;
-    if (sid >= A.n) return;
+    if (blockIdx.x >= A.nmseg) return;
+    const uint32_t sid = A.mseg[blockIdx.x] >> kRecUnitShift, seg = A.mseg[blockIdx.x] & ((1u << kRecUnitShift) - 1);
     const uint64_t in_len = A.in_len[sid];
-    if (in_len > A.rec_stride) return;
+    const uint64_t rp = A.rp0[sid];
+    if (rp == ~0ull) return;
     const int n = (int)in_len;
     const int tail = n > PM_TAIL ? n - PM_TAIL : 0;
     const int s0 = (int)(seg * PM_SEG), s1 = s0 + PM_SEG < tail ? s0 + PM_SEG : tail;
@@ -1186,7 +1216,7 @@ __global__ __launch_bounds__(PM_THREADS) void k_dfl_match(DeflateArgs A, uint32_
     const int ws = s0 > W_SIZE ? s0 - W_SIZE : 0;          // staged range [ws, we) (ws even)
     const int we = s1 + MAX_MATCH + 8 < n ? s1 + MAX_MATCH + 8 : n;
     const GLB uint8_t* in = (const GLB uint8_t*)(A.in + A.in_off[sid]);
-    const GLB uint16_t* pv = (const GLB uint16_t*)A.pv_buf + (uint64_t)sid * A.rec_stride;
+    const GLB uint16_t* pv = (const GLB uint16_t*)A.pv_buf + rp;
     {
         const int nw = (we - ws) >> 2;                     // whole dwords (unaligned global reads)
         uint32_t* w32 = (uint32_t*)win;
@@ -1196,24 +1226,25 @@ __global__ __launch_bounds__(PM_THREADS) void k_dfl_match(DeflateArgs A, uint32_
             w32[i] = v;
         }
         for (int i = 4 * nw + (int)tid; i < we - ws; i += PM_THREADS) win[i] = in[ws + i];
-        const int np = (s1 - ws) >> 1;                     // link pairs (ws even)
+        const int np = (s1 - ws) >> 1;                     // link pairs (ws even, rp a multiple of 64)
         uint32_t* p32 = (uint32_t*)pvl;
-        // links are staged relative to ws (0 for none, or at or below ws: below every walk's
-        // limit, and never a searchable head), so the walk indexes LDS with them directly
-        const uint32_t wsu = (uint32_t)ws;
+        // links (distances) are staged as the previous position relative to ws (0 for none,
+        // or at or below ws: below every walk's limit, and never a searchable head), so the
+        // walk indexes LDS with them directly
         for (int i = (int)tid; i < np; i += PM_THREADS) {
             const uint32_t v = *(const GLB uint32_t*)(pv + ws + 2 * i);
-            const uint32_t lo = v & 0xffffu, hi = v >> 16;
-            p32[i] = (lo > wsu ? lo - wsu : 0u) | ((hi > wsu ? hi - wsu : 0u) << 16);
+            const uint32_t lo = v & 0xffffu, hi = v >> 16;   // staged positions 2 i and 2 i + 1
+            const uint32_t r0 = 2u * (uint32_t)i, r1 = r0 + 1u;
+            p32[i] = (lo && lo < r0 ? r0 - lo : 0u) | ((hi && hi < r1 ? r1 - hi : 0u) << 16);
         }
         for (int i = 2 * np + (int)tid; i < s1 - ws; i += PM_THREADS) {
             const uint32_t v = pv[ws + i];
-            pvl[i] = (uint16_t)(v > wsu ? v - wsu : 0u);
+            pvl[i] = (uint16_t)(v && v < (uint32_t)i ? (uint32_t)i - v : 0u);
         }
         if (tid == 0) pm_next = s0 + (PM_THREADS / 64) * PM_CHUNK;
     }
     __syncthreads();
-    GLB uint64_t* rec = (GLB uint64_t*)A.rec_buf + (uint64_t)sid * A.rec_stride;
+    GLB uint64_t* rec = (GLB uint64_t*)A.rec_buf + rp;
     const int max_chain = c_config[A.level][3], qchain = max_chain >> 2, nice = c_config[A.level][2];
     // Positions in chunks of PM_CHUNK: each wave starts on its own chunk and takes the next
     // free one from an LDS counter when it has handed out its last position, so waves whose
@@ -1339,50 +1370,79 @@ __global__ __launch_bounds__(PM_THREADS) void k_dfl_match(DeflateArgs A, uint32_
 // bitstream -- its pending_buf overlay overtaken by the output, a pending_buf or
 // output slot overflow -- and is redone by the serial kernel (k_deflate, A.fast).
 
-// window byte i in the rebased coordinates of a search at a position with window offset off
-__device__ __forceinline__ uint32_t tail_byte(const GLB uint8_t* in, int n, int off, int i) {
-    const int P = i + off;
-    if (P < n) return in[P];
-    return (off && P >= WINDOW_SIZE) ? in[P - W_SIZE] : 0u;          // stale half after the slide
+// The window at the end of the input, in the reference's coordinates (deflate.ts:690-766): the
+// window (64 KiB, zero-filled at construction, deflate.ts:119) slides by 32 KiB when
+// fill_window finds strstart >= 65274 with lookahead < MIN_LOOKAHEAD; a slide copies the
+// upper half down and leaves the upper half as it was (stale), and fill_window then reads
+// input greedily.  After e slides (off = 32 Ki e) window index i holds input byte
+// i + off if i < F_e = min(64 Ki, n - off); otherwise what the same index held before the
+// last slide (index i + 32 Ki for the lower half, i for the upper half), back to zeros.
+// Only the last positions' searches (lookahead < MAX_MATCH) read past the input.
+__device__ uint32_t win_byte(const GLB uint8_t* in, int64_t n, int64_t off, int64_t i) {
+    for (int64_t e = off / W_SIZE;; --e) {
+        const int64_t base = e * W_SIZE;
+        const int64_t F = n - base < WINDOW_SIZE ? n - base : WINDOW_SIZE;
+        if (i < F) return in[base + i];
+        if (e == 0) return 0u;
+        if (i < W_SIZE) i += W_SIZE;
+    }
+}
+// window offset when the parse is at original position P: slide e happens at the first
+// visited position with strstart >= 65274 and lookahead < MIN_LOOKAHEAD in epoch e - 1 (both
+// grow with P, so every visited P has the offset this loop finds)
+__device__ __forceinline__ int64_t slide_off(int64_t n, int64_t P) {
+    int64_t off = 0;
+    for (;;) {
+        const int64_t fe = n < off + WINDOW_SIZE ? n : off + WINDOW_SIZE;
+        if (fe - P < MIN_LOOKAHEAD && P - off >= WINDOW_SIZE - MIN_LOOKAHEAD) off += W_SIZE;
+        else return off;
+    }
 }
 // deflate.ts:827-946 at original position P (lookahead >= MIN_MATCH), from best_len = 2, for
 // chain_length and chain_length >> 2 in one walk: the shorter walk is the longer one's first
-// qchain candidates.  Record word as in k_dfl_match (quarter in the high half).
-// The window slides when the parse reaches P >= 65274 with lookahead < MIN_LOOKAHEAD
-// (deflate.ts:711-738, 1075); the search runs in the coordinates the reference has then.
-__device__ uint64_t tail_search(const GLB uint8_t* in, const GLB uint16_t* pv, int n, int P, int chain_length, int nice) {
-    const int off = (P >= WINDOW_SIZE - MIN_LOOKAHEAD && n - P < MIN_LOOKAHEAD) ? W_SIZE : 0;
-    const int strstart = P - off;
-    auto rb = [&](int v) { return off ? (v >= W_SIZE ? v - W_SIZE : 0) : v; };
-    int cur = rb(pv[P]);
+// qchain candidates.  Record word as in k_dfl_match (quarter in the high half).  The search
+// runs in the window coordinates the reference has at P; pv holds each position's distance
+// to its previous same-hash position (0: none), and the reference's rebased links (0 below
+// the window) end a walk exactly where these would pass `limit`.
+__device__ uint64_t tail_search(const GLB uint8_t* in, const GLB uint16_t* pv, int64_t n, int64_t P, int chain_length,
+                                int nice) {
+    const int64_t off = slide_off(n, P);
+    const int strstart = (int)(P - off);
+    auto prev_of = [&](int64_t q) -> int {                // window index of q's predecessor (0: none)
+        const uint32_t d = pv[q];
+        const int64_t r = q - (int64_t)d;
+        return d && r > off ? (int)(r - off) : 0;
+    };
+    auto wb = [&](int i) -> uint32_t { return win_byte(in, n, off, i); };
+    int cur = prev_of(P);
     if (cur == 0 || ((strstart - cur) & 0xffff) > MAX_DIST) return 0u;      // no search (deflate.ts:1092)
-    const int lookahead = n - P;
+    const int lookahead = (int)(n - P);
     if (nice > lookahead) nice = lookahead;
     const int limit = strstart > MAX_DIST ? strstart - MAX_DIST : 0;
     const int qchain = chain_length >> 2;
     int best = MIN_MATCH - 1, bstart = 0, qbest = -1, qstart = 0, k = 0;
-    uint32_t scan_end1 = tail_byte(in, n, off, strstart + best - 1), scan_end = tail_byte(in, n, off, strstart + best);
-    const uint32_t c0 = tail_byte(in, n, off, strstart), c1 = tail_byte(in, n, off, strstart + 1);
+    uint32_t scan_end1 = wb(strstart + best - 1), scan_end = wb(strstart + best);
+    const uint32_t c0 = wb(strstart), c1 = wb(strstart + 1);
     // The link and the four checked bytes of a candidate are loaded together, and a long
     // compare takes 4 byte pairs per step, so the walk waits on one memory round trip per
     // candidate rather than on one per load.
     do {
         const int match = cur;
-        const int nx = rb(pv[cur + off]);
-        const uint32_t e0 = tail_byte(in, n, off, match + best), e1 = tail_byte(in, n, off, match + best - 1);
-        const uint32_t m0 = tail_byte(in, n, off, match), m1 = tail_byte(in, n, off, match + 1);
+        const int nx = prev_of(match + off);
+        const uint32_t e0 = wb(match + best), e1 = wb(match + best - 1);
+        const uint32_t m0 = wb(match), m1 = wb(match + 1);
         if ((e0 == scan_end) & (e1 == scan_end1) & (m0 == c0) & (m1 == c1)) {
             int len = 3;                      // byte 2 is not compared (equal hash, deflate.ts:891-897)
             for (bool go = true; go && len < MAX_MATCH;) {
-                uint32_t a[4], b[4];
+                uint32_t x[4], y[4];
 #pragma unroll
                 for (int i = 0; i < 4; ++i) {
-                    a[i] = tail_byte(in, n, off, strstart + len + i);
-                    b[i] = tail_byte(in, n, off, match + len + i);
+                    x[i] = wb(strstart + len + i);
+                    y[i] = wb(match + len + i);
                 }
 #pragma unroll
                 for (int i = 0; i < 4; ++i) {
-                    if (go && len < MAX_MATCH && a[i] == b[i]) ++len;
+                    if (go && len < MAX_MATCH && x[i] == y[i]) ++len;
                     else go = false;
                 }
             }
@@ -1390,8 +1450,8 @@ __device__ uint64_t tail_search(const GLB uint8_t* in, const GLB uint16_t* pv, i
                 bstart = match;
                 best = len;
                 if (len >= nice) break;
-                scan_end1 = tail_byte(in, n, off, strstart + best - 1);
-                scan_end = tail_byte(in, n, off, strstart + best);
+                scan_end1 = wb(strstart + best - 1);
+                scan_end = wb(strstart + best);
             }
         }
         if (++k == qchain) { qbest = best; qstart = bstart; }
@@ -1405,130 +1465,199 @@ __device__ uint64_t tail_search(const GLB uint8_t* in, const GLB uint16_t* pv, i
 __global__ __launch_bounds__(256) void k_dfl_tail(DeflateArgs A) {
     const uint32_t sid = blockIdx.x;
     if (sid >= A.n) return;
-    const uint64_t in_len = A.in_len[sid];
-    if (in_len > A.rec_stride) return;
-    const int n = (int)in_len, tail = n > PM_TAIL ? n - PM_TAIL : 0;
+    const uint64_t rp = A.rp0[sid];
+    if (rp == ~0ull) return;
+    const int64_t n = (int64_t)A.in_len[sid], tail = n > PM_TAIL ? n - PM_TAIL : 0;
     const GLB uint8_t* in = (const GLB uint8_t*)(A.in + A.in_off[sid]);
-    const GLB uint16_t* pv = (const GLB uint16_t*)A.pv_buf + (uint64_t)sid * A.rec_stride;
-    GLB uint64_t* rec = (GLB uint64_t*)A.rec_buf + (uint64_t)sid * A.rec_stride;
+    const GLB uint16_t* pv = (const GLB uint16_t*)A.pv_buf + rp;
+    GLB uint64_t* rec = (GLB uint64_t*)A.rec_buf + rp;
     const int max_chain = c_config[A.level][3], nice = c_config[A.level][2];
     // the last MIN_MATCH - 1 positions are not searched; their records carry only the byte
-    for (int P = tail + (int)threadIdx.x; P < n; P += 256) {
+    for (int64_t P = tail + (int64_t)threadIdx.x; P < n; P += 256) {
         const uint64_t r = P <= n - MIN_MATCH ? tail_search(in, pv, n, P, max_chain, nice) : 0ull;
         rec[P] = rec_word((uint32_t)r, (uint32_t)(r >> 32), in[P > 0 ? P - 1 : 0]);
     }
 }
 
-// k_dfl_parse: one lane per stream, the reference's loop with its scalars in registers.
-// At each position the record gives longest_match(prev_length): the record's candidate if
-// it is longer than prev_length, else prev_length, clamped to the lookahead.  (In the tail
-// with prev_length >= min(nice, lookahead) the reference returns the lookahead, and so does
-// this; otherwise its walk stops at the same candidate as the record's.)  Positions with
-// lookahead < MIN_MATCH are not searched here: the reference's result there is <= 2 either
-// way and nothing downstream tells the values apart.
+// k_dfl_parse: the reference's loop (deflate_slow, deflate.ts:1054-1182) with its scalars in
+// registers, one record load per step.  At each position the record gives
+// longest_match(prev_length): the record's candidate if it is longer than prev_length, else
+// prev_length, clamped to the lookahead.  (In the tail with prev_length >= min(nice,
+// lookahead) the reference returns the lookahead, and so does this; otherwise its walk stops
+// at the same candidate as the record's.)  Positions with lookahead < MIN_MATCH are not
+// searched here: the reference's result there is <= 2 either way and nothing downstream
+// tells the values apart.
+// Positions are original (absolute) ones.  The reference's window slides when fill_window
+// finds strstart >= 65274 with lookahead < MIN_LOOKAHEAD (deflate.ts:708-737); that changes
+// no decision (a search reads no byte past the input unless lookahead < MAX_MATCH, and
+// lookahead is n - P whenever it matters), only the window coordinates a flush records
+// (block_start < 0: no stored block, deflate.ts:648).
 // Symbols go to the stream's symbol buffer -- the front of its record buffer: symbol k is
 // written after record k/2 has been read -- as lc | dist << 8 (dist 0: literal lc).
+struct PState {
+    int n, level, good, max_lazy;
+    int strstart, match_length, match_start, match_available, block_start;
+    int64_t off;
+    uint32_t last_lit, matches, lx, nblk, sym0, nbcap;
+    // TRUNCATE_BLOCK's estimate needs only sum over the block's matches of 5 + extra bits of
+    // the distance code (deflate.ts:503-506), kept as a running sum: extra bits of distance
+    // d + 1 are 0 for d < 4, else floor(log2 d) - 1 (no dist_code table, no per-code counts)
+    uint32_t dxb;
+    GLB uint32_t* sym;
+    uint8_t* blk;                 // this stream's first block slot
+};
+__device__ __forceinline__ void ps_init(PState& st, const DeflateArgs& A, uint32_t sid, int n) {
+    st.n = n; st.level = A.level; st.good = c_config[A.level][0]; st.max_lazy = c_config[A.level][1];
+    st.strstart = 0; st.match_length = MIN_MATCH - 1; st.match_start = 0; st.match_available = 0;
+    st.block_start = 0; st.off = 0;
+    st.last_lit = 0; st.matches = 0; st.lx = 0; st.nblk = 0; st.sym0 = 0; st.dxb = 0;
+    st.sym = (GLB uint32_t*)A.rec_buf + 2 * A.rp0[sid];
+    st.blk = A.blk + (uint64_t)A.tb0[sid] * FB_SLOT;
+    st.nbcap = A.tb0[sid + 1] - A.tb0[sid];
+}
+__device__ __forceinline__ bool ps_tally(PState& st, int dist, int lc) {      // _tr_tally, deflate.ts:488-524
+    st.sym[st.lx++] = (uint32_t)lc | ((uint32_t)dist << 8);
+    st.last_lit++;
+    if (dist) {
+        st.matches++;
+        const uint32_t d = (uint32_t)(dist - 1);
+        st.dxb += 5u + (d < 4u ? 0u : 30u - (uint32_t)__builtin_clz(d));
+    }
+    if ((st.last_lit & 0x1fff) == 0 && st.level > 2) {                       // TRUNCATE_BLOCK
+        uint32_t out_length = st.last_lit * 8 + st.dxb;
+        const int in_length = st.strstart - st.block_start;
+        out_length >>= 3;
+        if (st.matches < st.last_lit / 2 && (int)out_length < in_length / 2) return true;
+    }
+    return st.last_lit == LIT_BUFSIZE - 1;
+}
+__device__ __forceinline__ void ps_flush(PState& st, uint32_t eof) {          // flush_block_only's bookkeeping
+    if (st.nblk < st.nbcap) {
+        GLB FBlock* B = (GLB FBlock*)(st.blk + (uint64_t)st.nblk * FB_SLOT);
+        B->sym0 = st.sym0; B->nsym = st.last_lit;
+        B->block_start = (int32_t)(st.block_start - st.off); B->strstart = (int32_t)(st.strstart - st.off);
+        B->off = st.off; B->eof = eof;
+    }
+    st.nblk++;
+    st.sym0 = st.lx; st.last_lit = 0; st.matches = 0; st.dxb = 0;
+    st.block_start = st.strstart;
+}
+// the step's fill_window: true when the input is used up (lookahead == 0)
+__device__ __forceinline__ bool ps_fill(PState& st) {
+    const int64_t fe = (int64_t)st.n < st.off + WINDOW_SIZE ? (int64_t)st.n : st.off + WINDOW_SIZE;
+    if (fe - st.strstart < MIN_LOOKAHEAD) {
+        if (st.strstart - st.off >= WINDOW_SIZE - MIN_LOOKAHEAD) st.off += W_SIZE;   // the slide
+        if (st.strstart == st.n) return true;
+    }
+    return false;
+}
+// one step at position strstart with its record r (rec_word) and the literal byte lb
+__device__ __forceinline__ void ps_step(PState& st, uint64_t r) {
+    const uint32_t lb = ((uint32_t)r >> 25) | (((uint32_t)(r >> 32) >> 18) & 128u);
+    const int lookahead = st.n - st.strstart;
+    const int prev_length = st.match_length, prev_match = st.match_start;
+    st.match_length = MIN_MATCH - 1;
+    // The reference also requires hash_head != 0 and (strstart - hash_head) <= MAX_DIST
+    // (deflate.ts:1092).  Where that fails the record is 0 (k_dfl_match / k_dfl_tail test
+    // the same), and a 0 record gives the step the same outcome as no search: match_length
+    // ends <= prev_length, so with prev_length >= MIN_MATCH the previous match is emitted
+    // either way, and otherwise it stays MIN_MATCH - 1.  So the link load is not needed.
+    if (lookahead >= MIN_MATCH && prev_length < st.max_lazy) {
+        const uint32_t e = prev_length >= st.good ? (uint32_t)(r >> 32) : (uint32_t)r;
+        const int len = (int)((e >> 16) & 511u);
+        int ml = prev_length;
+        if (len > prev_length) { ml = len; st.match_start = st.strstart - (int)(e & 0xffffu); }
+        st.match_length = ml < lookahead ? ml : lookahead;
+        if (st.match_length <= 5 && st.match_length == MIN_MATCH && st.strstart - st.match_start > 4096)
+            st.match_length = MIN_MATCH - 1;
+    }
+    if (prev_length >= MIN_MATCH && st.match_length <= prev_length) {
+        const bool bflush = ps_tally(st, st.strstart - 1 - prev_match, prev_length - MIN_MATCH);
+        // strstart+1 .. strstart+prev_length-2 are inserted (up to max_insert); their links
+        // are already in the chain buffer (k_dfl_chain), and the records carry the search
+        // test, so nothing is read here
+        st.strstart += prev_length - 1;
+        st.match_available = 0;
+        st.match_length = MIN_MATCH - 1;
+        if (bflush) ps_flush(st, 0);
+    } else if (st.match_available) {
+        const bool bflush = ps_tally(st, 0, (int)lb);
+        if (bflush) ps_flush(st, 0);
+        st.strstart++;
+    } else {
+        st.match_available = 1;
+        st.strstart++;
+    }
+}
+__device__ __forceinline__ void ps_finish(PState& st, const GLB uint8_t* in, GLB FStream* F) {
+    if (st.match_available) ps_tally(st, 0, in[st.strstart - 1]);
+    ps_flush(st, 1);
+    F->nblk = st.nblk;
+    F->flag = st.nblk > st.nbcap ? 1u : 0u;
+}
+// many streams: one lane each
 __global__ __launch_bounds__(64) void k_dfl_parse(DeflateArgs A) {
     const uint32_t lane = threadIdx.x, sid = blockIdx.x * 64 + lane;
     if (sid >= A.n) return;
     GLB DSlab* S = (GLB DSlab*)(A.state + (uint64_t)sid * SLAB_BYTES);
     GLB FStream* F = (GLB FStream*)S->window;
     const uint64_t in_len = A.in_len[sid];
-    if (in_len == 0 || in_len > A.rec_stride) { F->nblk = 0; F->flag = 1; return; }
+    if (in_len == 0 || A.rp0[sid] == ~0ull) { F->nblk = 0; F->flag = 1; return; }
+    const GLB uint8_t* in = (const GLB uint8_t*)(A.in + A.in_off[sid]);
+    const GLB uint64_t* rec = (const GLB uint64_t*)A.rec_buf + A.rp0[sid];
+    PState st;
+    ps_init(st, A, sid, (int)in_len);
+    for (;;) {
+        if (ps_fill(st)) break;
+        uint64_t r = rec[st.strstart];                        // the step's one load (rec_word)
+        asm volatile("" : "+v"(r));                           // here, not sunk into the branches
+        ps_step(st, r);
+    }
+    ps_finish(st, in, F);
+}
+// few long streams (the facade's one-buffer deflate()): one workgroup per stream; waves 1..3
+// stage the records in LDS chunks ahead of lane 0, which parses from LDS (a lone lane waits
+// on every dependent HBM load otherwise)
+#define PW_THREADS 256
+#define PW_CHUNK 4096                                    // records per LDS chunk (>= MAX_MATCH)
+__global__ __launch_bounds__(PW_THREADS) void k_dfl_parse_wide(DeflateArgs A) {
+    __shared__ uint64_t buf[2][PW_CHUNK];
+    const uint32_t sid = blockIdx.x, tid = threadIdx.x;
+    if (sid >= A.n) return;
+    GLB DSlab* S = (GLB DSlab*)(A.state + (uint64_t)sid * SLAB_BYTES);
+    GLB FStream* F = (GLB FStream*)S->window;
+    const uint64_t in_len = A.in_len[sid];
+    if (in_len == 0 || A.rp0[sid] == ~0ull) { if (tid == 0) { F->nblk = 0; F->flag = 1; } return; }
     const int n = (int)in_len;
     const GLB uint8_t* in = (const GLB uint8_t*)(A.in + A.in_off[sid]);
-    const GLB uint64_t* rec = (const GLB uint64_t*)A.rec_buf + (uint64_t)sid * A.rec_stride;
-    GLB uint32_t* sym = (GLB uint32_t*)A.rec_buf + (uint64_t)sid * A.rec_stride * 2;
-    const int level = A.level, good = c_config[level][0], max_lazy = c_config[level][1];
-    int strstart = 0, lookahead = n, match_length = MIN_MATCH - 1, match_start = 0, match_available = 0;
-    int block_start = 0, off = 0;
-    uint32_t last_lit = 0, matches = 0, lx = 0, nblk = 0, sym0 = 0;
-    // TRUNCATE_BLOCK's estimate needs only sum over the block's matches of 5 + extra bits of
-    // the distance code (deflate.ts:503-506), kept as a running sum: extra bits of distance
-    // d + 1 are 0 for d < 4, else floor(log2 d) - 1 (no dist_code table, no per-code counts)
-    uint32_t dxb = 0;
-    auto tally = [&](int dist, int lc) -> bool {             // _tr_tally, deflate.ts:488-524
-        sym[lx++] = (uint32_t)lc | ((uint32_t)dist << 8);
-        last_lit++;
-        if (dist) {
-            matches++;
-            const uint32_t d = (uint32_t)(dist - 1);
-            dxb += 5u + (d < 4u ? 0u : 30u - (uint32_t)__builtin_clz(d));
+    const GLB uint64_t* rec = (const GLB uint64_t*)A.rec_buf + A.rp0[sid];
+    const int nch = (n + PW_CHUNK - 1) / PW_CHUNK;
+    for (int i = (int)tid; i < PW_CHUNK && i < n; i += PW_THREADS) buf[0][i] = rec[i];
+    __syncthreads();
+    PState st;
+    bool done = false;
+    if (tid == 0) ps_init(st, A, sid, n);
+    for (int c = 0; c < nch; ++c) {
+        const int c1 = c + 1;
+        if (tid >= 64 && c1 < nch) {                    // stage the next chunk
+            const int b0 = c1 * PW_CHUNK, m = n - b0 < PW_CHUNK ? n - b0 : PW_CHUNK;
+            for (int i = (int)tid - 64; i < m; i += PW_THREADS - 64) buf[c1 & 1][i] = rec[b0 + i];
         }
-        if ((last_lit & 0x1fff) == 0 && level > 2) {         // TRUNCATE_BLOCK
-            uint32_t out_length = last_lit * 8 + dxb;
-            const int in_length = strstart - block_start;
-            out_length >>= 3;
-            if (matches < last_lit / 2 && (int)out_length < in_length / 2) return true;
-        }
-        return last_lit == LIT_BUFSIZE - 1;
-    };
-    auto flush = [&](uint32_t eof) {                        // flush_block_only's bookkeeping
-        if (nblk < FB_MAXB) {
-            GLB FBlock* B = &F->blk[nblk];
-            B->sym0 = sym0; B->nsym = last_lit;
-            B->block_start = block_start; B->strstart = strstart; B->off = off; B->eof = eof;
-        }
-        nblk++;
-        sym0 = lx; last_lit = 0; matches = 0; dxb = 0;
-        block_start = strstart;
-    };
-    for (;;) {
-        if (lookahead < MIN_LOOKAHEAD) {                     // fill_window: input exhausted; it may slide
-            if (!off && strstart >= W_SIZE + W_SIZE - MIN_LOOKAHEAD) {
-                match_start -= W_SIZE;
-                strstart -= W_SIZE;
-                block_start -= W_SIZE;
-                off = W_SIZE;
+        if (tid == 0 && !done) {
+            const int end = (c + 1) * PW_CHUNK, b0 = c * PW_CHUNK;
+            const uint64_t* cb = buf[c & 1];
+            for (;;) {
+                if (st.strstart >= end) break;             // the next chunk (a step moves <= MAX_MATCH)
+                if (ps_fill(st)) { done = true; break; }
+                ps_step(st, cb[st.strstart - b0]);
             }
-            if (lookahead == 0) break;
         }
-        const int P = strstart + off;                        // everything this step reads, at once
-        uint64_t r = rec[P];                                  // the step's one load (rec_word)
-        asm volatile("" : "+v"(r));                           // here, not sunk into the branches
-        const uint32_t lb = ((uint32_t)r >> 25) | (((uint32_t)(r >> 32) >> 18) & 128u);
-        const int prev_length = match_length, prev_match = match_start;
-        match_length = MIN_MATCH - 1;
-        // The reference also requires hash_head != 0 and (strstart - hash_head) <= MAX_DIST
-        // (deflate.ts:1092).  Where that fails the record is 0 (k_dfl_match / k_dfl_tail test
-        // the same), and a 0 record gives the step the same outcome as no search: match_length
-        // ends <= prev_length, so with prev_length >= MIN_MATCH the previous match is emitted
-        // either way, and otherwise it stays MIN_MATCH - 1.  So the link load is not needed.
-        if (lookahead >= MIN_MATCH && prev_length < max_lazy) {
-            const uint32_t e = prev_length >= good ? (uint32_t)(r >> 32) : (uint32_t)r;
-            const int len = (int)((e >> 16) & 511u);
-            int ml = prev_length;
-            if (len > prev_length) { ml = len; match_start = strstart - (int)(e & 0xffffu); }
-            match_length = ml < lookahead ? ml : lookahead;
-            if (match_length <= 5 && match_length == MIN_MATCH && strstart - match_start > 4096)
-                match_length = MIN_MATCH - 1;
-        }
-        if (prev_length >= MIN_MATCH && match_length <= prev_length) {
-            const bool bflush = tally(strstart - 1 - prev_match, prev_length - MIN_MATCH);
-            lookahead -= prev_length - 1;
-            // strstart+1 .. strstart+prev_length-2 are inserted (up to max_insert); their links
-            // are already in the chain buffer (k_dfl_chain), and the records carry the search
-            // test, so nothing is read here
-            const int last = strstart + prev_length - 2;
-            strstart = last + 1;
-            match_available = 0;
-            match_length = MIN_MATCH - 1;
-            if (bflush) flush(0);
-        } else if (match_available) {
-            const bool bflush = tally(0, (int)lb);
-            if (bflush) flush(0);
-            strstart++;
-            lookahead--;
-        } else {
-            match_available = 1;
-            strstart++;
-            lookahead--;
-        }
+        __syncthreads();
     }
-    if (match_available) tally(0, in[strstart - 1 + off]);
-    flush(1);
-    F->nblk = nblk;
-    F->flag = nblk > FB_MAXB ? 1u : 0u;
+    if (tid == 0) {
+        // (the records past the last chunk: none -- a stream's positions end at n)
+        ps_finish(st, in, F);
+    }
 }
 
 // tree context of the record path: LDS arrays, header bits into LDS words
@@ -1549,7 +1678,7 @@ struct LTreeCtx {
 // atomics), then lane 0 runs build_tree / scan_tree / build_bl_tree and the block type choice
 // exactly as _tr_flush_block does, and the wave exports the code table (code | len << 16)
 // and the block header bits.
-__global__ __launch_bounds__(64) void k_dfl_trees(DeflateArgs A) {
+__global__ __launch_bounds__(64) void k_dfl_trees(DeflateArgs A) {   // grid (n, ny): blocks y, y + ny, ...
     __shared__ uint16_t ltree[HEAP_SIZE * 2], dtree[(2 * D_CODES + 1) * 2], bltree[(2 * BL_CODES + 1) * 2];
     __shared__ uint16_t depth[2 * L_CODES + 1], heap[2 * L_CODES + 1], bl_count[16], next_code[16];
     __shared__ uint32_t hist[L_CODES + D_CODES];
@@ -1564,11 +1693,12 @@ __global__ __launch_bounds__(64) void k_dfl_trees(DeflateArgs A) {
     const GLB DTables* T = (const GLB DTables*)&g_dt;
     for (int i = (int)lane; i < 256; i += 64) lcode_t[i] = T->length_code[i];
     for (int i = (int)lane; i < 512; i += 64) dcode_t[i] = T->dist_code[i];
-    const GLB uint32_t* sym = (const GLB uint32_t*)A.rec_buf + (uint64_t)sid * A.rec_stride * 2;
+    const GLB uint32_t* sym = (const GLB uint32_t*)A.rec_buf + 2 * A.rp0[sid];
     const uint32_t nblk = F->nblk;
-    for (uint32_t b = 0; b < nblk; ++b) {
-        const uint32_t sym0 = F->blk[b].sym0, nsym = F->blk[b].nsym, eof = F->blk[b].eof;
-        const int block_start = F->blk[b].block_start, strstart = F->blk[b].strstart;
+    for (uint32_t b = blockIdx.y; b < nblk; b += gridDim.y) {
+        GLB FBlock* Bk = (GLB FBlock*)(A.blk + ((uint64_t)A.tb0[sid] + b) * FB_SLOT);
+        const uint32_t sym0 = Bk->sym0, nsym = Bk->nsym, eof = Bk->eof;
+        const int block_start = Bk->block_start, strstart = Bk->strstart;
         for (int i = (int)lane; i < L_CODES + D_CODES; i += 64) hist[i] = 0;
         for (int i = (int)lane; i < FB_HDR_WORDS; i += 64) hdr[i] = 0;
         for (int i = (int)lane; i < HEAP_SIZE * 2; i += 64) ltree[i] = 0;
@@ -1634,7 +1764,7 @@ __global__ __launch_bounds__(64) void k_dfl_trees(DeflateArgs A) {
         }
         __syncthreads();
         const uint32_t type = info[0], hbits = info[1];
-        GLB uint32_t* tab = (GLB uint32_t*)(S->pending + b * FB_TAB_BYTES);
+        GLB uint32_t* tab = (GLB uint32_t*)((GLB uint8_t*)Bk + 64);
         if (type != 0)
             for (int i = (int)lane; i < L_CODES + D_CODES; i += 64) {
                 uint32_t code, len;
@@ -1650,7 +1780,7 @@ __global__ __launch_bounds__(64) void k_dfl_trees(DeflateArgs A) {
             }
         for (uint32_t i = lane; i < (hbits + 31) / 32; i += 64) tab[FB_HDR_OFF / 4 + i] = hdr[i];
         if (lane == 0) {
-            F->blk[b].type = type; F->blk[b].hbits = hbits; F->blk[b].dbits = info[2]; F->blk[b].stored_len = info[3];
+            Bk->type = type; Bk->hbits = hbits; Bk->dbits = info[2]; Bk->stored_len = info[3];
         }
         __syncthreads();
     }
@@ -1681,8 +1811,7 @@ __global__ __launch_bounds__(EN_THREADS) void k_dfl_encode(DeflateArgs A) {
     __shared__ uint32_t codes[L_CODES + D_CODES];
     __shared__ uint8_t lcode_t[256], dcode_t[512];
     __shared__ uint16_t lbase[29], dbase[30];
-    __shared__ uint64_t bstart[FB_MAXB];
-    __shared__ uint32_t bcarry[FB_MAXB], wsum[EN_THREADS / 64];
+    __shared__ uint32_t wsum[EN_THREADS / 64];
     __shared__ uint32_t stg[EN_STG_WORDS];
     __shared__ uint64_t sh_end;
     __shared__ uint32_t sh_bad;
@@ -1701,28 +1830,32 @@ __global__ __launch_bounds__(EN_THREADS) void k_dfl_encode(DeflateArgs A) {
     const uint32_t hdr_bytes = A.format == SDZ_DEFLATE_ZLIB ? 2 : gzip ? 10 + (A.fname_len ? A.fname_len + 1 : 0) : 0;
     const uint32_t trl_bytes = A.format == SDZ_DEFLATE_ZLIB ? 4 : gzip ? 8 : 0;
     const uint64_t in_len = A.in_len[sid];
+    GLB uint8_t* slots = (GLB uint8_t*)(A.blk + (uint64_t)A.tb0[sid] * FB_SLOT);
+    auto blk_at = [&](uint32_t b) { return (GLB FBlock*)(slots + (uint64_t)b * FB_SLOT); };
     if (tid == 0) {
         uint64_t Tb = 8ull * hdr_bytes, al = Tb;             // bit position; last byte alignment
         uint32_t bad = 0;
         for (uint32_t b = 0; b < nblk; ++b) {
-            bstart[b] = Tb;
+            GLB FBlock* Bk = blk_at(b);
+            Bk->bstart = Tb;
             const uint32_t carry = (uint32_t)((Tb - al) & 15);  // bi_valid at the block's start
-            bcarry[b] = carry;
-            if (F->blk[b].type == 0) {
+            Bk->carry = carry;
+            if (Bk->type == 0) {
                 const uint32_t K = carry + 3, rem = K & 15;
                 const uint32_t pend = 2 * (K >> 4) + (rem > 8 ? 2 : rem > 0 ? 1 : 0) + 4;
-                if (pend + F->blk[b].stored_len > PENDING_SIZE) bad = 1;
-                Tb = ((Tb + 3 + 7) & ~7ull) + 32 + 8ull * F->blk[b].stored_len;
+                if (pend + Bk->stored_len > PENDING_SIZE) bad = 1;
+                Tb = ((Tb + 3 + 7) & ~7ull) + 32 + 8ull * Bk->stored_len;
                 al = Tb;
             } else {
-                Tb += F->blk[b].hbits + F->blk[b].dbits;
+                Tb += Bk->hbits + Bk->dbits;
             }
-            if (F->blk[b].eof) { Tb = (Tb + 7) & ~7ull; al = Tb; }
+            if (Bk->eof) { Tb = (Tb + 7) & ~7ull; al = Tb; }
         }
         if (Tb / 8 + trl_bytes > A.out_cap[sid]) bad = 1;
         sh_end = Tb;
         sh_bad = bad;
     }
+    __threadfence();                                         // (block layout: read by all threads)
     __syncthreads();
     if (sh_bad) { if (tid == 0) F->flag = 1; return; }
     const uint64_t total = sh_end / 8 + trl_bytes;
@@ -1755,17 +1888,18 @@ __global__ __launch_bounds__(EN_THREADS) void k_dfl_encode(DeflateArgs A) {
             for (uint32_t i = 0; i < A.fname_len; i++) orbits(80 + 8 * i, A.fname[i]);
         }
     }
-    const GLB uint32_t* sym = (const GLB uint32_t*)A.rec_buf + (uint64_t)sid * A.rec_stride * 2;
+    const GLB uint32_t* sym = (const GLB uint32_t*)A.rec_buf + 2 * A.rp0[sid];
     uint32_t bad = 0;
     for (uint32_t b = 0; b < nblk; ++b) {
-        const uint32_t type = F->blk[b].type, hbits = F->blk[b].hbits;
-        const GLB uint32_t* tab = (const GLB uint32_t*)(S->pending + b * FB_TAB_BYTES);
-        const uint64_t b0 = bstart[b];
+        const GLB FBlock* Bk = blk_at(b);
+        const uint32_t type = Bk->type, hbits = Bk->hbits;
+        const GLB uint32_t* tab = (const GLB uint32_t*)((const GLB uint8_t*)Bk + 64);
+        const uint64_t b0 = Bk->bstart;
         for (uint32_t i = tid; i < (hbits + 31) / 32; i += EN_THREADS) orbits(b0 + 32 * i, tab[FB_HDR_OFF / 4 + i]);
         if (type == 0) {                                     // _tr_stored_block: aligned LEN NLEN bytes
-            const uint32_t len = F->blk[b].stored_len;
+            const uint32_t len = Bk->stored_len;
             const uint64_t pay = ((b0 + 3 + 7) & ~7ull) / 8;
-            const GLB uint8_t* src = (const GLB uint8_t*)(A.in + A.in_off[sid]) + F->blk[b].off + F->blk[b].block_start;
+            const GLB uint8_t* src = (const GLB uint8_t*)(A.in + A.in_off[sid]) + Bk->off + Bk->block_start;
             for (uint32_t i = tid; i < 4 + len; i += EN_THREADS) {
                 uint8_t v;
                 if (i < 4) v = (uint8_t)((i < 2 ? len : ~len) >> (8 * (i & 1)));
@@ -1777,7 +1911,7 @@ __global__ __launch_bounds__(EN_THREADS) void k_dfl_encode(DeflateArgs A) {
         }
         for (uint32_t i = tid; i < L_CODES + D_CODES; i += EN_THREADS) codes[i] = tab[i];
         __syncthreads();
-        const uint32_t sym0 = F->blk[b].sym0, nsym = F->blk[b].nsym, items = nsym + 1;   // + END_BLOCK
+        const uint32_t sym0 = Bk->sym0, nsym = Bk->nsym, items = nsym + 1;   // + END_BLOCK
         auto sym_bits = [&](uint32_t j, uint32_t& lo, uint32_t& nlo, uint32_t& hi, uint32_t& nhi) {
             if (j == nsym) { const uint32_t c = codes[END_BLOCK]; lo = c & 0xffffu; nlo = c >> 16; nhi = 0; hi = 0; return; }
             const uint32_t s = sym[sym0 + j], lc = s & 255u, dist = s >> 8;
@@ -1792,7 +1926,7 @@ __global__ __launch_bounds__(EN_THREADS) void k_dfl_encode(DeflateArgs A) {
         };
         // rows of EN_THREADS symbols (coalesced reads): scan the bit counts, OR each symbol's
         // bits into an LDS image of the row, write the image out (edge words OR-ed)
-        const uint32_t carry = bcarry[b];
+        const uint32_t carry = Bk->carry;
         uint64_t rowbit = b0 + hbits;                        // slot-relative bit of the row's start
         for (uint32_t r0 = 0; r0 < items; r0 += EN_THREADS) {
             const uint32_t j = r0 + tid;
@@ -1851,6 +1985,22 @@ __global__ void k_max_u64(const uint64_t* v, uint32_t n, unsigned long long* out
     for (int o = 32; o > 0; o >>= 1) { unsigned long long x = __shfl_xor(m, o); m = x > m ? x : m; }
     if ((threadIdx.x & 63) == 0) atomicMax(out, m);
 }
+__global__ void k_sum_u64(const uint64_t* v, uint32_t n, unsigned long long* out) {
+    unsigned long long m = 0;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) m += v[i];
+    for (int o = 32; o > 0; o >>= 1) m += __shfl_xor(m, o);
+    if ((threadIdx.x & 63) == 0) atomicAdd(out, m);
+}
+int device_sum_u64(const uint64_t* v, uint32_t n, unsigned long long* d_slot, uint64_t* out, hipStream_t st) {
+    bool ok = hipMemsetAsync(d_slot, 0, sizeof *d_slot, st) == hipSuccess;
+    hipLaunchKernelGGL(k_sum_u64, dim3(64), dim3(256), 0, st, v, n, d_slot);
+    unsigned long long h = 0;
+    ok = ok && hipGetLastError() == hipSuccess;
+    ok = ok && hipMemcpyAsync(&h, d_slot, sizeof h, hipMemcpyDeviceToHost, st) == hipSuccess;
+    ok = ok && hipStreamSynchronize(st) == hipSuccess;
+    *out = h;
+    return ok ? 0 : -1;
+}
 int device_max_u64(const uint64_t* v, uint32_t n, unsigned long long* d_slot, uint64_t* out, hipStream_t st) {
     bool ok = hipMemsetAsync(d_slot, 0, sizeof *d_slot, st) == hipSuccess;
     hipLaunchKernelGGL(k_max_u64, dim3(64), dim3(256), 0, st, v, n, d_slot);
@@ -1874,10 +2024,10 @@ void launch_deflate(const DeflateArgs& a, hipStream_t st, hipStream_t side, hipE
     dim3 grid((a.n + DF_THREADS - 1) / DF_THREADS);
     hipLaunchKernelGGL(k_deflate_tables, dim3(1), dim3(1), 0, st);
     if (a.rec_buf && !c_config_host_fast(a.level)) {
-        const uint32_t nseg = (a.rec_stride + PM_SEG - 1) / PM_SEG;
         const int ck_kind = a.format == SDZ_DEFLATE_GZIP ? 1 : 0;
-        hipLaunchKernelGGL(k_dfl_chain, dim3((a.n + CH_WAVES - 1) / CH_WAVES), dim3(64 * CH_WAVES), 0, st, a);
-        hipLaunchKernelGGL(k_dfl_match, dim3(a.n * nseg), dim3(PM_THREADS), 0, st, a, nseg);
+        if (a.ncunit)
+            hipLaunchKernelGGL(k_dfl_chain, dim3((a.ncunit + CH_WAVES - 1) / CH_WAVES), dim3(64 * CH_WAVES), 0, st, a);
+        if (a.nmseg) hipLaunchKernelGGL(k_dfl_match, dim3(a.nmseg), dim3(PM_THREADS), 0, st, a);
         hipLaunchKernelGGL(k_dfl_tail, dim3(a.n), dim3(256), 0, st, a);
         const bool fork = side && ev && hipEventRecord(ev, st) == hipSuccess &&
                           hipStreamWaitEvent(side, ev, 0) == hipSuccess;
@@ -1885,8 +2035,9 @@ void launch_deflate(const DeflateArgs& a, hipStream_t st, hipStream_t side, hipE
             launch_checksum(a.in, a.in_off, a.in_len, nullptr, a.cks, a.n, ck_kind, side);
             (void)hipEventRecord(ev, side);
         }
-        hipLaunchKernelGGL(k_dfl_parse, grid, dim3(64), 0, st, a);
-        hipLaunchKernelGGL(k_dfl_trees, dim3(a.n), dim3(64), 0, st, a);
+        if (a.wide) hipLaunchKernelGGL(k_dfl_parse_wide, dim3(a.n), dim3(PW_THREADS), 0, st, a);
+        else hipLaunchKernelGGL(k_dfl_parse, grid, dim3(64), 0, st, a);
+        hipLaunchKernelGGL(k_dfl_trees, dim3(a.n, a.nbmax < 32 ? (a.nbmax ? a.nbmax : 1) : 32), dim3(64), 0, st, a);
         if (fork) (void)hipStreamWaitEvent(st, ev, 0);
         else launch_checksum(a.in, a.in_off, a.in_len, nullptr, a.cks, a.n, ck_kind, st);
         hipLaunchKernelGGL(k_dfl_encode, dim3(a.n), dim3(EN_THREADS), 0, st, a);

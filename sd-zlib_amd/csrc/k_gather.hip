@@ -1,0 +1,60 @@
+// k_gather.hip -- batched span copy on the device: dst[dst_off[i] ..] <- src[src_off[i] ..]
+// for n spans of len[i] bytes, in ONE launch (sdz_gather_device).
+//
+// Used to stage batches: the bench places 65,536 input slices at arbitrary source offsets
+// into their stream slots with one launch instead of 65,536 hipMemcpy dispatches (which a
+// --pmc pass instruments one by one), and the host-batch entry points scatter the records'
+// payloads out of the device pool the same way.  Not on the codec path: no reference
+// function behind it; pure HBM traffic (read len + write len per span).
+//
+// Layout: blockIdx.y cuts each span into GA_SLICES interleaved 4 KiB pieces, so a few huge
+// spans still spread over many CUs; a block copies its pieces as aligned destination dwords
+// (source dwords assembled from two aligned reads with v_alignbyte), head / tail bytes
+// separately.  Aligned source reads never leave the allocation a valid span lies in.
+#include "sdz_internal.h"
+
+namespace sdz {
+
+#define GA_THREADS 256
+#define GA_SLICES 8
+#define GA_PIECE 4096u
+
+__global__ __launch_bounds__(GA_THREADS) void k_gather(uint8_t* dst, const uint64_t* dst_off, const uint8_t* src,
+                                                       const uint64_t* src_off, const uint64_t* len, uint32_t n) {
+    const uint32_t sid = blockIdx.x;
+    if (sid >= n) return;
+    const uint64_t L = len[sid];
+    if (L == 0) return;
+    uint8_t* d = dst + dst_off[sid];
+    const uint8_t* s = src + src_off[sid];
+    // head: bytes until d is 4-aligned (block y = 0 only)
+    const uint32_t h0 = (uint32_t)((4u - ((uintptr_t)d & 3u)) & 3u);
+    const uint64_t h = L < h0 ? L : h0;
+    if (blockIdx.y == 0 && threadIdx.x < h) d[threadIdx.x] = s[threadIdx.x];
+    const uint64_t nw = (L - h) >> 2;                    // whole destination dwords
+    uint32_t* dw = (uint32_t*)(d + h);
+    const uint8_t* sb = s + h;
+    const uint32_t k = (uint32_t)((uintptr_t)sb & 3u);
+    const uint32_t* sw = (const uint32_t*)(sb - k);
+    const uint64_t wpp = GA_PIECE / 4;                   // dwords per piece
+    for (uint64_t p0 = (uint64_t)blockIdx.y * wpp; p0 < nw; p0 += (uint64_t)GA_SLICES * wpp) {
+        const uint64_t pe = p0 + wpp < nw ? p0 + wpp : nw;
+        for (uint64_t q = p0 + threadIdx.x; q < pe; q += GA_THREADS) {
+            const uint32_t lo = sw[q];
+            // the second dword holds bytes of this span only when k != 0
+            const uint32_t hi = k ? sw[q + 1] : 0u;
+            dw[q] = __builtin_amdgcn_alignbyte(hi, lo, k);
+        }
+    }
+    // tail bytes
+    const uint64_t t0 = h + 4 * nw;
+    if (blockIdx.y == GA_SLICES - 1 && threadIdx.x < L - t0) d[t0 + threadIdx.x] = s[t0 + threadIdx.x];
+}
+
+void launch_gather(uint8_t* dst, const uint64_t* dst_off, const uint8_t* src, const uint64_t* src_off,
+                   const uint64_t* len, uint32_t n, hipStream_t s) {
+    if (n == 0) return;
+    hipLaunchKernelGGL(k_gather, dim3(n, GA_SLICES), dim3(GA_THREADS), 0, s, dst, dst_off, src, src_off, len, n);
+}
+
+}  // namespace sdz

@@ -1152,7 +1152,7 @@ __device__ __forceinline__ void epochs(const InflateArgs& A, DSave* S, const uin
         bool cold = live && !S->full && S->mode != LM_DONE && !hot && (MODE == 0 || !S->stall);
         if (__ballot(cold)) {
             if (cold)
-                cold_run<MODE>(S, inp, ilen, cap, tb, tcap, lens, A.format, A.dict != nullptr, A.dict_adler,
+                cold_run<MODE>(S, inp, ilen, cap, tb, tcap, lens, A.format, A.dict != nullptr, dict_id_of(A.dict_adler, A.dict_adler_dev),
                                MODE == 1 && S->mode == LM_INIT ? 1u : 0u, G);
             hot = live && can_hot<MODE>(S, tbits, cap);
 #ifdef SDZ_TIMING
@@ -1216,11 +1216,11 @@ __global__ __launch_bounds__(IL_THREADS, 1) void k_inflate_decode(InflateArgs A,
         } else if (!resume) {
             live = true;
             if (A.streaming) cold_run<1>(S, inp, ilen, cap, tb, tcap, lens, A.format,
-                                         A.dict != nullptr, A.dict_adler, 1u, G);
+                                         A.dict != nullptr, dict_id_of(A.dict_adler, A.dict_adler_dev), 1u, G);
             else if (A.segmode) cold_run<2>(S, inp, ilen, cap, tb, tcap, lens, A.format,
-                                            A.dict != nullptr, A.dict_adler, 1u, G);
+                                            A.dict != nullptr, dict_id_of(A.dict_adler, A.dict_adler_dev), 1u, G);
             else cold_run<0>(S, inp, ilen, cap, tb, tcap, lens, A.format,
-                             A.dict != nullptr, A.dict_adler, 1u, G);
+                             A.dict != nullptr, dict_id_of(A.dict_adler, A.dict_adler_dev), 1u, G);
         } else if (S->mode != LM_DONE && !(round > 0 && S->stall)) {
             live = true;
             for (int k = 0; k < IL_REGION / 4; ++k) ((uint32_t*)region)[k] = ((const uint32_t*)S->region)[k];

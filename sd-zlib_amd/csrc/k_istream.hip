@@ -28,8 +28,31 @@ __global__ void k_istate_reset(uint8_t* dsave, uint8_t* rsave, uint32_t n) {
 
 // one block per stream: stage = carry ++ chunk; a finished stream given more bytes reports
 // them (the reference's append() throws "bad input data" there, sd-inflate.ts:130-132)
+// staging slot of stream i: SDZ_INFLATE_CARRY + in_len + 64 bytes (readable slack for the
+// decoder's 16-byte loads), 256-aligned; st_off = exclusive prefix sums, one workgroup
+#define SG_THREADS 1024
+__device__ __forceinline__ uint64_t stage_slot(uint64_t len) { return (SDZ_INFLATE_CARRY + len + 64 + 255) & ~255ull; }
+__global__ __launch_bounds__(SG_THREADS) void k_stage_slots(const uint64_t* in_len, uint32_t n, uint64_t* st_off) {
+    __shared__ uint64_t part[SG_THREADS];
+    const uint32_t t = threadIdx.x;
+    const uint32_t per = (n + SG_THREADS - 1) / SG_THREADS;
+    const uint32_t b = t * per < n ? t * per : n, e = b + per < n ? b + per : n;
+    uint64_t sum = 0;
+    for (uint32_t i = b; i < e; ++i) sum += stage_slot(in_len[i]);
+    part[t] = sum;
+    __syncthreads();
+    for (uint32_t o = 1; o < SG_THREADS; o <<= 1) {      // inclusive scan of the thread sums
+        const uint64_t v = t >= o ? part[t - o] : 0;
+        __syncthreads();
+        part[t] += v;
+        __syncthreads();
+    }
+    uint64_t run = t ? part[t - 1] : 0;
+    for (uint32_t i = b; i < e; ++i) { st_off[i] = run; run += stage_slot(in_len[i]); }
+}
+
 __global__ __launch_bounds__(256) void k_istate_stage(InflateArgs A, const uint8_t* in, const uint64_t* in_off,
-                                                      const uint64_t* in_len, uint8_t* stage, uint64_t stride,
+                                                      const uint64_t* in_len, uint8_t* stage,
                                                       uint64_t* st_off, uint64_t* st_len) {
     const uint32_t sid = blockIdx.x;
     if (sid >= A.n) return;
@@ -37,7 +60,7 @@ __global__ __launch_bounds__(256) void k_istate_stage(InflateArgs A, const uint8
     RSave* R = (RSave*)A.rsave + sid;
     const uint32_t nc = R->carry_len;
     const uint64_t nl = in_len[sid];
-    uint8_t* dst = stage + (uint64_t)sid * stride;
+    uint8_t* dst = stage + st_off[sid];
     const uint8_t* carry = A.carry + (uint64_t)sid * SDZ_INFLATE_CARRY;
     const uint8_t* src = in + in_off[sid];
     for (uint32_t k = threadIdx.x; k < nc; k += blockDim.x) dst[k] = carry[k];
@@ -51,7 +74,6 @@ __global__ __launch_bounds__(256) void k_istate_stage(InflateArgs A, const uint8
     }
     __syncthreads();
     if (threadIdx.x != 0) return;
-    st_off[sid] = (uint64_t)sid * stride;
     st_len[sid] = nc + nl;                         // R->carry_len stays: the staged input's carried head
     // a call that does not continue an append stopped at out_cap starts a new append():
     // its output chunks (and the running adler32's NMAX grid) start here
@@ -65,10 +87,10 @@ void launch_istate_reset(uint8_t* dsave, uint8_t* rsave, uint32_t n, hipStream_t
 }
 
 void launch_istate_stage(const InflateArgs& a, const uint8_t* in, const uint64_t* in_off, const uint64_t* in_len,
-                         uint8_t* stage, uint64_t stride, uint64_t* st_off, uint64_t* st_len, hipStream_t s) {
+                         uint8_t* stage, uint64_t* st_off, uint64_t* st_len, hipStream_t s) {
     if (!a.n) return;
-    hipLaunchKernelGGL(k_istate_stage, dim3(a.n), dim3(256), 0, s, a, in, in_off, in_len, stage, stride,
-                       st_off, st_len);
+    hipLaunchKernelGGL(k_stage_slots, dim3(1), dim3(SG_THREADS), 0, s, in_len, a.n, st_off);
+    hipLaunchKernelGGL(k_istate_stage, dim3(a.n), dim3(256), 0, s, a, in, in_off, in_len, stage, st_off, st_len);
 }
 
 }  // namespace sdz

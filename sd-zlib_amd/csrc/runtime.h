@@ -1,0 +1,84 @@
+// runtime.h -- host runtime pieces shared by sdz_runtime.cpp (single-device entry points)
+// and sdz_host.cpp (host-buffer batches, multi-GPU, RCCL): error reporting, per-device
+// locks and the stream-ordered device pools.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <mutex>
+#include <string>
+
+#include "sdz.h"
+
+namespace sdz {
+namespace rt {
+
+int fail(int code, const std::string& msg);
+int hip_fail(hipError_t e, const char* what);
+
+#define HIPCHK(x)                                             \
+    do {                                                      \
+        hipError_t e_ = (x);                                  \
+        if (e_ != hipSuccess) return ::sdz::rt::hip_fail(e_, #x); \
+    } while (0)
+
+int ensure_device();
+
+// Calls on one device are serialised (its pools and side stream are shared; recursive: a
+// host-batch call holds it around the *_device call it makes); calls on different devices
+// run concurrently -- sdz_*_batch_multi drives one host thread per GPU.
+constexpr int kMaxDev = 64;
+extern std::recursive_mutex g_dev_mu[kMaxDev];
+int cur_device(int* d);
+struct DevLock {
+    std::unique_lock<std::recursive_mutex> lk;
+    int rc = SDZ_API_OK;
+    DevLock() {
+        int d = 0;
+        rc = cur_device(&d);
+        if (rc == SDZ_API_OK) lk = std::unique_lock<std::recursive_mutex>(g_dev_mu[d]);
+    }
+};
+
+// Grow-only device scratch, one allocation per (purpose, device).  The *_device entry
+// points are asynchronous on the caller's stream, so a pool is stream-ordered: get()
+// makes the caller's stream wait for the event recorded after the pool's previous use
+// (on whatever stream that was), and done() records that event once this call's work
+// is enqueued.  Callers hold their device's lock (DevLock) between get() and done(), and
+// take each pool at most once per call.
+struct Pool {
+    struct Slot {
+        void* p = nullptr;
+        size_t cap = 0;
+        hipEvent_t ev = nullptr;      // recorded after the last enqueued use
+        bool pending = false;
+    };
+    Slot slots[kMaxDev];              // indexed by device id
+    int get(size_t bytes, hipStream_t s, void** out, Slot** slot);
+    static int done(Slot* S, hipStream_t s);
+};
+// records the pool's event on every exit path once get() succeeded
+struct PoolUse {
+    Pool& pool;
+    hipStream_t s;
+    Pool::Slot* slot = nullptr;
+    PoolUse(Pool& p, hipStream_t st) : pool(p), s(st) {}
+    int get(size_t bytes, void** out) { return pool.get(bytes, s, out, &slot); }
+    ~PoolUse() { if (slot) Pool::done(slot, s); }
+};
+extern Pool g_host;                   // host-buffer batches: staged inputs, outputs, records
+
+// pinned host staging, grow-only, one per device (used under the device's lock).  A user that
+// leaves copies from it in flight calls done(stream); the next get() waits for them.
+struct Pinned {
+    void* p[kMaxDev] = {};
+    size_t cap[kMaxDev] = {};
+    hipEvent_t ev[kMaxDev] = {};
+    bool pending[kMaxDev] = {};
+    int get(size_t bytes, void** out);
+    int done(hipStream_t s);
+};
+extern Pinned g_pinned;
+
+}  // namespace rt
+}  // namespace sdz

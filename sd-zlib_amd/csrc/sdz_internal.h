@@ -30,7 +30,8 @@ struct InflateArgs {
     uint8_t* scratch;            // n * kInflateScratchPerStream
     const uint8_t* dict;         // preset dictionary (last <= 32767 bytes used), may be null
     uint32_t dict_len;
-    int32_t dict_adler;          // adler32.ts of the full dictionary
+    int32_t dict_adler;          // adler32.ts of the full dictionary (when dict_adler_dev is null)
+    const int32_t* dict_adler_dev;  // ... or computed on the device by this call (no host sync)
     uint32_t n;
     int32_t format;
     // round machinery (phase 1 -> tokens -> phase 2)
@@ -76,8 +77,9 @@ void launch_seg_decode(const InflateArgs& a, hipStream_t s);
 void launch_seg_chain(const InflateArgs& a, SplitInfo* sp, uint32_t nsplit, const SegInfo* seg, const uint64_t* cand,
                       const void* segD, uint32_t* chain, uint64_t* chain_tok, uint32_t* split_state, hipStream_t s);
 void launch_seg_feed(const InflateArgs& a, uint32_t round, hipStream_t s);
+// st_off: the staging slots (prefix sums of SDZ_INFLATE_CARRY + in_len + 64, 256-aligned)
 void launch_istate_stage(const InflateArgs& a, const uint8_t* in, const uint64_t* in_off, const uint64_t* in_len,
-                         uint8_t* stage, uint64_t stride, uint64_t* st_off, uint64_t* st_len, hipStream_t s);
+                         uint8_t* stage, uint64_t* st_off, uint64_t* st_len, hipStream_t s);
 
 struct DeflateArgs {
     const uint8_t* in;
@@ -94,21 +96,33 @@ struct DeflateArgs {
     uint32_t n;
     int32_t level;
     int32_t format;
-    // record path (levels 4-9, inputs <= rec_stride <= 64 KiB): per stream rec_stride positions
-    uint64_t* rec_buf;           // n * rec_stride match records (null: classic path only)
-    uint16_t* pv_buf;            // n * rec_stride hash chain links
-    uint32_t rec_stride;
+    // record path (levels 4-9, inputs <= kDeflateRecMax; host plan, sdz_runtime.cpp): stream k
+    // owns positions [rp0[k], rp0[k] + in_len) of the record and link buffers (rp0[k] = ~0: not
+    // on the record path) and block slots [tb0[k], tb0[k + 1]); the match and chain kernels
+    // run over work-unit lists (k << 12 | unit)
+    uint64_t* rec_buf;           // match records, one per position (null: classic path only)
+    uint16_t* pv_buf;            // hash chain links: distance to the previous same-hash position
+    const uint64_t* rp0;         // n + 1 entries
+    const uint32_t* tb0;         // n + 1 entries
+    uint8_t* blk;                // block slots (FB_SLOT bytes each)
+    const uint32_t* mseg;        // match segments (PM_SEG positions each)
+    uint32_t nmseg;
+    const uint32_t* cunit;       // chain units (k_dfl_chain)
+    uint32_t ncunit;
+    uint32_t nbmax;              // most block slots of one stream (k_dfl_trees grid)
+    uint32_t wide;               // k_dfl_parse: one workgroup per stream (few, long streams)
     int32_t* cks;                // n input checksums (record path)
     uint32_t fast;               // set by launch_deflate: k_deflate redoes flagged streams only
     const uint8_t* dict;         // preset dictionary (deflateSetDictionary), may be null
     uint32_t dict_len;
     int32_t dict_adler;          // adler32.ts of the whole dictionary: the zlib header's DICTID
+    const int32_t* dict_adler_dev;  // ... or computed on the device by this call (no host sync)
     unsigned long long* dbg;     // phase cycle counters (SDZ_PHASE_TIMING), normally null
 };
 
 uint64_t deflate_state_bytes();
 void launch_deflate(const DeflateArgs& a, hipStream_t s, hipStream_t side = nullptr, hipEvent_t ev = nullptr);
-// the fast (not bit-exact) compressor (k_deflate_fast.hip): 16 KiB tiles, one block each
+// the fast (not bit-exact) compressor (k_deflate_fast.hip): 8 KiB tiles, one block each
 #define FT_TILE_BYTES 8192u
 #define FT_TILE_OUT 8256u                 // a tile's output slot (<= tile + 10 bytes)
 void launch_fast_tiles(const uint8_t* in, const uint64_t* in_off, const uint64_t* in_len, const uint32_t* tile_stream,
@@ -118,11 +132,23 @@ void launch_fast_concat(const DeflateArgs& a, const uint32_t* tile0, const uint8
 // incremental Deflater (k_deflate_stream): fresh state; one append (finish 0) / finish (1)
 void launch_deflate_reset(uint8_t* state, uint32_t n, hipStream_t s);
 void launch_deflate_stream(const DeflateArgs& a, uint32_t finish, hipStream_t s);
-constexpr uint32_t kDeflateRecMax = 65536;   // longest input on the record path
+constexpr uint64_t kDeflateRecMax = 64ull << 20;   // longest input on the record path
+constexpr uint32_t kRecUnitShift = 12;              // work units: k << 12 | unit (unit < 4096)
+uint64_t deflate_rec_blocks(uint64_t len);          // block slots a record-path stream needs
+uint32_t deflate_chain_units(uint64_t len);         // its k_dfl_chain units
+uint32_t deflate_match_segs(uint64_t len);          // its k_dfl_match segments
 // max of n device-resident u64 values (blocking; for scratch sizing); d_slot: 8 device bytes
 int device_max_u64(const uint64_t* v, uint32_t n, unsigned long long* d_slot, uint64_t* out, hipStream_t s);
+int device_sum_u64(const uint64_t* v, uint32_t n, unsigned long long* d_slot, uint64_t* out, hipStream_t s);
 
 void launch_checksum(const uint8_t* in, const uint64_t* in_off, const uint64_t* in_len,
                      const int32_t* seed, int32_t* result, uint32_t n, int kind, hipStream_t s);
+// one buffer, arguments by value (asynchronous: the DICTID of a dictionary)
+void launch_checksum_one(const uint8_t* in, uint64_t len, int kind, int32_t seed, int32_t* result, hipStream_t s);
+// batched span copy (k_gather.hip)
+void launch_gather(uint8_t* dst, const uint64_t* dst_off, const uint8_t* src, const uint64_t* src_off,
+                   const uint64_t* len, uint32_t n, hipStream_t s);
+// the DICTID a kernel compares / writes
+__device__ __forceinline__ int32_t dict_id_of(int32_t v, const int32_t* dev) { return dev ? *dev : v; }
 
 }  // namespace sdz

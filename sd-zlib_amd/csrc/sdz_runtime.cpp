@@ -13,19 +13,19 @@
 #include <vector>
 
 #include "sdz_internal.h"
+#include "runtime.h"
+
+#define FB_SLOT_BYTES (64 + 2048)            // k_deflate.hip FB_SLOT: a record-path block slot
 
 using namespace sdz;
 
-namespace {
+namespace sdz {
+namespace rt {
 
 thread_local std::string g_err;
-thread_local float g_last_ms = 0.f;
-thread_local hipEvent_t g_ev0 = nullptr, g_ev1 = nullptr;
-thread_local bool g_ev_pending = false;
-thread_local float g_extra_ms = 0.f;    // GPU time of the last call outside g_ev0..g_ev1 (split pre-pass)
-int g_timing = 0;
-float g_breakdown[3] = { 0.f, 0.f, 0.f };   // decode / resolve / finalize of the last inflate
-std::mutex g_mu;
+std::recursive_mutex g_dev_mu[kMaxDev];
+Pool g_host;
+Pinned g_pinned;
 
 int fail(int code, const std::string& msg) {
     g_err = msg;
@@ -36,12 +36,6 @@ int hip_fail(hipError_t e, const char* what) {
     return fail(SDZ_API_HIP_ERROR, std::string(what) + ": " + hipGetErrorString(e));
 }
 
-#define HIPCHK(x)                                             \
-    do {                                                      \
-        hipError_t e_ = (x);                                  \
-        if (e_ != hipSuccess) return hip_fail(e_, #x);        \
-    } while (0)
-
 int ensure_device() {
     int n = 0;
     hipError_t e = hipGetDeviceCount(&n);
@@ -50,70 +44,89 @@ int ensure_device() {
     return SDZ_API_OK;
 }
 
-// Grow-only device scratch, one allocation per (purpose, device).  The *_device entry
-// points are asynchronous on the caller's stream, so a pool is stream-ordered: get()
-// makes the caller's stream wait for the event recorded after the pool's previous use
-// (on whatever stream that was), and done() records that event once this call's work
-// is enqueued.  Callers hold g_mu between get() and done().
-struct Pool {
-    struct Slot {
-        void* p = nullptr;
-        size_t cap = 0;
-        hipEvent_t ev = nullptr;      // recorded after the last enqueued use
-        bool pending = false;
-    };
-    std::vector<Slot> slots;          // indexed by device id
-    Slot* cur = nullptr;
-    int get(size_t bytes, hipStream_t s, void** out) {
-        int d = 0;
-        HIPCHK(hipGetDevice(&d));
-        if ((size_t)d >= slots.size()) slots.resize((size_t)d + 1);
-        Slot& S = slots[(size_t)d];
-        if (!S.ev) HIPCHK(hipEventCreateWithFlags(&S.ev, hipEventDisableTiming));
-        if (S.p && S.cap < bytes) {
-            if (S.pending) HIPCHK(hipEventSynchronize(S.ev));
-            HIPCHK(hipFree(S.p));
-            S.p = nullptr;
-            S.cap = 0;
-            S.pending = false;
-        }
-        if (!S.p) {
-            size_t want = std::max(bytes, (size_t)1 << 20);
-            hipError_t e = hipMalloc(&S.p, want);
-            if (e != hipSuccess) { S.p = nullptr; return hip_fail(e, "hipMalloc(scratch)"); }
-            S.cap = want;
-        }
-        if (S.pending) HIPCHK(hipStreamWaitEvent(s, S.ev, 0));
-        cur = &S;
-        *out = S.p;
-        return SDZ_API_OK;
-    }
-    int done(hipStream_t s) {
-        if (!cur) return SDZ_API_OK;
-        Slot& S = *cur;
-        cur = nullptr;
-        HIPCHK(hipEventRecord(S.ev, s));
-        S.pending = true;
-        return SDZ_API_OK;
-    }
-};
-Pool g_inflate_scratch, g_deflate_state, g_tmp, g_stage, g_split, g_find;
-constexpr size_t kTmpFname = 256;     // g_tmp layout: [0, 256) small results, then the file name
-constexpr uint64_t kInflaterOutCap = 4ull << 20;   // sdz_inflater: output slot per device call
+int cur_device(int* d) {
+    HIPCHK(hipGetDevice(d));
+    if (*d < 0 || *d >= kMaxDev) return fail(SDZ_API_BAD_ARG, "device index out of range");
+    return SDZ_API_OK;
+}
 
-// records the pool's event on every exit path once get() succeeded
-struct PoolUse {
-    Pool& pool;
-    hipStream_t s;
-    bool held = false;
-    PoolUse(Pool& p, hipStream_t st) : pool(p), s(st) {}
-    int get(size_t bytes, void** out) {
-        int rc = pool.get(bytes, s, out);
-        held = rc == SDZ_API_OK;
-        return rc;
+int Pool::get(size_t bytes, hipStream_t s, void** out, Slot** slot) {
+    int d = 0;
+    if (int rc = cur_device(&d)) return rc;
+    Slot& S = slots[d];
+    if (!S.ev) HIPCHK(hipEventCreateWithFlags(&S.ev, hipEventDisableTiming));
+    if (S.p && S.cap < bytes) {
+        if (S.pending) HIPCHK(hipEventSynchronize(S.ev));
+        HIPCHK(hipFree(S.p));
+        S.p = nullptr;
+        S.cap = 0;
+        S.pending = false;
     }
-    ~PoolUse() { if (held) pool.done(s); }
-};
+    if (!S.p) {
+        size_t want = std::max(bytes, (size_t)1 << 20);
+        hipError_t e = hipMalloc(&S.p, want);
+        if (e != hipSuccess) { S.p = nullptr; return hip_fail(e, "hipMalloc(scratch)"); }
+        S.cap = want;
+    }
+    if (S.pending) HIPCHK(hipStreamWaitEvent(s, S.ev, 0));
+    *slot = &S;
+    *out = S.p;
+    return SDZ_API_OK;
+}
+
+int Pool::done(Slot* S, hipStream_t s) {
+    HIPCHK(hipEventRecord(S->ev, s));
+    S->pending = true;
+    return SDZ_API_OK;
+}
+
+int Pinned::get(size_t bytes, void** out) {
+    int d = 0;
+    if (int rc = cur_device(&d)) return rc;
+    if (pending[d]) {
+        HIPCHK(hipEventSynchronize(ev[d]));
+        pending[d] = false;
+    }
+    if (cap[d] < bytes) {
+        if (p[d]) HIPCHK(hipHostFree(p[d]));
+        p[d] = nullptr;
+        cap[d] = 0;
+        const size_t want = std::max(bytes, (size_t)1 << 20);
+        HIPCHK(hipHostMalloc(&p[d], want, hipHostMallocDefault));
+        cap[d] = want;
+    }
+    *out = p[d];
+    return SDZ_API_OK;
+}
+
+int Pinned::done(hipStream_t s) {
+    int d = 0;
+    if (int rc = cur_device(&d)) return rc;
+    if (!ev[d]) HIPCHK(hipEventCreateWithFlags(&ev[d], hipEventDisableTiming));
+    HIPCHK(hipEventRecord(ev[d], s));
+    pending[d] = true;
+    return SDZ_API_OK;
+}
+
+}  // namespace rt
+}  // namespace sdz
+
+using namespace sdz::rt;
+
+namespace {
+
+thread_local float g_last_ms = 0.f;
+thread_local hipEvent_t g_ev0 = nullptr, g_ev1 = nullptr;
+thread_local bool g_ev_pending = false;
+thread_local float g_extra_ms = 0.f;    // GPU time of the last call outside g_ev0..g_ev1 (split pre-pass)
+int g_timing = 0;
+thread_local float g_breakdown[3] = { 0.f, 0.f, 0.f };   // decode / resolve / finalize of the last inflate
+
+Pool g_inflate_scratch, g_deflate_state, g_tmp, g_stage, g_split, g_find;
+// g_tmp layout: [0, 64) a device max / sum, [64, 128) the dictionary's adler32 (DICTID),
+// [128, 256) small results, then the file name
+constexpr size_t kTmpMax = 0, kTmpDictId = 64, kTmpFname = 256;
+constexpr uint64_t kInflaterOutCap = 4ull << 20;   // sdz_inflater: output slot per device call
 
 void timing_begin(hipStream_t s) {
     if (!g_timing) return;
@@ -149,26 +162,20 @@ const char* const kZmsg[ZM_COUNT] = {
     "invalid literal/length code",
 };
 
-// one-shot device checksum of a device buffer (used for the dictionary's DICTID)
+// one-shot device checksum of a device buffer, blocking (the host checksum entry points)
 int device_checksum(const uint8_t* d_buf, uint64_t len, int kind, int32_t seed, int32_t* out,
                     hipStream_t s) {
     void* tmp = nullptr;
-    if (int rc = g_tmp.get(kTmpFname, s, &tmp)) return rc;
-    uint64_t* d_off = (uint64_t*)tmp;
-    uint64_t* d_len = d_off + 1;
-    int32_t* d_seed = (int32_t*)(d_off + 2);
-    int32_t* d_res = d_seed + 1;
-    struct { uint64_t off, len; int32_t seed, pad; } hv = { 0, len, seed, 0 };
     int32_t res = 0;
-    hipError_t e = hipMemcpyAsync(d_off, &hv, sizeof hv, hipMemcpyHostToDevice, s);
-    if (e == hipSuccess) {
-        launch_checksum(d_buf, d_off, d_len, d_seed, d_res, 1, kind, s);
-        e = hipGetLastError();
+    {
+        PoolUse use(g_tmp, s);
+        if (int rc = use.get(kTmpFname, &tmp)) return rc;
+        int32_t* d_res = (int32_t*)((uint8_t*)tmp + kTmpDictId);
+        launch_checksum_one(d_buf, len, kind, seed, d_res, s);
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipMemcpyAsync(&res, d_res, sizeof res, hipMemcpyDeviceToHost, s));
     }
-    if (e == hipSuccess) e = hipMemcpyAsync(&res, d_res, sizeof res, hipMemcpyDeviceToHost, s);
-    if (int rc = g_tmp.done(s)) return rc;
-    if (e == hipSuccess) e = hipStreamSynchronize(s);
-    if (e != hipSuccess) return hip_fail(e, "device checksum");
+    HIPCHK(hipStreamSynchronize(s));
     *out = res;
     return SDZ_API_OK;
 }
@@ -177,7 +184,7 @@ int device_checksum(const uint8_t* d_buf, uint64_t len, int kind, int32_t seed, 
 
 extern "C" {
 
-const char* sdz_last_error(void) { return g_err.c_str(); }
+const char* sdz_last_error(void) { return sdz::rt::g_err.c_str(); }
 int sdz_version(void) { return SDZ_ABI_VERSION; }
 
 int sdz_device_count(void) {
@@ -328,12 +335,11 @@ int inflate_run(InflateArgs& a, hipStream_t s, bool timing_started = false, int 
 // per device: the side stream the segments decode on (overlapping the first round's decode
 // of the other streams) and its completion event
 struct SideStream { hipStream_t s = nullptr; hipEvent_t ev = nullptr; };
-std::vector<SideStream> g_side;
+SideStream g_side[kMaxDev];
 int side_stream(SideStream** out) {
     int d = 0;
-    HIPCHK(hipGetDevice(&d));
-    if ((size_t)d >= g_side.size()) g_side.resize((size_t)d + 1);
-    SideStream& S = g_side[(size_t)d];
+    if (int rc = cur_device(&d)) return rc;
+    SideStream& S = g_side[d];
     if (!S.s) HIPCHK(hipStreamCreateWithFlags(&S.s, hipStreamNonBlocking));
     if (!S.ev) HIPCHK(hipEventCreateWithFlags(&S.ev, hipEventDisableTiming));
     *out = &S;
@@ -577,6 +583,10 @@ struct IStateLayout {
         bytes = carry + (size_t)n * SDZ_INFLATE_CARRY;
     }
 };
+int inflate_append_impl(void* state, const uint8_t* in, const uint64_t* in_off, const uint64_t* in_len,
+                        uint8_t* out, const uint64_t* out_off, const uint64_t* out_cap, sdz_inflate_record* rec,
+                        uint32_t n, int32_t format, const uint8_t* dict, uint32_t dict_len,
+                        const uint64_t* in_total_hint, hipStream_t s);
 
 }  // namespace
 
@@ -593,18 +603,23 @@ int sdz_inflate_batch_device(const uint8_t* in, const uint64_t* in_off, const ui
     if (format < SDZ_FMT_AUTO || format > SDZ_FMT_CONTAINER)
         return fail(SDZ_API_BAD_ARG, "sdz_inflate_batch_device: bad format");
     hipStream_t s = (hipStream_t)stream;
-    std::lock_guard<std::mutex> lk(g_mu);
-    int32_t dict_adler = 1;
-    if (dict) {
-        if (int rc = device_checksum(dict, dict_len, 0, 1, &dict_adler, s)) return rc;
-    }
+    DevLock lk;
+    if (lk.rc) return lk.rc;
     InflateArgs a{};
+    PoolUse tmp_use(g_tmp, s);
+    void* tmp = nullptr;
+    if (int rc = tmp_use.get(kTmpFname, &tmp)) return rc;
+    if (dict) {                                         // DICTID on the device: no host sync
+        int32_t* d_id = (int32_t*)((uint8_t*)tmp + kTmpDictId);
+        launch_checksum_one(dict, dict_len, 0, 1, d_id, s);
+        a.dict_adler_dev = d_id;
+    }
     PoolUse use(g_inflate_scratch, s);
     if (int rc = inflate_scratch(a, n, true, 0, s, use, nullptr)) return rc;
     a.in = in; a.in_off = in_off; a.in_len = in_len;
     a.out = out; a.out_off = out_off; a.out_cap = out_cap;
     a.rec = rec;
-    a.dict = dict; a.dict_len = dict_len; a.dict_adler = dict_adler;
+    a.dict = dict; a.dict_len = dict_len; a.dict_adler = 1;
     a.n = n; a.format = format;
     a.streaming = 0; a.window = nullptr; a.carry = nullptr;
     a.split_plan = nullptr; a.split_state = nullptr; a.segmode = 0;
@@ -650,43 +665,73 @@ int sdz_inflate_append_batch_device(void* state, const uint8_t* in, const uint64
         return fail(SDZ_API_BAD_ARG, "sdz_inflate_append_batch_device: null pointer");
     if (format != SDZ_FMT_RAW && format != SDZ_FMT_CONTAINER)
         return fail(SDZ_API_BAD_ARG, "sdz_inflate_append_batch_device: format must be RAW or CONTAINER");
-    hipStream_t s = (hipStream_t)stream;
-    std::lock_guard<std::mutex> lk(g_mu);
-    int32_t dict_adler = 1;
-    if (dict) {
-        if (int rc = device_checksum(dict, dict_len, 0, 1, &dict_adler, s)) return rc;
-    }
-    uint64_t mx = 0;
-    {
-        void* tmp = nullptr;
-        PoolUse tu(g_tmp, s);
-        if (int rc = tu.get(kTmpFname, &tmp)) return rc;
-        if (device_max_u64(in_len, n, (unsigned long long*)tmp, &mx, s))
-            return hip_fail(hipGetLastError(), "inflate append: input sizes");
-    }
-    // staging: carry ++ chunk per stream (+ 64 B of readable slack for the 16-byte loads)
-    const uint64_t stride = (SDZ_INFLATE_CARRY + mx + 64 + 255) & ~255ull;
+    return inflate_append_impl(state, in, in_off, in_len, out, out_off, out_cap, rec, n, format, dict, dict_len,
+                               nullptr, (hipStream_t)stream);
+}
+
+}  // extern "C"
+
+namespace {
+// The incremental call.  Staging: carry ++ chunk per stream, each stream its own slot of
+// SDZ_INFLATE_CARRY + in_len + 64 bytes (k_stage_slots: prefix sums on the device), so one
+// long chunk does not size every stream's slot.  The total comes from the host when the
+// caller knows it (in_total_hint: sdz_inflater_append), else from one device sum.
+int inflate_append_impl(void* state, const uint8_t* in, const uint64_t* in_off, const uint64_t* in_len,
+                        uint8_t* out, const uint64_t* out_off, const uint64_t* out_cap, sdz_inflate_record* rec,
+                        uint32_t n, int32_t format, const uint8_t* dict, uint32_t dict_len,
+                        const uint64_t* in_total_hint, hipStream_t s) {
+    DevLock lk;
+    if (lk.rc) return lk.rc;
     IStateLayout SL(n);
     InflateArgs a{};
+    PoolUse tmp_use(g_tmp, s);
+    void* tmp = nullptr;
+    if (int rc = tmp_use.get(kTmpFname, &tmp)) return rc;
+    uint64_t total = 0;
+    if (in_total_hint) total = *in_total_hint;
+    else if (device_sum_u64(in_len, n, (unsigned long long*)((uint8_t*)tmp + kTmpMax), &total, s))
+        return hip_fail(hipGetLastError(), "inflate append: input sizes");
+    if (dict) {
+        int32_t* d_id = (int32_t*)((uint8_t*)tmp + kTmpDictId);
+        launch_checksum_one(dict, dict_len, 0, 1, d_id, s);
+        a.dict_adler_dev = d_id;
+    }
     a.dsave = (uint8_t*)state + SL.ds;
     a.rsave = (uint8_t*)state + SL.rs;
     a.window = (uint8_t*)state + SL.win;
     a.carry = (uint8_t*)state + SL.carry;
     a.streaming = 1;
     a.n = n; a.format = format;
-    a.dict = dict; a.dict_len = dict_len; a.dict_adler = dict_adler;
+    a.dict = dict; a.dict_len = dict_len; a.dict_adler = 1;
+    // (256-aligned: the slot offsets and lengths follow it as u64 arrays)
+    const size_t stage_bytes = ((size_t)n * (SDZ_INFLATE_CARRY + 64 + 255) + total + 256 + 255) & ~(size_t)255;
     PoolUse use(g_inflate_scratch, s);
     uint8_t* ex = nullptr;
-    if (int rc = inflate_scratch(a, n, false, (size_t)n * stride + 16 * (size_t)n + 64, s, use, &ex)) return rc;
+    if (int rc = inflate_scratch(a, n, false, stage_bytes + 16 * (size_t)n + 64, s, use, &ex)) return rc;
     uint8_t* stage = ex;
-    uint64_t* st_off = (uint64_t*)(ex + (size_t)n * stride);
+    uint64_t* st_off = (uint64_t*)(ex + stage_bytes);
     uint64_t* st_len = st_off + n;
-    launch_istate_stage(a, in, in_off, in_len, stage, stride, st_off, st_len, s);
+    launch_istate_stage(a, in, in_off, in_len, stage, st_off, st_len, s);
+    if (getenv("SDZ_CHECK_STAGE")) {                    // development aid: staged runs inside the region
+        std::vector<uint64_t> o(n), l(n);
+        HIPCHK(hipMemcpyAsync(o.data(), st_off, n * 8, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipMemcpyAsync(l.data(), st_len, n * 8, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        fprintf(stderr, "sdz stage: n %u total %llu stage_bytes %zu base %p ex %p T %u st0 %llu/%llu\n", n,
+                (unsigned long long)total, stage_bytes, (void*)a.scratch, (void*)ex, a.round_tokens,
+                (unsigned long long)o[0], (unsigned long long)l[0]);
+        for (uint32_t i = 0; i < n; ++i)
+            if (o[i] + l[i] + 64 > stage_bytes) return fail(SDZ_API_BAD_ARG, "stage check: stream " + std::to_string(i));
+        if (getenv("SDZ_CHECK_STAGE")[0] == 's') return fail(SDZ_API_BAD_ARG, "stage check: stopped before decode");
+    }
     a.in = stage; a.in_off = st_off; a.in_len = st_len;
     a.out = out; a.out_off = out_off; a.out_cap = out_cap;
     a.rec = rec;
     return inflate_run(a, s);
 }
+}  // namespace
+
+extern "C" {
 
 // ----------------------------------------------------------------- deflate
 
@@ -714,35 +759,70 @@ int sdz_deflate_batch_device(const uint8_t* in, const uint64_t* in_off, const ui
     if (dict && format != SDZ_DEFLATE_ZLIB)
         return fail(SDZ_API_BAD_ARG, "Can only provide a dictionary for `deflate` containers.");
     hipStream_t s = (hipStream_t)stream;
-    std::lock_guard<std::mutex> lk(g_mu);
-    int32_t dict_adler = 1;
-    if (dict) {
-        if (int rc = device_checksum(dict, dict_len, 0, 1, &dict_adler, s)) return rc;
-    }
-    // per-stream state slabs: process in sub-batches so the slab pool stays bounded
-    // one lane per stream: fill the chip (64 Ki lanes = one wave per SIMD) when a
-    // quarter of free HBM holds the slabs, else as many as it does
-    uint64_t slab = deflate_state_bytes();
+    DevLock lk;
+    if (lk.rc) return lk.rc;
+    // per-stream state slabs: process in sub-batches so the pool stays bounded
+    const uint64_t slab = deflate_state_bytes();
     size_t mem_free = 0, mem_total = 0;
     if (hipMemGetInfo(&mem_free, &mem_total) != hipSuccess) mem_free = 16ull << 30;
-    // record path (levels 4-9, every input <= 64 KiB): hash chains and match records per
-    // position, found in parallel before the serial parse (k_deflate.hip)
     void* tmp = nullptr;
     PoolUse tmp_use(g_tmp, s);
     if (int rc = tmp_use.get(kTmpFname + fname_len + 64, &tmp)) return rc;
-    uint32_t stride = 0;
-    if (level >= 4 && !dict) {                    // a dictionary shifts the window: serial path
-        uint64_t mx = 0;
-        if (device_max_u64(in_len, n, (unsigned long long*)tmp, &mx, s))
-            return hip_fail(hipGetLastError(), "deflate: input sizes");
-        if (mx <= kDeflateRecMax) stride = (uint32_t)std::max<uint64_t>(64, (mx + 63) & ~63ull);
+    int32_t* d_dictid = nullptr;
+    if (dict) {                                   // DICTID on the device: no host sync
+        d_dictid = (int32_t*)((uint8_t*)tmp + kTmpDictId);
+        launch_checksum_one(dict, dict_len, 0, 1, d_dictid, s);
     }
-    const uint64_t per_stream = slab + (uint64_t)stride * (sizeof(uint64_t) + sizeof(uint16_t)) + sizeof(int32_t);
-    const uint32_t kMaxSlabs = (uint32_t)std::max<uint64_t>(1024, std::min<uint64_t>(65536, mem_free / 2 / per_stream));
-    uint32_t chunk = std::min(n, kMaxSlabs);
+    // Record path (levels 4-9, inputs up to kDeflateRecMax, no dictionary -- it moves the
+    // window): hash chains and match records per position found in parallel before the
+    // parse (k_deflate.hip).  The host plans it from the input sizes: each stream's record /
+    // link range, block slots, chain units and match segments, cut into sub-batches that
+    // fit half of free HBM.  Streams off the path run the serial kernel.
+    const bool recpath = level >= 4 && !dict;
+    std::vector<uint64_t> len(recpath ? n : 0);
+    if (recpath) {
+        HIPCHK(hipMemcpyAsync(len.data(), in_len, (size_t)n * 8, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+    }
+    auto on_path = [&](uint32_t i) { return recpath && len[i] > 0 && len[i] <= kDeflateRecMax; };
+    auto rec_cost = [&](uint32_t i) -> uint64_t {
+        if (!on_path(i)) return 0;
+        const uint64_t p = (len[i] + 63) & ~63ull;
+        return p * (sizeof(uint64_t) + sizeof(uint16_t)) + deflate_rec_blocks(len[i]) * FB_SLOT_BYTES + 64;
+    };
+    const uint64_t budget = std::max<uint64_t>(1ull << 30, mem_free / 2);
+    // sub-batches [cb[j], cb[j + 1])
+    std::vector<uint32_t> cb{ 0 };
+    {
+        uint64_t acc = 0;
+        const uint32_t cap = recpath ? 65536u
+                                     : (uint32_t)std::max<uint64_t>(1024, std::min<uint64_t>(65536, budget / slab));
+        for (uint32_t i = 0; i < n; ++i) {
+            const uint64_t c = slab + rec_cost(i) + 64;
+            if (i > cb.back() && (acc + c > budget || i - cb.back() >= cap)) { cb.push_back(i); acc = 0; }
+            acc += c;
+        }
+        cb.push_back(n);
+    }
+    // pool: the largest sub-batch's slabs, record buffers, block slots and plan arrays
+    uint64_t pool_bytes = 0;
+    for (size_t j = 0; j + 1 < cb.size(); ++j) {
+        uint64_t sb = 0, pos = 0, blk = 0, units = 0;
+        for (uint32_t i = cb[j]; i < cb[j + 1]; ++i) {
+            sb += slab;
+            if (on_path(i)) {
+                pos += (len[i] + 63) & ~63ull;
+                blk += deflate_rec_blocks(len[i]);
+                units += deflate_chain_units(len[i]) + deflate_match_segs(len[i]);
+            }
+        }
+        const uint64_t m = cb[j + 1] - cb[j];
+        const uint64_t b = sb + pos * 10 + blk * FB_SLOT_BYTES + m * 16 + 8 * (m + 1) + 4 * (m + 1) + 4 * units + 4096;
+        pool_bytes = std::max(pool_bytes, b);
+    }
     void* state = nullptr;
     PoolUse state_use(g_deflate_state, s);
-    if (int rc = state_use.get((size_t)chunk * per_stream, &state)) return rc;
+    if (int rc = state_use.get(pool_bytes, &state)) return rc;
     uint8_t* d_fname = nullptr;
     if (fname_len) {
         d_fname = (uint8_t*)tmp + kTmpFname;
@@ -754,25 +834,79 @@ int sdz_deflate_batch_device(const uint8_t* in, const uint64_t* in_off, const ui
         HIPCHK(hipMalloc(&dbg, 64 * sizeof(unsigned long long)));
         HIPCHK(hipMemsetAsync(dbg, 0, 64 * sizeof(unsigned long long), s));
     }
-    SideStream* side = nullptr;                   // the record path's tail + checksum run there
-    if (stride && side_stream(&side) != SDZ_API_OK) side = nullptr;
+    SideStream* side = nullptr;                   // the record path's input checksum runs there
+    if (recpath && side_stream(&side) != SDZ_API_OK) side = nullptr;
     timing_begin(s);
-    for (uint32_t b = 0; b < n; b += chunk) {
-        DeflateArgs a;
+    for (size_t j = 0; j + 1 < cb.size(); ++j) {
+        const uint32_t b = cb[j], m = cb[j + 1] - cb[j];
+        DeflateArgs a{};
         a.dbg = dbg;
-        uint32_t m = std::min(chunk, n - b);
         a.in = in; a.in_off = in_off + b; a.in_len = in_len + b;
         a.out = out; a.out_off = out_off + b; a.out_cap = out_cap + b;
         a.rec = rec + b; a.state = (uint8_t*)state;
-        a.rec_stride = stride;
-        a.rec_buf = stride ? (uint64_t*)((uint8_t*)state + (size_t)chunk * slab) : nullptr;
-        a.pv_buf = stride ? (uint16_t*)((uint8_t*)a.rec_buf + (size_t)chunk * stride * sizeof(uint64_t)) : nullptr;
-        a.cks = stride ? (int32_t*)((uint8_t*)a.pv_buf + (size_t)chunk * stride * sizeof(uint16_t)) : nullptr;
         a.fast = 0;
-        a.dict = dict; a.dict_len = dict_len; a.dict_adler = dict_adler;
+        a.dict = dict; a.dict_len = dict_len; a.dict_adler = 1; a.dict_adler_dev = d_dictid;
         a.fname = d_fname; a.fname_len = fname_len; a.mtime = mtime;
         a.n = m; a.level = level; a.format = format;
-        launch_deflate(a, s, side ? side->s : nullptr, side ? side->ev : nullptr);
+        if (recpath) {
+            // the plan: rp0 / tb0 (m + 1 each), then the unit lists
+            std::vector<uint64_t> rp0(m + 1);
+            std::vector<uint32_t> tb0(m + 1), units;
+            uint64_t pos = 0;
+            uint32_t blk = 0, nbmax = 0, nm = 0;
+            for (uint32_t k = 0; k < m; ++k) {
+                const uint32_t i = b + k;
+                tb0[k] = blk;
+                if (!on_path(i)) { rp0[k] = ~0ull; continue; }
+                rp0[k] = pos;
+                pos += (len[i] + 63) & ~63ull;
+                const uint32_t nb = (uint32_t)deflate_rec_blocks(len[i]);
+                blk += nb;
+                nbmax = std::max(nbmax, nb);
+                const uint32_t ms = deflate_match_segs(len[i]);
+                for (uint32_t u = 0; u < ms; ++u) units.push_back(k << kRecUnitShift | u);
+                nm += ms;
+            }
+            rp0[m] = pos;
+            tb0[m] = blk;
+            const uint32_t nmseg = nm;
+            for (uint32_t k = 0; k < m; ++k) {
+                if (rp0[k] == ~0ull) continue;
+                const uint32_t cu = deflate_chain_units(len[b + k]);
+                for (uint32_t u = 0; u < cu; ++u) units.push_back(k << kRecUnitShift | u);
+            }
+            uint8_t* B = (uint8_t*)state;
+            size_t o = (size_t)m * slab;
+            a.rec_buf = (uint64_t*)(B + o); o += (size_t)pos * 8;
+            a.pv_buf = (uint16_t*)(B + o); o += ((size_t)pos * 2 + 255) & ~(size_t)255;
+            a.blk = B + o; o += (size_t)blk * FB_SLOT_BYTES;
+            a.cks = (int32_t*)(B + o); o += ((size_t)m * 4 + 255) & ~(size_t)255;
+            uint64_t* d_rp0 = (uint64_t*)(B + o); o += (((size_t)m + 1) * 8 + 255) & ~(size_t)255;
+            uint32_t* d_tb0 = (uint32_t*)(B + o); o += (((size_t)m + 1) * 4 + 255) & ~(size_t)255;
+            uint32_t* d_units = (uint32_t*)(B + o);
+            // plan -> device through the pinned staging buffer (one copy, waited for below)
+            const size_t pb = rp0.size() * 8 + tb0.size() * 4 + units.size() * 4;
+            void* pin = nullptr;
+            if (int rc = g_pinned.get(pb + 64, &pin)) return rc;
+            uint8_t* P = (uint8_t*)pin;
+            std::memcpy(P, rp0.data(), rp0.size() * 8);
+            std::memcpy(P + rp0.size() * 8, tb0.data(), tb0.size() * 4);
+            if (!units.empty()) std::memcpy(P + rp0.size() * 8 + tb0.size() * 4, units.data(), units.size() * 4);
+            HIPCHK(hipMemcpyAsync(d_rp0, P, rp0.size() * 8, hipMemcpyHostToDevice, s));
+            HIPCHK(hipMemcpyAsync(d_tb0, P + rp0.size() * 8, tb0.size() * 4, hipMemcpyHostToDevice, s));
+            if (!units.empty())
+                HIPCHK(hipMemcpyAsync(d_units, P + rp0.size() * 8 + tb0.size() * 4, units.size() * 4,
+                                      hipMemcpyHostToDevice, s));
+            a.rp0 = d_rp0; a.tb0 = d_tb0;
+            a.mseg = d_units; a.nmseg = nmseg;
+            a.cunit = d_units + nmseg; a.ncunit = (uint32_t)units.size() - nmseg;
+            a.nbmax = nbmax;
+            a.wide = m <= 256 ? 1u : 0u;                // few streams: the LDS-staged parse
+            if (int rc = g_pinned.done(s)) return rc;    // (the next get() waits for the plan copies)
+            launch_deflate(a, s, side ? side->s : nullptr, side ? side->ev : nullptr);
+        } else {
+            launch_deflate(a, s, nullptr, nullptr);
+        }
     }
     timing_end(s);
     if (phases) {
@@ -810,7 +944,8 @@ int sdz_crc32_batch_device(const uint8_t* in, const uint64_t* in_off, const uint
 static int host_checksum(const uint8_t* buf, size_t len, int32_t seed, int kind, int32_t* out) {
     if (int rc = ensure_device()) return rc;
     if (!out || (!buf && len)) return fail(SDZ_API_BAD_ARG, "checksum: null pointer");
-    std::lock_guard<std::mutex> lk(g_mu);
+    DevLock lk;
+    if (lk.rc) return lk.rc;
     hipStream_t s = nullptr;
     void* d = nullptr;
     PoolUse use(g_stage, s);
@@ -832,68 +967,6 @@ int32_t sdz_adler32(const uint8_t* buf, size_t len, int32_t seed) {
 int32_t sdz_crc32(const uint8_t* buf, size_t len, int32_t seed) {
     int32_t r = 0;
     return sdz_crc32_checked(buf, len, seed, &r) == SDZ_API_OK ? r : 0;
-}
-
-// ----------------------------------------------------------------- host wrappers
-
-namespace {
-struct HostBatch {
-    uint8_t* d_in = nullptr;
-    uint8_t* d_out = nullptr;
-    uint64_t* d_meta = nullptr;
-    void* d_rec = nullptr;
-    ~HostBatch() {
-        if (d_in) hipFree(d_in);
-        if (d_out) hipFree(d_out);
-        if (d_meta) hipFree(d_meta);
-        if (d_rec) hipFree(d_rec);
-    }
-};
-}  // namespace
-
-int sdz_inflate_batch(const uint8_t* const* in, const size_t* in_len, uint8_t* const* out,
-                      const size_t* out_cap, sdz_inflate_record* rec, uint32_t n, int32_t format,
-                      const uint8_t* dict, size_t dict_len) {
-    if (int rc = ensure_device()) return rc;
-    if (n == 0) return SDZ_API_OK;
-    // LPT order: longest streams first so each wave decodes similar lengths
-    std::vector<uint32_t> ord(n);
-    std::iota(ord.begin(), ord.end(), 0u);
-    std::stable_sort(ord.begin(), ord.end(), [&](uint32_t a, uint32_t b) { return in_len[a] > in_len[b]; });
-    std::vector<uint64_t> meta(4 * (size_t)n);
-    uint64_t ti = 0, to = 0;
-    for (uint32_t k = 0; k < n; ++k) {
-        uint32_t i = ord[k];
-        meta[k] = ti; meta[n + k] = in_len[i];
-        meta[2 * (size_t)n + k] = to; meta[3 * (size_t)n + k] = out_cap[i];
-        ti += (in_len[i] + 15) & ~(uint64_t)15;
-        to += (out_cap[i] + 7) & ~(uint64_t)7;
-    }
-    HostBatch hb;
-    HIPCHK(hipMalloc(&hb.d_in, ti + 128));
-    HIPCHK(hipMalloc(&hb.d_out, to + 64));
-    HIPCHK(hipMalloc(&hb.d_meta, meta.size() * sizeof(uint64_t)));
-    HIPCHK(hipMalloc(&hb.d_rec, (size_t)n * sizeof(sdz_inflate_record)));
-    uint8_t* d_dict = nullptr;
-    if (dict) { HIPCHK(hipMalloc(&d_dict, dict_len + 64)); HIPCHK(hipMemcpy(d_dict, dict, dict_len, hipMemcpyHostToDevice)); }
-    for (uint32_t k = 0; k < n; ++k)
-        if (in_len[ord[k]]) HIPCHK(hipMemcpy(hb.d_in + meta[k], in[ord[k]], in_len[ord[k]], hipMemcpyHostToDevice));
-    HIPCHK(hipMemcpy(hb.d_meta, meta.data(), meta.size() * sizeof(uint64_t), hipMemcpyHostToDevice));
-    int rc = sdz_inflate_batch_device(hb.d_in, hb.d_meta, hb.d_meta + n, hb.d_out, hb.d_meta + 2 * (size_t)n,
-                                      hb.d_meta + 3 * (size_t)n, (sdz_inflate_record*)hb.d_rec, n, format,
-                                      d_dict, (uint32_t)dict_len, nullptr);
-    if (rc) { if (d_dict) hipFree(d_dict); return rc; }
-    HIPCHK(hipDeviceSynchronize());
-    if (d_dict) hipFree(d_dict);
-    std::vector<sdz_inflate_record> r(n);
-    HIPCHK(hipMemcpy(r.data(), hb.d_rec, (size_t)n * sizeof(sdz_inflate_record), hipMemcpyDeviceToHost));
-    for (uint32_t k = 0; k < n; ++k) {
-        uint32_t i = ord[k];
-        rec[i] = r[k];
-        uint64_t len = std::min<uint64_t>(r[k].out_len, out_cap[i]);
-        if (len && out[i]) HIPCHK(hipMemcpy(out[i], hb.d_out + meta[2 * (size_t)n + k], len, hipMemcpyDeviceToHost));
-    }
-    return SDZ_API_OK;
 }
 
 // ------------------------------------------------------------ incremental deflate
@@ -932,14 +1005,16 @@ int sdz_deflate_append_batch_device(void* state, const uint8_t* in, const uint64
     if (dict && format != SDZ_DEFLATE_ZLIB)
         return fail(SDZ_API_BAD_ARG, "Can only provide a dictionary for `deflate` containers.");
     hipStream_t s = (hipStream_t)stream;
-    std::lock_guard<std::mutex> lk(g_mu);
-    int32_t dict_adler = 1;
-    if (dict) {
-        if (int rc = device_checksum(dict, dict_len, 0, 1, &dict_adler, s)) return rc;
-    }
+    DevLock lk;
+    if (lk.rc) return lk.rc;
     void* tmp = nullptr;
     PoolUse tmp_use(g_tmp, s);
     if (int rc = tmp_use.get(kTmpFname + fname_len + 64, &tmp)) return rc;
+    int32_t* d_dictid = nullptr;
+    if (dict) {                                   // DICTID on the device: no host sync
+        d_dictid = (int32_t*)((uint8_t*)tmp + kTmpDictId);
+        launch_checksum_one(dict, dict_len, 0, 1, d_dictid, s);
+    }
     uint8_t* d_fname = nullptr;
     if (fname_len) {
         d_fname = (uint8_t*)tmp + kTmpFname;
@@ -949,7 +1024,7 @@ int sdz_deflate_append_batch_device(void* state, const uint8_t* in, const uint64
     a.in = in; a.in_off = in_off; a.in_len = in_len;
     a.out = out; a.out_off = out_off; a.out_cap = out_cap;
     a.rec = rec; a.state = (uint8_t*)state;
-    a.dict = dict; a.dict_len = dict_len; a.dict_adler = dict_adler;
+    a.dict = dict; a.dict_len = dict_len; a.dict_adler = 1; a.dict_adler_dev = d_dictid;
     a.fname = d_fname; a.fname_len = fname_len; a.mtime = mtime;
     a.n = n; a.level = level; a.format = format;
     timing_begin(s);
@@ -978,7 +1053,8 @@ int sdz_deflate_fast_batch_device(const uint8_t* in, const uint64_t* in_off, con
     if (!in || !in_off || !in_len || !out || !out_off || !out_cap || !rec)
         return fail(SDZ_API_BAD_ARG, "sdz_deflate_fast_batch_device: null pointer");
     hipStream_t s = (hipStream_t)stream;
-    std::lock_guard<std::mutex> lk(g_mu);
+    DevLock lk;
+    if (lk.rc) return lk.rc;
     // the tiles: which stream, which of its tiles (host plan from the input sizes)
     std::vector<uint64_t> len(n);
     HIPCHK(hipMemcpyAsync(len.data(), in_len, n * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
@@ -1091,9 +1167,9 @@ int sdz_inflater_append(sdz_inflater* z, const uint8_t* data, size_t len, const 
     for (uint64_t from = 0;;) {
         uint64_t meta[4] = { from, len - from, 0, kInflaterOutCap };
         HIPCHK(hipMemcpy(z->d_meta, meta, sizeof meta, hipMemcpyHostToDevice));
-        int rc = sdz_inflate_append_batch_device(z->d_state, z->d_in, z->d_meta, z->d_meta + 1, z->d_out,
-                                                 z->d_meta + 2, z->d_meta + 3, z->d_rec, 1, z->format,
-                                                 z->d_dict, z->dict_len, nullptr);
+        const uint64_t hint = len - from;                 // (host-known: no device sum)
+        int rc = inflate_append_impl(z->d_state, z->d_in, z->d_meta, z->d_meta + 1, z->d_out, z->d_meta + 2,
+                                     z->d_meta + 3, z->d_rec, 1, z->format, z->d_dict, z->dict_len, &hint, nullptr);
         if (rc) return rc;
         HIPCHK(hipMemcpy(rec, z->d_rec, sizeof *rec, hipMemcpyDeviceToHost));
         size_t o = z->out.size();
@@ -1200,50 +1276,5 @@ int sdz_deflater_append(sdz_deflater* z, const uint8_t* data, size_t len, int32_
 }
 
 void sdz_deflater_destroy(sdz_deflater* z) { delete z; }
-
-int sdz_deflate_batch(const uint8_t* const* in, const size_t* in_len, uint8_t* const* out,
-                      const size_t* out_cap, sdz_deflate_record* rec, uint32_t n, int32_t level,
-                      int32_t format, const uint8_t* fname, size_t fname_len, uint32_t mtime,
-                      const uint8_t* dict, size_t dict_len) {
-    if (int rc = ensure_device()) return rc;
-    if (n == 0) return SDZ_API_OK;
-    uint8_t* d_dict = nullptr;
-    if (dict) {
-        HIPCHK(hipMalloc(&d_dict, dict_len + 64));
-        hipError_t e = hipMemcpy(d_dict, dict, dict_len, hipMemcpyHostToDevice);
-        if (e != hipSuccess) { hipFree(d_dict); return hip_fail(e, "hipMemcpy(dict)"); }
-    }
-    struct DictFree { uint8_t* p; ~DictFree() { if (p) hipFree(p); } } dict_free{ d_dict };
-    std::vector<uint64_t> meta(4 * (size_t)n);
-    uint64_t ti = 0, to = 0;
-    for (uint32_t i = 0; i < n; ++i) {
-        meta[i] = ti; meta[n + i] = in_len[i];
-        meta[2 * (size_t)n + i] = to; meta[3 * (size_t)n + i] = out_cap[i];
-        ti += (in_len[i] + 15) & ~(uint64_t)15;
-        to += (out_cap[i] + 7) & ~(uint64_t)7;
-    }
-    HostBatch hb;
-    HIPCHK(hipMalloc(&hb.d_in, ti + 128));
-    HIPCHK(hipMalloc(&hb.d_out, to + 64));
-    HIPCHK(hipMalloc(&hb.d_meta, meta.size() * sizeof(uint64_t)));
-    HIPCHK(hipMalloc(&hb.d_rec, (size_t)n * sizeof(sdz_deflate_record)));
-    for (uint32_t i = 0; i < n; ++i)
-        if (in_len[i]) HIPCHK(hipMemcpy(hb.d_in + meta[i], in[i], in_len[i], hipMemcpyHostToDevice));
-    HIPCHK(hipMemcpy(hb.d_meta, meta.data(), meta.size() * sizeof(uint64_t), hipMemcpyHostToDevice));
-    int rc = sdz_deflate_batch_device(hb.d_in, hb.d_meta, hb.d_meta + n, hb.d_out, hb.d_meta + 2 * (size_t)n,
-                                      hb.d_meta + 3 * (size_t)n, (sdz_deflate_record*)hb.d_rec, n, level,
-                                      format, fname, (uint32_t)fname_len, mtime, d_dict, (uint32_t)dict_len,
-                                      nullptr);
-    if (rc) return rc;
-    HIPCHK(hipDeviceSynchronize());
-    std::vector<sdz_deflate_record> r(n);
-    HIPCHK(hipMemcpy(r.data(), hb.d_rec, (size_t)n * sizeof(sdz_deflate_record), hipMemcpyDeviceToHost));
-    for (uint32_t i = 0; i < n; ++i) {
-        rec[i] = r[i];
-        uint64_t len = std::min<uint64_t>(r[i].out_len, out_cap[i]);
-        if (len && out[i]) HIPCHK(hipMemcpy(out[i], hb.d_out + meta[2 * (size_t)n + i], len, hipMemcpyDeviceToHost));
-    }
-    return SDZ_API_OK;
-}
 
 }  // extern "C"

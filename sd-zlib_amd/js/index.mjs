@@ -7,9 +7,12 @@
 // Inflater.append() decodes each chunk on the GPU as it arrives: the stream's
 // decoder state, window, unfinished input and running checksum stay on the
 // device between appends (sdz_inflater_*), and append() returns the output the
-// reference's append() returns, in 16 KiB chunks (zstream.ts:11).  Deflater
-// compresses on the GPU at finish(); merged outputs are identical to the
-// reference's.
+// reference's append() returns, in the same arrays: one per 16 KiB ZStream pass
+// (zstream.ts:11; pinned against the oracle's restatement of sd-inflate.ts:101-150).
+// Deflater.append()/finish() compress each chunk on the GPU as it arrives (sdz_deflater_*:
+// window, hash chains, pending block and checksum stay on the device) and return the
+// reference's arrays: the container header on its own, 16 KiB passes, the trailer on its
+// own (sd-deflate.ts:199-250).
 import { createRequire } from "module";
 
 const require = createRequire(import.meta.url);
@@ -103,6 +106,7 @@ export class Inflater {
 		this.handle = null;
 		this.head = [];          // the stream's first bytes (gzip FNAME)
 		this.headLen = 0;
+		this.keepHead = true;
 		this.last = undefined;
 		this.done = false;
 		this.error = null;
@@ -125,13 +129,17 @@ export class Inflater {
 		if (this.handle === null) {
 			this.handle = addon.inflaterCreate(this.raw, this.dict || null);
 		}
-		if (this.headLen < 65536) {
-			const h = chunk.subarray(0, 65536 - this.headLen);
-			this.head.push(h);
-			this.headLen += h.length;
+		if (this.keepHead) {                     // input until the header is past (gzip FNAME bytes)
+			this.head.push(chunk.slice());
+			this.headLen += chunk.length;
 		}
 		const r = addon.inflaterAppend(this.handle, chunk);
 		this.last = r;
+		if (this.keepHead && (r.data.length > 0 || r.status !== "TRUNCATED")) {
+			// output (or the end) means the header is complete: keep only the FNAME's bytes
+			this.head = [mergeBuffers(this.head).slice(0, r.nameOff + r.nameLen)];
+			this.keepHead = false;
+		}
 		if (r.status !== "TRUNCATED") {
 			this.done = true;
 			try {
@@ -233,6 +241,7 @@ export class Deflater {
 		});
 		this.fileName = new Uint8Array(name);
 		this.handle = null;
+		this.started = false;       // a non-empty append happened (Deflate.status left INIT)
 		this.mtime = undefined;     // gzip MTIME override (tests); default Date.now() at the first append
 	}
 
@@ -245,9 +254,20 @@ export class Deflater {
 		}
 		const r = addon.deflaterAppend(this.handle, chunk, finish);
 		if (r.status !== "OK") {
-			throw new Error("deflating: " + r.status);
+			throw new Error("deflating: ");     // sd-deflate.ts:213, 241: z.msg, never set by deflate.ts
 		}
-		return chunks(r.data);
+		return r.data;
+	}
+
+	// sd-deflate.ts:199-206: the container header is pushed as an array of its own
+	headerLength(out) {
+		if (this.format === "deflate") {
+			return out.length > 1 && out[1] === 0x20 ? 6 : 2;     // 78 20 + DICTID, or 78 01
+		}
+		if (this.format === "gzip") {
+			return 10 + (this.fileName.length ? this.fileName.length + 1 : 0);
+		}
+		return 0;
 	}
 
 	append(data) {
@@ -258,14 +278,26 @@ export class Deflater {
 		if (!chunk.length) {
 			return [];
 		}
-		return this.call(chunk, false);
+		const first = !this.started;
+		const out = this.call(chunk, false);
+		this.started = true;
+		const h = first ? this.headerLength(out) : 0;
+		const res = h ? [out.subarray(0, h)] : [];
+		return res.concat(chunks(out.subarray(h)));
 	}
 
+	// sd-deflate.ts:228-253: the 16 KiB passes of deflate(FINISH), then the trailer
 	finish() {
-		if (this.handle === null) {
+		if (this.handle === null || !this.started) {
 			throw new Error("Cannot call finish before at least 1 call to append");
 		}
-		return this.call(new Uint8Array(0), true);
+		const out = this.call(new Uint8Array(0), true);
+		const t = this.format === "deflate" ? 4 : this.format === "gzip" ? 8 : 0;
+		const res = chunks(out.subarray(0, out.length - t));
+		if (t) {
+			res.push(out.subarray(out.length - t));
+		}
+		return res;
 	}
 }
 
@@ -285,23 +317,38 @@ export function deflate(data, options) {
 	const mtime = Math.floor(Date.now() / 1000);      // sd-deflate.ts:140
 	const r = addon.deflateBatch([input], d.level, fmt, d.fileName, mtime, d.dict || null)[0];
 	if (r.status !== "OK") {
-		throw new Error("deflating: " + r.status);
+		throw new Error("deflating: ");         // sd-deflate.ts:213 (z.msg is never set)
 	}
 	return r.data;
 }
 
-// batched entry points (the GPU's native shape; not in the reference API)
-export function inflateBatch(streams, outCaps, format) {
+// batched entry points (the GPU's native shape; not in the reference API).
+// inflateBatch(streams, {outCaps, format, dictionary, devices}) -- with `devices` (HIP device
+// ids) the batch is LPT-sharded over those GPUs, one host thread each, and the records are
+// all-gathered over RCCL (sdz_inflate_batch_multi); the result array then carries `stats`
+// (wallMs, computeMs, gatherMs, per-shard streams / bytes / kernelMs).  The older positional
+// form inflateBatch(streams, outCaps, format) is still accepted.
+export function inflateBatch(streams, options, format) {
+	const o = Array.isArray(options) ? { outCaps: options, format } : (options || {});
 	const views = streams.map(s => u8ArrayFromBufferSource(s));
-	const caps = outCaps || views.map(v => Math.max(65536, v.length * 8));
-	return addon.inflateBatch(views, format === undefined ? FMT_AUTO : format, caps, null);
+	const caps = o.outCaps || views.map(v => Math.max(65536, v.length * 8));
+	const dict = o.dictionary ? u8ArrayFromBufferSource(o.dictionary) : null;
+	return addon.inflateBatch(views, o.format === undefined ? FMT_AUTO : o.format, caps, dict,
+		o.devices && o.devices.length ? o.devices : null);
 }
 
+// deflateBatch(streams, {level, format, fileName, mtime, dictionary, devices})
 export function deflateBatch(streams, options) {
 	const o = options || {};
 	const views = streams.map(s => u8ArrayFromBufferSource(s));
 	const fmt = o.format === "raw" ? 0 : o.format === "gzip" ? 2 : 1;
-	return addon.deflateBatch(views, o.level || 6, fmt, new Uint8Array(0), o.mtime || 0, null);
+	const name = new Uint8Array(Array.from(o.fileName || "").map(c => {
+		const cc = c.charCodeAt(0);
+		return cc > 0xff ? 95 : cc;
+	}));
+	const dict = o.dictionary ? u8ArrayFromBufferSource(o.dictionary) : null;
+	return addon.deflateBatch(views, o.level || 6, fmt, name, o.mtime || 0, dict,
+		o.devices && o.devices.length ? o.devices : null);
 }
 
 export function deviceCount() {

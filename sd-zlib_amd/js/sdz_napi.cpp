@@ -54,6 +54,46 @@ void set_bool(napi_env env, napi_value o, const char* k, bool b) {
     napi_set_named_property(env, o, k, x);
 }
 
+// devices: an optional array of HIP device ids (sdz_*_batch_multi); false when absent/empty
+bool get_devices(napi_env env, size_t argc, napi_value* argv, size_t k, std::vector<int32_t>* devs) {
+    if (argc <= k) return false;
+    bool is_arr = false;
+    napi_is_array(env, argv[k], &is_arr);
+    if (!is_arr) return false;
+    uint32_t nd = 0;
+    napi_get_array_length(env, argv[k], &nd);
+    for (uint32_t i = 0; i < nd; ++i) {
+        napi_value e;
+        int32_t d = 0;
+        if (napi_get_element(env, argv[k], i, &e) != napi_ok || napi_get_value_int32(env, e, &d) != napi_ok) return false;
+        devs->push_back(d);
+    }
+    return !devs->empty();
+}
+
+// the multi-GPU call's stats as a JS object (gather timed apart from compute)
+napi_value stats_object(napi_env env, const sdz_multi_stats& st) {
+    napi_value o, ks;
+    napi_create_object(env, &o);
+    napi_value x;
+    napi_create_double(env, st.wall_ms, &x); napi_set_named_property(env, o, "wallMs", x);
+    napi_create_double(env, st.compute_ms, &x); napi_set_named_property(env, o, "computeMs", x);
+    napi_create_double(env, st.gather_ms, &x); napi_set_named_property(env, o, "gatherMs", x);
+    set_bool(env, o, "rccl", st.collective != 0);
+    napi_create_array_with_length(env, (size_t)st.nshards, &ks);
+    for (int32_t k = 0; k < st.nshards; ++k) {
+        napi_value sh;
+        napi_create_object(env, &sh);
+        set_int(env, sh, "streams", st.streams[k]);
+        set_int(env, sh, "bytesIn", (int64_t)st.bytes_in[k]);
+        set_int(env, sh, "bytesOut", (int64_t)st.bytes_out[k]);
+        napi_create_double(env, st.kernel_ms[k], &x); napi_set_named_property(env, sh, "kernelMs", x);
+        napi_set_element(env, ks, (uint32_t)k, sh);
+    }
+    napi_set_named_property(env, o, "shards", ks);
+    return o;
+}
+
 const char* verdict(int v) { return v == SDZ_MATCH ? "match" : v == SDZ_MISMATCH ? "mismatch" : "unchecked"; }
 const char* status_name(int s) {
     switch (s) {
@@ -71,10 +111,11 @@ const char* status_name(int s) {
     }
 }
 
-// inflateBatch(streams: Uint8Array[], format: number, outCaps: number[], dict: Uint8Array|null)
+// inflateBatch(streams: Uint8Array[], format: number, outCaps: number[], dict: Uint8Array|null,
+//              devices?: number[]) -- with devices, LPT shards over those GPUs (result.stats)
 napi_value InflateBatch(napi_env env, napi_callback_info info) {
-    size_t argc = 4;
-    napi_value argv[4];
+    size_t argc = 5;
+    napi_value argv[5];
     NAPI_OK(napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr));
     uint32_t n = 0;
     NAPI_OK(napi_get_array_length(env, argv[0], &n));
@@ -105,7 +146,12 @@ napi_value InflateBatch(napi_env env, napi_callback_info info) {
     napi_typeof(env, argv[3], &dt);
     if (dt != napi_null && dt != napi_undefined) get_bytes(env, argv[3], &dict, &dict_len);
     std::vector<sdz_inflate_record> rec(n);
-    int rc = sdz_inflate_batch(in.data(), in_len.data(), out.data(), cap.data(), rec.data(), n, fmt, dict, dict_len);
+    std::vector<int32_t> devs;
+    const bool multi = get_devices(env, argc, argv, 4, &devs);
+    sdz_multi_stats st;
+    int rc = multi ? sdz_inflate_batch_multi(in.data(), in_len.data(), out.data(), cap.data(), rec.data(), n, fmt, dict,
+                                             dict_len, devs.data(), (int32_t)devs.size(), &st)
+                   : sdz_inflate_batch(in.data(), in_len.data(), out.data(), cap.data(), rec.data(), n, fmt, dict, dict_len);
     if (rc) {
         napi_throw_error(env, nullptr, (std::string("libsdz: ") + sdz_last_error()).c_str());
         return nullptr;
@@ -135,14 +181,15 @@ napi_value InflateBatch(napi_env env, napi_callback_info info) {
         napi_set_named_property(env, o, "data", ta);
         NAPI_OK(napi_set_element(env, arr, i, o));
     }
+    if (multi) napi_set_named_property(env, arr, "stats", stats_object(env, st));
     return arr;
 }
 
 // deflateBatch(streams: Uint8Array[], level, format, fileNameLatin1: Uint8Array, mtime,
-//              dict: Uint8Array|null)
+//              dict: Uint8Array|null, devices?: number[])
 napi_value DeflateBatch(napi_env env, napi_callback_info info) {
-    size_t argc = 6;
-    napi_value argv[6];
+    size_t argc = 7;
+    napi_value argv[7];
     NAPI_OK(napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr));
     uint32_t n = 0;
     NAPI_OK(napi_get_array_length(env, argv[0], &n));
@@ -180,8 +227,14 @@ napi_value DeflateBatch(napi_env env, napi_callback_info info) {
         out[i] = (uint8_t*)p;
     }
     std::vector<sdz_deflate_record> rec(n);
-    int rc = sdz_deflate_batch(in.data(), in_len.data(), out.data(), cap.data(), rec.data(), n, level, fmt,
-                               fname_len ? fname : nullptr, fname_len, mtime, dict, dict_len);
+    std::vector<int32_t> devs;
+    const bool multi = get_devices(env, argc, argv, 6, &devs);
+    sdz_multi_stats st;
+    int rc = multi ? sdz_deflate_batch_multi(in.data(), in_len.data(), out.data(), cap.data(), rec.data(), n, level, fmt,
+                                             fname_len ? fname : nullptr, fname_len, mtime, dict, dict_len, devs.data(),
+                                             (int32_t)devs.size(), &st)
+                   : sdz_deflate_batch(in.data(), in_len.data(), out.data(), cap.data(), rec.data(), n, level, fmt,
+                                       fname_len ? fname : nullptr, fname_len, mtime, dict, dict_len);
     if (rc) {
         napi_throw_error(env, nullptr, (std::string("libsdz: ") + sdz_last_error()).c_str());
         return nullptr;
@@ -199,6 +252,7 @@ napi_value DeflateBatch(napi_env env, napi_callback_info info) {
         napi_set_named_property(env, o, "data", ta);
         NAPI_OK(napi_set_element(env, arr, i, o));
     }
+    if (multi) napi_set_named_property(env, arr, "stats", stats_object(env, st));
     return arr;
 }
 

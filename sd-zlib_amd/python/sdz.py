@@ -65,7 +65,19 @@ EXPORTS = [
     "sdz_deflate_state_bytes", "sdz_deflate_append_bound", "sdz_deflate_state_reset_device",
     "sdz_deflate_append_batch_device", "sdz_deflater_create", "sdz_deflater_append", "sdz_deflater_destroy",
     "sdz_deflate_fast_bound", "sdz_deflate_fast_batch_device",
+    "sdz_gather_device", "sdz_lpt_shard", "sdz_inflate_batch_multi", "sdz_deflate_batch_multi",
+    "sdz_comm_unique_id", "sdz_comm_init_rank", "sdz_comm_allgather_device", "sdz_comm_allreduce_max",
+    "sdz_comm_destroy",
 ]
+
+MAX_SHARDS = 16
+
+
+class MultiStats(ctypes.Structure):
+    _fields_ = [("wall_ms", ctypes.c_double), ("compute_ms", ctypes.c_double), ("gather_ms", ctypes.c_double),
+                ("kernel_ms", ctypes.c_float * MAX_SHARDS), ("bytes_in", ctypes.c_uint64 * MAX_SHARDS),
+                ("bytes_out", ctypes.c_uint64 * MAX_SHARDS), ("streams", ctypes.c_uint32 * MAX_SHARDS),
+                ("nshards", ctypes.c_int32), ("collective", ctypes.c_int32)]
 
 _lib = None
 
@@ -156,6 +168,26 @@ def lib():
         L.sdz_deflate_fast_bound.restype = ctypes.c_uint64
         L.sdz_deflate_fast_batch_device.argtypes = [vp, vp, vp, vp, vp, vp, vp, u32, i32, vp, u32, u32, vp]
         L.sdz_deflate_fast_batch_device.restype = ctypes.c_int
+    if hasattr(L, "sdz_gather_device"):
+        L.sdz_gather_device.argtypes = [vp, vp, vp, vp, vp, u32, vp]
+        L.sdz_gather_device.restype = ctypes.c_int
+        L.sdz_lpt_shard.argtypes = [vp, u32, u32, vp]
+        L.sdz_lpt_shard.restype = ctypes.c_int
+        i32p = ctypes.POINTER(i32)
+        L.sdz_inflate_batch_multi.argtypes = L.sdz_inflate_batch.argtypes + [i32p, i32, ctypes.POINTER(MultiStats)]
+        L.sdz_inflate_batch_multi.restype = ctypes.c_int
+        L.sdz_deflate_batch_multi.argtypes = L.sdz_deflate_batch.argtypes + [i32p, i32, ctypes.POINTER(MultiStats)]
+        L.sdz_deflate_batch_multi.restype = ctypes.c_int
+        L.sdz_comm_unique_id.argtypes = [vp]
+        L.sdz_comm_unique_id.restype = ctypes.c_int
+        L.sdz_comm_init_rank.argtypes = [vp, i32, i32]
+        L.sdz_comm_init_rank.restype = vp
+        L.sdz_comm_allgather_device.argtypes = [vp, vp, vp, ctypes.c_uint64]
+        L.sdz_comm_allgather_device.restype = ctypes.c_int
+        L.sdz_comm_allreduce_max.argtypes = [vp, ctypes.POINTER(ctypes.c_double)]
+        L.sdz_comm_allreduce_max.restype = ctypes.c_int
+        L.sdz_comm_destroy.argtypes = [vp]
+        L.sdz_comm_destroy.restype = ctypes.c_int
     _lib = L
     return L
 
@@ -209,6 +241,114 @@ def inflate_batch(streams, out_caps=None, fmt=FMT_AUTO, dictionary=None):
     _check(L.sdz_inflate_batch(ins, in_len, outs, caps, recs, n, fmt, d, len(d) if d else 0))
     return [_record_dict(recs[i], bufs[i].raw[:min(recs[i].out_len, out_caps[i])], streams[i])
             for i in range(n)]
+
+
+def lpt_shard(sizes, nshards):
+    """Shard index of each stream (sdz_lpt_shard: largest first onto the least-loaded shard)."""
+    n = len(sizes)
+    owner = (ctypes.c_uint32 * max(1, n))()
+    _check(lib().sdz_lpt_shard(_u64_array(list(sizes)) if n else None, n, nshards, owner))
+    return list(owner[:n])
+
+
+def _stats_dict(st):
+    k = st.nshards
+    return {"wall_ms": st.wall_ms, "compute_ms": st.compute_ms, "gather_ms": st.gather_ms,
+            "rccl": bool(st.collective), "kernel_ms": list(st.kernel_ms[:k]), "bytes_in": list(st.bytes_in[:k]),
+            "bytes_out": list(st.bytes_out[:k]), "streams": list(st.streams[:k])}
+
+
+def inflate_batch_multi(streams, devices, out_caps=None, fmt=FMT_AUTO, dictionary=None):
+    """inflate_batch LPT-sharded over `devices` (one host thread per GPU; records all-gathered
+    over RCCL, or a loopback gather when a device repeats).  Returns (records, stats)."""
+    L = lib()
+    n = len(streams)
+    streams = [bytes(s) for s in streams]
+    if out_caps is None:
+        out_caps = [max(1 << 16, 8 * len(s)) for s in streams]
+    ins = (ctypes.c_char_p * n)(*streams)
+    in_len = (ctypes.c_size_t * n)(*[len(s) for s in streams])
+    bufs = [ctypes.create_string_buffer(max(1, c)) for c in out_caps]
+    outs = (ctypes.c_void_p * n)(*[ctypes.addressof(b) for b in bufs])
+    caps = (ctypes.c_size_t * n)(*out_caps)
+    recs = (InflateRecord * n)()
+    d = bytes(dictionary) if dictionary is not None else None
+    devs = (ctypes.c_int32 * len(devices))(*devices)
+    st = MultiStats()
+    _check(L.sdz_inflate_batch_multi(ins, in_len, outs, caps, recs, n, fmt, d, len(d) if d else 0, devs,
+                                     len(devices), ctypes.byref(st)))
+    return ([_record_dict(recs[i], bufs[i].raw[:min(recs[i].out_len, out_caps[i])], streams[i]) for i in range(n)],
+            _stats_dict(st))
+
+
+def deflate_batch_multi(streams, devices, level=6, format="deflate", file_name_latin1=b"", mtime=0,
+                        dictionary=None):
+    """deflate_batch LPT-sharded over `devices`.  Returns (results, stats)."""
+    L = lib()
+    n = len(streams)
+    streams = [bytes(s) for s in streams]
+    fmt = DEFLATE_FORMATS[format]
+    caps_l = [int(L.sdz_deflate_bound(len(s), fmt, len(file_name_latin1))) for s in streams]
+    ins = (ctypes.c_char_p * n)(*streams)
+    in_len = (ctypes.c_size_t * n)(*[len(s) for s in streams])
+    bufs = [ctypes.create_string_buffer(c) for c in caps_l]
+    outs = (ctypes.c_void_p * n)(*[ctypes.addressof(b) for b in bufs])
+    caps = (ctypes.c_size_t * n)(*caps_l)
+    recs = (DeflateRecord * n)()
+    fn = bytes(file_name_latin1)
+    d = bytes(dictionary) if dictionary is not None else None
+    devs = (ctypes.c_int32 * len(devices))(*devices)
+    st = MultiStats()
+    _check(L.sdz_deflate_batch_multi(ins, in_len, outs, caps, recs, n, level, fmt, fn or None, len(fn),
+                                     mtime & 0xFFFFFFFF, d, len(d) if d is not None else 0, devs, len(devices),
+                                     ctypes.byref(st)))
+    return ([{"status": STATUS.get(recs[i].status, recs[i].status), "checksum": recs[i].checksum,
+              "data": bufs[i].raw[:recs[i].out_len]} for i in range(n)], _stats_dict(st))
+
+
+class Comm:
+    """One rank of an RCCL communicator inside libsdz (one process per GPU): the id travels
+    by the caller's own means (e.g. a torchrun TCP store), then every rank joins on its
+    current device.  all-gather of device buffers, and a max-allreduce of a host value."""
+
+    ID_BYTES = 128
+
+    @staticmethod
+    def unique_id():
+        b = ctypes.create_string_buffer(Comm.ID_BYTES)
+        _check(lib().sdz_comm_unique_id(b))
+        return b.raw
+
+    def __init__(self, uid, nranks, rank):
+        self.nranks, self.rank = nranks, rank
+        self.h = lib().sdz_comm_init_rank(bytes(uid), nranks, rank)
+        if not self.h:
+            raise SdzError("libsdz: %s" % lib().sdz_last_error().decode())
+
+    def allgather_device(self, send_ptr, recv_ptr, nbytes):
+        _check(lib().sdz_comm_allgather_device(self.h, send_ptr, recv_ptr, nbytes))
+
+    def allgather_bytes(self, data):
+        """every rank's `data` (equal lengths) through the device, in rank order"""
+        nb = len(data)
+        src, dst = DeviceBuffer(nb), DeviceBuffer(nb * self.nranks)
+        if nb:
+            src.upload(data)
+        self.allgather_device(src.ptr, dst.ptr, nb)
+        out = dst.download(nb * self.nranks)
+        src.free()
+        dst.free()
+        return [out[r * nb:(r + 1) * nb] for r in range(self.nranks)]
+
+    def max(self, v):
+        x = ctypes.c_double(v)
+        _check(lib().sdz_comm_allreduce_max(self.h, ctypes.byref(x)))
+        return x.value
+
+    def close(self):
+        if self.h:
+            lib().sdz_comm_destroy(self.h)
+            self.h = None
 
 
 def inflate_one(data, fmt=FMT_AUTO, dictionary=None):
@@ -387,6 +527,7 @@ class InflateStreams:
             self.dict.upload(bytes(dictionary))
             self.dict_len = len(dictionary)
         self.heads = [b""] * n
+        self.keep = [True] * n
         self.sent = [0] * n               # stream offset after the bytes passed so far
 
     def append(self, chunks, out_cap=1 << 20):
@@ -419,10 +560,13 @@ class InflateStreams:
         recs = (InflateRecord * n).from_buffer_copy(d_rec.download(n * ctypes.sizeof(InflateRecord)))
         res = []
         for i in range(n):
-            if len(self.heads[i]) < 65536:
-                self.heads[i] += chunks[i][:65536 - len(self.heads[i])]
+            if self.keep[i]:              # input until the header is past (gzip FNAME bytes)
+                self.heads[i] += chunks[i]
             data = d_out.download(recs[i].out_len, out_off[i]) if recs[i].out_len else b""
             r = _record_dict(recs[i], data, self.heads[i])
+            if self.keep[i] and (recs[i].out_len or r["status"] != "TRUNCATED"):
+                self.heads[i] = self.heads[i][:recs[i].name_off + recs[i].name_len]
+                self.keep[i] = False
             r["out_full"] = bool(recs[i].out_full)
             end = self.sent[i] + len(chunks[i])
             keep = end - recs[i].in_used if recs[i].out_full else 0
@@ -511,6 +655,7 @@ class Inflater:
         self._h = None
         self._rec = None
         self._head = b""                 # the stream's first bytes, for the gzip FNAME
+        self._keep_head = True
         self._done = False
         self._err = None
 
@@ -531,8 +676,8 @@ class Inflater:
             raise self._err
         if self._done:                   # sd-inflate.ts:130-132: nothing of this chunk consumed
             raise SdzError("inflate error: bad input data")
-        if len(self._head) < 65536:
-            self._head += chunk[:65536 - len(self._head)]
+        if self._keep_head:              # input until the header is past (gzip FNAME bytes)
+            self._head += chunk
         rec = InflateRecord()
         optr, olen = ctypes.c_void_p(), ctypes.c_size_t()
         _check(lib().sdz_inflater_append(self._handle(), chunk, len(chunk), ctypes.byref(optr),
@@ -540,6 +685,10 @@ class Inflater:
         out = ctypes.string_at(optr, olen.value) if olen.value else b""
         self._rec = rec
         r = _record_dict(rec, out, self._head)
+        if self._keep_head and (rec.out_len or r["status"] != "TRUNCATED"):
+            # output (or the end) means the header is complete: keep only the FNAME's bytes
+            self._head = self._head[:rec.name_off + rec.name_len]
+            self._keep_head = False
         if r["status"] != "TRUNCATED":
             self._done = True
             try:
@@ -622,6 +771,7 @@ class Deflater:
         self._level, self._fmt = level, fmt
         self._name = _latin1(file_name or "")
         self._h = None
+        self._started = False            # a non-empty append happened (Deflate.status left INIT)
         self.mtime = None                # gzip MTIME: None = Math.floor(Date.now()/1000) at the first append
 
     def _handle(self):
@@ -641,22 +791,38 @@ class Deflater:
                                          ctypes.byref(optr), ctypes.byref(olen), ctypes.byref(rec)))
         return rec, (ctypes.string_at(optr, olen.value) if olen.value else b"")
 
+    def _header_len(self, out):
+        """sd-deflate.ts:199-206 pushes the container header as an array of its own"""
+        if self._fmt == "deflate":
+            return 6 if len(out) > 1 and out[1] == 0x20 else 2       # 78 20 + DICTID, or 78 01
+        if self._fmt == "gzip":
+            return 10 + (len(self._name) + 1 if self._name else 0)
+        return 0
+
     def append(self, data):
+        """The arrays sd-deflate.ts:173-221 returns: the header first (first append), then the
+        16 KiB ZStream passes (zstream.ts:11) of this call's compressed bytes."""
         chunk = _u8(data)
         if not chunk:
             return []                    # sd-deflate.ts:180-182
+        first = not self._started
         rec, out = self._call(chunk, False)
         if rec.status != 0:
-            raise SdzError("deflating: " + STATUS.get(rec.status, str(rec.status)))
-        return _chunks(out)
+            raise SdzError("deflating: ")    # sd-deflate.ts:213: z.msg, never set by deflate.ts
+        self._started = True
+        h = self._header_len(out) if first else 0
+        return ([out[:h]] if h else []) + _chunks(out[h:])
 
     def finish(self):
-        if self._h is None:
+        """sd-deflate.ts:228-253: the 16 KiB passes of deflate(FINISH), then the trailer."""
+        if self._h is None or not self._started:
             raise SdzError("Cannot call finish before at least 1 call to append")
         rec, out = self._call(b"", True)
         if rec.status != 0:
-            raise SdzError("deflating: " + STATUS.get(rec.status, str(rec.status)))
-        return _chunks(out)
+            raise SdzError("deflating: ")    # sd-deflate.ts:241
+        t = {"deflate": 4, "gzip": 8}.get(self._fmt, 0)
+        body = out[:len(out) - t]
+        return _chunks(body) + ([out[len(out) - t:]] if t else [])
 
     def __del__(self):
         try:
@@ -678,5 +844,5 @@ def deflate(data, options=None):
     mtime = d.mtime if d.mtime is not None else int(math.floor(time.time()))
     r = deflate_batch([inp], d._level, d._fmt, d._name, mtime, dictionary=d._dict)[0]
     if r["status"] != "OK":
-        raise SdzError("deflating: " + r["status"])
+        raise SdzError("deflating: ")        # sd-deflate.ts:213 (z.msg is never set)
     return r["data"]

@@ -5,7 +5,8 @@ ranks by size (LPT: largest first, onto the rank with the fewest bytes so far) a
 each rank runs the single-GPU C ABI on its shard.  The only collective is the
 all-gather of the fixed-size per-stream records at the end (RCCL on GPUs via the
 "nccl" backend; gloo in the CPU tests), after which every rank can reassemble the
-records in the original stream order.
+records in the original stream order.  With the engine's own communicator (sdz.Comm: RCCL
+inside libsdz, one rank per process) the gather never touches torch.distributed.
 """
 import heapq
 
@@ -41,6 +42,19 @@ def gather_records(rec_bytes, rec_size, shards, rank, device="cpu"):
     result = [None] * total
     for r in range(world):
         data = outs[r].cpu().numpy().tobytes()
+        for k, i in enumerate(shards[r]):
+            result[i] = data[k * rec_size:(k + 1) * rec_size]
+    return result
+
+
+def gather_records_comm(comm, rec_bytes, rec_size, shards):
+    """gather_records over libsdz's RCCL communicator (sdz.Comm.allgather_bytes)."""
+    n_max = max(len(s) for s in shards)
+    buf = bytearray(n_max * rec_size)
+    buf[:len(rec_bytes)] = rec_bytes
+    parts = comm.allgather_bytes(bytes(buf))
+    result = [None] * sum(len(s) for s in shards)
+    for r, data in enumerate(parts):
         for k, i in enumerate(shards[r]):
             result[i] = data[k * rec_size:(k + 1) * rec_size]
     return result

@@ -4,7 +4,7 @@
 import { readFileSync } from "fs";
 import { fileURLToPath } from "url";
 import { dirname, join } from "path";
-import { inflate, deflate, Inflater, Deflater, adler32, crc32, mergeBuffers } from "../../sd-zlib_amd/js/index.mjs";
+import { inflate, deflate, Inflater, Deflater, adler32, crc32, mergeBuffers, inflateBatch, deflateBatch } from "../../sd-zlib_amd/js/index.mjs";
 
 const here = dirname(fileURLToPath(import.meta.url));
 const golden = name => new Uint8Array(readFileSync(join(here, "..", "golden", name)));
@@ -79,6 +79,47 @@ check("deflate L6 == reference fixture", eq(deflate(text, { level: 6 }), golden(
 	const inf = new Inflater({ dictionary: words });
 	const out = mergeBuffers(inf.append(comp));
 	check("dictionary round trip", comp[0] === 0x78 && comp[1] === 0x20 && eq(out, src) && inf.finish().success);
+}
+{
+	// the reference's arrays: Inflater.append -> 16 KiB ZStream passes (sd-inflate.ts:101-150)
+	const inf = new Inflater();
+	const a = inf.append(golden("paradiselost.part1.deflate"));
+	const b = inf.append(golden("paradiselost.part2.deflate"));
+	const full = x => x.slice(0, -1).every(c => c.length === 16384);
+	check("Inflater arrays are 16 KiB passes", a.length > 1 && b.length > 1 && full(a) && full(b) &&
+		eq(mergeBuffers(a.concat(b)), text));
+	// Deflater: the header alone, 16 KiB passes, the trailer alone (sd-deflate.ts:199-250)
+	const d = new Deflater({ level: 6, format: "gzip", fileName: "p.txt" });
+	const x = d.append(text);
+	const f = d.finish();
+	check("Deflater arrays: header | passes | trailer", x[0].length === 10 + 6 && full(x.slice(1)) &&
+		f[f.length - 1].length === 8 && full(f.slice(0, -1)));
+	let m = "";
+	try { d.append(new Uint8Array([1, 2, 3])); } catch (e) { m = e.message; }
+	check("append after finish: deflating + z.msg", m === "deflating: ");
+}
+{
+	// a gzip FNAME longer than 64 KiB comes back whole
+	const name = "n".repeat(70000) + ".txt";
+	const d = new Deflater({ level: 6, format: "gzip", fileName: name });
+	const comp = mergeBuffers(d.append(golden("simple.txt")).concat(d.finish()));
+	const inf = new Inflater();
+	inf.append(comp);
+	check("gzip FNAME > 64 KiB", inf.finish().fileName === name);
+}
+{
+	// batched entry points over GPUs: LPT shards, records all-gathered (RCCL one rank / loopback)
+	const streams = [golden("paradiselost.deflate"), golden("simple.deflate"), golden("paradiselost.gz"),
+		golden("simple.raw")];
+	const want = [text, golden("simple.txt"), text, golden("simple.txt")];
+	for (const devices of [[0], [0, 0]]) {
+		const r = inflateBatch(streams, { outCaps: want.map(w => w.length + 64), devices });
+		check("inflateBatch devices " + JSON.stringify(devices), r.every((x, i) => x.success && eq(x.data, want[i])) &&
+			r.stats && r.stats.shards.length === devices.length && r.stats.rccl === (devices.length === 1));
+	}
+	const dz = deflateBatch([text, golden("simple.txt")], { level: 6, devices: [0, 0] });
+	check("deflateBatch devices [0,0]", eq(dz[0].data, golden("paradiselost.deflate")) &&
+		eq(dz[1].data, golden("simple.deflate")));
 }
 check("adler32 KAT", adler32(golden("simple.txt")) === -1612443532);
 check("crc32 KAT", crc32(golden("simple.txt")) === 1488305224);

@@ -45,7 +45,7 @@ def test_library_exports_every_declared_symbol(built):
 def test_library_loads_and_python_binding_matches(built):
     import sdz
     L = sdz.lib()
-    assert L.sdz_version() == 3
+    assert L.sdz_version() == 4
     assert sorted(sdz.EXPORTS) == declared_functions()
     for name in sdz.EXPORTS:
         assert hasattr(L, name)

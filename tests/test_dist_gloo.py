@@ -1,4 +1,6 @@
-"""N>1 path on CPU: LPT sharding + record all-gather across 2 gloo ranks (no GPU)."""
+"""N>1 path: LPT sharding (libsdz's sdz_lpt_shard and the Python mirror agree) and the
+record all-gather across 2 gloo ranks on CPU; and, on the GPU box, 2 ranks that each run the
+real engine on their LPT shard of a C4-shaped batch and gather the records."""
 import os
 import random
 import socket
@@ -23,6 +25,18 @@ def test_lpt_shard_balances_and_covers():
 
 def test_lpt_shard_deterministic_for_equal_sizes():
     assert sdz_dist.lpt_shard([7] * 8, 2) == [[0, 2, 4, 6], [1, 3, 5, 7]]
+
+
+def test_lpt_shard_libsdz_matches_python():
+    """the C ABI's sdz_lpt_shard (used by sdz_*_batch_multi) is the same assignment"""
+    import sdz
+    rng = random.Random(9)
+    for world in (1, 2, 3, 8):
+        for n in (0, 1, 7, 500):
+            sizes = [int(4096 * 2 ** rng.uniform(0, 12)) if k % 5 else 4096 for k in range(n)]
+            owner = sdz.lpt_shard(sizes, world)
+            shards = sdz_dist.lpt_shard(sizes, world)
+            assert [sorted(i for i in range(n) if owner[i] == r) for r in range(world)] == shards
 
 
 def _free_port():
@@ -67,3 +81,57 @@ def test_gather_records_world2_gloo():
         assert len(got) == len(sizes)
         for i, (st, rk, olen, idx) in enumerate(got):
             assert (st, rk, olen, idx) == (0, owner[i], sizes[i] * 3, i)
+
+
+def _engine_worker(rank, world, port, q):
+    """one rank: the real engine on this rank's LPT shard, records all-gathered (gloo)"""
+    import torch.distributed as dist
+    import sdz
+    from test_gpu_multi import _mixed_batch
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    plain, comp = _mixed_batch(40, seed=21)
+    shards = sdz_dist.lpt_shard([len(c) for c in comp], world)
+    mine = shards[rank]
+    import ctypes
+    n = len(mine)
+    ins = (ctypes.c_char_p * n)(*[comp[i] for i in mine])
+    in_len = (ctypes.c_size_t * n)(*[len(comp[i]) for i in mine])
+    bufs = [ctypes.create_string_buffer(len(plain[i]) + 64) for i in mine]
+    outs = (ctypes.c_void_p * n)(*[ctypes.addressof(b) for b in bufs])
+    caps = (ctypes.c_size_t * n)(*[len(plain[i]) + 64 for i in mine])
+    recs = (sdz.InflateRecord * n)()
+    assert sdz.lib().sdz_inflate_batch(ins, in_len, outs, caps, recs, n, sdz.FMT_AUTO, None, 0) == 0
+    ok = all(bufs[k].raw[:recs[k].out_len] == plain[i] for k, i in enumerate(mine))
+    allrec = sdz_dist.gather_records(bytes(recs), 64, shards, rank)
+    dist.destroy_process_group()
+    q.put((rank, ok, [(r[0:4], r[8:16]) for r in allrec]))      # (status, out_len) per stream
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(300)
+def test_engine_shards_world2_gloo():
+    import struct
+    from test_gpu_multi import _mixed_batch
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_engine_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in procs:
+        rank, ok, recs = q.get(timeout=240)
+        res[rank] = (ok, recs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    plain, _ = _mixed_batch(40, seed=21)
+    for rank in (0, 1):
+        ok, recs = res[rank]
+        assert ok
+        assert len(recs) == len(plain)
+        for i, (st, ln) in enumerate(recs):
+            assert struct.unpack("<i", st)[0] == 0, i                   # SDZ_OK on every stream
+            assert struct.unpack("<Q", ln)[0] == len(plain[i]), i      # out_len, in stream order

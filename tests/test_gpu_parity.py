@@ -2,7 +2,8 @@
 
 Bit-exact bar for every byte, index and verdict.  Sizes are chosen so the
 oracle finishes in seconds; full-size configs are covered by size-independent
-properties (round trips, checksum of checksums) in test_gpu_scale.py.
+properties (round trips, checksum of checksums: bench.py checks every record of its
+full-size runs) and the C4-shaped batches of test_gpu_multi.py and test_gpu_split.py.
 """
 import random
 import struct
@@ -344,6 +345,29 @@ def test_deflate_record_path_bitexact(paradise):
             for g, d in zip(gpu, inputs):
                 exp = O.deflate(d, level=level, format=fmt, file_name="x.txt", mtime=77)
                 assert g["status"] == "OK" and g["data"] == exp, (level, fmt, len(d))
+
+
+def test_deflate_record_path_long_inputs(paradise):
+    """Inputs past 64 KiB on the record path: window slides every 32 KiB (deflate.ts:708-737)
+    -- chain units with 32 KiB of history, matches across segments, the last positions
+    searched in the slid window with its stale upper half, blocks whose start slid out of
+    the window (no stored block, deflate.ts:648) -- one stream alone (the LDS-staged parse)
+    and in a batch (one lane per stream)."""
+    rng = random.Random(13)
+    inputs = [paradise, text_corpus(rng, 300000), bytes(rng.getrandbits(8) for _ in range(200000)),
+              _periodic(rng, 150000), _overlay_stress(rng, 200000), binary_corpus(rng, 250000),
+              bytes(rng.getrandbits(8) for _ in range(100000)) + text_corpus(rng, 200000), b"a" * 300000,
+              text_corpus(rng, 98305), text_corpus(rng, 131073)]
+    for level in (4, 6, 9):
+        exp = [O.deflate(d, level=level) for d in inputs]
+        one = sdz.deflate_batch([paradise], level=level)[0]
+        assert one["status"] == "OK" and one["data"] == exp[0], level
+        gpu = sdz.deflate_batch(inputs, level=level)
+        for g, e, d in zip(gpu, exp, inputs):
+            assert g["status"] == "OK" and g["data"] == e, (level, len(d))
+    # gzip + file name through the facade (one buffer: the drop-in's deflate())
+    g = sdz.deflate(paradise, {"level": 6, "format": "gzip", "fileName": "p.txt"})
+    assert g[10:] == O.deflate(paradise, level=6, format="gzip", file_name="p.txt", mtime=0)[10:]
 
 
 def test_deflate_record_path_output_overflow(paradise):

@@ -238,3 +238,61 @@ def test_node_facade_smoke():
     r = subprocess.run([node, os.path.join(root, "tests", "node", "smoke.mjs")], capture_output=True,
                        text=True, timeout=120)
     assert r.returncode == 0, r.stdout + r.stderr
+
+
+def test_inflater_arrays_match_reference_chunks():
+    """Inflater.append returns the reference's arrays, not only its bytes: one Uint8Array per
+    16 KiB ZStream pass (sd-inflate.ts:101-150), as the oracle's restatement pushes them."""
+    text = golden("paradiselost.txt")
+    rng = random.Random(44)
+    cases = [[golden("paradiselost.part1.deflate"), golden("paradiselost.part2.deflate")],
+             [golden("paradiselost.gz")]]
+    for _ in range(6):
+        comp = zlib.compress(text[rng.randrange(200000):][:rng.randrange(1000, 250000)], rng.randint(1, 9))
+        cases.append(split(comp, [rng.randrange(len(comp)) for _ in range(rng.randint(0, 4))]))
+    for parts in cases:
+        per, ref = O.inflater_chunks(parts)
+        inf = sdz.Inflater()
+        got = [[len(a) for a in inf.append(p)] for p in parts]
+        assert got == [per[k] if parts[k] else [] for k in range(len(parts))]
+        assert inf.finish()["success"] == ref["success"]
+
+
+def test_deflater_arrays_header_passes_trailer():
+    """Deflater.append/finish return the reference's arrays (sd-deflate.ts:199-250): the
+    container header alone, 16 KiB passes, the trailer alone; and its error text."""
+    text = golden("paradiselost.txt")
+    for fmt, hlen, tlen in (("deflate", 2, 4), ("gzip", 10 + len("x.txt") + 1, 8), ("raw", 0, 0)):
+        d = sdz.Deflater({"level": 6, "format": fmt, "fileName": "x.txt" if fmt == "gzip" else None})
+        d.mtime = 0
+        a = d.append(text[:100000])
+        b = d.append(text[100000:])
+        f = d.finish()
+        if hlen:
+            assert len(a[0]) == hlen
+        body = a[1:] if hlen else a
+        assert all(len(x) == 16384 for x in body[:-1]) and all(len(x) == 16384 for x in b[:-1])
+        if tlen:
+            assert len(f[-1]) == tlen
+        merged = b"".join(a + b + f)
+        assert merged == O.deflater_run([text[:100000], text[100000:]], 6, fmt,
+                                        file_name="x.txt" if fmt == "gzip" else None, mtime=0)
+    # the reference throws "deflating: " + z.msg, and deflate.ts never sets z.msg
+    d = sdz.Deflater({"level": 1})
+    d.append(b"abc")
+    d.finish()
+    with pytest.raises(sdz.SdzError) as e:
+        d.append(b"more")                                 # append after finish: a stream error
+    assert str(e.value) == "deflating: "
+
+
+def test_gzip_long_file_name_kept():
+    """a FNAME longer than 64 KiB comes back whole (the facade keeps the input
+    until the header is past, not a fixed 64 KiB head)"""
+    name = "n" * 70000 + ".txt"
+    data = golden("simple.txt") * 50
+    comp = O.deflate(data, level=6, format="gzip", file_name=name, mtime=0)
+    inf = sdz.Inflater()
+    out = b"".join(inf.append(comp))
+    res = inf.finish()
+    assert out == data and res["success"] and res["fileName"] == name

@@ -222,3 +222,27 @@ def test_deflater_per_call_outputs(paradise):
             if fmt == "gzip":
                 assert outs[0][:2] == b"\x1f\x8b"
             assert zlib.decompress(b"".join(outs), {"deflate": 15, "gzip": 31, "raw": -15}[fmt]) == paradise
+
+
+def test_inflater_arrays_are_16k_passes():
+    """sd-inflate.ts:101-150 pushes one array per ZStream pass: every array but the last of an
+    append() is a full 16 KiB OUTPUT_BUFSIZE (zstream.ts:11) -- checked on the restatement
+    over random corpora (stored blocks included), levels, containers and split points.  The
+    facades return append()'s bytes in 16 KiB arrays on the strength of this."""
+    text = golden("paradiselost.txt")
+    rng = random.Random(12)
+    for trial in range(60):
+        n = rng.randint(1, 200000)
+        data = text[rng.randrange(len(text) - n):][:n]
+        if trial % 3 == 0:
+            data = bytes(rng.getrandbits(8) for _ in range(min(n, 30000))) + data[:20000]
+        fmt = ("raw", "deflate", "gzip")[trial % 3]
+        comp = O.deflate(data, level=rng.randint(1, 9), format=fmt)
+        cuts = sorted(rng.randrange(len(comp) + 1) for _ in range(rng.randint(0, 5)))
+        parts = [comp[a:b] for a, b in zip([0] + cuts, cuts + [len(comp)])]
+        per, r = O.inflater_chunks(parts, raw=fmt == "raw")
+        # (a split dynamic header or stored block can fail in the reference itself: A9 / A10)
+        assert r["data"] == data or not r["success"]
+        for p, arrays in zip(parts, per):
+            assert all(c == 16384 for c in arrays[:-1]), arrays
+            assert sum(arrays) <= len(data)

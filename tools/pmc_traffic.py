@@ -5,13 +5,17 @@ One launch of sdz_inflate_batch_device = k_inflate_decode + k_inflate_resolve
 (per round) + k_inflate_finalize.  Per MI355X_MICROARCH.md (HBM/rocprofv3):
 FETCH_SIZE and WRITE_SIZE come from separate passes, are in KiB, and on gfx950
 FETCH_SIZE reports half of the bytes of wide reads -- doubled here.
-Usage: pmc_traffic.py <prof dir> <steps> <out.json>
+Usage: pmc_traffic.py <prof dir> <steps> <out.json> [kernel prefixes, comma-separated]
+(default sdz::k_inflate; the deflate leg: sdz::k_dfl,sdz::k_deflate,sdz::k_checksum)
 """
 import collections
 import csv
 import json
 import os
 import sys
+
+
+PREFIXES = ("sdz::k_inflate",)
 
 
 def per_kernel(path, counter):
@@ -21,7 +25,7 @@ def per_kernel(path, counter):
         if r["Counter_Name"] != counter:
             continue
         k = r["Kernel_Name"].split("(")[0]
-        if not k.startswith("sdz::k_inflate"):
+        if not k.startswith(PREFIXES):
             continue
         tot[k] += float(r["Counter_Value"])
         n[k] += 1
@@ -29,7 +33,10 @@ def per_kernel(path, counter):
 
 
 def main():
+    global PREFIXES
     root, steps, out = sys.argv[1], int(sys.argv[2]), sys.argv[3]
+    if len(sys.argv) > 4:
+        PREFIXES = tuple(sys.argv[4].split(","))
     f, nf = per_kernel(os.path.join(root, "pmc_fetch", "run_counter_collection.csv"), "FETCH_SIZE")
     w, nw = per_kernel(os.path.join(root, "pmc_write", "run_counter_collection.csv"), "WRITE_SIZE")
     kernels = sorted(set(f) | set(w))

@@ -82,10 +82,14 @@ class Slots:
             self.in_len.append(len(pool[j]))
             o += up(len(pool[j]))
         self.d_in = sdz.DeviceBuffer(o + 128)
-        for i, j in enumerate(pick):
-            rc = L.sdz_copy_device_to_device(self.d_in.ptr + self.in_off[i], self.d_pool.ptr + self.pool_off[j],
-                                             len(pool[j]))
-            assert rc == 0, L.sdz_last_error()
+        # every stream's copy of its pool payload in one k_gather launch (sdz_gather_device)
+        gm = self.in_off + [self.pool_off[j] for j in pick] + self.in_len
+        d_gm = sdz.DeviceBuffer(8 * max(1, len(gm)))
+        d_gm.upload(bytes((ctypes.c_uint64 * len(gm))(*gm)))
+        k = self.n
+        rc = L.sdz_gather_device(self.d_in.ptr, d_gm.ptr, self.d_pool.ptr, d_gm.ptr + 8 * k, d_gm.ptr + 16 * k, k, None)
+        assert rc == 0 and L.sdz_sync(None) == 0, L.sdz_last_error()
+        d_gm.free()
         self.out_off, self.out_cap, o = [], [], 0
         for c in out_caps:
             self.out_off.append(o)
