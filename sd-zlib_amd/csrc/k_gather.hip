@@ -27,6 +27,17 @@ __global__ __launch_bounds__(GA_THREADS) void k_gather(uint8_t* dst, const uint6
     if (L == 0) return;
     uint8_t* d = dst + dst_off[sid];
     const uint8_t* s = src + src_off[sid];
+    if ((((uintptr_t)d | (uintptr_t)s) & 15) == 0) {     // both 16-aligned: 16-byte vectors
+        const uint64_t nv = L >> 4;
+        const uint64_t vpp = GA_PIECE / 16;
+        for (uint64_t p0 = (uint64_t)blockIdx.y * vpp; p0 < nv; p0 += (uint64_t)GA_SLICES * vpp) {
+            const uint64_t pe = p0 + vpp < nv ? p0 + vpp : nv;
+            for (uint64_t q = p0 + threadIdx.x; q < pe; q += GA_THREADS) ((uint4*)d)[q] = ((const uint4*)s)[q];
+        }
+        const uint64_t t0 = nv << 4;
+        if (blockIdx.y == GA_SLICES - 1 && threadIdx.x < L - t0) d[t0 + threadIdx.x] = s[t0 + threadIdx.x];
+        return;
+    }
     // head: bytes until d is 4-aligned (block y = 0 only)
     const uint32_t h0 = (uint32_t)((4u - ((uintptr_t)d & 3u)) & 3u);
     const uint64_t h = L < h0 ? L : h0;

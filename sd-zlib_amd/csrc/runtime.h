@@ -67,6 +67,9 @@ struct PoolUse {
     ~PoolUse() { if (slot) Pool::done(slot, s); }
 };
 extern Pool g_host;                   // host-buffer batches: staged inputs, outputs, records
+// kernel timing (sdz_set_timing): HIP events on the launch stream around a call's kernels
+void timing_begin(hipStream_t s);
+void timing_end(hipStream_t s);
 
 // pinned host staging, grow-only, one per device (used under the device's lock).  A user that
 // leaves copies from it in flight calls done(stream); the next get() waits for them.

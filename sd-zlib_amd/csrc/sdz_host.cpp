@@ -363,7 +363,9 @@ int sdz_gather_device(uint8_t* dst, const uint64_t* dst_off, const uint8_t* src,
     if (int rc = ensure_device()) return rc;
     if (n == 0) return SDZ_API_OK;
     if (!dst || !dst_off || !src || !src_off || !len) return fail(SDZ_API_BAD_ARG, "sdz_gather_device: null pointer");
+    timing_begin((hipStream_t)stream);
     launch_gather(dst, dst_off, src, src_off, len, n, (hipStream_t)stream);
+    timing_end((hipStream_t)stream);
     HIPCHK(hipGetLastError());
     return SDZ_API_OK;
 }

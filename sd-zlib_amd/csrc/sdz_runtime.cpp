@@ -99,6 +99,23 @@ int Pinned::get(size_t bytes, void** out) {
     return SDZ_API_OK;
 }
 
+thread_local hipEvent_t g_ev0 = nullptr, g_ev1 = nullptr;
+thread_local bool g_ev_pending = false;
+thread_local float g_extra_ms = 0.f;    // GPU time of the last call outside g_ev0..g_ev1 (split pre-pass)
+int g_timing = 0;
+
+void timing_begin(hipStream_t s) {
+    if (!g_timing) return;
+    g_extra_ms = 0.f;
+    if (!g_ev0) { hipEventCreate(&g_ev0); hipEventCreate(&g_ev1); }
+    hipEventRecord(g_ev0, s);
+}
+void timing_end(hipStream_t s) {
+    if (!g_timing) return;
+    hipEventRecord(g_ev1, s);
+    g_ev_pending = true;
+}
+
 int Pinned::done(hipStream_t s) {
     int d = 0;
     if (int rc = cur_device(&d)) return rc;
@@ -116,10 +133,6 @@ using namespace sdz::rt;
 namespace {
 
 thread_local float g_last_ms = 0.f;
-thread_local hipEvent_t g_ev0 = nullptr, g_ev1 = nullptr;
-thread_local bool g_ev_pending = false;
-thread_local float g_extra_ms = 0.f;    // GPU time of the last call outside g_ev0..g_ev1 (split pre-pass)
-int g_timing = 0;
 thread_local float g_breakdown[3] = { 0.f, 0.f, 0.f };   // decode / resolve / finalize of the last inflate
 
 Pool g_inflate_scratch, g_deflate_state, g_tmp, g_stage, g_split, g_find;
@@ -127,18 +140,6 @@ Pool g_inflate_scratch, g_deflate_state, g_tmp, g_stage, g_split, g_find;
 // [128, 256) small results, then the file name
 constexpr size_t kTmpMax = 0, kTmpDictId = 64, kTmpFname = 256;
 constexpr uint64_t kInflaterOutCap = 4ull << 20;   // sdz_inflater: output slot per device call
-
-void timing_begin(hipStream_t s) {
-    if (!g_timing) return;
-    g_extra_ms = 0.f;
-    if (!g_ev0) { hipEventCreate(&g_ev0); hipEventCreate(&g_ev1); }
-    hipEventRecord(g_ev0, s);
-}
-void timing_end(hipStream_t s) {
-    if (!g_timing) return;
-    hipEventRecord(g_ev1, s);
-    g_ev_pending = true;
-}
 
 const char* const kZmsg[ZM_COUNT] = {
     "",
