@@ -1660,6 +1660,329 @@ __global__ __launch_bounds__(PW_THREADS) void k_dfl_parse_wide(DeflateArgs A) {
     }
 }
 
+// ------------------------------------------------------------------ segment-parallel lazy parse
+// deflate_slow's parse (deflate.ts:1054-1182) is a walk over step positions whose state between
+// steps is (prev_length, prev_match, match_available) and whose step reads one record.  Block
+// flushes do not feed back into it (they only cut the symbol sequence: _tr_tally's verdict,
+// deflate.ts:488-524), so the symbols are found first and cut into blocks afterwards:
+//   k_lz_spec    one lane per segment (2^lz_shift positions) parses it from a fresh state
+//                (prev_length 2, nothing pending) -- a guess -- and records, by position, the
+//                state before each step and the symbol the step emits;
+//   k_lz_join    one lane per segment boundary carries the previous segment's parse on into
+//                the segment until it stands on a position the segment's own parse visited in
+//                the same state: both are one parse from there (lazy parses fall back into step
+//                within a few symbols, so that is a handful of steps);
+//   k_lz_fix     one lane per stream takes the boundaries in order: where a join crossed a
+//                whole segment without meeting its parse (long matches out of phase: runs),
+//                the true parse entering the next segment is that join's carry, and the next
+//                join is redone from it;
+//   k_lz_count / k_lz_scan / k_lz_emit   the symbols in order into the stream's symbol buffer;
+//   k_lz_blocks  one workgroup per stream cuts them into blocks where _tr_tally would flush
+//                (TRUNCATE_BLOCK at 8192 symbols, LIT_BUFSIZE - 1), the sums it tests reduced
+//                over the block's symbols.
+// The result is the serial parse's (k_dfl_parse) symbol for symbol, block for block.
+struct LzSt {
+    int s, ml, ms, avail;           // step position; prev_length, prev_match, match_available
+};
+#define LZ_SYM 0x80000000u          // a step's symbol word: emitted flag | lc | dist << 8
+#define LZ_THREADS 64
+// the state as compared between parses: prev_match only matters with prev_length >= MIN_MATCH
+__device__ __forceinline__ uint32_t lz_pack(const LzSt& t) {
+    return t.ml >= MIN_MATCH ? (uint32_t)t.ml | ((uint32_t)(t.s - t.ms) << 9) | ((uint32_t)t.avail << 25)
+                             : (uint32_t)(MIN_MATCH - 1) | ((uint32_t)t.avail << 25);
+}
+__device__ __forceinline__ uint64_t lz_save(const LzSt& t) { return (uint64_t)(uint32_t)t.s | ((uint64_t)lz_pack(t) << 32); }
+__device__ __forceinline__ LzSt lz_load(uint64_t v) {
+    const uint32_t p = (uint32_t)(v >> 32);
+    LzSt t;
+    t.s = (int)(uint32_t)v;
+    t.ml = (int)(p & 511u);
+    t.ms = t.s - (int)((p >> 9) & 0xffffu);
+    t.avail = (int)((p >> 25) & 1u);
+    return t;
+}
+// one step of deflate_slow at t.s with the record r there (as ps_step); returns the symbol
+// it emits (LZ_SYM set) or 0
+__device__ __forceinline__ uint32_t lz_step(LzSt& t, uint64_t r, int n, int good, int max_lazy) {
+    const int lookahead = n - t.s;
+    const int prev_length = t.ml, prev_match = t.ms;
+    int ml = MIN_MATCH - 1, ms = t.ms;
+    if (lookahead >= MIN_MATCH && prev_length < max_lazy) {
+        const uint32_t e = prev_length >= good ? (uint32_t)(r >> 32) : (uint32_t)r;
+        const int len = (int)((e >> 16) & 511u);
+        ml = prev_length;
+        if (len > prev_length) { ml = len; ms = t.s - (int)(e & 0xffffu); }
+        ml = ml < lookahead ? ml : lookahead;
+        if (ml == MIN_MATCH && t.s - ms > 4096) ml = MIN_MATCH - 1;           // TOO_FAR
+    }
+    if (prev_length >= MIN_MATCH && ml <= prev_length) {
+        const uint32_t sym = (uint32_t)(prev_length - MIN_MATCH) | ((uint32_t)(t.s - 1 - prev_match) << 8) | LZ_SYM;
+        t.s += prev_length - 1;
+        t.avail = 0; t.ml = MIN_MATCH - 1; t.ms = 0;
+        return sym;
+    }
+    const uint32_t lb = ((uint32_t)r >> 25) | (((uint32_t)(r >> 32) >> 18) & 128u);
+    const uint32_t sym = t.avail ? (lb | LZ_SYM) : 0u;
+    t.avail = 1; t.ml = ml; t.ms = ms;
+    t.s += 1;
+    return sym;
+}
+struct LzSeg {
+    uint32_t k, j;                  // stream, segment within it
+    uint64_t rp;
+    int n, g, h;                    // stream length; the segment's positions [g, h)
+};
+__device__ __forceinline__ LzSeg lz_seg(const DeflateArgs& A, uint32_t seg) {
+    LzSeg q;
+    q.k = A.lz_seg[seg];
+    q.j = seg - A.lz_sg0[q.k];
+    q.rp = A.rp0[q.k];
+    q.n = (int)A.in_len[q.k];
+    q.g = (int)(q.j << A.lz_shift);
+    q.h = q.g + (1 << A.lz_shift) < q.n ? q.g + (1 << A.lz_shift) : q.n;
+    return q;
+}
+__global__ __launch_bounds__(LZ_THREADS) void k_lz_spec(DeflateArgs A) {
+    const uint32_t seg = blockIdx.x * LZ_THREADS + threadIdx.x;
+    if (seg >= A.nlseg) return;
+    const LzSeg q = lz_seg(A, seg);
+    const int good = c_config[A.level][0], max_lazy = c_config[A.level][1];
+    const GLB uint64_t* rec = (const GLB uint64_t*)A.rec_buf + q.rp;
+    GLB uint64_t* w = (GLB uint64_t*)A.lz_w + q.rp;
+    GLB uint64_t* v1 = (GLB uint64_t*)A.lz_v1 + (q.rp >> 6);
+    GLB uint64_t* e1 = (GLB uint64_t*)A.lz_e1 + (q.rp >> 6);
+    LzSt t{q.g, MIN_MATCH - 1, 0, 0};
+    uint64_t va = 0, ea = 0;
+    int wc = q.g >> 6;
+    auto one = [&](int s, uint64_t r) {
+        for (; (s >> 6) != wc; ++wc) { v1[wc] = va; e1[wc] = ea; va = 0; ea = 0; }
+        const uint32_t st = lz_pack(t);
+        const uint32_t sym = lz_step(t, r, q.n, good, max_lazy);
+        va |= 1ull << (s & 63);
+        if (sym) ea |= 1ull << (s & 63);
+        w[s] = (uint64_t)st | ((uint64_t)sym << 32);
+    };
+    while (t.s < q.h) {
+        // two records per round trip: a step moves on by one position except after a match
+        const int s = t.s;
+        const uint64_t r0 = rec[s], r1 = rec[s + 1 < q.n ? s + 1 : s];
+        one(s, r0);
+        if (t.s == s + 1 && t.s < q.h) one(s + 1, r1);
+    }
+    for (; wc <= ((q.h - 1) >> 6); ++wc) { v1[wc] = va; e1[wc] = ea; va = 0; ea = 0; }
+    A.lz_end[seg] = lz_save(t);
+    if (q.j == 0) A.lz_c[seg] = 0;                            // the first segment's parse is the true one
+}
+// carry the parse t on through segment q until it meets the segment's phase-1 parse (same
+// position, same state); returns that position, or q.h (t then is the state leaving the
+// segment).  Writes the symbols of its steps (lz_s2, lz_e2 words [g, returned position)).
+__device__ int lz_join_run(const DeflateArgs& A, const LzSeg& q, LzSt& t, int good, int max_lazy) {
+    const GLB uint64_t* rec = (const GLB uint64_t*)A.rec_buf + q.rp;
+    const GLB uint64_t* w = (const GLB uint64_t*)A.lz_w + q.rp;
+    const GLB uint64_t* v1 = (const GLB uint64_t*)A.lz_v1 + (q.rp >> 6);
+    GLB uint32_t* s2 = (GLB uint32_t*)A.lz_s2 + q.rp;
+    GLB uint64_t* e2 = (GLB uint64_t*)A.lz_e2 + (q.rp >> 6);
+    uint64_t ea = 0;
+    int wc = q.g >> 6;
+    uint64_t vw = t.s < q.h ? v1[t.s >> 6] : 0ull;
+    int c = q.h;
+    while (t.s < q.h) {
+        const int s = t.s;
+        if ((s >> 6) != wc) {
+            for (; (s >> 6) != wc; ++wc) { e2[wc] = ea; ea = 0; }
+            vw = v1[wc];
+        }
+        const uint64_t r = rec[s];
+        if (((vw >> (s & 63)) & 1ull) && (uint32_t)w[s] == lz_pack(t)) { c = s; break; }
+        const uint32_t sym = lz_step(t, r, q.n, good, max_lazy);
+        if (sym) { ea |= 1ull << (s & 63); s2[s] = sym; }
+    }
+    if (c > q.g)
+        for (; wc <= ((c - 1) >> 6); ++wc) { e2[wc] = ea; ea = 0; }
+    return c;
+}
+__global__ __launch_bounds__(LZ_THREADS) void k_lz_join(DeflateArgs A) {
+    const uint32_t seg = blockIdx.x * LZ_THREADS + threadIdx.x;
+    if (seg >= A.nlseg) return;
+    const LzSeg q = lz_seg(A, seg);
+    if (q.j == 0) return;
+    LzSt t = lz_load(A.lz_end[seg - 1]);
+    A.lz_c[seg] = (uint32_t)lz_join_run(A, q, t, c_config[A.level][0], c_config[A.level][1]);
+    A.lz_carry[seg] = lz_save(t);
+}
+__global__ __launch_bounds__(LZ_THREADS) void k_lz_fix(DeflateArgs A) {
+    const uint32_t k = blockIdx.x * LZ_THREADS + threadIdx.x;
+    if (k >= A.n || A.rp0[k] == ~0ull) return;
+    const uint32_t base = A.lz_sg0[k], K = A.lz_sg0[k + 1] - base;
+    if (K == 0) return;
+    const int good = c_config[A.level][0], max_lazy = c_config[A.level][1];
+    bool ok = true;                                            // segment j - 1's parse is true at its end
+    LzSt t{0, 0, 0, 0};
+    for (uint32_t j = 1; j < K; ++j) {
+        const LzSeg q = lz_seg(A, base + j);
+        if (ok) {
+            if ((int)A.lz_c[base + j] < q.h) continue;         // met: true from there
+            t = lz_load(A.lz_carry[base + j]);                 // crossed the segment: its carry is true
+            ok = false;
+            continue;
+        }
+        const int c = lz_join_run(A, q, t, good, max_lazy);
+        A.lz_c[base + j] = (uint32_t)c;
+        if (c < q.h) ok = true;
+    }
+    const LzSt f = ok ? lz_load(A.lz_end[base + K - 1]) : t;
+    A.lz_fin[k] = (uint32_t)f.avail;                            // deflate_slow's last literal (deflate.ts:1172)
+}
+// bits of word wi that belong to positions [a, b)
+__device__ __forceinline__ uint64_t lz_range(int wi, int a, int b) {
+    const int lo = wi << 6;
+    const uint64_t ma = a <= lo ? ~0ull : a >= lo + 64 ? 0ull : ~0ull << (a - lo);
+    const uint64_t mb = b >= lo + 64 ? ~0ull : b <= lo ? 0ull : ~(~0ull << (b - lo));
+    return ma & mb;
+}
+__global__ __launch_bounds__(LZ_THREADS) void k_lz_count(DeflateArgs A) {
+    const uint32_t seg = blockIdx.x * LZ_THREADS + threadIdx.x;
+    if (seg >= A.nlseg) return;
+    const LzSeg q = lz_seg(A, seg);
+    const int c = (int)A.lz_c[seg];
+    const GLB uint64_t* e1 = (const GLB uint64_t*)A.lz_e1 + (q.rp >> 6);
+    const GLB uint64_t* e2 = (const GLB uint64_t*)A.lz_e2 + (q.rp >> 6);
+    uint32_t cnt = 0;
+    for (int wi = q.g >> 6; wi <= ((q.h - 1) >> 6); ++wi) {
+        const uint64_t m2 = lz_range(wi, q.g, c), m1 = lz_range(wi, c, q.h);
+        cnt += (uint32_t)__popcll((m2 ? e2[wi] : 0ull) & m2) + (uint32_t)__popcll(e1[wi] & m1);
+    }
+    if (seg + 1 == A.lz_sg0[q.k + 1]) cnt += A.lz_fin[q.k] & 1u;
+    A.lz_cnt[seg] = cnt;
+}
+__global__ __launch_bounds__(LZ_THREADS) void k_lz_scan(DeflateArgs A) {
+    const uint32_t k = blockIdx.x * LZ_THREADS + threadIdx.x;
+    if (k >= A.n || A.rp0[k] == ~0ull) return;
+    uint32_t o = 0;
+    for (uint32_t s = A.lz_sg0[k]; s < A.lz_sg0[k + 1]; ++s) {
+        const uint32_t c = A.lz_cnt[s];
+        A.lz_cnt[s] = o;
+        o += c;
+    }
+    A.lz_fin[k] |= o << 1;
+}
+// symbols to the front of the stream's record buffer (no record is read any more)
+__global__ __launch_bounds__(LZ_THREADS) void k_lz_emit(DeflateArgs A) {
+    const uint32_t seg = blockIdx.x * LZ_THREADS + threadIdx.x;
+    if (seg >= A.nlseg) return;
+    const LzSeg q = lz_seg(A, seg);
+    const int c = (int)A.lz_c[seg];
+    const GLB uint64_t* w = (const GLB uint64_t*)A.lz_w + q.rp;
+    const GLB uint32_t* s2 = (const GLB uint32_t*)A.lz_s2 + q.rp;
+    const GLB uint64_t* e1 = (const GLB uint64_t*)A.lz_e1 + (q.rp >> 6);
+    const GLB uint64_t* e2 = (const GLB uint64_t*)A.lz_e2 + (q.rp >> 6);
+    GLB uint32_t* sym = (GLB uint32_t*)A.rec_buf + 2 * q.rp;
+    uint32_t o = A.lz_cnt[seg];
+    for (int wi = q.g >> 6; wi <= ((q.h - 1) >> 6); ++wi) {
+        const uint64_t m2 = lz_range(wi, q.g, c), m1 = lz_range(wi, c, q.h);
+        uint64_t b2 = (m2 ? e2[wi] : 0ull) & m2, b1 = e1[wi] & m1;
+        for (uint64_t b = b1 | b2; b; b &= b - 1) {
+            const int p = (wi << 6) + __builtin_ctzll(b);
+            const uint32_t v = p < c ? s2[p] : (uint32_t)(w[p] >> 32);
+            sym[o++] = v & ~LZ_SYM;
+        }
+    }
+    if (seg + 1 == A.lz_sg0[q.k + 1] && (A.lz_fin[q.k] & 1u))
+        sym[o] = ((const GLB uint8_t*)A.in)[A.in_off[q.k] + (uint64_t)q.n - 1];
+}
+// block cuts: _tr_tally returns true at last_lit == 8192 when TRUNCATE_BLOCK's estimate says
+// so (level > 2), and at last_lit == LIT_BUFSIZE - 1; the final literal's verdict is ignored
+// (deflate.ts:1172-1176).  At a cut, strstart - block_start is the block's bytes, less the
+// cutting match's length - 1 (its tally precedes strstart += prev_length - 1).
+#define LB_THREADS 256
+struct LzSums { uint32_t mat, dxb, cov, last; };
+__device__ __forceinline__ uint32_t lb_sum(uint32_t v, uint32_t* red) {
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    const uint32_t wv = threadIdx.x >> 6;
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) red[wv] = v;
+    __syncthreads();
+    uint32_t t = 0;
+    for (uint32_t i = 0; i < LB_THREADS / 64; ++i) t += red[i];
+    return t;
+}
+// sums over symbols [a, b): matches, extra-bit estimate, bytes covered by [a, b - 1), and by b - 1
+__device__ LzSums lb_sums(const GLB uint32_t* sym, uint32_t a, uint32_t b, uint32_t* red) {
+    uint32_t mat = 0, dxb = 0, cov = 0, last = 0;
+    for (uint32_t i = a + threadIdx.x; i < b; i += LB_THREADS) {
+        const uint32_t v = sym[i], dist = v >> 8;
+        const uint32_t len = dist ? (v & 255u) + MIN_MATCH : 1u;
+        if (dist) {
+            const uint32_t d = dist - 1;
+            mat += 1;
+            dxb += 5u + (d < 4u ? 0u : 30u - (uint32_t)__builtin_clz(d));
+        }
+        if (i + 1 < b) cov += len;
+        else last = len;
+    }
+    LzSums r;
+    r.mat = lb_sum(mat, red);
+    r.dxb = lb_sum(dxb, red);
+    r.cov = lb_sum(cov, red);
+    r.last = lb_sum(last, red);
+    return r;
+}
+__global__ __launch_bounds__(LB_THREADS) void k_lz_blocks(DeflateArgs A) {
+    __shared__ uint32_t red[LB_THREADS / 64];
+    const uint32_t sid = blockIdx.x;
+    if (sid >= A.n) return;
+    GLB DSlab* S = (GLB DSlab*)(A.state + (uint64_t)sid * SLAB_BYTES);
+    GLB FStream* F = (GLB FStream*)S->window;
+    const uint64_t in_len = A.in_len[sid];
+    if (in_len == 0 || A.rp0[sid] == ~0ull) {
+        if (threadIdx.x == 0) { F->nblk = 0; F->flag = 1; }
+        return;
+    }
+    const int64_t n = (int64_t)in_len;
+    const uint32_t fin = A.lz_fin[sid], nsym = fin >> 1, nchk = nsym - (fin & 1u);
+    const GLB uint32_t* sym = (const GLB uint32_t*)A.rec_buf + 2 * A.rp0[sid];
+    GLB uint8_t* slots = (GLB uint8_t*)(A.blk + (uint64_t)A.tb0[sid] * FB_SLOT);
+    const uint32_t nbcap = A.tb0[sid + 1] - A.tb0[sid];
+    uint32_t nb = 0, b0 = 0;
+    int64_t block_start = 0;
+    for (;;) {
+        uint32_t cnt = 0, eof = 0;
+        int64_t step = n, strstart = n;                        // the cutting step's position; strstart after it
+        if (b0 + 8192 <= nchk) {
+            const LzSums a = lb_sums(sym, b0, b0 + 8192, red);
+            const int64_t in_length = a.cov + 1;
+            const uint32_t out_length = (8192u * 8u + a.dxb) >> 3;
+            if (a.mat < 4096 && (int64_t)out_length < in_length / 2) {
+                cnt = 8192;
+                step = block_start + in_length;
+                strstart = block_start + a.cov + a.last;
+            } else if (b0 + LIT_BUFSIZE - 1 <= nchk) {
+                const LzSums b = lb_sums(sym, b0 + 8192, b0 + LIT_BUFSIZE - 1, red);
+                cnt = LIT_BUFSIZE - 1;
+                const int64_t before = (int64_t)a.cov + a.last + b.cov;   // symbols [b0, b0 + 16382)
+                step = block_start + before + 1;
+                strstart = block_start + before + b.last;
+            }
+        }
+        if (cnt == 0) { cnt = nsym - b0; eof = 1; }
+        if (threadIdx.x == 0 && nb < nbcap) {
+            const int64_t off = slide_off(n, step);
+            GLB FBlock* B = (GLB FBlock*)(slots + (uint64_t)nb * FB_SLOT);
+            B->sym0 = b0; B->nsym = cnt;
+            B->block_start = (int32_t)(block_start - off); B->strstart = (int32_t)(strstart - off);
+            B->off = off; B->eof = eof;
+        }
+        nb++;
+        b0 += cnt;
+        block_start = strstart;
+        if (eof) break;
+    }
+    if (threadIdx.x == 0) {
+        F->nblk = nb;
+        F->flag = nb > nbcap ? 1u : 0u;
+    }
+}
+
 // tree context of the record path: LDS arrays, header bits into LDS words
 struct LTreeCtx {
     uint16_t *heap, *depth, *bl_count, *next_code, *bltree;
@@ -2035,7 +2358,16 @@ void launch_deflate(const DeflateArgs& a, hipStream_t st, hipStream_t side, hipE
             launch_checksum(a.in, a.in_off, a.in_len, nullptr, a.cks, a.n, ck_kind, side);
             (void)hipEventRecord(ev, side);
         }
-        if (a.wide) hipLaunchKernelGGL(k_dfl_parse_wide, dim3(a.n), dim3(PW_THREADS), 0, st, a);
+        if (a.lz_shift && a.nlseg) {
+            const dim3 gseg((a.nlseg + LZ_THREADS - 1) / LZ_THREADS), gstr((a.n + LZ_THREADS - 1) / LZ_THREADS);
+            hipLaunchKernelGGL(k_lz_spec, gseg, dim3(LZ_THREADS), 0, st, a);
+            hipLaunchKernelGGL(k_lz_join, gseg, dim3(LZ_THREADS), 0, st, a);
+            hipLaunchKernelGGL(k_lz_fix, gstr, dim3(LZ_THREADS), 0, st, a);
+            hipLaunchKernelGGL(k_lz_count, gseg, dim3(LZ_THREADS), 0, st, a);
+            hipLaunchKernelGGL(k_lz_scan, gstr, dim3(LZ_THREADS), 0, st, a);
+            hipLaunchKernelGGL(k_lz_emit, gseg, dim3(LZ_THREADS), 0, st, a);
+            hipLaunchKernelGGL(k_lz_blocks, dim3(a.n), dim3(LB_THREADS), 0, st, a);
+        } else if (a.wide) hipLaunchKernelGGL(k_dfl_parse_wide, dim3(a.n), dim3(PW_THREADS), 0, st, a);
         else hipLaunchKernelGGL(k_dfl_parse, grid, dim3(64), 0, st, a);
         hipLaunchKernelGGL(k_dfl_trees, dim3(a.n, a.nbmax < 32 ? (a.nbmax ? a.nbmax : 1) : 32), dim3(64), 0, st, a);
         if (fork) (void)hipStreamWaitEvent(st, ev, 0);

@@ -111,6 +111,22 @@ struct DeflateArgs {
     uint32_t ncunit;
     uint32_t nbmax;              // most block slots of one stream (k_dfl_trees grid)
     uint32_t wide;               // k_dfl_parse: one workgroup per stream (few, long streams)
+    // segment-parallel lazy parse (k_lz_*, k_deflate.hip): stream k's positions cut into
+    // segments of 1 << lz_shift, global segment ids [lz_sg0[k], lz_sg0[k + 1])
+    uint32_t lz_shift;           // 0: the serial parse kernels instead
+    uint32_t nlseg;
+    const uint32_t* lz_sg0;      // n + 1 entries
+    const uint32_t* lz_seg;      // nlseg entries: the stream of each segment
+    uint64_t* lz_w;              // per position (rp0 + p): phase-1 state before the step | symbol << 32
+    uint32_t* lz_s2;             // per position: the join / fix symbols
+    uint64_t* lz_v1;             // bitmaps, word (rp0 + p) >> 6: phase-1 step positions,
+    uint64_t* lz_e1;             //   phase-1 symbols,
+    uint64_t* lz_e2;             //   join / fix symbols
+    uint64_t* lz_end;            // per segment: the phase-1 parse's state where it left the segment
+    uint64_t* lz_carry;          // per segment: the join's state where it left the segment
+    uint32_t* lz_c;              // per segment: first position whose phase-1 parse is the true one
+    uint32_t* lz_cnt;            // per segment: symbols, then their exclusive prefix in the stream
+    uint32_t* lz_fin;            // per stream: bit 0 the final literal, bits 1.. the symbol count
     int32_t* cks;                // n input checksums (record path)
     uint32_t fast;               // set by launch_deflate: k_deflate redoes flagged streams only
     const uint8_t* dict;         // preset dictionary (deflateSetDictionary), may be null

@@ -786,10 +786,25 @@ int sdz_deflate_batch_device(const uint8_t* in, const uint64_t* in_off, const ui
         HIPCHK(hipStreamSynchronize(s));
     }
     auto on_path = [&](uint32_t i) { return recpath && len[i] > 0 && len[i] <= kDeflateRecMax; };
+    // segment-parallel parse (k_lz_*): segments of 2^lz_shift positions, shorter ones when the
+    // batch is small so a single long stream still spreads over many lanes
+    uint32_t lz_shift = 0;
+    if (recpath && !getenv("SDZ_SERIAL_PARSE")) {
+        uint64_t tot = 0;
+        for (uint32_t i = 0; i < n; ++i)
+            if (on_path(i)) tot += len[i];
+        lz_shift = 9;
+        while (lz_shift < 12 && (tot >> (lz_shift + 1)) >= 65536) ++lz_shift;
+        if (const char* e = getenv("SDZ_LZ_SHIFT"))            // tests: segment size 2^6 .. 2^16
+            lz_shift = (uint32_t)std::min(16, std::max(6, atoi(e)));
+    }
+    auto lz_segs = [&](uint64_t l) -> uint64_t { return lz_shift ? (l + (1ull << lz_shift) - 1) >> lz_shift : 0; };
+    // per position: record 8, link 2, parse words 8 + 4 + 3 bitmaps; per segment 28
+    const uint64_t kPosBytes = lz_shift ? 8 + 2 + 8 + 4 + 1 : 8 + 2;
     auto rec_cost = [&](uint32_t i) -> uint64_t {
         if (!on_path(i)) return 0;
         const uint64_t p = (len[i] + 63) & ~63ull;
-        return p * (sizeof(uint64_t) + sizeof(uint16_t)) + deflate_rec_blocks(len[i]) * FB_SLOT_BYTES + 64;
+        return p * kPosBytes + lz_segs(len[i]) * 32 + deflate_rec_blocks(len[i]) * FB_SLOT_BYTES + 64;
     };
     const uint64_t budget = std::max<uint64_t>(1ull << 30, mem_free / 2);
     // sub-batches [cb[j], cb[j + 1])
@@ -808,17 +823,19 @@ int sdz_deflate_batch_device(const uint8_t* in, const uint64_t* in_off, const ui
     // pool: the largest sub-batch's slabs, record buffers, block slots and plan arrays
     uint64_t pool_bytes = 0;
     for (size_t j = 0; j + 1 < cb.size(); ++j) {
-        uint64_t sb = 0, pos = 0, blk = 0, units = 0;
+        uint64_t sb = 0, pos = 0, blk = 0, units = 0, segs = 0;
         for (uint32_t i = cb[j]; i < cb[j + 1]; ++i) {
             sb += slab;
             if (on_path(i)) {
                 pos += (len[i] + 63) & ~63ull;
                 blk += deflate_rec_blocks(len[i]);
                 units += deflate_chain_units(len[i]) + deflate_match_segs(len[i]);
+                segs += lz_segs(len[i]);
             }
         }
         const uint64_t m = cb[j + 1] - cb[j];
-        const uint64_t b = sb + pos * 10 + blk * FB_SLOT_BYTES + m * 16 + 8 * (m + 1) + 4 * (m + 1) + 4 * units + 4096;
+        const uint64_t b = sb + pos * kPosBytes + blk * FB_SLOT_BYTES + m * 16 + 8 * (m + 1) + 4 * (m + 1) + 4 * units +
+                           (lz_shift ? 4 * (m + 1) + 4 * m + 32 * segs + 16 * 256 : 0) + 4096;
         pool_bytes = std::max(pool_bytes, b);
     }
     void* state = nullptr;
@@ -876,28 +893,62 @@ int sdz_deflate_batch_device(const uint8_t* in, const uint64_t* in_off, const ui
                 const uint32_t cu = deflate_chain_units(len[b + k]);
                 for (uint32_t u = 0; u < cu; ++u) units.push_back(k << kRecUnitShift | u);
             }
+            // parse segments: sg0 (m + 1), then the stream of each segment
+            std::vector<uint32_t> lzs;
+            if (lz_shift) {
+                lzs.resize(m + 1);
+                for (uint32_t k = 0; k < m; ++k) {
+                    lzs[k] = (uint32_t)(lzs.size() - (m + 1));
+                    if (rp0[k] == ~0ull) continue;
+                    const uint64_t K = lz_segs(len[b + k]);
+                    for (uint64_t q = 0; q < K; ++q) lzs.push_back(k);
+                }
+                lzs[m] = (uint32_t)(lzs.size() - (m + 1));
+            }
+            const uint32_t nlseg = lz_shift ? lzs[m] : 0;
             uint8_t* B = (uint8_t*)state;
             size_t o = (size_t)m * slab;
-            a.rec_buf = (uint64_t*)(B + o); o += (size_t)pos * 8;
-            a.pv_buf = (uint16_t*)(B + o); o += ((size_t)pos * 2 + 255) & ~(size_t)255;
-            a.blk = B + o; o += (size_t)blk * FB_SLOT_BYTES;
-            a.cks = (int32_t*)(B + o); o += ((size_t)m * 4 + 255) & ~(size_t)255;
-            uint64_t* d_rp0 = (uint64_t*)(B + o); o += (((size_t)m + 1) * 8 + 255) & ~(size_t)255;
-            uint32_t* d_tb0 = (uint32_t*)(B + o); o += (((size_t)m + 1) * 4 + 255) & ~(size_t)255;
-            uint32_t* d_units = (uint32_t*)(B + o);
+            auto take = [&](size_t bytes) { uint8_t* p = B + o; o += (bytes + 255) & ~(size_t)255; return p; };
+            a.rec_buf = (uint64_t*)take((size_t)pos * 8);
+            a.pv_buf = (uint16_t*)take((size_t)pos * 2);
+            a.blk = take((size_t)blk * FB_SLOT_BYTES);
+            a.cks = (int32_t*)take((size_t)m * 4);
+            uint64_t* d_rp0 = (uint64_t*)take(((size_t)m + 1) * 8);
+            uint32_t* d_tb0 = (uint32_t*)take(((size_t)m + 1) * 4);
+            uint32_t* d_units = (uint32_t*)take(units.size() * 4);
+            uint32_t* d_lzs = (uint32_t*)take(lzs.size() * 4);
+            if (lz_shift) {
+                a.lz_shift = lz_shift;
+                a.nlseg = nlseg;
+                a.lz_sg0 = d_lzs;
+                a.lz_seg = d_lzs + (m + 1);
+                a.lz_w = (uint64_t*)take((size_t)pos * 8);
+                a.lz_s2 = (uint32_t*)take((size_t)pos * 4);
+                a.lz_v1 = (uint64_t*)take((size_t)pos / 8);
+                a.lz_e1 = (uint64_t*)take((size_t)pos / 8);
+                a.lz_e2 = (uint64_t*)take((size_t)pos / 8);
+                a.lz_end = (uint64_t*)take((size_t)nlseg * 8);
+                a.lz_carry = (uint64_t*)take((size_t)nlseg * 8);
+                a.lz_c = (uint32_t*)take((size_t)nlseg * 4);
+                a.lz_cnt = (uint32_t*)take((size_t)nlseg * 4);
+                a.lz_fin = (uint32_t*)take((size_t)m * 4);
+            }
+            if (o > pool_bytes) return fail(SDZ_API_OOM, "deflate: record plan exceeds its pool");
             // plan -> device through the pinned staging buffer (one copy, waited for below)
-            const size_t pb = rp0.size() * 8 + tb0.size() * 4 + units.size() * 4;
+            const size_t pb = rp0.size() * 8 + tb0.size() * 4 + units.size() * 4 + lzs.size() * 4;
             void* pin = nullptr;
             if (int rc = g_pinned.get(pb + 64, &pin)) return rc;
             uint8_t* P = (uint8_t*)pin;
             std::memcpy(P, rp0.data(), rp0.size() * 8);
             std::memcpy(P + rp0.size() * 8, tb0.data(), tb0.size() * 4);
-            if (!units.empty()) std::memcpy(P + rp0.size() * 8 + tb0.size() * 4, units.data(), units.size() * 4);
+            uint8_t* Pu = P + rp0.size() * 8 + tb0.size() * 4;
+            if (!units.empty()) std::memcpy(Pu, units.data(), units.size() * 4);
+            uint8_t* Pl = Pu + units.size() * 4;
+            if (!lzs.empty()) std::memcpy(Pl, lzs.data(), lzs.size() * 4);
             HIPCHK(hipMemcpyAsync(d_rp0, P, rp0.size() * 8, hipMemcpyHostToDevice, s));
             HIPCHK(hipMemcpyAsync(d_tb0, P + rp0.size() * 8, tb0.size() * 4, hipMemcpyHostToDevice, s));
-            if (!units.empty())
-                HIPCHK(hipMemcpyAsync(d_units, P + rp0.size() * 8 + tb0.size() * 4, units.size() * 4,
-                                      hipMemcpyHostToDevice, s));
+            if (!units.empty()) HIPCHK(hipMemcpyAsync(d_units, Pu, units.size() * 4, hipMemcpyHostToDevice, s));
+            if (!lzs.empty()) HIPCHK(hipMemcpyAsync(d_lzs, Pl, lzs.size() * 4, hipMemcpyHostToDevice, s));
             a.rp0 = d_rp0; a.tb0 = d_tb0;
             a.mseg = d_units; a.nmseg = nmseg;
             a.cunit = d_units + nmseg; a.ncunit = (uint32_t)units.size() - nmseg;

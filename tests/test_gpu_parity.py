@@ -370,6 +370,30 @@ def test_deflate_record_path_long_inputs(paradise):
     assert g[10:] == O.deflate(paradise, level=6, format="gzip", file_name="p.txt", mtime=0)[10:]
 
 
+@pytest.mark.parametrize("shift", [6, 9, 12])
+def test_deflate_segment_parse(monkeypatch, paradise, shift):
+    """The segment-parallel lazy parse (k_lz_*) at forced segment sizes 2^6 (matches that jump
+    whole segments), 2^9 (one long stream) and 2^12 (batches): joins that meet the segment's
+    own parse, long runs whose parses stay out of phase across many segments (k_lz_fix), the
+    final literal, TRUNCATE_BLOCK and LIT_BUFSIZE cuts -- bit-exact with the oracle and with
+    the serial parse kernel (SDZ_SERIAL_PARSE)."""
+    rng = random.Random(17 + shift)
+    inputs = [paradise, bytes(300000), b"ab" * 70000 + text_corpus(rng, 50000),
+              _periodic(rng, 120000), bytes(rng.getrandbits(8) for _ in range(70000)),
+              text_corpus(rng, 5000) + bytes(40000) + text_corpus(rng, 30000) + b"z" * 3000,
+              _overlay_stress(rng, 90000), text_corpus(rng, 700), b"q" * 259]
+    monkeypatch.setenv("SDZ_LZ_SHIFT", str(shift))
+    for level in (4, 6, 9):
+        exp = [O.deflate(d, level=level) for d in inputs]
+        gpu = sdz.deflate_batch(inputs, level=level)
+        for i, (g, e) in enumerate(zip(gpu, exp)):
+            assert g["status"] == "OK" and g["data"] == e, (level, i)
+    monkeypatch.delenv("SDZ_LZ_SHIFT")
+    monkeypatch.setenv("SDZ_SERIAL_PARSE", "1")
+    g = sdz.deflate_batch(inputs[:4], level=6)
+    assert [x["data"] for x in g] == [O.deflate(d, level=6) for d in inputs[:4]]
+
+
 def test_deflate_record_path_output_overflow(paradise):
     """An output slot one byte short is an overflow; an exact one is not."""
     inputs = [paradise[:65536], paradise[65536:100000]]
