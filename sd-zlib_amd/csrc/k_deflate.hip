@@ -1938,7 +1938,15 @@ __global__ __launch_bounds__(LB_THREADS) void k_lz_blocks(DeflateArgs A) {
         if (threadIdx.x == 0) { F->nblk = 0; F->flag = 1; }
         return;
     }
+    if (A.lz_act && (A.lz_act[sid] & 1u)) {                    // fast levels: not settled, serial kernel
+        if (threadIdx.x == 0) { F->nblk = 0; F->flag = 1; }
+        return;
+    }
     const int64_t n = (int64_t)in_len;
+    // deflate_slow tallies a literal or match one step after its position (the cutting step is
+    // one past the bytes before it), deflate_fast at it; TRUNCATE_BLOCK only above level 2
+    const int64_t plus = A.level >= 4 ? 1 : 0;
+    const bool trunc = A.level > 2;
     const uint32_t fin = A.lz_fin[sid], nsym = fin >> 1, nchk = nsym - (fin & 1u);
     const GLB uint32_t* sym = (const GLB uint32_t*)A.rec_buf + 2 * A.rp0[sid];
     GLB uint8_t* slots = (GLB uint8_t*)(A.blk + (uint64_t)A.tb0[sid] * FB_SLOT);
@@ -1950,9 +1958,9 @@ __global__ __launch_bounds__(LB_THREADS) void k_lz_blocks(DeflateArgs A) {
         int64_t step = n, strstart = n;                        // the cutting step's position; strstart after it
         if (b0 + 8192 <= nchk) {
             const LzSums a = lb_sums(sym, b0, b0 + 8192, red);
-            const int64_t in_length = a.cov + 1;
+            const int64_t in_length = a.cov + plus;
             const uint32_t out_length = (8192u * 8u + a.dxb) >> 3;
-            if (a.mat < 4096 && (int64_t)out_length < in_length / 2) {
+            if (trunc && a.mat < 4096 && (int64_t)out_length < in_length / 2) {
                 cnt = 8192;
                 step = block_start + in_length;
                 strstart = block_start + a.cov + a.last;
@@ -1960,7 +1968,7 @@ __global__ __launch_bounds__(LB_THREADS) void k_lz_blocks(DeflateArgs A) {
                 const LzSums b = lb_sums(sym, b0 + 8192, b0 + LIT_BUFSIZE - 1, red);
                 cnt = LIT_BUFSIZE - 1;
                 const int64_t before = (int64_t)a.cov + a.last + b.cov;   // symbols [b0, b0 + 16382)
-                step = block_start + before + 1;
+                step = block_start + before + plus;
                 strstart = block_start + before + b.last;
             }
         }
@@ -1981,6 +1989,282 @@ __global__ __launch_bounds__(LB_THREADS) void k_lz_blocks(DeflateArgs A) {
         F->nblk = nb;
         F->flag = nb > nbcap ? 1u : 0u;
     }
+}
+
+// ------------------------------------------------------------------ fast levels on the record path
+// deflate_fast (deflate.ts:953-1049) inserts the string at every step with lookahead >=
+// MIN_MATCH and at the positions inside a match of at most max_lazy_match bytes, but not inside
+// longer matches: its hash chains depend on its own parse.  The positions it inserts are the
+// unique fixed point of  I -> the parse whose searches walk the chains of I -> the positions
+// that parse inserts  (a step at s reads I below s only, so by induction over positions any
+// fixed point is the reference's), and iterating from I = every position reaches it: a round
+// settles at least everything before the first difference, and the changes of a round are
+// local (10-50 rounds on text, each touching fewer positions).  A round: k_fz_match (every
+// position's search on the links of k_dfl_chain, stepping over positions outside I),
+// the segment-parallel parse of k_lz_* with the step position as its whole state
+// (k_fz_spec / k_fz_join / k_fz_fix), k_fz_merge (the next I, and whether it changed) and
+// k_fz_roll (streams whose I did not change are settled and leave the rounds).  The symbols of
+// their last round then take the slow levels' way (k_lz_count / scan / emit / blocks).
+__device__ __forceinline__ bool fz_in(const GLB uint64_t* I, int64_t q) { return (I[q >> 6] >> (q & 63)) & 1ull; }
+// bits of one bitmap set in increasing position order, words written as they are left behind
+struct BitW {
+    GLB uint64_t* dst;
+    int wc;
+    uint64_t acc;
+    __device__ void to(int p) { for (; (p >> 6) != wc; ++wc) { dst[wc] = acc; acc = 0; } }
+    __device__ void set(int p) { to(p); acc |= 1ull << (p & 63); }
+    __device__ void end(int g, int e) {                      // write the words up to position e - 1
+        if (e > g)
+            for (; wc <= ((e - 1) >> 6); ++wc) { dst[wc] = acc; acc = 0; }
+    }
+};
+// common prefix of in[a ..] and in[b ..] (a < b, b + MAX_MATCH <= input length), <= MAX_MATCH
+__device__ __forceinline__ int fz_len(const GLB uint8_t* in, int a, int b) {
+    int l = 0;
+    for (; l < MAX_MATCH - 2; l += 4) {
+        uint32_t x, y;
+        __builtin_memcpy(&x, (const uint8_t*)(in + a + l), 4);
+        __builtin_memcpy(&y, (const uint8_t*)(in + b + l), 4);
+        if (x ^ y) return l + (int)(__builtin_ctz(x ^ y) >> 3);
+    }
+    while (l < MAX_MATCH && in[a + l] == in[b + l]) ++l;
+    return l;
+}
+// the previous position of I on q's hash chain above `lo` (0: none)
+__device__ __forceinline__ int fz_prev(const GLB uint16_t* pv, const GLB uint64_t* I, int q, int lo) {
+    for (;;) {
+        const uint32_t d = pv[q];
+        q -= (int)d;
+        if (!d || q <= lo) return 0;
+        if (fz_in(I, q)) return q;
+    }
+}
+// longest_match (deflate.ts:827-946) as deflate_fast calls it at P (best_len from
+// MIN_MATCH - 1, every candidate of the chain of I counted) with P + MIN_LOOKAHEAD <= n: only
+// input bytes are read.  Record: len << 16 | dist, 0 below MIN_MATCH.
+__device__ uint32_t fz_search(const GLB uint8_t* in, const GLB uint16_t* pv, const GLB uint64_t* I, int P, int chain,
+                              int nice) {
+    // hash_head: not 0, within MAX_DIST (deflate.ts:986); the walk continues above limit
+    int cur = fz_prev(pv, I, P, P > MAX_DIST ? P - MAX_DIST - 1 : 0);
+    if (cur == 0) return 0u;
+    const int limit = P > MAX_DIST ? P - MAX_DIST : 0;
+    int best = MIN_MATCH - 1, bpos = 0;
+    for (;;) {
+        const int len = fz_len(in, cur, P);
+        if (len > best) {
+            best = len; bpos = cur;
+            if (len >= nice) break;
+        }
+        if (--chain == 0) break;
+        cur = fz_prev(pv, I, cur, limit);
+        if (cur == 0) break;
+    }
+    return best >= MIN_MATCH ? ((uint32_t)best << 16) | (uint32_t)(P - bpos) : 0u;
+}
+// the same for the last positions (lookahead < MIN_LOOKAHEAD), in the window the reference
+// has there (stale bytes past the input: see tail_search)
+__device__ uint32_t fz_tail(const GLB uint8_t* in, const GLB uint16_t* pv, const GLB uint64_t* I, int64_t n, int64_t P,
+                            int chain_length, int nice) {
+    const int64_t off = slide_off(n, P);
+    const int strstart = (int)(P - off);
+    auto prev_of = [&](int64_t q, int lo) -> int {       // window index of the previous position of I above lo
+        for (;;) {
+            const uint32_t d = pv[q];
+            q -= (int64_t)d;
+            if (!d || q - off <= lo) return 0;
+            if (fz_in(I, q)) return (int)(q - off);
+        }
+    };
+    auto wb = [&](int i) -> uint32_t { return win_byte(in, n, off, i); };
+    int cur = prev_of(P, strstart > MAX_DIST ? strstart - MAX_DIST - 1 : 0);
+    if (cur == 0) return 0u;
+    const int lookahead = (int)(n - P);
+    if (nice > lookahead) nice = lookahead;
+    const int limit = strstart > MAX_DIST ? strstart - MAX_DIST : 0;
+    int best = MIN_MATCH - 1, bstart = 0;
+    uint32_t scan_end1 = wb(strstart + best - 1), scan_end = wb(strstart + best);
+    const uint32_t c0 = wb(strstart), c1 = wb(strstart + 1);
+    do {
+        const int match = cur;
+        const int nx = prev_of(match + off, limit);
+        const uint32_t e0 = wb(match + best), e1 = wb(match + best - 1);
+        const uint32_t m0 = wb(match), m1 = wb(match + 1);
+        if ((e0 == scan_end) & (e1 == scan_end1) & (m0 == c0) & (m1 == c1)) {
+            int len = 3;                      // byte 2 is not compared (equal hash, deflate.ts:891-897)
+            while (len < MAX_MATCH && wb(strstart + len) == wb(match + len)) ++len;
+            if (len > best) {
+                bstart = match;
+                best = len;
+                if (len >= nice) break;
+                scan_end1 = wb(strstart + best - 1);
+                scan_end = wb(strstart + best);
+            }
+        }
+        cur = nx;
+    } while (cur > limit && --chain_length != 0);
+    if (best > lookahead) best = lookahead;
+    return best >= MIN_MATCH ? ((uint32_t)best << 16) | (uint32_t)(strstart - bstart) : 0u;
+}
+__global__ __launch_bounds__(256) void k_fz_init(DeflateArgs A) {     // I = every position with lookahead >= 3
+    const uint32_t seg = blockIdx.x * 256 + threadIdx.x;
+    if (seg >= A.nlseg) return;
+    const LzSeg q = lz_seg(A, seg);
+    GLB uint64_t* I = (GLB uint64_t*)A.lz_i + (q.rp >> 6);
+    for (int wi = q.g >> 6; wi <= ((q.h - 1) >> 6); ++wi) I[wi] = lz_range(wi, q.g, q.n - MIN_MATCH + 1);
+    if (q.j == 0) A.lz_act[q.k] = 1u;
+}
+__global__ __launch_bounds__(256) void k_fz_match(DeflateArgs A) {
+    const uint32_t seg = blockIdx.x;
+    if (seg >= A.nlseg) return;
+    const LzSeg q = lz_seg(A, seg);
+    if (!(A.lz_act[q.k] & 1u)) return;
+    const GLB uint8_t* in = (const GLB uint8_t*)(A.in + A.in_off[q.k]);
+    const GLB uint16_t* pv = (const GLB uint16_t*)A.pv_buf + q.rp;
+    const GLB uint64_t* I = (const GLB uint64_t*)A.lz_i + (q.rp >> 6);
+    GLB uint64_t* rec = (GLB uint64_t*)A.rec_buf + q.rp;
+    const int nice = c_config[A.level][2], chain = c_config[A.level][3];
+    for (int p = q.g + (int)threadIdx.x; p < q.h; p += 256) {
+        uint32_t r = 0;
+        if (q.n - p >= MIN_MATCH)
+            r = p + MIN_LOOKAHEAD <= q.n ? fz_search(in, pv, I, p, chain, nice) : fz_tail(in, pv, I, q.n, p, chain, nice);
+        rec[p] = r;
+    }
+}
+// one deflate_fast step at s (deflate.ts:974-1033): its symbol, the positions it inserts
+// (I.set), the next step position; *iin: the positions inside its match are inserted
+__device__ __forceinline__ uint32_t fz_step(int& s, uint32_t r, const GLB uint8_t* in, int n, int max_ins, BitW& I,
+                                            bool& iin) {
+    const int lookahead = n - s;
+    if (lookahead >= MIN_MATCH) I.set(s);
+    const int len = (int)(r >> 16);
+    if (len >= MIN_MATCH) {
+        iin = len <= max_ins && lookahead - len >= MIN_MATCH;
+        if (iin)
+            for (int i = 1; i < len; ++i) I.set(s + i);
+        const uint32_t sym = (uint32_t)(len - MIN_MATCH) | ((r & 0xffffu) << 8) | LZ_SYM;
+        s += len;
+        return sym;
+    }
+    iin = false;
+    const uint32_t sym = (uint32_t)in[s] | LZ_SYM;
+    s += 1;
+    return sym;
+}
+__global__ __launch_bounds__(LZ_THREADS) void k_fz_spec(DeflateArgs A) {
+    const uint32_t seg = blockIdx.x * LZ_THREADS + threadIdx.x;
+    if (seg >= A.nlseg) return;
+    const LzSeg q = lz_seg(A, seg);
+    if (!(A.lz_act[q.k] & 1u)) return;
+    const GLB uint8_t* in = (const GLB uint8_t*)(A.in + A.in_off[q.k]);
+    const GLB uint64_t* rec = (const GLB uint64_t*)A.rec_buf + q.rp;
+    GLB uint64_t* w = (GLB uint64_t*)A.lz_w + q.rp;
+    const int max_ins = c_config[A.level][1];
+    BitW V{(GLB uint64_t*)A.lz_v1 + (q.rp >> 6), q.g >> 6, 0};
+    BitW I{(GLB uint64_t*)A.lz_i1 + (q.rp >> 6), q.g >> 6, 0};
+    int s = q.g;
+    bool iin = false;
+    while (s < q.h) {
+        const int p = s;
+        const uint32_t r = (uint32_t)rec[p];
+        V.set(p);
+        const uint32_t sym = fz_step(s, r, in, q.n, max_ins, I, iin);
+        w[p] = (uint64_t)sym << 32;
+    }
+    // (interior bits past h belong to the next segment's join: BitW.end stops at h)
+    I.acc &= (I.wc << 6) + 64 <= q.h ? ~0ull : lz_range(I.wc, q.g, q.h);
+    V.end(q.g, q.h);
+    I.end(q.g, q.h);
+    A.lz_end[seg] = (uint64_t)(uint32_t)s | ((uint64_t)(iin ? 1u : 0u) << 32);
+    if (q.j == 0) A.lz_c[seg] = 0;
+}
+// carry the parse at s on through segment q until it stands on a step position of the
+// segment's own parse (the step position is the whole state); positions [g, s) lie inside the
+// match crossing in (inserted iff cin).  Returns the meeting position or q.h.
+__device__ int fz_join_run(const DeflateArgs& A, const LzSeg& q, int& s, bool& cin, int max_ins) {
+    const GLB uint8_t* in = (const GLB uint8_t*)(A.in + A.in_off[q.k]);
+    const GLB uint64_t* rec = (const GLB uint64_t*)A.rec_buf + q.rp;
+    const GLB uint64_t* v1 = (const GLB uint64_t*)A.lz_v1 + (q.rp >> 6);
+    GLB uint32_t* s2 = (GLB uint32_t*)A.lz_s2 + q.rp;
+    BitW E{(GLB uint64_t*)A.lz_e2 + (q.rp >> 6), q.g >> 6, 0};
+    BitW I{(GLB uint64_t*)A.lz_i2 + (q.rp >> 6), q.g >> 6, 0};
+    if (cin)
+        for (int p = q.g; p < s && p < q.h; ++p) I.set(p);
+    int c = q.h, vwc = -1;
+    uint64_t vw = 0;
+    while (s < q.h) {
+        if ((s >> 6) != vwc) { vwc = s >> 6; vw = v1[vwc]; }
+        if ((vw >> (s & 63)) & 1ull) { c = s; break; }
+        const int p = s;
+        const uint32_t r = (uint32_t)rec[p];
+        E.set(p);
+        s2[p] = fz_step(s, r, in, q.n, max_ins, I, cin);
+    }
+    if (c == q.h) I.acc &= (I.wc << 6) + 64 <= q.h ? ~0ull : lz_range(I.wc, q.g, q.h);
+    E.end(q.g, c);
+    I.end(q.g, c);
+    return c;
+}
+__global__ __launch_bounds__(LZ_THREADS) void k_fz_join(DeflateArgs A) {
+    const uint32_t seg = blockIdx.x * LZ_THREADS + threadIdx.x;
+    if (seg >= A.nlseg) return;
+    const LzSeg q = lz_seg(A, seg);
+    if (q.j == 0 || !(A.lz_act[q.k] & 1u)) return;
+    const uint64_t e = A.lz_end[seg - 1];
+    int s = (int)(uint32_t)e;
+    bool cin = (e >> 32) != 0;
+    A.lz_c[seg] = (uint32_t)fz_join_run(A, q, s, cin, c_config[A.level][1]);
+    A.lz_carry[seg] = (uint64_t)(uint32_t)s | ((uint64_t)(cin ? 1u : 0u) << 32);
+}
+__global__ __launch_bounds__(LZ_THREADS) void k_fz_fix(DeflateArgs A) {
+    const uint32_t k = blockIdx.x * LZ_THREADS + threadIdx.x;
+    if (k >= A.n || A.rp0[k] == ~0ull || !(A.lz_act[k] & 1u)) return;
+    const uint32_t base = A.lz_sg0[k], K = A.lz_sg0[k + 1] - base;
+    const int max_ins = c_config[A.level][1];
+    bool ok = true;
+    int s = 0;
+    bool cin = false;
+    for (uint32_t j = 1; j < K; ++j) {
+        const LzSeg q = lz_seg(A, base + j);
+        if (ok) {
+            if ((int)A.lz_c[base + j] < q.h) continue;
+            const uint64_t e = A.lz_carry[base + j];
+            s = (int)(uint32_t)e;
+            cin = (e >> 32) != 0;
+            ok = false;
+            continue;
+        }
+        const int c = fz_join_run(A, q, s, cin, max_ins);
+        A.lz_c[base + j] = (uint32_t)c;
+        if (c < q.h) ok = true;
+    }
+    A.lz_fin[k] = 0;                                            // deflate_fast leaves no pending literal
+}
+// the next I of each segment ([g, c) from the join, [c, h) from its own parse); a stream
+// whose I changed anywhere goes another round
+__global__ __launch_bounds__(LZ_THREADS) void k_fz_merge(DeflateArgs A) {
+    const uint32_t seg = blockIdx.x * LZ_THREADS + threadIdx.x;
+    if (seg >= A.nlseg) return;
+    const LzSeg q = lz_seg(A, seg);
+    if (!(A.lz_act[q.k] & 1u)) return;
+    const int c = (int)A.lz_c[seg];
+    GLB uint64_t* I = (GLB uint64_t*)A.lz_i + (q.rp >> 6);
+    const GLB uint64_t* i1 = (const GLB uint64_t*)A.lz_i1 + (q.rp >> 6);
+    const GLB uint64_t* i2 = (const GLB uint64_t*)A.lz_i2 + (q.rp >> 6);
+    bool changed = false;
+    for (int wi = q.g >> 6; wi <= ((q.h - 1) >> 6); ++wi) {
+        const uint64_t m2 = lz_range(wi, q.g, c), m1 = lz_range(wi, c, q.h);
+        const uint64_t nw = ((m2 ? i2[wi] : 0ull) & m2) | (i1[wi] & m1);
+        if (nw != I[wi]) { changed = true; I[wi] = nw; }
+    }
+    if (changed) atomicOr(&A.lz_act[q.k], 2u);
+}
+__global__ __launch_bounds__(256) void k_fz_roll(DeflateArgs A) {
+    const uint32_t k = blockIdx.x * 256 + threadIdx.x;
+    if (k >= A.n) return;
+    const uint32_t a = A.lz_act[k];
+    if (!(a & 1u)) return;
+    A.lz_act[k] = (a >> 1) & 1u;
+    if (a & 2u) atomicAdd(A.lz_nact, 1u);
 }
 
 // tree context of the record path: LDS arrays, header bits into LDS words
@@ -2336,6 +2620,7 @@ int device_max_u64(const uint64_t* v, uint32_t n, unsigned long long* d_slot, ui
 }
 
 static bool c_config_host_fast(int level) { return level >= 1 && level <= 3; }
+constexpr uint32_t kFzRounds = 1024;                       // then the unsettled streams go serial
 
 // side/ev (optional): a second stream and an event for it.  The input checksum depends on
 // nothing else: it runs on the side stream beside the parse and the trees, which are
@@ -2346,12 +2631,15 @@ void launch_deflate(const DeflateArgs& a, hipStream_t st, hipStream_t side, hipE
     if (a.n == 0) return;
     dim3 grid((a.n + DF_THREADS - 1) / DF_THREADS);
     hipLaunchKernelGGL(k_deflate_tables, dim3(1), dim3(1), 0, st);
-    if (a.rec_buf && !c_config_host_fast(a.level)) {
+    const bool fastlv = c_config_host_fast(a.level);
+    if (a.rec_buf && (!fastlv || (a.lz_shift && a.nlseg))) {
         const int ck_kind = a.format == SDZ_DEFLATE_GZIP ? 1 : 0;
         if (a.ncunit)
             hipLaunchKernelGGL(k_dfl_chain, dim3((a.ncunit + CH_WAVES - 1) / CH_WAVES), dim3(64 * CH_WAVES), 0, st, a);
-        if (a.nmseg) hipLaunchKernelGGL(k_dfl_match, dim3(a.nmseg), dim3(PM_THREADS), 0, st, a);
-        hipLaunchKernelGGL(k_dfl_tail, dim3(a.n), dim3(256), 0, st, a);
+        if (!fastlv) {
+            if (a.nmseg) hipLaunchKernelGGL(k_dfl_match, dim3(a.nmseg), dim3(PM_THREADS), 0, st, a);
+            hipLaunchKernelGGL(k_dfl_tail, dim3(a.n), dim3(256), 0, st, a);
+        }
         const bool fork = side && ev && hipEventRecord(ev, st) == hipSuccess &&
                           hipStreamWaitEvent(side, ev, 0) == hipSuccess;
         if (fork) {
@@ -2360,9 +2648,29 @@ void launch_deflate(const DeflateArgs& a, hipStream_t st, hipStream_t side, hipE
         }
         if (a.lz_shift && a.nlseg) {
             const dim3 gseg((a.nlseg + LZ_THREADS - 1) / LZ_THREADS), gstr((a.n + LZ_THREADS - 1) / LZ_THREADS);
-            hipLaunchKernelGGL(k_lz_spec, gseg, dim3(LZ_THREADS), 0, st, a);
-            hipLaunchKernelGGL(k_lz_join, gseg, dim3(LZ_THREADS), 0, st, a);
-            hipLaunchKernelGGL(k_lz_fix, gstr, dim3(LZ_THREADS), 0, st, a);
+            if (fastlv) {
+                // rounds of the inserted-position fixed point; the host reads the number of
+                // streams still moving after each (one small copy + sync per round)
+                (void)hipMemsetAsync(a.lz_act, 0, (size_t)a.n * 4, st);
+                hipLaunchKernelGGL(k_fz_init, dim3((a.nlseg + 255) / 256), dim3(256), 0, st, a);
+                for (uint32_t round = 0; round < kFzRounds; ++round) {
+                    hipLaunchKernelGGL(k_fz_match, dim3(a.nlseg), dim3(256), 0, st, a);
+                    hipLaunchKernelGGL(k_fz_spec, gseg, dim3(LZ_THREADS), 0, st, a);
+                    hipLaunchKernelGGL(k_fz_join, gseg, dim3(LZ_THREADS), 0, st, a);
+                    hipLaunchKernelGGL(k_fz_fix, gstr, dim3(LZ_THREADS), 0, st, a);
+                    hipLaunchKernelGGL(k_fz_merge, gseg, dim3(LZ_THREADS), 0, st, a);
+                    (void)hipMemsetAsync(a.lz_nact, 0, 4, st);
+                    hipLaunchKernelGGL(k_fz_roll, dim3((a.n + 255) / 256), dim3(256), 0, st, a);
+                    uint32_t moving = 0;
+                    if (hipMemcpyAsync(&moving, a.lz_nact, 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
+                        hipStreamSynchronize(st) != hipSuccess || moving == 0)
+                        break;
+                }
+            } else {
+                hipLaunchKernelGGL(k_lz_spec, gseg, dim3(LZ_THREADS), 0, st, a);
+                hipLaunchKernelGGL(k_lz_join, gseg, dim3(LZ_THREADS), 0, st, a);
+                hipLaunchKernelGGL(k_lz_fix, gstr, dim3(LZ_THREADS), 0, st, a);
+            }
             hipLaunchKernelGGL(k_lz_count, gseg, dim3(LZ_THREADS), 0, st, a);
             hipLaunchKernelGGL(k_lz_scan, gstr, dim3(LZ_THREADS), 0, st, a);
             hipLaunchKernelGGL(k_lz_emit, gseg, dim3(LZ_THREADS), 0, st, a);

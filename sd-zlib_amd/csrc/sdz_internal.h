@@ -127,6 +127,12 @@ struct DeflateArgs {
     uint32_t* lz_c;              // per segment: first position whose phase-1 parse is the true one
     uint32_t* lz_cnt;            // per segment: symbols, then their exclusive prefix in the stream
     uint32_t* lz_fin;            // per stream: bit 0 the final literal, bits 1.. the symbol count
+    // fast levels (1-3, k_fz_*): the inserted-position fixed point, iterated per stream
+    uint64_t* lz_i;              // bitmap: positions inserted into the hash chains (current guess)
+    uint64_t* lz_i1;             // bitmaps of the next guess: phase-1 parses,
+    uint64_t* lz_i2;             //   joins / fixes
+    uint32_t* lz_act;            // per stream: bit 0 still iterating, bit 1 changed this round
+    uint32_t* lz_nact;           // one counter: streams still iterating after a round
     int32_t* cks;                // n input checksums (record path)
     uint32_t fast;               // set by launch_deflate: k_deflate redoes flagged streams only
     const uint8_t* dict;         // preset dictionary (deflateSetDictionary), may be null

@@ -779,7 +779,9 @@ int sdz_deflate_batch_device(const uint8_t* in, const uint64_t* in_off, const ui
     // parse (k_deflate.hip).  The host plans it from the input sizes: each stream's record /
     // link range, block slots, chain units and match segments, cut into sub-batches that
     // fit half of free HBM.  Streams off the path run the serial kernel.
-    const bool recpath = level >= 4 && !dict;
+    // levels 1-3 take it with the segment-parallel parse only (their chains need its rounds)
+    const bool lz_on = !getenv("SDZ_SERIAL_PARSE");
+    const bool recpath = (level >= 4 || lz_on) && !dict;
     std::vector<uint64_t> len(recpath ? n : 0);
     if (recpath) {
         HIPCHK(hipMemcpyAsync(len.data(), in_len, (size_t)n * 8, hipMemcpyDeviceToHost, s));
@@ -789,7 +791,7 @@ int sdz_deflate_batch_device(const uint8_t* in, const uint64_t* in_off, const ui
     // segment-parallel parse (k_lz_*): segments of 2^lz_shift positions, shorter ones when the
     // batch is small so a single long stream still spreads over many lanes
     uint32_t lz_shift = 0;
-    if (recpath && !getenv("SDZ_SERIAL_PARSE")) {
+    if (recpath && lz_on) {
         uint64_t tot = 0;
         for (uint32_t i = 0; i < n; ++i)
             if (on_path(i)) tot += len[i];
@@ -835,7 +837,7 @@ int sdz_deflate_batch_device(const uint8_t* in, const uint64_t* in_off, const ui
         }
         const uint64_t m = cb[j + 1] - cb[j];
         const uint64_t b = sb + pos * kPosBytes + blk * FB_SLOT_BYTES + m * 16 + 8 * (m + 1) + 4 * (m + 1) + 4 * units +
-                           (lz_shift ? 4 * (m + 1) + 4 * m + 32 * segs + 16 * 256 : 0) + 4096;
+                           (lz_shift ? 4 * (m + 1) + 8 * m + 32 * segs + 20 * 256 : 0) + 4096;
         pool_bytes = std::max(pool_bytes, b);
     }
     void* state = nullptr;
@@ -932,6 +934,14 @@ int sdz_deflate_batch_device(const uint8_t* in, const uint64_t* in_off, const ui
                 a.lz_c = (uint32_t*)take((size_t)nlseg * 4);
                 a.lz_cnt = (uint32_t*)take((size_t)nlseg * 4);
                 a.lz_fin = (uint32_t*)take((size_t)m * 4);
+                if (level <= 3) {
+                    a.lz_e1 = a.lz_v1;                  // deflate_fast emits a symbol at every step
+                    a.lz_i = (uint64_t*)take((size_t)pos / 8);
+                    a.lz_i1 = (uint64_t*)take((size_t)pos / 8);
+                    a.lz_i2 = (uint64_t*)take((size_t)pos / 8);
+                    a.lz_act = (uint32_t*)take((size_t)m * 4);
+                    a.lz_nact = (uint32_t*)take(4);
+                }
             }
             if (o > pool_bytes) return fail(SDZ_API_OOM, "deflate: record plan exceeds its pool");
             // plan -> device through the pinned staging buffer (one copy, waited for below)

@@ -372,7 +372,8 @@ def test_deflate_record_path_long_inputs(paradise):
 
 @pytest.mark.parametrize("shift", [6, 9, 12])
 def test_deflate_segment_parse(monkeypatch, paradise, shift):
-    """The segment-parallel lazy parse (k_lz_*) at forced segment sizes 2^6 (matches that jump
+    """The segment-parallel parses -- lazy (k_lz_*, levels 4-9) and deflate_fast's rounds of
+    inserted positions (k_fz_*, levels 1-3) -- at forced segment sizes 2^6 (matches that jump
     whole segments), 2^9 (one long stream) and 2^12 (batches): joins that meet the segment's
     own parse, long runs whose parses stay out of phase across many segments (k_lz_fix), the
     final literal, TRUNCATE_BLOCK and LIT_BUFSIZE cuts -- bit-exact with the oracle and with
@@ -383,7 +384,7 @@ def test_deflate_segment_parse(monkeypatch, paradise, shift):
               text_corpus(rng, 5000) + bytes(40000) + text_corpus(rng, 30000) + b"z" * 3000,
               _overlay_stress(rng, 90000), text_corpus(rng, 700), b"q" * 259]
     monkeypatch.setenv("SDZ_LZ_SHIFT", str(shift))
-    for level in (4, 6, 9):
+    for level in (1, 2, 3, 4, 6, 9):
         exp = [O.deflate(d, level=level) for d in inputs]
         gpu = sdz.deflate_batch(inputs, level=level)
         for i, (g, e) in enumerate(zip(gpu, exp)):
