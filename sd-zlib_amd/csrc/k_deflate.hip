@@ -1810,28 +1810,43 @@ __global__ __launch_bounds__(LZ_THREADS) void k_lz_join(DeflateArgs A) {
     A.lz_c[seg] = (uint32_t)lz_join_run(A, q, t, c_config[A.level][0], c_config[A.level][1]);
     A.lz_carry[seg] = lz_save(t);
 }
-__global__ __launch_bounds__(LZ_THREADS) void k_lz_fix(DeflateArgs A) {
-    const uint32_t k = blockIdx.x * LZ_THREADS + threadIdx.x;
+__global__ __launch_bounds__(64) void k_lz_fix(DeflateArgs A) {      // one wave per stream (as k_fz_fix)
+    const uint32_t k = blockIdx.x, lane = threadIdx.x;
     if (k >= A.n || A.rp0[k] == ~0ull) return;
     const uint32_t base = A.lz_sg0[k], K = A.lz_sg0[k + 1] - base;
     if (K == 0) return;
     const int good = c_config[A.level][0], max_lazy = c_config[A.level][1];
-    bool ok = true;                                            // segment j - 1's parse is true at its end
+    bool ok = true;                                            // the last segment's parse is true at its end
     LzSt t{0, 0, 0, 0};
-    for (uint32_t j = 1; j < K; ++j) {
-        const LzSeg q = lz_seg(A, base + j);
-        if (ok) {
-            if ((int)A.lz_c[base + j] < q.h) continue;         // met: true from there
-            t = lz_load(A.lz_carry[base + j]);                 // crossed the segment: its carry is true
-            ok = false;
-            continue;
+    uint32_t j = 1;
+    while (j < K) {
+        uint32_t found = K;
+        for (; j < K; j += 64) {
+            const uint32_t jj = j + lane;
+            const bool un = jj < K && (int)A.lz_c[base + jj] >= lz_seg(A, base + jj).h;
+            const uint64_t m = __ballot(un);
+            if (m) { found = j + (uint32_t)__builtin_ctzll(m); break; }
         }
-        const int c = lz_join_run(A, q, t, good, max_lazy);
-        A.lz_c[base + j] = (uint32_t)c;
-        if (c < q.h) ok = true;
+        if (found >= K) break;
+        uint32_t next = K;
+        if (lane == 0) {
+            t = lz_load(A.lz_carry[base + found]);             // crossed its segment: the carry is true
+            ok = false;
+            uint32_t jj = found + 1;
+            for (; jj < K; ++jj) {
+                const LzSeg q = lz_seg(A, base + jj);
+                const int c = lz_join_run(A, q, t, good, max_lazy);
+                A.lz_c[base + jj] = (uint32_t)c;
+                if (c < q.h) { ok = true; break; }
+            }
+            next = jj + 1;
+        }
+        j = __shfl(next, 0);
     }
-    const LzSt f = ok ? lz_load(A.lz_end[base + K - 1]) : t;
-    A.lz_fin[k] = (uint32_t)f.avail;                            // deflate_slow's last literal (deflate.ts:1172)
+    if (lane == 0) {
+        const LzSt f = ok ? lz_load(A.lz_end[base + K - 1]) : t;
+        A.lz_fin[k] = (uint32_t)f.avail;                        // deflate_slow's last literal (deflate.ts:1172)
+    }
 }
 // bits of word wi that belong to positions [a, b)
 __device__ __forceinline__ uint64_t lz_range(int wi, int a, int b) {
@@ -2123,7 +2138,7 @@ __global__ __launch_bounds__(256) void k_fz_match(DeflateArgs A) {
     const GLB uint64_t* I = (const GLB uint64_t*)A.lz_i + (q.rp >> 6);
     GLB uint64_t* rec = (GLB uint64_t*)A.rec_buf + q.rp;
     const int nice = c_config[A.level][2], chain = c_config[A.level][3];
-    for (int p = q.g + (int)threadIdx.x; p < q.h; p += 256) {
+    for (int p = q.g + (int)threadIdx.x; p < q.h; p += (int)blockDim.x) {
         uint32_t r = 0;
         if (q.n - p >= MIN_MATCH)
             r = p + MIN_LOOKAHEAD <= q.n ? fz_search(in, pv, I, p, chain, nice) : fz_tail(in, pv, I, q.n, p, chain, nice);
@@ -2132,8 +2147,7 @@ __global__ __launch_bounds__(256) void k_fz_match(DeflateArgs A) {
 }
 // one deflate_fast step at s (deflate.ts:974-1033): its symbol, the positions it inserts
 // (I.set), the next step position; *iin: the positions inside its match are inserted
-__device__ __forceinline__ uint32_t fz_step(int& s, uint32_t r, const GLB uint8_t* in, int n, int max_ins, BitW& I,
-                                            bool& iin) {
+__device__ __forceinline__ uint32_t fz_step(int& s, uint32_t r, uint32_t lit, int n, int max_ins, BitW& I, bool& iin) {
     const int lookahead = n - s;
     if (lookahead >= MIN_MATCH) I.set(s);
     const int len = (int)(r >> 16);
@@ -2146,9 +2160,8 @@ __device__ __forceinline__ uint32_t fz_step(int& s, uint32_t r, const GLB uint8_
         return sym;
     }
     iin = false;
-    const uint32_t sym = (uint32_t)in[s] | LZ_SYM;
     s += 1;
-    return sym;
+    return lit | LZ_SYM;
 }
 __global__ __launch_bounds__(LZ_THREADS) void k_fz_spec(DeflateArgs A) {
     const uint32_t seg = blockIdx.x * LZ_THREADS + threadIdx.x;
@@ -2163,11 +2176,28 @@ __global__ __launch_bounds__(LZ_THREADS) void k_fz_spec(DeflateArgs A) {
     BitW I{(GLB uint64_t*)A.lz_i1 + (q.rp >> 6), q.g >> 6, 0};
     int s = q.g;
     bool iin = false;
+    // records and bytes of 4 positions per round trip: a literal moves on by one
+    int wb0 = -0x40000000;
+    uint32_t r0 = 0, r1 = 0, r2 = 0, r3 = 0, lw = 0;
     while (s < q.h) {
         const int p = s;
-        const uint32_t r = (uint32_t)rec[p];
+        if (p - wb0 >= 4) {
+            wb0 = p;
+            const int last = q.n - 1;
+            r0 = (uint32_t)rec[p];
+            r1 = (uint32_t)rec[p + 1 < last ? p + 1 : last];
+            r2 = (uint32_t)rec[p + 2 < last ? p + 2 : last];
+            r3 = (uint32_t)rec[p + 3 < last ? p + 3 : last];
+            if (p + 4 <= q.n) __builtin_memcpy(&lw, (const uint8_t*)(in + p), 4);
+            else {
+                lw = 0;
+                for (int i = 0; p + i < q.n; ++i) lw |= (uint32_t)in[p + i] << (8 * i);
+            }
+        }
+        const int o = p - wb0;
+        const uint32_t r = o == 0 ? r0 : o == 1 ? r1 : o == 2 ? r2 : r3;
         V.set(p);
-        const uint32_t sym = fz_step(s, r, in, q.n, max_ins, I, iin);
+        const uint32_t sym = fz_step(s, r, (lw >> (8 * o)) & 255u, q.n, max_ins, I, iin);
         w[p] = (uint64_t)sym << 32;
     }
     // (interior bits past h belong to the next segment's join: BitW.end stops at h)
@@ -2197,7 +2227,7 @@ __device__ int fz_join_run(const DeflateArgs& A, const LzSeg& q, int& s, bool& c
         const int p = s;
         const uint32_t r = (uint32_t)rec[p];
         E.set(p);
-        s2[p] = fz_step(s, r, in, q.n, max_ins, I, cin);
+        s2[p] = fz_step(s, r, in[p], q.n, max_ins, I, cin);
     }
     if (c == q.h) I.acc &= (I.wc << 6) + 64 <= q.h ? ~0ull : lz_range(I.wc, q.g, q.h);
     E.end(q.g, c);
@@ -2215,29 +2245,40 @@ __global__ __launch_bounds__(LZ_THREADS) void k_fz_join(DeflateArgs A) {
     A.lz_c[seg] = (uint32_t)fz_join_run(A, q, s, cin, c_config[A.level][1]);
     A.lz_carry[seg] = (uint64_t)(uint32_t)s | ((uint64_t)(cin ? 1u : 0u) << 32);
 }
-__global__ __launch_bounds__(LZ_THREADS) void k_fz_fix(DeflateArgs A) {
-    const uint32_t k = blockIdx.x * LZ_THREADS + threadIdx.x;
+// one wave per stream: the boundaries whose join crossed its segment are found 64 at a time;
+// from each, lane 0 redoes the following joins until one meets its segment's parse
+__global__ __launch_bounds__(64) void k_fz_fix(DeflateArgs A) {
+    const uint32_t k = blockIdx.x, lane = threadIdx.x;
     if (k >= A.n || A.rp0[k] == ~0ull || !(A.lz_act[k] & 1u)) return;
     const uint32_t base = A.lz_sg0[k], K = A.lz_sg0[k + 1] - base;
     const int max_ins = c_config[A.level][1];
-    bool ok = true;
-    int s = 0;
-    bool cin = false;
-    for (uint32_t j = 1; j < K; ++j) {
-        const LzSeg q = lz_seg(A, base + j);
-        if (ok) {
-            if ((int)A.lz_c[base + j] < q.h) continue;
-            const uint64_t e = A.lz_carry[base + j];
-            s = (int)(uint32_t)e;
-            cin = (e >> 32) != 0;
-            ok = false;
-            continue;
+    uint32_t j = 1;
+    while (j < K) {
+        uint32_t found = K;
+        for (; j < K; j += 64) {
+            const uint32_t jj = j + lane;
+            const bool un = jj < K && (int)A.lz_c[base + jj] >= lz_seg(A, base + jj).h;
+            const uint64_t m = __ballot(un);
+            if (m) { found = j + (uint32_t)__builtin_ctzll(m); break; }
         }
-        const int c = fz_join_run(A, q, s, cin, max_ins);
-        A.lz_c[base + j] = (uint32_t)c;
-        if (c < q.h) ok = true;
+        if (found >= K) break;
+        uint32_t next = K;
+        if (lane == 0) {
+            const uint64_t e = A.lz_carry[base + found];
+            int s = (int)(uint32_t)e;
+            bool cin = (e >> 32) != 0;
+            uint32_t jj = found + 1;
+            for (; jj < K; ++jj) {
+                const LzSeg q = lz_seg(A, base + jj);
+                const int c = fz_join_run(A, q, s, cin, max_ins);
+                A.lz_c[base + jj] = (uint32_t)c;
+                if (c < q.h) break;
+            }
+            next = jj + 1;
+        }
+        j = __shfl(next, 0);
     }
-    A.lz_fin[k] = 0;                                            // deflate_fast leaves no pending literal
+    if (lane == 0) A.lz_fin[k] = 0;                             // deflate_fast leaves no pending literal
 }
 // the next I of each segment ([g, c) from the join, [c, h) from its own parse); a stream
 // whose I changed anywhere goes another round
@@ -2654,10 +2695,10 @@ void launch_deflate(const DeflateArgs& a, hipStream_t st, hipStream_t side, hipE
                 (void)hipMemsetAsync(a.lz_act, 0, (size_t)a.n * 4, st);
                 hipLaunchKernelGGL(k_fz_init, dim3((a.nlseg + 255) / 256), dim3(256), 0, st, a);
                 for (uint32_t round = 0; round < kFzRounds; ++round) {
-                    hipLaunchKernelGGL(k_fz_match, dim3(a.nlseg), dim3(256), 0, st, a);
+                    hipLaunchKernelGGL(k_fz_match, dim3(a.nlseg), dim3(a.lz_shift >= 8 ? 256 : 1u << a.lz_shift), 0, st, a);
                     hipLaunchKernelGGL(k_fz_spec, gseg, dim3(LZ_THREADS), 0, st, a);
                     hipLaunchKernelGGL(k_fz_join, gseg, dim3(LZ_THREADS), 0, st, a);
-                    hipLaunchKernelGGL(k_fz_fix, gstr, dim3(LZ_THREADS), 0, st, a);
+                    hipLaunchKernelGGL(k_fz_fix, dim3(a.n), dim3(64), 0, st, a);
                     hipLaunchKernelGGL(k_fz_merge, gseg, dim3(LZ_THREADS), 0, st, a);
                     (void)hipMemsetAsync(a.lz_nact, 0, 4, st);
                     hipLaunchKernelGGL(k_fz_roll, dim3((a.n + 255) / 256), dim3(256), 0, st, a);
@@ -2669,7 +2710,7 @@ void launch_deflate(const DeflateArgs& a, hipStream_t st, hipStream_t side, hipE
             } else {
                 hipLaunchKernelGGL(k_lz_spec, gseg, dim3(LZ_THREADS), 0, st, a);
                 hipLaunchKernelGGL(k_lz_join, gseg, dim3(LZ_THREADS), 0, st, a);
-                hipLaunchKernelGGL(k_lz_fix, gstr, dim3(LZ_THREADS), 0, st, a);
+                hipLaunchKernelGGL(k_lz_fix, dim3(a.n), dim3(64), 0, st, a);
             }
             hipLaunchKernelGGL(k_lz_count, gseg, dim3(LZ_THREADS), 0, st, a);
             hipLaunchKernelGGL(k_lz_scan, gstr, dim3(LZ_THREADS), 0, st, a);

@@ -797,6 +797,7 @@ int sdz_deflate_batch_device(const uint8_t* in, const uint64_t* in_off, const ui
             if (on_path(i)) tot += len[i];
         lz_shift = 9;
         while (lz_shift < 12 && (tot >> (lz_shift + 1)) >= 65536) ++lz_shift;
+        if (level <= 3) lz_shift = std::max(7u, lz_shift - 2);   // deflate_fast: its state is the position alone
         if (const char* e = getenv("SDZ_LZ_SHIFT"))            // tests: segment size 2^6 .. 2^16
             lz_shift = (uint32_t)std::min(16, std::max(6, atoi(e)));
     }

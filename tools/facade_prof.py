@@ -20,7 +20,10 @@ def main():
     cases = [("inflate", lambda: sdz.inflate(comp))]
     for lv in (1, 4, 6, 9):
         cases.append(("deflate_L%d" % lv, lambda lv=lv: sdz.deflate(text, {"level": lv})))
+    only = sys.argv[2].split(",") if len(sys.argv) > 2 else None
     for name, f in cases:
+        if only and name not in only:
+            continue
         f()
         ts = []
         for _ in range(reps):
