@@ -2126,13 +2126,29 @@ __global__ __launch_bounds__(256) void k_fz_init(DeflateArgs A) {     // I = eve
     const LzSeg q = lz_seg(A, seg);
     GLB uint64_t* I = (GLB uint64_t*)A.lz_i + (q.rp >> 6);
     for (int wi = q.g >> 6; wi <= ((q.h - 1) >> 6); ++wi) I[wi] = lz_range(wi, q.g, q.n - MIN_MATCH + 1);
+    A.fz_rc[seg] = 0; A.fz_chg[seg] = 0; A.fz_fx[seg] = 0;
     if (q.j == 0) A.lz_act[q.k] = 1u;
 }
+// A round recomputes only what the last round's changes of I can reach: a segment's
+// searches read I over the 32 KiB before it, its parse reads its own records, a join its own
+// and the previous segment's parse.
 __global__ __launch_bounds__(256) void k_fz_match(DeflateArgs A) {
+    __shared__ int any;
     const uint32_t seg = blockIdx.x;
     if (seg >= A.nlseg) return;
     const LzSeg q = lz_seg(A, seg);
     if (!(A.lz_act[q.k] & 1u)) return;
+    if (A.lz_round > 1) {
+        if (threadIdx.x == 0) any = 0;
+        __syncthreads();
+        const uint32_t w = ((uint32_t)(W_SIZE + MAX_MATCH) >> A.lz_shift) + 1u;
+        const uint32_t j0 = q.j > w ? q.j - w : 0u;
+        for (uint32_t jj = j0 + threadIdx.x; jj <= q.j; jj += blockDim.x)
+            if (A.fz_chg[seg - q.j + jj] == A.lz_round - 1) any = 1;
+        __syncthreads();
+        if (!any) return;
+    }
+    if (threadIdx.x == 0) A.fz_rc[seg] = A.lz_round;
     const GLB uint8_t* in = (const GLB uint8_t*)(A.in + A.in_off[q.k]);
     const GLB uint16_t* pv = (const GLB uint16_t*)A.pv_buf + q.rp;
     const GLB uint64_t* I = (const GLB uint64_t*)A.lz_i + (q.rp >> 6);
@@ -2167,7 +2183,7 @@ __global__ __launch_bounds__(LZ_THREADS) void k_fz_spec(DeflateArgs A) {
     const uint32_t seg = blockIdx.x * LZ_THREADS + threadIdx.x;
     if (seg >= A.nlseg) return;
     const LzSeg q = lz_seg(A, seg);
-    if (!(A.lz_act[q.k] & 1u)) return;
+    if (!(A.lz_act[q.k] & 1u) || A.fz_rc[seg] != A.lz_round) return;
     const GLB uint8_t* in = (const GLB uint8_t*)(A.in + A.in_off[q.k]);
     const GLB uint64_t* rec = (const GLB uint64_t*)A.rec_buf + q.rp;
     GLB uint64_t* w = (GLB uint64_t*)A.lz_w + q.rp;
@@ -2239,6 +2255,7 @@ __global__ __launch_bounds__(LZ_THREADS) void k_fz_join(DeflateArgs A) {
     if (seg >= A.nlseg) return;
     const LzSeg q = lz_seg(A, seg);
     if (q.j == 0 || !(A.lz_act[q.k] & 1u)) return;
+    if (A.fz_rc[seg] != A.lz_round && A.fz_rc[seg - 1] != A.lz_round) return;
     const uint64_t e = A.lz_end[seg - 1];
     int s = (int)(uint32_t)e;
     bool cin = (e >> 32) != 0;
@@ -2272,6 +2289,7 @@ __global__ __launch_bounds__(64) void k_fz_fix(DeflateArgs A) {
                 const LzSeg q = lz_seg(A, base + jj);
                 const int c = fz_join_run(A, q, s, cin, max_ins);
                 A.lz_c[base + jj] = (uint32_t)c;
+                A.fz_fx[base + jj] = A.lz_round;
                 if (c < q.h) break;
             }
             next = jj + 1;
@@ -2287,6 +2305,8 @@ __global__ __launch_bounds__(LZ_THREADS) void k_fz_merge(DeflateArgs A) {
     if (seg >= A.nlseg) return;
     const LzSeg q = lz_seg(A, seg);
     if (!(A.lz_act[q.k] & 1u)) return;
+    if (A.fz_rc[seg] != A.lz_round && (q.j == 0 || A.fz_rc[seg - 1] != A.lz_round) && A.fz_fx[seg] != A.lz_round)
+        return;
     const int c = (int)A.lz_c[seg];
     GLB uint64_t* I = (GLB uint64_t*)A.lz_i + (q.rp >> 6);
     const GLB uint64_t* i1 = (const GLB uint64_t*)A.lz_i1 + (q.rp >> 6);
@@ -2297,7 +2317,10 @@ __global__ __launch_bounds__(LZ_THREADS) void k_fz_merge(DeflateArgs A) {
         const uint64_t nw = ((m2 ? i2[wi] : 0ull) & m2) | (i1[wi] & m1);
         if (nw != I[wi]) { changed = true; I[wi] = nw; }
     }
-    if (changed) atomicOr(&A.lz_act[q.k], 2u);
+    if (changed) {
+        A.fz_chg[seg] = A.lz_round;
+        atomicOr(&A.lz_act[q.k], 2u);
+    }
 }
 __global__ __launch_bounds__(256) void k_fz_roll(DeflateArgs A) {
     const uint32_t k = blockIdx.x * 256 + threadIdx.x;
@@ -2694,14 +2717,16 @@ void launch_deflate(const DeflateArgs& a, hipStream_t st, hipStream_t side, hipE
                 // streams still moving after each (one small copy + sync per round)
                 (void)hipMemsetAsync(a.lz_act, 0, (size_t)a.n * 4, st);
                 hipLaunchKernelGGL(k_fz_init, dim3((a.nlseg + 255) / 256), dim3(256), 0, st, a);
-                for (uint32_t round = 0; round < kFzRounds; ++round) {
-                    hipLaunchKernelGGL(k_fz_match, dim3(a.nlseg), dim3(a.lz_shift >= 8 ? 256 : 1u << a.lz_shift), 0, st, a);
-                    hipLaunchKernelGGL(k_fz_spec, gseg, dim3(LZ_THREADS), 0, st, a);
-                    hipLaunchKernelGGL(k_fz_join, gseg, dim3(LZ_THREADS), 0, st, a);
-                    hipLaunchKernelGGL(k_fz_fix, dim3(a.n), dim3(64), 0, st, a);
-                    hipLaunchKernelGGL(k_fz_merge, gseg, dim3(LZ_THREADS), 0, st, a);
+                for (uint32_t round = 1; round <= kFzRounds; ++round) {
+                    DeflateArgs r = a;
+                    r.lz_round = round;
+                    hipLaunchKernelGGL(k_fz_match, dim3(a.nlseg), dim3(a.lz_shift >= 8 ? 256 : 1u << a.lz_shift), 0, st, r);
+                    hipLaunchKernelGGL(k_fz_spec, gseg, dim3(LZ_THREADS), 0, st, r);
+                    hipLaunchKernelGGL(k_fz_join, gseg, dim3(LZ_THREADS), 0, st, r);
+                    hipLaunchKernelGGL(k_fz_fix, dim3(a.n), dim3(64), 0, st, r);
+                    hipLaunchKernelGGL(k_fz_merge, gseg, dim3(LZ_THREADS), 0, st, r);
                     (void)hipMemsetAsync(a.lz_nact, 0, 4, st);
-                    hipLaunchKernelGGL(k_fz_roll, dim3((a.n + 255) / 256), dim3(256), 0, st, a);
+                    hipLaunchKernelGGL(k_fz_roll, dim3((a.n + 255) / 256), dim3(256), 0, st, r);
                     uint32_t moving = 0;
                     if (hipMemcpyAsync(&moving, a.lz_nact, 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
                         hipStreamSynchronize(st) != hipSuccess || moving == 0)

@@ -133,6 +133,10 @@ struct DeflateArgs {
     uint64_t* lz_i2;             //   joins / fixes
     uint32_t* lz_act;            // per stream: bit 0 still iterating, bit 1 changed this round
     uint32_t* lz_nact;           // one counter: streams still iterating after a round
+    uint32_t lz_round;           // the round (from 1); per segment, the last round that
+    uint32_t* fz_rc;             //   recomputed its records,
+    uint32_t* fz_chg;            //   changed its part of I,
+    uint32_t* fz_fx;             //   had its join redone by k_fz_fix
     int32_t* cks;                // n input checksums (record path)
     uint32_t fast;               // set by launch_deflate: k_deflate redoes flagged streams only
     const uint8_t* dict;         // preset dictionary (deflateSetDictionary), may be null

@@ -779,25 +779,38 @@ int sdz_deflate_batch_device(const uint8_t* in, const uint64_t* in_off, const ui
     // parse (k_deflate.hip).  The host plans it from the input sizes: each stream's record /
     // link range, block slots, chain units and match segments, cut into sub-batches that
     // fit half of free HBM.  Streams off the path run the serial kernel.
-    // levels 1-3 take it with the segment-parallel parse only (their chains need its rounds)
+    // Levels 1-3 take it with the segment-parallel parse only (their chains need its rounds of
+    // inserted positions, k_deflate.hip): for streams over 256 KiB, or batches up to 64 MiB --
+    // a large batch of short streams keeps every lane of the serial kernel busy, which beats
+    // the rounds (C3 shape at L1: 0.80 s serial, 6.8 s in rounds).
+    const bool fastlv = level <= 3;
     const bool lz_on = !getenv("SDZ_SERIAL_PARSE");
-    const bool recpath = (level >= 4 || lz_on) && !dict;
+    const bool recpath = (!fastlv || lz_on) && !dict;
     std::vector<uint64_t> len(recpath ? n : 0);
     if (recpath) {
         HIPCHK(hipMemcpyAsync(len.data(), in_len, (size_t)n * 8, hipMemcpyDeviceToHost, s));
         HIPCHK(hipStreamSynchronize(s));
     }
-    auto on_path = [&](uint32_t i) { return recpath && len[i] > 0 && len[i] <= kDeflateRecMax; };
-    // segment-parallel parse (k_lz_*): segments of 2^lz_shift positions, shorter ones when the
-    // batch is small so a single long stream still spreads over many lanes
+    uint64_t tot_all = 0;
+    for (uint32_t i = 0; i < (recpath ? n : 0); ++i)
+        if (len[i] > 0 && len[i] <= kDeflateRecMax) tot_all += len[i];
+    auto on_path = [&](uint32_t i) {
+        if (!recpath || len[i] == 0 || len[i] > kDeflateRecMax) return false;
+        return !fastlv || len[i] > (256u << 10) || tot_all <= (64ull << 20);
+    };
+    // the parse of levels 4-9: segment-parallel (k_lz_*, segments of 2^lz_shift positions,
+    // shorter when the batch is small so one long stream still spreads over many lanes) unless
+    // a lane per stream finishes first -- it runs as long as the longest stream (~0.6 us per
+    // byte), the segments as long as the whole batch (~13.5 ms per GiB): C3 38.6 vs 58 ms
     uint32_t lz_shift = 0;
     if (recpath && lz_on) {
-        uint64_t tot = 0;
+        uint64_t tot = 0, mx = 0;
         for (uint32_t i = 0; i < n; ++i)
-            if (on_path(i)) tot += len[i];
+            if (on_path(i)) { tot += len[i]; mx = std::max<uint64_t>(mx, len[i]); }
         lz_shift = 9;
         while (lz_shift < 12 && (tot >> (lz_shift + 1)) >= 65536) ++lz_shift;
-        if (level <= 3) lz_shift = std::max(7u, lz_shift - 2);   // deflate_fast: its state is the position alone
+        if (fastlv) lz_shift = std::max(7u, lz_shift - 2);      // deflate_fast: its state is the position alone
+        else if (tot >= (mx << 15)) lz_shift = 0;
         if (const char* e = getenv("SDZ_LZ_SHIFT"))            // tests: segment size 2^6 .. 2^16
             lz_shift = (uint32_t)std::min(16, std::max(6, atoi(e)));
     }
@@ -807,7 +820,7 @@ int sdz_deflate_batch_device(const uint8_t* in, const uint64_t* in_off, const ui
     auto rec_cost = [&](uint32_t i) -> uint64_t {
         if (!on_path(i)) return 0;
         const uint64_t p = (len[i] + 63) & ~63ull;
-        return p * kPosBytes + lz_segs(len[i]) * 32 + deflate_rec_blocks(len[i]) * FB_SLOT_BYTES + 64;
+        return p * kPosBytes + lz_segs(len[i]) * 44 + deflate_rec_blocks(len[i]) * FB_SLOT_BYTES + 64;
     };
     const uint64_t budget = std::max<uint64_t>(1ull << 30, mem_free / 2);
     // sub-batches [cb[j], cb[j + 1])
@@ -838,7 +851,7 @@ int sdz_deflate_batch_device(const uint8_t* in, const uint64_t* in_off, const ui
         }
         const uint64_t m = cb[j + 1] - cb[j];
         const uint64_t b = sb + pos * kPosBytes + blk * FB_SLOT_BYTES + m * 16 + 8 * (m + 1) + 4 * (m + 1) + 4 * units +
-                           (lz_shift ? 4 * (m + 1) + 8 * m + 32 * segs + 20 * 256 : 0) + 4096;
+                           (lz_shift ? 4 * (m + 1) + 8 * m + 44 * segs + 24 * 256 : 0) + 4096;
         pool_bytes = std::max(pool_bytes, b);
     }
     void* state = nullptr;
@@ -942,6 +955,9 @@ int sdz_deflate_batch_device(const uint8_t* in, const uint64_t* in_off, const ui
                     a.lz_i2 = (uint64_t*)take((size_t)pos / 8);
                     a.lz_act = (uint32_t*)take((size_t)m * 4);
                     a.lz_nact = (uint32_t*)take(4);
+                    a.fz_rc = (uint32_t*)take((size_t)nlseg * 4);
+                    a.fz_chg = (uint32_t*)take((size_t)nlseg * 4);
+                    a.fz_fx = (uint32_t*)take((size_t)nlseg * 4);
                 }
             }
             if (o > pool_bytes) return fail(SDZ_API_OOM, "deflate: record plan exceeds its pool");
