@@ -1181,6 +1181,9 @@ __global__ __launch_bounds__(64 * CH_WAVES) void k_dfl_chain(DeflateArgs A) {
 #ifndef PM_REFILL
 #define PM_REFILL 8                                     // idle lanes that trigger a refill
 #endif
+#ifndef PM_LAZYW4
+#define PM_LAZYW4 1
+#endif
 #define PM_WINB (W_SIZE + PM_SEG + MAX_MATCH + 16)     // staged window bytes
 #define PM_PV (W_SIZE + PM_SEG)                         // staged links
 // record word of position p: the full-chain result (len << 16 | dist) in the low half, the
@@ -1261,7 +1264,7 @@ __global__ __launch_bounds__(PM_THREADS) void k_dfl_match(DeflateArgs A) {
     // link of a step does not wait on the previous one).  cur, nxt, bpos, qpos, limit and sp
     // (the position itself) are relative to ws; p is absolute.
     int p = s0, sp = 0, cur = 0, nxt = 0, best = 0, bpos = 0, qbest = 0, qpos = 0, chain = 0, limit = 0;
-    uint32_t s4 = 0;
+    uint32_t s4 = 0, sbv = 0;
     for (;;) {
         // Idle lanes store their records and take the next positions once PM_REFILL lanes
         // are idle (or all are): the refill and the record store then run once per several
@@ -1293,6 +1296,9 @@ __global__ __launch_bounds__(PM_THREADS) void k_dfl_match(DeflateArgs A) {
                     sp = p - ws;
                     cur = pvl[sp];                              // hash_head
                     best = MIN_MATCH - 1; bpos = 0; qbest = -1;
+#if PM_LAZYW4
+                    sbv = win[sp + best];
+#endif
                     limit = (p > MAX_DIST ? p - MAX_DIST : 0) - ws;   // >= 0
                     s4 = pm_w4(win, (uint32_t)sp);
                     const bool search = cur != 0 && sp - cur <= MAX_DIST;  // deflate.ts:1092
@@ -1312,11 +1318,24 @@ __global__ __launch_bounds__(PM_THREADS) void k_dfl_match(DeflateArgs A) {
         const bool l2 = live && go1;                          // c2 is walked (unless nice at c1)
         const uint32_t c1 = (uint32_t)(live ? cur : sp), c2 = (uint32_t)(l2 ? nxt : sp);
         const int c3 = pvl[c2];
+#if PM_LAZYW4
+        // the 4-byte head compare only for candidates that pass the byte at best: once best
+        // has grown most candidates fail there, and the skipped loads are random window reads
+        // (LDS bank conflicts).  The byte of the position at best is kept in a register.
+        const uint32_t sb = sbv, wb1 = win[c1 + best], wb2 = win[c2 + best];
+        const bool go2 = c3 > limit && chain > 2;            // ... and after c2
+        const int c4 = pvl[l2 && go2 ? c3 : sp];
+        const bool cand1 = live && wb1 == sb, cand2 = l2 && wb2 == sb;
+        uint32_t x1 = 0, x2 = 0;
+        if (cand1) x1 = pm_w4(win, c1) ^ s4;
+        if (cand2) x2 = pm_w4(win, c2) ^ s4;
+#else
         const uint32_t sb = win[sp + best], wb1 = win[c1 + best], wb2 = win[c2 + best];
         uint32_t x1 = pm_w4(win, c1) ^ s4, x2 = pm_w4(win, c2) ^ s4;
         const bool go2 = c3 > limit && chain > 2;            // ... and after c2
         const int c4 = pvl[l2 && go2 ? c3 : sp];
         const bool cand1 = live && wb1 == sb, cand2 = l2 && wb2 == sb;
+#endif
         int len1 = x1 ? (int)(__builtin_ctz(x1) >> 3) : 4;
         int len2 = x2 ? (int)(__builtin_ctz(x2) >> 3) : 4;
         bool more1 = cand1 && x1 == 0, more2 = cand2 && x2 == 0;
@@ -1349,6 +1368,9 @@ __global__ __launch_bounds__(PM_THREADS) void k_dfl_match(DeflateArgs A) {
         qbest = cap2 ? best : qbest;
         qpos = cap2 ? bpos : qpos;
         const bool fin = live && (!w2 || (upd2 && len2 >= nice) || !go2);
+#if PM_LAZYW4
+        if (upd1 || upd2) sbv = win[sp + best];
+#endif
         cur = c3;
         nxt = c4;
         pend = pend || fin;                                   // stored at the next refill

@@ -59,7 +59,38 @@ export interface InflateBatchRecord {
 	data: Uint8Array;
 }
 
-export declare function inflateBatch(streams: BufferSource[], outCaps?: number[], format?: 0 | 1 | 2): InflateBatchRecord[];
-export declare function deflateBatch(streams: BufferSource[],
-	options?: { level?: number; format?: "raw" | "deflate" | "gzip"; mtime?: number }): { status: string; checksum: number; data: Uint8Array }[];
+/** Multi-GPU stats (sdz_multi_stats): present on the result array when `devices` was given. */
+export interface MultiStats {
+	wallMs: number;
+	computeMs: number;
+	/** record all-gather, timed apart from compute */
+	gatherMs: number;
+	/** true: ncclAllGather over distinct devices; false: loopback (a device listed twice) */
+	rccl: boolean;
+	/** one entry per device of the list, in list order (LPT shards) */
+	shards: { streams: number; bytesIn: number; bytesOut: number; kernelMs: number }[];
+}
+
+export interface InflateBatchOptions {
+	/** output slot per stream (default max(64 KiB, 8 x input)) */
+	outCaps?: number[];
+	/** 0 raw, 1 zlib/gzip, 2 auto-detect as inflate() (default 2) */
+	format?: 0 | 1 | 2;
+	dictionary?: BufferSource;
+	/** GPUs to shard over (LPT by size, one host thread per GPU, records gathered over RCCL) */
+	devices?: number[];
+}
+export interface DeflateBatchOptions {
+	level?: number;
+	format?: "raw" | "deflate" | "gzip";
+	fileName?: string;
+	mtime?: number;
+	dictionary?: BufferSource;
+	devices?: number[];
+}
+
+export declare function inflateBatch(streams: BufferSource[], options?: InflateBatchOptions | number[],
+	format?: 0 | 1 | 2): InflateBatchRecord[] & { stats?: MultiStats };
+export declare function deflateBatch(streams: BufferSource[], options?: DeflateBatchOptions):
+	{ status: string; checksum: number; data: Uint8Array }[] & { stats?: MultiStats };
 export declare function deviceCount(): number;
