@@ -359,9 +359,18 @@ __device__ __forceinline__ bool map_all(const uint8_t* fmap, bool act, uint32_t 
     }
     return miss == 0;
 }
+#ifndef RS_WAKE
+#define RS_WAKE 0                     // s_wakeup after each publish: sleeping waves poll at once
+#endif
+__device__ __forceinline__ void rs_wake() {
+#if RS_WAKE
+    asm volatile("s_wakeup" ::: "memory");
+#endif
+}
 __device__ __forceinline__ void publish_wf(uint32_t* wf, uint32_t v1) {
     lds_release();
     if ((threadIdx.x & 63u) == 0) lds_put(wf, v1);
+    rs_wake();
 }
 
 __global__ __launch_bounds__(RS_THREADS) __attribute__((amdgpu_waves_per_eu(RS_WPE, RS_WPE))) void k_inflate_resolve(InflateArgs A, uint32_t round) {
@@ -476,6 +485,7 @@ __global__ __launch_bounds__(RS_THREADS) __attribute__((amdgpu_waves_per_eu(RS_W
         if (bad) break;
         if (lane == 0) __hip_atomic_store(&chain, ((uint64_t)g << 32) | (Sg + T), __ATOMIC_RELAXED,
                                           __HIP_MEMORY_SCOPE_WORKGROUP);
+        rs_wake();
         RS_TICK(1);
 
         // 2. copy rounds
@@ -619,6 +629,7 @@ __global__ __launch_bounds__(RS_THREADS) __attribute__((amdgpu_waves_per_eu(RS_W
             gm -= gm >= 65521u ? 65521u : 0u;
             lds_release();                                // our ring reads are complete
             if (lane == 0) lds_put(&wwb, WB);
+            rs_wake();
         }
     }
     if (timed) for (int k = 0; k < 8; ++k) atomicAdd(&A.dbg[k], tacc[k]);

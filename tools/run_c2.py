@@ -45,7 +45,7 @@ def main():
         L.sdz_sync(None)
         drec = (sdz.DeflateRecord * args.streams).from_buffer_copy(
             b.d_rec.download(args.streams * ctypes.sizeof(sdz.DeflateRecord)))
-        r = inflate_distinct(sdz, L, b, drec, text, offs, 65536, args.steps, lambda: None, lambda x: x, 1)
+        r, _ = inflate_distinct(sdz, L, b, drec, text, offs, 65536, args.steps, lambda: None, lambda x: x, 1)
         print("distinct inflate: kernel %.3f ms %s, %.1f GB/s out, parity %s"
               % (r["roofline"]["kernel_ms"], r["roofline"]["kernels_ms"],
                  r["config"]["bytes_out_per_gpu"] / r["roofline"]["kernel_ms"] / 1e6, r["parity"]), flush=True)
