@@ -69,7 +69,7 @@ struct DSlab {                      // per-stream HBM state
 
 #define SLAB_BYTES ((sizeof(DSlab) + 255) & ~(uint64_t)255)
 
-// record path (levels 4-9, inputs up to kDeflateRecMax): per stream a FStream header in its
+// record path (inputs up to kDeflateRecMax): per stream a FStream header in its
 // slab, and per block a slot (FBlock + code table + header words) in the block area; records,
 // links and symbols in the record buffers (positions from rp0[k]).
 #define PM_TAIL (MAX_MATCH + MIN_MATCH + 1)       // last positions: searched by k_dfl_tail
@@ -1265,6 +1265,7 @@ __global__ __launch_bounds__(PM_THREADS) void k_dfl_match(DeflateArgs A) {
     // (the position itself) are relative to ws; p is absolute.
     int p = s0, sp = 0, cur = 0, nxt = 0, best = 0, bpos = 0, qbest = 0, qpos = 0, chain = 0, limit = 0;
     uint32_t s4 = 0, sbv = 0;
+    (void)sbv;
     for (;;) {
         // Idle lanes store their records and take the next positions once PM_REFILL lanes
         // are idle (or all are): the refill and the record store then run once per several
@@ -1414,6 +1415,12 @@ __device__ uint32_t win_byte(const GLB uint8_t* in, int64_t n, int64_t off, int6
 // grow with P, so every visited P has the offset this loop finds)
 __device__ __forceinline__ int64_t slide_off(int64_t n, int64_t P) {
     int64_t off = 0;
+    // the slides with the window's end still inside the input happen at P - off >= 65275
+    // (fe - P < MIN_LOOKAHEAD with fe = off + 64 Ki): taken in one go, the loop does the rest
+    if (P >= WINDOW_SIZE - MIN_LOOKAHEAD + 1 && n >= WINDOW_SIZE) {
+        const int64_t e = (P - (WINDOW_SIZE - MIN_LOOKAHEAD + 1)) / W_SIZE + 1, emid = (n - WINDOW_SIZE) / W_SIZE + 1;
+        off = (int64_t)W_SIZE * (e < emid ? e : emid);
+    }
     for (;;) {
         const int64_t fe = n < off + WINDOW_SIZE ? n : off + WINDOW_SIZE;
         if (fe - P < MIN_LOOKAHEAD && P - off >= WINDOW_SIZE - MIN_LOOKAHEAD) off += W_SIZE;

@@ -23,6 +23,11 @@ int hip_fail(hipError_t e, const char* what);
     } while (0)
 
 int ensure_device();
+// sdz_deflate_batch_device with the input lengths optionally known on the host
+int deflate_batch_device(const uint8_t* in, const uint64_t* in_off, const uint64_t* in_len, uint8_t* out,
+                         const uint64_t* out_off, const uint64_t* out_cap, sdz_deflate_record* rec, uint32_t n,
+                         int32_t level, int32_t format, const uint8_t* fname, uint32_t fname_len, uint32_t mtime,
+                         const uint8_t* dict, uint32_t dict_len, void* stream, const uint64_t* host_len);
 
 // Calls on one device are serialised (its pools and side stream are shared; recursive: a
 // host-batch call holds it around the *_device call it makes); calls on different devices
@@ -82,6 +87,7 @@ struct Pinned {
     int done(hipStream_t s);
 };
 extern Pinned g_pinned;
+extern Pinned g_plan_pinned;                      // the deflate plan's staging (beside a host batch's)
 
 }  // namespace rt
 }  // namespace sdz

@@ -37,6 +37,7 @@ namespace {
 
 constexpr uint32_t kDirectOut = 32;            // up to this many streams: outputs copied one by one
 constexpr uint64_t kPackInMax = 256ull << 20;  // inputs up to this size are packed (pinned, one copy)
+constexpr uint64_t kEagerOut = 4ull << 20;     // output slots up to this total come back with the records
 
 double now_ms() {
     return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
@@ -119,6 +120,7 @@ int host_shard(const uint8_t* const* in, const size_t* in_len, uint8_t* const* o
     }
     std::memcpy(P + pin_meta, meta.data(), meta.size() * 8);
     HIPCHK(hipMemcpyAsync(d_meta, P + pin_meta, meta.size() * 8, hipMemcpyHostToDevice, s));
+    if (int rc = g_pinned.done(s)) return rc;       // (the next get() waits for these copies)
     uint8_t* d_dict = nullptr;
     if (C.dict) {
         d_dict = B + o_dict;
@@ -133,13 +135,22 @@ int host_shard(const uint8_t* const* in, const size_t* in_len, uint8_t* const* o
     int rc = C.inflate
         ? sdz_inflate_batch_device(B + o_in, d_meta, d_meta + m, B + o_out, d_meta + 2 * (size_t)m, d_meta + 3 * (size_t)m,
                                    (sdz_inflate_record*)(B + o_rec), m, C.format, d_dict, (uint32_t)C.dict_len, s)
-        : sdz_deflate_batch_device(B + o_in, d_meta, d_meta + m, B + o_out, d_meta + 2 * (size_t)m, d_meta + 3 * (size_t)m,
-                                   (sdz_deflate_record*)(B + o_rec), m, C.level, C.format, C.fname, C.fname_len,
-                                   C.mtime, d_dict, (uint32_t)C.dict_len, s);
+        : rt::deflate_batch_device(B + o_in, d_meta, d_meta + m, B + o_out, d_meta + 2 * (size_t)m,
+                                   d_meta + 3 * (size_t)m, (sdz_deflate_record*)(B + o_rec), m, C.level, C.format,
+                                   C.fname, C.fname_len, C.mtime, d_dict, (uint32_t)C.dict_len, s, meta.data() + m);
     if (rc) return rc;
     HIPCHK(hipEventRecord(e1, s));
-    // records back (one copy), then the outputs
+    // records back (one copy), then the outputs; small output slots come back with the
+    // records, under the same wait (the drop-in's one-buffer calls)
     std::vector<uint8_t> recs((size_t)m * rsz);
+    const bool eager = !compact && to <= kEagerOut;
+    uint8_t* ebuf = nullptr;
+    if (eager && to) {
+        void* ep = nullptr;
+        if (int rc2 = g_pinned.get(al(to, 256), &ep)) return rc2;
+        ebuf = (uint8_t*)ep;
+        HIPCHK(hipMemcpyAsync(ebuf, B + o_out, to, hipMemcpyDeviceToHost, s));
+    }
     HIPCHK(hipMemcpyAsync(recs.data(), B + o_rec, recs.size(), hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
     HIPCHK(hipEventElapsedTime(&R.kernel_ms, e0, e1));
@@ -148,7 +159,13 @@ int host_shard(const uint8_t* const* in, const size_t* in_len, uint8_t* const* o
         const uint64_t len = C.inflate ? ((const sdz_inflate_record*)r)->out_len : ((const sdz_deflate_record*)r)->out_len;
         return std::min<uint64_t>(len, out_cap[R.order[k]]);
     };
-    if (!compact) {
+    if (eager) {
+        for (uint32_t k = 0; k < m; ++k) {
+            const uint64_t len = out_len_of(k);
+            R.bytes_out += len;
+            if (len && out[R.order[k]]) std::memcpy(out[R.order[k]], ebuf + meta[2 * (size_t)m + k], len);
+        }
+    } else if (!compact) {
         for (uint32_t k = 0; k < m; ++k) {
             const uint64_t len = out_len_of(k);
             R.bytes_out += len;

@@ -99,7 +99,7 @@ struct DeflateArgs {
     // record path (levels 4-9, inputs <= kDeflateRecMax; host plan, sdz_runtime.cpp): stream k
     // owns positions [rp0[k], rp0[k] + in_len) of the record and link buffers (rp0[k] = ~0: not
     // on the record path) and block slots [tb0[k], tb0[k + 1]); the match and chain kernels
-    // run over work-unit lists (k << 12 | unit)
+    // run over work-unit lists (k << kRecUnitShift | unit)
     uint64_t* rec_buf;           // match records, one per position (null: classic path only)
     uint16_t* pv_buf;            // hash chain links: distance to the previous same-hash position
     const uint64_t* rp0;         // n + 1 entries
@@ -158,8 +158,8 @@ void launch_fast_concat(const DeflateArgs& a, const uint32_t* tile0, const uint8
 // incremental Deflater (k_deflate_stream): fresh state; one append (finish 0) / finish (1)
 void launch_deflate_reset(uint8_t* state, uint32_t n, hipStream_t s);
 void launch_deflate_stream(const DeflateArgs& a, uint32_t finish, hipStream_t s);
-constexpr uint64_t kDeflateRecMax = 64ull << 20;   // longest input on the record path
-constexpr uint32_t kRecUnitShift = 12;              // work units: k << 12 | unit (unit < 4096)
+constexpr uint64_t kDeflateRecMax = 1ull << 30;    // longest input on the record path
+constexpr uint32_t kRecUnitShift = 16;              // work units: k << 16 | unit (k, unit < 65536)
 uint64_t deflate_rec_blocks(uint64_t len);          // block slots a record-path stream needs
 uint32_t deflate_chain_units(uint64_t len);         // its k_dfl_chain units
 uint32_t deflate_match_segs(uint64_t len);          // its k_dfl_match segments

@@ -26,6 +26,7 @@ thread_local std::string g_err;
 std::recursive_mutex g_dev_mu[kMaxDev];
 Pool g_host;
 Pinned g_pinned;
+Pinned g_plan_pinned;
 
 int fail(int code, const std::string& msg) {
     g_err = msg;
@@ -750,6 +751,17 @@ int sdz_deflate_batch_device(const uint8_t* in, const uint64_t* in_off, const ui
                              sdz_deflate_record* rec, uint32_t n, int32_t level, int32_t format,
                              const uint8_t* fname, uint32_t fname_len, uint32_t mtime,
                              const uint8_t* dict, uint32_t dict_len, void* stream) {
+    return rt::deflate_batch_device(in, in_off, in_len, out, out_off, out_cap, rec, n, level, format, fname, fname_len,
+                                    mtime, dict, dict_len, stream, nullptr);
+}
+}  // extern "C"
+
+// host_len (optional): the n input lengths on the host too (the host-buffer path knows
+// them), which spares the plan's device-to-host read and its wait
+int rt::deflate_batch_device(const uint8_t* in, const uint64_t* in_off, const uint64_t* in_len, uint8_t* out,
+                             const uint64_t* out_off, const uint64_t* out_cap, sdz_deflate_record* rec, uint32_t n,
+                             int32_t level, int32_t format, const uint8_t* fname, uint32_t fname_len, uint32_t mtime,
+                             const uint8_t* dict, uint32_t dict_len, void* stream, const uint64_t* host_len) {
     if (int rc = ensure_device()) return rc;
     if (n == 0) return SDZ_API_OK;
     if (level < 1 || level > 9) return fail(SDZ_API_BAD_ARG, "level must be between 1 and 9, inclusive");
@@ -774,7 +786,7 @@ int sdz_deflate_batch_device(const uint8_t* in, const uint64_t* in_off, const ui
         d_dictid = (int32_t*)((uint8_t*)tmp + kTmpDictId);
         launch_checksum_one(dict, dict_len, 0, 1, d_dictid, s);
     }
-    // Record path (levels 4-9, inputs up to kDeflateRecMax, no dictionary -- it moves the
+    // Record path (inputs up to kDeflateRecMax = 1 GiB, no dictionary -- it moves the
     // window): hash chains and match records per position found in parallel before the
     // parse (k_deflate.hip).  The host plans it from the input sizes: each stream's record /
     // link range, block slots, chain units and match segments, cut into sub-batches that
@@ -787,7 +799,9 @@ int sdz_deflate_batch_device(const uint8_t* in, const uint64_t* in_off, const ui
     const bool lz_on = !getenv("SDZ_SERIAL_PARSE");
     const bool recpath = (!fastlv || lz_on) && !dict;
     std::vector<uint64_t> len(recpath ? n : 0);
-    if (recpath) {
+    if (recpath && host_len) {
+        std::copy(host_len, host_len + n, len.begin());
+    } else if (recpath) {
         HIPCHK(hipMemcpyAsync(len.data(), in_len, (size_t)n * 8, hipMemcpyDeviceToHost, s));
         HIPCHK(hipStreamSynchronize(s));
     }
@@ -964,7 +978,7 @@ int sdz_deflate_batch_device(const uint8_t* in, const uint64_t* in_off, const ui
             // plan -> device through the pinned staging buffer (one copy, waited for below)
             const size_t pb = rp0.size() * 8 + tb0.size() * 4 + units.size() * 4 + lzs.size() * 4;
             void* pin = nullptr;
-            if (int rc = g_pinned.get(pb + 64, &pin)) return rc;
+            if (int rc = g_plan_pinned.get(pb + 64, &pin)) return rc;
             uint8_t* P = (uint8_t*)pin;
             std::memcpy(P, rp0.data(), rp0.size() * 8);
             std::memcpy(P + rp0.size() * 8, tb0.data(), tb0.size() * 4);
@@ -981,7 +995,7 @@ int sdz_deflate_batch_device(const uint8_t* in, const uint64_t* in_off, const ui
             a.cunit = d_units + nmseg; a.ncunit = (uint32_t)units.size() - nmseg;
             a.nbmax = nbmax;
             a.wide = m <= 256 ? 1u : 0u;                // few streams: the LDS-staged parse
-            if (int rc = g_pinned.done(s)) return rc;    // (the next get() waits for the plan copies)
+            if (int rc = g_plan_pinned.done(s)) return rc;   // (the next get() waits for the plan copies)
             launch_deflate(a, s, side ? side->s : nullptr, side ? side->ev : nullptr);
         } else {
             launch_deflate(a, s, nullptr, nullptr);
@@ -1000,6 +1014,7 @@ int sdz_deflate_batch_device(const uint8_t* in, const uint64_t* in_off, const ui
     HIPCHK(hipGetLastError());
     return SDZ_API_OK;
 }
+extern "C" {
 
 // ----------------------------------------------------------------- checksums
 

@@ -395,6 +395,27 @@ def test_deflate_segment_parse(monkeypatch, paradise, shift):
     assert [x["data"] for x in g] == [O.deflate(d, level=6) for d in inputs[:4]]
 
 
+def test_deflate_record_path_over_64mib(paradise):
+    """One 70 MB buffer (the drop-in's deflate() of a large file) stays on the record path
+    (up to 1 GiB: 16-bit unit ids, closed-form window slides): bit-exact at L1 (rounds of
+    inserted positions) and L6 (segment-parallel lazy parse), and it inflates back."""
+    rng = random.Random(19)
+    parts, n = [], 0
+    while n < 70_000_000:
+        b = bytearray(paradise)
+        for j in range(rng.randrange(500), len(b), 997):
+            b[j] = rng.randrange(32, 127)
+        parts.append(bytes(b))
+        n += len(b)
+    big = b"".join(parts)[:70_000_000]
+    for level in (1, 6):
+        g = sdz.deflate_batch([big], level=level)[0]
+        assert g["status"] == "OK"
+        assert g["data"] == O.deflate(big, level=level), level
+    back = sdz.inflate_batch([g["data"]], [len(big) + 64])[0]
+    assert back["success"] and back["data"] == big
+
+
 def test_deflate_record_path_output_overflow(paradise):
     """An output slot one byte short is an overflow; an exact one is not."""
     inputs = [paradise[:65536], paradise[65536:100000]]
