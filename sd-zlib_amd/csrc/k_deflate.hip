@@ -2746,16 +2746,21 @@ void launch_deflate(const DeflateArgs& a, hipStream_t st, hipStream_t side, hipE
                 // streams still moving after each (one small copy + sync per round)
                 (void)hipMemsetAsync(a.lz_act, 0, (size_t)a.n * 4, st);
                 hipLaunchKernelGGL(k_fz_init, dim3((a.nlseg + 255) / 256), dim3(256), 0, st, a);
-                for (uint32_t round = 1; round <= kFzRounds; ++round) {
-                    DeflateArgs r = a;
-                    r.lz_round = round;
-                    hipLaunchKernelGGL(k_fz_match, dim3(a.nlseg), dim3(a.lz_shift >= 8 ? 256 : 1u << a.lz_shift), 0, st, r);
-                    hipLaunchKernelGGL(k_fz_spec, gseg, dim3(LZ_THREADS), 0, st, r);
-                    hipLaunchKernelGGL(k_fz_join, gseg, dim3(LZ_THREADS), 0, st, r);
-                    hipLaunchKernelGGL(k_fz_fix, dim3(a.n), dim3(64), 0, st, r);
-                    hipLaunchKernelGGL(k_fz_merge, gseg, dim3(LZ_THREADS), 0, st, r);
-                    (void)hipMemsetAsync(a.lz_nact, 0, 4, st);
-                    hipLaunchKernelGGL(k_fz_roll, dim3((a.n + 255) / 256), dim3(256), 0, st, r);
+                // rounds are queued in batches of 1, 2, 4, then 8 between reads (a settled
+                // stream's kernels return at once, so the rounds past the end cost launches only)
+                for (uint32_t round = 1; round <= kFzRounds;) {
+                    const uint32_t batch = round < 8 ? round : 8;
+                    for (uint32_t b = 0; b < batch && round <= kFzRounds; ++b, ++round) {
+                        DeflateArgs r = a;
+                        r.lz_round = round;
+                        hipLaunchKernelGGL(k_fz_match, dim3(a.nlseg), dim3(a.lz_shift >= 8 ? 256 : 1u << a.lz_shift), 0, st, r);
+                        hipLaunchKernelGGL(k_fz_spec, gseg, dim3(LZ_THREADS), 0, st, r);
+                        hipLaunchKernelGGL(k_fz_join, gseg, dim3(LZ_THREADS), 0, st, r);
+                        hipLaunchKernelGGL(k_fz_fix, dim3(a.n), dim3(64), 0, st, r);
+                        hipLaunchKernelGGL(k_fz_merge, gseg, dim3(LZ_THREADS), 0, st, r);
+                        (void)hipMemsetAsync(a.lz_nact, 0, 4, st);
+                        hipLaunchKernelGGL(k_fz_roll, dim3((a.n + 255) / 256), dim3(256), 0, st, r);
+                    }
                     uint32_t moving = 0;
                     if (hipMemcpyAsync(&moving, a.lz_nact, 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
                         hipStreamSynchronize(st) != hipSuccess || moving == 0)

@@ -1305,6 +1305,7 @@ int run_inflate_rounds(const InflateArgs& a, hipStream_t s, uint32_t* host_activ
         if (kernel_ms) (void)hipEventRecord(ev[1], s);
         hipLaunchKernelGGL(k_inflate_resolve, g2, dim3(resolve_block_threads()), 0, s, a, round);
         if (kernel_ms) (void)hipEventRecord(ev[2], s);
+        if (a.one_round && !a.split_plan) break;         // (times read after finalize)
         if (hipMemcpyAsync(host_active, a.active, sizeof(uint32_t), hipMemcpyDeviceToHost, s) != hipSuccess) { rc = -1; break; }
         if (hipStreamSynchronize(s) != hipSuccess) { rc = -1; break; }
         if (kernel_ms) {
@@ -1322,6 +1323,13 @@ int run_inflate_rounds(const InflateArgs& a, hipStream_t s, uint32_t* host_activ
         if (kernel_ms) {
             (void)hipEventRecord(ev[3], s);
             (void)hipEventSynchronize(ev[3]);
+            if (a.one_round && !a.split_plan) {
+                float t0 = 0.f, t1 = 0.f;
+                (void)hipEventElapsedTime(&t0, ev[0], ev[1]);
+                (void)hipEventElapsedTime(&t1, ev[1], ev[2]);
+                kernel_ms[0] = t0;
+                kernel_ms[1] = t1;
+            }
             float t2 = 0.f;
             (void)hipEventElapsedTime(&t2, ev[2], ev[3]);
             kernel_ms[2] = t2;

@@ -23,6 +23,11 @@ int hip_fail(hipError_t e, const char* what);
     } while (0)
 
 int ensure_device();
+// sdz_inflate_batch_device with the input lengths and output capacities optionally on the host
+int inflate_batch_device(const uint8_t* in, const uint64_t* in_off, const uint64_t* in_len, uint8_t* out,
+                         const uint64_t* out_off, const uint64_t* out_cap, sdz_inflate_record* rec, uint32_t n,
+                         int32_t format, const uint8_t* dict, uint32_t dict_len, void* stream, const uint64_t* host_len,
+                         const uint64_t* host_cap);
 // sdz_deflate_batch_device with the input lengths optionally known on the host
 int deflate_batch_device(const uint8_t* in, const uint64_t* in_off, const uint64_t* in_len, uint8_t* out,
                          const uint64_t* out_off, const uint64_t* out_cap, sdz_deflate_record* rec, uint32_t n,

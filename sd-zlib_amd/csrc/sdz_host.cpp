@@ -133,8 +133,9 @@ int host_shard(const uint8_t* const* in, const size_t* in_len, uint8_t* const* o
     struct EvFree { hipEvent_t a, b; ~EvFree() { hipEventDestroy(a); hipEventDestroy(b); } } evf{ e0, e1 };
     HIPCHK(hipEventRecord(e0, s));
     int rc = C.inflate
-        ? sdz_inflate_batch_device(B + o_in, d_meta, d_meta + m, B + o_out, d_meta + 2 * (size_t)m, d_meta + 3 * (size_t)m,
-                                   (sdz_inflate_record*)(B + o_rec), m, C.format, d_dict, (uint32_t)C.dict_len, s)
+        ? rt::inflate_batch_device(B + o_in, d_meta, d_meta + m, B + o_out, d_meta + 2 * (size_t)m,
+                                   d_meta + 3 * (size_t)m, (sdz_inflate_record*)(B + o_rec), m, C.format, d_dict,
+                                   (uint32_t)C.dict_len, s, meta.data() + m, meta.data() + 3 * (size_t)m)
         : rt::deflate_batch_device(B + o_in, d_meta, d_meta + m, B + o_out, d_meta + 2 * (size_t)m,
                                    d_meta + 3 * (size_t)m, (sdz_deflate_record*)(B + o_rec), m, C.level, C.format,
                                    C.fname, C.fname_len, C.mtime, d_dict, (uint32_t)C.dict_len, s, meta.data() + m);

@@ -57,6 +57,9 @@ struct InflateArgs {
     const SplitInfo* spinfo;     // segment mode: the split streams (candidate counts)
     const uint64_t* cand;        // segment mode: sorted candidates, SP_CAND_MAX per split stream
     uint32_t* segtok;            // segment mode: the segment token pool
+    // host-side hints (host pointers / flags; kernels never read them)
+    const uint64_t* host_len;    // the n input lengths, when the caller has them on the host
+    uint32_t one_round;          // every stream finishes in one round: no active-count read-back
 };
 
 uint64_t inflate_dsave_bytes();  // per stream decode state

@@ -405,8 +405,12 @@ int inflate_split_start(const InflateArgs& a, hipStream_t s, PoolUse& find_use, 
     uint64_t split_min = 16 << 10;
     if (const char* e = getenv("SDZ_SPLIT_MIN")) split_min = strtoull(e, nullptr, 10);
     std::vector<uint64_t> len(n);
-    HIPCHK(hipMemcpyAsync(len.data(), a.in_len, n * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
-    HIPCHK(hipStreamSynchronize(s));
+    if (a.host_len) {
+        std::copy(a.host_len, a.host_len + n, len.begin());
+    } else {
+        HIPCHK(hipMemcpyAsync(len.data(), a.in_len, n * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+    }
     uint64_t thr = 0;
     if (const char* e = getenv("SDZ_SPLIT_SHARE")) {
         uint64_t total = 0;
@@ -598,6 +602,18 @@ int sdz_inflate_batch_device(const uint8_t* in, const uint64_t* in_off, const ui
                              uint8_t* out, const uint64_t* out_off, const uint64_t* out_cap,
                              sdz_inflate_record* rec, uint32_t n, int32_t format,
                              const uint8_t* dict, uint32_t dict_len, void* stream) {
+    return rt::inflate_batch_device(in, in_off, in_len, out, out_off, out_cap, rec, n, format, dict, dict_len, stream,
+                                    nullptr, nullptr);
+}
+}  // extern "C"
+
+// host_len / host_cap (optional): the lengths and output capacities on the host too (the
+// host-buffer path): no length read-back for the split plan, and when every stream's output
+// fits one round's tokens (a token is >= 1 output byte), no active-count read-back either
+int rt::inflate_batch_device(const uint8_t* in, const uint64_t* in_off, const uint64_t* in_len, uint8_t* out,
+                             const uint64_t* out_off, const uint64_t* out_cap, sdz_inflate_record* rec, uint32_t n,
+                             int32_t format, const uint8_t* dict, uint32_t dict_len, void* stream,
+                             const uint64_t* host_len, const uint64_t* host_cap) {
     if (int rc = ensure_device()) return rc;
     if (n == 0) return SDZ_API_OK;
     if (!in || !in_off || !in_len || !out || !out_off || !out_cap || !rec)
@@ -625,6 +641,14 @@ int sdz_inflate_batch_device(const uint8_t* in, const uint64_t* in_off, const ui
     a.n = n; a.format = format;
     a.streaming = 0; a.window = nullptr; a.carry = nullptr;
     a.split_plan = nullptr; a.split_state = nullptr; a.segmode = 0;
+    a.host_len = host_len;
+    a.one_round = 0;
+    if (host_len && host_cap) {
+        bool one = true;
+        for (uint32_t i = 0; i < n && one; ++i)
+            one = host_cap[i] + 16 <= a.round_tokens && host_len[i] <= (1ull << 28);
+        a.one_round = one ? 1u : 0u;
+    }
     PoolUse find_use(g_find, s);
     SplitHost sh;
     if (int rc = inflate_split_start(a, s, find_use, sh)) return rc;
@@ -643,6 +667,8 @@ int sdz_inflate_batch_device(const uint8_t* in, const uint64_t* in_off, const ui
     }
     return rc;
 }
+
+extern "C" {
 
 uint64_t sdz_inflate_state_bytes(uint32_t n) { return IStateLayout(n).bytes; }
 

@@ -17,7 +17,11 @@ def main():
     golden = os.path.join(ROOT, "tests", "golden")
     text = open(os.path.join(golden, "paradiselost.txt"), "rb").read()
     comp = open(os.path.join(golden, "paradiselost.deflate"), "rb").read()
-    cases = [("inflate", lambda: sdz.inflate(comp))]
+    simple_c = open(os.path.join(golden, "simple.deflate"), "rb").read()
+    simple_t = open(os.path.join(golden, "simple.txt"), "rb").read()
+    cases = [("inflate_simple", lambda: sdz.inflate(simple_c)),
+             ("deflate_simple", lambda: sdz.deflate(simple_t, {"level": 6})),
+             ("inflate", lambda: sdz.inflate(comp))]
     for lv in (1, 4, 6, 9):
         cases.append(("deflate_L%d" % lv, lambda lv=lv: sdz.deflate(text, {"level": lv})))
     only = sys.argv[2].split(",") if len(sys.argv) > 2 else None
