@@ -110,7 +110,7 @@ struct DTables {
     uint16_t static_dtree[30 * 2];
     uint8_t extra_lbits[29], extra_dbits[30], extra_blbits[19];
 };
-__device__ DTables g_dt;                                     // built once per launch (k_deflate_tables)
+__device__ DTables g_dt;                                     // built once per device (dt_ready)
 __constant__ uint8_t c_extra_lbits[29] = { 0, 0, 0, 0, 0, 0, 0, 0, 1, 1, 1, 1, 2, 2, 2, 2, 3, 3, 3, 3, 4, 4, 4, 4, 5, 5, 5, 5, 0 };
 __constant__ uint8_t c_extra_dbits[30] = { 0, 0, 0, 0, 1, 1, 2, 2, 3, 3, 4, 4, 5, 5, 6, 6, 7, 7, 8, 8, 9, 9, 10, 10, 11, 11, 12, 12, 13, 13 };
 __constant__ uint8_t c_extra_blbits[19] = { 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 2, 3, 7 };
@@ -164,6 +164,16 @@ __global__ void k_deflate_tables() {
         }
         for (n = 0; n < 30; n++) { T.static_dtree[n * 2 + 1] = 5; T.static_dtree[n * 2] = (uint16_t)bitrev_n((uint32_t)n, 5); }
     }
+}
+
+// the tables depend on nothing: built on a device's first compress call, and waited for there
+// (a later call may run on another stream)
+static bool g_dt_ready[64];
+static void dt_ready(hipStream_t s) {
+    int d = 0;
+    if (hipGetDevice(&d) == hipSuccess && d >= 0 && d < 64 && g_dt_ready[d]) return;
+    hipLaunchKernelGGL(k_deflate_tables, dim3(1), dim3(1), 0, s);
+    if (hipStreamSynchronize(s) == hipSuccess && d >= 0 && d < 64) g_dt_ready[d] = true;
 }
 
 // scalar state of one stream (deflate.ts:102-194), registers
@@ -1049,7 +1059,7 @@ void launch_deflate_reset(uint8_t* state, uint32_t n, hipStream_t s) {
 }
 void launch_deflate_stream(const DeflateArgs& a, uint32_t finish, hipStream_t s) {
     if (!a.n) return;
-    hipLaunchKernelGGL(k_deflate_tables, dim3(1), dim3(1), 0, s);
+    dt_ready(s);
     hipLaunchKernelGGL(k_deflate_stream, dim3((a.n + DF_THREADS - 1) / DF_THREADS), dim3(DF_THREADS), 0, s, a, finish);
 }
 
@@ -2723,7 +2733,7 @@ constexpr uint32_t kFzRounds = 1024;                       // then the unsettled
 void launch_deflate(const DeflateArgs& a, hipStream_t st, hipStream_t side, hipEvent_t ev) {
     if (a.n == 0) return;
     dim3 grid((a.n + DF_THREADS - 1) / DF_THREADS);
-    hipLaunchKernelGGL(k_deflate_tables, dim3(1), dim3(1), 0, st);
+    dt_ready(st);
     const bool fastlv = c_config_host_fast(a.level);
     if (a.rec_buf && (!fastlv || (a.lz_shift && a.nlseg))) {
         const int ck_kind = a.format == SDZ_DEFLATE_GZIP ? 1 : 0;
