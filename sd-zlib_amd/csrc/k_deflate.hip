@@ -1778,7 +1778,9 @@ __device__ __forceinline__ LzSeg lz_seg(const DeflateArgs& A, uint32_t seg) {
     q.rp = A.rp0[q.k];
     q.n = (int)A.in_len[q.k];
     q.g = (int)(q.j << A.lz_shift);
-    q.h = q.g + (1 << A.lz_shift) < q.n ? q.g + (1 << A.lz_shift) : q.n;
+    // deflate(NO_FLUSH) steps while lookahead >= MIN_LOOKAHEAD (deflate.ts:1060-1066)
+    const int nend = A.noflush ? (q.n >= MIN_LOOKAHEAD ? q.n - MIN_LOOKAHEAD + 1 : 0) : q.n;
+    q.h = q.g + (1 << A.lz_shift) < nend ? q.g + (1 << A.lz_shift) : nend;
     return q;
 }
 __global__ __launch_bounds__(LZ_THREADS) void k_lz_spec(DeflateArgs A) {
@@ -1884,7 +1886,9 @@ __global__ __launch_bounds__(64) void k_lz_fix(DeflateArgs A) {      // one wave
     }
     if (lane == 0) {
         const LzSt f = ok ? lz_load(A.lz_end[base + K - 1]) : t;
-        A.lz_fin[k] = (uint32_t)f.avail;                        // deflate_slow's last literal (deflate.ts:1172)
+        // deflate_slow's last literal (deflate.ts:1172) -- not under NO_FLUSH: it stays pending
+        A.lz_fin[k] = A.noflush ? 0u : (uint32_t)f.avail;
+        ((GLB FStream*)((GLB DSlab*)(A.state + (uint64_t)k * SLAB_BYTES))->window)->pad[0] = (uint32_t)f.s;
     }
 }
 // bits of word wi that belong to positions [a, b)
@@ -1918,7 +1922,11 @@ __global__ __launch_bounds__(LZ_THREADS) void k_lz_scan(DeflateArgs A) {
         A.lz_cnt[s] = o;
         o += c;
     }
-    A.lz_fin[k] |= o << 1;
+    // (no segment: NO_FLUSH before MIN_LOOKAHEAD bytes, nothing parsed)
+    const uint32_t fin = A.lz_sg0[k + 1] > A.lz_sg0[k] ? (A.lz_fin[k] & 1u) : 0u;
+    if (A.lz_sg0[k + 1] == A.lz_sg0[k])
+        ((GLB FStream*)((GLB DSlab*)(A.state + (uint64_t)k * SLAB_BYTES))->window)->pad[0] = 0u;
+    A.lz_fin[k] = fin | (o << 1);
 }
 // symbols to the front of the stream's record buffer (no record is read any more)
 __global__ __launch_bounds__(LZ_THREADS) void k_lz_emit(DeflateArgs A) {
@@ -2026,7 +2034,10 @@ __global__ __launch_bounds__(LB_THREADS) void k_lz_blocks(DeflateArgs A) {
                 strstart = block_start + before + b.last;
             }
         }
-        if (cnt == 0) { cnt = nsym - b0; eof = 1; }
+        if (cnt == 0) {
+            if (A.noflush) break;                              // the open block stays pending
+            cnt = nsym - b0; eof = 1;
+        }
         if (threadIdx.x == 0 && nb < nbcap) {
             const int64_t off = slide_off(n, step);
             GLB FBlock* B = (GLB FBlock*)(slots + (uint64_t)nb * FB_SLOT);
@@ -2308,6 +2319,8 @@ __global__ __launch_bounds__(64) void k_fz_fix(DeflateArgs A) {
     if (k >= A.n || A.rp0[k] == ~0ull || !(A.lz_act[k] & 1u)) return;
     const uint32_t base = A.lz_sg0[k], K = A.lz_sg0[k + 1] - base;
     const int max_ins = c_config[A.level][1];
+    bool fok = true;                                            // (lane 0) the last chain met its segment
+    int fs = 0;                                                 // (lane 0) else where it ended
     uint32_t j = 1;
     while (j < K) {
         uint32_t found = K;
@@ -2324,18 +2337,25 @@ __global__ __launch_bounds__(64) void k_fz_fix(DeflateArgs A) {
             int s = (int)(uint32_t)e;
             bool cin = (e >> 32) != 0;
             uint32_t jj = found + 1;
+            fs = s;
+            fok = false;
             for (; jj < K; ++jj) {
                 const LzSeg q = lz_seg(A, base + jj);
                 const int c = fz_join_run(A, q, s, cin, max_ins);
                 A.lz_c[base + jj] = (uint32_t)c;
                 A.fz_fx[base + jj] = A.lz_round;
-                if (c < q.h) break;
+                if (c < q.h) { fok = true; break; }
             }
+            fs = s;
             next = jj + 1;
         }
         j = __shfl(next, 0);
     }
-    if (lane == 0) A.lz_fin[k] = 0;                             // deflate_fast leaves no pending literal
+    if (lane == 0) {
+        A.lz_fin[k] = 0;                                        // deflate_fast leaves no pending literal
+        const int f = fok && K ? (int)(uint32_t)A.lz_end[base + K - 1] : fs;
+        ((GLB FStream*)((GLB DSlab*)(A.state + (uint64_t)k * SLAB_BYTES))->window)->pad[0] = (uint32_t)f;
+    }
 }
 // the next I of each segment ([g, c) from the join, [c, h) from its own parse); a stream
 // whose I changed anywhere goes another round
@@ -2523,7 +2543,7 @@ __global__ __launch_bounds__(EN_THREADS) void k_dfl_encode(DeflateArgs A) {
     __shared__ uint16_t lbase[29], dbase[30];
     __shared__ uint32_t wsum[EN_THREADS / 64];
     __shared__ uint32_t stg[EN_STG_WORDS];
-    __shared__ uint64_t sh_end;
+    __shared__ uint64_t sh_end, sh_al;
     __shared__ uint32_t sh_bad;
     const uint32_t sid = blockIdx.x, tid = threadIdx.x;
     if (sid >= A.n) return;
@@ -2538,7 +2558,7 @@ __global__ __launch_bounds__(EN_THREADS) void k_dfl_encode(DeflateArgs A) {
     const uint32_t nblk = F->nblk;
     const bool gzip = A.format == SDZ_DEFLATE_GZIP;
     const uint32_t hdr_bytes = A.format == SDZ_DEFLATE_ZLIB ? 2 : gzip ? 10 + (A.fname_len ? A.fname_len + 1 : 0) : 0;
-    const uint32_t trl_bytes = A.format == SDZ_DEFLATE_ZLIB ? 4 : gzip ? 8 : 0;
+    const uint32_t trl_bytes = A.noflush ? 0u : A.format == SDZ_DEFLATE_ZLIB ? 4 : gzip ? 8 : 0;
     const uint64_t in_len = A.in_len[sid];
     GLB uint8_t* slots = (GLB uint8_t*)(A.blk + (uint64_t)A.tb0[sid] * FB_SLOT);
     auto blk_at = [&](uint32_t b) { return (GLB FBlock*)(slots + (uint64_t)b * FB_SLOT); };
@@ -2561,14 +2581,15 @@ __global__ __launch_bounds__(EN_THREADS) void k_dfl_encode(DeflateArgs A) {
             }
             if (Bk->eof) { Tb = (Tb + 7) & ~7ull; al = Tb; }
         }
-        if (Tb / 8 + trl_bytes > A.out_cap[sid]) bad = 1;
+        if ((Tb + 7) / 8 + trl_bytes > A.out_cap[sid]) bad = 1;
         sh_end = Tb;
+        sh_al = al;
         sh_bad = bad;
     }
     __threadfence();                                         // (block layout: read by all threads)
     __syncthreads();
     if (sh_bad) { if (tid == 0) F->flag = 1; return; }
-    const uint64_t total = sh_end / 8 + trl_bytes;
+    const uint64_t total = (sh_end + 7) / 8 + trl_bytes;   // (NO_FLUSH: the last partial byte too)
     GLB uint8_t* out = (GLB uint8_t*)(A.out + A.out_off[sid]);
     {                                                        // zero the slot's bytes [0, total)
         const uint64_t mis = (4 - ((uintptr_t)out & 3)) & 3, head = mis < total ? mis : total;
@@ -2677,13 +2698,22 @@ __global__ __launch_bounds__(EN_THREADS) void k_dfl_encode(DeflateArgs A) {
     __syncthreads();
     if (tid == 0) {
         if (sh_bad) { F->flag = 1; return; }
-        const uint32_t cks = (uint32_t)A.cks[sid];
+        const uint32_t cks = A.cks_in ? (uint32_t)*A.cks_in : (uint32_t)A.cks[sid];
         const uint64_t e = sh_end;
-        if (A.format == SDZ_DEFLATE_ZLIB)
-            orbits(e, ((cks >> 24) & 0xff) | ((cks >> 8) & 0xff00) | ((cks << 8) & 0xff0000) | (cks << 24));
-        else if (gzip) { orbits(e, cks); orbits(e + 32, (uint32_t)in_len); }
         sdz_deflate_record R;
         R.status = SDZ_OK; R.checksum = (int32_t)cks; R.out_len = total; R.reserved = 0;
+        if (A.noflush) {
+            // what deflate(NO_FLUSH) has put in pending_buf: bytes up to the last byte-aligned
+            // point, then the 16-bit units send_bits filled -- it writes a unit once a value
+            // overflows it, so up to 16 bits stay in bi_buf (deflate.ts:347-366)
+            const uint64_t al = sh_al;
+            R.out_len = al / 8 + (e > al ? 2 * ((e - al - 1) / 16) : 0);
+            R.reserved = F->pad[0];
+        } else if (A.format == SDZ_DEFLATE_ZLIB) {
+            orbits(e, ((cks >> 24) & 0xff) | ((cks >> 8) & 0xff00) | ((cks << 8) & 0xff0000) | (cks << 24));
+        } else if (gzip) {
+            orbits(e, cks); orbits(e + 32, (uint32_t)in_len);
+        }
         A.rec[sid] = R;
     }
 }
@@ -2735,7 +2765,7 @@ void launch_deflate(const DeflateArgs& a, hipStream_t st, hipStream_t side, hipE
     dim3 grid((a.n + DF_THREADS - 1) / DF_THREADS);
     dt_ready(st);
     const bool fastlv = c_config_host_fast(a.level);
-    if (a.rec_buf && (!fastlv || (a.lz_shift && a.nlseg))) {
+    if (a.rec_buf && (!fastlv || (a.lz_shift && (a.nlseg || a.noflush)))) {
         const int ck_kind = a.format == SDZ_DEFLATE_GZIP ? 1 : 0;
         if (a.ncunit)
             hipLaunchKernelGGL(k_dfl_chain, dim3((a.ncunit + CH_WAVES - 1) / CH_WAVES), dim3(64 * CH_WAVES), 0, st, a);
@@ -2749,12 +2779,13 @@ void launch_deflate(const DeflateArgs& a, hipStream_t st, hipStream_t side, hipE
             launch_checksum(a.in, a.in_off, a.in_len, nullptr, a.cks, a.n, ck_kind, side);
             (void)hipEventRecord(ev, side);
         }
-        if (a.lz_shift && a.nlseg) {
+        if (a.lz_shift && (a.nlseg || a.noflush)) {       // (NO_FLUSH may have nothing to parse yet)
             const dim3 gseg((a.nlseg + LZ_THREADS - 1) / LZ_THREADS), gstr((a.n + LZ_THREADS - 1) / LZ_THREADS);
-            if (fastlv) {
+            if (fastlv) (void)hipMemsetAsync(a.lz_act, 0, (size_t)a.n * 4, st);
+            if (!a.nlseg) {
+            } else if (fastlv) {
                 // rounds of the inserted-position fixed point; the host reads the number of
                 // streams still moving after each (one small copy + sync per round)
-                (void)hipMemsetAsync(a.lz_act, 0, (size_t)a.n * 4, st);
                 hipLaunchKernelGGL(k_fz_init, dim3((a.nlseg + 255) / 256), dim3(256), 0, st, a);
                 // rounds are queued in batches of 1, 2, 4, then 8 between reads (a settled
                 // stream's kernels return at once, so the rounds past the end cost launches only)
@@ -2781,9 +2812,9 @@ void launch_deflate(const DeflateArgs& a, hipStream_t st, hipStream_t side, hipE
                 hipLaunchKernelGGL(k_lz_join, gseg, dim3(LZ_THREADS), 0, st, a);
                 hipLaunchKernelGGL(k_lz_fix, dim3(a.n), dim3(64), 0, st, a);
             }
-            hipLaunchKernelGGL(k_lz_count, gseg, dim3(LZ_THREADS), 0, st, a);
+            if (a.nlseg) hipLaunchKernelGGL(k_lz_count, gseg, dim3(LZ_THREADS), 0, st, a);
             hipLaunchKernelGGL(k_lz_scan, gstr, dim3(LZ_THREADS), 0, st, a);
-            hipLaunchKernelGGL(k_lz_emit, gseg, dim3(LZ_THREADS), 0, st, a);
+            if (a.nlseg) hipLaunchKernelGGL(k_lz_emit, gseg, dim3(LZ_THREADS), 0, st, a);
             hipLaunchKernelGGL(k_lz_blocks, dim3(a.n), dim3(LB_THREADS), 0, st, a);
         } else if (a.wide) hipLaunchKernelGGL(k_dfl_parse_wide, dim3(a.n), dim3(PW_THREADS), 0, st, a);
         else hipLaunchKernelGGL(k_dfl_parse, grid, dim3(64), 0, st, a);
@@ -2791,6 +2822,7 @@ void launch_deflate(const DeflateArgs& a, hipStream_t st, hipStream_t side, hipE
         if (fork) (void)hipStreamWaitEvent(st, ev, 0);
         else launch_checksum(a.in, a.in_off, a.in_len, nullptr, a.cks, a.n, ck_kind, st);
         hipLaunchKernelGGL(k_dfl_encode, dim3(a.n), dim3(EN_THREADS), 0, st, a);
+        if (a.noflush) return;                               // (the caller redoes a flagged stream)
         DeflateArgs f = a;
         f.fast = 1;                                          // streams the record path handed back
         hipLaunchKernelGGL(k_deflate, grid, dim3(DF_THREADS), 0, st, f);

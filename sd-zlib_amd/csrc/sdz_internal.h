@@ -140,6 +140,12 @@ struct DeflateArgs {
     uint32_t* fz_rc;             //   recomputed its records,
     uint32_t* fz_chg;            //   changed its part of I,
     uint32_t* fz_fx;             //   had its join redone by k_fz_fix
+    // Deflater.append on the record path (sdz_deflater_*): deflate(NO_FLUSH) -- the parse
+    // stops at the first step with lookahead < MIN_LOOKAHEAD, only the blocks cut before it are
+    // flushed, no trailer; the record's out_len is what the reference's pending buffer holds
+    // then, its `reserved` field the stop position.  Flagged streams are not redone here.
+    uint32_t noflush;
+    const int32_t* cks_in;       // the running checksum (chunk-wise, as sd-deflate.ts:185-190), or null
     int32_t* cks;                // n input checksums (record path)
     uint32_t fast;               // set by launch_deflate: k_deflate redoes flagged streams only
     const uint8_t* dict;         // preset dictionary (deflateSetDictionary), may be null

@@ -787,7 +787,8 @@ int sdz_deflate_batch_device(const uint8_t* in, const uint64_t* in_off, const ui
 int rt::deflate_batch_device(const uint8_t* in, const uint64_t* in_off, const uint64_t* in_len, uint8_t* out,
                              const uint64_t* out_off, const uint64_t* out_cap, sdz_deflate_record* rec, uint32_t n,
                              int32_t level, int32_t format, const uint8_t* fname, uint32_t fname_len, uint32_t mtime,
-                             const uint8_t* dict, uint32_t dict_len, void* stream, const uint64_t* host_len) {
+                             const uint8_t* dict, uint32_t dict_len, void* stream, const uint64_t* host_len,
+                             uint32_t noflush, const int32_t* cks_in) {
     if (int rc = ensure_device()) return rc;
     if (n == 0) return SDZ_API_OK;
     if (level < 1 || level > 9) return fail(SDZ_API_BAD_ARG, "level must be between 1 and 9, inclusive");
@@ -850,11 +851,15 @@ int rt::deflate_batch_device(const uint8_t* in, const uint64_t* in_off, const ui
         lz_shift = 9;
         while (lz_shift < 12 && (tot >> (lz_shift + 1)) >= 65536) ++lz_shift;
         if (fastlv) lz_shift = std::max(7u, lz_shift - 2);      // deflate_fast: its state is the position alone
-        else if (tot >= (mx << 15)) lz_shift = 0;
+        else if (tot >= (mx << 15) && !noflush) lz_shift = 0;
         if (const char* e = getenv("SDZ_LZ_SHIFT"))            // tests: segment size 2^6 .. 2^16
             lz_shift = (uint32_t)std::min(16, std::max(6, atoi(e)));
     }
-    auto lz_segs = [&](uint64_t l) -> uint64_t { return lz_shift ? (l + (1ull << lz_shift) - 1) >> lz_shift : 0; };
+    // (NO_FLUSH: steps up to lookahead MIN_LOOKAHEAD only, as k_deflate.hip's lz_seg)
+    auto lz_segs = [&](uint64_t l) -> uint64_t {
+        if (noflush) l = l >= 262 ? l - 261 : 0;
+        return lz_shift ? (l + (1ull << lz_shift) - 1) >> lz_shift : 0;
+    };
     // per position: record 8, link 2, parse words 8 + 4 + 3 bitmaps; per segment 28
     const uint64_t kPosBytes = lz_shift ? 8 + 2 + 8 + 4 + 1 : 8 + 2;
     auto rec_cost = [&](uint32_t i) -> uint64_t {
@@ -922,6 +927,7 @@ int rt::deflate_batch_device(const uint8_t* in, const uint64_t* in_off, const ui
         a.dict = dict; a.dict_len = dict_len; a.dict_adler = 1; a.dict_adler_dev = d_dictid;
         a.fname = d_fname; a.fname_len = fname_len; a.mtime = mtime;
         a.n = m; a.level = level; a.format = format;
+        a.noflush = noflush; a.cks_in = cks_in;
         if (recpath) {
             // the plan: rp0 / tb0 (m + 1 each), then the unit lists
             std::vector<uint64_t> rp0(m + 1);
@@ -1309,6 +1315,17 @@ void sdz_inflater_destroy(sdz_inflater* z) { delete z; }
 
 }  // extern "C"
 
+// A Deflater runs on the record path while it can: every append re-runs the record path
+// over all input so far in NO_FLUSH mode (the parse stops where deflate(NO_FLUSH) returns
+// NeedMore, only the blocks cut before that are flushed) and returns the bytes past what
+// earlier calls returned -- the same bytes the reference's append() returns, since the parse,
+// the block cuts and the bit layout do not depend on where earlier calls stopped.  Two cases
+// would differ, and switch the Deflater to the serial kernel, replaying every earlier append
+// into its state: a block the record path hands back (the pending_buf overlay overtaken,
+// SURVEY A7, or a slot overflow), and a call stopping exactly where the window slides one step
+// earlier than in one pass (fill_window at strstart = 65274 + 32 Ki e with no more input).
+// Dictionaries, inputs past kDeflateRecMax and SDZ_SERIAL_PARSE take the serial kernel from
+// the start.
 struct sdz_deflater {
     int32_t level = 6, format = SDZ_DEFLATE_ZLIB;
     std::vector<uint8_t> fname;
@@ -1323,49 +1340,28 @@ struct sdz_deflater {
     uint64_t* d_meta = nullptr;                   // in_off, in_len, out_off, out_cap
     sdz_deflate_record* d_rec = nullptr;
     std::vector<uint8_t> out;
+    // record mode
+    bool rec_mode = false;
+    int32_t status = 0;                           // 0 nothing appended, 1 appending, 2 finished
+    std::vector<uint8_t> hist;                    // every byte appended (the serial replay's source)
+    std::vector<size_t> calls;                    // each append's length (the replay's call boundaries)
+    uint64_t total = 0, out_done = 0;
+    int32_t running = 0;                          // the chunk-wise running checksum
+    uint8_t* d_all = nullptr;                     // the input so far, on the device
+    size_t all_cap = 0;
+    int32_t* d_ck = nullptr;
+    std::vector<uint8_t> trailer;                 // a second finish() returns it again
     ~sdz_deflater() {
-        for (void* p : { (void*)d_state, (void*)d_dict, (void*)d_in, (void*)d_out, (void*)d_meta, (void*)d_rec })
+        for (void* p : { (void*)d_state, (void*)d_dict, (void*)d_in, (void*)d_out, (void*)d_meta, (void*)d_rec,
+                         (void*)d_all, (void*)d_ck })
             if (p) hipFree(p);
     }
 };
 
-extern "C" {
-
-sdz_deflater* sdz_deflater_create(int32_t level, int32_t format, const uint8_t* fname, size_t fname_len,
-                                  uint32_t mtime, const uint8_t* dict, size_t dict_len) {
-    if (ensure_device()) return nullptr;
-    if (level < 1 || level > 9) { fail(SDZ_API_BAD_ARG, "level must be between 1 and 9, inclusive"); return nullptr; }
-    if (format < SDZ_DEFLATE_RAW || format > SDZ_DEFLATE_GZIP) {
-        fail(SDZ_API_BAD_ARG, "container must be one of `raw`, `deflate`, `gzip`");
-        return nullptr;
-    }
-    if (dict && format != SDZ_DEFLATE_ZLIB) {
-        fail(SDZ_API_BAD_ARG, "Can only provide a dictionary for `deflate` containers.");
-        return nullptr;
-    }
-    sdz_deflater* z = new sdz_deflater;
-    z->level = level; z->format = format; z->mtime = mtime;
-    if (fname && fname_len) z->fname.assign(fname, fname + fname_len);
-    hipError_t e = hipMalloc(&z->d_state, sdz_deflate_state_bytes(1));
-    if (e == hipSuccess) e = hipMalloc(&z->d_meta, 4 * sizeof(uint64_t));
-    if (e == hipSuccess) e = hipMalloc(&z->d_rec, sizeof(sdz_deflate_record));
-    if (e == hipSuccess && dict) {
-        z->dict_len = (uint32_t)dict_len;
-        e = hipMalloc(&z->d_dict, dict_len + 64);
-        if (e == hipSuccess && dict_len) e = hipMemcpy(z->d_dict, dict, dict_len, hipMemcpyHostToDevice);
-    }
-    if (e != hipSuccess || sdz_deflate_state_reset_device(z->d_state, 1, nullptr) != SDZ_API_OK) {
-        if (e != hipSuccess) hip_fail(e, "sdz_deflater_create");
-        delete z;
-        return nullptr;
-    }
-    return z;
-}
-
-int sdz_deflater_append(sdz_deflater* z, const uint8_t* data, size_t len, int32_t finish,
-                        const uint8_t** out, size_t* out_len, sdz_deflate_record* rec) {
-    if (!z || !out || !out_len || !rec || (!data && len)) return fail(SDZ_API_BAD_ARG, "sdz_deflater_append: null pointer");
-    z->out.clear();
+namespace {
+// one call of the serial kernel (k_deflate_stream) on the Deflater's device state
+int deflater_serial_call(sdz_deflater* z, const uint8_t* data, size_t len, int32_t finish, sdz_deflate_record* rec,
+                         bool keep_out) {
     if (len + 64 > z->in_cap) {
         if (z->d_in) hipFree(z->d_in);
         z->d_in = nullptr;
@@ -1388,8 +1384,178 @@ int sdz_deflater_append(sdz_deflater* z, const uint8_t* data, size_t len, int32_
                                              z->mtime, z->d_dict, z->dict_len, finish, nullptr);
     if (rc) return rc;
     HIPCHK(hipMemcpy(rec, z->d_rec, sizeof *rec, hipMemcpyDeviceToHost));
-    z->out.resize(rec->out_len);
-    if (rec->out_len) HIPCHK(hipMemcpy(z->out.data(), z->d_out, rec->out_len, hipMemcpyDeviceToHost));
+    if (keep_out) {
+        z->out.resize(rec->out_len);
+        if (rec->out_len) HIPCHK(hipMemcpy(z->out.data(), z->d_out, rec->out_len, hipMemcpyDeviceToHost));
+    }
+    return SDZ_API_OK;
+}
+
+// leave the record path: the serial state after every append so far (their outputs were
+// returned already and are not read again)
+int deflater_to_serial(sdz_deflater* z, size_t upto_calls) {
+    z->rec_mode = false;
+    size_t o = 0;
+    for (size_t i = 0; i < upto_calls; ++i) {
+        sdz_deflate_record r{};
+        if (int rc = deflater_serial_call(z, z->hist.data() + o, z->calls[i], 0, &r, false)) return rc;
+        o += z->calls[i];
+    }
+    std::vector<uint8_t>().swap(z->hist);
+    std::vector<size_t>().swap(z->calls);
+    if (z->d_all) { hipFree(z->d_all); z->d_all = nullptr; z->all_cap = 0; }
+    return SDZ_API_OK;
+}
+
+// one append / finish on the record path; *how: 0 done, 1 done but later calls run serially
+// (the window-slide corner), 2 handed back (nothing changed: the call is to be redone serially)
+int deflater_record_call(sdz_deflater* z, const uint8_t* data, size_t len, int32_t finish, sdz_deflate_record* rec,
+                         int* how) {
+    *how = 0;
+    const uint64_t total = z->total + len;
+    if (total + 64 > z->all_cap) {
+        const size_t cap = std::max<size_t>(std::max<size_t>(total + 64, 2 * z->all_cap), 1 << 16);
+        uint8_t* p = nullptr;
+        HIPCHK(hipMalloc(&p, cap));
+        if (z->total) HIPCHK(hipMemcpy(p, z->d_all, z->total, hipMemcpyDeviceToDevice));
+        if (z->d_all) hipFree(z->d_all);
+        z->d_all = p;
+        z->all_cap = cap;
+    }
+    if (len) HIPCHK(hipMemcpy(z->d_all + z->total, data, len, hipMemcpyHostToDevice));
+    if (!z->d_ck) HIPCHK(hipMalloc(&z->d_ck, 64));
+    // the running checksum over this chunk only, seeded with the last (adler32.ts's NMAX
+    // quirk applies per chunk, as in sd-deflate.ts:185-190)
+    const int kind = z->format == SDZ_DEFLATE_GZIP ? 1 : 0;
+    const int32_t seed = z->status == 0 ? (kind ? 0 : 1) : z->running;
+    launch_checksum_one(z->d_all + z->total, len, kind, seed, z->d_ck, nullptr);
+    HIPCHK(hipGetLastError());
+    const uint64_t cap = sdz_deflate_bound(total, z->format, (uint32_t)z->fname.size());
+    if (cap > z->out_cap) {
+        if (z->d_out) hipFree(z->d_out);
+        z->d_out = nullptr;
+        z->out_cap = std::max<size_t>(cap, 2 * z->out_cap);
+        HIPCHK(hipMalloc(&z->d_out, z->out_cap));
+    }
+    uint64_t meta[4] = { 0, total, 0, cap };
+    HIPCHK(hipMemcpy(z->d_meta, meta, sizeof meta, hipMemcpyHostToDevice));
+    HIPCHK(hipMemset(z->d_rec, 0xff, sizeof(sdz_deflate_record)));      // a handed-back stream leaves it so
+    int rc = rt::deflate_batch_device(z->d_all, z->d_meta, z->d_meta + 1, z->d_out, z->d_meta + 2, z->d_meta + 3,
+                                      z->d_rec, 1, z->level, z->format, z->fname.empty() ? nullptr : z->fname.data(),
+                                      (uint32_t)z->fname.size(), z->mtime, nullptr, 0, nullptr, &total,
+                                      finish ? 0u : 1u, z->d_ck);
+    if (rc) return rc;
+    sdz_deflate_record r{};
+    HIPCHK(hipMemcpy(&r, z->d_rec, sizeof r, hipMemcpyDeviceToHost));
+    if (r.status != SDZ_OK) { *how = 2; return SDZ_API_OK; }
+    if (!finish) {
+        // a stop at strstart = 65274 + 32 Ki e: the reference's fill_window slides there
+        // (no more input), one pass would a step later -- serial from the next call on
+        const uint64_t st = r.reserved;
+        if (st >= 65274 && st % 32768 == 32506) *how = 1;
+        // tests: leave the record path after this many calls (the replay, exercised)
+        if (const char* e = getenv("SDZ_DEFLATER_SWITCH_AT"))
+            if (z->calls.size() + 1 >= (size_t)atoi(e)) *how = 1;
+    }
+    if (r.out_len < z->out_done) return fail(SDZ_API_HIP_ERROR, "deflater: output shrank");
+    z->out.resize(r.out_len - z->out_done);
+    if (!z->out.empty())
+        HIPCHK(hipMemcpy(z->out.data(), z->d_out + z->out_done, z->out.size(), hipMemcpyDeviceToHost));
+    z->out_done = r.out_len;
+    z->total = total;
+    z->running = r.checksum;
+    *rec = r;
+    rec->out_len = z->out.size();
+    rec->reserved = 0;
+    return SDZ_API_OK;
+}
+}  // namespace
+
+extern "C" {
+
+sdz_deflater* sdz_deflater_create(int32_t level, int32_t format, const uint8_t* fname, size_t fname_len,
+                                  uint32_t mtime, const uint8_t* dict, size_t dict_len) {
+    if (ensure_device()) return nullptr;
+    if (level < 1 || level > 9) { fail(SDZ_API_BAD_ARG, "level must be between 1 and 9, inclusive"); return nullptr; }
+    if (format < SDZ_DEFLATE_RAW || format > SDZ_DEFLATE_GZIP) {
+        fail(SDZ_API_BAD_ARG, "container must be one of `raw`, `deflate`, `gzip`");
+        return nullptr;
+    }
+    if (dict && format != SDZ_DEFLATE_ZLIB) {
+        fail(SDZ_API_BAD_ARG, "Can only provide a dictionary for `deflate` containers.");
+        return nullptr;
+    }
+    sdz_deflater* z = new sdz_deflater;
+    z->level = level; z->format = format; z->mtime = mtime;
+    z->rec_mode = !dict && !getenv("SDZ_SERIAL_PARSE") && !getenv("SDZ_SERIAL_DEFLATER");
+    if (fname && fname_len) z->fname.assign(fname, fname + fname_len);
+    hipError_t e = hipMalloc(&z->d_state, sdz_deflate_state_bytes(1));
+    if (e == hipSuccess) e = hipMalloc(&z->d_meta, 4 * sizeof(uint64_t));
+    if (e == hipSuccess) e = hipMalloc(&z->d_rec, sizeof(sdz_deflate_record));
+    if (e == hipSuccess && dict) {
+        z->dict_len = (uint32_t)dict_len;
+        e = hipMalloc(&z->d_dict, dict_len + 64);
+        if (e == hipSuccess && dict_len) e = hipMemcpy(z->d_dict, dict, dict_len, hipMemcpyHostToDevice);
+    }
+    if (e != hipSuccess || sdz_deflate_state_reset_device(z->d_state, 1, nullptr) != SDZ_API_OK) {
+        if (e != hipSuccess) hip_fail(e, "sdz_deflater_create");
+        delete z;
+        return nullptr;
+    }
+    return z;
+}
+
+int sdz_deflater_append(sdz_deflater* z, const uint8_t* data, size_t len, int32_t finish,
+                        const uint8_t** out, size_t* out_len, sdz_deflate_record* rec) {
+    if (!z || !out || !out_len || !rec || (!data && len)) return fail(SDZ_API_BAD_ARG, "sdz_deflater_append: null pointer");
+    z->out.clear();
+    *out = z->out.data();
+    *out_len = 0;
+    if (z->rec_mode && z->total + len > kDeflateRecMax)
+        if (int rc = deflater_to_serial(z, z->calls.size())) return rc;
+    if (z->rec_mode) {
+        // the reference's call protocol (sd-deflate.ts:180-182, 211-214, 232-234), as k_deflate_stream
+        sdz_deflate_record r{};
+        r.status = SDZ_OK;
+        r.checksum = z->running;
+        if ((finish && z->status == 0) || (!finish && z->status == 2 && len)) {
+            r.status = SDZ_DATA_ERROR;
+            *rec = r;
+            return SDZ_API_OK;
+        }
+        if (!finish && len == 0) { *rec = r; return SDZ_API_OK; }
+        if (finish && z->status == 2) {                       // deflate(FINISH) again: the trailer again
+            z->out = z->trailer;
+            *out = z->out.data();
+            *out_len = z->out.size();
+            *rec = r;
+            return SDZ_API_OK;
+        }
+        int how = 0;
+        if (int rc = deflater_record_call(z, data, len, finish, rec, &how)) return rc;
+        if (how < 2) {
+            z->hist.insert(z->hist.end(), data, data + len);
+            z->calls.push_back(len);
+            z->status = finish ? 2 : 1;
+            if (finish) {
+                const size_t t = z->format == SDZ_DEFLATE_ZLIB ? 4 : z->format == SDZ_DEFLATE_GZIP ? 8 : 0;
+                z->trailer.assign(z->out.end() - std::min(t, z->out.size()), z->out.end());
+            }
+            if (how == 1) {                                   // later calls: serial, from this state
+                std::vector<uint8_t> keep;
+                keep.swap(z->out);
+                if (int rc = deflater_to_serial(z, z->calls.size())) return rc;
+                z->out.swap(keep);
+            }
+            *out = z->out.data();
+            *out_len = z->out.size();
+            return SDZ_API_OK;
+        }
+        // handed back: replay the earlier calls into the serial state, then this one
+        z->out.clear();
+        if (int rc = deflater_to_serial(z, z->calls.size())) return rc;
+    }
+    if (int rc = deflater_serial_call(z, data, len, finish, rec, true)) return rc;
     *out = z->out.data();
     *out_len = z->out.size();
     return SDZ_API_OK;

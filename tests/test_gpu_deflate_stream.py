@@ -127,3 +127,35 @@ def test_errors_and_repeated_finish(paradise):
     with pytest.raises(sdz.SdzError, match="deflating"):
         d.append(b"more")
     assert d.append(b"") == []
+
+
+def test_record_path_deflater_hands_over_to_serial(monkeypatch, paradise):
+    """Deflater.append runs on the record path (NO_FLUSH re-runs over the input so far) and
+    falls back to the serial kernel, replaying the earlier appends into its state, when a block
+    is handed back (the pending_buf overlay overtaken) or a call stops at the window-slide
+    corner; forced here after each of the first calls.  Per-call bytes equal the reference's
+    either way."""
+    import test_gpu_parity as P
+    rng = random.Random(23)
+    src = paradise[:180000]
+    parts = split(src, rng.sample(range(1, len(src)), 6))
+    for level in (1, 6):
+        exp = O.deflater_parts(parts, level=level, format="gzip", file_name="p.txt", mtime=1234567)
+        for at in (1, 2, 4):
+            monkeypatch.setenv("SDZ_DEFLATER_SWITCH_AT", str(at))
+            assert run_deflater(parts, level, "gzip", "p.txt") == exp, (level, at)
+        monkeypatch.delenv("SDZ_DEFLATER_SWITCH_AT")
+    # overlay-overtaken blocks: the record path hands the call back
+    stress = P._overlay_stress(rng, 200000)
+    parts = split(stress, [70000, 130000])
+    exp = O.deflater_parts(parts, level=6, format="deflate", mtime=1234567)
+    assert run_deflater(parts, 6, "deflate") == exp
+
+
+def test_record_path_deflater_large_appends(paradise):
+    """Few large appends (the drop-in's streaming use): per-call bytes as the reference's."""
+    big = paradise * 4
+    parts = split(big, [300000, 1000000, 1500000])
+    for level in (1, 6, 9):
+        exp = O.deflater_parts(parts, level=level, format="deflate", mtime=1234567)
+        assert run_deflater(parts, level, "deflate") == exp, level
