@@ -1550,7 +1550,7 @@ __device__ __forceinline__ void ps_init(PState& st, const DeflateArgs& A, uint32
     st.strstart = 0; st.match_length = MIN_MATCH - 1; st.match_start = 0; st.match_available = 0;
     st.block_start = 0; st.off = 0;
     st.last_lit = 0; st.matches = 0; st.lx = 0; st.nblk = 0; st.sym0 = 0; st.dxb = 0;
-    st.sym = (GLB uint32_t*)A.rec_buf + 2 * A.rp0[sid];
+    st.sym = (GLB uint32_t*)A.sym_buf + 2 * A.rp0[sid];
     st.blk = A.blk + (uint64_t)A.tb0[sid] * FB_SLOT;
     st.nbcap = A.tb0[sid + 1] - A.tb0[sid];
 }
@@ -1938,7 +1938,7 @@ __global__ __launch_bounds__(LZ_THREADS) void k_lz_emit(DeflateArgs A) {
     const GLB uint32_t* s2 = (const GLB uint32_t*)A.lz_s2 + q.rp;
     const GLB uint64_t* e1 = (const GLB uint64_t*)A.lz_e1 + (q.rp >> 6);
     const GLB uint64_t* e2 = (const GLB uint64_t*)A.lz_e2 + (q.rp >> 6);
-    GLB uint32_t* sym = (GLB uint32_t*)A.rec_buf + 2 * q.rp;
+    GLB uint32_t* sym = (GLB uint32_t*)A.sym_buf + 2 * q.rp;
     uint32_t o = A.lz_cnt[seg];
     for (int wi = q.g >> 6; wi <= ((q.h - 1) >> 6); ++wi) {
         const uint64_t m2 = lz_range(wi, q.g, c), m1 = lz_range(wi, c, q.h);
@@ -2010,7 +2010,7 @@ __global__ __launch_bounds__(LB_THREADS) void k_lz_blocks(DeflateArgs A) {
     const int64_t plus = A.level >= 4 ? 1 : 0;
     const bool trunc = A.level > 2;
     const uint32_t fin = A.lz_fin[sid], nsym = fin >> 1, nchk = nsym - (fin & 1u);
-    const GLB uint32_t* sym = (const GLB uint32_t*)A.rec_buf + 2 * A.rp0[sid];
+    const GLB uint32_t* sym = (const GLB uint32_t*)A.sym_buf + 2 * A.rp0[sid];
     GLB uint8_t* slots = (GLB uint8_t*)(A.blk + (uint64_t)A.tb0[sid] * FB_SLOT);
     const uint32_t nbcap = A.tb0[sid + 1] - A.tb0[sid];
     uint32_t nb = 0, b0 = 0;
@@ -2423,7 +2423,7 @@ __global__ __launch_bounds__(64) void k_dfl_trees(DeflateArgs A) {   // grid (n,
     const GLB DTables* T = (const GLB DTables*)&g_dt;
     for (int i = (int)lane; i < 256; i += 64) lcode_t[i] = T->length_code[i];
     for (int i = (int)lane; i < 512; i += 64) dcode_t[i] = T->dist_code[i];
-    const GLB uint32_t* sym = (const GLB uint32_t*)A.rec_buf + 2 * A.rp0[sid];
+    const GLB uint32_t* sym = (const GLB uint32_t*)A.sym_buf + 2 * A.rp0[sid];
     const uint32_t nblk = F->nblk;
     for (uint32_t b = blockIdx.y; b < nblk; b += gridDim.y) {
         GLB FBlock* Bk = (GLB FBlock*)(A.blk + ((uint64_t)A.tb0[sid] + b) * FB_SLOT);
@@ -2619,7 +2619,7 @@ __global__ __launch_bounds__(EN_THREADS) void k_dfl_encode(DeflateArgs A) {
             for (uint32_t i = 0; i < A.fname_len; i++) orbits(80 + 8 * i, A.fname[i]);
         }
     }
-    const GLB uint32_t* sym = (const GLB uint32_t*)A.rec_buf + 2 * A.rp0[sid];
+    const GLB uint32_t* sym = (const GLB uint32_t*)A.sym_buf + 2 * A.rp0[sid];
     uint32_t bad = 0;
     for (uint32_t b = 0; b < nblk; ++b) {
         const GLB FBlock* Bk = blk_at(b);

@@ -28,12 +28,19 @@ int inflate_batch_device(const uint8_t* in, const uint64_t* in_off, const uint64
                          const uint64_t* out_off, const uint64_t* out_cap, sdz_inflate_record* rec, uint32_t n,
                          int32_t format, const uint8_t* dict, uint32_t dict_len, void* stream, const uint64_t* host_len,
                          const uint64_t* host_cap);
+// a Deflater's own record and link buffers (one stream, positions from 0): records below
+// rec_from and links below pv_from are final from earlier calls and not recomputed
+struct DeflateExt {
+    uint64_t* rec;
+    uint16_t* pv;
+    uint64_t rec_from, pv_from;
+};
 // sdz_deflate_batch_device with the input lengths optionally known on the host
 int deflate_batch_device(const uint8_t* in, const uint64_t* in_off, const uint64_t* in_len, uint8_t* out,
                          const uint64_t* out_off, const uint64_t* out_cap, sdz_deflate_record* rec, uint32_t n,
                          int32_t level, int32_t format, const uint8_t* fname, uint32_t fname_len, uint32_t mtime,
                          const uint8_t* dict, uint32_t dict_len, void* stream, const uint64_t* host_len,
-                         uint32_t noflush = 0, const int32_t* cks_in = nullptr);
+                         uint32_t noflush = 0, const int32_t* cks_in = nullptr, const DeflateExt* ext = nullptr);
 
 // Calls on one device are serialised (its pools and side stream are shared; recursive: a
 // host-batch call holds it around the *_device call it makes); calls on different devices

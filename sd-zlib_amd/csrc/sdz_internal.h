@@ -105,6 +105,8 @@ struct DeflateArgs {
     // run over work-unit lists (k << kRecUnitShift | unit)
     uint64_t* rec_buf;           // match records, one per position (null: classic path only)
     uint16_t* pv_buf;            // hash chain links: distance to the previous same-hash position
+    uint32_t* sym_buf;           // the parse's symbols, u32 index 2 rp0[k] (normally rec_buf itself:
+                                 // records are dead once parsed; a Deflater keeps its records)
     const uint64_t* rp0;         // n + 1 entries
     const uint32_t* tb0;         // n + 1 entries
     uint8_t* blk;                // block slots (FB_SLOT bytes each)

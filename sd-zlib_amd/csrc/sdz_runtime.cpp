@@ -141,6 +141,7 @@ Pool g_inflate_scratch, g_deflate_state, g_tmp, g_stage, g_split, g_find;
 // [128, 256) small results, then the file name
 constexpr size_t kTmpMax = 0, kTmpDictId = 64, kTmpFname = 256;
 constexpr uint64_t kInflaterOutCap = 4ull << 20;   // sdz_inflater: output slot per device call
+constexpr size_t kInflaterOnePassMin = 32u << 10;  // sdz_inflater: a first append this long tries the one-pass path
 
 const char* const kZmsg[ZM_COUNT] = {
     "",
@@ -788,7 +789,7 @@ int rt::deflate_batch_device(const uint8_t* in, const uint64_t* in_off, const ui
                              const uint64_t* out_off, const uint64_t* out_cap, sdz_deflate_record* rec, uint32_t n,
                              int32_t level, int32_t format, const uint8_t* fname, uint32_t fname_len, uint32_t mtime,
                              const uint8_t* dict, uint32_t dict_len, void* stream, const uint64_t* host_len,
-                             uint32_t noflush, const int32_t* cks_in) {
+                             uint32_t noflush, const int32_t* cks_in, const DeflateExt* ext) {
     if (int rc = ensure_device()) return rc;
     if (n == 0) return SDZ_API_OK;
     if (level < 1 || level > 9) return fail(SDZ_API_BAD_ARG, "level must be between 1 and 9, inclusive");
@@ -851,7 +852,7 @@ int rt::deflate_batch_device(const uint8_t* in, const uint64_t* in_off, const ui
         lz_shift = 9;
         while (lz_shift < 12 && (tot >> (lz_shift + 1)) >= 65536) ++lz_shift;
         if (fastlv) lz_shift = std::max(7u, lz_shift - 2);      // deflate_fast: its state is the position alone
-        else if (tot >= (mx << 15) && !noflush) lz_shift = 0;
+        else if (tot >= (mx << 15) && !noflush && !ext) lz_shift = 0;
         if (const char* e = getenv("SDZ_LZ_SHIFT"))            // tests: segment size 2^6 .. 2^16
             lz_shift = (uint32_t)std::min(16, std::max(6, atoi(e)));
     }
@@ -944,8 +945,11 @@ int rt::deflate_batch_device(const uint8_t* in, const uint64_t* in_off, const ui
                 blk += nb;
                 nbmax = std::max(nbmax, nb);
                 const uint32_t ms = deflate_match_segs(len[i]);
-                for (uint32_t u = 0; u < ms; ++u) units.push_back(k << kRecUnitShift | u);
-                nm += ms;
+                for (uint32_t u = 0; u < ms; ++u) {
+                    if (ext && (uint64_t)(u + 1) * 16384 <= ext->rec_from) continue;   // final from earlier calls
+                    units.push_back(k << kRecUnitShift | u);
+                    ++nm;
+                }
             }
             rp0[m] = pos;
             tb0[m] = blk;
@@ -953,7 +957,10 @@ int rt::deflate_batch_device(const uint8_t* in, const uint64_t* in_off, const ui
             for (uint32_t k = 0; k < m; ++k) {
                 if (rp0[k] == ~0ull) continue;
                 const uint32_t cu = deflate_chain_units(len[b + k]);
-                for (uint32_t u = 0; u < cu; ++u) units.push_back(k << kRecUnitShift | u);
+                for (uint32_t u = 0; u < cu; ++u) {
+                    if (ext && 65536ull + (uint64_t)u * 32768 <= ext->pv_from) continue;
+                    units.push_back(k << kRecUnitShift | u);
+                }
             }
             // parse segments: sg0 (m + 1), then the stream of each segment
             std::vector<uint32_t> lzs;
@@ -971,8 +978,15 @@ int rt::deflate_batch_device(const uint8_t* in, const uint64_t* in_off, const ui
             uint8_t* B = (uint8_t*)state;
             size_t o = (size_t)m * slab;
             auto take = [&](size_t bytes) { uint8_t* p = B + o; o += (bytes + 255) & ~(size_t)255; return p; };
-            a.rec_buf = (uint64_t*)take((size_t)pos * 8);
-            a.pv_buf = (uint16_t*)take((size_t)pos * 2);
+            if (ext) {                                    // a Deflater's own records and links
+                a.rec_buf = ext->rec;
+                a.pv_buf = ext->pv;
+                a.sym_buf = (uint32_t*)take((size_t)pos * 8);
+            } else {
+                a.rec_buf = (uint64_t*)take((size_t)pos * 8);
+                a.pv_buf = (uint16_t*)take((size_t)pos * 2);
+                a.sym_buf = (uint32_t*)a.rec_buf;
+            }
             a.blk = take((size_t)blk * FB_SLOT_BYTES);
             a.cks = (int32_t*)take((size_t)m * 4);
             uint64_t* d_rp0 = (uint64_t*)take(((size_t)m + 1) * 8);
@@ -1244,8 +1258,15 @@ struct sdz_inflater {
     sdz_inflate_record* d_rec = nullptr;
     std::vector<uint8_t> out;
     uint64_t in_total = 0;                        // stream bytes passed before this append
+    // a first append holding a whole stream went through the one-pass path (block-parallel
+    // decode); later appends return its final record again, as the incremental state would
+    bool one_pass = false;
+    sdz_inflate_record done_rec{};
+    uint8_t* d_big = nullptr;
+    size_t big_cap = 0;
     ~sdz_inflater() {
-        for (void* p : { (void*)d_state, (void*)d_dict, (void*)d_in, (void*)d_out, (void*)d_meta, (void*)d_rec })
+        for (void* p : { (void*)d_state, (void*)d_dict, (void*)d_in, (void*)d_out, (void*)d_meta, (void*)d_rec,
+                         (void*)d_big })
             if (p) hipFree(p);
     }
 };
@@ -1287,7 +1308,47 @@ int sdz_inflater_append(sdz_inflater* z, const uint8_t* data, size_t len, const 
         z->in_cap = std::max<size_t>(len + 64, 1 << 16);
         HIPCHK(hipMalloc(&z->d_in, z->in_cap));
     }
+    if (z->one_pass) {
+        *rec = z->done_rec;
+        rec->out_len = 0;
+        *out = z->out.data();
+        *out_len = 0;
+        return SDZ_API_OK;
+    }
     if (len) HIPCHK(hipMemcpy(z->d_in, data, len, hipMemcpyHostToDevice));
+    if (z->in_total == 0 && len >= kInflaterOnePassMin && !getenv("SDZ_INFLATER_STREAM_ONLY")) {
+        // The first append, a large one: when the stream ends inside it (one buffer appended
+        // whole, the common use) the one-pass path -- block-parallel decode of long streams
+        // (k_split.hip) -- gives the same bytes and the same record (its running checksum is
+        // counted from the stream start, as an append's from its own output start).  Anything
+        // else (the stream continues, an error, output past the slot) leaves no trace: the
+        // incremental path below runs as before.
+        const uint64_t cap = std::min<uint64_t>((uint64_t)len * 8 + (1u << 20), 1ull << 31);
+        if (cap + 64 > z->big_cap) {
+            if (z->d_big) hipFree(z->d_big);
+            z->d_big = nullptr;
+            z->big_cap = cap + 64;
+            HIPCHK(hipMalloc(&z->d_big, z->big_cap));
+        }
+        uint64_t meta[4] = { 0, len, 0, cap };
+        HIPCHK(hipMemcpy(z->d_meta, meta, sizeof meta, hipMemcpyHostToDevice));
+        int rc = sdz_inflate_batch_device(z->d_in, z->d_meta, z->d_meta + 1, z->d_big, z->d_meta + 2, z->d_meta + 3,
+                                          z->d_rec, 1, z->format, z->d_dict, z->dict_len, nullptr);
+        if (rc) return rc;
+        sdz_inflate_record r{};
+        HIPCHK(hipMemcpy(&r, z->d_rec, sizeof r, hipMemcpyDeviceToHost));
+        if (r.status == SDZ_OK) {
+            z->out.resize(r.out_len);
+            if (r.out_len) HIPCHK(hipMemcpy(z->out.data(), z->d_big, r.out_len, hipMemcpyDeviceToHost));
+            z->one_pass = true;
+            z->done_rec = r;
+            z->in_total += len;
+            *rec = r;
+            *out = z->out.data();
+            *out_len = z->out.size();
+            return SDZ_API_OK;
+        }
+    }
     // more calls while the output slot fills up; each passes the chunk's bytes the device
     // did not take (record in_used: stream offset of the first byte not consumed or held)
     for (uint64_t from = 0;;) {
@@ -1351,9 +1412,15 @@ struct sdz_deflater {
     size_t all_cap = 0;
     int32_t* d_ck = nullptr;
     std::vector<uint8_t> trailer;                 // a second finish() returns it again
+    // the record path's records and links, kept between calls: only the positions the new
+    // bytes can change are searched again (records from MIN_LOOKAHEAD before the old end,
+    // links from 2 before it)
+    uint64_t* d_recs = nullptr;
+    uint16_t* d_links = nullptr;
+    size_t recs_cap = 0;                          // positions
     ~sdz_deflater() {
         for (void* p : { (void*)d_state, (void*)d_dict, (void*)d_in, (void*)d_out, (void*)d_meta, (void*)d_rec,
-                         (void*)d_all, (void*)d_ck })
+                         (void*)d_all, (void*)d_ck, (void*)d_recs, (void*)d_links })
             if (p) hipFree(p);
     }
 };
@@ -1404,6 +1471,9 @@ int deflater_to_serial(sdz_deflater* z, size_t upto_calls) {
     std::vector<uint8_t>().swap(z->hist);
     std::vector<size_t>().swap(z->calls);
     if (z->d_all) { hipFree(z->d_all); z->d_all = nullptr; z->all_cap = 0; }
+    if (z->d_recs) { hipFree(z->d_recs); z->d_recs = nullptr; }
+    if (z->d_links) { hipFree(z->d_links); z->d_links = nullptr; }
+    z->recs_cap = 0;
     return SDZ_API_OK;
 }
 
@@ -1440,10 +1510,27 @@ int deflater_record_call(sdz_deflater* z, const uint8_t* data, size_t len, int32
     uint64_t meta[4] = { 0, total, 0, cap };
     HIPCHK(hipMemcpy(z->d_meta, meta, sizeof meta, hipMemcpyHostToDevice));
     HIPCHK(hipMemset(z->d_rec, 0xff, sizeof(sdz_deflate_record)));      // a handed-back stream leaves it so
+    const size_t npos = (total + 63) & ~(size_t)63;
+    if (npos > z->recs_cap) {                         // grow, keeping what earlier calls found
+        const size_t c = std::max<size_t>(npos, 2 * z->recs_cap);
+        uint64_t* r = nullptr;
+        uint16_t* l = nullptr;
+        HIPCHK(hipMalloc(&r, c * 8));
+        HIPCHK(hipMalloc(&l, c * 2 + 256));
+        if (z->recs_cap) {
+            HIPCHK(hipMemcpy(r, z->d_recs, z->recs_cap * 8, hipMemcpyDeviceToDevice));
+            HIPCHK(hipMemcpy(l, z->d_links, z->recs_cap * 2, hipMemcpyDeviceToDevice));
+        }
+        if (z->d_recs) hipFree(z->d_recs);
+        if (z->d_links) hipFree(z->d_links);
+        z->d_recs = r; z->d_links = l; z->recs_cap = c;
+    }
+    const uint64_t old = z->total;
+    rt::DeflateExt ext{ z->d_recs, z->d_links, old >= 262 ? old - 262 : 0, old >= 2 ? old - 2 : 0 };
     int rc = rt::deflate_batch_device(z->d_all, z->d_meta, z->d_meta + 1, z->d_out, z->d_meta + 2, z->d_meta + 3,
                                       z->d_rec, 1, z->level, z->format, z->fname.empty() ? nullptr : z->fname.data(),
                                       (uint32_t)z->fname.size(), z->mtime, nullptr, 0, nullptr, &total,
-                                      finish ? 0u : 1u, z->d_ck);
+                                      finish ? 0u : 1u, z->d_ck, &ext);
     if (rc) return rc;
     sdz_deflate_record r{};
     HIPCHK(hipMemcpy(&r, z->d_rec, sizeof r, hipMemcpyDeviceToHost));

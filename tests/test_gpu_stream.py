@@ -296,3 +296,38 @@ def test_gzip_long_file_name_kept():
     out = b"".join(inf.append(comp))
     res = inf.finish()
     assert out == data and res["success"] and res["fileName"] == name
+
+
+def test_inflater_one_pass_first_append(monkeypatch):
+    """A first append of >= 32 KiB holding a whole stream takes the one-pass path (block-parallel
+    decode): its bytes and record equal the incremental path's; a stream continuing past the
+    append, or an error, falls back to the incremental path untouched."""
+    comp = golden("paradiselost.gz")
+    text = golden("paradiselost.txt")
+
+    def one(parts):
+        inf = sdz.Inflater()
+        out = b"".join(b"".join(inf.append(p)) for p in parts)
+        return out, inf.finish()
+    a = one([comp])
+    monkeypatch.setenv("SDZ_INFLATER_STREAM_ONLY", "1")
+    b = one([comp])
+    monkeypatch.delenv("SDZ_INFLATER_STREAM_ONLY")
+    assert a == b and a[0] == text and a[1]["success"] and a[1]["fileName"] == "paradiselost.txt"
+    # the stream continues past the first append: the incremental path, as before
+    c = one([comp[:100000], comp[100000:]])
+    assert c == a
+    # a damaged stream: the same error either way
+    bad = bytearray(golden("paradiselost.deflate"))
+    bad[50000] ^= 0xFF
+    errs = []
+    for env in (None, "1"):
+        if env:
+            monkeypatch.setenv("SDZ_INFLATER_STREAM_ONLY", env)
+        inf = sdz.Inflater()
+        try:
+            inf.append(bytes(bad))
+            errs.append(("ok", inf.finish()["success"]))
+        except sdz.SdzError as e:
+            errs.append(("err", str(e)))
+    assert errs[0] == errs[1]

@@ -47,6 +47,15 @@ def main():
     print("Inflater 64K appends %s ms" % t(inf_64k), flush=True)
     print("deflate() L6         %s ms" % t(lambda: sdz.deflate(text, {"level": 6})), flush=True)
     print("Deflater one append  %s ms" % t(def_whole, 1), flush=True)
+    big = text * 10
+
+    def def_stream():
+        d = sdz.Deflater({"level": 6})
+        for o in range(0, len(big), 65536):
+            d.append(big[o:o + 65536])
+        d.finish()
+    print("Deflater 4.7 MB in 64 KiB appends %s ms" % t(def_stream, 1), flush=True)
+    print("deflate() 4.7 MB     %s ms" % t(lambda: sdz.deflate(big, {"level": 6}), 2), flush=True)
 
 
 if __name__ == "__main__":
