@@ -1389,6 +1389,323 @@ __global__ __launch_bounds__(PM_THREADS) void k_dfl_match(DeflateArgs A) {
     }
 }
 
+// ------------------------------------------------------------------ levels 4-9: search over 4-byte chains
+// longest_match (deflate.ts:827-946) from best_len = 2 returns the first candidate (most recent)
+// of maximal length among the first K = max_chain entries of the hash chain -- each above `limit`
+// but the first, which may sit at MAX_DIST -- cut at the first one reaching nice_match.  A
+// candidate passes its pre-check only if bytes 0-1 agree, and with an equal 15-bit hash byte 2
+// then agrees too (HASH_SHIFT 5: byte 2's bits are the hash's low 5 and, xor'd with byte 1, the
+// next 3).  So a result of 4 or more comes from the positions sharing the first 4 bytes, and a
+// result of 3 is the first chain entry whose bytes 0-1 agree.  Text chains hold ~3x more entries
+// than share 4 bytes (paradiselost.txt at L6: 35.8 candidates per search against 11.4), so:
+//   k_dfl_link4  per position x, the first entry of x's chain (within the K that x's own search
+//                could visit) that shares x's first 4 bytes, and its rank there (the gap).  Ranks
+//                add up along a 4-byte chain -- the chain of link4(x) continues x's chain -- so a
+//                walk from p knows each 4-byte candidate's rank in p's chain from the gaps alone,
+//                and a link whose gap passes K can never be followed from anywhere;
+//   k_dfl_match4 per position, the walk over that 4-byte chain with the window, links and gaps
+//                in LDS, then (when no candidate of 4+ bytes is in the window) the rank-1 entry
+//                checked for a 3-byte match -- the chain walked further only for a hash collision.
+// Both chain lengths come from one walk as in k_dfl_match (the quarter window is ranks <= K/4).
+// Link word: (gap - 1) << 16 | distance, 0 if none (k_dfl_match4 stages it packed, m4_pack).
+#define L4_CHUNK 128
+#ifndef L4_WALKERS
+#define L4_WALKERS 2
+#endif
+__global__ __launch_bounds__(PM_THREADS) void k_dfl_link4(DeflateArgs A) {
+    __shared__ __attribute__((aligned(16))) uint8_t win[(PM_WINB + 15) & ~15];
+    __shared__ __attribute__((aligned(16))) uint16_t pvl[PM_PV];
+    __shared__ int pm_next;
+    const uint32_t tid = threadIdx.x;
+    const uint32_t lane = tid & 63u, wv = tid >> 6;
+    // four consecutive units (a stream's segments: they share history) on one XCD (block % 8)
+    const uint32_t bb = blockIdx.x, u = (bb & ~31u) | ((bb & 7u) << 2) | ((bb >> 3) & 3u);
+    if (u >= A.nmseg) return;
+    const uint32_t sid = A.mseg[u] >> kRecUnitShift, seg = A.mseg[u] & ((1u << kRecUnitShift) - 1);
+    const uint64_t rp = A.rp0[sid];
+    if (rp == ~0ull) return;
+    const int n = (int)A.in_len[sid];
+    const int tail = n > PM_TAIL ? n - PM_TAIL : 0;
+    const int s0 = (int)(seg * PM_SEG), s1 = s0 + PM_SEG < tail ? s0 + PM_SEG : tail;
+    if (s0 >= s1) return;
+    const int ws = s0 > W_SIZE ? s0 - W_SIZE : 0;
+    const int we = s1 + MAX_MATCH + 8 < n ? s1 + MAX_MATCH + 8 : n;
+    const GLB uint8_t* in = (const GLB uint8_t*)(A.in + A.in_off[sid]);
+    const GLB uint16_t* pv = (const GLB uint16_t*)A.pv_buf + rp;
+    {                                                      // staging as k_dfl_match
+        const int nw = (we - ws) >> 2;
+        uint32_t* w32 = (uint32_t*)win;
+        for (int i = (int)tid; i < nw; i += PM_THREADS) {
+            uint32_t v;
+            __builtin_memcpy(&v, (const uint8_t*)(in + ws + 4 * i), 4);
+            w32[i] = v;
+        }
+        for (int i = 4 * nw + (int)tid; i < we - ws; i += PM_THREADS) win[i] = in[ws + i];
+        const int np = (s1 - ws) >> 1;
+        uint32_t* p32 = (uint32_t*)pvl;
+        for (int i = (int)tid; i < np; i += PM_THREADS) {
+            const uint32_t v = *(const GLB uint32_t*)(pv + ws + 2 * i);
+            const uint32_t lo = v & 0xffffu, hi = v >> 16;
+            const uint32_t r0 = 2u * (uint32_t)i, r1 = r0 + 1u;
+            p32[i] = (lo && lo < r0 ? r0 - lo : 0u) | ((hi && hi < r1 ? r1 - hi : 0u) << 16);
+        }
+        for (int i = 2 * np + (int)tid; i < s1 - ws; i += PM_THREADS) {
+            const uint32_t v = pv[ws + i];
+            pvl[i] = (uint16_t)(v && v < (uint32_t)i ? (uint32_t)i - v : 0u);
+        }
+        if (tid == 0) pm_next = s0 + (PM_THREADS / 64) * L4_CHUNK;
+    }
+    __syncthreads();
+    GLB uint32_t* l4 = (GLB uint32_t*)A.l4_buf + rp;
+    const int K = c_config[A.level][3];
+    const int c0 = s0 + (int)wv * L4_CHUNK;
+    int next = c0 < s1 ? c0 : s1;
+    int q1 = c0 + L4_CHUNK < s1 ? c0 + L4_CHUNK : s1;
+    // L4_WALKERS walks per lane, stepped together so their LDS round trips overlap.  Per walk:
+    // r the rank of cur in p's chain (0: idle), res the link word found so far
+    int p[L4_WALKERS], sp[L4_WALKERS], cur[L4_WALKERS], r[L4_WALKERS], limit[L4_WALKERS];
+    uint32_t s4[L4_WALKERS], res[L4_WALKERS];
+    bool pend[L4_WALKERS];
+#pragma unroll
+    for (int k = 0; k < L4_WALKERS; ++k) { p[k] = s0; sp[k] = cur[k] = r[k] = limit[k] = 0; s4[k] = res[k] = 0; pend[k] = false; }
+    for (;;) {
+        uint64_t im[L4_WALKERS];
+        int nidle = 0;
+#pragma unroll
+        for (int k = 0; k < L4_WALKERS; ++k) { im[k] = __ballot(r[k] <= 0); nidle += __popcll(im[k]); }
+        if (nidle >= PM_REFILL || nidle == 64 * L4_WALKERS) {
+#pragma unroll
+            for (int k = 0; k < L4_WALKERS; ++k)
+                if (pend[k]) { l4[p[k]] = res[k]; pend[k] = false; }
+            if (next >= q1) {
+                const int b = __builtin_amdgcn_readfirstlane(lane == 0 ? atomicAdd(&pm_next, L4_CHUNK) : 0);
+                if (b < s1) {
+                    next = b;
+                    q1 = b + L4_CHUNK < s1 ? b + L4_CHUNK : s1;
+                }
+            }
+            if (next >= q1 && nidle == 64 * L4_WALKERS) break;
+#pragma unroll
+            for (int k = 0; k < L4_WALKERS; ++k) {
+                if (next < q1) {
+                    const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(im[k] >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)im[k], 0u));
+                    const int pn = next + (int)rank;
+                    next += __popcll(im[k]);
+                    if (r[k] <= 0 && pn < q1) {
+                        p[k] = pn;
+                        sp[k] = pn - ws;
+                        cur[k] = pvl[sp[k]];
+                        limit[k] = (pn > MAX_DIST ? pn - MAX_DIST : 0) - ws;
+                        s4[k] = pm_w4(win, (uint32_t)sp[k]);
+                        res[k] = 0;
+                        const bool go = cur[k] != 0 && sp[k] - cur[k] <= MAX_DIST;   // the first entry (deflate.ts:1092)
+                        r[k] = go ? 1 : 0;
+                        pend[k] = !go;
+                    }
+                }
+            }
+        }
+        uint32_t x[L4_WALKERS];
+        int nc[L4_WALKERS];
+#pragma unroll
+        for (int k = 0; k < L4_WALKERS; ++k) {            // all reads first: one round trip for all walks
+            const int c = r[k] > 0 ? cur[k] : sp[k];
+            x[k] = pm_w4(win, (uint32_t)c) ^ s4[k];
+            nc[k] = pvl[c];
+        }
+#pragma unroll
+        for (int k = 0; k < L4_WALKERS; ++k) {            // one chain entry per walk and step
+            const bool live = r[k] > 0, hit = live && x[k] == 0;
+            res[k] = hit ? ((uint32_t)(r[k] - 1) << 16) | (uint32_t)(sp[k] - cur[k]) : res[k];
+            const bool fin = live && (hit || nc[k] <= limit[k] || r[k] >= K);   // (nc == 0: the chain ends)
+            cur[k] = live ? nc[k] : cur[k];
+            r[k] = fin ? 0 : live ? r[k] + 1 : r[k];
+            pend[k] = pend[k] || fin;
+        }
+    }
+}
+
+#ifndef M4_SUB
+#define M4_SUB PM_SEG                                    // positions per workgroup
+#endif
+#define M4_NSUB (PM_SEG / M4_SUB)
+#define M4_WINB (W_SIZE + M4_SUB + MAX_MATCH + 16)
+#define M4_PV (W_SIZE + M4_SUB)
+static uint32_t match4_blocks(uint32_t nmseg) { return (nmseg * M4_NSUB + 127u) & ~127u; }
+static uint32_t link4_blocks(uint32_t nmseg) { return (nmseg + 31u) & ~31u; }
+// A link staged in LDS as 16 bits: distance << 3 | gap for distances below 8192 and gaps up to 7
+// (~94 % of the links walked on text); 0: none; else 8 (the word is read from HBM)
+__device__ __forceinline__ uint16_t m4_pack(uint32_t v) {
+    const uint32_t d = v & 0xffffu, g = (v >> 16) + 1u;
+    return (uint16_t)(d == 0u ? 0u : d < 8192u && g <= 7u ? d << 3 | g : 8u);
+}
+__device__ __forceinline__ void m4_link(const uint16_t* lk, const GLB uint32_t* l4g, int x, int& dist, int& gap) {
+    if (x < 0) { dist = 0; gap = 0; return; }
+    const uint32_t e = lk[x];
+    if (e & 7u) { dist = (int)(e >> 3); gap = (int)(e & 7u); return; }
+    const uint32_t v = e ? l4g[x] : 0u;
+    dist = (int)(v & 0xffffu);
+    gap = (int)(v >> 16) + 1;
+}
+// window bytes x .. x + 15 as 4 words (5 aligned dword reads)
+__device__ __forceinline__ void m4_w16(const uint8_t* w, uint32_t x, uint32_t (&m)[4]) {
+    const uint32_t* w32 = (const uint32_t*)w + (x >> 2);
+    const uint32_t s = x & 3u;
+    uint32_t d[5];
+#pragma unroll
+    for (int i = 0; i < 5; ++i) d[i] = w32[i];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) m[i] = __builtin_amdgcn_alignbyte(d[i + 1], d[i], s);
+}
+// equal leading bytes of two 16-byte strings, from their xor words (16: all equal)
+__device__ __forceinline__ int m4_lcp16(uint32_t x0, uint32_t x1, uint32_t x2, uint32_t x3) {
+    const int k = x0 ? 0 : x1 ? 4 : x2 ? 8 : x3 ? 12 : 16;
+    const uint32_t x = x0 ? x0 : x1 ? x1 : x2 ? x2 : x3;
+    return k == 16 ? 16 : k + (int)(__builtin_ctz(x) >> 3);
+}
+// the first chain entry (in rank order) with bytes 0-1 equal to p's (a 3-byte match, see above),
+// walked over the HBM links past a hash collision at rank 1: rank << 16 | its position relative
+// to ws, 0 if none within K (positions relative to ws)
+__device__ __forceinline__ uint32_t m4_first3(const GLB uint16_t* pv, const uint8_t* win, int ws, int sp, int first,
+                                              int limit, int K) {
+    const uint32_t b0 = win[sp], b1 = win[sp + 1];
+    int c = first;
+    for (int r = 1; r <= K; ++r) {
+        if (win[c] == b0 && win[c + 1] == b1) return (uint32_t)r << 16 | (uint32_t)c;
+        const int d = (int)pv[c + ws];
+        c -= d;
+        if (d == 0 || c <= limit) return 0u;
+    }
+    return 0u;
+}
+__global__ __launch_bounds__(PM_THREADS) void k_dfl_match4(DeflateArgs A) {
+    __shared__ __attribute__((aligned(16))) uint8_t win[(M4_WINB + 15) & ~15];
+    __shared__ __attribute__((aligned(16))) uint16_t lk[M4_PV];   // m4_pack words
+    __shared__ int pm_next;
+    const uint32_t tid = threadIdx.x;
+    const uint32_t lane = tid & 63u, wv = tid >> 6;
+    // block -> (unit, part): of each 128 blocks, the 16 on XCD x (block % 8) take items 16 x .. 16 x + 15
+    const uint32_t bb = blockIdx.x, item = (bb & ~127u) | ((bb & 7u) << 4) | ((bb >> 3) & 15u);
+    const uint32_t u = item / M4_NSUB, part = item % M4_NSUB;
+    if (u >= A.nmseg) return;
+    const uint32_t sid = A.mseg[u] >> kRecUnitShift, seg = A.mseg[u] & ((1u << kRecUnitShift) - 1);
+    const uint64_t rp = A.rp0[sid];
+    if (rp == ~0ull) return;
+    const int n = (int)A.in_len[sid];
+    const int tail = n > PM_TAIL ? n - PM_TAIL : 0;
+    const int g1 = (int)(seg * PM_SEG) + PM_SEG < tail ? (int)(seg * PM_SEG) + PM_SEG : tail;
+    const int s0 = (int)(seg * PM_SEG + part * M4_SUB), s1 = s0 + M4_SUB < g1 ? s0 + M4_SUB : g1;
+    if (s0 >= s1) return;
+    const int ws = s0 > W_SIZE ? s0 - W_SIZE : 0;
+    const int we = s1 + MAX_MATCH + 8 < n ? s1 + MAX_MATCH + 8 : n;
+    const GLB uint8_t* in = (const GLB uint8_t*)(A.in + A.in_off[sid]);
+    const GLB uint16_t* pv = (const GLB uint16_t*)A.pv_buf + rp;
+    const GLB uint32_t* l4g = (const GLB uint32_t*)A.l4_buf + rp + ws;   // relative to ws
+    {
+        const int nw = (we - ws) >> 2;
+        uint32_t* w32 = (uint32_t*)win;
+        for (int i = (int)tid; i < nw; i += PM_THREADS) {
+            uint32_t v;
+            __builtin_memcpy(&v, (const uint8_t*)(in + ws + 4 * i), 4);
+            w32[i] = v;
+        }
+        for (int i = 4 * nw + (int)tid; i < we - ws; i += PM_THREADS) win[i] = in[ws + i];
+        for (int i = (int)tid; i < s1 - ws; i += PM_THREADS) lk[i] = m4_pack(l4g[i]);
+        if (tid == 0) pm_next = s0 + (PM_THREADS / 64) * PM_CHUNK;
+    }
+    __syncthreads();
+    GLB uint64_t* rec = (GLB uint64_t*)A.rec_buf + rp;
+    const int K = c_config[A.level][3], Kq = K >> 2, nice = c_config[A.level][2];
+    const int c0 = s0 + (int)wv * PM_CHUNK;
+    int next = c0 < s1 ? c0 : s1;
+    int q1 = c0 + PM_CHUNK < s1 ? c0 + PM_CHUNK : s1;
+    // per lane: position p (sp relative to ws), its chain's first entry and limit (relative),
+    // the 4-byte candidate cur with its rank cum; live: walking; srch: p searches at all
+    int p = s0, sp = 0, cur = 0, cum = 0, first = 0, limit = 0, best = 2, bpos = 0, qbest = 2, qpos = 0;
+    uint32_t pw[4] = { 0, 0, 0, 0 };                         // p's bytes 4-19
+    bool live = false, pend = false, srch = false;
+    for (;;) {
+        const uint64_t im = __ballot(!live);
+        const int nidle = __popcll(im);
+        if (nidle >= PM_REFILL || nidle == 64) {
+            if (pend) {
+                if (srch && qbest < 4) {                     // 3-byte matches (rank-1 entry, or past a collision)
+                    const uint32_t f = m4_first3(pv, win, ws, sp, first, limit, K);
+                    const int r3 = (int)(f >> 16), f3 = (int)(f & 0xffffu);
+                    if (r3 && best < 4) { best = 3; bpos = f3; }
+                    if (r3 && r3 <= Kq) { qbest = 3; qpos = f3; }
+                }
+                const uint32_t full = best > MIN_MATCH - 1 ? ((uint32_t)best << 16) | (uint32_t)(sp - bpos) : 0u;
+                const uint32_t quarter = qbest > MIN_MATCH - 1 ? ((uint32_t)qbest << 16) | (uint32_t)(sp - qpos) : 0u;
+                rec[p] = rec_word(full, quarter, win[p > 0 ? sp - 1 : 0]);
+                pend = false;
+            }
+            if (next >= q1) {
+                const int b = __builtin_amdgcn_readfirstlane(lane == 0 ? atomicAdd(&pm_next, PM_CHUNK) : 0);
+                if (b < s1) {
+                    next = b;
+                    q1 = b + PM_CHUNK < s1 ? b + PM_CHUNK : s1;
+                }
+            }
+            if (next >= q1 && nidle == 64) break;
+            if (next < q1) {
+                const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(im >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)im, 0u));
+                const int pn = next + (int)rank;
+                next += nidle;
+                if (!live && pn < q1) {
+                    p = pn;
+                    sp = p - ws;
+                    const int d3 = (int)pv[p];
+                    srch = d3 != 0 && d3 <= MAX_DIST;          // deflate.ts:1092
+                    first = sp - d3;
+                    limit = (p > MAX_DIST ? p - MAX_DIST : 0) - ws;
+                    best = 2; bpos = 0; qbest = 2; qpos = 0;
+                    m4_w16(win, (uint32_t)(sp + 4), pw);
+                    int l = 0;
+                    cum = 0;
+                    m4_link(lk, l4g, srch ? sp : -1, l, cum);
+                    cur = sp - l;
+                    live = l != 0 && cum <= K && (cum == 1 || cur > limit);
+                    pend = !live;
+                }
+            }
+        }
+        if (live) {
+            // one LDS round trip per candidate: its link and gap, and its bytes 4-19 against p's
+            // (in registers); no pre-check at best -- every 4-byte candidate's length is found
+            int nl, ng;
+            m4_link(lk, l4g, cur, nl, ng);
+            uint32_t m[4];
+            m4_w16(win, (uint32_t)(cur + 4), m);
+            int len = 4 + m4_lcp16(m[0] ^ pw[0], m[1] ^ pw[1], m[2] ^ pw[2], m[3] ^ pw[3]);
+            bool more = len == 20;
+            while (__ballot(more)) {                           // matches past 20 bytes
+                if (more) {
+                    uint32_t a[4], b[4];
+                    m4_w16(win, (uint32_t)(cur + len), a);
+                    m4_w16(win, (uint32_t)(sp + len), b);
+                    const int d = m4_lcp16(a[0] ^ b[0], a[1] ^ b[1], a[2] ^ b[2], a[3] ^ b[3]);
+                    len += d;
+                    more = d == 16 && len < MAX_MATCH;
+                }
+            }
+            len = len > MAX_MATCH ? MAX_MATCH : len;
+            const bool upd = len > best;
+            best = upd ? len : best;
+            bpos = upd ? cur : bpos;
+            const bool cap = cum <= Kq;
+            qbest = cap ? best : qbest;
+            qpos = cap ? bpos : qpos;
+            const int ncur = cur - nl, ncum = cum + ng;
+            const bool fin = (upd && len >= nice) || nl == 0 || ncum > K || ncur <= limit;
+            cur = ncur;
+            cum = ncum;
+            live = !fin;
+            pend = pend || fin;
+        }
+    }
+}
+
 // ------------------------------------------------------------------ record path: tail, parse, trees, encode
 // After k_dfl_chain / k_dfl_match the rest of deflate_slow is split by what it depends on:
 //   k_dfl_tail   records of the last PM_TAIL positions (the reference's longest_match itself);
@@ -2770,7 +3087,10 @@ void launch_deflate(const DeflateArgs& a, hipStream_t st, hipStream_t side, hipE
         if (a.ncunit)
             hipLaunchKernelGGL(k_dfl_chain, dim3((a.ncunit + CH_WAVES - 1) / CH_WAVES), dim3(64 * CH_WAVES), 0, st, a);
         if (!fastlv) {
-            if (a.nmseg) hipLaunchKernelGGL(k_dfl_match, dim3(a.nmseg), dim3(PM_THREADS), 0, st, a);
+            if (a.nmseg && a.l4_buf) {                        // the 4-byte chains
+                hipLaunchKernelGGL(k_dfl_link4, dim3(link4_blocks(a.nmseg)), dim3(PM_THREADS), 0, st, a);
+                hipLaunchKernelGGL(k_dfl_match4, dim3(match4_blocks(a.nmseg)), dim3(PM_THREADS), 0, st, a);
+            } else if (a.nmseg) hipLaunchKernelGGL(k_dfl_match, dim3(a.nmseg), dim3(PM_THREADS), 0, st, a);
             hipLaunchKernelGGL(k_dfl_tail, dim3(a.n), dim3(256), 0, st, a);
         }
         const bool fork = side && ev && hipEventRecord(ev, st) == hipSuccess &&

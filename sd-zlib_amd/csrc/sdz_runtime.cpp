@@ -142,6 +142,7 @@ Pool g_inflate_scratch, g_deflate_state, g_tmp, g_stage, g_split, g_find;
 constexpr size_t kTmpMax = 0, kTmpDictId = 64, kTmpFname = 256;
 constexpr uint64_t kInflaterOutCap = 4ull << 20;   // sdz_inflater: output slot per device call
 constexpr size_t kInflaterOnePassMin = 32u << 10;  // sdz_inflater: a first append this long tries the one-pass path
+constexpr bool kMatch4Default = false;           // deflate levels 4-9: the 4-byte chain search (SDZ_MATCH4)
 
 const char* const kZmsg[ZM_COUNT] = {
     "",
@@ -861,8 +862,13 @@ int rt::deflate_batch_device(const uint8_t* in, const uint64_t* in_off, const ui
         if (noflush) l = l >= 262 ? l - 261 : 0;
         return lz_shift ? (l + (1ull << lz_shift) - 1) >> lz_shift : 0;
     };
-    // per position: record 8, link 2, parse words 8 + 4 + 3 bitmaps; per segment 28
-    const uint64_t kPosBytes = lz_shift ? 8 + 2 + 8 + 4 + 1 : 8 + 2;
+    // levels 4-9 search over 4-byte chains (k_dfl_link4 / k_dfl_match4; SDZ_MATCH4=1 / 0 overrides the default);
+    // a Deflater keeps its own records and links between calls and stays on k_dfl_match
+    const char* m4e = getenv("SDZ_MATCH4");
+    const bool m4_on = m4e ? m4e[0] == '1' : kMatch4Default;
+    const bool match4 = recpath && !ext && level >= 4 && m4_on;
+    // per position: record 8, link 2, parse words 8 + 4 + 3 bitmaps, 4-byte link 4; per segment 28
+    const uint64_t kPosBytes = (lz_shift ? 8 + 2 + 8 + 4 + 1 : 8 + 2) + (match4 ? 4 : 0);
     auto rec_cost = [&](uint32_t i) -> uint64_t {
         if (!on_path(i)) return 0;
         const uint64_t p = (len[i] + 63) & ~63ull;
@@ -986,6 +992,7 @@ int rt::deflate_batch_device(const uint8_t* in, const uint64_t* in_off, const ui
                 a.rec_buf = (uint64_t*)take((size_t)pos * 8);
                 a.pv_buf = (uint16_t*)take((size_t)pos * 2);
                 a.sym_buf = (uint32_t*)a.rec_buf;
+                if (match4) a.l4_buf = (uint32_t*)take((size_t)pos * 4);
             }
             a.blk = take((size_t)blk * FB_SLOT_BYTES);
             a.cks = (int32_t*)take((size_t)m * 4);

@@ -347,6 +347,51 @@ def test_deflate_record_path_bitexact(paradise):
                 assert g["status"] == "OK" and g["data"] == exp, (level, fmt, len(d))
 
 
+def _collision_text(rng, n):
+    """Words whose first letters flip case at random: 'a'/'A' differ in bit 5, which the 15-bit
+    hash drops from byte 0 (deflate.ts HASH_SHIFT 5), so chains mix 'the'/'The'-style strings
+    and the first chain entry is often a collision (k_dfl_match4's walk past it)."""
+    words = [b"the", b"thee", b"three", b"then", b"there", b"them", b"thy", b"thou", b"a", b"and",
+             b"art", b"ark", b"as", b"bright", b"Bright", b"night", b"knight"]
+    out = bytearray()
+    while len(out) < n:
+        w = bytearray(rng.choice(words))
+        if rng.random() < 0.4:
+            w[0] ^= 0x20
+        out += w + rng.choice([b" ", b" ", b", ", b"\n"])
+    return bytes(out[:n])
+
+
+def _rank_stress(rng, n):
+    """One 4-byte string repeated hundreds of times between rarer ones sharing its first 3
+    bytes: 4-byte chain links whose rank in the hash chain passes max_chain (16 .. 256)."""
+    out = bytearray()
+    while len(out) < n:
+        k = rng.choice([3, 20, 120, 250, 300])
+        out += b"xyzA" * k + b"xyz" + bytes([rng.randrange(66, 91)]) + bytes(rng.getrandbits(8) for _ in range(5))
+    return bytes(out[:n])
+
+
+@pytest.mark.parametrize("level", [4, 5, 6, 7, 8, 9])
+def test_deflate_4byte_chain_search(monkeypatch, paradise, level):
+    """Levels 4-9 search over 4-byte chains (k_dfl_link4 / k_dfl_match4): bit-exact with the
+    oracle and with the hash-chain walk (k_dfl_match, SDZ_MATCH4=0) on hash collisions, ranks
+    past max_chain (gaps past 256 at levels 8-9), long runs, random bytes and the bench's text
+    slices."""
+    monkeypatch.setenv("SDZ_MATCH4", "1")
+    rng = random.Random(23 + level)
+    inputs = [_collision_text(rng, 65536), _collision_text(rng, 150000), _rank_stress(rng, 65536),
+              _rank_stress(rng, 120000), paradise[7:65543], text_corpus(rng, 40000) + b"b" * 30000,
+              bytes(rng.getrandbits(8) for _ in range(50000)), _periodic(rng, 70000), binary_corpus(rng, 80000)]
+    exp = [O.deflate(d, level=level) for d in inputs]
+    gpu = sdz.deflate_batch(inputs, level=level)
+    for i, (g, e) in enumerate(zip(gpu, exp)):
+        assert g["status"] == "OK" and g["data"] == e, (level, i)
+    monkeypatch.setenv("SDZ_MATCH4", "0")
+    old = sdz.deflate_batch(inputs, level=level)
+    assert [g["data"] for g in old] == exp
+
+
 def test_deflate_record_path_long_inputs(paradise):
     """Inputs past 64 KiB on the record path: window slides every 32 KiB (deflate.ts:708-737)
     -- chain units with 32 KiB of history, matches across segments, the last positions
