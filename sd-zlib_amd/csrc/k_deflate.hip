@@ -1403,21 +1403,18 @@ __global__ __launch_bounds__(PM_THREADS) void k_dfl_match(DeflateArgs A) {
 //                add up along a 4-byte chain -- the chain of link4(x) continues x's chain -- so a
 //                walk from p knows each 4-byte candidate's rank in p's chain from the gaps alone,
 //                and a link whose gap passes K can never be followed from anywhere;
-//   k_dfl_match4 per position, the walk over that 4-byte chain with the window, links and gaps
-//                in LDS, then (when no candidate of 4+ bytes is in the window) the rank-1 entry
-//                checked for a 3-byte match -- the chain walked further only for a hash collision.
+//                The same walk finds the first entry whose bytes 0-1 agree: the result when no
+//                entry of 4+ bytes is in the window (a 4-byte entry is one, so it comes first);
+//   k_dfl_match4 per position, the walk over that 4-byte chain with the window and the links
+//                (with their gaps) in LDS.
 // Both chain lengths come from one walk as in k_dfl_match (the quarter window is ranks <= K/4).
 // Link word: (gap - 1) << 16 | distance, 0 if none (k_dfl_match4 stages it packed, m4_pack).
-#define L4_CHUNK 128
-#ifndef L4_WALKERS
-#define L4_WALKERS 2
-#endif
 __global__ __launch_bounds__(PM_THREADS) void k_dfl_link4(DeflateArgs A) {
     __shared__ __attribute__((aligned(16))) uint8_t win[(PM_WINB + 15) & ~15];
     __shared__ __attribute__((aligned(16))) uint16_t pvl[PM_PV];
     __shared__ int pm_next;
     const uint32_t tid = threadIdx.x;
-    const uint32_t lane = tid & 63u, wv = tid >> 6;
+    const uint32_t lane = tid & 63u;
     // four consecutive units (a stream's segments: they share history) on one XCD (block % 8)
     const uint32_t bb = blockIdx.x, u = (bb & ~31u) | ((bb & 7u) << 2) | ((bb >> 3) & 3u);
     if (u >= A.nmseg) return;
@@ -1453,76 +1450,65 @@ __global__ __launch_bounds__(PM_THREADS) void k_dfl_link4(DeflateArgs A) {
             const uint32_t v = pv[ws + i];
             pvl[i] = (uint16_t)(v && v < (uint32_t)i ? (uint32_t)i - v : 0u);
         }
-        if (tid == 0) pm_next = s0 + (PM_THREADS / 64) * L4_CHUNK;
+        if (tid == 0) pm_next = s0;
     }
     __syncthreads();
     GLB uint32_t* l4 = (GLB uint32_t*)A.l4_buf + rp;
-    const int K = c_config[A.level][3];
-    const int c0 = s0 + (int)wv * L4_CHUNK;
-    int next = c0 < s1 ? c0 : s1;
-    int q1 = c0 + L4_CHUNK < s1 ? c0 + L4_CHUNK : s1;
-    // L4_WALKERS walks per lane, stepped together so their LDS round trips overlap.  Per walk:
-    // r the rank of cur in p's chain (0: idle), res the link word found so far
-    int p[L4_WALKERS], sp[L4_WALKERS], cur[L4_WALKERS], r[L4_WALKERS], limit[L4_WALKERS];
-    uint32_t s4[L4_WALKERS], res[L4_WALKERS];
-    bool pend[L4_WALKERS];
-#pragma unroll
-    for (int k = 0; k < L4_WALKERS; ++k) { p[k] = s0; sp[k] = cur[k] = r[k] = limit[k] = 0; s4[k] = res[k] = 0; pend[k] = false; }
+    GLB uint16_t* f3o = (GLB uint16_t*)A.f3_buf + rp;
+    const int K = c_config[A.level][3], Kq = K >> 2;
+    // Each lane walks one position at a time and takes the next from an LDS counter itself,
+    // one step ahead: its first link and 4 bytes are read in the step after the take, beside
+    // the running walk's reads, so a new walk starts without a round trip of its own (walks are
+    // short -- 7 entries on average at L6 -- and a wave-wide refill ran at nearly every step).
+    // Walk: cur (relative) at rank r, res the link word so far, f3 the first entry whose bytes
+    // 0-1 agree (the 3-byte match): distance | (rank <= K/4) << 15, 0: none.
+    int sp = 0, cur = 0, r = 0, limit = 0;
+    uint32_t s4 = 0, res = 0, f3 = 0;
+    bool busy = false;
+    int np = 0, ncur = 0, stg = 0;                           // the next position: 0 take, 1 read, 2 ready, 3 none
+    uint32_t ns4 = 0;
+    unsigned long long n_hop = 0, n_step = 0;                 // SDZ_PHASE_TIMING counters
     for (;;) {
-        uint64_t im[L4_WALKERS];
-        int nidle = 0;
-#pragma unroll
-        for (int k = 0; k < L4_WALKERS; ++k) { im[k] = __ballot(r[k] <= 0); nidle += __popcll(im[k]); }
-        if (nidle >= PM_REFILL || nidle == 64 * L4_WALKERS) {
-#pragma unroll
-            for (int k = 0; k < L4_WALKERS; ++k)
-                if (pend[k]) { l4[p[k]] = res[k]; pend[k] = false; }
-            if (next >= q1) {
-                const int b = __builtin_amdgcn_readfirstlane(lane == 0 ? atomicAdd(&pm_next, L4_CHUNK) : 0);
-                if (b < s1) {
-                    next = b;
-                    q1 = b + L4_CHUNK < s1 ? b + L4_CHUNK : s1;
-                }
-            }
-            if (next >= q1 && nidle == 64 * L4_WALKERS) break;
-#pragma unroll
-            for (int k = 0; k < L4_WALKERS; ++k) {
-                if (next < q1) {
-                    const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(im[k] >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)im[k], 0u));
-                    const int pn = next + (int)rank;
-                    next += __popcll(im[k]);
-                    if (r[k] <= 0 && pn < q1) {
-                        p[k] = pn;
-                        sp[k] = pn - ws;
-                        cur[k] = pvl[sp[k]];
-                        limit[k] = (pn > MAX_DIST ? pn - MAX_DIST : 0) - ws;
-                        s4[k] = pm_w4(win, (uint32_t)sp[k]);
-                        res[k] = 0;
-                        const bool go = cur[k] != 0 && sp[k] - cur[k] <= MAX_DIST;   // the first entry (deflate.ts:1092)
-                        r[k] = go ? 1 : 0;
-                        pend[k] = !go;
-                    }
-                }
+        // reads: the walk's entry, and the taken position's first link and bytes
+        const int c = busy ? cur : 0;
+        const uint32_t x = pm_w4(win, (uint32_t)c) ^ s4;
+        const int nc = pvl[c];
+        int pc = 0;
+        uint32_t pw = 0;
+        if (stg == 1) { pc = pvl[np - ws]; pw = pm_w4(win, (uint32_t)(np - ws)); }
+        if (A.dbg) { ++n_step; n_hop += __popcll(__ballot(busy)); }
+        if (busy) {                                       // one chain entry
+            const bool hit = x == 0;
+            res = hit ? ((uint32_t)(r - 1) << 16) | (uint32_t)(sp - cur) : res;
+            if (f3 == 0 && (x & 0xffffu) == 0)            // (a 4-byte entry is a 3-byte one too)
+                f3 = (uint32_t)(sp - cur) | (r <= Kq ? 0x8000u : 0u);
+            const bool fin = hit || nc <= limit || r >= K;    // (nc == 0: the chain ends; limit >= 0)
+            cur = nc;
+            ++r;
+            if (fin) {
+                l4[sp + ws] = res;
+                f3o[sp + ws] = (uint16_t)f3;
+                busy = false;
             }
         }
-        uint32_t x[L4_WALKERS];
-        int nc[L4_WALKERS];
-#pragma unroll
-        for (int k = 0; k < L4_WALKERS; ++k) {            // all reads first: one round trip for all walks
-            const int c = r[k] > 0 ? cur[k] : sp[k];
-            x[k] = pm_w4(win, (uint32_t)c) ^ s4[k];
-            nc[k] = pvl[c];
+        if (stg == 1) { ncur = pc; ns4 = pw; stg = 2; }
+        if (!busy && stg == 2) {                          // start the next walk
+            sp = np - ws;
+            cur = ncur;
+            s4 = ns4;
+            res = 0; f3 = 0; r = 1;
+            limit = (np > MAX_DIST ? np - MAX_DIST : 0) - ws;
+            busy = cur != 0 && sp - cur <= MAX_DIST;      // the first entry (deflate.ts:1092)
+            if (!busy) { l4[np] = 0u; f3o[np] = 0; }
+            stg = 0;
         }
-#pragma unroll
-        for (int k = 0; k < L4_WALKERS; ++k) {            // one chain entry per walk and step
-            const bool live = r[k] > 0, hit = live && x[k] == 0;
-            res[k] = hit ? ((uint32_t)(r[k] - 1) << 16) | (uint32_t)(sp[k] - cur[k]) : res[k];
-            const bool fin = live && (hit || nc[k] <= limit[k] || r[k] >= K);   // (nc == 0: the chain ends)
-            cur[k] = live ? nc[k] : cur[k];
-            r[k] = fin ? 0 : live ? r[k] + 1 : r[k];
-            pend[k] = pend[k] || fin;
+        if (stg == 0) {
+            np = atomicAdd(&pm_next, 1);
+            stg = np < s1 ? 1 : 3;
         }
+        if (!__ballot(busy || stg != 3)) break;
     }
+    if (A.dbg && lane == 0) { atomicAdd(&A.dbg[8], n_hop); atomicAdd(&A.dbg[9], n_step); }
 }
 
 #ifndef M4_SUB
@@ -1539,11 +1525,9 @@ __device__ __forceinline__ uint16_t m4_pack(uint32_t v) {
     const uint32_t d = v & 0xffffu, g = (v >> 16) + 1u;
     return (uint16_t)(d == 0u ? 0u : d < 8192u && g <= 7u ? d << 3 | g : 8u);
 }
-__device__ __forceinline__ void m4_link(const uint16_t* lk, const GLB uint32_t* l4g, int x, int& dist, int& gap) {
-    if (x < 0) { dist = 0; gap = 0; return; }
-    const uint32_t e = lk[x];
+__device__ __forceinline__ void m4_unpack(uint32_t e, const GLB uint32_t* l4g, int x, bool live, int& dist, int& gap) {
     if (e & 7u) { dist = (int)(e >> 3); gap = (int)(e & 7u); return; }
-    const uint32_t v = e ? l4g[x] : 0u;
+    const uint32_t v = e && live ? l4g[x] : 0u;
     dist = (int)(v & 0xffffu);
     gap = (int)(v >> 16) + 1;
 }
@@ -1563,27 +1547,12 @@ __device__ __forceinline__ int m4_lcp16(uint32_t x0, uint32_t x1, uint32_t x2, u
     const uint32_t x = x0 ? x0 : x1 ? x1 : x2 ? x2 : x3;
     return k == 16 ? 16 : k + (int)(__builtin_ctz(x) >> 3);
 }
-// the first chain entry (in rank order) with bytes 0-1 equal to p's (a 3-byte match, see above),
-// walked over the HBM links past a hash collision at rank 1: rank << 16 | its position relative
-// to ws, 0 if none within K (positions relative to ws)
-__device__ __forceinline__ uint32_t m4_first3(const GLB uint16_t* pv, const uint8_t* win, int ws, int sp, int first,
-                                              int limit, int K) {
-    const uint32_t b0 = win[sp], b1 = win[sp + 1];
-    int c = first;
-    for (int r = 1; r <= K; ++r) {
-        if (win[c] == b0 && win[c + 1] == b1) return (uint32_t)r << 16 | (uint32_t)c;
-        const int d = (int)pv[c + ws];
-        c -= d;
-        if (d == 0 || c <= limit) return 0u;
-    }
-    return 0u;
-}
 __global__ __launch_bounds__(PM_THREADS) void k_dfl_match4(DeflateArgs A) {
     __shared__ __attribute__((aligned(16))) uint8_t win[(M4_WINB + 15) & ~15];
     __shared__ __attribute__((aligned(16))) uint16_t lk[M4_PV];   // m4_pack words
     __shared__ int pm_next;
     const uint32_t tid = threadIdx.x;
-    const uint32_t lane = tid & 63u, wv = tid >> 6;
+    const uint32_t lane = tid & 63u;
     // block -> (unit, part): of each 128 blocks, the 16 on XCD x (block % 8) take items 16 x .. 16 x + 15
     const uint32_t bb = blockIdx.x, item = (bb & ~127u) | ((bb & 7u) << 4) | ((bb >> 3) & 15u);
     const uint32_t u = item / M4_NSUB, part = item % M4_NSUB;
@@ -1599,7 +1568,7 @@ __global__ __launch_bounds__(PM_THREADS) void k_dfl_match4(DeflateArgs A) {
     const int ws = s0 > W_SIZE ? s0 - W_SIZE : 0;
     const int we = s1 + MAX_MATCH + 8 < n ? s1 + MAX_MATCH + 8 : n;
     const GLB uint8_t* in = (const GLB uint8_t*)(A.in + A.in_off[sid]);
-    const GLB uint16_t* pv = (const GLB uint16_t*)A.pv_buf + rp;
+    const GLB uint16_t* f3g = (const GLB uint16_t*)A.f3_buf + rp;
     const GLB uint32_t* l4g = (const GLB uint32_t*)A.l4_buf + rp + ws;   // relative to ws
     {
         const int nw = (we - ws) >> 2;
@@ -1611,99 +1580,94 @@ __global__ __launch_bounds__(PM_THREADS) void k_dfl_match4(DeflateArgs A) {
         }
         for (int i = 4 * nw + (int)tid; i < we - ws; i += PM_THREADS) win[i] = in[ws + i];
         for (int i = (int)tid; i < s1 - ws; i += PM_THREADS) lk[i] = m4_pack(l4g[i]);
-        if (tid == 0) pm_next = s0 + (PM_THREADS / 64) * PM_CHUNK;
+        if (tid == 0) pm_next = s0;
     }
     __syncthreads();
     GLB uint64_t* rec = (GLB uint64_t*)A.rec_buf + rp;
     const int K = c_config[A.level][3], Kq = K >> 2, nice = c_config[A.level][2];
-    const int c0 = s0 + (int)wv * PM_CHUNK;
-    int next = c0 < s1 ? c0 : s1;
-    int q1 = c0 + PM_CHUNK < s1 ? c0 + PM_CHUNK : s1;
-    // per lane: position p (sp relative to ws), its chain's first entry and limit (relative),
-    // the 4-byte candidate cur with its rank cum; live: walking; srch: p searches at all
-    int p = s0, sp = 0, cur = 0, cum = 0, first = 0, limit = 0, best = 2, bpos = 0, qbest = 2, qpos = 0;
-    uint32_t pw[4] = { 0, 0, 0, 0 };                         // p's bytes 4-19
-    bool live = false, pend = false, srch = false;
+    // Each lane walks one position at a time and takes the next from an LDS counter itself,
+    // one step ahead (as k_dfl_link4): the taken position's link, its bytes 4-19 and its 3-byte
+    // entry are read in the step after the take, beside the running walk's reads.
+    // Walk: position sp (relative to ws), its limit, the 4-byte candidate cur at rank cum.
+    int sp = -1, cur = 0, cum = 0, limit = 0, best = 2, bpos = 0, qbest = 2, qpos = 0;   // sp < 0: none
+    uint32_t pw[4] = { 0, 0, 0, 0 }, f3w = 0;                 // p's bytes 4-19; its 3-byte entry
+    bool busy = false;
+    int np = 0, stg = 0;                                     // the next position: 0 take, 1 read, 2 ready, 3 none
+    uint32_t ne = 0, npw[4] = { 0, 0, 0, 0 }, nf3 = 0;
+    unsigned long long n_cand = 0, n_step = 0;               // SDZ_PHASE_TIMING counters
     for (;;) {
-        const uint64_t im = __ballot(!live);
-        const int nidle = __popcll(im);
-        if (nidle >= PM_REFILL || nidle == 64) {
-            if (pend) {
-                if (srch && qbest < 4) {                     // 3-byte matches (rank-1 entry, or past a collision)
-                    const uint32_t f = m4_first3(pv, win, ws, sp, first, limit, K);
-                    const int r3 = (int)(f >> 16), f3 = (int)(f & 0xffffu);
-                    if (r3 && best < 4) { best = 3; bpos = f3; }
-                    if (r3 && r3 <= Kq) { qbest = 3; qpos = f3; }
-                }
-                const uint32_t full = best > MIN_MATCH - 1 ? ((uint32_t)best << 16) | (uint32_t)(sp - bpos) : 0u;
-                const uint32_t quarter = qbest > MIN_MATCH - 1 ? ((uint32_t)qbest << 16) | (uint32_t)(sp - qpos) : 0u;
-                rec[p] = rec_word(full, quarter, win[p > 0 ? sp - 1 : 0]);
-                pend = false;
-            }
-            if (next >= q1) {
-                const int b = __builtin_amdgcn_readfirstlane(lane == 0 ? atomicAdd(&pm_next, PM_CHUNK) : 0);
-                if (b < s1) {
-                    next = b;
-                    q1 = b + PM_CHUNK < s1 ? b + PM_CHUNK : s1;
-                }
-            }
-            if (next >= q1 && nidle == 64) break;
-            if (next < q1) {
-                const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(im >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)im, 0u));
-                const int pn = next + (int)rank;
-                next += nidle;
-                if (!live && pn < q1) {
-                    p = pn;
-                    sp = p - ws;
-                    const int d3 = (int)pv[p];
-                    srch = d3 != 0 && d3 <= MAX_DIST;          // deflate.ts:1092
-                    first = sp - d3;
-                    limit = (p > MAX_DIST ? p - MAX_DIST : 0) - ws;
-                    best = 2; bpos = 0; qbest = 2; qpos = 0;
-                    m4_w16(win, (uint32_t)(sp + 4), pw);
-                    int l = 0;
-                    cum = 0;
-                    m4_link(lk, l4g, srch ? sp : -1, l, cum);
-                    cur = sp - l;
-                    live = l != 0 && cum <= K && (cum == 1 || cur > limit);
-                    pend = !live;
-                }
+        // reads: the candidate's link and bytes 4-19; the taken position's link, bytes, 3-byte entry
+        const int c = busy ? cur : 0;
+        const uint32_t e = lk[c];
+        uint32_t m[4];
+        m4_w16(win, (uint32_t)(c + 4), m);
+        uint32_t pe = 0, ppw[4] = { 0, 0, 0, 0 }, pf3 = 0;
+        if (stg == 1) {
+            pe = lk[np - ws];
+            m4_w16(win, (uint32_t)(np - ws + 4), ppw);
+            pf3 = f3g[np];
+        }
+        if (A.dbg) { ++n_step; n_cand += __popcll(__ballot(busy)); }
+        int len = 0, nl = 0, ng = 0;
+        bool more = false;
+        if (busy) {
+            m4_unpack(e, l4g, c, true, nl, ng);
+            len = 4 + m4_lcp16(m[0] ^ pw[0], m[1] ^ pw[1], m[2] ^ pw[2], m[3] ^ pw[3]);
+            more = len == 20;
+        }
+        while (__ballot(more)) {                             // matches past 20 bytes
+            if (more) {
+                uint32_t a[4], b[4];
+                m4_w16(win, (uint32_t)(cur + len), a);
+                m4_w16(win, (uint32_t)(sp + len), b);
+                const int d = m4_lcp16(a[0] ^ b[0], a[1] ^ b[1], a[2] ^ b[2], a[3] ^ b[3]);
+                len += d;
+                more = d == 16 && len < MAX_MATCH;
             }
         }
-        if (live) {
-            // one LDS round trip per candidate: its link and gap, and its bytes 4-19 against p's
-            // (in registers); no pre-check at best -- every 4-byte candidate's length is found
-            int nl, ng;
-            m4_link(lk, l4g, cur, nl, ng);
-            uint32_t m[4];
-            m4_w16(win, (uint32_t)(cur + 4), m);
-            int len = 4 + m4_lcp16(m[0] ^ pw[0], m[1] ^ pw[1], m[2] ^ pw[2], m[3] ^ pw[3]);
-            bool more = len == 20;
-            while (__ballot(more)) {                           // matches past 20 bytes
-                if (more) {
-                    uint32_t a[4], b[4];
-                    m4_w16(win, (uint32_t)(cur + len), a);
-                    m4_w16(win, (uint32_t)(sp + len), b);
-                    const int d = m4_lcp16(a[0] ^ b[0], a[1] ^ b[1], a[2] ^ b[2], a[3] ^ b[3]);
-                    len += d;
-                    more = d == 16 && len < MAX_MATCH;
-                }
-            }
+        if (busy) {
             len = len > MAX_MATCH ? MAX_MATCH : len;
             const bool upd = len > best;
             best = upd ? len : best;
             bpos = upd ? cur : bpos;
-            const bool cap = cum <= Kq;
-            qbest = cap ? best : qbest;
-            qpos = cap ? bpos : qpos;
+            if (cum <= Kq) { qbest = best; qpos = bpos; }
             const int ncur = cur - nl, ncum = cum + ng;
             const bool fin = (upd && len >= nice) || nl == 0 || ncum > K || ncur <= limit;
             cur = ncur;
             cum = ncum;
-            live = !fin;
-            pend = pend || fin;
+            busy = !fin;
         }
+        if (stg == 1) { ne = pe; npw[0] = ppw[0]; npw[1] = ppw[1]; npw[2] = ppw[2]; npw[3] = ppw[3]; nf3 = pf3; stg = 2; }
+        // finish: the record of a walk that just ended (or of a position without 4-byte links)
+        if (!busy && sp >= 0) {
+            const int f3d = (int)(f3w & 0x7fffu);
+            if (best < 4 && f3d) { best = 3; bpos = sp - f3d; }
+            if (qbest < 4 && (f3w & 0x8000u)) { qbest = 3; qpos = sp - f3d; }
+            const uint32_t full = best > MIN_MATCH - 1 ? ((uint32_t)best << 16) | (uint32_t)(sp - bpos) : 0u;
+            const uint32_t quarter = qbest > MIN_MATCH - 1 ? ((uint32_t)qbest << 16) | (uint32_t)(sp - qpos) : 0u;
+            rec[sp + ws] = rec_word(full, quarter, win[sp + ws > 0 ? sp - 1 : 0]);
+            sp = -1;                                         // (no position in hand)
+        }
+        if (sp < 0 && stg == 2) {                            // start the next walk
+            sp = np - ws;
+            pw[0] = npw[0]; pw[1] = npw[1]; pw[2] = npw[2]; pw[3] = npw[3];
+            f3w = nf3;
+            limit = (np > MAX_DIST ? np - MAX_DIST : 0) - ws;
+            best = 2; bpos = 0; qbest = 2; qpos = 0;
+            int l = 0, g = 0;
+            m4_unpack(ne, l4g, sp, true, l, g);              // (no search at p: no link, deflate.ts:1092)
+            cur = sp - l;
+            cum = g;
+            busy = l != 0 && g <= K && (g == 1 || cur > limit);
+            stg = 0;
+        }
+        if (stg == 0) {
+            np = atomicAdd(&pm_next, 1);
+            stg = np < s1 ? 1 : 3;
+        }
+        if (!__ballot(busy || sp >= 0 || stg != 3)) break;
     }
+    if (A.dbg && lane == 0) { atomicAdd(&A.dbg[11], n_cand); atomicAdd(&A.dbg[12], n_step); }
 }
 
 // ------------------------------------------------------------------ record path: tail, parse, trees, encode

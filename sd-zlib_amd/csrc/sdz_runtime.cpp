@@ -867,8 +867,8 @@ int rt::deflate_batch_device(const uint8_t* in, const uint64_t* in_off, const ui
     const char* m4e = getenv("SDZ_MATCH4");
     const bool m4_on = m4e ? m4e[0] == '1' : kMatch4Default;
     const bool match4 = recpath && !ext && level >= 4 && m4_on;
-    // per position: record 8, link 2, parse words 8 + 4 + 3 bitmaps, 4-byte link 4; per segment 28
-    const uint64_t kPosBytes = (lz_shift ? 8 + 2 + 8 + 4 + 1 : 8 + 2) + (match4 ? 4 : 0);
+    // per position: record 8, link 2, parse words 8 + 4 + 3 bitmaps, 4-byte link 4 + 3-byte entry 2; per segment 28
+    const uint64_t kPosBytes = (lz_shift ? 8 + 2 + 8 + 4 + 1 : 8 + 2) + (match4 ? 6 : 0);
     auto rec_cost = [&](uint32_t i) -> uint64_t {
         if (!on_path(i)) return 0;
         const uint64_t p = (len[i] + 63) & ~63ull;
@@ -992,7 +992,10 @@ int rt::deflate_batch_device(const uint8_t* in, const uint64_t* in_off, const ui
                 a.rec_buf = (uint64_t*)take((size_t)pos * 8);
                 a.pv_buf = (uint16_t*)take((size_t)pos * 2);
                 a.sym_buf = (uint32_t*)a.rec_buf;
-                if (match4) a.l4_buf = (uint32_t*)take((size_t)pos * 4);
+                if (match4) {
+                    a.l4_buf = (uint32_t*)take((size_t)pos * 4);
+                    a.f3_buf = (uint16_t*)take((size_t)pos * 2);
+                }
             }
             a.blk = take((size_t)blk * FB_SLOT_BYTES);
             a.cks = (int32_t*)take((size_t)m * 4);
@@ -1060,7 +1063,7 @@ int rt::deflate_batch_device(const uint8_t* in, const uint64_t* in_off, const ui
         HIPCHK(hipMemcpyAsync(h, dbg, sizeof h, hipMemcpyDeviceToHost, s));
         HIPCHK(hipStreamSynchronize(s));
         fprintf(stderr, "sdz deflate phases:");
-        for (int k = 0; k < 8; ++k) fprintf(stderr, " %llu", h[k]);
+        for (int k = 0; k < 16; ++k) fprintf(stderr, " %llu", h[k]);
         fprintf(stderr, "\n");
         hipFree(dbg);
     }
