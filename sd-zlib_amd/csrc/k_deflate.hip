@@ -1511,13 +1511,12 @@ __global__ __launch_bounds__(PM_THREADS) void k_dfl_link4(DeflateArgs A) {
     if (A.dbg && lane == 0) { atomicAdd(&A.dbg[8], n_hop); atomicAdd(&A.dbg[9], n_step); }
 }
 
-#ifndef M4_SUB
-#define M4_SUB PM_SEG                                    // positions per workgroup
+#ifndef M4_WALKERS
+#define M4_WALKERS 1                                     // 2: measured no faster
 #endif
-#define M4_NSUB (PM_SEG / M4_SUB)
-#define M4_WINB (W_SIZE + M4_SUB + MAX_MATCH + 16)
-#define M4_PV (W_SIZE + M4_SUB)
-static uint32_t match4_blocks(uint32_t nmseg) { return (nmseg * M4_NSUB + 127u) & ~127u; }
+#define M4_WINB (W_SIZE + PM_SEG + MAX_MATCH + 16)
+#define M4_PV (W_SIZE + PM_SEG)
+static uint32_t match4_blocks(uint32_t nmseg) { return (nmseg + 127u) & ~127u; }
 static uint32_t link4_blocks(uint32_t nmseg) { return (nmseg + 31u) & ~31u; }
 // A link staged in LDS as 16 bits: distance << 3 | gap for distances below 8192 and gaps up to 7
 // (~94 % of the links walked on text); 0: none; else 8 (the word is read from HBM)
@@ -1553,9 +1552,9 @@ __global__ __launch_bounds__(PM_THREADS) void k_dfl_match4(DeflateArgs A) {
     __shared__ int pm_next;
     const uint32_t tid = threadIdx.x;
     const uint32_t lane = tid & 63u;
-    // block -> (unit, part): of each 128 blocks, the 16 on XCD x (block % 8) take items 16 x .. 16 x + 15
+    // block -> unit: of each 128 blocks, the 16 on XCD x (block % 8) take units 16 x .. 16 x + 15
     const uint32_t bb = blockIdx.x, item = (bb & ~127u) | ((bb & 7u) << 4) | ((bb >> 3) & 15u);
-    const uint32_t u = item / M4_NSUB, part = item % M4_NSUB;
+    const uint32_t u = item;
     if (u >= A.nmseg) return;
     const uint32_t sid = A.mseg[u] >> kRecUnitShift, seg = A.mseg[u] & ((1u << kRecUnitShift) - 1);
     const uint64_t rp = A.rp0[sid];
@@ -1563,7 +1562,7 @@ __global__ __launch_bounds__(PM_THREADS) void k_dfl_match4(DeflateArgs A) {
     const int n = (int)A.in_len[sid];
     const int tail = n > PM_TAIL ? n - PM_TAIL : 0;
     const int g1 = (int)(seg * PM_SEG) + PM_SEG < tail ? (int)(seg * PM_SEG) + PM_SEG : tail;
-    const int s0 = (int)(seg * PM_SEG + part * M4_SUB), s1 = s0 + M4_SUB < g1 ? s0 + M4_SUB : g1;
+    const int s0 = (int)(seg * PM_SEG), s1 = g1;
     if (s0 >= s1) return;
     const int ws = s0 > W_SIZE ? s0 - W_SIZE : 0;
     const int we = s1 + MAX_MATCH + 8 < n ? s1 + MAX_MATCH + 8 : n;
@@ -1585,87 +1584,119 @@ __global__ __launch_bounds__(PM_THREADS) void k_dfl_match4(DeflateArgs A) {
     __syncthreads();
     GLB uint64_t* rec = (GLB uint64_t*)A.rec_buf + rp;
     const int K = c_config[A.level][3], Kq = K >> 2, nice = c_config[A.level][2];
-    // Each lane walks one position at a time and takes the next from an LDS counter itself,
-    // one step ahead (as k_dfl_link4): the taken position's link, its bytes 4-19 and its 3-byte
-    // entry are read in the step after the take, beside the running walk's reads.
-    // Walk: position sp (relative to ws), its limit, the 4-byte candidate cur at rank cum.
-    int sp = -1, cur = 0, cum = 0, limit = 0, best = 2, bpos = 0, qbest = 2, qpos = 0;   // sp < 0: none
-    uint32_t pw[4] = { 0, 0, 0, 0 }, f3w = 0;                 // p's bytes 4-19; its 3-byte entry
-    bool busy = false;
+    // Each lane runs M4_WALKERS walks side by side (their LDS round trips overlap) and takes
+    // the next position from an LDS counter itself, one step ahead (as k_dfl_link4): the taken
+    // position's link, its bytes 4-19 and its 3-byte entry are read in the step after the take,
+    // beside the running walks' reads; the first walker free takes it.
+    // Walk k: position sp (relative to ws; < 0 none), its limit, the 4-byte candidate cur at rank cum.
+    constexpr int W = M4_WALKERS;
+    int sp[W], cur[W], cum[W], limit[W], best[W], bpos[W], qbest[W], qpos[W];
+    uint32_t pw[W][4], f3w[W];                               // p's bytes 4-19; its 3-byte entry
+    bool busy[W];
+#pragma unroll
+    for (int k = 0; k < W; ++k) {
+        sp[k] = -1; cur[k] = cum[k] = limit[k] = bpos[k] = qpos[k] = 0; best[k] = qbest[k] = 2;
+        pw[k][0] = pw[k][1] = pw[k][2] = pw[k][3] = f3w[k] = 0u;
+        busy[k] = false;
+    }
     int np = 0, stg = 0;                                     // the next position: 0 take, 1 read, 2 ready, 3 none
     uint32_t ne = 0, npw[4] = { 0, 0, 0, 0 }, nf3 = 0;
     unsigned long long n_cand = 0, n_step = 0;               // SDZ_PHASE_TIMING counters
     for (;;) {
-        // reads: the candidate's link and bytes 4-19; the taken position's link, bytes, 3-byte entry
-        const int c = busy ? cur : 0;
-        const uint32_t e = lk[c];
-        uint32_t m[4];
-        m4_w16(win, (uint32_t)(c + 4), m);
+        // reads: each candidate's link and bytes 4-19; the taken position's link, bytes, 3-byte entry
+        uint32_t e[W], m[W][4];
+#pragma unroll
+        for (int k = 0; k < W; ++k) {
+            const int c = busy[k] ? cur[k] : 0;
+            e[k] = lk[c];
+            m4_w16(win, (uint32_t)(c + 4), m[k]);
+        }
         uint32_t pe = 0, ppw[4] = { 0, 0, 0, 0 }, pf3 = 0;
         if (stg == 1) {
             pe = lk[np - ws];
             m4_w16(win, (uint32_t)(np - ws + 4), ppw);
             pf3 = f3g[np];
         }
-        if (A.dbg) { ++n_step; n_cand += __popcll(__ballot(busy)); }
-        int len = 0, nl = 0, ng = 0;
-        bool more = false;
-        if (busy) {
-            m4_unpack(e, l4g, c, true, nl, ng);
-            len = 4 + m4_lcp16(m[0] ^ pw[0], m[1] ^ pw[1], m[2] ^ pw[2], m[3] ^ pw[3]);
-            more = len == 20;
+        if (A.dbg) {
+            ++n_step;
+#pragma unroll
+            for (int k = 0; k < W; ++k) n_cand += __popcll(__ballot(busy[k]));
         }
-        while (__ballot(more)) {                             // matches past 20 bytes
-            if (more) {
-                uint32_t a[4], b[4];
-                m4_w16(win, (uint32_t)(cur + len), a);
-                m4_w16(win, (uint32_t)(sp + len), b);
-                const int d = m4_lcp16(a[0] ^ b[0], a[1] ^ b[1], a[2] ^ b[2], a[3] ^ b[3]);
-                len += d;
-                more = d == 16 && len < MAX_MATCH;
+        int len[W], nl[W], ng[W];
+        bool more[W];
+#pragma unroll
+        for (int k = 0; k < W; ++k) {
+            nl[k] = ng[k] = 0;
+            m4_unpack(e[k], l4g, cur[k], busy[k], nl[k], ng[k]);
+            len[k] = 4 + m4_lcp16(m[k][0] ^ pw[k][0], m[k][1] ^ pw[k][1], m[k][2] ^ pw[k][2], m[k][3] ^ pw[k][3]);
+            more[k] = busy[k] && len[k] == 20;
+        }
+        for (;;) {                                           // matches past 20 bytes
+            bool any = false;
+#pragma unroll
+            for (int k = 0; k < W; ++k) any = any || more[k];
+            if (!__ballot(any)) break;
+#pragma unroll
+            for (int k = 0; k < W; ++k) {
+                if (more[k]) {
+                    uint32_t a[4], b[4];
+                    m4_w16(win, (uint32_t)(cur[k] + len[k]), a);
+                    m4_w16(win, (uint32_t)(sp[k] + len[k]), b);
+                    const int d = m4_lcp16(a[0] ^ b[0], a[1] ^ b[1], a[2] ^ b[2], a[3] ^ b[3]);
+                    len[k] += d;
+                    more[k] = d == 16 && len[k] < MAX_MATCH;
+                }
             }
         }
-        if (busy) {
-            len = len > MAX_MATCH ? MAX_MATCH : len;
-            const bool upd = len > best;
-            best = upd ? len : best;
-            bpos = upd ? cur : bpos;
-            if (cum <= Kq) { qbest = best; qpos = bpos; }
-            const int ncur = cur - nl, ncum = cum + ng;
-            const bool fin = (upd && len >= nice) || nl == 0 || ncum > K || ncur <= limit;
-            cur = ncur;
-            cum = ncum;
-            busy = !fin;
+#pragma unroll
+        for (int k = 0; k < W; ++k) {
+            const int ln = len[k] > MAX_MATCH ? MAX_MATCH : len[k];
+            const bool upd = busy[k] && ln > best[k];
+            best[k] = upd ? ln : best[k];
+            bpos[k] = upd ? cur[k] : bpos[k];
+            const bool cap = busy[k] && cum[k] <= Kq;
+            qbest[k] = cap ? best[k] : qbest[k];
+            qpos[k] = cap ? bpos[k] : qpos[k];
+            const int ncur = cur[k] - nl[k], ncum = cum[k] + ng[k];
+            const bool fin = (upd && ln >= nice) || nl[k] == 0 || ncum > K || ncur <= limit[k];
+            cur[k] = busy[k] ? ncur : cur[k];
+            cum[k] = busy[k] ? ncum : cum[k];
+            busy[k] = busy[k] && !fin;
         }
         if (stg == 1) { ne = pe; npw[0] = ppw[0]; npw[1] = ppw[1]; npw[2] = ppw[2]; npw[3] = ppw[3]; nf3 = pf3; stg = 2; }
-        // finish: the record of a walk that just ended (or of a position without 4-byte links)
-        if (!busy && sp >= 0) {
-            const int f3d = (int)(f3w & 0x7fffu);
-            if (best < 4 && f3d) { best = 3; bpos = sp - f3d; }
-            if (qbest < 4 && (f3w & 0x8000u)) { qbest = 3; qpos = sp - f3d; }
-            const uint32_t full = best > MIN_MATCH - 1 ? ((uint32_t)best << 16) | (uint32_t)(sp - bpos) : 0u;
-            const uint32_t quarter = qbest > MIN_MATCH - 1 ? ((uint32_t)qbest << 16) | (uint32_t)(sp - qpos) : 0u;
-            rec[sp + ws] = rec_word(full, quarter, win[sp + ws > 0 ? sp - 1 : 0]);
-            sp = -1;                                         // (no position in hand)
-        }
-        if (sp < 0 && stg == 2) {                            // start the next walk
-            sp = np - ws;
-            pw[0] = npw[0]; pw[1] = npw[1]; pw[2] = npw[2]; pw[3] = npw[3];
-            f3w = nf3;
-            limit = (np > MAX_DIST ? np - MAX_DIST : 0) - ws;
-            best = 2; bpos = 0; qbest = 2; qpos = 0;
-            int l = 0, g = 0;
-            m4_unpack(ne, l4g, sp, true, l, g);              // (no search at p: no link, deflate.ts:1092)
-            cur = sp - l;
-            cum = g;
-            busy = l != 0 && g <= K && (g == 1 || cur > limit);
-            stg = 0;
+#pragma unroll
+        for (int k = 0; k < W; ++k) {
+            if (!busy[k] && sp[k] >= 0) {                    // the record of a walk that ended
+                const int f3d = (int)(f3w[k] & 0x7fffu);     // below 4 bytes: k_dfl_link4's 3-byte entry
+                if (best[k] < 4 && f3d) { best[k] = 3; bpos[k] = sp[k] - f3d; }
+                if (qbest[k] < 4 && (f3w[k] & 0x8000u)) { qbest[k] = 3; qpos[k] = sp[k] - f3d; }
+                const uint32_t full = best[k] > MIN_MATCH - 1 ? ((uint32_t)best[k] << 16) | (uint32_t)(sp[k] - bpos[k]) : 0u;
+                const uint32_t quarter = qbest[k] > MIN_MATCH - 1 ? ((uint32_t)qbest[k] << 16) | (uint32_t)(sp[k] - qpos[k]) : 0u;
+                rec[sp[k] + ws] = rec_word(full, quarter, win[sp[k] + ws > 0 ? sp[k] - 1 : 0]);
+                sp[k] = -1;
+            }
+            if (sp[k] < 0 && stg == 2) {                     // start the taken position
+                sp[k] = np - ws;
+                pw[k][0] = npw[0]; pw[k][1] = npw[1]; pw[k][2] = npw[2]; pw[k][3] = npw[3];
+                f3w[k] = nf3;
+                limit[k] = (np > MAX_DIST ? np - MAX_DIST : 0) - ws;
+                best[k] = 2; bpos[k] = 0; qbest[k] = 2; qpos[k] = 0;
+                int l = 0, g = 0;
+                m4_unpack(ne, l4g, sp[k], true, l, g);       // (no search at p: no link, deflate.ts:1092)
+                cur[k] = sp[k] - l;
+                cum[k] = g;
+                busy[k] = l != 0 && g <= K && (g == 1 || cur[k] > limit[k]);
+                stg = 0;
+            }
         }
         if (stg == 0) {
             np = atomicAdd(&pm_next, 1);
             stg = np < s1 ? 1 : 3;
         }
-        if (!__ballot(busy || sp >= 0 || stg != 3)) break;
+        bool act = stg != 3;
+#pragma unroll
+        for (int k = 0; k < W; ++k) act = act || busy[k] || sp[k] >= 0;
+        if (!__ballot(act)) break;
     }
     if (A.dbg && lane == 0) { atomicAdd(&A.dbg[11], n_cand); atomicAdd(&A.dbg[12], n_step); }
 }
