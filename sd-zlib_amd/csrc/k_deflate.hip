@@ -1183,6 +1183,9 @@ __global__ __launch_bounds__(64 * CH_WAVES) void k_dfl_chain(DeflateArgs A) {
 // so the wave runs ~ (total candidates / 64) steps, not (longest chain x positions / 64).
 // Record per position: bits 0-15 distance, 16-24 length (<= 2: no candidate beats
 // MIN_MATCH - 1) -- chain max_chain in the low word, max_chain >> 2 in the high word.
+// With seg_merge the host lists a stream's segment 0 for segments 0-2 (no history before them:
+// the same 48 KiB of window and links is staged), first in the list -- workgroups go to the XCDs
+// round-robin in list order, so the long ones are spread over all 8 and start first.
 #define PM_SEG 16384
 #define PM_THREADS 1024
 #ifndef PM_CHUNK
@@ -1224,7 +1227,8 @@ __global__ __launch_bounds__(PM_THREADS) void k_dfl_match(DeflateArgs A) {
     if (rp == ~0ull) return;
     const int n = (int)in_len;
     const int tail = n > PM_TAIL ? n - PM_TAIL : 0;
-    const int s0 = (int)(seg * PM_SEG), s1 = s0 + PM_SEG < tail ? s0 + PM_SEG : tail;
+    const int s0 = (int)(seg * PM_SEG), e0 = s0 + (A.seg_merge && seg == 0 ? 3 * PM_SEG : PM_SEG);
+    const int s1 = e0 < tail ? e0 : tail;
     if (s0 >= s1) return;
     const int ws = s0 > W_SIZE ? s0 - W_SIZE : 0;          // staged range [ws, we) (ws even)
     const int we = s1 + MAX_MATCH + 8 < n ? s1 + MAX_MATCH + 8 : n;
@@ -1423,7 +1427,8 @@ __global__ __launch_bounds__(PM_THREADS) void k_dfl_link4(DeflateArgs A) {
     if (rp == ~0ull) return;
     const int n = (int)A.in_len[sid];
     const int tail = n > PM_TAIL ? n - PM_TAIL : 0;
-    const int s0 = (int)(seg * PM_SEG), s1 = s0 + PM_SEG < tail ? s0 + PM_SEG : tail;
+    const int s0 = (int)(seg * PM_SEG), e0 = s0 + (A.seg_merge && seg == 0 ? 3 * PM_SEG : PM_SEG);
+    const int s1 = e0 < tail ? e0 : tail;
     if (s0 >= s1) return;
     const int ws = s0 > W_SIZE ? s0 - W_SIZE : 0;
     const int we = s1 + MAX_MATCH + 8 < n ? s1 + MAX_MATCH + 8 : n;
@@ -1561,7 +1566,8 @@ __global__ __launch_bounds__(PM_THREADS) void k_dfl_match4(DeflateArgs A) {
     if (rp == ~0ull) return;
     const int n = (int)A.in_len[sid];
     const int tail = n > PM_TAIL ? n - PM_TAIL : 0;
-    const int g1 = (int)(seg * PM_SEG) + PM_SEG < tail ? (int)(seg * PM_SEG) + PM_SEG : tail;
+    const int ge = (int)(seg * PM_SEG) + (A.seg_merge && seg == 0 ? 3 * PM_SEG : PM_SEG);
+    const int g1 = ge < tail ? ge : tail;
     const int s0 = (int)(seg * PM_SEG), s1 = g1;
     if (s0 >= s1) return;
     const int ws = s0 > W_SIZE ? s0 - W_SIZE : 0;

@@ -115,6 +115,7 @@ struct DeflateArgs {
     uint8_t* blk;                // block slots (FB_SLOT bytes each)
     const uint32_t* mseg;        // match segments (PM_SEG positions each)
     uint32_t nmseg;
+    uint32_t seg_merge;          // match kernels: a stream's segment 0 also covers segments 1-2
     const uint32_t* cunit;       // chain units (k_dfl_chain)
     uint32_t ncunit;
     uint32_t nbmax;              // most block slots of one stream (k_dfl_trees grid)

@@ -867,6 +867,10 @@ int rt::deflate_batch_device(const uint8_t* in, const uint64_t* in_off, const ui
     const char* m4e = getenv("SDZ_MATCH4");
     const bool m4_on = m4e ? m4e[0] == '1' : kMatch4Default;
     const bool match4 = recpath && !ext && level >= 4 && m4_on;
+    // a stream's first three match segments in one workgroup (not for a Deflater: its list skips
+    // the segments final from earlier calls); SDZ_SEG_MERGE=0 turns it off
+    const char* sme = getenv("SDZ_SEG_MERGE");
+    const bool seg_merge = recpath && !ext && !(sme && sme[0] == '0');
     // per position: record 8, link 2, parse words 8 + 4 + 3 bitmaps, 4-byte link 4 + 3-byte entry 2; per segment 28
     const uint64_t kPosBytes = (lz_shift ? 8 + 2 + 8 + 4 + 1 : 8 + 2) + (match4 ? 6 : 0);
     auto rec_cost = [&](uint32_t i) -> uint64_t {
@@ -953,9 +957,16 @@ int rt::deflate_batch_device(const uint8_t* in, const uint64_t* in_off, const ui
                 const uint32_t ms = deflate_match_segs(len[i]);
                 for (uint32_t u = 0; u < ms; ++u) {
                     if (ext && (uint64_t)(u + 1) * 16384 <= ext->rec_from) continue;   // final from earlier calls
+                    if (seg_merge && u > 0) continue;    // (second pass below)
                     units.push_back(k << kRecUnitShift | u);
                     ++nm;
                 }
+            }
+            // seg_merge: every stream's segment 0 (covering segments 0-2) first, then segments 3..
+            for (uint32_t k = 0; seg_merge && k < m; ++k) {
+                if (rp0[k] == ~0ull) continue;
+                const uint32_t ms = deflate_match_segs(len[b + k]);
+                for (uint32_t u = 3; u < ms; ++u) { units.push_back(k << kRecUnitShift | u); ++nm; }
             }
             rp0[m] = pos;
             tb0[m] = blk;
@@ -1048,6 +1059,7 @@ int rt::deflate_batch_device(const uint8_t* in, const uint64_t* in_off, const ui
             if (!lzs.empty()) HIPCHK(hipMemcpyAsync(d_lzs, Pl, lzs.size() * 4, hipMemcpyHostToDevice, s));
             a.rp0 = d_rp0; a.tb0 = d_tb0;
             a.mseg = d_units; a.nmseg = nmseg;
+            a.seg_merge = seg_merge ? 1u : 0u;
             a.cunit = d_units + nmseg; a.ncunit = (uint32_t)units.size() - nmseg;
             a.nbmax = nbmax;
             a.wide = m <= 256 ? 1u : 0u;                // few streams: the LDS-staged parse
