@@ -1413,6 +1413,11 @@ __global__ __launch_bounds__(PM_THREADS) void k_dfl_match(DeflateArgs A) {
 //                (with their gaps) in LDS.
 // Both chain lengths come from one walk as in k_dfl_match (the quarter window is ranks <= K/4).
 // Link word: (gap - 1) << 16 | distance, 0 if none (k_dfl_match4 stages it packed, m4_pack).
+// the record (k_dfl_match's word) of a search whose best is the 3-byte entry f3 (k_dfl_link4)
+__device__ __forceinline__ uint64_t m4_rec3(uint32_t f3, uint32_t lb) {
+    const uint32_t d = f3 & 0x7fffu, w = d ? (3u << 16) | d : 0u;
+    return rec_word(w, (f3 & 0x8000u) ? w : 0u, lb);
+}
 __global__ __launch_bounds__(PM_THREADS) void k_dfl_link4(DeflateArgs A) {
     __shared__ __attribute__((aligned(16))) uint8_t win[(PM_WINB + 15) & ~15];
     __shared__ __attribute__((aligned(16))) uint16_t pvl[PM_PV];
@@ -1459,14 +1464,16 @@ __global__ __launch_bounds__(PM_THREADS) void k_dfl_link4(DeflateArgs A) {
     }
     __syncthreads();
     GLB uint32_t* l4 = (GLB uint32_t*)A.l4_buf + rp;
-    GLB uint16_t* f3o = (GLB uint16_t*)A.f3_buf + rp;
+    GLB uint64_t* rec = (GLB uint64_t*)A.rec_buf + rp;
     const int K = c_config[A.level][3], Kq = K >> 2;
     // Each lane walks one position at a time and takes the next from an LDS counter itself,
     // one step ahead: its first link and 4 bytes are read in the step after the take, beside
     // the running walk's reads, so a new walk starts without a round trip of its own (walks are
     // short -- 7 entries on average at L6 -- and a wave-wide refill ran at nearly every step).
     // Walk: cur (relative) at rank r, res the link word so far, f3 the first entry whose bytes
-    // 0-1 agree (the 3-byte match): distance | (rank <= K/4) << 15, 0: none.
+    // 0-1 agree (the 3-byte match): distance | (rank <= K/4) << 15, 0: none.  The position's
+    // record is written here as if no entry of 4+ bytes existed; k_dfl_match4 replaces the
+    // halves (chain lengths) in which its walk finds one.
     int sp = 0, cur = 0, r = 0, limit = 0;
     uint32_t s4 = 0, res = 0, f3 = 0;
     bool busy = false;
@@ -1492,7 +1499,7 @@ __global__ __launch_bounds__(PM_THREADS) void k_dfl_link4(DeflateArgs A) {
             ++r;
             if (fin) {
                 l4[sp + ws] = res;
-                f3o[sp + ws] = (uint16_t)f3;
+                rec[sp + ws] = m4_rec3(f3, win[sp + ws > 0 ? sp - 1 : 0]);
                 busy = false;
             }
         }
@@ -1504,7 +1511,7 @@ __global__ __launch_bounds__(PM_THREADS) void k_dfl_link4(DeflateArgs A) {
             res = 0; f3 = 0; r = 1;
             limit = (np > MAX_DIST ? np - MAX_DIST : 0) - ws;
             busy = cur != 0 && sp - cur <= MAX_DIST;      // the first entry (deflate.ts:1092)
-            if (!busy) { l4[np] = 0u; f3o[np] = 0; }
+            if (!busy) { l4[np] = 0u; rec[np] = m4_rec3(0u, win[np > 0 ? sp - 1 : 0]); }
             stg = 0;
         }
         if (stg == 0) {
@@ -1520,18 +1527,23 @@ __global__ __launch_bounds__(PM_THREADS) void k_dfl_link4(DeflateArgs A) {
 #define M4_WALKERS 1                                     // 2: measured no faster
 #endif
 #define M4_WINB (W_SIZE + PM_SEG + MAX_MATCH + 16)
+#define M4_ESC 3968                                      // escape side table (fills the LDS)
 #define M4_PV (W_SIZE + PM_SEG)
 static uint32_t match4_blocks(uint32_t nmseg) { return (nmseg + 127u) & ~127u; }
 static uint32_t link4_blocks(uint32_t nmseg) { return (nmseg + 31u) & ~31u; }
 // A link staged in LDS as 16 bits: distance << 3 | gap for distances below 8192 and gaps up to 7
-// (~94 % of the links walked on text); 0: none; else 8 (the word is read from HBM)
+// (~94 % of the links walked on text); 0: none; else an escape, (k + 1) << 3 with the word in
+// the side table's entry k (m4_pack returns 8 for it; 0x1fff << 3: in HBM, the table full)
 __device__ __forceinline__ uint16_t m4_pack(uint32_t v) {
     const uint32_t d = v & 0xffffu, g = (v >> 16) + 1u;
     return (uint16_t)(d == 0u ? 0u : d < 8192u && g <= 7u ? d << 3 | g : 8u);
 }
-__device__ __forceinline__ void m4_unpack(uint32_t e, const GLB uint32_t* l4g, int x, bool live, int& dist, int& gap) {
+template <bool kHbm>
+__device__ __forceinline__ void m4_unpack(uint32_t e, const uint32_t* esc, const GLB uint32_t* l4g, int x, bool live,
+                                          int& dist, int& gap) {
     if (e & 7u) { dist = (int)(e >> 3); gap = (int)(e & 7u); return; }
-    const uint32_t v = e && live ? l4g[x] : 0u;
+    uint32_t v = 0;
+    if (e != 0u && live) v = kHbm && (e >> 3) == 0x1fffu ? l4g[x] : esc[(e >> 3) - 1u];
     dist = (int)(v & 0xffffu);
     gap = (int)(v >> 16) + 1;
 }
@@ -1551,62 +1563,29 @@ __device__ __forceinline__ int m4_lcp16(uint32_t x0, uint32_t x1, uint32_t x2, u
     const uint32_t x = x0 ? x0 : x1 ? x1 : x2 ? x2 : x3;
     return k == 16 ? 16 : k + (int)(__builtin_ctz(x) >> 3);
 }
-__global__ __launch_bounds__(PM_THREADS) void k_dfl_match4(DeflateArgs A) {
-    __shared__ __attribute__((aligned(16))) uint8_t win[(M4_WINB + 15) & ~15];
-    __shared__ __attribute__((aligned(16))) uint16_t lk[M4_PV];   // m4_pack words
-    __shared__ int pm_next;
-    const uint32_t tid = threadIdx.x;
-    const uint32_t lane = tid & 63u;
-    // block -> unit: of each 128 blocks, the 16 on XCD x (block % 8) take units 16 x .. 16 x + 15
-    const uint32_t bb = blockIdx.x, item = (bb & ~127u) | ((bb & 7u) << 4) | ((bb >> 3) & 15u);
-    const uint32_t u = item;
-    if (u >= A.nmseg) return;
-    const uint32_t sid = A.mseg[u] >> kRecUnitShift, seg = A.mseg[u] & ((1u << kRecUnitShift) - 1);
-    const uint64_t rp = A.rp0[sid];
-    if (rp == ~0ull) return;
-    const int n = (int)A.in_len[sid];
-    const int tail = n > PM_TAIL ? n - PM_TAIL : 0;
-    const int ge = (int)(seg * PM_SEG) + (A.seg_merge && seg == 0 ? 3 * PM_SEG : PM_SEG);
-    const int g1 = ge < tail ? ge : tail;
-    const int s0 = (int)(seg * PM_SEG), s1 = g1;
-    if (s0 >= s1) return;
-    const int ws = s0 > W_SIZE ? s0 - W_SIZE : 0;
-    const int we = s1 + MAX_MATCH + 8 < n ? s1 + MAX_MATCH + 8 : n;
-    const GLB uint8_t* in = (const GLB uint8_t*)(A.in + A.in_off[sid]);
-    const GLB uint16_t* f3g = (const GLB uint16_t*)A.f3_buf + rp;
-    const GLB uint32_t* l4g = (const GLB uint32_t*)A.l4_buf + rp + ws;   // relative to ws
-    {
-        const int nw = (we - ws) >> 2;
-        uint32_t* w32 = (uint32_t*)win;
-        for (int i = (int)tid; i < nw; i += PM_THREADS) {
-            uint32_t v;
-            __builtin_memcpy(&v, (const uint8_t*)(in + ws + 4 * i), 4);
-            w32[i] = v;
-        }
-        for (int i = 4 * nw + (int)tid; i < we - ws; i += PM_THREADS) win[i] = in[ws + i];
-        for (int i = (int)tid; i < s1 - ws; i += PM_THREADS) lk[i] = m4_pack(l4g[i]);
-        if (tid == 0) pm_next = s0;
-    }
-    __syncthreads();
-    GLB uint64_t* rec = (GLB uint64_t*)A.rec_buf + rp;
-    const int K = c_config[A.level][3], Kq = K >> 2, nice = c_config[A.level][2];
+// k_dfl_match4's walks (kHbm: the escape table overflowed, some link words stay in HBM)
+template <bool kHbm>
+__device__ __forceinline__ void m4_walks(const uint8_t* win, const uint16_t* lk, const uint32_t* esc,
+                                         const GLB uint32_t* l4g, GLB uint64_t* rec, int* pm_next, int ws, int s1,
+                                         int K, int Kq, int nice, unsigned long long* dbg, uint32_t lane) {
     // Each lane runs M4_WALKERS walks side by side (their LDS round trips overlap) and takes
     // the next position from an LDS counter itself, one step ahead (as k_dfl_link4): the taken
-    // position's link, its bytes 4-19 and its 3-byte entry are read in the step after the take,
-    // beside the running walks' reads; the first walker free takes it.
+    // position's link and bytes 4-19 are read in the step after the take, beside the running
+    // walks' reads; the first walker free takes it.  No HBM loads in the loop (a wait on one
+    // would also wait for every record store before it).
     // Walk k: position sp (relative to ws; < 0 none), its limit, the 4-byte candidate cur at rank cum.
     constexpr int W = M4_WALKERS;
     int sp[W], cur[W], cum[W], limit[W], best[W], bpos[W], qbest[W], qpos[W];
-    uint32_t pw[W][4], f3w[W];                               // p's bytes 4-19; its 3-byte entry
+    uint32_t pw[W][4];                                       // p's bytes 4-19
     bool busy[W];
 #pragma unroll
     for (int k = 0; k < W; ++k) {
         sp[k] = -1; cur[k] = cum[k] = limit[k] = bpos[k] = qpos[k] = 0; best[k] = qbest[k] = 2;
-        pw[k][0] = pw[k][1] = pw[k][2] = pw[k][3] = f3w[k] = 0u;
+        pw[k][0] = pw[k][1] = pw[k][2] = pw[k][3] = 0u;
         busy[k] = false;
     }
     int np = 0, stg = 0;                                     // the next position: 0 take, 1 read, 2 ready, 3 none
-    uint32_t ne = 0, npw[4] = { 0, 0, 0, 0 }, nf3 = 0;
+    uint32_t ne = 0, npw[4] = { 0, 0, 0, 0 };
     unsigned long long n_cand = 0, n_step = 0;               // SDZ_PHASE_TIMING counters
     for (;;) {
         // reads: each candidate's link and bytes 4-19; the taken position's link, bytes, 3-byte entry
@@ -1617,13 +1596,12 @@ __global__ __launch_bounds__(PM_THREADS) void k_dfl_match4(DeflateArgs A) {
             e[k] = lk[c];
             m4_w16(win, (uint32_t)(c + 4), m[k]);
         }
-        uint32_t pe = 0, ppw[4] = { 0, 0, 0, 0 }, pf3 = 0;
+        uint32_t pe = 0, ppw[4] = { 0, 0, 0, 0 };
         if (stg == 1) {
             pe = lk[np - ws];
             m4_w16(win, (uint32_t)(np - ws + 4), ppw);
-            pf3 = f3g[np];
         }
-        if (A.dbg) {
+        if (dbg) {
             ++n_step;
 #pragma unroll
             for (int k = 0; k < W; ++k) n_cand += __popcll(__ballot(busy[k]));
@@ -1633,7 +1611,7 @@ __global__ __launch_bounds__(PM_THREADS) void k_dfl_match4(DeflateArgs A) {
 #pragma unroll
         for (int k = 0; k < W; ++k) {
             nl[k] = ng[k] = 0;
-            m4_unpack(e[k], l4g, cur[k], busy[k], nl[k], ng[k]);
+            m4_unpack<kHbm>(e[k], esc, l4g, cur[k], busy[k], nl[k], ng[k]);
             len[k] = 4 + m4_lcp16(m[k][0] ^ pw[k][0], m[k][1] ^ pw[k][1], m[k][2] ^ pw[k][2], m[k][3] ^ pw[k][3]);
             more[k] = busy[k] && len[k] == 20;
         }
@@ -1669,26 +1647,24 @@ __global__ __launch_bounds__(PM_THREADS) void k_dfl_match4(DeflateArgs A) {
             cum[k] = busy[k] ? ncum : cum[k];
             busy[k] = busy[k] && !fin;
         }
-        if (stg == 1) { ne = pe; npw[0] = ppw[0]; npw[1] = ppw[1]; npw[2] = ppw[2]; npw[3] = ppw[3]; nf3 = pf3; stg = 2; }
+        if (stg == 1) { ne = pe; npw[0] = ppw[0]; npw[1] = ppw[1]; npw[2] = ppw[2]; npw[3] = ppw[3]; stg = 2; }
 #pragma unroll
         for (int k = 0; k < W; ++k) {
-            if (!busy[k] && sp[k] >= 0) {                    // the record of a walk that ended
-                const int f3d = (int)(f3w[k] & 0x7fffu);     // below 4 bytes: k_dfl_link4's 3-byte entry
-                if (best[k] < 4 && f3d) { best[k] = 3; bpos[k] = sp[k] - f3d; }
-                if (qbest[k] < 4 && (f3w[k] & 0x8000u)) { qbest[k] = 3; qpos[k] = sp[k] - f3d; }
-                const uint32_t full = best[k] > MIN_MATCH - 1 ? ((uint32_t)best[k] << 16) | (uint32_t)(sp[k] - bpos[k]) : 0u;
-                const uint32_t quarter = qbest[k] > MIN_MATCH - 1 ? ((uint32_t)qbest[k] << 16) | (uint32_t)(sp[k] - qpos[k]) : 0u;
-                rec[sp[k] + ws] = rec_word(full, quarter, win[sp[k] + ws > 0 ? sp[k] - 1 : 0]);
+            if (!busy[k] && sp[k] >= 0) {                    // a walk ended: the halves it improves
+                // (k_dfl_link4 wrote the record of the 3-byte entry; rec_word's layout)
+                const uint32_t lb = win[sp[k] + ws > 0 ? sp[k] - 1 : 0];
+                GLB uint32_t* r32 = (GLB uint32_t*)(rec + sp[k] + ws);
+                if (best[k] >= 4) r32[0] = ((uint32_t)best[k] << 16 | (uint32_t)(sp[k] - bpos[k])) | ((lb & 127u) << 25);
+                if (qbest[k] >= 4) r32[1] = ((uint32_t)qbest[k] << 16 | (uint32_t)(sp[k] - qpos[k])) | ((lb >> 7) << 25);
                 sp[k] = -1;
             }
             if (sp[k] < 0 && stg == 2) {                     // start the taken position
                 sp[k] = np - ws;
                 pw[k][0] = npw[0]; pw[k][1] = npw[1]; pw[k][2] = npw[2]; pw[k][3] = npw[3];
-                f3w[k] = nf3;
                 limit[k] = (np > MAX_DIST ? np - MAX_DIST : 0) - ws;
                 best[k] = 2; bpos[k] = 0; qbest[k] = 2; qpos[k] = 0;
                 int l = 0, g = 0;
-                m4_unpack(ne, l4g, sp[k], true, l, g);       // (no search at p: no link, deflate.ts:1092)
+                m4_unpack<kHbm>(ne, esc, l4g, sp[k], true, l, g);  // (no search at p: no link, deflate.ts:1092)
                 cur[k] = sp[k] - l;
                 cum[k] = g;
                 busy[k] = l != 0 && g <= K && (g == 1 || cur[k] > limit[k]);
@@ -1696,7 +1672,7 @@ __global__ __launch_bounds__(PM_THREADS) void k_dfl_match4(DeflateArgs A) {
             }
         }
         if (stg == 0) {
-            np = atomicAdd(&pm_next, 1);
+            np = atomicAdd(pm_next, 1);
             stg = np < s1 ? 1 : 3;
         }
         bool act = stg != 3;
@@ -1704,7 +1680,60 @@ __global__ __launch_bounds__(PM_THREADS) void k_dfl_match4(DeflateArgs A) {
         for (int k = 0; k < W; ++k) act = act || busy[k] || sp[k] >= 0;
         if (!__ballot(act)) break;
     }
-    if (A.dbg && lane == 0) { atomicAdd(&A.dbg[11], n_cand); atomicAdd(&A.dbg[12], n_step); }
+    if (dbg && lane == 0) { atomicAdd(&dbg[11], n_cand); atomicAdd(&dbg[12], n_step); }
+}
+__global__ __launch_bounds__(PM_THREADS) void k_dfl_match4(DeflateArgs A) {
+    __shared__ __attribute__((aligned(16))) uint8_t win[(M4_WINB + 15) & ~15];
+    __shared__ __attribute__((aligned(16))) uint16_t lk[M4_PV];   // m4_pack words
+    __shared__ uint32_t esc[M4_ESC];                               // link words of the escapes
+    __shared__ int pm_next, esc_n;
+    const uint32_t tid = threadIdx.x;
+    const uint32_t lane = tid & 63u;
+    // block -> unit: of each 128 blocks, the 16 on XCD x (block % 8) take units 16 x .. 16 x + 15
+    const uint32_t bb = blockIdx.x, item = (bb & ~127u) | ((bb & 7u) << 4) | ((bb >> 3) & 15u);
+    const uint32_t u = item;
+    if (u >= A.nmseg) return;
+    const uint32_t sid = A.mseg[u] >> kRecUnitShift, seg = A.mseg[u] & ((1u << kRecUnitShift) - 1);
+    const uint64_t rp = A.rp0[sid];
+    if (rp == ~0ull) return;
+    const int n = (int)A.in_len[sid];
+    const int tail = n > PM_TAIL ? n - PM_TAIL : 0;
+    const int ge = (int)(seg * PM_SEG) + (A.seg_merge && seg == 0 ? 3 * PM_SEG : PM_SEG);
+    const int g1 = ge < tail ? ge : tail;
+    const int s0 = (int)(seg * PM_SEG), s1 = g1;
+    if (s0 >= s1) return;
+    const int ws = s0 > W_SIZE ? s0 - W_SIZE : 0;
+    const int we = s1 + MAX_MATCH + 8 < n ? s1 + MAX_MATCH + 8 : n;
+    const GLB uint8_t* in = (const GLB uint8_t*)(A.in + A.in_off[sid]);
+    const GLB uint32_t* l4g = (const GLB uint32_t*)A.l4_buf + rp + ws;   // relative to ws
+    if (tid == 0) esc_n = 0;
+    __syncthreads();
+    {
+        const int nw = (we - ws) >> 2;
+        uint32_t* w32 = (uint32_t*)win;
+        for (int i = (int)tid; i < nw; i += PM_THREADS) {
+            uint32_t v;
+            __builtin_memcpy(&v, (const uint8_t*)(in + ws + 4 * i), 4);
+            w32[i] = v;
+        }
+        for (int i = 4 * nw + (int)tid; i < we - ws; i += PM_THREADS) win[i] = in[ws + i];
+        for (int i = (int)tid; i < s1 - ws; i += PM_THREADS) {
+            const uint32_t v = l4g[i];
+            uint32_t e = m4_pack(v);
+            if (e == 8u) {                                     // an escape: its word in the side table
+                const int k = atomicAdd(&esc_n, 1);
+                if (k < M4_ESC) { esc[k] = v; e = (uint32_t)(k + 1) << 3; }
+                else e = 0x1fffu << 3;                         // (table full: the word stays in HBM)
+            }
+            lk[i] = (uint16_t)e;
+        }
+        if (tid == 0) pm_next = s0;
+    }
+    __syncthreads();
+    GLB uint64_t* rec = (GLB uint64_t*)A.rec_buf + rp;
+    const int K = c_config[A.level][3], Kq = K >> 2, nice = c_config[A.level][2];
+    if (esc_n > M4_ESC) m4_walks<true>(win, lk, esc, l4g, rec, &pm_next, ws, s1, K, Kq, nice, A.dbg, lane);
+    else m4_walks<false>(win, lk, esc, l4g, rec, &pm_next, ws, s1, K, Kq, nice, A.dbg, lane);
 }
 
 // ------------------------------------------------------------------ record path: tail, parse, trees, encode

@@ -107,7 +107,6 @@ struct DeflateArgs {
     uint16_t* pv_buf;            // hash chain links: distance to the previous same-hash position
     uint32_t* l4_buf;            // levels 4-9 (null: k_dfl_match): per position the 4-byte chain link
                                  // and its rank in the hash chain (k_dfl_link4)
-    uint16_t* f3_buf;            // ... and the first chain entry with bytes 0-1 equal (3-byte match)
     uint32_t* sym_buf;           // the parse's symbols, u32 index 2 rp0[k] (normally rec_buf itself:
                                  // records are dead once parsed; a Deflater keeps its records)
     const uint64_t* rp0;         // n + 1 entries

@@ -871,8 +871,8 @@ int rt::deflate_batch_device(const uint8_t* in, const uint64_t* in_off, const ui
     // the segments final from earlier calls); SDZ_SEG_MERGE=0 turns it off
     const char* sme = getenv("SDZ_SEG_MERGE");
     const bool seg_merge = recpath && !ext && !(sme && sme[0] == '0');
-    // per position: record 8, link 2, parse words 8 + 4 + 3 bitmaps, 4-byte link 4 + 3-byte entry 2; per segment 28
-    const uint64_t kPosBytes = (lz_shift ? 8 + 2 + 8 + 4 + 1 : 8 + 2) + (match4 ? 6 : 0);
+    // per position: record 8, link 2, parse words 8 + 4 + 3 bitmaps, 4-byte link 4; per segment 28
+    const uint64_t kPosBytes = (lz_shift ? 8 + 2 + 8 + 4 + 1 : 8 + 2) + (match4 ? 4 : 0);
     auto rec_cost = [&](uint32_t i) -> uint64_t {
         if (!on_path(i)) return 0;
         const uint64_t p = (len[i] + 63) & ~63ull;
@@ -1003,10 +1003,7 @@ int rt::deflate_batch_device(const uint8_t* in, const uint64_t* in_off, const ui
                 a.rec_buf = (uint64_t*)take((size_t)pos * 8);
                 a.pv_buf = (uint16_t*)take((size_t)pos * 2);
                 a.sym_buf = (uint32_t*)a.rec_buf;
-                if (match4) {
-                    a.l4_buf = (uint32_t*)take((size_t)pos * 4);
-                    a.f3_buf = (uint16_t*)take((size_t)pos * 2);
-                }
+                if (match4) a.l4_buf = (uint32_t*)take((size_t)pos * 4);
             }
             a.blk = take((size_t)blk * FB_SLOT_BYTES);
             a.cks = (int32_t*)take((size_t)m * 4);

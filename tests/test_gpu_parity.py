@@ -376,13 +376,14 @@ def _rank_stress(rng, n):
 def test_deflate_4byte_chain_search(monkeypatch, paradise, level):
     """Levels 4-9 search over 4-byte chains (k_dfl_link4 / k_dfl_match4): bit-exact with the
     oracle and with the hash-chain walk (k_dfl_match, SDZ_MATCH4=0) on hash collisions, ranks
-    past max_chain (gaps past 256 at levels 8-9), long runs, random bytes and the bench's text
-    slices."""
+    past max_chain (gaps past 256 at levels 8-9), long runs, random bytes, the bench's text
+    slices, and links too far for the 16-bit LDS form (the escape table, and its overflow)."""
     monkeypatch.setenv("SDZ_MATCH4", "1")
     rng = random.Random(23 + level)
     inputs = [_collision_text(rng, 65536), _collision_text(rng, 150000), _rank_stress(rng, 65536),
               _rank_stress(rng, 120000), paradise[7:65543], text_corpus(rng, 40000) + b"b" * 30000,
-              bytes(rng.getrandbits(8) for _ in range(50000)), _periodic(rng, 70000), binary_corpus(rng, 80000)]
+              bytes(rng.getrandbits(8) for _ in range(50000)), _periodic(rng, 70000), binary_corpus(rng, 80000),
+              bytes(rng.getrandbits(8) for _ in range(10000)) * 7]     # every link 10,000 back: escapes
     exp = [O.deflate(d, level=level) for d in inputs]
     gpu = sdz.deflate_batch(inputs, level=level)
     for i, (g, e) in enumerate(zip(gpu, exp)):
