@@ -1280,6 +1280,7 @@ __global__ __launch_bounds__(PM_THREADS) void k_dfl_match(DeflateArgs A) {
     int p = s0, sp = 0, cur = 0, nxt = 0, best = 0, bpos = 0, qbest = 0, qpos = 0, chain = 0, limit = 0;
     uint32_t s4 = 0, sbv = 0;
     (void)sbv;
+    unsigned long long n_live = 0, n_step = 0, n_fill = 0;   // SDZ_PHASE_TIMING counters
     for (;;) {
         // Idle lanes store their records and take the next positions once PM_REFILL lanes
         // are idle (or all are): the refill and the record store then run once per several
@@ -1302,6 +1303,7 @@ __global__ __launch_bounds__(PM_THREADS) void k_dfl_match(DeflateArgs A) {
                 }
             }
             if (next >= q1 && nidle == 64) break;
+            ++n_fill;
             if (next < q1) {
                 const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(im >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)im, 0u));
                 const int pn = next + (int)rank;
@@ -1329,6 +1331,7 @@ __global__ __launch_bounds__(PM_THREADS) void k_dfl_match(DeflateArgs A) {
         // a candidate that passes gets its exact length.  The links after c2 (c3, then c4)
         // are read in turn, so the next step starts with two candidates again.
         const bool live = chain > 0;
+        if (A.dbg) { ++n_step; n_live += __popcll(__ballot(live)); }
         const bool go1 = nxt > limit && chain > 1;           // the walk continues after c1
         const bool l2 = live && go1;                          // c2 is walked (unless nice at c1)
         const uint32_t c1 = (uint32_t)(live ? cur : sp), c2 = (uint32_t)(l2 ? nxt : sp);
@@ -1391,6 +1394,7 @@ __global__ __launch_bounds__(PM_THREADS) void k_dfl_match(DeflateArgs A) {
         pend = pend || fin;                                   // stored at the next refill
         chain = fin ? 0 : chain - 2;
     }
+    if (A.dbg && lane == 0) { atomicAdd(&A.dbg[13], n_live); atomicAdd(&A.dbg[14], n_step); atomicAdd(&A.dbg[15], n_fill); }
 }
 
 // ------------------------------------------------------------------ levels 4-9: search over 4-byte chains
