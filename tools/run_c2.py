@@ -22,6 +22,7 @@ def main():
     ap.add_argument("--steps", type=int, default=2)
     ap.add_argument("--streams", type=int, default=65536)
     ap.add_argument("--level", type=int, default=6)
+    ap.add_argument("--slice", type=int, default=65536, help="deflate: bytes per stream")
     args = ap.parse_args()
     L = sdz.lib()
     L.sdz_set_timing(1)
@@ -76,12 +77,13 @@ def main():
     else:
         # the bench's C3 layout: distinct slices of paradiselost.txt at xorshift64 offsets
         # (identical streams would run the serial parse without any lane divergence)
-        b = DeviceBatch(sdz, text[:65536], args.streams, int(L.sdz_deflate_bound(65536, 1, 0)))
+        sl = args.slice
+        b = DeviceBatch(sdz, text[:sl], args.streams, int(L.sdz_deflate_bound(sl, 1, 0)))
         if not args.same:
-            fill_slices(sdz, b, text, slice_offsets(args.streams, len(text) - 65536), 65536)
+            fill_slices(sdz, b, text, slice_offsets(args.streams, len(text) - sl), sl)
         for i in range(args.steps):
             ms = deflate_step(sdz, b, args.level, 1)
-            print("deflate step %d: kernel %.3f ms, %.2f GB/s in" % (i, ms, 65536 * args.streams / ms / 1e6),
+            print("deflate step %d: kernel %.3f ms, %.2f GB/s in" % (i, ms, sl * args.streams / ms / 1e6),
                   flush=True)
     b.free()
 
