@@ -1,9 +1,6 @@
-# development GPU call: deflate with and without the 4-byte chain search by slice size and level
+# development GPU call: deflate parity, then the C3 kernel split
 export TMPDIR=/tmp; mkdir -p gpurun_out
-for m in 0 1; do
-  echo "== SDZ_MATCH4=$m"
-  for sl in 16384 32768 49152 131072; do for lv in 6 9; do
-    n=$((65536 * 65536 / sl))
-    SDZ_MATCH4=$m timeout -k 10 120 python3 tools/run_c2.py --mode deflate --steps 1 --level $lv --slice $sl --streams $n 2>&1 | grep step | sed "s/^/slice $sl L$lv /" || exit 1
-  done; done
-done
+timeout -k 10 400 python3 -u -m pytest tests/test_gpu_parity.py tests/test_gpu_deflate_stream.py tests/test_gpu_dict.py -x -q --timeout 200 --timeout-method thread -k "deflate or dict" > gpurun_out/pt_dev.log 2>&1; rc=$?; tail -1 gpurun_out/pt_dev.log; [ $rc -ne 0 ] && exit $rc
+rm -rf gpurun_out/devkt
+timeout -k 10 200 rocprofv3 --kernel-trace --stats -d gpurun_out/devkt -o run -- python3 tools/run_c2.py --mode deflate --steps 1 > gpurun_out/dev.log 2>&1 || exit 1
+grep "step" gpurun_out/dev.log; python3 tools/kt_db.py gpurun_out/devkt/run_results.db | head -8
