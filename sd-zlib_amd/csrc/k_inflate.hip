@@ -47,7 +47,7 @@ namespace sdz {
 #define IL_TSTRIDE 136                // LDS bytes per stream for the token stage (8-aligned)
 #define IL_BAD_IDX 300                // rank selected by codes past lim[15]
 #ifndef IL_PEEK_PAR
-#define IL_PEEK_PAR 0                 // peek from the pre-refill words beside the refill's compare
+#define IL_PEEK_PAR 1                 // peek from the pre-refill words beside the refill's compare
 #endif
 
 // LDS: per-stream symbol tables, then per-stream token stages (file scope, so the

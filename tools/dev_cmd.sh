@@ -1,7 +1,5 @@
-# development GPU call: C3 with the segment-parallel parse at forced segment sizes
+# development GPU call: the full GPU suite, then the bench line
 export TMPDIR=/tmp; mkdir -p gpurun_out
-for sh in 16 15 14 13; do
-  rm -rf gpurun_out/devkt
-  SDZ_LZ_SHIFT=$sh timeout -k 10 200 rocprofv3 --kernel-trace --stats -d gpurun_out/devkt -o run -- python3 tools/run_c2.py --mode deflate --steps 1 > gpurun_out/dev.log 2>&1 || exit 1
-  echo "== shift $sh"; grep "step" gpurun_out/dev.log; python3 tools/kt_db.py gpurun_out/devkt/run_results.db | grep "k_lz\|k_dfl_parse"
-done
+timeout -k 10 700 python3 -u -m pytest tests -m gpu -x -q --timeout 240 --timeout-method thread > gpurun_out/pt.log 2>&1; rc=$?; tail -1 gpurun_out/pt.log; [ $rc -ne 0 ] && exit $rc
+timeout -k 10 400 python3 bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err || exit 1
+python3 -c "import json; d=json.loads(open('gpurun_out/bench.json').read()); print(d['value'], d['roofline']['kernels_ms'], d['inflate_distinct']['roofline']['kernels_ms'], d['deflate']['kernel_ms'])"
