@@ -1794,8 +1794,66 @@ __device__ __forceinline__ int64_t slide_off(int64_t n, int64_t P) {
 // runs in the window coordinates the reference has at P; pv holds each position's distance
 // to its previous same-hash position (0: none), and the reference's rebased links (0 below
 // the window) end a walk exactly where these would pass `limit`.
-// The search itself, on window accessors: prevw(i) the window index of index i's predecessor
-// (0: none), wb(i) the window byte at index i (strstart: P's window index).
+__device__ uint64_t tail_search(const GLB uint8_t* in, const GLB uint16_t* pv, int64_t n, int64_t P, int chain_length,
+                                int nice) {
+    const int64_t off = slide_off(n, P);
+    const int strstart = (int)(P - off);
+    auto prev_of = [&](int64_t q) -> int {                // window index of q's predecessor (0: none)
+        const uint32_t d = pv[q];
+        const int64_t r = q - (int64_t)d;
+        return d && r > off ? (int)(r - off) : 0;
+    };
+    auto wb = [&](int i) -> uint32_t { return win_byte(in, n, off, i); };
+    int cur = prev_of(P);
+    if (cur == 0 || ((strstart - cur) & 0xffff) > MAX_DIST) return 0u;      // no search (deflate.ts:1092)
+    const int lookahead = (int)(n - P);
+    if (nice > lookahead) nice = lookahead;
+    const int limit = strstart > MAX_DIST ? strstart - MAX_DIST : 0;
+    const int qchain = chain_length >> 2;
+    int best = MIN_MATCH - 1, bstart = 0, qbest = -1, qstart = 0, k = 0;
+    uint32_t scan_end1 = wb(strstart + best - 1), scan_end = wb(strstart + best);
+    const uint32_t c0 = wb(strstart), c1 = wb(strstart + 1);
+    // The link and the four checked bytes of a candidate are loaded together, and a long
+    // compare takes 4 byte pairs per step, so the walk waits on one memory round trip per
+    // candidate rather than on one per load.
+    do {
+        const int match = cur;
+        const int nx = prev_of(match + off);
+        const uint32_t e0 = wb(match + best), e1 = wb(match + best - 1);
+        const uint32_t m0 = wb(match), m1 = wb(match + 1);
+        if ((e0 == scan_end) & (e1 == scan_end1) & (m0 == c0) & (m1 == c1)) {
+            int len = 3;                      // byte 2 is not compared (equal hash, deflate.ts:891-897)
+            for (bool go = true; go && len < MAX_MATCH;) {
+                uint32_t x[4], y[4];
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    x[i] = wb(strstart + len + i);
+                    y[i] = wb(match + len + i);
+                }
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    if (go && len < MAX_MATCH && x[i] == y[i]) ++len;
+                    else go = false;
+                }
+            }
+            if (len > best) {
+                bstart = match;
+                best = len;
+                if (len >= nice) break;
+                scan_end1 = wb(strstart + best - 1);
+                scan_end = wb(strstart + best);
+            }
+        }
+        if (++k == qchain) { qbest = best; qstart = bstart; }
+        cur = nx;
+    } while (cur > limit && --chain_length != 0);
+    if (qbest < 0) { qbest = best; qstart = bstart; }
+    const uint32_t full = best > MIN_MATCH - 1 ? ((uint32_t)best << 16) | (uint32_t)(strstart - bstart) : 0u;
+    const uint32_t quarter = qbest > MIN_MATCH - 1 ? ((uint32_t)qbest << 16) | (uint32_t)(strstart - qstart) : 0u;
+    return ((uint64_t)quarter << 32) | full;
+}
+// tail_search's walk (above) on window accessors, for k_dfl_tail_lds: prevw(i) the window index
+// of index i's predecessor (0: none), wb(i) the window byte at index i (strstart: P's index).
 template <class PrevW, class WB>
 __device__ __forceinline__ uint64_t tail_core(int strstart, int64_t n, int64_t P, int chain_length, int nice,
                                               PrevW prevw, WB wb) {
@@ -1846,24 +1904,6 @@ __device__ __forceinline__ uint64_t tail_core(int strstart, int64_t n, int64_t P
     const uint32_t full = best > MIN_MATCH - 1 ? ((uint32_t)best << 16) | (uint32_t)(strstart - bstart) : 0u;
     const uint32_t quarter = qbest > MIN_MATCH - 1 ? ((uint32_t)qbest << 16) | (uint32_t)(strstart - qstart) : 0u;
     return ((uint64_t)quarter << 32) | full;
-}
-// deflate.ts:827-946 at original position P (lookahead >= MIN_MATCH), from best_len = 2, for
-// chain_length and chain_length >> 2 in one walk: the shorter walk is the longer one's first
-// qchain candidates.  Record word as in k_dfl_match (quarter in the high half).  The search
-// runs in the window coordinates the reference has at P; pv holds each position's distance
-// to its previous same-hash position (0: none), and the reference's rebased links (0 below
-// the window) end a walk exactly where these would pass `limit`.
-__device__ uint64_t tail_search(const GLB uint8_t* in, const GLB uint16_t* pv, int64_t n, int64_t P, int chain_length,
-                                int nice) {
-    const int64_t off = slide_off(n, P);
-    auto prevw = [&](int i) -> int {                      // window index of i's predecessor (0: none)
-        const int64_t q = i + off;
-        const uint32_t d = pv[q];
-        const int64_t r = q - (int64_t)d;
-        return d && r > off ? (int)(r - off) : 0;
-    };
-    auto wb = [&](int i) -> uint32_t { return win_byte(in, n, off, i); };
-    return tail_core((int)(P - off), n, P, chain_length, nice, prevw, wb);
 }
 // k_dfl_tail with the window the last positions search (and its links) staged in LDS, per
 // group of positions with one window offset (a slide can fall inside the last PM_TAIL
