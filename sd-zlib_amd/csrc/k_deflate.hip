@@ -1852,110 +1852,6 @@ __device__ uint64_t tail_search(const GLB uint8_t* in, const GLB uint16_t* pv, i
     const uint32_t quarter = qbest > MIN_MATCH - 1 ? ((uint32_t)qbest << 16) | (uint32_t)(strstart - qstart) : 0u;
     return ((uint64_t)quarter << 32) | full;
 }
-// tail_search's walk (above) on window accessors, for k_dfl_tail_lds: prevw(i) the window index
-// of index i's predecessor (0: none), wb(i) the window byte at index i (strstart: P's index).
-template <class PrevW, class WB>
-__device__ __forceinline__ uint64_t tail_core(int strstart, int64_t n, int64_t P, int chain_length, int nice,
-                                              PrevW prevw, WB wb) {
-    int cur = prevw(strstart);
-    if (cur == 0 || ((strstart - cur) & 0xffff) > MAX_DIST) return 0u;      // no search (deflate.ts:1092)
-    const int lookahead = (int)(n - P);
-    if (nice > lookahead) nice = lookahead;
-    const int limit = strstart > MAX_DIST ? strstart - MAX_DIST : 0;
-    const int qchain = chain_length >> 2;
-    int best = MIN_MATCH - 1, bstart = 0, qbest = -1, qstart = 0, k = 0;
-    uint32_t scan_end1 = wb(strstart + best - 1), scan_end = wb(strstart + best);
-    const uint32_t c0 = wb(strstart), c1 = wb(strstart + 1);
-    // The link and the four checked bytes of a candidate are loaded together, and a long
-    // compare takes 4 byte pairs per step, so the walk waits on one memory round trip per
-    // candidate rather than on one per load.
-    do {
-        const int match = cur;
-        const int nx = prevw(match);
-        const uint32_t e0 = wb(match + best), e1 = wb(match + best - 1);
-        const uint32_t m0 = wb(match), m1 = wb(match + 1);
-        if ((e0 == scan_end) & (e1 == scan_end1) & (m0 == c0) & (m1 == c1)) {
-            int len = 3;                      // byte 2 is not compared (equal hash, deflate.ts:891-897)
-            for (bool go = true; go && len < MAX_MATCH;) {
-                uint32_t x[4], y[4];
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    x[i] = wb(strstart + len + i);
-                    y[i] = wb(match + len + i);
-                }
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    if (go && len < MAX_MATCH && x[i] == y[i]) ++len;
-                    else go = false;
-                }
-            }
-            if (len > best) {
-                bstart = match;
-                best = len;
-                if (len >= nice) break;
-                scan_end1 = wb(strstart + best - 1);
-                scan_end = wb(strstart + best);
-            }
-        }
-        if (++k == qchain) { qbest = best; qstart = bstart; }
-        cur = nx;
-    } while (cur > limit && --chain_length != 0);
-    if (qbest < 0) { qbest = best; qstart = bstart; }
-    const uint32_t full = best > MIN_MATCH - 1 ? ((uint32_t)best << 16) | (uint32_t)(strstart - bstart) : 0u;
-    const uint32_t quarter = qbest > MIN_MATCH - 1 ? ((uint32_t)qbest << 16) | (uint32_t)(strstart - qstart) : 0u;
-    return ((uint64_t)quarter << 32) | full;
-}
-// k_dfl_tail with the window the last positions search (and its links) staged in LDS, per
-// group of positions with one window offset (a slide can fall inside the last PM_TAIL
-// positions: at most two groups).  The walks then wait on LDS instead of HBM round trips.
-#define TL_WIN (MAX_DIST + PM_TAIL + MAX_MATCH + 16)     // window bytes a group's searches read
-#define TL_LNK (MAX_DIST + PM_TAIL + 8)                  // links: from the lowest limit to the last position
-__global__ __launch_bounds__(256) void k_dfl_tail_lds(DeflateArgs A) {
-    __shared__ uint8_t W[(TL_WIN + 3) & ~3];
-    __shared__ uint16_t Lk[TL_LNK];
-    __shared__ long long psplit;
-    const uint32_t sid = blockIdx.x;
-    if (sid >= A.n) return;
-    const uint64_t rp = A.rp0[sid];
-    if (rp == ~0ull) return;
-    const int64_t n = (int64_t)A.in_len[sid], tail = n > PM_TAIL ? n - PM_TAIL : 0;
-    if (tail >= n) return;
-    const GLB uint8_t* in = (const GLB uint8_t*)(A.in + A.in_off[sid]);
-    const GLB uint16_t* pv = (const GLB uint16_t*)A.pv_buf + rp;
-    GLB uint64_t* rec = (GLB uint64_t*)A.rec_buf + rp;
-    const int max_chain = c_config[A.level][3], nice = c_config[A.level][2];
-    const int64_t offA = slide_off(n, tail), offB = slide_off(n, n - 1);
-    if (threadIdx.x == 0) psplit = n;
-    __syncthreads();
-    if (offA != offB)                                    // the first position of the second group
-        for (int64_t P = tail + (int64_t)threadIdx.x; P < n; P += 256)
-            if (slide_off(n, P) != offA) atomicMin(&psplit, (long long)P);
-    __syncthreads();
-    const int64_t ps = psplit;
-    for (int g = 0; g < (offA == offB ? 1 : 2); ++g) {
-        const int64_t off = g == 0 ? offA : offB, p0 = g == 0 ? tail : ps, p1 = g == 0 ? ps : n;
-        if (p0 >= p1) continue;
-        const int s_first = (int)(p0 - off), s_last = (int)(p1 - 1 - off);
-        const int lo = s_first > MAX_DIST ? s_first - MAX_DIST : 0;
-        const int whi = s_last + MAX_MATCH + 16, lhi = s_last + 1;   // [lo, whi) bytes, [lo, lhi) links
-        for (int i = lo + (int)threadIdx.x; i < whi; i += 256) W[i - lo] = (uint8_t)win_byte(in, n, off, i);
-        for (int i = lo + (int)threadIdx.x; i < lhi; i += 256) {
-            const int64_t q = i + off;
-            const uint32_t d = pv[q];
-            const int64_t r = q - (int64_t)d;
-            Lk[i - lo] = (uint16_t)(d && r > off ? r - off : 0);
-        }
-        __syncthreads();
-        auto prevw = [&](int i) -> int { return (int)Lk[i - lo]; };
-        auto wb = [&](int i) -> uint32_t { return W[i - lo]; };
-        // the last MIN_MATCH - 1 positions are not searched; their records carry only the byte
-        for (int64_t P = p0 + (int64_t)threadIdx.x; P < p1; P += 256) {
-            const uint64_t r = P <= n - MIN_MATCH ? tail_core((int)(P - off), n, P, max_chain, nice, prevw, wb) : 0ull;
-            rec[P] = rec_word((uint32_t)r, (uint32_t)(r >> 32), in[P > 0 ? P - 1 : 0]);
-        }
-        __syncthreads();
-    }
-}
 __global__ __launch_bounds__(256) void k_dfl_tail(DeflateArgs A) {
     const uint32_t sid = blockIdx.x;
     if (sid >= A.n) return;
@@ -3208,10 +3104,6 @@ int device_max_u64(const uint64_t* v, uint32_t n, unsigned long long* d_slot, ui
 }
 
 static bool c_config_host_fast(int level) { return level >= 1 && level <= 3; }
-static bool tail_lds() {                                  // SDZ_TAIL_LDS=1 / 0 overrides the default
-    const char* e = getenv("SDZ_TAIL_LDS");
-    return e ? e[0] == '1' : false;
-}
 constexpr uint32_t kFzRounds = 1024;                       // then the unsettled streams go serial
 
 // side/ev (optional): a second stream and an event for it.  The input checksum depends on
@@ -3233,8 +3125,7 @@ void launch_deflate(const DeflateArgs& a, hipStream_t st, hipStream_t side, hipE
                 hipLaunchKernelGGL(k_dfl_link4, dim3(link4_blocks(a.nmseg)), dim3(PM_THREADS), 0, st, a);
                 hipLaunchKernelGGL(k_dfl_match4, dim3(match4_blocks(a.nmseg)), dim3(PM_THREADS), 0, st, a);
             } else if (a.nmseg) hipLaunchKernelGGL(k_dfl_match, dim3(a.nmseg), dim3(PM_THREADS), 0, st, a);
-            if (tail_lds()) hipLaunchKernelGGL(k_dfl_tail_lds, dim3(a.n), dim3(256), 0, st, a);
-            else hipLaunchKernelGGL(k_dfl_tail, dim3(a.n), dim3(256), 0, st, a);
+            hipLaunchKernelGGL(k_dfl_tail, dim3(a.n), dim3(256), 0, st, a);
         }
         const bool fork = side && ev && hipEventRecord(ev, st) == hipSuccess &&
                           hipStreamWaitEvent(side, ev, 0) == hipSuccess;
