@@ -357,15 +357,48 @@ def cpu_deflater(srcs, level):
     return one
 
 
+def cpu_threads():
+    """Host threads for the CPU baseline: every core this process may run on, capped at the
+    GPU box's CPU share for one GPU (OMP_NUM_THREADS, 16 there; the box's nproc counts the
+    whole machine, whose other cores belong to the other GPUs' jobs)."""
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except AttributeError:
+        avail = os.cpu_count() or 1
+    share = os.environ.get("OMP_NUM_THREADS")
+    return max(1, min(avail, int(share))) if share and share.isdigit() else max(1, avail), avail
+
+
 def cpu_baseline(work_one, seconds, unit_bytes_fn, sample):
     """all-threads and one-thread runs of the same work; value in MB/s of unit_bytes_fn"""
-    threads = max(1, min(16, os.cpu_count() or 1))
+    threads, avail = cpu_threads()
     cnt, nb, dt = cpu_run(work_one, seconds, threads)
     c1, nb1, d1 = cpu_run(work_one, max(0.5, seconds / 2), 1)
+    per_core = unit_bytes_fn(c1, nb1) / d1 / 1e6
+    nproc = os.cpu_count() or 1
     return {"value": round(unit_bytes_fn(cnt, nb) / dt / 1e6, 2), "unit": "MB/s", "cores": threads, "kind": "port",
-            "per_core_MBps": round(unit_bytes_fn(c1, nb1) / d1 / 1e6, 2),
-            "sample": "%s: %d units on %d threads in %.1f s; per core: %d in %.1f s on 1 thread"
-                      % (sample, cnt, threads, dt, c1, d1)}
+            "per_core_MBps": round(per_core, 2), "nproc": nproc, "affinity_cores": avail,
+            "all_cores_linear_MBps": round(per_core * nproc, 1),
+            "sample": "%s: %d units on %d threads in %.1f s; per core: %d in %.1f s on 1 thread; threads = the "
+                      "box's CPU share for one GPU (OMP_NUM_THREADS) of nproc %d; all_cores_linear_MBps = per-core "
+                      "x nproc, the machine-wide ceiling" % (sample, cnt, threads, dt, c1, d1, nproc)}
+
+
+def node_facade():
+    """The reference's perf case (test/perf.html:54-87: 20 samples of deflate(paradiselost.txt,
+    {level: 4}) and inflate(paradiselost.gz), extremes dropped) and C1 inflate(simple.deflate),
+    through the drop-in ES module under Node (tests/node/perf.mjs); ms."""
+    import shutil
+    import subprocess
+    node = shutil.which("node")
+    addon = os.path.join(ROOT, "sd-zlib_amd", "js", "sdz_napi.node")
+    if node is None or not os.path.exists(addon):
+        return {"skipped": "node or the N-API addon is not available"}
+    r = subprocess.run([node, os.path.join(ROOT, "tests", "node", "perf.mjs")], capture_output=True, text=True,
+                       timeout=300)
+    if r.returncode != 0:
+        return {"error": (r.stderr or r.stdout)[-400:]}
+    return json.loads(r.stdout.strip().splitlines()[-1])
 
 
 def facade_latency(sdz, reps=40):
@@ -444,7 +477,7 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=1.5)
     ap.add_argument("--deflate-streams", type=int, default=65536,
                     help="streams for the deflate leg (64 KiB slices, L6); 0 disables")
-    ap.add_argument("--deflate-steps", type=int, default=1)
+    ap.add_argument("--deflate-steps", type=int, default=3)
     ap.add_argument("--fast-steps", type=int, default=2,
                     help="steps of the opt-in fast (not bit-exact) compressor leg on the C3 slices (0: skip)")
     ap.add_argument("--distinct-steps", type=int, default=3,
@@ -458,7 +491,25 @@ def main():
                     help="streams for the host-buffer (PCIe-inclusive) inflate probe, e.g. 2048; off by "
                          "default so that the rocprofv3 stats of the default command hold C2 launches only")
     ap.add_argument("--latency", type=int, default=1, help="C1-style single-call latency of the facade (0: skip)")
+    ap.add_argument("--node", type=int, default=1,
+                    help="time the reference's own perf case (test/perf.html) through the Node facade (0: skip)")
     args = ap.parse_args()
+
+    # --gpus N (N > 1) outside torchrun: one rank per GPU under torch.distributed.run, started
+    # as a child process before anything touches a GPU; this process exits with its code
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        import socket
+        import subprocess
+        with socket.socket() as so:
+            so.bind(("127.0.0.1", 0))
+            port = so.getsockname()[1]
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(args.gpus),
+               "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+        log("bench.py: --gpus %d -> %s" % (args.gpus, " ".join(cmd)))
+        raise SystemExit(subprocess.call(cmd))
+    if int(os.environ.get("WORLD_SIZE", "1")) != args.gpus:
+        log("bench.py: WORLD_SIZE=%s differs from --gpus %d; n_gpus reports the ranks that ran"
+            % (os.environ.get("WORLD_SIZE"), args.gpus))
 
     import sdz
     L = sdz.lib()
@@ -633,6 +684,9 @@ def main():
     latency = None
     if rank == 0 and args.latency > 0:
         latency = facade_latency(sdz)
+    nodef = None
+    if rank == 0 and args.node > 0:
+        nodef = node_facade()
 
     cpu = None
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
@@ -681,6 +735,7 @@ def main():
         "inflate_distinct": distinct,
         "mixed": mixed,
         "facade_latency": latency,
+        "node_facade": nodef,
     }
     if rank == 0:
         print(json.dumps(line), flush=True)

@@ -206,6 +206,28 @@ __device__ __forceinline__ void ring_step(Hot& L) {
         if (lvl <= 32 && L.vp < L.vend) { L.s1 = *L.vp++; L.ns = 2; }
     }
 }
+// the same ring step for the wave decoder (k_inflate_wdec), whose tokens have their own stage
+__device__ __forceinline__ void ring_step_wd(Hot& L) {
+    if (L.ns) {
+        uint32_t k = (L.wpos >> 2) & 15u;
+        *(uint2*)(L.ring + k) = make_uint2(L.s0.x, L.s0.y);
+        *(uint2*)(L.ring + k + 2) = make_uint2(L.s0.z, L.s0.w);
+        L.wpos += 16;
+        if (L.ns == 2) {
+            k = (L.wpos >> 2) & 15u;
+            *(uint2*)(L.ring + k) = make_uint2(L.s1.x, L.s1.y);
+            *(uint2*)(L.ring + k + 2) = make_uint2(L.s1.z, L.s1.w);
+            L.wpos += 16;
+        }
+        L.ns = 0;
+    }
+    uint32_t lvl = L.wpos - L.rpos;
+    if (lvl <= 48 && L.vp < L.vend) {
+        L.s0 = *L.vp++;
+        L.ns = 1;
+        if (lvl <= 32 && L.vp < L.vend) { L.s1 = *L.vp++; L.ns = 2; }
+    }
+}
 __device__ __forceinline__ void br_init(Hot& L, const uint8_t* p, uint64_t bitpos, uint64_t total_bits,
                                         uint32_t* ring) {
     uintptr_t addr = (uintptr_t)(p + (bitpos >> 3));
@@ -994,14 +1016,22 @@ __device__ __forceinline__ bool seg_is_cand(const SegStop& G, uint64_t bit) {
     return lo < G.ncand && G.cand[lo] == bit;
 }
 
-template <int MODE>
+// WD: called by lane 0 of the wave decoder (k_inflate_wdec, one stream per wave: its own LDS
+// symbol bytes and token stage); force_slow: decode the current block's symbols with the
+// exact slow step to its end (the wave decoder's hand-back for errors, output room, tables
+// past its LDS budget and the last bits of the input)
+__shared__ __attribute__((aligned(16))) uint8_t wd_region[IL_REGION + 12];
+__shared__ __attribute__((aligned(16))) uint32_t wd_stage[IL_TSTRIDE / 4];
+template <int MODE, bool WD = false>
 __device__ __noinline__ void cold_run(DSave* S, const uint8_t* inp, uint64_t ilen, uint64_t cap,
                                       uint32_t* tb, uint32_t tcap, uint8_t* lens, int32_t format, int32_t has_dict,
-                                      int32_t dict_adler, uint32_t init, SegStop G) {
+                                      int32_t dict_adler, uint32_t init, SegStop G, int force_slow = 0) {
     Lane L;
     Tree LL, DD;
-    uint8_t* region = lane_region();
-    L.tb = tb; L.ts = lane_stage(); L.tcap = tcap; L.lens = lens;
+    uint8_t* region;
+    if constexpr (WD) { region = wd_region; L.ts = wd_stage; }
+    else { region = lane_region(); L.ts = lane_stage(); }
+    L.tb = tb; L.tcap = tcap; L.lens = lens;
     L.streaming = MODE == 1; L.stall = 0; L.ubit = 0;
     if (init) {
         L.mode = LM_TYPE; L.last = 0; L.status = SDZ_OK; L.zmsg = 0; L.container = SDZ_CONTAINER_RAW;
@@ -1038,10 +1068,11 @@ __device__ __noinline__ void cold_run(DSave* S, const uint8_t* inp, uint64_t ile
             if (L.mode == LM_TYPE && L.ubit != G.start && seg_is_cand(G, L.ubit)) { L.stall = SEG_HANDOVER; break; }
         }
         if (L.mode == LM_CODES) {
-            if (br_avail(L) >= 64 && (MODE != 1 || L.room >= 258)) break;   // hot_ready's preconditions
+            if (!force_slow && br_avail(L) >= 64 && (MODE != 1 || L.room >= 258)) break;   // hot_ready's preconditions
             slow_step(L, LL, DD, region);
             if (L.ntok + 3 > L.tcap) L.full = true;
         } else {
+            force_slow = 0;                               // (the block it applied to has ended)
             block_step(L, LL, DD, region);
             if (L.avail0 - L.avail > (1 << 28)) L.full = true;   // keeps the saturated counter exact
         }
@@ -1256,6 +1287,451 @@ __global__ __launch_bounds__(IL_THREADS, 1) void k_inflate_decode(InflateArgs A,
         for (int k = 0; k < IL_REGION / 4; ++k) ((uint32_t*)S->region)[k] = ((const uint32_t*)region)[k];
 }
 
+// ------------------------------------------------------------------ wave decoder
+//
+// k_inflate_wdec: one WAVE per stream.  Huffman codes resynchronise: decoding a block from a
+// bit offset that is not a symbol start falls onto the true symbol boundaries after a few
+// symbols (on text: median 6, 99.9 % within 76 symbols / 1,058 bits, measured on
+// paradiselost slices).  So an iteration cuts the current block's bits from the known
+// position B0 into up to 64 chunks of C bits, and lane j decodes chunk j speculatively with
+// the block's tables:
+//   - lane j > 0 records the symbol starts of its first WD_W bits in an LDS bitmap and emits
+//     one token per symbol there (so that the token index at a recorded start is the number
+//     of recorded starts before it);
+//   - past its chunk's end, lane j keeps decoding until it stands on a symbol start that
+//     lane j + 1 recorded (SYNC): from there both decode the same symbols, so lane j stops
+//     and lane j + 1's tokens from that index on are the true ones;
+//   - a lane also stops at an end of block (EOB), an invalid code (ERR), its token capacity
+//     (CAP), the last 64 input bits (END), or WD_W bits past its chunk without a sync (NOSYNC).
+// Lane 0 starts on a true symbol start, so the lanes 0..J linked by SYNCs decode exactly the
+// serial symbol sequence, J being the first lane that stopped otherwise; the stream goes on
+// from J's stop position.  Their tokens are compacted (in place, downwards) to the stream's
+// token ring, where k_inflate_resolve reads them as from k_inflate_decode.
+// Everything that is not the symbol loop of a Huffman block -- container header, block
+// headers and trees, stored blocks, trailer, the last input bits, and the exact handling of
+// errors and output room (a room overflow or an ERR hands the block to the slow step from
+// the iteration's start) -- is cold_run<0, WD> on lane 0.
+// Decoding uses two-level lookup tables in LDS (root 10 / 8 bits, built from the canonical
+// trees by the whole wave) instead of the lane-per-stream decoder's table-free registers: a
+// wave holds one stream, and its latency is hidden by the other waves on the SIMD.
+#ifndef WD_W
+#define WD_W 1024                 // bits of a lane's boundary map
+#endif
+#define WD_BMW (WD_W / 32)
+#ifndef WD_CAP
+#define WD_CAP 512                // provisional tokens per lane and iteration
+#endif
+#define WD_LLR 10                 // root bits of the literal/length table
+#define WD_DR 8                   // ... of the distance table
+#define WD_LLT 1536               // table entries (root + subtables)
+#define WD_DT 768
+#ifndef WD_CMAX
+#define WD_CMAX 4096              // chunk bits
+#endif
+#define WD_CMIN 256
+#define WD_MINSPEC 512            // bits past the last-64 reserve below which lane 0 runs the slow step
+#define WD_TST 16                 // token stage per lane (LDS)
+#define WD_INV 511u               // table symbol: invalid code
+
+__shared__ __attribute__((aligned(16))) uint16_t wd_ll[WD_LLT];
+__shared__ __attribute__((aligned(16))) uint16_t wd_dt[WD_DT];
+__shared__ __attribute__((aligned(16))) uint32_t wd_bm[64 * WD_BMW];
+__shared__ __attribute__((aligned(16))) uint32_t wd_ring[64 * 18];
+__shared__ __attribute__((aligned(16))) uint32_t wd_tst[64 * WD_TST];
+__shared__ __attribute__((aligned(16))) uint32_t wd_tree[2 * 33];   // lim[16], pk[17] of LL then DD
+
+enum : uint32_t { WR_RUN = 0, WR_SYNC, WR_EOB, WR_ERR, WR_CAP, WR_END, WR_NOSYNC, WR_CHUNK, WR_OFF };
+
+template <int CTRL, int ROWS>
+__device__ __forceinline__ uint32_t wd_dpp_add(uint32_t x) {
+    return x + (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, ROWS, 0xf, false);
+}
+__device__ __forceinline__ uint32_t wd_scan(uint32_t x) {   // inclusive wave scan (DPP)
+    x = wd_dpp_add<0x111, 0xf>(x);
+    x = wd_dpp_add<0x112, 0xf>(x);
+    x = wd_dpp_add<0x114, 0xf>(x);
+    x = wd_dpp_add<0x118, 0xf>(x);
+    x = wd_dpp_add<0x142, 0xa>(x);
+    x = wd_dpp_add<0x143, 0xc>(x);
+    return x;
+}
+__device__ __forceinline__ uint32_t wd_uni(uint32_t x) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)x); }
+__device__ __forceinline__ uint32_t wd_at(uint32_t x, uint32_t l) { return (uint32_t)__builtin_amdgcn_readlane((int)x, (int)l); }
+
+// table symbol of the code with 15-bit MSB-first prefix rc (low bits zero past the code's
+// length), and that length: literals 0-255, 256 end of block, 257-285 lengths, distance
+// symbols 0-29, WD_INV for codes past the tree's last code and the invalid symbols
+__device__ __forceinline__ uint32_t wd_code(const HTree& T, const uint8_t* syms, bool lit, uint32_t rc, uint32_t& len) {
+    if (rc >= T.lim[15]) { len = 15; return WD_INV; }
+    const uint32_t v = tsel(T, rc);
+    const int32_t idx = pk_rank(v, rc);
+    len = 15u - (v & 15u);
+    if (lit) {
+        if (idx >= 288) return WD_INV;
+        const uint32_t b = syms[idx];
+        if (idx < (int32_t)((v >> 5) & 511u)) return b;
+        return b >= 30 ? WD_INV : 256u + b;              // symbols 286, 287 (fixed tree): invalid
+    }
+    if (idx >= 30) return WD_INV;
+    return syms[IL_DSYM + idx];
+}
+// Two-level table: root entry = len | sym << 4 (direct) or 0x8000 | k | off << 4 (codes longer
+// than R bits under this prefix: a subtable of 2^k entries at off, k = the longest code's
+// length - R).  Returns false if the subtables do not fit (the block then runs the slow step).
+template <int R>
+__device__ __forceinline__ bool wd_table(const HTree& T, const uint8_t* syms, bool lit, uint16_t* tab, uint32_t cap) {
+    const uint32_t lane = threadIdx.x & 63u;
+    constexpr uint32_t NR = 1u << R, PER = NR / 64;
+    uint32_t need = 0;
+    uint32_t ks[PER];
+#pragma unroll
+    for (uint32_t m = 0; m < PER; ++m) {
+        const uint32_t i = lane + 64u * m;
+        const uint32_t rc = __builtin_bitreverse32(i) >> 17;
+        uint32_t len, k = 0;
+        uint32_t sym = wd_code(T, syms, lit, rc, len);
+        if (rc < T.lim[15] && len > R) {
+            uint32_t lm;
+            (void)wd_code(T, syms, lit, rc | ((1u << (15 - R)) - 1u), lm);
+            k = lm - R;
+            need += 1u << k;
+        } else if (rc >= T.lim[15]) {
+            len = 1;                                      // every code under this prefix is invalid
+            sym = WD_INV;
+        }
+        ks[m] = k;
+        if (k == 0) tab[i] = (uint16_t)(len | (sym << 4));
+    }
+    const uint32_t incl = wd_scan(need);
+    const uint32_t total = wd_at(incl, 63);
+    if (NR + total > cap) return false;
+    uint32_t off = NR + incl - need;
+#pragma unroll
+    for (uint32_t m = 0; m < PER; ++m) {
+        const uint32_t k = ks[m];
+        if (k == 0) continue;
+        const uint32_t i = lane + 64u * m;
+        tab[i] = (uint16_t)(0x8000u | k | (off << 4));
+        for (uint32_t j = 0; j < (1u << k); ++j) {
+            uint32_t len;
+            const uint32_t x = i | (j << R);
+            const uint32_t sym = wd_code(T, syms, lit, __builtin_bitreverse32(x) >> 17, len);
+            tab[off + j] = (uint16_t)(len | (sym << 4));
+        }
+        off += 1u << k;
+    }
+    return true;
+}
+// both tables from the trees in wd_tree and the symbol bytes in wd_region (whole wave)
+__device__ __noinline__ bool wd_build() {
+    HTree LL, DD;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) { LL.lim[k] = wd_tree[k]; DD.lim[k] = wd_tree[33 + k]; }
+#pragma unroll
+    for (int k = 0; k < 17; ++k) { LL.pk[k] = wd_tree[16 + k]; DD.pk[k] = wd_tree[33 + 16 + k]; }
+    const bool a = wd_table<WD_LLR>(LL, wd_region, true, wd_ll, WD_LLT);
+    const bool b = wd_table<WD_DR>(DD, wd_region, false, wd_dt, WD_DT);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+    return a && b;
+}
+
+// one symbol's table entry: root, then the subtable when the root entry links
+__device__ __forceinline__ uint32_t wd_look_ll(uint32_t pw) {
+    uint32_t e = wd_ll[pw & ((1u << WD_LLR) - 1u)];
+    if (e & 0x8000u) e = wd_ll[((e >> 4) & 2047u) + ((pw >> WD_LLR) & ((1u << (e & 15u)) - 1u))];
+    return e;
+}
+__device__ __forceinline__ uint32_t wd_look_d(uint32_t pw) {
+    uint32_t e = wd_dt[pw & ((1u << WD_DR) - 1u)];
+    if (e & 0x8000u) e = wd_dt[((e >> 4) & 2047u) + ((pw >> WD_DR) & ((1u << (e & 15u)) - 1u))];
+    return e;
+}
+
+struct WdRes {
+    uint32_t st, stop, ntk, synco;
+};
+
+// One speculative iteration of the current block from S->bitpos (all of the wave; see the
+// head comment).  Commits the chained lanes' tokens and the stream position to S (lane 0).
+// Returns 0: go on; 1: the block ended, or the last input bits need the cold path; 2: the
+// slow step must take this block from S->bitpos (an invalid code, or the output room);
+// 3: no token room left this round.  cmax: chunk bits (halved on CAP stops).
+__device__ __noinline__ int wd_iteration(DSave* S, const uint8_t* inp, uint64_t ilen, uint64_t cap,
+                                         uint32_t* tb, uint32_t tcap, uint64_t B0, uint32_t ntok0, uint64_t pos0,
+                                         uint32_t& cmax) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t tbits = ilen * 8;
+    const uint64_t lim64 = tbits - 64 - B0;
+    const uint32_t lim = (uint32_t)(lim64 > (1ull << 30) ? (1ull << 30) : lim64);
+    uint32_t C = lim / 64u;
+    C = C < WD_CMIN ? WD_CMIN : C > cmax ? cmax : C;
+    uint32_t n = lim / C;
+    n = n < 1u ? 1u : n > 64u ? 64u : n;
+    const uint32_t P0 = (ntok0 + 7u) & ~7u;               // provisional area: 8-token aligned
+    const uint32_t space = tcap > P0 + 8u ? tcap - P0 - 8u : 0u;
+    if (space < 64u) return 3;
+    if (space / n < 64u) n = space / 64u;
+    uint32_t tcapl = space / n;
+    tcapl = (tcapl > WD_CAP ? WD_CAP : tcapl) & ~7u;
+
+    const bool on = lane < n;
+    const bool lastl = lane == n - 1u;
+    const uint32_t bj = lane * C;
+    const uint32_t bn = lastl ? n * C : (lane + 1u) * C;
+    uint32_t* bm = wd_bm + lane * WD_BMW;
+    uint32_t* bmn = wd_bm + ((lane + 1u) & 63u) * WD_BMW;
+    uint32_t* tst = wd_tst + lane * WD_TST;
+    GLB uint32_t* prov = (GLB uint32_t*)(tb + P0 + lane * tcapl);
+#pragma unroll
+    for (int k = 0; k < WD_BMW; k += 4) *(uint4*)(bm + k) = make_uint4(0, 0, 0, 0);
+
+    Hot H;
+    H.ring = wd_ring + lane * 18u;
+    uint32_t Kc = 0;
+    if (on) {
+        br_init(H, inp, B0 + bj, tbits, H.ring);
+        H.vend = (g_uint4*)(((uintptr_t)(inp + ilen) + 15) & ~(uintptr_t)15);
+        Kc = (uint32_t)(H.base_bit - B0) + (uint32_t)H.avail0;   // rel = Kc - avail + bo
+    } else {
+        H.ns = 0; H.vp = H.vend = nullptr; H.wpos = H.rpos = 0; H.avail = 0; H.bo = 0;
+    }
+    uint32_t st = on ? WR_RUN : WR_OFF;
+    uint32_t prog = on ? 0u : 0x80000000u;                // offset recorded so far | stopped
+    uint32_t ntk = 0, nfl = 0, litw = 0, nlit = 0, stop = 0, synco = 0;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_wave_barrier();
+
+    auto push = [&](uint32_t t) { tst[ntk & (WD_TST - 1)] = t; ntk++; };
+    auto halt = [&](uint32_t why, uint32_t at) { st = why; stop = at; prog |= 0x80000000u; };
+
+    for (;;) {
+        const bool run = st == WR_RUN;
+        if (run) ring_step_wd(H);
+        // staged tokens -> the lane's provisional slot, 8 at a time (at most 8 per 4 steps)
+        {
+            const bool f = ntk - nfl >= 8u;
+            if (__ballot(f)) {
+                if (f) {
+                    const uint4* s4 = (const uint4*)(tst + (nfl & (WD_TST - 1)));
+                    const uint4 a = s4[0], b = s4[1];
+                    GLB uint4* d = (GLB uint4*)(prov + nfl);
+                    d[0] = a; d[1] = b;
+                    nfl += 8u;
+                }
+            }
+        }
+        // the successor's progress, for lanes past their chunk (stale by up to 4 steps: safe)
+        uint32_t sp = 0x80000000u;
+        {
+            const bool ov = run && !lastl && (Kc - (uint32_t)H.avail + H.bo) >= bn;
+            if (__ballot(ov)) sp = __shfl_down(prog, 1);
+        }
+#pragma unroll
+        for (int rep = 0; rep < 4; ++rep) {
+            if (st != WR_RUN) continue;
+            const uint32_t p = Kc - (uint32_t)H.avail + H.bo;
+            const uint32_t off = p - bj;
+            if (lane && off < WD_W) __hip_atomic_fetch_or(bm + (off >> 5), 1u << (off & 31u), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            prog = off;
+            if (p >= lim) { halt(WR_END, p); continue; }
+            if (ntk + 3u > tcapl) { halt(WR_CAP, p); continue; }
+            if (p >= bn) {
+                if (lastl) { halt(WR_CHUNK, p); continue; }
+                const uint32_t o = p - bn;
+                if (o >= WD_W) { halt(WR_NOSYNC, p); continue; }
+                if (o > (sp & 0x7fffffffu)) {
+                    if (sp >> 31) halt(WR_NOSYNC, p);
+                    continue;                             // the successor has not recorded o yet
+                }
+                if ((bmn[o >> 5] >> (o & 31u)) & 1u) { halt(WR_SYNC, p); synco = o; continue; }
+            }
+            uint32_t pw = br_refill_peek(H);
+            uint32_t e = wd_look_ll(pw);
+            uint32_t len = e & 15u, sym = (e >> 4) & 511u;
+            if (sym < 256u) {
+                H.bo += len;
+                litw |= sym << (8u * nlit);
+                ++nlit;
+                if (nlit == 3u || (lane && off < WD_W)) {  // one token per symbol in the recorded bits
+                    push(((nlit - 1u) << 24) | litw);
+                    nlit = 0; litw = 0;
+                }
+                continue;
+            }
+            if (sym == 256u) { H.bo += len; halt(WR_EOB, p + len); continue; }
+            if (sym > 285u) { halt(WR_ERR, p); continue; }
+            uint32_t ex;
+            uint32_t mlen = len_base(sym - 256u, ex);
+            mlen += (pw >> len) & ((1u << ex) - 1u);
+            H.bo += len + ex;
+            pw = br_refill_peek(H);
+            e = wd_look_d(pw);
+            len = e & 15u; sym = (e >> 4) & 511u;
+            if (sym >= 30u) { halt(WR_ERR, p); continue; }
+            uint32_t dist = dist_base(sym, ex);
+            dist += (pw >> len) & ((1u << ex) - 1u);
+            H.bo += len + ex;
+            if (nlit) { push(((nlit - 1u) << 24) | litw); nlit = 0; litw = 0; }
+            push(0x80000000u | ((mlen - 3u) << 16) | (dist - 1u));
+        }
+        if (!__ballot(st == WR_RUN)) break;
+    }
+    // pending literals, then the rest of the stage
+    if (nlit) { push(((nlit - 1u) << 24) | litw); nlit = 0; }
+    for (uint32_t q = nfl; q < ntk; ++q) prov[q] = tst[q & (WD_TST - 1)];
+
+    // the successor's start index: its recorded starts before the sync offset
+    uint32_t k = 0;
+    {
+        const bool sy = st == WR_SYNC;
+        const uint32_t wmax = sy ? synco >> 5 : 0u;
+        for (uint32_t w = 0; __ballot(sy && w <= wmax); ++w) {
+            if (sy && w <= wmax) {
+                uint32_t x = bmn[w];
+                if (w == wmax) x &= (1u << (synco & 31u)) - 1u;
+                k += __popc(x);
+            }
+        }
+    }
+    const uint32_t s0 = __shfl_up(k, 1);
+    const uint32_t s = lane ? s0 : 0u;
+    const uint64_t M = __ballot(st == WR_SYNC);
+    const uint32_t J = (uint32_t)__builtin_ctzll(~M);     // first lane not chained to its successor
+    const bool inc = lane <= J;
+    const uint32_t c = inc && ntk >= s ? ntk - s : 0u;
+    const uint32_t incl = wd_scan(c);
+    const uint32_t total = wd_at(incl, 63);
+    const uint32_t excl = incl - c;
+    const uint32_t stJ = wd_at(st, J), stopJ = wd_at(stop, J);
+    __threadfence_block();                                // provisional tokens visible to every lane
+    // compaction, lane by lane in order: destinations never pass their sources
+    uint32_t bytes = 0;
+    for (uint32_t j = 0; j <= J; ++j) {
+        const uint32_t cj = wd_at(c, j), sj = wd_at(s, j), dj = wd_at(excl, j);
+        const uint32_t* src = tb + P0 + j * tcapl + sj;
+        uint32_t* dst = tb + ntok0 + dj;
+        for (uint32_t q = lane; q < cj; q += 64u) {
+            const uint32_t t = src[q];
+            dst[q] = t;
+            bytes += (int32_t)t < 0 ? ((t >> 16) & 255u) + 3u : ((t >> 24) & 3u) + 1u;
+        }
+        __builtin_amdgcn_s_waitcnt(0);                    // this lane's reads are done before the next stores
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) bytes += __shfl_xor(bytes, o);
+    if (stJ == WR_CAP && J == 0 && cmax > WD_CMIN) cmax >>= 1;
+    if (pos0 + bytes > cap) return 2;                     // the slow step reports the overflow exactly
+    if (lane == 0) {
+        S->ntok = ntok0 + total;
+        S->pos = pos0 + bytes;
+        S->bitpos = B0 + stopJ;
+        S->litw = 0;
+        S->nlit = 0;
+        if (stJ == WR_EOB) S->mode = S->last ? LM_TRAILER : LM_TYPE;
+    }
+    __threadfence_block();
+    return stJ == WR_EOB || stJ == WR_END ? 1 : stJ == WR_ERR ? 2 : 0;
+}
+
+// lane 0: cold_run on the stream's state, with the open 32-token line staged from HBM before
+// and everything (pending literals included) written back after
+__device__ __forceinline__ void wd_cold(const InflateArgs& A, DSave* S, const uint8_t* inp, uint64_t ilen,
+                                        uint64_t cap, uint32_t* tb, uint32_t tcap, uint8_t* lens, uint32_t init,
+                                        int force_slow) {
+    if ((threadIdx.x & 63u) == 0) {
+        if (!init) {
+            const uint32_t nt = S->ntok, b = nt & ~(IL_TSTAGE - 1u);
+            for (uint32_t j = b; j < nt; ++j) wd_stage[j - b] = tb[j];
+        }
+        SegStop G = { 0, nullptr, 0 };
+        cold_run<0, true>(S, inp, ilen, cap, tb, tcap, lens, A.format, A.dict != nullptr,
+                          dict_id_of(A.dict_adler, A.dict_adler_dev), init, G, force_slow);
+        Core H;
+        H.tb = tb; H.ts = wd_stage; H.ntok = S->ntok; H.litw = S->litw; H.nlit = S->nlit;
+        tok_finish(H);
+        S->ntok = H.ntok; S->litw = 0; S->nlit = 0;
+        const uint32_t* tl = (const uint32_t*)&S->LL;
+        const uint32_t* td = (const uint32_t*)&S->DD;
+        for (int k = 0; k < 33; ++k) { wd_tree[k] = tl[k]; wd_tree[33 + k] = td[k]; }
+    }
+    __threadfence_block();
+    __builtin_amdgcn_wave_barrier();
+}
+
+__global__ __launch_bounds__(64) void k_inflate_wdec(InflateArgs A, uint32_t round) {
+    const uint32_t sid = blockIdx.x, lane = threadIdx.x;
+    if (sid >= A.n) return;
+    DSave* S = (DSave*)A.dsave + sid;
+    uint32_t* tb = A.tokens + (uint64_t)sid * A.round_tokens;
+    const uint32_t tcap = A.round_tokens;
+    uint8_t* lens = A.scratch + (uint64_t)sid * kInflateScratchPerStream;
+    const uint8_t* inp = A.in + A.in_off[sid];
+    const uint64_t ilen = A.in_len[sid];
+    const uint64_t cap = A.out_cap[sid];
+    const uint64_t tbits = ilen * 8;
+    bool live = false;
+    if (round == 0 && (A.out_off[sid] & 7)) {
+        if (lane == 0) {
+            S->mode = LM_DONE; S->status = SDZ_BAD_RECORD; S->zmsg = 0; S->bitpos = 0; S->pos = 0;
+            S->container = SDZ_CONTAINER_RAW; S->stored_ck = 0; S->stored_size = 0; S->mtime = 0;
+            S->name_off = 0; S->name_len = 0; S->dict_used = 0; S->ntok = 0; S->litw = 0;
+            S->nlit = 0; S->full = 0; S->stall = 0;
+        }
+    } else if (round == 0) {
+        live = true;
+        wd_cold(A, S, inp, ilen, cap, tb, tcap, lens, 1u, 0);
+    } else if (wd_uni(lane == 0 ? (uint32_t)S->mode : 0u) != LM_DONE) {
+        live = true;
+        for (uint32_t k = lane; k < IL_REGION / 4; k += 64) ((uint32_t*)wd_region)[k] = ((const uint32_t*)S->region)[k];
+        if (lane < 33) { wd_tree[lane] = ((const uint32_t*)&S->LL)[lane]; wd_tree[33 + lane] = ((const uint32_t*)&S->DD)[lane]; }
+        if (lane == 0) { S->ntok = 0; S->full = 0; }
+        __threadfence_block();
+        __builtin_amdgcn_wave_barrier();
+    }
+    bool stale = true;
+    int fslow = 0;
+    uint32_t cmax = WD_CMAX;
+    while (live) {
+        // the stream's state as lane 0 left it (lane 0 reads its own stores; broadcast)
+        const uint32_t mode = wd_uni(lane == 0 ? (uint32_t)S->mode : 0u);
+        const uint32_t full = wd_uni(lane == 0 ? (uint32_t)S->full : 0u);
+        if (mode == LM_DONE || full) break;
+        const uint64_t bp = lane == 0 ? S->bitpos : 0;
+        const uint64_t B0 = ((uint64_t)wd_uni((uint32_t)(bp >> 32)) << 32) | wd_uni((uint32_t)bp);
+        const uint32_t ntok = wd_uni(lane == 0 ? S->ntok : 0u);
+        const uint64_t ps = lane == 0 ? S->pos : 0;
+        const uint64_t pos = ((uint64_t)wd_uni((uint32_t)(ps >> 32)) << 32) | wd_uni((uint32_t)ps);
+        if (mode == LM_CODES && !fslow && tbits >= B0 + 64 + WD_MINSPEC && tcap >= ntok + 80u) {
+            if (stale) {
+                if (!wd_build()) { fslow = 1; continue; }
+                stale = false;
+            }
+            const int r = wd_iteration(S, inp, ilen, cap, tb, tcap, B0, ntok, pos, cmax);
+            if (r == 2) fslow = 1;
+            else if (r == 3) fslow = 1;
+            continue;
+        }
+        wd_cold(A, S, inp, ilen, cap, tb, tcap, lens, 0u, (fslow || mode == LM_CODES) ? 1 : 0);
+        fslow = 0;
+        stale = true;
+    }
+    const uint32_t smode = wd_uni(lane == 0 ? (uint32_t)S->mode : 0u);
+    const uint32_t sstall = wd_uni(lane == 0 ? (uint32_t)S->stall : 0u);
+    if (lane == 0) {
+        const bool more = live && smode != LM_DONE && !sstall;
+        if (more) atomicAdd(A.active, 1u);
+        if (!live) { A.ntok[sid] = 0; A.flags[sid] = 2; }
+        else {
+            A.ntok[sid] = S->ntok;
+            A.flags[sid] = smode == LM_DONE ? 1u : sstall ? 3u : 0u;
+        }
+    }
+    if (live && smode != LM_DONE)
+        for (uint32_t k = lane; k < IL_REGION / 4; k += 64) ((uint32_t*)S->region)[k] = ((const uint32_t*)wd_region)[k];
+}
+
 void launch_seg_decode(const InflateArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(k_inflate_decode, dim3((a.n + IL_STREAMS - 1) / IL_STREAMS), dim3(IL_THREADS), 0, s, a, 0u);
 }
@@ -1282,10 +1758,15 @@ int run_inflate_rounds(const InflateArgs& a, hipStream_t s, uint32_t* host_activ
         kernel_ms[0] = kernel_ms[1] = kernel_ms[2] = 0.f;
     }
     int rc = 0;
+    // the wave decoder (k_inflate_wdec) for one-shot batches; the lane decoder keeps the
+    // incremental mode and the block-parallel split of long streams
+    static const int wd_env = [] { const char* e = getenv("SDZ_WDEC"); return e ? atoi(e) : 0; }();
+    const bool use_wd = wd_env != 0 && !a.streaming && !a.segmode && !a.split_plan;
     for (uint32_t round = 0;; ++round) {
         if (hipMemsetAsync(a.active, 0, sizeof(uint32_t), s) != hipSuccess) { rc = -1; break; }
         if (kernel_ms) (void)hipEventRecord(ev[0], s);
-        hipLaunchKernelGGL(k_inflate_decode, g1, dim3(IL_THREADS), 0, s, a, round);
+        if (use_wd) hipLaunchKernelGGL(k_inflate_wdec, dim3(a.n), dim3(64), 0, s, a, round);
+        else hipLaunchKernelGGL(k_inflate_decode, g1, dim3(IL_THREADS), 0, s, a, round);
         if (round == 0 && hook) {
             if (int hr = hook(hook_ctx)) { rc = hr; break; }
         }

@@ -16,6 +16,7 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <atomic>
 #include <chrono>
 #include <condition_variable>
 #include <cstring>
@@ -70,7 +71,8 @@ uint64_t al(uint64_t x, uint64_t a) { return (x + a - 1) / a * a; }
 // buffers.  rec_host (nullable) receives each stream's record at its caller index; the device
 // records stay in the pool (rec_cap slots) for a gather.  Holds the device's lock.
 int host_shard(const uint8_t* const* in, const size_t* in_len, uint8_t* const* out, const size_t* out_cap,
-               const std::vector<uint32_t>& ids, uint32_t rec_cap, const Codec& C, void* rec_host, ShardOut& R) {
+               const std::vector<uint32_t>& ids, uint32_t rec_cap, const Codec& C, void* rec_host, ShardOut& R,
+               void* rec_dev = nullptr) {
     DevLock lk;
     if (lk.rc) return lk.rc;
     const uint32_t m = (uint32_t)ids.size();
@@ -153,6 +155,9 @@ int host_shard(const uint8_t* const* in, const size_t* in_len, uint8_t* const* o
         HIPCHK(hipMemcpyAsync(ebuf, B + o_out, to, hipMemcpyDeviceToHost, s));
     }
     HIPCHK(hipMemcpyAsync(recs.data(), B + o_rec, recs.size(), hipMemcpyDeviceToHost, s));
+    // multi-GPU: the records (rec_cap slots, padding zeroed) into the caller's gather slot, which
+    // the caller keeps (its own pool use) until the all-gather is done
+    if (rec_dev) HIPCHK(hipMemcpyAsync(rec_dev, B + o_rec, (size_t)rec_cap * rsz, hipMemcpyDeviceToDevice, s));
     HIPCHK(hipStreamSynchronize(s));
     HIPCHK(hipEventElapsedTime(&R.kernel_ms, e0, e1));
     auto out_len_of = [&](uint32_t k) -> uint64_t {
@@ -199,7 +204,7 @@ int host_shard(const uint8_t* const* in, const size_t* in_len, uint8_t* const* o
     if (rec_host)
         for (uint32_t k = 0; k < m; ++k)
             std::memcpy((uint8_t*)rec_host + (size_t)R.order[k] * rsz, recs.data() + (size_t)k * rsz, rsz);
-    R.d_rec = B + o_rec;
+    R.d_rec = rec_dev ? rec_dev : B + o_rec;
     return SDZ_API_OK;
 }
 
@@ -255,10 +260,25 @@ struct Barrier {
 };
 
 Pool g_gather;                                   // per device: the all-gathered records
+// Multi-GPU calls are serialised: each takes a lock per device for its shard and meets the
+// others at a barrier, so two calls on overlapping device lists could each hold a device the
+// other waits for.  (Single-device calls only take their device's lock and never wait on a
+// barrier, so they interleave with a multi call safely.)
+std::mutex g_multi_mu;
+
+// a failed or half-done collective leaves the communicators unusable: abort and forget them
+void comms_abort(const std::vector<int32_t>& devs) {
+    std::lock_guard<std::mutex> lk(g_comm_mu);
+    auto it = g_comms.find(devs);
+    if (it == g_comms.end()) return;
+    for (ncclComm_t c : it->second) (void)ncclCommAbort(c);
+    g_comms.erase(it);
+}
 
 int multi_batch(const uint8_t* const* in, const size_t* in_len, uint8_t* const* out, const size_t* out_cap,
                 void* rec, uint32_t n, const Codec& C, const int32_t* devices, int32_t ndev,
                 sdz_multi_stats* stats) {
+    std::lock_guard<std::mutex> serial(g_multi_mu);
     const double t0 = now_ms();
     if (int rc = ensure_device()) return rc;
     if (ndev < 1 || ndev > SDZ_MAX_SHARDS || !devices) return fail(SDZ_API_BAD_ARG, "multi: 1..SDZ_MAX_SHARDS devices");
@@ -285,6 +305,7 @@ int multi_batch(const uint8_t* const* in, const size_t* in_len, uint8_t* const* 
     if (rccl)
         if (int rc = comms_for(devs, &comms)) return rc;
     const size_t rsz = C.rec_size();
+    const size_t slot_bytes = (size_t)max_m * rsz;
     std::vector<ShardOut> R(ndev);
     std::vector<int> rcs(ndev, SDZ_API_OK);
     std::vector<std::string> errs(ndev);
@@ -294,20 +315,27 @@ int multi_batch(const uint8_t* const* in, const size_t* in_len, uint8_t* const* 
     std::mutex tmu;
     auto shard = [&](int k) {
         int rc = hipSetDevice(devs[k]) == hipSuccess ? SDZ_API_OK : fail(SDZ_API_HIP_ERROR, "hipSetDevice");
-        // with RCCL the device stays locked from the shard's records to the all-gather (they
-        // live in its pool); loopback shards share devices, and hand their records to the host
-        // themselves (the "gather"), so they lock per call
-        std::unique_ptr<DevLock> hold;
-        if (rc == SDZ_API_OK && rccl) { hold.reset(new DevLock); rc = hold->rc; }
+        // RCCL: the shard's gather buffer (ndev slots; its own records copied into slot k, an
+        // in-place all-gather) is taken BEFORE the barrier and held by this use until the
+        // collective is done -- its lifetime does not depend on any lock.  Loopback shards
+        // share devices and hand their records to the host themselves (the "gather").
+        PoolUse guse(g_gather, nullptr);
+        uint8_t* g = nullptr;
+        if (rc == SDZ_API_OK && rccl) {
+            DevLock lk;                            // (pool get under the device's lock)
+            rc = lk.rc;
+            void* gp = nullptr;
+            if (rc == SDZ_API_OK) rc = guse.get((size_t)ndev * slot_bytes + 256, &gp);
+            g = (uint8_t*)gp;
+        }
+        uint8_t* mine = g ? g + (size_t)k * slot_bytes : nullptr;
         if (rc == SDZ_API_OK && !ids[k].empty())
-            rc = host_shard(in, in_len, out, out_cap, ids[k], max_m, C, loopback ? rec : nullptr, R[k]);
+            rc = host_shard(in, in_len, out, out_cap, ids[k], max_m, C, loopback ? rec : nullptr, R[k], mine);
         else if (rc == SDZ_API_OK && rccl) {
             // an empty shard still joins the all-gather with zeroed records
-            void* b = nullptr;
-            PoolUse use(g_host, nullptr);
-            rc = use.get((size_t)max_m * rsz + 256, &b);
-            if (rc == SDZ_API_OK && hipMemsetAsync(b, 0, (size_t)max_m * rsz, nullptr) != hipSuccess) rc = SDZ_API_HIP_ERROR;
-            R[k].d_rec = b;
+            hipError_t e = hipMemsetAsync(mine, 0, slot_bytes, nullptr);
+            if (e != hipSuccess) rc = hip_fail(e, "empty shard: hipMemsetAsync");
+            R[k].d_rec = mine;
         }
         rcs[k] = rc;
         if (rc) errs[k] = sdz_last_error();
@@ -315,25 +343,26 @@ int multi_batch(const uint8_t* const* in, const size_t* in_len, uint8_t* const* 
             std::lock_guard<std::mutex> lk(tmu);
             t_compute = std::max(t_compute, now_ms() - t0);
         }
-        bar.wait();                                 // every shard computed (or failed)
+        bar.wait();                                 // every shard computed (or failed) and holds its slot
         if (k == 0) t_gather0 = now_ms();
         bool any_fail = false;
         for (int q = 0; q < ndev; ++q) any_fail = any_fail || rcs[q] != SDZ_API_OK;
-        if (any_fail || !rccl) return;
-        // RCCL all-gather of the fixed-size records (max_m slots per shard)
-        void* g = nullptr;
-        PoolUse use(g_gather, nullptr);
-        int r2 = use.get((size_t)ndev * max_m * rsz + 256, &g);
-        if (r2 == SDZ_API_OK) {
-            ncclResult_t nr = ncclAllGather(R[k].d_rec, g, (size_t)max_m * rsz, ncclUint8, (*comms)[k], nullptr);
-            if (nr != ncclSuccess) r2 = fail(SDZ_API_HIP_ERROR, std::string("ncclAllGather: ") + ncclGetErrorString(nr));
-        }
+        if (any_fail || !rccl) return;              // no rank enqueues a collective
+        // RCCL all-gather of the fixed-size records (max_m slots per shard), in place
+        int r2 = SDZ_API_OK;
+        ncclResult_t nr = ncclAllGather(mine, g, slot_bytes, ncclUint8, (*comms)[k], nullptr);
+        if (nr != ncclSuccess) r2 = fail(SDZ_API_HIP_ERROR, std::string("ncclAllGather: ") + ncclGetErrorString(nr));
         if (r2 == SDZ_API_OK && k == 0) {
-            gathered.resize((size_t)ndev * max_m * rsz);
+            gathered.resize((size_t)ndev * slot_bytes);
             if (hipMemcpyAsync(gathered.data(), g, gathered.size(), hipMemcpyDeviceToHost, nullptr) != hipSuccess)
                 r2 = fail(SDZ_API_HIP_ERROR, "records to host");
         }
-        if (r2 == SDZ_API_OK && hipStreamSynchronize(nullptr) != hipSuccess) r2 = fail(SDZ_API_HIP_ERROR, "gather sync");
+        if (r2 != SDZ_API_OK) {
+            // the other ranks are (or will be) inside the collective: abort it instead of waiting
+            comms_abort(devs);
+        } else if (hipStreamSynchronize(nullptr) != hipSuccess) {
+            r2 = fail(SDZ_API_HIP_ERROR, "gather sync");
+        }
         if (r2) { rcs[k] = r2; errs[k] = sdz_last_error(); }
     };
     std::vector<std::thread> th;

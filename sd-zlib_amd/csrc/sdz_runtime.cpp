@@ -141,6 +141,8 @@ Pool g_inflate_scratch, g_deflate_state, g_tmp, g_stage, g_split, g_find;
 // [128, 256) small results, then the file name
 constexpr size_t kTmpMax = 0, kTmpDictId = 64, kTmpFname = 256;
 constexpr uint64_t kInflaterOutCap = 4ull << 20;   // sdz_inflater: output slot per device call
+constexpr uint64_t kDeflaterRedo = 8;             // sdz_deflater: record mode while redone bytes <= 8 x input
+constexpr uint64_t kDeflaterRedoFloor = 64ull << 20;  //   + 64 MiB, then serial
 constexpr size_t kInflaterOnePassMin = 32u << 10;  // sdz_inflater: a first append this long tries the one-pass path
 constexpr bool kMatch4Default = false;           // deflate levels 4-9: the 4-byte chain search (SDZ_MATCH4)
 
@@ -1342,23 +1344,28 @@ int sdz_inflater_append(sdz_inflater* z, const uint8_t* data, size_t len, const 
         // counted from the stream start, as an append's from its own output start).  Anything
         // else (the stream continues, an error, output past the slot) leaves no trace: the
         // incremental path below runs as before.
+        // Its output slot is only a try: if it cannot be had, the incremental path runs; it is
+        // freed on every way out (the bytes are copied to the host on success).
         const uint64_t cap = std::min<uint64_t>((uint64_t)len * 8 + (1u << 20), 1ull << 31);
-        if (cap + 64 > z->big_cap) {
-            if (z->d_big) hipFree(z->d_big);
-            z->d_big = nullptr;
-            z->big_cap = cap + 64;
-            HIPCHK(hipMalloc(&z->d_big, z->big_cap));
+        uint8_t* big = nullptr;
+        if (hipMalloc(&big, cap + 64) != hipSuccess) {
+            (void)hipGetLastError();                      // (clear the sticky error: not a failure)
+            big = nullptr;
         }
-        uint64_t meta[4] = { 0, len, 0, cap };
-        HIPCHK(hipMemcpy(z->d_meta, meta, sizeof meta, hipMemcpyHostToDevice));
-        int rc = sdz_inflate_batch_device(z->d_in, z->d_meta, z->d_meta + 1, z->d_big, z->d_meta + 2, z->d_meta + 3,
-                                          z->d_rec, 1, z->format, z->d_dict, z->dict_len, nullptr);
-        if (rc) return rc;
+        struct BigFree { uint8_t*& p; ~BigFree() { if (p) hipFree(p); } } bigfree{ big };
         sdz_inflate_record r{};
-        HIPCHK(hipMemcpy(&r, z->d_rec, sizeof r, hipMemcpyDeviceToHost));
+        r.status = SDZ_INTERNAL;
+        if (big) {
+            uint64_t meta[4] = { 0, len, 0, cap };
+            HIPCHK(hipMemcpy(z->d_meta, meta, sizeof meta, hipMemcpyHostToDevice));
+            int rc = sdz_inflate_batch_device(z->d_in, z->d_meta, z->d_meta + 1, big, z->d_meta + 2, z->d_meta + 3,
+                                              z->d_rec, 1, z->format, z->d_dict, z->dict_len, nullptr);
+            if (rc) return rc;
+            HIPCHK(hipMemcpy(&r, z->d_rec, sizeof r, hipMemcpyDeviceToHost));
+        }
         if (r.status == SDZ_OK) {
             z->out.resize(r.out_len);
-            if (r.out_len) HIPCHK(hipMemcpy(z->out.data(), z->d_big, r.out_len, hipMemcpyDeviceToHost));
+            if (r.out_len) HIPCHK(hipMemcpy(z->out.data(), big, r.out_len, hipMemcpyDeviceToHost));
             z->one_pass = true;
             z->done_rec = r;
             z->in_total += len;
@@ -1426,6 +1433,7 @@ struct sdz_deflater {
     std::vector<uint8_t> hist;                    // every byte appended (the serial replay's source)
     std::vector<size_t> calls;                    // each append's length (the replay's call boundaries)
     uint64_t total = 0, out_done = 0;
+    uint64_t redo = 0;                            // input bytes the record-mode calls have processed
     int32_t running = 0;                          // the chunk-wise running checksum
     uint8_t* d_all = nullptr;                     // the input so far, on the device
     size_t all_cap = 0;
@@ -1637,8 +1645,23 @@ int sdz_deflater_append(sdz_deflater* z, const uint8_t* data, size_t len, int32_
             *rec = r;
             return SDZ_API_OK;
         }
+        // Each record-mode call redoes the parse, the block cuts and the encoding over all the
+        // input so far, so many small appends cost O(calls x total).  Once that redone work
+        // passes kDeflaterRedo x the input (+ a floor), the Deflater goes serial (linear).
+        const uint64_t after = z->total + len;
+        uint64_t rfloor = kDeflaterRedoFloor;
+        if (const char* e = getenv("SDZ_DEFLATER_REDO_FLOOR")) rfloor = strtoull(e, nullptr, 10);   // tests
+        if (!finish && z->redo + after > kDeflaterRedo * after + rfloor) {
+            if (int rc = deflater_to_serial(z, z->calls.size())) return rc;
+            if (int rc = deflater_serial_call(z, data, len, finish, rec, true)) return rc;
+            z->status = 1;
+            *out = z->out.data();
+            *out_len = z->out.size();
+            return SDZ_API_OK;
+        }
         int how = 0;
         if (int rc = deflater_record_call(z, data, len, finish, rec, &how)) return rc;
+        if (how < 2) z->redo += after;
         if (how < 2) {
             z->hist.insert(z->hist.end(), data, data + len);
             z->calls.push_back(len);

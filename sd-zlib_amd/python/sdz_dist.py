@@ -25,36 +25,47 @@ def lpt_shard(sizes, world):
     return [sorted(s) for s in shards]
 
 
-def gather_records(rec_bytes, rec_size, shards, rank, device="cpu"):
-    """All-gather every rank's packed records (bytes, rec_size each, in its shard's
-    order) and return the records of all streams in original order (list of bytes).
-    Ranks may hold different counts: records are padded to the largest shard."""
-    import torch
-    import torch.distributed as dist
-    world = len(shards)
+def _pad(rec_bytes, rec_size, shards):
+    """a rank's records padded to the largest shard: the fixed slot every rank contributes"""
     n_max = max(len(s) for s in shards)
     buf = bytearray(n_max * rec_size)
     buf[:len(rec_bytes)] = rec_bytes
-    t = torch.frombuffer(buf, dtype=torch.uint8).to(device)
-    outs = [torch.empty_like(t) for _ in range(world)]
-    dist.all_gather(outs, t)
-    total = sum(len(s) for s in shards)
-    result = [None] * total
-    for r in range(world):
-        data = outs[r].cpu().numpy().tobytes()
-        for k, i in enumerate(shards[r]):
-            result[i] = data[k * rec_size:(k + 1) * rec_size]
-    return result
+    return bytes(buf)
 
 
-def gather_records_comm(comm, rec_bytes, rec_size, shards):
-    """gather_records over libsdz's RCCL communicator (sdz.Comm.allgather_bytes)."""
-    n_max = max(len(s) for s in shards)
-    buf = bytearray(n_max * rec_size)
-    buf[:len(rec_bytes)] = rec_bytes
-    parts = comm.allgather_bytes(bytes(buf))
+def _reassemble(parts, rec_size, shards):
+    """rank r's slot holds the records of shards[r] in order: back to stream order"""
     result = [None] * sum(len(s) for s in shards)
     for r, data in enumerate(parts):
         for k, i in enumerate(shards[r]):
             result[i] = data[k * rec_size:(k + 1) * rec_size]
     return result
+
+
+class TorchComm:
+    """sdz.Comm's allgather_bytes over torch.distributed (gloo on the CPU, or "nccl" with
+    device="cuda"), so that tests run the gather's record layout without RCCL."""
+
+    def __init__(self, device="cpu"):
+        self.device = device
+
+    def allgather_bytes(self, data):
+        import torch
+        import torch.distributed as dist
+        t = torch.frombuffer(bytearray(data), dtype=torch.uint8).to(self.device)
+        outs = [torch.empty_like(t) for _ in range(dist.get_world_size())]
+        dist.all_gather(outs, t)
+        return [o.cpu().numpy().tobytes() for o in outs]
+
+
+def gather_records_comm(comm, rec_bytes, rec_size, shards):
+    """All-gather every rank's packed records (bytes, rec_size each, in its shard's order)
+    over `comm` (sdz.Comm: RCCL inside libsdz; or TorchComm) and return the records of all
+    streams in original order (list of bytes).  Ranks may hold different counts: each
+    contributes a slot padded to the largest shard."""
+    return _reassemble(comm.allgather_bytes(_pad(rec_bytes, rec_size, shards)), rec_size, shards)
+
+
+def gather_records(rec_bytes, rec_size, shards, rank, device="cpu"):
+    """gather_records_comm over torch.distributed (the process group already initialised)"""
+    return gather_records_comm(TorchComm(device), rec_bytes, rec_size, shards)

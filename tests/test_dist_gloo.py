@@ -84,7 +84,9 @@ def test_gather_records_world2_gloo():
 
 
 def _engine_worker(rank, world, port, q):
-    """one rank: the real engine on this rank's LPT shard, records all-gathered (gloo)"""
+    """one rank: the real engine on this rank's LPT shard, the records all-gathered with the
+    layout the C ABI's gather uses (sdz_dist.gather_records_comm, here over gloo); rank 0 also
+    runs the whole batch in one call, the single-device reference for every record byte"""
     import torch.distributed as dist
     import sdz
     from test_gpu_multi import _mixed_batch
@@ -93,20 +95,30 @@ def _engine_worker(rank, world, port, q):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     plain, comp = _mixed_batch(40, seed=21)
     shards = sdz_dist.lpt_shard([len(c) for c in comp], world)
-    mine = shards[rank]
     import ctypes
-    n = len(mine)
-    ins = (ctypes.c_char_p * n)(*[comp[i] for i in mine])
-    in_len = (ctypes.c_size_t * n)(*[len(comp[i]) for i in mine])
-    bufs = [ctypes.create_string_buffer(len(plain[i]) + 64) for i in mine]
-    outs = (ctypes.c_void_p * n)(*[ctypes.addressof(b) for b in bufs])
-    caps = (ctypes.c_size_t * n)(*[len(plain[i]) + 64 for i in mine])
-    recs = (sdz.InflateRecord * n)()
-    assert sdz.lib().sdz_inflate_batch(ins, in_len, outs, caps, recs, n, sdz.FMT_AUTO, None, 0) == 0
-    ok = all(bufs[k].raw[:recs[k].out_len] == plain[i] for k, i in enumerate(mine))
-    allrec = sdz_dist.gather_records(bytes(recs), 64, shards, rank)
+
+    def run(idx):
+        n = len(idx)
+        ins = (ctypes.c_char_p * n)(*[comp[i] for i in idx])
+        in_len = (ctypes.c_size_t * n)(*[len(comp[i]) for i in idx])
+        bufs = [ctypes.create_string_buffer(len(plain[i]) + 64) for i in idx]
+        outs = (ctypes.c_void_p * n)(*[ctypes.addressof(b) for b in bufs])
+        caps = (ctypes.c_size_t * n)(*[len(plain[i]) + 64 for i in idx])
+        recs = (sdz.InflateRecord * n)()
+        assert sdz.lib().sdz_inflate_batch(ins, in_len, outs, caps, recs, n, sdz.FMT_AUTO, None, 0) == 0
+        ok = all(bufs[k].raw[:recs[k].out_len] == plain[i] for k, i in enumerate(idx))
+        return ok, bytes(recs)
+    mine = shards[rank]
+    ok, recs = run(mine)
+    rsz = ctypes.sizeof(sdz.InflateRecord)
+    allrec = sdz_dist.gather_records_comm(sdz_dist.TorchComm(), recs, rsz, shards)
+    whole = None
+    if rank == 0:
+        wok, wrec = run(list(range(len(comp))))
+        ok = ok and wok
+        whole = [wrec[i * rsz:(i + 1) * rsz] for i in range(len(comp))]
     dist.destroy_process_group()
-    q.put((rank, ok, [(r[0:4], r[8:16]) for r in allrec]))      # (status, out_len) per stream
+    q.put((rank, ok, allrec, whole))
 
 
 @pytest.mark.gpu
@@ -122,16 +134,18 @@ def test_engine_shards_world2_gloo():
         p.start()
     res = {}
     for _ in procs:
-        rank, ok, recs = q.get(timeout=240)
-        res[rank] = (ok, recs)
+        rank, ok, recs, whole = q.get(timeout=240)
+        res[rank] = (ok, recs, whole)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
     plain, _ = _mixed_batch(40, seed=21)
+    whole = res[0][2]
     for rank in (0, 1):
-        ok, recs = res[rank]
+        ok, recs, _ = res[rank]
         assert ok
         assert len(recs) == len(plain)
-        for i, (st, ln) in enumerate(recs):
-            assert struct.unpack("<i", st)[0] == 0, i                   # SDZ_OK on every stream
-            assert struct.unpack("<Q", ln)[0] == len(plain[i]), i      # out_len, in stream order
+        for i, r in enumerate(recs):
+            assert struct.unpack("<i", r[0:4])[0] == 0, i                   # SDZ_OK on every stream
+            assert struct.unpack("<Q", r[8:16])[0] == len(plain[i]), i     # out_len, in stream order
+            assert r == whole[i], i                                          # every byte of the record

@@ -159,3 +159,21 @@ def test_record_path_deflater_large_appends(paradise):
     for level in (1, 6, 9):
         exp = O.deflater_parts(parts, level=level, format="deflate", mtime=1234567)
         assert run_deflater(parts, level, "deflate") == exp, level
+
+
+@pytest.mark.timeout(300)
+def test_many_small_appends_stay_linear(monkeypatch, paradise):
+    """A multi-MB stream appended in 8 KiB chunks: the record-mode Deflater redoes all the
+    input so far per call, so past a bound on that redone work (kDeflaterRedo x input + a floor,
+    here a 1 MiB floor) it goes serial.  Per-call bytes match the reference, the switch
+    included, and the whole run stays within a linear budget."""
+    import time
+    monkeypatch.setenv("SDZ_DEFLATER_REDO_FLOOR", str(1 << 20))
+    data = (paradise * 5)[:2 << 20]
+    parts = [data[o:o + 8192] for o in range(0, len(data), 8192)]
+    exp = O.deflater_parts(parts, level=6, format="deflate")
+    t0 = time.perf_counter()
+    got = run_deflater(parts, 6, "deflate")
+    dt = time.perf_counter() - t0
+    assert got == exp
+    assert dt < 120, dt
