@@ -1022,12 +1022,15 @@ __device__ __forceinline__ bool seg_is_cand(const SegStop& G, uint64_t bit) {
 // past its LDS budget and the last bits of the input)
 __shared__ __attribute__((aligned(16))) uint8_t wd_region[IL_REGION + 12];
 __shared__ __attribute__((aligned(16))) uint32_t wd_stage[IL_TSTRIDE / 4];
+__shared__ Tree wd_LL, wd_DD;                     // the wave decoder's trees (LDS: not cold_run's registers)
 template <int MODE, bool WD = false>
 __device__ __noinline__ void cold_run(DSave* S, const uint8_t* inp, uint64_t ilen, uint64_t cap,
                                       uint32_t* tb, uint32_t tcap, uint8_t* lens, int32_t format, int32_t has_dict,
                                       int32_t dict_adler, uint32_t init, SegStop G, int force_slow = 0) {
     Lane L;
-    Tree LL, DD;
+    Tree LLr, DDr;
+    Tree& LL = WD ? wd_LL : LLr;
+    Tree& DD = WD ? wd_DD : DDr;
     uint8_t* region;
     if constexpr (WD) { region = wd_region; L.ts = wd_stage; }
     else { region = lane_region(); L.ts = lane_stage(); }
@@ -1338,7 +1341,6 @@ __shared__ __attribute__((aligned(16))) uint16_t wd_dt[WD_DT];
 __shared__ __attribute__((aligned(16))) uint32_t wd_bm[64 * WD_BMW];
 __shared__ __attribute__((aligned(16))) uint32_t wd_ring[64 * 18];
 __shared__ __attribute__((aligned(16))) uint32_t wd_tst[64 * WD_TST];
-__shared__ __attribute__((aligned(16))) uint32_t wd_tree[2 * 33];   // lim[16], pk[17] of LL then DD
 
 enum : uint32_t { WR_RUN = 0, WR_SYNC, WR_EOB, WR_ERR, WR_CAP, WR_END, WR_NOSYNC, WR_CHUNK, WR_OFF };
 
@@ -1426,9 +1428,9 @@ __device__ __forceinline__ bool wd_table(const HTree& T, const uint8_t* syms, bo
 __device__ __noinline__ bool wd_build() {
     HTree LL, DD;
 #pragma unroll
-    for (int k = 0; k < 16; ++k) { LL.lim[k] = wd_tree[k]; DD.lim[k] = wd_tree[33 + k]; }
+    for (int k = 0; k < 16; ++k) { LL.lim[k] = wd_LL.lim[k]; DD.lim[k] = wd_DD.lim[k]; }
 #pragma unroll
-    for (int k = 0; k < 17; ++k) { LL.pk[k] = wd_tree[16 + k]; DD.pk[k] = wd_tree[33 + 16 + k]; }
+    for (int k = 0; k < 17; ++k) { LL.pk[k] = wd_LL.pk[k]; DD.pk[k] = wd_DD.pk[k]; }
     const bool a = wd_table<WD_LLR>(LL, wd_region, true, wd_ll, WD_LLT);
     const bool b = wd_table<WD_DR>(DD, wd_region, false, wd_dt, WD_DT);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
@@ -1449,6 +1451,246 @@ __device__ __forceinline__ uint32_t wd_look_d(uint32_t pw) {
     return e;
 }
 
+// ------------------------------------------------------------------ fused resolve
+//
+// The wave decoder writes the bytes itself (FUSED): after an iteration's join, the chained lanes
+// know their tokens and, by a scan of their byte counts, where their bytes go.  Each lane then
+// copies its own tokens' bytes in order, through a 128-byte ring of its own in LDS (the decode's
+// boundary maps are dead by then), to the output in HBM in aligned 16-byte blocks.  A source
+// closer than WR_NEAR bytes inside the lane's own bytes comes from its ring; anything else from
+// HBM -- the lane's own flushed bytes, earlier iterations', or other lanes' bytes, which a lane
+// reads only once their owner has published (after a store wait, at a round's end) that they are
+// in HBM.  Lane 0's sources are its own or older, so every round moves it on, and lane j is
+// unblocked once the lanes before it are done.  No tokens cross HBM, no window is staged, and
+// the stream needs no second kernel; adler32's sums are folded in at the flushes.
+#define WR_RB 128u                // per-lane output ring (LDS bytes; address-keyed)
+#define WR_NEAR 120u              // sources this close (in the lane's own bytes) read the ring
+#ifndef WR_STEPS
+#define WR_STEPS 32               // 4-byte steps per lane and round
+#endif
+#define WR_ROUND_LIMIT (1u << 22)
+
+__shared__ int32_t wr_ost[65];    // chunk starts (relative to the iteration's output start); [J+1..] = end
+__shared__ int32_t wr_prog[64];   // published: bytes below this are in HBM and visible
+
+__device__ __forceinline__ uint32_t wr_get4(const uint32_t* r32, uint32_t ga) {     // 4 ring bytes at address ga
+    const uint32_t w0 = r32[(ga >> 2) & (WR_RB / 4 - 1)], w1 = r32[((ga >> 2) + 1) & (WR_RB / 4 - 1)];
+    return __builtin_amdgcn_alignbyte(w1, w0, ga & 3u);
+}
+__device__ __forceinline__ uint32_t wr_gread4(const uint8_t* p) {                  // 4 HBM bytes at p (any alignment)
+    const uint32_t* a = (const uint32_t*)((uintptr_t)p & ~(uintptr_t)3);
+    const uint32_t k = (uint32_t)(uintptr_t)p & 3u;
+    const uint32_t w0 = a[0];
+    const uint32_t w1 = k ? a[1] : 0u;
+    return __builtin_amdgcn_alignbyte(w1, w0, k);
+}
+// 4 bytes of the period-`dist` (1..3) pattern P starting at phase ph (as k_resolve.hip's rep4)
+__device__ __forceinline__ uint32_t wr_rep4(uint32_t P, uint32_t dist, uint32_t ph) {
+    const uint32_t lo = dist == 3 ? 0x00020100u : dist == 2 ? 0x01000100u : 0u;
+    const uint32_t hi = dist == 3 ? 0x01000201u : lo;
+    return __builtin_amdgcn_perm(P, P, __builtin_amdgcn_alignbyte(hi, lo, ph));
+}
+__device__ __forceinline__ uint32_t wr_owner(int32_t y, uint32_t J) {             // lane whose chunk holds y
+    uint32_t lo = 0, hi = J;                              // ost[lo] <= y < ost[hi + 1]
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi + 1) >> 1;
+        if (wr_ost[mid] <= y) lo = mid; else hi = mid - 1;
+    }
+    return lo;
+}
+// bytes [a, e) (relative, e <= the asking lane's chunk start) in HBM and visible?
+__device__ __forceinline__ bool wr_ready(int32_t a, int32_t e, uint32_t J) {
+    int32_t x = e;
+    const int32_t lo = a > 0 ? a : 0;
+    for (int guard = 0; x > lo && guard < 65; ++guard) {
+        const uint32_t i = wr_owner(x - 1, J);
+        if (wr_prog[i] < x) return false;
+        x = wr_ost[i];
+    }
+    return true;
+}
+struct WrAcc {
+    uint32_t S;                       // sum of bytes
+    uint64_t T;                       // sum of position * byte (positions mod 65521)
+};
+__shared__ uint32_t wr_accS[64];      // per lane, across the stream's iterations (LDS: the noinline
+__shared__ uint64_t wr_accT[64];      // phases pass nothing through scratch)
+__device__ __forceinline__ void wr_adler_byte(WrAcc& A, uint64_t pos, uint32_t b) {
+    A.S += b;
+    A.T += (uint64_t)(uint32_t)(pos % 65521u) * b;
+}
+__device__ __forceinline__ void wr_adler_word(WrAcc& A, uint32_t pm, uint32_t v) {   // pm: position of byte 0 mod 65521
+    const uint32_t s4 = __builtin_amdgcn_udot4(v, 0x01010101u, 0u, false);
+    A.S += s4;
+    A.T += (uint64_t)pm * s4 + __builtin_amdgcn_udot4(v, 0x03020100u, 0u, false);
+}
+// byte x (relative) of the output: zeros before the stream's output start; the lane's own bytes
+// from o on (ring = their most recent WR_RB, when `ring`) else from HBM
+__device__ __forceinline__ uint32_t wr_byte(const uint8_t* rg, const uint8_t* ob, uint64_t IB, uint32_t gb, int32_t x,
+                                            int32_t o, bool ring) {
+    if ((int64_t)IB + x < 0) return 0u;
+    if (ring && x >= o) return rg[(gb + (uint32_t)x) & (WR_RB - 1)];
+    return *(volatile const uint8_t*)(ob + x);
+}
+// one ring byte range [fl, to) to HBM with byte stores (chunk heads and tails, forced flushes)
+__device__ __forceinline__ void wr_flush_bytes(const uint8_t* rg, uint8_t* ob, uint64_t IB, uint32_t gb, int32_t fl,
+                                               int32_t to, WrAcc& A) {
+    for (int32_t x = fl; x < to; ++x) {
+        const uint32_t b = rg[(gb + (uint32_t)x) & (WR_RB - 1)];
+        ob[x] = (uint8_t)b;
+        wr_adler_byte(A, IB + (uint64_t)x, b);
+    }
+}
+// flush whole aligned 16-byte blocks below `to` (at most `maxb`); the head of a chunk by bytes
+__device__ __forceinline__ void wr_flush(const uint8_t* rg, uint8_t* ob, uint64_t IB, uint32_t gb, int32_t& fl, int32_t to,
+                                         int maxb, WrAcc& A) {
+    const uint32_t mis = (gb + (uint32_t)fl) & 15u;
+    if (mis) {
+        const int32_t h = fl + (int32_t)(16u - mis);
+        if (to < h) return;
+        wr_flush_bytes(rg, ob, IB, gb, fl, h, A);
+        fl = h;
+    }
+    for (int k = 0; k < maxb && to - fl >= 16; ++k) {
+        const uint4 v = *(const uint4*)(rg + ((gb + (uint32_t)fl) & (WR_RB - 1)));
+        *(uint4*)(ob + fl) = v;
+        const uint32_t pm = (uint32_t)((IB + (uint64_t)fl) % 65521u);
+        wr_adler_word(A, pm, v.x);
+        wr_adler_word(A, pm + 4, v.y);
+        wr_adler_word(A, pm + 8, v.z);
+        wr_adler_word(A, pm + 12, v.w);
+        fl += 16;
+    }
+}
+
+// The resolve phase of one iteration (all lanes; lanes > J idle).  tk: the lane's tokens
+// [0, nt); o: its chunk start (relative to the output position IB = S->pos at the iteration's
+// start); ob = out + IB.  Returns false if the round watchdog tripped.
+__device__ __noinline__ bool wr_resolve(const uint32_t* tk, uint32_t nt, int32_t o, int32_t oend, bool inc, uint32_t J,
+                                        uint8_t* ob, uint64_t IB) {
+    const uint32_t lane = threadIdx.x & 63u;
+    WrAcc A = { wr_accS[lane], wr_accT[lane] };
+    uint8_t* rg = (uint8_t*)(wd_bm + lane * (WR_RB / 4));
+    const uint32_t* r32 = (const uint32_t*)rg;
+    const uint32_t gb = (uint32_t)(uintptr_t)ob;          // ring index of relative position x: (gb + x) & 127
+    if (lane <= J) { wr_ost[lane] = o; wr_prog[lane] = o; }
+    if (lane == J) for (uint32_t k = J + 1; k <= 64; ++k) wr_ost[k] = oend;
+    __threadfence_block();
+    __builtin_amdgcn_wave_barrier();
+    int32_t q = o, fl = o;                                // write position, flushed position
+    uint32_t idx = 0;                                     // next token
+    uint32_t t = inc && nt ? tk[0] : 0u, tn = inc && nt > 1 ? tk[1] : 0u;
+    uint32_t rem = 0, lw = 0, d = 0, P = 0, ph = 0;       // the token in progress
+    bool lit = false;
+    bool done = !inc;
+    bool ok = true;
+    for (uint32_t round = 0;; ++round) {
+        bool blocked = false;
+        for (int step = 0; step < WR_STEPS; ++step) {
+            if (done || blocked) continue;
+            if (rem == 0) {
+                if (idx == nt) {                          // the chunk is complete
+                    wr_flush(rg, ob, IB, gb, fl, q, 64, A);
+                    wr_flush_bytes(rg, ob, IB, gb, fl, q, A);
+                    fl = q;
+                    done = true;
+                    continue;
+                }
+                if ((int32_t)t < 0) {                     // a match: are its other-lane sources in HBM?
+                    const uint32_t L = ((t >> 16) & 255u) + 3u, dd = (t & 0x7fffu) + 1u;
+                    const int32_t a = q - (int32_t)dd;
+                    if (a < o) {
+                        const int32_t b = a + (int32_t)(L < dd ? L : dd);
+                        if (!wr_ready(a, b < o ? b : o, J)) { blocked = true; continue; }
+                        if (dd <= WR_NEAR) {              // the rest is in our unflushed bytes: to HBM first
+                            wr_flush(rg, ob, IB, gb, fl, q, 64, A);
+                            wr_flush_bytes(rg, ob, IB, gb, fl, q, A);
+                            fl = q;
+                        }
+                    }
+                    rem = L; d = dd; lit = false;
+                    if (d < 4) {                          // the period's bytes (before q)
+                        P = 0;
+                        for (uint32_t k = 0; k < d; ++k)
+                            P |= wr_byte(rg, ob, IB, gb, q - (int32_t)d + (int32_t)k, o, true) << (8 * k);
+                        ph = 0;
+                    }
+                } else {
+                    rem = ((t >> 24) & 3u) + 1u; lw = t & 0xffffffu; lit = true;
+                }
+                ++idx;
+                t = tn;
+                tn = idx + 1 < nt ? tk[idx + 1] : 0u;
+            }
+            // one step: up to 4 bytes of the token in progress
+            const uint32_t n = rem < 4u ? rem : 4u;
+            uint32_t v;
+            if (lit) { v = lw; lw >>= 8 * n; }
+            else if (d < 4) { v = wr_rep4(P, d, ph); ph = d == 3 ? (ph == 2 ? 0u : ph + 1u) : 0u; }
+            else {
+                // ring: near sources in our own bytes; HBM: far ones (our own flushed long
+                // since), other lanes' (published), earlier iterations'; mixed reads bytewise
+                const int32_t sp = q - (int32_t)d;
+                const bool near = d <= WR_NEAR;
+                const bool pos_ok = (int64_t)IB + sp >= 0;
+                if (near && sp >= o) v = wr_get4(r32, gb + (uint32_t)sp);
+                else if (pos_ok && (!near || sp + 4 <= o)) v = wr_gread4(ob + sp);
+                else {
+                    v = 0;
+                    for (uint32_t k = 0; k < 4; ++k) v |= wr_byte(rg, ob, IB, gb, sp + (int32_t)k, o, near) << (8 * k);
+                }
+            }
+#pragma unroll
+            for (uint32_t k = 0; k < 4; ++k)
+                if (k < n) rg[(gb + (uint32_t)q + k) & (WR_RB - 1)] = (uint8_t)(v >> (8 * k));
+            q += (int32_t)n;
+            rem -= n;
+            if (q - fl >= 32) wr_flush(rg, ob, IB, gb, fl, q, 1, A);
+        }
+        // round end: our stores complete, then publish how far our bytes are in HBM
+        __builtin_amdgcn_s_waitcnt(0);
+        __threadfence_block();
+        if (lane <= J) wr_prog[lane] = fl;
+        __threadfence_block();
+        __builtin_amdgcn_wave_barrier();
+        if (!__ballot(!done)) break;
+        if (round > WR_ROUND_LIMIT) { ok = false; break; }
+    }
+    wr_accS[lane] = A.S % 65521u;
+    wr_accT[lane] = A.T % 65521u;
+    return ok;
+}
+
+// lane 0: the bytes of tokens [t0, t1) of the ring (cold_run's: stored blocks, slow steps) at
+// output position IB, one at a time (sources are bytes already in HBM, zeros before the start)
+__device__ __noinline__ void wr_serial(const uint32_t* tb, uint32_t t0, uint32_t t1, uint8_t* out, uint64_t IB) {
+    WrAcc A = { wr_accS[0], wr_accT[0] };
+    uint64_t q = IB;
+    for (uint32_t i = t0; i < t1; ++i) {
+        const uint32_t t = tb[i];
+        if ((int32_t)t >= 0) {
+            const uint32_t n = ((t >> 24) & 3u) + 1u;
+            for (uint32_t k = 0; k < n; ++k) {
+                const uint32_t b = (t >> (8 * k)) & 255u;
+                out[q] = (uint8_t)b;
+                wr_adler_byte(A, q, b);
+                ++q;
+            }
+        } else {
+            const uint32_t L = ((t >> 16) & 255u) + 3u, d = (t & 0x7fffu) + 1u;
+            for (uint32_t k = 0; k < L; ++k) {
+                const int64_t s = (int64_t)q - d;
+                const uint32_t b = s < 0 ? 0u : (uint32_t)*(volatile const uint8_t*)(out + s);
+                out[q] = (uint8_t)b;
+                wr_adler_byte(A, q, b);
+                ++q;
+            }
+        }
+    }
+    wr_accS[0] = A.S % 65521u;
+    wr_accT[0] = A.T % 65521u;
+}
+
 struct WdRes {
     uint32_t st, stop, ntk, synco;
 };
@@ -1458,16 +1700,19 @@ struct WdRes {
 // Returns 0: go on; 1: the block ended, or the last input bits need the cold path; 2: the
 // slow step must take this block from S->bitpos (an invalid code, or the output room);
 // 3: no token room left this round.  cmax: chunk bits (halved on CAP stops).
+template <bool FUSED>
 __device__ __noinline__ int wd_iteration(DSave* S, const uint8_t* inp, uint64_t ilen, uint64_t cap,
                                          uint32_t* tb, uint32_t tcap, uint64_t B0, uint32_t ntok0, uint64_t pos0,
-                                         uint32_t& cmax) {
+                                         uint32_t& cmax, uint8_t* out) {
     const uint32_t lane = threadIdx.x & 63u;
     const uint64_t tbits = ilen * 8;
     const uint64_t lim64 = tbits - 64 - B0;
     const uint32_t lim = (uint32_t)(lim64 > (1ull << 30) ? (1ull << 30) : lim64);
-    uint32_t C = lim / 64u;
+    // chunks of C bits covering [0, lim) when 64 of them can (lanes past the block's end decode
+    // nothing of use; CMAX x 64 bits is about one block of 16 Ki symbols of text)
+    uint32_t C = (lim + 63u) / 64u;
     C = C < WD_CMIN ? WD_CMIN : C > cmax ? cmax : C;
-    uint32_t n = lim / C;
+    uint32_t n = (lim + C - 1u) / C;
     n = n < 1u ? 1u : n > 64u ? 64u : n;
     const uint32_t P0 = (ntok0 + 7u) & ~7u;               // provisional area: 8-token aligned
     const uint32_t space = tcap > P0 + 8u ? tcap - P0 - 8u : 0u;
@@ -1499,7 +1744,7 @@ __device__ __noinline__ int wd_iteration(DSave* S, const uint8_t* inp, uint64_t 
     }
     uint32_t st = on ? WR_RUN : WR_OFF;
     uint32_t prog = on ? 0u : 0x80000000u;                // offset recorded so far | stopped
-    uint32_t ntk = 0, nfl = 0, litw = 0, nlit = 0, stop = 0, synco = 0;
+    uint32_t ntk = 0, nfl = 0, litw = 0, nlit = 0, stop = 0, synco = 0, outb = 0;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
     __builtin_amdgcn_wave_barrier();
 
@@ -1552,6 +1797,7 @@ __device__ __noinline__ int wd_iteration(DSave* S, const uint8_t* inp, uint64_t 
             uint32_t len = e & 15u, sym = (e >> 4) & 511u;
             if (sym < 256u) {
                 H.bo += len;
+                ++outb;
                 litw |= sym << (8u * nlit);
                 ++nlit;
                 if (nlit == 3u || (lane && off < WD_W)) {  // one token per symbol in the recorded bits
@@ -1575,6 +1821,7 @@ __device__ __noinline__ int wd_iteration(DSave* S, const uint8_t* inp, uint64_t 
             H.bo += len + ex;
             if (nlit) { push(((nlit - 1u) << 24) | litw); nlit = 0; litw = 0; }
             push(0x80000000u | ((mlen - 3u) << 16) | (dist - 1u));
+            outb += mlen;
         }
         if (!__ballot(st == WR_RUN)) break;
     }
@@ -1606,6 +1853,30 @@ __device__ __noinline__ int wd_iteration(DSave* S, const uint8_t* inp, uint64_t 
     const uint32_t excl = incl - c;
     const uint32_t stJ = wd_at(st, J), stopJ = wd_at(stop, J);
     __threadfence_block();                                // provisional tokens visible to every lane
+    if constexpr (FUSED) {
+        // the chained lanes' byte counts (a successor's tokens from its sync index on), their
+        // output chunks by a scan, then every lane writes its own chunk's bytes
+        uint32_t before = 0;
+        if (inc) for (uint32_t q = 0; q < s; ++q) {
+            const uint32_t t = prov[q];
+            before += (int32_t)t < 0 ? ((t >> 16) & 255u) + 3u : ((t >> 24) & 3u) + 1u;
+        }
+        const uint32_t mine = inc ? outb - before : 0u;
+        const uint32_t binc = wd_scan(mine);
+        const uint32_t btot = wd_at(binc, 63);
+        if (stJ == WR_CAP && J == 0 && cmax > WD_CMIN) cmax >>= 1;
+        if (pos0 + btot > cap) return 2;                  // the slow step reports the overflow exactly
+        const bool ok = wr_resolve((const uint32_t*)(prov + s), c, (int32_t)(binc - mine), (int32_t)btot, inc, J,
+                                   out + pos0, pos0);
+        if (lane == 0) {
+            S->pos = pos0 + btot;
+            S->bitpos = B0 + stopJ;
+            if (!ok) { S->mode = LM_DONE; S->status = SDZ_INTERNAL; S->zmsg = 5; }
+            else if (stJ == WR_EOB) S->mode = S->last ? LM_TRAILER : LM_TYPE;
+        }
+        __threadfence_block();
+        return !ok ? 1 : stJ == WR_EOB || stJ == WR_END ? 1 : stJ == WR_ERR ? 2 : 0;
+    }
     // compaction, lane by lane in order: destinations never pass their sources
     uint32_t bytes = 0;
     for (uint32_t j = 0; j <= J; ++j) {
@@ -1652,14 +1923,93 @@ __device__ __forceinline__ void wd_cold(const InflateArgs& A, DSave* S, const ui
         H.tb = tb; H.ts = wd_stage; H.ntok = S->ntok; H.litw = S->litw; H.nlit = S->nlit;
         tok_finish(H);
         S->ntok = H.ntok; S->litw = 0; S->nlit = 0;
-        const uint32_t* tl = (const uint32_t*)&S->LL;
-        const uint32_t* td = (const uint32_t*)&S->DD;
-        for (int k = 0; k < 33; ++k) { wd_tree[k] = tl[k]; wd_tree[33 + k] = td[k]; }
     }
     __threadfence_block();
     __builtin_amdgcn_wave_barrier();
 }
 
+// adler32.ts:34-105 over n output bytes from p, from state (s1, s2), NMAX quirk (sum2 += BASE
+// after each whole 5552-byte block instead of a reduction) -- k_resolve.hip's adler_quirk_ring
+__device__ int32_t wd_adler_quirk(const uint8_t* p, uint32_t len, uint32_t s1, uint32_t s2in) {
+    uint64_t a = s1, s2 = s2in;
+    while (len >= 5552) {
+        len -= 5552;
+        for (int i = 0; i < 5552; ++i) { a += *p++; s2 += a; }
+        a %= 65521u;
+        s2 += 65521u;
+    }
+    if (len) {
+        while (len--) { a += *p++; s2 += a; }
+        a %= 65521u;
+        s2 %= 65521u;
+    }
+    return (int32_t)((uint32_t)a | ((uint32_t)s2 << 16));
+}
+
+// the one-shot record and verdicts (sd-inflate.ts:134-179), as k_inflate_resolve's epilogue for a
+// call without incremental state; gzip's crc32 comes from k_inflate_finalize (lane 0)
+__device__ __noinline__ void wd_record(const InflateArgs& A, const DSave* S, uint32_t sid, uint64_t pos,
+                                       uint32_t S_all, uint32_t T_all, const uint8_t* out, bool failed) {
+    const bool gz = S->container == SDZ_CONTAINER_GZIP;
+    const uint64_t ilen = A.in_len[sid];
+    sdz_inflate_record Rc;
+    Rc.status = failed ? SDZ_INTERNAL : S->status;
+    Rc.zmsg = S->zmsg;
+    Rc.out_len = pos;
+    uint64_t used = (S->bitpos + 7) >> 3;
+    Rc.in_used = used > ilen ? ilen : used;
+    Rc.stored_checksum = S->stored_ck;
+    const bool have = pos > 0;
+    int32_t running = 0;
+    if (!gz) {
+        uint32_t a1 = 1, a2 = 0;
+        if (pos) {
+            const uint32_t nm = (uint32_t)(pos % 65521u);
+            const uint32_t b1 = (uint32_t)(((uint64_t)a1 + S_all) % 65521u);
+            const uint32_t b2 = (uint32_t)(((uint64_t)a2 + (uint64_t)nm * a1 + (uint64_t)nm * S_all + 65521ull * 65521ull - T_all) % 65521u);
+            a1 = b1;
+            a2 = b2;
+        }
+        const uint32_t rr = (uint32_t)(pos & 16383u);
+        if (!failed && (rr == 5552u || rr == 11104u)) {
+            // the final 16 KiB chunk of 5552 / 11104 bytes leaves sum2 unreduced: replay it from
+            // the state at its start (recovered from the plain state and its bytes)
+            const uint8_t* tail = out + (pos - rr);
+            uint64_t qa = 0, qb = 0;
+            for (uint32_t k = 0; k < rr; ++k) { const uint32_t v = tail[k]; qa += v; qb += (uint64_t)(rr - k) * v; }
+            uint32_t s1s = 1, s2s = 0;
+            if (pos != rr) {
+                s1s = (uint32_t)((a1 + 65521u - (uint32_t)(qa % 65521u)) % 65521u);
+                s2s = (uint32_t)(((uint64_t)a2 + 65521ull * 65521ull - (uint64_t)rr * s1s - qb % 65521u) % 65521u);
+            }
+            running = wd_adler_quirk(tail, rr, s1s, s2s);
+        } else {
+            running = (int32_t)(a1 | (a2 << 16));
+        }
+    }
+    Rc.running_checksum = have ? running : 0;
+    Rc.stored_size = S->stored_size;
+    Rc.mtime = S->mtime;
+    Rc.name_off = S->name_off;
+    Rc.name_len = S->name_len;
+    Rc.container = (uint8_t)S->container;
+    const bool complete = !failed && S->mode == LM_DONE && (S->status == SDZ_OK || S->status == SDZ_TRAILING);
+    Rc.complete = complete ? 1 : 0;
+    const uint8_t cv = S->stored_ck == 0 ? SDZ_UNCHECKED : ((have && S->stored_ck == running) ? SDZ_MATCH : SDZ_MISMATCH);
+    const uint8_t sv = S->stored_size == 0 ? SDZ_UNCHECKED
+                     : ((int64_t)S->stored_size == (int64_t)pos ? SDZ_MATCH : SDZ_MISMATCH);
+    Rc.checksum_verdict = cv;
+    Rc.size_verdict = sv;
+    Rc.success = (complete && cv != SDZ_MISMATCH && sv != SDZ_MISMATCH) ? 1 : 0;
+    Rc.out_full = 0;
+    if (!complete && Rc.status == SDZ_OK) Rc.status = SDZ_TRUNCATED;
+    for (int k = 0; k < 10; ++k) Rc.reserved[k] = 0;
+    A.rec[sid] = Rc;
+}
+
+// FUSED: the wave writes the stream's bytes and record itself (one launch, no token rounds,
+// no k_inflate_resolve); else tokens for k_inflate_resolve, in rounds
+template <bool FUSED>
 __global__ __launch_bounds__(64) void k_inflate_wdec(InflateArgs A, uint32_t round) {
     const uint32_t sid = blockIdx.x, lane = threadIdx.x;
     if (sid >= A.n) return;
@@ -1671,6 +2021,8 @@ __global__ __launch_bounds__(64) void k_inflate_wdec(InflateArgs A, uint32_t rou
     const uint64_t ilen = A.in_len[sid];
     const uint64_t cap = A.out_cap[sid];
     const uint64_t tbits = ilen * 8;
+    uint8_t* out = A.out + A.out_off[sid];
+    if (FUSED) { wr_accS[lane] = 0; wr_accT[lane] = 0; }
     bool live = false;
     if (round == 0 && (A.out_off[sid] & 7)) {
         if (lane == 0) {
@@ -1685,7 +2037,7 @@ __global__ __launch_bounds__(64) void k_inflate_wdec(InflateArgs A, uint32_t rou
     } else if (wd_uni(lane == 0 ? (uint32_t)S->mode : 0u) != LM_DONE) {
         live = true;
         for (uint32_t k = lane; k < IL_REGION / 4; k += 64) ((uint32_t*)wd_region)[k] = ((const uint32_t*)S->region)[k];
-        if (lane < 33) { wd_tree[lane] = ((const uint32_t*)&S->LL)[lane]; wd_tree[33 + lane] = ((const uint32_t*)&S->DD)[lane]; }
+        if (lane == 0) { wd_LL = S->LL; wd_DD = S->DD; }
         if (lane == 0) { S->ntok = 0; S->full = 0; }
         __threadfence_block();
         __builtin_amdgcn_wave_barrier();
@@ -1693,7 +2045,24 @@ __global__ __launch_bounds__(64) void k_inflate_wdec(InflateArgs A, uint32_t rou
     bool stale = true;
     int fslow = 0;
     uint32_t cmax = WD_CMAX;
+    uint64_t cold_pos = 0;                                // FUSED: output position of the cold tokens
+    bool failed = false;
     while (live) {
+        if (FUSED) {
+            // cold_run's tokens (headers produce none; stored blocks and slow steps do): their bytes
+            // now, by lane 0, so that the ring is empty for the next iteration
+            const uint32_t nt = wd_uni(lane == 0 ? S->ntok : 0u);
+            if (nt) {
+                if (lane == 0) {
+                    wr_serial(tb, 0, nt, out, cold_pos);
+                    S->ntok = 0;
+                    S->full = 0;
+                }
+                __builtin_amdgcn_s_waitcnt(0);
+                __threadfence_block();
+                __builtin_amdgcn_wave_barrier();
+            }
+        }
         // the stream's state as lane 0 left it (lane 0 reads its own stores; broadcast)
         const uint32_t mode = wd_uni(lane == 0 ? (uint32_t)S->mode : 0u);
         const uint32_t full = wd_uni(lane == 0 ? (uint32_t)S->full : 0u);
@@ -1708,17 +2077,30 @@ __global__ __launch_bounds__(64) void k_inflate_wdec(InflateArgs A, uint32_t rou
                 if (!wd_build()) { fslow = 1; continue; }
                 stale = false;
             }
-            const int r = wd_iteration(S, inp, ilen, cap, tb, tcap, B0, ntok, pos, cmax);
+            const int r = wd_iteration<FUSED>(S, inp, ilen, cap, tb, tcap, B0, ntok, pos, cmax, out);
             if (r == 2) fslow = 1;
             else if (r == 3) fslow = 1;
             continue;
         }
+        cold_pos = pos;
         wd_cold(A, S, inp, ilen, cap, tb, tcap, lens, 0u, (fslow || mode == LM_CODES) ? 1 : 0);
         fslow = 0;
         stale = true;
     }
     const uint32_t smode = wd_uni(lane == 0 ? (uint32_t)S->mode : 0u);
     const uint32_t sstall = wd_uni(lane == 0 ? (uint32_t)S->stall : 0u);
+    if constexpr (FUSED) {
+        // the record: adler sums of every lane (each reduced mod 65521)
+        uint64_t s1 = wr_accS[lane], s2 = wr_accT[lane];
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) { s1 += __shfl_xor(s1, o); s2 += __shfl_xor(s2, o); }
+        if (lane == 0) {
+            A.ntok[sid] = 0;
+            A.flags[sid] = 1;
+            wd_record(A, S, sid, live ? S->pos : 0, (uint32_t)(s1 % 65521u), (uint32_t)(s2 % 65521u), out, failed);
+        }
+        return;
+    }
     if (lane == 0) {
         const bool more = live && smode != LM_DONE && !sstall;
         if (more) atomicAdd(A.active, 1u);
@@ -1743,6 +2125,11 @@ void launch_inflate_finalize(const InflateArgs& a, hipStream_t s);
 
 // the state arrays are indexed as DSave* / RSave* arrays: the strides are the struct sizes
 uint64_t inflate_dsave_bytes() { return sizeof(DSave); }
+int inflate_wdec_mode() {
+    const char* e = getenv("SDZ_WDEC");
+    return e ? atoi(e) : 0;
+}
+bool inflate_wdec_enabled() { return inflate_wdec_mode() != 0; }
 uint64_t inflate_rsave_bytes() { return sizeof(RSave); }
 
 // host driver: rounds of (decode, resolve) until no stream needs another round.
@@ -1759,13 +2146,20 @@ int run_inflate_rounds(const InflateArgs& a, hipStream_t s, uint32_t* host_activ
     }
     int rc = 0;
     // the wave decoder (k_inflate_wdec) for one-shot batches; the lane decoder keeps the
-    // incremental mode and the block-parallel split of long streams
-    static const int wd_env = [] { const char* e = getenv("SDZ_WDEC"); return e ? atoi(e) : 0; }();
-    const bool use_wd = wd_env != 0 && !a.streaming && !a.segmode && !a.split_plan;
+    // incremental mode (and the block-parallel split of long streams, off with the wave decoder)
+    const bool use_wd = inflate_wdec_enabled() && !a.streaming && !a.segmode && !a.split_plan;
+    // fused (SDZ_WDEC=2): one-shot calls without a preset dictionary
+    const bool fused = use_wd && inflate_wdec_mode() == 2 && a.dict == nullptr;
     for (uint32_t round = 0;; ++round) {
         if (hipMemsetAsync(a.active, 0, sizeof(uint32_t), s) != hipSuccess) { rc = -1; break; }
         if (kernel_ms) (void)hipEventRecord(ev[0], s);
-        if (use_wd) hipLaunchKernelGGL(k_inflate_wdec, dim3(a.n), dim3(64), 0, s, a, round);
+        if (fused) {                                   // one launch: bytes and records (then finalize)
+            hipLaunchKernelGGL(k_inflate_wdec<true>, dim3(a.n), dim3(64), 0, s, a, 0u);
+            if (kernel_ms) (void)hipEventRecord(ev[1], s);
+            if (kernel_ms) (void)hipEventRecord(ev[2], s);
+            break;
+        }
+        if (use_wd) hipLaunchKernelGGL(k_inflate_wdec<false>, dim3(a.n), dim3(64), 0, s, a, round);
         else hipLaunchKernelGGL(k_inflate_decode, g1, dim3(IL_THREADS), 0, s, a, round);
         if (round == 0 && hook) {
             if (int hr = hook(hook_ctx)) { rc = hr; break; }
@@ -1804,7 +2198,7 @@ int run_inflate_rounds(const InflateArgs& a, hipStream_t s, uint32_t* host_activ
         if (kernel_ms) {
             (void)hipEventRecord(ev[3], s);
             (void)hipEventSynchronize(ev[3]);
-            if (a.one_round && !a.split_plan) {
+            if ((a.one_round || fused) && !a.split_plan) {
                 float t0 = 0.f, t1 = 0.f;
                 (void)hipEventElapsedTime(&t0, ev[0], ev[1]);
                 (void)hipEventElapsedTime(&t1, ev[1], ev[2]);

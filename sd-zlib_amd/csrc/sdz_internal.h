@@ -63,6 +63,7 @@ struct InflateArgs {
 };
 
 uint64_t inflate_dsave_bytes();  // per stream decode state
+bool inflate_wdec_enabled();     // one-shot batches decode with k_inflate_wdec (SDZ_WDEC)
 uint64_t inflate_rsave_bytes();  // per stream resolve state
 // hook (optional): called once on the host right after the first round's decode is queued
 // (the split pre-pass's second half); a nonzero return ends the rounds with that code

@@ -406,6 +406,7 @@ struct SplitHost {
 int inflate_split_start(const InflateArgs& a, hipStream_t s, PoolUse& find_use, SplitHost& H) {
     const uint32_t n = a.n;
     if (const char* e = getenv("SDZ_SPLIT")) if (atoi(e) == 0) return SDZ_API_OK;
+    if (inflate_wdec_enabled()) return SDZ_API_OK;      // the wave decoder is parallel inside a block
     uint64_t split_min = 16 << 10;
     if (const char* e = getenv("SDZ_SPLIT_MIN")) split_min = strtoull(e, nullptr, 10);
     std::vector<uint64_t> len(n);
