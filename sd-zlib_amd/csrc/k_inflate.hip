@@ -1336,11 +1336,12 @@ __global__ __launch_bounds__(IL_THREADS, 1) void k_inflate_decode(InflateArgs A,
 #define WD_TST 16                 // token stage per lane (LDS)
 #define WD_INV 511u               // table symbol: invalid code
 
-__shared__ __attribute__((aligned(16))) uint16_t wd_ll[WD_LLT];
-__shared__ __attribute__((aligned(16))) uint16_t wd_dt[WD_DT];
+__shared__ __attribute__((aligned(16))) uint32_t wd_tab[WD_LLT + WD_DT];   // literal/length, then distance
+#define wd_ll wd_tab
+#define wd_dt (wd_tab + WD_LLT)
 __shared__ __attribute__((aligned(16))) uint32_t wd_bm[64 * WD_BMW];
 __shared__ __attribute__((aligned(16))) uint32_t wd_ring[64 * 18];
-__shared__ __attribute__((aligned(16))) uint32_t wd_tst[64 * WD_TST];
+__shared__ __attribute__((aligned(16))) uint32_t wd_tst[64 * (WD_TST + 4)];   // + a dummy slot per lane
 
 enum : uint32_t { WR_RUN = 0, WR_SYNC, WR_EOB, WR_ERR, WR_CAP, WR_END, WR_NOSYNC, WR_CHUNK, WR_OFF };
 
@@ -1377,11 +1378,25 @@ __device__ __forceinline__ uint32_t wd_code(const HTree& T, const uint8_t* syms,
     if (idx >= 30) return WD_INV;
     return syms[IL_DSYM + idx];
 }
-// Two-level table: root entry = len | sym << 4 (direct) or 0x8000 | k | off << 4 (codes longer
-// than R bits under this prefix: a subtable of 2^k entries at off, k = the longest code's
-// length - R).  Returns false if the subtables do not fit (the block then runs the slow step).
+// A decoded code as the symbol loop uses it: code length (bits 0-3), extra bits (4-7), kind
+// (8-9: 0 literal, 1 length, 2 distance, 3 end of block (value 0) or invalid code (value 1)) and
+// value (16-31: the literal, or the base length / distance the extra bits are added to)
+__device__ __forceinline__ uint32_t wd_entry(uint32_t sym, uint32_t len, bool lit) {
+    uint32_t x, kind, val;
+    if (lit) {
+        if (sym < 256u) { kind = 0u; val = sym; x = 0u; }
+        else if (sym == 256u) { kind = 3u; val = 0u; x = 0u; }
+        else if (sym <= 285u) { kind = 1u; val = len_base(sym - 256u, x); }
+        else { kind = 3u; val = 1u; x = 0u; }
+    } else if (sym < 30u) { kind = 2u; val = dist_base(sym, x); }
+    else { kind = 3u; val = 1u; x = 0u; }
+    return len | (x << 4) | (kind << 8) | (val << 16);
+}
+// Two-level table of wd_entry words: a root entry is the code's (direct), or 0x8000 | k | off << 16
+// (codes longer than R bits under this prefix: a subtable of 2^k entries at off, k = the longest
+// code's length - R).  Returns false if the subtables do not fit (the block then runs the slow step).
 template <int R>
-__device__ __forceinline__ bool wd_table(const HTree& T, const uint8_t* syms, bool lit, uint16_t* tab, uint32_t cap) {
+__device__ __forceinline__ bool wd_table(const HTree& T, const uint8_t* syms, bool lit, uint32_t* tab, uint32_t cap) {
     const uint32_t lane = threadIdx.x & 63u;
     constexpr uint32_t NR = 1u << R, PER = NR / 64;
     uint32_t need = 0;
@@ -1402,7 +1417,7 @@ __device__ __forceinline__ bool wd_table(const HTree& T, const uint8_t* syms, bo
             sym = WD_INV;
         }
         ks[m] = k;
-        if (k == 0) tab[i] = (uint16_t)(len | (sym << 4));
+        if (k == 0) tab[i] = wd_entry(sym, len, lit);
     }
     const uint32_t incl = wd_scan(need);
     const uint32_t total = wd_at(incl, 63);
@@ -1413,12 +1428,12 @@ __device__ __forceinline__ bool wd_table(const HTree& T, const uint8_t* syms, bo
         const uint32_t k = ks[m];
         if (k == 0) continue;
         const uint32_t i = lane + 64u * m;
-        tab[i] = (uint16_t)(0x8000u | k | (off << 4));
+        tab[i] = 0x8000u | k | (off << 16);
         for (uint32_t j = 0; j < (1u << k); ++j) {
             uint32_t len;
             const uint32_t x = i | (j << R);
             const uint32_t sym = wd_code(T, syms, lit, __builtin_bitreverse32(x) >> 17, len);
-            tab[off + j] = (uint16_t)(len | (sym << 4));
+            tab[off + j] = wd_entry(sym, len, lit);
         }
         off += 1u << k;
     }
@@ -1439,257 +1454,6 @@ __device__ __noinline__ bool wd_build() {
     return a && b;
 }
 
-// one symbol's table entry: root, then the subtable when the root entry links
-__device__ __forceinline__ uint32_t wd_look_ll(uint32_t pw) {
-    uint32_t e = wd_ll[pw & ((1u << WD_LLR) - 1u)];
-    if (e & 0x8000u) e = wd_ll[((e >> 4) & 2047u) + ((pw >> WD_LLR) & ((1u << (e & 15u)) - 1u))];
-    return e;
-}
-__device__ __forceinline__ uint32_t wd_look_d(uint32_t pw) {
-    uint32_t e = wd_dt[pw & ((1u << WD_DR) - 1u)];
-    if (e & 0x8000u) e = wd_dt[((e >> 4) & 2047u) + ((pw >> WD_DR) & ((1u << (e & 15u)) - 1u))];
-    return e;
-}
-
-// ------------------------------------------------------------------ fused resolve
-//
-// The wave decoder writes the bytes itself (FUSED): after an iteration's join, the chained lanes
-// know their tokens and, by a scan of their byte counts, where their bytes go.  Each lane then
-// copies its own tokens' bytes in order, through a 128-byte ring of its own in LDS (the decode's
-// boundary maps are dead by then), to the output in HBM in aligned 16-byte blocks.  A source
-// closer than WR_NEAR bytes inside the lane's own bytes comes from its ring; anything else from
-// HBM -- the lane's own flushed bytes, earlier iterations', or other lanes' bytes, which a lane
-// reads only once their owner has published (after a store wait, at a round's end) that they are
-// in HBM.  Lane 0's sources are its own or older, so every round moves it on, and lane j is
-// unblocked once the lanes before it are done.  No tokens cross HBM, no window is staged, and
-// the stream needs no second kernel; adler32's sums are folded in at the flushes.
-#define WR_RB 128u                // per-lane output ring (LDS bytes; address-keyed)
-#define WR_NEAR 120u              // sources this close (in the lane's own bytes) read the ring
-#ifndef WR_STEPS
-#define WR_STEPS 32               // 4-byte steps per lane and round
-#endif
-#define WR_ROUND_LIMIT (1u << 22)
-
-__shared__ int32_t wr_ost[65];    // chunk starts (relative to the iteration's output start); [J+1..] = end
-__shared__ int32_t wr_prog[64];   // published: bytes below this are in HBM and visible
-
-__device__ __forceinline__ uint32_t wr_get4(const uint32_t* r32, uint32_t ga) {     // 4 ring bytes at address ga
-    const uint32_t w0 = r32[(ga >> 2) & (WR_RB / 4 - 1)], w1 = r32[((ga >> 2) + 1) & (WR_RB / 4 - 1)];
-    return __builtin_amdgcn_alignbyte(w1, w0, ga & 3u);
-}
-__device__ __forceinline__ uint32_t wr_gread4(const uint8_t* p) {                  // 4 HBM bytes at p (any alignment)
-    const uint32_t* a = (const uint32_t*)((uintptr_t)p & ~(uintptr_t)3);
-    const uint32_t k = (uint32_t)(uintptr_t)p & 3u;
-    const uint32_t w0 = a[0];
-    const uint32_t w1 = k ? a[1] : 0u;
-    return __builtin_amdgcn_alignbyte(w1, w0, k);
-}
-// 4 bytes of the period-`dist` (1..3) pattern P starting at phase ph (as k_resolve.hip's rep4)
-__device__ __forceinline__ uint32_t wr_rep4(uint32_t P, uint32_t dist, uint32_t ph) {
-    const uint32_t lo = dist == 3 ? 0x00020100u : dist == 2 ? 0x01000100u : 0u;
-    const uint32_t hi = dist == 3 ? 0x01000201u : lo;
-    return __builtin_amdgcn_perm(P, P, __builtin_amdgcn_alignbyte(hi, lo, ph));
-}
-__device__ __forceinline__ uint32_t wr_owner(int32_t y, uint32_t J) {             // lane whose chunk holds y
-    uint32_t lo = 0, hi = J;                              // ost[lo] <= y < ost[hi + 1]
-    while (lo < hi) {
-        const uint32_t mid = (lo + hi + 1) >> 1;
-        if (wr_ost[mid] <= y) lo = mid; else hi = mid - 1;
-    }
-    return lo;
-}
-// bytes [a, e) (relative, e <= the asking lane's chunk start) in HBM and visible?
-__device__ __forceinline__ bool wr_ready(int32_t a, int32_t e, uint32_t J) {
-    int32_t x = e;
-    const int32_t lo = a > 0 ? a : 0;
-    for (int guard = 0; x > lo && guard < 65; ++guard) {
-        const uint32_t i = wr_owner(x - 1, J);
-        if (wr_prog[i] < x) return false;
-        x = wr_ost[i];
-    }
-    return true;
-}
-struct WrAcc {
-    uint32_t S;                       // sum of bytes
-    uint64_t T;                       // sum of position * byte (positions mod 65521)
-};
-__shared__ uint32_t wr_accS[64];      // per lane, across the stream's iterations (LDS: the noinline
-__shared__ uint64_t wr_accT[64];      // phases pass nothing through scratch)
-__device__ __forceinline__ void wr_adler_byte(WrAcc& A, uint64_t pos, uint32_t b) {
-    A.S += b;
-    A.T += (uint64_t)(uint32_t)(pos % 65521u) * b;
-}
-__device__ __forceinline__ void wr_adler_word(WrAcc& A, uint32_t pm, uint32_t v) {   // pm: position of byte 0 mod 65521
-    const uint32_t s4 = __builtin_amdgcn_udot4(v, 0x01010101u, 0u, false);
-    A.S += s4;
-    A.T += (uint64_t)pm * s4 + __builtin_amdgcn_udot4(v, 0x03020100u, 0u, false);
-}
-// byte x (relative) of the output: zeros before the stream's output start; the lane's own bytes
-// from o on (ring = their most recent WR_RB, when `ring`) else from HBM
-__device__ __forceinline__ uint32_t wr_byte(const uint8_t* rg, const uint8_t* ob, uint64_t IB, uint32_t gb, int32_t x,
-                                            int32_t o, bool ring) {
-    if ((int64_t)IB + x < 0) return 0u;
-    if (ring && x >= o) return rg[(gb + (uint32_t)x) & (WR_RB - 1)];
-    return *(volatile const uint8_t*)(ob + x);
-}
-// one ring byte range [fl, to) to HBM with byte stores (chunk heads and tails, forced flushes)
-__device__ __forceinline__ void wr_flush_bytes(const uint8_t* rg, uint8_t* ob, uint64_t IB, uint32_t gb, int32_t fl,
-                                               int32_t to, WrAcc& A) {
-    for (int32_t x = fl; x < to; ++x) {
-        const uint32_t b = rg[(gb + (uint32_t)x) & (WR_RB - 1)];
-        ob[x] = (uint8_t)b;
-        wr_adler_byte(A, IB + (uint64_t)x, b);
-    }
-}
-// flush whole aligned 16-byte blocks below `to` (at most `maxb`); the head of a chunk by bytes
-__device__ __forceinline__ void wr_flush(const uint8_t* rg, uint8_t* ob, uint64_t IB, uint32_t gb, int32_t& fl, int32_t to,
-                                         int maxb, WrAcc& A) {
-    const uint32_t mis = (gb + (uint32_t)fl) & 15u;
-    if (mis) {
-        const int32_t h = fl + (int32_t)(16u - mis);
-        if (to < h) return;
-        wr_flush_bytes(rg, ob, IB, gb, fl, h, A);
-        fl = h;
-    }
-    for (int k = 0; k < maxb && to - fl >= 16; ++k) {
-        const uint4 v = *(const uint4*)(rg + ((gb + (uint32_t)fl) & (WR_RB - 1)));
-        *(uint4*)(ob + fl) = v;
-        const uint32_t pm = (uint32_t)((IB + (uint64_t)fl) % 65521u);
-        wr_adler_word(A, pm, v.x);
-        wr_adler_word(A, pm + 4, v.y);
-        wr_adler_word(A, pm + 8, v.z);
-        wr_adler_word(A, pm + 12, v.w);
-        fl += 16;
-    }
-}
-
-// The resolve phase of one iteration (all lanes; lanes > J idle).  tk: the lane's tokens
-// [0, nt); o: its chunk start (relative to the output position IB = S->pos at the iteration's
-// start); ob = out + IB.  Returns false if the round watchdog tripped.
-__device__ __noinline__ bool wr_resolve(const uint32_t* tk, uint32_t nt, int32_t o, int32_t oend, bool inc, uint32_t J,
-                                        uint8_t* ob, uint64_t IB) {
-    const uint32_t lane = threadIdx.x & 63u;
-    WrAcc A = { wr_accS[lane], wr_accT[lane] };
-    uint8_t* rg = (uint8_t*)(wd_bm + lane * (WR_RB / 4));
-    const uint32_t* r32 = (const uint32_t*)rg;
-    const uint32_t gb = (uint32_t)(uintptr_t)ob;          // ring index of relative position x: (gb + x) & 127
-    if (lane <= J) { wr_ost[lane] = o; wr_prog[lane] = o; }
-    if (lane == J) for (uint32_t k = J + 1; k <= 64; ++k) wr_ost[k] = oend;
-    __threadfence_block();
-    __builtin_amdgcn_wave_barrier();
-    int32_t q = o, fl = o;                                // write position, flushed position
-    uint32_t idx = 0;                                     // next token
-    uint32_t t = inc && nt ? tk[0] : 0u, tn = inc && nt > 1 ? tk[1] : 0u;
-    uint32_t rem = 0, lw = 0, d = 0, P = 0, ph = 0;       // the token in progress
-    bool lit = false;
-    bool done = !inc;
-    bool ok = true;
-    for (uint32_t round = 0;; ++round) {
-        bool blocked = false;
-        for (int step = 0; step < WR_STEPS; ++step) {
-            if (done || blocked) continue;
-            if (rem == 0) {
-                if (idx == nt) {                          // the chunk is complete
-                    wr_flush(rg, ob, IB, gb, fl, q, 64, A);
-                    wr_flush_bytes(rg, ob, IB, gb, fl, q, A);
-                    fl = q;
-                    done = true;
-                    continue;
-                }
-                if ((int32_t)t < 0) {                     // a match: are its other-lane sources in HBM?
-                    const uint32_t L = ((t >> 16) & 255u) + 3u, dd = (t & 0x7fffu) + 1u;
-                    const int32_t a = q - (int32_t)dd;
-                    if (a < o) {
-                        const int32_t b = a + (int32_t)(L < dd ? L : dd);
-                        if (!wr_ready(a, b < o ? b : o, J)) { blocked = true; continue; }
-                        if (dd <= WR_NEAR) {              // the rest is in our unflushed bytes: to HBM first
-                            wr_flush(rg, ob, IB, gb, fl, q, 64, A);
-                            wr_flush_bytes(rg, ob, IB, gb, fl, q, A);
-                            fl = q;
-                        }
-                    }
-                    rem = L; d = dd; lit = false;
-                    if (d < 4) {                          // the period's bytes (before q)
-                        P = 0;
-                        for (uint32_t k = 0; k < d; ++k)
-                            P |= wr_byte(rg, ob, IB, gb, q - (int32_t)d + (int32_t)k, o, true) << (8 * k);
-                        ph = 0;
-                    }
-                } else {
-                    rem = ((t >> 24) & 3u) + 1u; lw = t & 0xffffffu; lit = true;
-                }
-                ++idx;
-                t = tn;
-                tn = idx + 1 < nt ? tk[idx + 1] : 0u;
-            }
-            // one step: up to 4 bytes of the token in progress
-            const uint32_t n = rem < 4u ? rem : 4u;
-            uint32_t v;
-            if (lit) { v = lw; lw >>= 8 * n; }
-            else if (d < 4) { v = wr_rep4(P, d, ph); ph = d == 3 ? (ph == 2 ? 0u : ph + 1u) : 0u; }
-            else {
-                // ring: near sources in our own bytes; HBM: far ones (our own flushed long
-                // since), other lanes' (published), earlier iterations'; mixed reads bytewise
-                const int32_t sp = q - (int32_t)d;
-                const bool near = d <= WR_NEAR;
-                const bool pos_ok = (int64_t)IB + sp >= 0;
-                if (near && sp >= o) v = wr_get4(r32, gb + (uint32_t)sp);
-                else if (pos_ok && (!near || sp + 4 <= o)) v = wr_gread4(ob + sp);
-                else {
-                    v = 0;
-                    for (uint32_t k = 0; k < 4; ++k) v |= wr_byte(rg, ob, IB, gb, sp + (int32_t)k, o, near) << (8 * k);
-                }
-            }
-#pragma unroll
-            for (uint32_t k = 0; k < 4; ++k)
-                if (k < n) rg[(gb + (uint32_t)q + k) & (WR_RB - 1)] = (uint8_t)(v >> (8 * k));
-            q += (int32_t)n;
-            rem -= n;
-            if (q - fl >= 32) wr_flush(rg, ob, IB, gb, fl, q, 1, A);
-        }
-        // round end: our stores complete, then publish how far our bytes are in HBM
-        __builtin_amdgcn_s_waitcnt(0);
-        __threadfence_block();
-        if (lane <= J) wr_prog[lane] = fl;
-        __threadfence_block();
-        __builtin_amdgcn_wave_barrier();
-        if (!__ballot(!done)) break;
-        if (round > WR_ROUND_LIMIT) { ok = false; break; }
-    }
-    wr_accS[lane] = A.S % 65521u;
-    wr_accT[lane] = A.T % 65521u;
-    return ok;
-}
-
-// lane 0: the bytes of tokens [t0, t1) of the ring (cold_run's: stored blocks, slow steps) at
-// output position IB, one at a time (sources are bytes already in HBM, zeros before the start)
-__device__ __noinline__ void wr_serial(const uint32_t* tb, uint32_t t0, uint32_t t1, uint8_t* out, uint64_t IB) {
-    WrAcc A = { wr_accS[0], wr_accT[0] };
-    uint64_t q = IB;
-    for (uint32_t i = t0; i < t1; ++i) {
-        const uint32_t t = tb[i];
-        if ((int32_t)t >= 0) {
-            const uint32_t n = ((t >> 24) & 3u) + 1u;
-            for (uint32_t k = 0; k < n; ++k) {
-                const uint32_t b = (t >> (8 * k)) & 255u;
-                out[q] = (uint8_t)b;
-                wr_adler_byte(A, q, b);
-                ++q;
-            }
-        } else {
-            const uint32_t L = ((t >> 16) & 255u) + 3u, d = (t & 0x7fffu) + 1u;
-            for (uint32_t k = 0; k < L; ++k) {
-                const int64_t s = (int64_t)q - d;
-                const uint32_t b = s < 0 ? 0u : (uint32_t)*(volatile const uint8_t*)(out + s);
-                out[q] = (uint8_t)b;
-                wr_adler_byte(A, q, b);
-                ++q;
-            }
-        }
-    }
-    wr_accS[0] = A.S % 65521u;
-    wr_accT[0] = A.T % 65521u;
-}
 
 struct WdRes {
     uint32_t st, stop, ntk, synco;
@@ -1700,11 +1464,17 @@ struct WdRes {
 // Returns 0: go on; 1: the block ended, or the last input bits need the cold path; 2: the
 // slow step must take this block from S->bitpos (an invalid code, or the output room);
 // 3: no token room left this round.  cmax: chunk bits (halved on CAP stops).
-template <bool FUSED>
 __device__ __noinline__ int wd_iteration(DSave* S, const uint8_t* inp, uint64_t ilen, uint64_t cap,
                                          uint32_t* tb, uint32_t tcap, uint64_t B0, uint32_t ntok0, uint64_t pos0,
-                                         uint32_t& cmax, uint8_t* out) {
+                                         uint32_t& cmax, unsigned long long* dbg) {
     const uint32_t lane = threadIdx.x & 63u;
+#ifdef SDZ_TIMING
+    // development: dbg[18] loop cycles, [19] join cycles, [20] iterations, [21] CAP stops of J,
+    // [22] symbol steps of all lanes, [23] tokens committed, [24] chained lanes, [25] lanes used,
+    // [26] ERR / [27] NOSYNC / [28] EOB stops of J, [30] chunk bits (sum)
+    const unsigned long long tw0 = dbg ? clock64() : 0;
+    uint32_t nsym = 0;
+#endif
     const uint64_t tbits = ilen * 8;
     const uint64_t lim64 = tbits - 64 - B0;
     const uint32_t lim = (uint32_t)(lim64 > (1ull << 30) ? (1ull << 30) : lim64);
@@ -1727,7 +1497,7 @@ __device__ __noinline__ int wd_iteration(DSave* S, const uint8_t* inp, uint64_t 
     const uint32_t bn = lastl ? n * C : (lane + 1u) * C;
     uint32_t* bm = wd_bm + lane * WD_BMW;
     uint32_t* bmn = wd_bm + ((lane + 1u) & 63u) * WD_BMW;
-    uint32_t* tst = wd_tst + lane * WD_TST;
+    uint32_t* tst = wd_tst + lane * (WD_TST + 4);
     GLB uint32_t* prov = (GLB uint32_t*)(tb + P0 + lane * tcapl);
 #pragma unroll
     for (int k = 0; k < WD_BMW; k += 4) *(uint4*)(bm + k) = make_uint4(0, 0, 0, 0);
@@ -1744,16 +1514,104 @@ __device__ __noinline__ int wd_iteration(DSave* S, const uint8_t* inp, uint64_t 
     }
     uint32_t st = on ? WR_RUN : WR_OFF;
     uint32_t prog = on ? 0u : 0x80000000u;                // offset recorded so far | stopped
-    uint32_t ntk = 0, nfl = 0, litw = 0, nlit = 0, stop = 0, synco = 0, outb = 0;
+    uint32_t ntk = 0, nfl = 0, litw = 0, nlit = 0, stop = 0, synco = 0;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
     __builtin_amdgcn_wave_barrier();
 
     auto push = [&](uint32_t t) { tst[ntk & (WD_TST - 1)] = t; ntk++; };
-    auto halt = [&](uint32_t why, uint32_t at) { st = why; stop = at; prog |= 0x80000000u; };
+#ifndef SDZ_TIMING
+    uint32_t nsym = 0;
+#endif
+    // one code from table `tbase` (root bits rb) at peek pw: the root word, or its subtable's
+    // (a wave-uniform branch, taken when some lane's code is longer than the root)
+    auto look = [&](uint32_t tbase, uint32_t rb, uint32_t pw, uint32_t act) -> uint32_t {
+        uint32_t e = wd_tab[tbase + (pw & ((1u << rb) - 1u))];
+        if (__ballot(act & (e >> 15) & 1u))
+            if (e & 0x8000u) e = wd_tab[tbase + (e >> 16) + ((pw >> rb) & ((1u << (e & 15u)) - 1u))];
+        return e;
+    };
+
+    // One symbol per step, the same instructions on every lane: the literal/length code, then a
+    // distance code decoded for every lane (some lane of 64 almost always has a match) and used by
+    // the lanes that have one; kind, extra bits and base value come with the table words.  Flags
+    // are 0/1 integers combined with & and | (short-circuit && and || compile to exec-mask
+    // branches).  Stops at a symbol start (chunk end, sync, input end, token room) are checked
+    // only in 4-step groups where some lane may reach one (CAREFUL); end of block and invalid
+    // codes in every step.
+    auto step = [&](auto carefulc, uint32_t spv, uint32_t sstop) {
+        constexpr bool CAREFUL = decltype(carefulc)::value;
+        const uint32_t run = st == WR_RUN;
+        const uint32_t pw = br_refill_peek(H);            // (a refill never moves the position)
+        const uint32_t p = Kc - (uint32_t)H.avail + H.bo;
+        const uint32_t off = p - bj;
+        uint32_t dec = run;
+        if constexpr (CAREFUL) {
+            const uint32_t past = run & (p >= bn);
+            const uint32_t o = p - bn;
+            const uint32_t inw = past & (uint32_t)!lastl & (o < WD_W);
+            const uint32_t chk = inw & (o <= spv);
+            const uint32_t bw = bmn[chk ? (o >> 5) : 0u];
+            const uint32_t syn = chk & ((bw >> (o & 31u)) & 1u);
+            const uint32_t waitS = inw & (o > spv) & (sstop ^ 1u);
+            const uint32_t nosync = past & (uint32_t)!lastl & (syn ^ 1u) & ((o >= WD_W) | ((o > spv) & sstop));
+            const uint32_t why = !run ? (uint32_t)WR_RUN : p >= lim ? (uint32_t)WR_END : ntk + 3u > tcapl ? (uint32_t)WR_CAP
+                               : !past ? (uint32_t)WR_RUN : lastl ? (uint32_t)WR_CHUNK : syn ? (uint32_t)WR_SYNC
+                               : nosync ? (uint32_t)WR_NOSYNC : (uint32_t)WR_RUN;
+            const uint32_t halt = run & (why != WR_RUN);
+            dec = run & (why == WR_RUN) & (waitS ^ 1u);
+            st = halt ? why : st;
+            stop = halt ? p : stop;
+            synco = halt ? o : synco;
+            prog |= halt << 31;
+        }
+        // record our symbol starts in the first WD_W bits (an OR of 0 elsewhere)
+        const uint32_t head = (lane != 0u) & (off < WD_W);
+        const uint32_t rec = dec & head;
+        __hip_atomic_fetch_or(bm + (rec ? off >> 5 : 0u), rec << (off & 31u), __ATOMIC_RELAXED,
+                              __HIP_MEMORY_SCOPE_WORKGROUP);
+        prog = run ? (off | (prog & 0x80000000u)) : prog;
+        nsym += dec;
+        // the literal/length code
+        const uint32_t e = look(0u, WD_LLR, pw, dec);
+        const uint32_t len = e & 15u, xb = (e >> 4) & 15u, kind = (e >> 8) & 3u;
+        const uint32_t val = (e >> 16) + __builtin_amdgcn_ubfe(pw, len, xb);
+        const uint32_t isLit = kind == 0u, isLen = kind == 1u, isSp = kind == 3u;
+        H.bo += (dec & (isSp ^ 1u)) ? len + xb : 0u;
+        // the distance code (every lane; used by the lanes at a length code)
+        const uint32_t pw2 = br_refill_peek(H);
+        const uint32_t d = look(WD_LLT, WD_DR, pw2, dec & isLen);
+        const uint32_t dlen = d & 15u, dxb = (d >> 4) & 15u;
+        const uint32_t dist = (d >> 16) + __builtin_amdgcn_ubfe(pw2, dlen, dxb);
+        const uint32_t derr = isLen & (((d >> 8) & 3u) != 2u);
+        const uint32_t isM = isLen & (derr ^ 1u);
+        H.bo += (dec & isM) ? dlen + dxb : 0u;
+        // tokens: literals packed up to 3 (one per token in the recorded bits), a match after its
+        // pending literals
+        const uint32_t litw2 = litw | (val << (8u * nlit));
+        const uint32_t nlit2 = nlit + 1u;
+        const uint32_t emitL = isLit & ((nlit2 >= 3u) | head);
+        const uint32_t emitP = isM & (nlit != 0u);          // a match's pending literals first
+        const uint32_t tokL = ((isLit ? nlit : nlit - 1u) << 24) | (isLit ? litw2 : litw);
+        const uint32_t tokM = 0x80000000u | ((val - 3u) << 16) | (dist - 1u);
+        const uint32_t e1 = dec & (emitL | emitP), e2 = dec & isM;
+        tst[e1 ? (ntk & (WD_TST - 1u)) : (uint32_t)WD_TST] = tokL;
+        tst[e2 ? ((ntk + e1) & (WD_TST - 1u)) : (uint32_t)WD_TST] = tokM;
+        ntk += e1 + e2;
+        const uint32_t keepL = isLit & (emitL ^ 1u);      // literal still pending
+        const uint32_t litwN = keepL ? litw2 : (isLit | isM) ? 0u : litw;
+        const uint32_t nlitN = keepL ? nlit2 : (isLit | isM) ? 0u : nlit;
+        litw = dec ? litwN : litw;
+        nlit = dec ? nlitN : nlit;
+        // end of block (value 0) or an invalid code (value 1, or a bad distance code)
+        const uint32_t sp_ = dec & (isSp | derr);
+        const uint32_t eob = isSp & (val == 0u);
+        st = sp_ ? (eob ? (uint32_t)WR_EOB : (uint32_t)WR_ERR) : st;
+        stop = sp_ ? (eob ? p + len : p) : stop;
+        prog |= sp_ << 31;
+    };
 
     for (;;) {
-        const bool run = st == WR_RUN;
-        if (run) ring_step_wd(H);
+        if (st == WR_RUN) ring_step_wd(H);
         // staged tokens -> the lane's provisional slot, 8 at a time (at most 8 per 4 steps)
         {
             const bool f = ntk - nfl >= 8u;
@@ -1767,64 +1625,27 @@ __device__ __noinline__ int wd_iteration(DSave* S, const uint8_t* inp, uint64_t 
                 }
             }
         }
-        // the successor's progress, for lanes past their chunk (stale by up to 4 steps: safe)
-        uint32_t sp = 0x80000000u;
-        {
-            const bool ov = run && !lastl && (Kc - (uint32_t)H.avail + H.bo) >= bn;
-            if (__ballot(ov)) sp = __shfl_down(prog, 1);
-        }
+        // a lane may reach a stop in the next 4 steps (28 bits at most per step)?
+        const uint32_t pn = Kc - (uint32_t)H.avail + H.bo;
+        const bool nearE = st == WR_RUN && (pn + 4u * 48u >= bn || pn + 4u * 48u >= lim || ntk + 12u > tcapl);
+        if (__ballot(nearE)) {
+            // the successor's progress (stale by up to 4 steps: safe), for lanes past their chunk
+            // or reaching it in these steps; "offset 0, running" when not fetched
+            uint32_t sp = 0u;
+            if (__ballot(st == WR_RUN && !lastl && pn + 4u * 48u >= bn)) sp = __shfl_down(prog, 1);
+            const uint32_t spv = sp & 0x7fffffffu;
+            const uint32_t sstop = sp >> 31;
 #pragma unroll
-        for (int rep = 0; rep < 4; ++rep) {
-            if (st != WR_RUN) continue;
-            const uint32_t p = Kc - (uint32_t)H.avail + H.bo;
-            const uint32_t off = p - bj;
-            if (lane && off < WD_W) __hip_atomic_fetch_or(bm + (off >> 5), 1u << (off & 31u), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            prog = off;
-            if (p >= lim) { halt(WR_END, p); continue; }
-            if (ntk + 3u > tcapl) { halt(WR_CAP, p); continue; }
-            if (p >= bn) {
-                if (lastl) { halt(WR_CHUNK, p); continue; }
-                const uint32_t o = p - bn;
-                if (o >= WD_W) { halt(WR_NOSYNC, p); continue; }
-                if (o > (sp & 0x7fffffffu)) {
-                    if (sp >> 31) halt(WR_NOSYNC, p);
-                    continue;                             // the successor has not recorded o yet
-                }
-                if ((bmn[o >> 5] >> (o & 31u)) & 1u) { halt(WR_SYNC, p); synco = o; continue; }
-            }
-            uint32_t pw = br_refill_peek(H);
-            uint32_t e = wd_look_ll(pw);
-            uint32_t len = e & 15u, sym = (e >> 4) & 511u;
-            if (sym < 256u) {
-                H.bo += len;
-                ++outb;
-                litw |= sym << (8u * nlit);
-                ++nlit;
-                if (nlit == 3u || (lane && off < WD_W)) {  // one token per symbol in the recorded bits
-                    push(((nlit - 1u) << 24) | litw);
-                    nlit = 0; litw = 0;
-                }
-                continue;
-            }
-            if (sym == 256u) { H.bo += len; halt(WR_EOB, p + len); continue; }
-            if (sym > 285u) { halt(WR_ERR, p); continue; }
-            uint32_t ex;
-            uint32_t mlen = len_base(sym - 256u, ex);
-            mlen += (pw >> len) & ((1u << ex) - 1u);
-            H.bo += len + ex;
-            pw = br_refill_peek(H);
-            e = wd_look_d(pw);
-            len = e & 15u; sym = (e >> 4) & 511u;
-            if (sym >= 30u) { halt(WR_ERR, p); continue; }
-            uint32_t dist = dist_base(sym, ex);
-            dist += (pw >> len) & ((1u << ex) - 1u);
-            H.bo += len + ex;
-            if (nlit) { push(((nlit - 1u) << 24) | litw); nlit = 0; litw = 0; }
-            push(0x80000000u | ((mlen - 3u) << 16) | (dist - 1u));
-            outb += mlen;
+            for (int rep = 0; rep < 4; ++rep) step(std::true_type{}, spv, sstop);
+        } else {
+#pragma unroll
+            for (int rep = 0; rep < 4; ++rep) step(std::false_type{}, 0u, 0u);
         }
         if (!__ballot(st == WR_RUN)) break;
     }
+#ifdef SDZ_TIMING
+    const unsigned long long tw1 = dbg ? clock64() : 0;
+#endif
     // pending literals, then the rest of the stage
     if (nlit) { push(((nlit - 1u) << 24) | litw); nlit = 0; }
     for (uint32_t q = nfl; q < ntk; ++q) prov[q] = tst[q & (WD_TST - 1)];
@@ -1852,31 +1673,23 @@ __device__ __noinline__ int wd_iteration(DSave* S, const uint8_t* inp, uint64_t 
     const uint32_t total = wd_at(incl, 63);
     const uint32_t excl = incl - c;
     const uint32_t stJ = wd_at(st, J), stopJ = wd_at(stop, J);
-    __threadfence_block();                                // provisional tokens visible to every lane
-    if constexpr (FUSED) {
-        // the chained lanes' byte counts (a successor's tokens from its sync index on), their
-        // output chunks by a scan, then every lane writes its own chunk's bytes
-        uint32_t before = 0;
-        if (inc) for (uint32_t q = 0; q < s; ++q) {
-            const uint32_t t = prov[q];
-            before += (int32_t)t < 0 ? ((t >> 16) & 255u) + 3u : ((t >> 24) & 3u) + 1u;
-        }
-        const uint32_t mine = inc ? outb - before : 0u;
-        const uint32_t binc = wd_scan(mine);
-        const uint32_t btot = wd_at(binc, 63);
-        if (stJ == WR_CAP && J == 0 && cmax > WD_CMIN) cmax >>= 1;
-        if (pos0 + btot > cap) return 2;                  // the slow step reports the overflow exactly
-        const bool ok = wr_resolve((const uint32_t*)(prov + s), c, (int32_t)(binc - mine), (int32_t)btot, inc, J,
-                                   out + pos0, pos0);
+#ifdef SDZ_TIMING
+    if (dbg) {
+        uint32_t ns = nsym;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) ns += __shfl_xor(ns, o);
+        const uint64_t nsy = __ballot(st == WR_NOSYNC);
         if (lane == 0) {
-            S->pos = pos0 + btot;
-            S->bitpos = B0 + stopJ;
-            if (!ok) { S->mode = LM_DONE; S->status = SDZ_INTERNAL; S->zmsg = 5; }
-            else if (stJ == WR_EOB) S->mode = S->last ? LM_TRAILER : LM_TYPE;
+            atomicAdd(&dbg[18], tw1 - tw0); atomicAdd(&dbg[20], 1ull); atomicAdd(&dbg[21], stJ == WR_CAP ? 1ull : 0ull);
+            atomicAdd(&dbg[22], (unsigned long long)ns); atomicAdd(&dbg[23], (unsigned long long)total);
+            atomicAdd(&dbg[24], (unsigned long long)(J + 1)); atomicAdd(&dbg[25], (unsigned long long)n);
+            atomicAdd(&dbg[26], stJ == WR_ERR ? 1ull : 0ull); atomicAdd(&dbg[27], nsy ? 1ull : 0ull);
+            atomicAdd(&dbg[28], stJ == WR_EOB ? 1ull : 0ull); atomicAdd(&dbg[30], (unsigned long long)C);
+            atomicAdd(&dbg[19], clock64() - tw1);
         }
-        __threadfence_block();
-        return !ok ? 1 : stJ == WR_EOB || stJ == WR_END ? 1 : stJ == WR_ERR ? 2 : 0;
     }
+#endif
+    __threadfence_block();                                // provisional tokens visible to every lane
     // compaction, lane by lane in order: destinations never pass their sources
     uint32_t bytes = 0;
     for (uint32_t j = 0; j <= J; ++j) {
@@ -1928,88 +1741,7 @@ __device__ __forceinline__ void wd_cold(const InflateArgs& A, DSave* S, const ui
     __builtin_amdgcn_wave_barrier();
 }
 
-// adler32.ts:34-105 over n output bytes from p, from state (s1, s2), NMAX quirk (sum2 += BASE
-// after each whole 5552-byte block instead of a reduction) -- k_resolve.hip's adler_quirk_ring
-__device__ int32_t wd_adler_quirk(const uint8_t* p, uint32_t len, uint32_t s1, uint32_t s2in) {
-    uint64_t a = s1, s2 = s2in;
-    while (len >= 5552) {
-        len -= 5552;
-        for (int i = 0; i < 5552; ++i) { a += *p++; s2 += a; }
-        a %= 65521u;
-        s2 += 65521u;
-    }
-    if (len) {
-        while (len--) { a += *p++; s2 += a; }
-        a %= 65521u;
-        s2 %= 65521u;
-    }
-    return (int32_t)((uint32_t)a | ((uint32_t)s2 << 16));
-}
-
-// the one-shot record and verdicts (sd-inflate.ts:134-179), as k_inflate_resolve's epilogue for a
-// call without incremental state; gzip's crc32 comes from k_inflate_finalize (lane 0)
-__device__ __noinline__ void wd_record(const InflateArgs& A, const DSave* S, uint32_t sid, uint64_t pos,
-                                       uint32_t S_all, uint32_t T_all, const uint8_t* out, bool failed) {
-    const bool gz = S->container == SDZ_CONTAINER_GZIP;
-    const uint64_t ilen = A.in_len[sid];
-    sdz_inflate_record Rc;
-    Rc.status = failed ? SDZ_INTERNAL : S->status;
-    Rc.zmsg = S->zmsg;
-    Rc.out_len = pos;
-    uint64_t used = (S->bitpos + 7) >> 3;
-    Rc.in_used = used > ilen ? ilen : used;
-    Rc.stored_checksum = S->stored_ck;
-    const bool have = pos > 0;
-    int32_t running = 0;
-    if (!gz) {
-        uint32_t a1 = 1, a2 = 0;
-        if (pos) {
-            const uint32_t nm = (uint32_t)(pos % 65521u);
-            const uint32_t b1 = (uint32_t)(((uint64_t)a1 + S_all) % 65521u);
-            const uint32_t b2 = (uint32_t)(((uint64_t)a2 + (uint64_t)nm * a1 + (uint64_t)nm * S_all + 65521ull * 65521ull - T_all) % 65521u);
-            a1 = b1;
-            a2 = b2;
-        }
-        const uint32_t rr = (uint32_t)(pos & 16383u);
-        if (!failed && (rr == 5552u || rr == 11104u)) {
-            // the final 16 KiB chunk of 5552 / 11104 bytes leaves sum2 unreduced: replay it from
-            // the state at its start (recovered from the plain state and its bytes)
-            const uint8_t* tail = out + (pos - rr);
-            uint64_t qa = 0, qb = 0;
-            for (uint32_t k = 0; k < rr; ++k) { const uint32_t v = tail[k]; qa += v; qb += (uint64_t)(rr - k) * v; }
-            uint32_t s1s = 1, s2s = 0;
-            if (pos != rr) {
-                s1s = (uint32_t)((a1 + 65521u - (uint32_t)(qa % 65521u)) % 65521u);
-                s2s = (uint32_t)(((uint64_t)a2 + 65521ull * 65521ull - (uint64_t)rr * s1s - qb % 65521u) % 65521u);
-            }
-            running = wd_adler_quirk(tail, rr, s1s, s2s);
-        } else {
-            running = (int32_t)(a1 | (a2 << 16));
-        }
-    }
-    Rc.running_checksum = have ? running : 0;
-    Rc.stored_size = S->stored_size;
-    Rc.mtime = S->mtime;
-    Rc.name_off = S->name_off;
-    Rc.name_len = S->name_len;
-    Rc.container = (uint8_t)S->container;
-    const bool complete = !failed && S->mode == LM_DONE && (S->status == SDZ_OK || S->status == SDZ_TRAILING);
-    Rc.complete = complete ? 1 : 0;
-    const uint8_t cv = S->stored_ck == 0 ? SDZ_UNCHECKED : ((have && S->stored_ck == running) ? SDZ_MATCH : SDZ_MISMATCH);
-    const uint8_t sv = S->stored_size == 0 ? SDZ_UNCHECKED
-                     : ((int64_t)S->stored_size == (int64_t)pos ? SDZ_MATCH : SDZ_MISMATCH);
-    Rc.checksum_verdict = cv;
-    Rc.size_verdict = sv;
-    Rc.success = (complete && cv != SDZ_MISMATCH && sv != SDZ_MISMATCH) ? 1 : 0;
-    Rc.out_full = 0;
-    if (!complete && Rc.status == SDZ_OK) Rc.status = SDZ_TRUNCATED;
-    for (int k = 0; k < 10; ++k) Rc.reserved[k] = 0;
-    A.rec[sid] = Rc;
-}
-
-// FUSED: the wave writes the stream's bytes and record itself (one launch, no token rounds,
-// no k_inflate_resolve); else tokens for k_inflate_resolve, in rounds
-template <bool FUSED>
+// tokens for k_inflate_resolve, in rounds
 __global__ __launch_bounds__(64) void k_inflate_wdec(InflateArgs A, uint32_t round) {
     const uint32_t sid = blockIdx.x, lane = threadIdx.x;
     if (sid >= A.n) return;
@@ -2021,8 +1753,14 @@ __global__ __launch_bounds__(64) void k_inflate_wdec(InflateArgs A, uint32_t rou
     const uint64_t ilen = A.in_len[sid];
     const uint64_t cap = A.out_cap[sid];
     const uint64_t tbits = ilen * 8;
-    uint8_t* out = A.out + A.out_off[sid];
-    if (FUSED) { wr_accS[lane] = 0; wr_accT[lane] = 0; }
+#ifdef SDZ_TIMING
+    // development: the first 64 streams' waves (dbg[14] total cycles, [15] cold runs, [16] cold
+    // cycles, [17] table builds' cycles, [29] iteration cycles, [31] table builds)
+    unsigned long long* wdbg = A.dbg && sid < 64 ? A.dbg : nullptr;
+    const unsigned long long tk0 = wdbg ? clock64() : 0;
+#else
+    unsigned long long* wdbg = nullptr;
+#endif
     bool live = false;
     if (round == 0 && (A.out_off[sid] & 7)) {
         if (lane == 0) {
@@ -2033,7 +1771,13 @@ __global__ __launch_bounds__(64) void k_inflate_wdec(InflateArgs A, uint32_t rou
         }
     } else if (round == 0) {
         live = true;
+#ifdef SDZ_TIMING
+        const unsigned long long tc0 = wdbg ? clock64() : 0;
+#endif
         wd_cold(A, S, inp, ilen, cap, tb, tcap, lens, 1u, 0);
+#ifdef SDZ_TIMING
+        if (wdbg && lane == 0) { atomicAdd(&wdbg[16], clock64() - tc0); atomicAdd(&wdbg[15], 1ull); }
+#endif
     } else if (wd_uni(lane == 0 ? (uint32_t)S->mode : 0u) != LM_DONE) {
         live = true;
         for (uint32_t k = lane; k < IL_REGION / 4; k += 64) ((uint32_t*)wd_region)[k] = ((const uint32_t*)S->region)[k];
@@ -2045,24 +1789,7 @@ __global__ __launch_bounds__(64) void k_inflate_wdec(InflateArgs A, uint32_t rou
     bool stale = true;
     int fslow = 0;
     uint32_t cmax = WD_CMAX;
-    uint64_t cold_pos = 0;                                // FUSED: output position of the cold tokens
-    bool failed = false;
     while (live) {
-        if (FUSED) {
-            // cold_run's tokens (headers produce none; stored blocks and slow steps do): their bytes
-            // now, by lane 0, so that the ring is empty for the next iteration
-            const uint32_t nt = wd_uni(lane == 0 ? S->ntok : 0u);
-            if (nt) {
-                if (lane == 0) {
-                    wr_serial(tb, 0, nt, out, cold_pos);
-                    S->ntok = 0;
-                    S->full = 0;
-                }
-                __builtin_amdgcn_s_waitcnt(0);
-                __threadfence_block();
-                __builtin_amdgcn_wave_barrier();
-            }
-        }
         // the stream's state as lane 0 left it (lane 0 reads its own stores; broadcast)
         const uint32_t mode = wd_uni(lane == 0 ? (uint32_t)S->mode : 0u);
         const uint32_t full = wd_uni(lane == 0 ? (uint32_t)S->full : 0u);
@@ -2074,33 +1801,42 @@ __global__ __launch_bounds__(64) void k_inflate_wdec(InflateArgs A, uint32_t rou
         const uint64_t pos = ((uint64_t)wd_uni((uint32_t)(ps >> 32)) << 32) | wd_uni((uint32_t)ps);
         if (mode == LM_CODES && !fslow && tbits >= B0 + 64 + WD_MINSPEC && tcap >= ntok + 80u) {
             if (stale) {
-                if (!wd_build()) { fslow = 1; continue; }
+#ifdef SDZ_TIMING
+                const unsigned long long tb0 = wdbg ? clock64() : 0;
+#endif
+                const bool okb = wd_build();
+#ifdef SDZ_TIMING
+                if (wdbg && lane == 0) { atomicAdd(&wdbg[17], clock64() - tb0); atomicAdd(&wdbg[31], 1ull); }
+#endif
+                if (!okb) { fslow = 1; continue; }
                 stale = false;
             }
-            const int r = wd_iteration<FUSED>(S, inp, ilen, cap, tb, tcap, B0, ntok, pos, cmax, out);
+#ifdef SDZ_TIMING
+            const unsigned long long tb0 = wdbg ? clock64() : 0;
+#endif
+            const int r = wd_iteration(S, inp, ilen, cap, tb, tcap, B0, ntok, pos, cmax, wdbg);
+#ifdef SDZ_TIMING
+            if (wdbg && lane == 0) atomicAdd(&wdbg[29], clock64() - tb0);
+#endif
             if (r == 2) fslow = 1;
             else if (r == 3) fslow = 1;
             continue;
         }
-        cold_pos = pos;
+#ifdef SDZ_TIMING
+        const unsigned long long tc0 = wdbg ? clock64() : 0;
+#endif
         wd_cold(A, S, inp, ilen, cap, tb, tcap, lens, 0u, (fslow || mode == LM_CODES) ? 1 : 0);
+#ifdef SDZ_TIMING
+        if (wdbg && lane == 0) { atomicAdd(&wdbg[16], clock64() - tc0); atomicAdd(&wdbg[15], 1ull); }
+#endif
         fslow = 0;
         stale = true;
     }
+#ifdef SDZ_TIMING
+    if (wdbg && lane == 0) atomicAdd(&wdbg[14], clock64() - tk0);
+#endif
     const uint32_t smode = wd_uni(lane == 0 ? (uint32_t)S->mode : 0u);
     const uint32_t sstall = wd_uni(lane == 0 ? (uint32_t)S->stall : 0u);
-    if constexpr (FUSED) {
-        // the record: adler sums of every lane (each reduced mod 65521)
-        uint64_t s1 = wr_accS[lane], s2 = wr_accT[lane];
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) { s1 += __shfl_xor(s1, o); s2 += __shfl_xor(s2, o); }
-        if (lane == 0) {
-            A.ntok[sid] = 0;
-            A.flags[sid] = 1;
-            wd_record(A, S, sid, live ? S->pos : 0, (uint32_t)(s1 % 65521u), (uint32_t)(s2 % 65521u), out, failed);
-        }
-        return;
-    }
     if (lane == 0) {
         const bool more = live && smode != LM_DONE && !sstall;
         if (more) atomicAdd(A.active, 1u);
@@ -2148,18 +1884,10 @@ int run_inflate_rounds(const InflateArgs& a, hipStream_t s, uint32_t* host_activ
     // the wave decoder (k_inflate_wdec) for one-shot batches; the lane decoder keeps the
     // incremental mode (and the block-parallel split of long streams, off with the wave decoder)
     const bool use_wd = inflate_wdec_enabled() && !a.streaming && !a.segmode && !a.split_plan;
-    // fused (SDZ_WDEC=2): one-shot calls without a preset dictionary
-    const bool fused = use_wd && inflate_wdec_mode() == 2 && a.dict == nullptr;
     for (uint32_t round = 0;; ++round) {
         if (hipMemsetAsync(a.active, 0, sizeof(uint32_t), s) != hipSuccess) { rc = -1; break; }
         if (kernel_ms) (void)hipEventRecord(ev[0], s);
-        if (fused) {                                   // one launch: bytes and records (then finalize)
-            hipLaunchKernelGGL(k_inflate_wdec<true>, dim3(a.n), dim3(64), 0, s, a, 0u);
-            if (kernel_ms) (void)hipEventRecord(ev[1], s);
-            if (kernel_ms) (void)hipEventRecord(ev[2], s);
-            break;
-        }
-        if (use_wd) hipLaunchKernelGGL(k_inflate_wdec<false>, dim3(a.n), dim3(64), 0, s, a, round);
+        if (use_wd) hipLaunchKernelGGL(k_inflate_wdec, dim3(a.n), dim3(64), 0, s, a, round);
         else hipLaunchKernelGGL(k_inflate_decode, g1, dim3(IL_THREADS), 0, s, a, round);
         if (round == 0 && hook) {
             if (int hr = hook(hook_ctx)) { rc = hr; break; }
@@ -2198,7 +1926,7 @@ int run_inflate_rounds(const InflateArgs& a, hipStream_t s, uint32_t* host_activ
         if (kernel_ms) {
             (void)hipEventRecord(ev[3], s);
             (void)hipEventSynchronize(ev[3]);
-            if ((a.one_round || fused) && !a.split_plan) {
+            if (a.one_round && !a.split_plan) {
                 float t0 = 0.f, t1 = 0.f;
                 (void)hipEventElapsedTime(&t0, ev[0], ev[1]);
                 (void)hipEventElapsedTime(&t1, ev[1], ev[2]);

@@ -323,7 +323,7 @@ int inflate_run(InflateArgs& a, hipStream_t s, bool timing_started = false, int 
         HIPCHK(hipMemcpyAsync(h, a.dbg, sizeof h, hipMemcpyDeviceToHost, s));
         HIPCHK(hipStreamSynchronize(s));
         fprintf(stderr, "sdz phases:");
-        for (int k = 0; k < 16; ++k) fprintf(stderr, " %llu", h[k]);
+        for (int k = 0; k < 32; ++k) fprintf(stderr, " %llu", h[k]);
         fprintf(stderr, "\n");
         hipFree(a.dbg);
     }
@@ -1075,7 +1075,7 @@ int rt::deflate_batch_device(const uint8_t* in, const uint64_t* in_off, const ui
         HIPCHK(hipMemcpyAsync(h, dbg, sizeof h, hipMemcpyDeviceToHost, s));
         HIPCHK(hipStreamSynchronize(s));
         fprintf(stderr, "sdz deflate phases:");
-        for (int k = 0; k < 16; ++k) fprintf(stderr, " %llu", h[k]);
+        for (int k = 0; k < 32; ++k) fprintf(stderr, " %llu", h[k]);
         fprintf(stderr, "\n");
         hipFree(dbg);
     }

@@ -141,3 +141,31 @@ def test_incremental_skewed_batch():
     res = st.append(chunks, out_cap=[len(text) * 8 + 64] + [256] * (n - 1))
     assert res[0]["success"] and res[0]["data"] == text * 8
     assert all(r["success"] and r["data"] == b"hello world " * 10 for r in res[1:])
+
+
+def test_concurrent_multi_calls_same_devices():
+    """Two host threads call inflate_batch_multi on the same device list at once (ctypes drops the
+    GIL): the library serialises multi calls, so neither waits on the other's shard at a barrier
+    (overlapping device locks held across the all-gather deadlocked), and both
+    return every record intact."""
+    import threading
+    plain, comp = _mixed_batch(24, seed=5)
+    caps = [len(p) + 64 for p in plain]
+    res, errs = [None, None], []
+
+    def run(k):
+        try:
+            res[k], _ = sdz.inflate_batch_multi(comp, [0, 0], out_caps=caps)
+        except Exception as e:                            # reported below, not swallowed
+            errs.append(e)
+
+    ts = [threading.Thread(target=run, args=(k,)) for k in range(2)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(60)
+    assert not any(t.is_alive() for t in ts), "multi calls deadlocked"
+    assert not errs, errs
+    for recs in res:
+        for r, p in zip(recs, plain):
+            assert r["status"] == "OK" and r["data"] == p

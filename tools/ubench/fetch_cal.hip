@@ -1,0 +1,74 @@
+// FETCH_SIZE / WRITE_SIZE calibration for the access widths the deflate and inflate kernels use
+// (MI355X_MICROARCH.md, HBM/rocprofv3: only 16-byte-per-lane streaming reads are calibrated, at
+// 1/2).  Each kernel touches a known set of bytes of a 2 GiB buffer (well past the 256 MiB
+// Infinity Cache), once:
+//   k_stream16   16 B per lane, coalesced, the whole buffer               (bytes = 2 GiB)
+//   k_scatter1   1 B per lane at a distinct 128-B line (a permutation)    (lines = 16 Mi)
+//   k_scatter8   8 B per lane at a distinct 128-B line                    (lines = 16 Mi)
+//   k_lane8      8 B per lane, lane i reading line-sequentially its own 64 KiB span
+//                (k_dfl_parse's lane-per-stream record walk)            (bytes = 2 GiB)
+//   k_store8     8 B per lane, the same lane-per-span pattern as a store  (bytes = 2 GiB)
+// tools/ubench/fetch_cal.sh runs it under separate FETCH_SIZE / WRITE_SIZE passes and prints
+// counter KiB x 1024 / known bytes per kernel.
+//   hipcc --offload-arch=gfx950 -O3 -o fetch_cal tools/ubench/fetch_cal.hip
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+
+static constexpr uint64_t kBytes = 2ull << 30;
+static constexpr uint64_t kLines = kBytes / 128;
+
+__global__ void k_stream16(const uint4* __restrict__ a, uint32_t* out) {
+    uint32_t acc = 0;
+    for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < kBytes / 16; i += (uint64_t)gridDim.x * 256) {
+        const uint4 v = a[i];
+        acc ^= v.x ^ v.y ^ v.z ^ v.w;
+    }
+    if (acc == 0x12345678u) out[0] = acc;
+}
+// line index of the i-th access: an odd multiplier mod 2^24 is a permutation of the lines
+__device__ __forceinline__ uint64_t perm(uint64_t i) { return (i * 2654435761ull) & (kLines - 1); }
+__global__ void k_scatter1(const uint8_t* __restrict__ a, uint32_t* out) {
+    uint32_t acc = 0;
+    for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < kLines; i += (uint64_t)gridDim.x * 256)
+        acc += a[perm(i) * 128 + (i & 127)];
+    if (acc == 0x12345678u) out[0] = acc;
+}
+__global__ void k_scatter8(const uint64_t* __restrict__ a, uint32_t* out) {
+    uint64_t acc = 0;
+    for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < kLines; i += (uint64_t)gridDim.x * 256)
+        acc += a[perm(i) * 16 + (i & 15)];
+    if (acc == 0x12345678u) out[0] = (uint32_t)acc;
+}
+// 32 Ki lanes, each walking its own 64 KiB span 8 bytes at a time
+__global__ void k_lane8(const uint64_t* __restrict__ a, uint32_t* out) {
+    const uint64_t lane = blockIdx.x * 256ull + threadIdx.x;
+    const uint64_t* p = a + lane * (65536 / 8);
+    uint64_t acc = 0;
+    for (uint32_t k = 0; k < 65536 / 8; ++k) acc += p[k];
+    if (acc == 0x12345678u) out[0] = (uint32_t)acc;
+}
+__global__ void k_store8(uint64_t* __restrict__ a) {
+    const uint64_t lane = blockIdx.x * 256ull + threadIdx.x;
+    uint64_t* p = a + lane * (65536 / 8);
+    for (uint32_t k = 0; k < 65536 / 8; ++k) p[k] = lane * 31 + k;
+}
+
+int main() {
+    uint8_t* a = nullptr;
+    uint32_t* out = nullptr;
+    if (hipMalloc(&a, kBytes) != hipSuccess || hipMalloc(&out, 64) != hipSuccess) return 1;
+    (void)hipMemset(a, 1, kBytes);
+    (void)hipDeviceSynchronize();
+    const uint32_t lanes = (uint32_t)(kBytes / 65536);   // 32 Ki spans of 64 KiB
+    hipLaunchKernelGGL(k_stream16, dim3(4096), dim3(256), 0, 0, (const uint4*)a, out);
+    hipLaunchKernelGGL(k_scatter1, dim3(4096), dim3(256), 0, 0, a, out);
+    hipLaunchKernelGGL(k_scatter8, dim3(4096), dim3(256), 0, 0, (const uint64_t*)a, out);
+    hipLaunchKernelGGL(k_lane8, dim3(lanes / 256), dim3(256), 0, 0, (const uint64_t*)a, out);
+    hipLaunchKernelGGL(k_store8, dim3(lanes / 256), dim3(256), 0, 0, (uint64_t*)a);
+    if (hipDeviceSynchronize() != hipSuccess) return 1;
+    printf("known bytes: stream16 %llu, scatter1 lines %llu (x128 B %llu), scatter8 lines %llu, lane8 %llu, store8 %llu\n",
+           (unsigned long long)kBytes, (unsigned long long)kLines, (unsigned long long)(kLines * 128),
+           (unsigned long long)kLines, (unsigned long long)kBytes, (unsigned long long)kBytes);
+    return 0;
+}
