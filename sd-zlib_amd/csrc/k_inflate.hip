@@ -1016,24 +1016,18 @@ __device__ __forceinline__ bool seg_is_cand(const SegStop& G, uint64_t bit) {
     return lo < G.ncand && G.cand[lo] == bit;
 }
 
-// WD: called by lane 0 of the wave decoder (k_inflate_wdec, one stream per wave: its own LDS
-// symbol bytes and token stage); force_slow: decode the current block's symbols with the
-// exact slow step to its end (the wave decoder's hand-back for errors, output room, tables
-// past its LDS budget and the last bits of the input)
-__shared__ __attribute__((aligned(16))) uint8_t wd_region[IL_REGION + 12];
-__shared__ __attribute__((aligned(16))) uint32_t wd_stage[IL_TSTRIDE / 4];
-__shared__ Tree wd_LL, wd_DD;                     // the wave decoder's trees (LDS: not cold_run's registers)
-template <int MODE, bool WD = false>
+__shared__ __attribute__((aligned(16))) uint8_t wd_region[IL_REGION + 12];   // the wave decoder's symbol bytes
+__shared__ Tree wd_LL, wd_DD;                     // ... and trees (from the stream's state)
+// force_slow: decode the current block's symbols with the exact slow step to its end (the wave
+// decoder's hand-back for errors, output room, tables past its LDS budget and the last input bits)
+template <int MODE>
 __device__ __noinline__ void cold_run(DSave* S, const uint8_t* inp, uint64_t ilen, uint64_t cap,
                                       uint32_t* tb, uint32_t tcap, uint8_t* lens, int32_t format, int32_t has_dict,
                                       int32_t dict_adler, uint32_t init, SegStop G, int force_slow = 0) {
     Lane L;
-    Tree LLr, DDr;
-    Tree& LL = WD ? wd_LL : LLr;
-    Tree& DD = WD ? wd_DD : DDr;
-    uint8_t* region;
-    if constexpr (WD) { region = wd_region; L.ts = wd_stage; }
-    else { region = lane_region(); L.ts = lane_stage(); }
+    Tree LL, DD;
+    uint8_t* region = lane_region();
+    L.ts = lane_stage();
     L.tb = tb; L.tcap = tcap; L.lens = lens;
     L.streaming = MODE == 1; L.stall = 0; L.ubit = 0;
     if (init) {
@@ -1335,13 +1329,17 @@ __global__ __launch_bounds__(IL_THREADS, 1) void k_inflate_decode(InflateArgs A,
 #define WD_MINSPEC 512            // bits past the last-64 reserve below which lane 0 runs the slow step
 #define WD_TST 16                 // token stage per lane (LDS)
 #define WD_INV 511u               // table symbol: invalid code
+#ifndef WD_WPE
+#define WD_WPE 2                  // waves per SIMD the register budget is sized for (<= 256 VGPRs)
+#endif
 
 __shared__ __attribute__((aligned(16))) uint32_t wd_tab[WD_LLT + WD_DT];   // literal/length, then distance
 #define wd_ll wd_tab
 #define wd_dt (wd_tab + WD_LLT)
 __shared__ __attribute__((aligned(16))) uint32_t wd_bm[64 * WD_BMW];
 __shared__ __attribute__((aligned(16))) uint32_t wd_ring[64 * 18];
-__shared__ __attribute__((aligned(16))) uint32_t wd_tst[64 * (WD_TST + 4)];   // + a dummy slot per lane
+__shared__ __attribute__((aligned(16))) uint32_t wd_tst[64 * WD_TST];
+__shared__ uint32_t wd_tdum[64];                  // a dummy token slot per lane (stores that do not push)
 
 enum : uint32_t { WR_RUN = 0, WR_SYNC, WR_EOB, WR_ERR, WR_CAP, WR_END, WR_NOSYNC, WR_CHUNK, WR_OFF };
 
@@ -1465,7 +1463,7 @@ struct WdRes {
 // slow step must take this block from S->bitpos (an invalid code, or the output room);
 // 3: no token room left this round.  cmax: chunk bits (halved on CAP stops).
 __device__ __noinline__ int wd_iteration(DSave* S, const uint8_t* inp, uint64_t ilen, uint64_t cap,
-                                         uint32_t* tb, uint32_t tcap, uint64_t B0, uint32_t ntok0, uint64_t pos0,
+                                         uint32_t* tb, uint32_t tcap, uint32_t* pv, uint64_t B0, uint32_t ntok0, uint64_t pos0,
                                          uint32_t& cmax, unsigned long long* dbg) {
     const uint32_t lane = threadIdx.x & 63u;
 #ifdef SDZ_TIMING
@@ -1484,8 +1482,7 @@ __device__ __noinline__ int wd_iteration(DSave* S, const uint8_t* inp, uint64_t 
     C = C < WD_CMIN ? WD_CMIN : C > cmax ? cmax : C;
     uint32_t n = (lim + C - 1u) / C;
     n = n < 1u ? 1u : n > 64u ? 64u : n;
-    const uint32_t P0 = (ntok0 + 7u) & ~7u;               // provisional area: 8-token aligned
-    const uint32_t space = tcap > P0 + 8u ? tcap - P0 - 8u : 0u;
+    const uint32_t space = tcap > ntok0 + 8u ? tcap - ntok0 - 8u : 0u;   // ring room for the chained tokens
     if (space < 64u) return 3;
     if (space / n < 64u) n = space / 64u;
     uint32_t tcapl = space / n;
@@ -1497,8 +1494,9 @@ __device__ __noinline__ int wd_iteration(DSave* S, const uint8_t* inp, uint64_t 
     const uint32_t bn = lastl ? n * C : (lane + 1u) * C;
     uint32_t* bm = wd_bm + lane * WD_BMW;
     uint32_t* bmn = wd_bm + ((lane + 1u) & 63u) * WD_BMW;
-    uint32_t* tst = wd_tst + lane * (WD_TST + 4);
-    GLB uint32_t* prov = (GLB uint32_t*)(tb + P0 + lane * tcapl);
+    uint32_t* tst = wd_tst + lane * WD_TST;
+    uint32_t* tdum = wd_tdum + lane;
+    GLB uint32_t* prov = (GLB uint32_t*)(pv + lane * tcapl);
 #pragma unroll
     for (int k = 0; k < WD_BMW; k += 4) *(uint4*)(bm + k) = make_uint4(0, 0, 0, 0);
 
@@ -1594,8 +1592,8 @@ __device__ __noinline__ int wd_iteration(DSave* S, const uint8_t* inp, uint64_t 
         const uint32_t tokL = ((isLit ? nlit : nlit - 1u) << 24) | (isLit ? litw2 : litw);
         const uint32_t tokM = 0x80000000u | ((val - 3u) << 16) | (dist - 1u);
         const uint32_t e1 = dec & (emitL | emitP), e2 = dec & isM;
-        tst[e1 ? (ntk & (WD_TST - 1u)) : (uint32_t)WD_TST] = tokL;
-        tst[e2 ? ((ntk + e1) & (WD_TST - 1u)) : (uint32_t)WD_TST] = tokM;
+        *(e1 ? tst + (ntk & (WD_TST - 1u)) : tdum) = tokL;
+        *(e2 ? tst + ((ntk + e1) & (WD_TST - 1u)) : tdum) = tokM;
         ntk += e1 + e2;
         const uint32_t keepL = isLit & (emitL ^ 1u);      // literal still pending
         const uint32_t litwN = keepL ? litw2 : (isLit | isM) ? 0u : litw;
@@ -1689,22 +1687,49 @@ __device__ __noinline__ int wd_iteration(DSave* S, const uint8_t* inp, uint64_t 
         }
     }
 #endif
-    __threadfence_block();                                // provisional tokens visible to every lane
-    // compaction, lane by lane in order: destinations never pass their sources
+    // compaction: chunk by chunk, the whole wave copies each chained lane's tokens (from its
+    // successor's start index on) into the ring -- coalesced, 4 chunks' loads in flight at a time
+    // (the provisional slots are a buffer of their own, so no copy overwrites another's source).
+    // Loads and stores past a chunk's count go to the lane's dummy slot: no per-token branch.
     uint32_t bytes = 0;
-    for (uint32_t j = 0; j <= J; ++j) {
-        const uint32_t cj = wd_at(c, j), sj = wd_at(s, j), dj = wd_at(excl, j);
-        const uint32_t* src = tb + P0 + j * tcapl + sj;
-        uint32_t* dst = tb + ntok0 + dj;
-        for (uint32_t q = lane; q < cj; q += 64u) {
-            const uint32_t t = src[q];
-            dst[q] = t;
-            bytes += (int32_t)t < 0 ? ((t >> 16) & 255u) + 3u : ((t >> 24) & 3u) + 1u;
+#ifdef SDZ_TIMING
+    const unsigned long long tc0 = dbg ? clock64() : 0;   // dbg[12]: compaction cycles
+#endif
+    {
+        GLB uint32_t* dst0 = (GLB uint32_t*)(tb + ntok0);
+        GLB uint32_t* dum = (GLB uint32_t*)(pv + 64u * WD_CAP + lane);
+        for (uint32_t j0 = 0; j0 <= J; j0 += 4u) {
+            uint32_t v[4][WD_CAP / 64];
+            uint32_t cj[4], dj[4];
+#pragma unroll
+            for (uint32_t jj = 0; jj < 4u; ++jj) {
+                const uint32_t j = j0 + jj < 64u ? j0 + jj : 63u;
+                cj[jj] = j0 + jj <= J ? wd_at(c, j) : 0u;
+                dj[jj] = wd_at(excl, j);
+                const GLB uint32_t* src = (const GLB uint32_t*)(pv + j * tcapl + wd_at(s, j));
+#pragma unroll
+                for (uint32_t k = 0; k < WD_CAP / 64; ++k) {
+                    const uint32_t q = lane + 64u * k;
+                    v[jj][k] = *(q < cj[jj] ? src + q : (const GLB uint32_t*)dum);
+                }
+            }
+#pragma unroll
+            for (uint32_t jj = 0; jj < 4u; ++jj)
+#pragma unroll
+                for (uint32_t k = 0; k < WD_CAP / 64; ++k) {
+                    const uint32_t q = lane + 64u * k;
+                    const bool in = q < cj[jj];
+                    const uint32_t t = v[jj][k];
+                    *(in ? dst0 + dj[jj] + q : dum) = t;
+                    bytes += !in ? 0u : (int32_t)t < 0 ? ((t >> 16) & 255u) + 3u : ((t >> 24) & 3u) + 1u;
+                }
         }
-        __builtin_amdgcn_s_waitcnt(0);                    // this lane's reads are done before the next stores
     }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) bytes += __shfl_xor(bytes, o);
+#ifdef SDZ_TIMING
+    if (dbg && lane == 0) atomicAdd(&dbg[12], clock64() - tc0);
+#endif
     if (stJ == WR_CAP && J == 0 && cmax > WD_CMIN) cmax >>= 1;
     if (pos0 + bytes > cap) return 2;                     // the slow step reports the overflow exactly
     if (lane == 0) {
@@ -1719,32 +1744,21 @@ __device__ __noinline__ int wd_iteration(DSave* S, const uint8_t* inp, uint64_t 
     return stJ == WR_EOB || stJ == WR_END ? 1 : stJ == WR_ERR ? 2 : 0;
 }
 
-// lane 0: cold_run on the stream's state, with the open 32-token line staged from HBM before
-// and everything (pending literals included) written back after
-__device__ __forceinline__ void wd_cold(const InflateArgs& A, DSave* S, const uint8_t* inp, uint64_t ilen,
-                                        uint64_t cap, uint32_t* tb, uint32_t tcap, uint8_t* lens, uint32_t init,
-                                        int force_slow) {
-    if ((threadIdx.x & 63u) == 0) {
-        if (!init) {
-            const uint32_t nt = S->ntok, b = nt & ~(IL_TSTAGE - 1u);
-            for (uint32_t j = b; j < nt; ++j) wd_stage[j - b] = tb[j];
-        }
-        SegStop G = { 0, nullptr, 0 };
-        cold_run<0, true>(S, inp, ilen, cap, tb, tcap, lens, A.format, A.dict != nullptr,
-                          dict_id_of(A.dict_adler, A.dict_adler_dev), init, G, force_slow);
-        Core H;
-        H.tb = tb; H.ts = wd_stage; H.ntok = S->ntok; H.litw = S->litw; H.nlit = S->nlit;
-        tok_finish(H);
-        S->ntok = H.ntok; S->litw = 0; S->nlit = 0;
-    }
-    __threadfence_block();
-    __builtin_amdgcn_wave_barrier();
-}
-
-// tokens for k_inflate_resolve, in rounds
-__global__ __launch_bounds__(64) void k_inflate_wdec(InflateArgs A, uint32_t round) {
-    const uint32_t sid = blockIdx.x, lane = threadIdx.x;
-    if (sid >= A.n) return;
+// The wave decoder's block-level work -- container header, block headers and trees, stored blocks,
+// the trailer, the last input bits, and the exact slow step for blocks the wave declined (an
+// invalid code, the output room, tables past the LDS budget) -- runs in k_inflate_wcold, one LANE
+// per stream as in k_inflate_decode (cold_run), so that 64 streams' serial header work shares a
+// wave.  k_inflate_wdec (one WAVE per stream) then decodes the block's symbols; the host
+// alternates the two until no stream needs block-level work in this round.
+// first: the round's first launch (round 0: starts the streams; later rounds: resumes the streams
+// whose token ring filled).  A.flags: 2 = not live this round (finished earlier), else 0 until
+// k_inflate_wdec records the round's end.
+__global__ __launch_bounds__(IL_THREADS, 1) void k_inflate_wcold(InflateArgs A, uint32_t round, uint32_t first) {
+    uint8_t* region = lane_region();
+    uint32_t* ts = lane_stage();
+    const uint32_t gid = blockIdx.x * IL_STREAMS + lane_slot();
+    if (gid >= A.n || (threadIdx.x & 63u) >= IL_WAVE_LANES) return;
+    const uint32_t sid = gid;
     DSave* S = (DSave*)A.dsave + sid;
     uint32_t* tb = A.tokens + (uint64_t)sid * A.round_tokens;
     const uint32_t tcap = A.round_tokens;
@@ -1752,55 +1766,83 @@ __global__ __launch_bounds__(64) void k_inflate_wdec(InflateArgs A, uint32_t rou
     const uint8_t* inp = A.in + A.in_off[sid];
     const uint64_t ilen = A.in_len[sid];
     const uint64_t cap = A.out_cap[sid];
+    const int32_t did = dict_id_of(A.dict_adler, A.dict_adler_dev);
+    const SegStop G = { 0, nullptr, 0 };
+    uint32_t init = 0;
+    int force_slow = 0;
+    if (first) {
+        if (round == 0 && (A.out_off[sid] & 7)) {
+            S->mode = LM_DONE; S->status = SDZ_BAD_RECORD; S->zmsg = 0; S->bitpos = 0; S->pos = 0;
+            S->container = SDZ_CONTAINER_RAW; S->stored_ck = 0; S->stored_size = 0; S->mtime = 0;
+            S->name_off = 0; S->name_len = 0; S->dict_used = 0; S->ntok = 0; S->litw = 0;
+            S->nlit = 0; S->full = 0; S->stall = 0;
+            A.ntok[sid] = 0; A.flags[sid] = 2;
+            return;
+        }
+        if (round > 0 && S->mode == LM_DONE) { A.ntok[sid] = 0; A.flags[sid] = 2; return; }
+        A.flags[sid] = 0;
+        if (round == 0) init = 1;
+        else { S->ntok = 0; S->full = 0; }               // a new round: the token ring from 0
+    } else {
+        if (A.flags[sid] == 2 || S->mode == LM_DONE || S->full) return;
+        force_slow = S->mode == LM_CODES ? 1 : 0;        // the wave declined the rest of this block
+    }
+    if (!init) {
+        for (int k = 0; k < IL_REGION / 4; ++k) ((uint32_t*)region)[k] = ((const uint32_t*)S->region)[k];
+        const uint32_t nt = S->ntok, b = nt & ~(IL_TSTAGE - 1u);   // the open 32-token line
+        for (uint32_t q = b; q < nt; ++q) ts[q - b] = tb[q];
+    }
+    cold_run<0>(S, inp, ilen, cap, tb, tcap, lens, A.format, A.dict != nullptr, did, init, G, force_slow);
+    Core H;                                              // flush the token stage
+    H.tb = tb; H.ts = ts; H.ntok = S->ntok; H.litw = S->litw; H.nlit = S->nlit;
+    tok_finish(H);
+    S->ntok = H.ntok; S->litw = 0; S->nlit = 0;
+    if (S->mode == LM_CODES)
+        for (int k = 0; k < IL_REGION / 4; ++k) ((uint32_t*)S->region)[k] = ((const uint32_t*)region)[k];
+}
+
+// One WAVE per stream: the current block's symbols by speculative iterations, until the block
+// ends, the input's last bits, or anything the wave declines (k_inflate_wcold takes those).
+// Records the stream's round state for k_inflate_resolve; counts the streams that need block-level
+// work (A.active[1]) and those whose token ring filled (A.active[0], another round).
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WD_WPE, WD_WPE))) void k_inflate_wdec(InflateArgs A, uint32_t round) {
+    const uint32_t sid = blockIdx.x, lane = threadIdx.x;
+    if (sid >= A.n) return;
+    if (wd_uni(lane == 0 ? A.flags[sid] : 0u) == 2u) return;   // not live this round
+    DSave* S = (DSave*)A.dsave + sid;
+    uint32_t* tb = A.tokens + (uint64_t)sid * A.round_tokens;
+    const uint32_t tcap = A.round_tokens;
+    const uint8_t* inp = A.in + A.in_off[sid];
+    const uint64_t ilen = A.in_len[sid];
+    const uint64_t cap = A.out_cap[sid];
     const uint64_t tbits = ilen * 8;
 #ifdef SDZ_TIMING
-    // development: the first 64 streams' waves (dbg[14] total cycles, [15] cold runs, [16] cold
-    // cycles, [17] table builds' cycles, [29] iteration cycles, [31] table builds)
+    // development: the first 64 streams' waves (dbg[14] total cycles, [15] launches, [17] table
+    // builds' cycles, [29] iteration cycles, [31] table builds)
     unsigned long long* wdbg = A.dbg && sid < 64 ? A.dbg : nullptr;
     const unsigned long long tk0 = wdbg ? clock64() : 0;
 #else
     unsigned long long* wdbg = nullptr;
 #endif
-    bool live = false;
-    if (round == 0 && (A.out_off[sid] & 7)) {
-        if (lane == 0) {
-            S->mode = LM_DONE; S->status = SDZ_BAD_RECORD; S->zmsg = 0; S->bitpos = 0; S->pos = 0;
-            S->container = SDZ_CONTAINER_RAW; S->stored_ck = 0; S->stored_size = 0; S->mtime = 0;
-            S->name_off = 0; S->name_len = 0; S->dict_used = 0; S->ntok = 0; S->litw = 0;
-            S->nlit = 0; S->full = 0; S->stall = 0;
-        }
-    } else if (round == 0) {
-        live = true;
-#ifdef SDZ_TIMING
-        const unsigned long long tc0 = wdbg ? clock64() : 0;
-#endif
-        wd_cold(A, S, inp, ilen, cap, tb, tcap, lens, 1u, 0);
-#ifdef SDZ_TIMING
-        if (wdbg && lane == 0) { atomicAdd(&wdbg[16], clock64() - tc0); atomicAdd(&wdbg[15], 1ull); }
-#endif
-    } else if (wd_uni(lane == 0 ? (uint32_t)S->mode : 0u) != LM_DONE) {
-        live = true;
+    const uint32_t mode0 = wd_uni(lane == 0 ? (uint32_t)S->mode : 0u);
+    const uint32_t full0 = wd_uni(lane == 0 ? (uint32_t)S->full : 0u);
+    if (mode0 == LM_CODES && !full0) {
         for (uint32_t k = lane; k < IL_REGION / 4; k += 64) ((uint32_t*)wd_region)[k] = ((const uint32_t*)S->region)[k];
         if (lane == 0) { wd_LL = S->LL; wd_DD = S->DD; }
-        if (lane == 0) { S->ntok = 0; S->full = 0; }
         __threadfence_block();
         __builtin_amdgcn_wave_barrier();
-    }
-    bool stale = true;
-    int fslow = 0;
-    uint32_t cmax = WD_CMAX;
-    while (live) {
-        // the stream's state as lane 0 left it (lane 0 reads its own stores; broadcast)
-        const uint32_t mode = wd_uni(lane == 0 ? (uint32_t)S->mode : 0u);
-        const uint32_t full = wd_uni(lane == 0 ? (uint32_t)S->full : 0u);
-        if (mode == LM_DONE || full) break;
-        const uint64_t bp = lane == 0 ? S->bitpos : 0;
-        const uint64_t B0 = ((uint64_t)wd_uni((uint32_t)(bp >> 32)) << 32) | wd_uni((uint32_t)bp);
-        const uint32_t ntok = wd_uni(lane == 0 ? S->ntok : 0u);
-        const uint64_t ps = lane == 0 ? S->pos : 0;
-        const uint64_t pos = ((uint64_t)wd_uni((uint32_t)(ps >> 32)) << 32) | wd_uni((uint32_t)ps);
-        if (mode == LM_CODES && !fslow && tbits >= B0 + 64 + WD_MINSPEC && tcap >= ntok + 80u) {
-            if (stale) {
+        bool built = false;
+        uint32_t cmax = WD_CMAX;
+        for (;;) {
+            // the stream's state as lane 0 left it (lane 0 reads its own stores; broadcast)
+            if (wd_uni(lane == 0 ? (uint32_t)S->mode : 0u) != LM_CODES) break;   // the block ended
+            const uint64_t bp = lane == 0 ? S->bitpos : 0;
+            const uint64_t B0 = ((uint64_t)wd_uni((uint32_t)(bp >> 32)) << 32) | wd_uni((uint32_t)bp);
+            const uint32_t ntok = wd_uni(lane == 0 ? S->ntok : 0u);
+            const uint64_t ps = lane == 0 ? S->pos : 0;
+            const uint64_t pos = ((uint64_t)wd_uni((uint32_t)(ps >> 32)) << 32) | wd_uni((uint32_t)ps);
+            if (tbits < B0 + 64 + WD_MINSPEC || tcap < ntok + 80u) break;   // the slow step's
+            if (!built) {
 #ifdef SDZ_TIMING
                 const unsigned long long tb0 = wdbg ? clock64() : 0;
 #endif
@@ -1808,46 +1850,30 @@ __global__ __launch_bounds__(64) void k_inflate_wdec(InflateArgs A, uint32_t rou
 #ifdef SDZ_TIMING
                 if (wdbg && lane == 0) { atomicAdd(&wdbg[17], clock64() - tb0); atomicAdd(&wdbg[31], 1ull); }
 #endif
-                if (!okb) { fslow = 1; continue; }
-                stale = false;
+                if (!okb) break;
+                built = true;
             }
 #ifdef SDZ_TIMING
             const unsigned long long tb0 = wdbg ? clock64() : 0;
 #endif
-            const int r = wd_iteration(S, inp, ilen, cap, tb, tcap, B0, ntok, pos, cmax, wdbg);
+            const int r = wd_iteration(S, inp, ilen, cap, tb, tcap, A.wdprov + (uint64_t)sid * kWdProvTokens, B0, ntok,
+                                       pos, cmax, wdbg);
 #ifdef SDZ_TIMING
             if (wdbg && lane == 0) atomicAdd(&wdbg[29], clock64() - tb0);
 #endif
-            if (r == 2) fslow = 1;
-            else if (r == 3) fslow = 1;
-            continue;
+            if (r >= 2) break;                           // the slow step takes the block from here
         }
-#ifdef SDZ_TIMING
-        const unsigned long long tc0 = wdbg ? clock64() : 0;
-#endif
-        wd_cold(A, S, inp, ilen, cap, tb, tcap, lens, 0u, (fslow || mode == LM_CODES) ? 1 : 0);
-#ifdef SDZ_TIMING
-        if (wdbg && lane == 0) { atomicAdd(&wdbg[16], clock64() - tc0); atomicAdd(&wdbg[15], 1ull); }
-#endif
-        fslow = 0;
-        stale = true;
     }
 #ifdef SDZ_TIMING
-    if (wdbg && lane == 0) atomicAdd(&wdbg[14], clock64() - tk0);
+    if (wdbg && lane == 0) { atomicAdd(&wdbg[14], clock64() - tk0); atomicAdd(&wdbg[15], 1ull); }
 #endif
-    const uint32_t smode = wd_uni(lane == 0 ? (uint32_t)S->mode : 0u);
-    const uint32_t sstall = wd_uni(lane == 0 ? (uint32_t)S->stall : 0u);
     if (lane == 0) {
-        const bool more = live && smode != LM_DONE && !sstall;
-        if (more) atomicAdd(A.active, 1u);
-        if (!live) { A.ntok[sid] = 0; A.flags[sid] = 2; }
-        else {
-            A.ntok[sid] = S->ntok;
-            A.flags[sid] = smode == LM_DONE ? 1u : sstall ? 3u : 0u;
-        }
+        const uint32_t m = (uint32_t)S->mode, f = (uint32_t)S->full;
+        A.ntok[sid] = S->ntok;
+        A.flags[sid] = m == LM_DONE ? 1u : 0u;
+        if (m != LM_DONE && !f) atomicAdd(A.active + 1, 1u);   // block-level work next
+        if (m != LM_DONE && f) atomicAdd(A.active, 1u);        // another round
     }
-    if (live && smode != LM_DONE)
-        for (uint32_t k = lane; k < IL_REGION / 4; k += 64) ((uint32_t*)S->region)[k] = ((const uint32_t*)wd_region)[k];
 }
 
 void launch_seg_decode(const InflateArgs& a, hipStream_t s) {
@@ -1883,12 +1909,25 @@ int run_inflate_rounds(const InflateArgs& a, hipStream_t s, uint32_t* host_activ
     int rc = 0;
     // the wave decoder (k_inflate_wdec) for one-shot batches; the lane decoder keeps the
     // incremental mode (and the block-parallel split of long streams, off with the wave decoder)
-    const bool use_wd = inflate_wdec_enabled() && !a.streaming && !a.segmode && !a.split_plan;
+    const bool use_wd = inflate_wdec_enabled() && a.wdprov && !a.streaming && !a.segmode && !a.split_plan;
     for (uint32_t round = 0;; ++round) {
         if (hipMemsetAsync(a.active, 0, sizeof(uint32_t), s) != hipSuccess) { rc = -1; break; }
         if (kernel_ms) (void)hipEventRecord(ev[0], s);
-        if (use_wd) hipLaunchKernelGGL(k_inflate_wdec, dim3(a.n), dim3(64), 0, s, a, round);
-        else hipLaunchKernelGGL(k_inflate_decode, g1, dim3(IL_THREADS), 0, s, a, round);
+        if (use_wd) {
+            // block-level work (a lane per stream) and the blocks' symbols (a wave per stream),
+            // alternately, until no stream of this round needs block-level work
+            for (uint32_t it = 0;; ++it) {
+                hipLaunchKernelGGL(k_inflate_wcold, g1, dim3(IL_THREADS), 0, s, a, round, it == 0 ? 1u : 0u);
+                if (hipMemsetAsync(a.active, 0, 2 * sizeof(uint32_t), s) != hipSuccess) { rc = -1; break; }
+                hipLaunchKernelGGL(k_inflate_wdec, dim3(a.n), dim3(64), 0, s, a, round);
+                if (hipMemcpyAsync(host_active, a.active + 1, sizeof(uint32_t), hipMemcpyDeviceToHost, s) != hipSuccess ||
+                    hipStreamSynchronize(s) != hipSuccess) { rc = -1; break; }
+                if (*host_active == 0) break;
+            }
+            if (rc) break;
+        } else {
+            hipLaunchKernelGGL(k_inflate_decode, g1, dim3(IL_THREADS), 0, s, a, round);
+        }
         if (round == 0 && hook) {
             if (int hr = hook(hook_ctx)) { rc = hr; break; }
         }

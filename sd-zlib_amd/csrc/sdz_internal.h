@@ -17,6 +17,9 @@ enum ZMsg : int32_t {
 
 // bytes of per-stream global scratch used by the inflate kernel (code lengths)
 constexpr uint64_t kInflateScratchPerStream = 320;
+// the wave decoder's provisional token slots per stream (64 lanes x WD_CAP tokens, then a dummy
+// slot per lane for the compaction's masked-off stores)
+constexpr uint64_t kWdProvTokens = 64 * 512 + 64;
 #define IS_WIN 32768u                 // incremental mode: window bytes per stream
 
 struct InflateArgs {
@@ -42,6 +45,7 @@ struct InflateArgs {
     uint32_t* ntok;              // n
     uint32_t* flags;             // n: 0 more rounds, 1 finished this round, 2 finished earlier
     uint32_t* active;            // 1 counter
+    uint32_t* wdprov;            // wave decoder (one-shot calls): n * kWdProvTokens provisional tokens
     unsigned long long* dbg;     // phase cycle counters (SDZ_PHASE_TIMING), normally null
     // incremental mode (sdz_inflate_append_batch_device): input may continue in a later
     // call, so streams stall at the end of their input instead of ending TRUNCATED

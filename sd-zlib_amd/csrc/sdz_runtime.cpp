@@ -290,7 +290,11 @@ int inflate_scratch(InflateArgs& a, uint32_t n, bool own_state, size_t extra, hi
     const size_t off_rs = off_ds + (own_state ? (size_t)n * dsb : 0);
     const size_t off_tk = (off_rs + (own_state ? (size_t)n * rsb : 0) + 255) & ~(size_t)255;
     const size_t off_nt = off_tk + (size_t)n * T * 4;
-    const size_t off_ex = (off_nt + (size_t)n * 8 + 256 + 255) & ~(size_t)255;
+    // the wave decoder's provisional tokens (one-shot calls): each lane's chunk is decoded into a
+    // slot of its own there and compacted into the token ring after the iteration's join
+    const bool wdp = own_state && inflate_wdec_enabled();
+    const size_t off_wp = (off_nt + (size_t)n * 8 + 256 + 255) & ~(size_t)255;
+    const size_t off_ex = (off_wp + (wdp ? (size_t)n * kWdProvTokens * 4 : 0) + 255) & ~(size_t)255;
     void* scratch = nullptr;
     if (int rc = use.get(off_ex + extra, &scratch)) return rc;
     uint8_t* base = (uint8_t*)scratch;
@@ -301,6 +305,7 @@ int inflate_scratch(InflateArgs& a, uint32_t n, bool own_state, size_t extra, hi
     a.ntok = (uint32_t*)(base + off_nt);
     a.flags = a.ntok + n;
     a.active = a.flags + n;
+    a.wdprov = wdp ? (uint32_t*)(base + off_wp) : nullptr;
     if (extra_out) *extra_out = base + off_ex;
     return SDZ_API_OK;
 }
