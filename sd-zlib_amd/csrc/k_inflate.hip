@@ -23,6 +23,7 @@
 // Reference quirks mirrored: root-bits "need" at end of
 // input (infcodes.ts:368-387), huft_build's MANY=1400 table budget, incomplete
 // single-code trees, the gzip FEXTRA mode that never advances (inflate.ts:343-345).
+#include <vector>
 #include "inflate_state.h"
 #include <type_traits>
 
@@ -1016,7 +1017,7 @@ __device__ __forceinline__ bool seg_is_cand(const SegStop& G, uint64_t bit) {
     return lo < G.ncand && G.cand[lo] == bit;
 }
 
-__shared__ __attribute__((aligned(16))) uint8_t wd_region[IL_REGION + 12];   // the wave decoder's symbol bytes
+__shared__ __attribute__((aligned(16))) uint8_t wd_region[IL_REGION];   // the wave decoder's symbol bytes
 __shared__ Tree wd_LL, wd_DD;                     // ... and trees (from the stream's state)
 // force_slow: decode the current block's symbols with the exact slow step to its end (the wave
 // decoder's hand-back for errors, output room, tables past its LDS budget and the last input bits)
@@ -1315,13 +1316,14 @@ __global__ __launch_bounds__(IL_THREADS, 1) void k_inflate_decode(InflateArgs A,
 #define WD_W 1024                 // bits of a lane's boundary map
 #endif
 #define WD_BMW (WD_W / 32)
+#define WD_BMS (WD_BMW + 1)       // a lane's map stride: odd, so that lanes at one offset hit 32 banks
 #ifndef WD_CAP
 #define WD_CAP 512                // provisional tokens per lane and iteration
 #endif
 #define WD_LLR 10                 // root bits of the literal/length table
 #define WD_DR 8                   // ... of the distance table
 #define WD_LLT 1536               // table entries (root + subtables)
-#define WD_DT 768
+#define WD_DT 736                 // (6 waves per CU: the LDS total stays below 160 KiB / 6)
 #ifndef WD_CMAX
 #define WD_CMAX 4096              // chunk bits
 #endif
@@ -1336,10 +1338,12 @@ __global__ __launch_bounds__(IL_THREADS, 1) void k_inflate_decode(InflateArgs A,
 __shared__ __attribute__((aligned(16))) uint32_t wd_tab[WD_LLT + WD_DT];   // literal/length, then distance
 #define wd_ll wd_tab
 #define wd_dt (wd_tab + WD_LLT)
-__shared__ __attribute__((aligned(16))) uint32_t wd_bm[64 * WD_BMW];
+__shared__ __attribute__((aligned(16))) uint32_t wd_bm[64 * WD_BMS];
 __shared__ __attribute__((aligned(16))) uint32_t wd_ring[64 * 18];
-__shared__ __attribute__((aligned(16))) uint32_t wd_tst[64 * WD_TST];
-__shared__ uint32_t wd_tdum[64];                  // a dummy token slot per lane (stores that do not push)
+// token stage: WD_TST slots + a dummy slot (stores that do not push) per lane; the odd stride puts
+// the lanes' flush reads at one slot on 32 banks
+#define WD_TSS (WD_TST + 1)
+__shared__ __attribute__((aligned(16))) uint32_t wd_tst[64 * WD_TSS];
 
 enum : uint32_t { WR_RUN = 0, WR_SYNC, WR_EOB, WR_ERR, WR_CAP, WR_END, WR_NOSYNC, WR_CHUNK, WR_OFF };
 
@@ -1492,13 +1496,13 @@ __device__ __noinline__ int wd_iteration(DSave* S, const uint8_t* inp, uint64_t 
     const bool lastl = lane == n - 1u;
     const uint32_t bj = lane * C;
     const uint32_t bn = lastl ? n * C : (lane + 1u) * C;
-    uint32_t* bm = wd_bm + lane * WD_BMW;
-    uint32_t* bmn = wd_bm + ((lane + 1u) & 63u) * WD_BMW;
-    uint32_t* tst = wd_tst + lane * WD_TST;
-    uint32_t* tdum = wd_tdum + lane;
+    uint32_t* bm = wd_bm + lane * WD_BMS;
+    uint32_t* bmn = wd_bm + ((lane + 1u) & 63u) * WD_BMS;
+    uint32_t* tst = wd_tst + lane * WD_TSS;
+    uint32_t* tdum = tst + WD_TST;
     GLB uint32_t* prov = (GLB uint32_t*)(pv + lane * tcapl);
 #pragma unroll
-    for (int k = 0; k < WD_BMW; k += 4) *(uint4*)(bm + k) = make_uint4(0, 0, 0, 0);
+    for (int k = 0; k < WD_BMW; ++k) bm[k] = 0u;
 
     Hot H;
     H.ring = wd_ring + lane * 18u;
@@ -1615,10 +1619,13 @@ __device__ __noinline__ int wd_iteration(DSave* S, const uint8_t* inp, uint64_t 
             const bool f = ntk - nfl >= 8u;
             if (__ballot(f)) {
                 if (f) {
-                    const uint4* s4 = (const uint4*)(tst + (nfl & (WD_TST - 1)));
-                    const uint4 a = s4[0], b = s4[1];
+                    const uint32_t* s1 = tst + (nfl & (WD_TST - 1));
+                    uint32_t v[8];
+#pragma unroll
+                    for (int k = 0; k < 8; ++k) v[k] = s1[k];
                     GLB uint4* d = (GLB uint4*)(prov + nfl);
-                    d[0] = a; d[1] = b;
+                    d[0] = make_uint4(v[0], v[1], v[2], v[3]);
+                    d[1] = make_uint4(v[4], v[5], v[6], v[7]);
                     nfl += 8u;
                 }
             }
@@ -1889,9 +1896,24 @@ void launch_inflate_finalize(const InflateArgs& a, hipStream_t s);
 uint64_t inflate_dsave_bytes() { return sizeof(DSave); }
 int inflate_wdec_mode() {
     const char* e = getenv("SDZ_WDEC");
-    return e ? atoi(e) : 0;
+    return e && *e ? (atoi(e) != 0 ? 1 : 0) : -1;
 }
-bool inflate_wdec_enabled() { return inflate_wdec_mode() != 0; }
+bool inflate_wave_policy(uint32_t n, const uint64_t* host_len, const uint64_t* dev_len, void* stream) {
+    const int m = inflate_wdec_mode();
+    if (m >= 0) return m == 1;
+    if (n == 0 || n > kWdAutoStreams) return false;
+    std::vector<uint64_t> len;
+    if (!host_len) {
+        len.resize(n);
+        if (hipMemcpyAsync(len.data(), dev_len, n * sizeof(uint64_t), hipMemcpyDeviceToHost, (hipStream_t)stream) != hipSuccess ||
+            hipStreamSynchronize((hipStream_t)stream) != hipSuccess)
+            return false;
+        host_len = len.data();
+    }
+    for (uint32_t i = 0; i < n; ++i)
+        if (host_len[i] > kWdAutoBytes) return false;
+    return true;
+}
 uint64_t inflate_rsave_bytes() { return sizeof(RSave); }
 
 // host driver: rounds of (decode, resolve) until no stream needs another round.
@@ -1909,7 +1931,7 @@ int run_inflate_rounds(const InflateArgs& a, hipStream_t s, uint32_t* host_activ
     int rc = 0;
     // the wave decoder (k_inflate_wdec) for one-shot batches; the lane decoder keeps the
     // incremental mode (and the block-parallel split of long streams, off with the wave decoder)
-    const bool use_wd = inflate_wdec_enabled() && a.wdprov && !a.streaming && !a.segmode && !a.split_plan;
+    const bool use_wd = a.wave && a.wdprov && !a.streaming && !a.segmode && !a.split_plan;
     for (uint32_t round = 0;; ++round) {
         if (hipMemsetAsync(a.active, 0, sizeof(uint32_t), s) != hipSuccess) { rc = -1; break; }
         if (kernel_ms) (void)hipEventRecord(ev[0], s);

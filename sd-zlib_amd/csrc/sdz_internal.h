@@ -45,7 +45,8 @@ struct InflateArgs {
     uint32_t* ntok;              // n
     uint32_t* flags;             // n: 0 more rounds, 1 finished this round, 2 finished earlier
     uint32_t* active;            // 1 counter
-    uint32_t* wdprov;            // wave decoder (one-shot calls): n * kWdProvTokens provisional tokens
+    uint32_t wave;               // 1: this one-shot call decodes with the wave decoder (inflate_wave_policy)
+    uint32_t* wdprov;            // ... whose provisional tokens: n * kWdProvTokens
     unsigned long long* dbg;     // phase cycle counters (SDZ_PHASE_TIMING), normally null
     // incremental mode (sdz_inflate_append_batch_device): input may continue in a later
     // call, so streams stall at the end of their input instead of ending TRUNCATED
@@ -67,7 +68,14 @@ struct InflateArgs {
 };
 
 uint64_t inflate_dsave_bytes();  // per stream decode state
-bool inflate_wdec_enabled();     // one-shot batches decode with k_inflate_wdec (SDZ_WDEC)
+// one-shot batches: decode with the wave decoder (k_inflate_wdec, a wave per stream) rather than the
+// lane decoder (k_inflate_decode, a lane per stream)?  SDZ_WDEC=1 / 0 forces it; by default for
+// batches of at most kWdAutoStreams streams of at most kWdAutoBytes compressed bytes each (the lane
+// decoder's time is its longest stream's serial decode, the wave decoder's the batch's total)
+constexpr uint32_t kWdAutoStreams = 8192;
+constexpr uint64_t kWdAutoBytes = 4ull << 20;
+int inflate_wdec_mode();         // SDZ_WDEC: -1 unset, 0 off, 1 on
+bool inflate_wave_policy(uint32_t n, const uint64_t* host_len, const uint64_t* dev_len, void* stream);
 uint64_t inflate_rsave_bytes();  // per stream resolve state
 // hook (optional): called once on the host right after the first round's decode is queued
 // (the split pre-pass's second half); a nonzero return ends the rounds with that code

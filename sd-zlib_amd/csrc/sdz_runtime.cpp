@@ -292,7 +292,7 @@ int inflate_scratch(InflateArgs& a, uint32_t n, bool own_state, size_t extra, hi
     const size_t off_nt = off_tk + (size_t)n * T * 4;
     // the wave decoder's provisional tokens (one-shot calls): each lane's chunk is decoded into a
     // slot of its own there and compacted into the token ring after the iteration's join
-    const bool wdp = own_state && inflate_wdec_enabled();
+    const bool wdp = own_state && a.wave;
     const size_t off_wp = (off_nt + (size_t)n * 8 + 256 + 255) & ~(size_t)255;
     const size_t off_ex = (off_wp + (wdp ? (size_t)n * kWdProvTokens * 4 : 0) + 255) & ~(size_t)255;
     void* scratch = nullptr;
@@ -411,7 +411,7 @@ struct SplitHost {
 int inflate_split_start(const InflateArgs& a, hipStream_t s, PoolUse& find_use, SplitHost& H) {
     const uint32_t n = a.n;
     if (const char* e = getenv("SDZ_SPLIT")) if (atoi(e) == 0) return SDZ_API_OK;
-    if (inflate_wdec_enabled()) return SDZ_API_OK;      // the wave decoder is parallel inside a block
+    if (a.wave) return SDZ_API_OK;                       // the wave decoder is parallel inside a block
     uint64_t split_min = 16 << 10;
     if (const char* e = getenv("SDZ_SPLIT_MIN")) split_min = strtoull(e, nullptr, 10);
     std::vector<uint64_t> len(n);
@@ -643,6 +643,7 @@ int rt::inflate_batch_device(const uint8_t* in, const uint64_t* in_off, const ui
         a.dict_adler_dev = d_id;
     }
     PoolUse use(g_inflate_scratch, s);
+    a.wave = inflate_wave_policy(n, host_len, in_len, s) ? 1u : 0u;
     if (int rc = inflate_scratch(a, n, true, 0, s, use, nullptr)) return rc;
     a.in = in; a.in_off = in_off; a.in_len = in_len;
     a.out = out; a.out_off = out_off; a.out_cap = out_cap;

@@ -7,6 +7,8 @@
 //   k_scatter8   8 B per lane at a distinct 128-B line                    (lines = 16 Mi)
 //   k_lane8      8 B per lane, lane i reading line-sequentially its own 64 KiB span
 //                (k_dfl_parse's lane-per-stream record walk)            (bytes = 2 GiB)
+//   k_lane16     16 B per lane, the same per-lane spans (k_inflate_decode's input refills)
+//                                                                        (bytes = 2 GiB)
 //   k_store8     8 B per lane, the same lane-per-span pattern as a store  (bytes = 2 GiB)
 // tools/ubench/fetch_cal.sh runs it under separate FETCH_SIZE / WRITE_SIZE passes and prints
 // counter KiB x 1024 / known bytes per kernel.
@@ -48,6 +50,13 @@ __global__ void k_lane8(const uint64_t* __restrict__ a, uint32_t* out) {
     for (uint32_t k = 0; k < 65536 / 8; ++k) acc += p[k];
     if (acc == 0x12345678u) out[0] = (uint32_t)acc;
 }
+__global__ void k_lane16(const uint4* __restrict__ a, uint32_t* out) {
+    const uint64_t lane = blockIdx.x * 256ull + threadIdx.x;
+    const uint4* p = a + lane * (65536 / 16);
+    uint32_t acc = 0;
+    for (uint32_t k = 0; k < 65536 / 16; ++k) { const uint4 v = p[k]; acc ^= v.x ^ v.y ^ v.z ^ v.w; }
+    if (acc == 0x12345678u) out[0] = acc;
+}
 __global__ void k_store8(uint64_t* __restrict__ a) {
     const uint64_t lane = blockIdx.x * 256ull + threadIdx.x;
     uint64_t* p = a + lane * (65536 / 8);
@@ -65,6 +74,7 @@ int main() {
     hipLaunchKernelGGL(k_scatter1, dim3(4096), dim3(256), 0, 0, a, out);
     hipLaunchKernelGGL(k_scatter8, dim3(4096), dim3(256), 0, 0, (const uint64_t*)a, out);
     hipLaunchKernelGGL(k_lane8, dim3(lanes / 256), dim3(256), 0, 0, (const uint64_t*)a, out);
+    hipLaunchKernelGGL(k_lane16, dim3(lanes / 256), dim3(256), 0, 0, (const uint4*)a, out);
     hipLaunchKernelGGL(k_store8, dim3(lanes / 256), dim3(256), 0, 0, (uint64_t*)a);
     if (hipDeviceSynchronize() != hipSuccess) return 1;
     printf("known bytes: stream16 %llu, scatter1 lines %llu (x128 B %llu), scatter8 lines %llu, lane8 %llu, store8 %llu\n",
