@@ -1894,19 +1894,40 @@ struct PState {
     // d + 1 are 0 for d < 4, else floor(log2 d) - 1 (no dist_code table, no per-code counts)
     uint32_t dxb;
     GLB uint32_t* sym;
+    uint32_t* stg;                // null, or an LDS stage of PS_STG symbols written as whole 64-B pieces
     uint8_t* blk;                 // this stream's first block slot
 };
+#define PS_STG 16
 __device__ __forceinline__ void ps_init(PState& st, const DeflateArgs& A, uint32_t sid, int n) {
     st.n = n; st.level = A.level; st.good = c_config[A.level][0]; st.max_lazy = c_config[A.level][1];
     st.strstart = 0; st.match_length = MIN_MATCH - 1; st.match_start = 0; st.match_available = 0;
     st.block_start = 0; st.off = 0;
     st.last_lit = 0; st.matches = 0; st.lx = 0; st.nblk = 0; st.sym0 = 0; st.dxb = 0;
     st.sym = (GLB uint32_t*)A.sym_buf + 2 * A.rp0[sid];
+    st.stg = nullptr;
     st.blk = A.blk + (uint64_t)A.tb0[sid] * FB_SLOT;
     st.nbcap = A.tb0[sid + 1] - A.tb0[sid];
 }
+// the staged symbols [lx & ~(PS_STG - 1), lx) to the symbol buffer
+__device__ __forceinline__ void ps_drain(PState& st) {
+    const uint32_t k0 = st.lx & ~(PS_STG - 1u);
+    for (uint32_t k = k0; k < st.lx; ++k) st.sym[k] = st.stg[k - k0];
+}
 __device__ __forceinline__ bool ps_tally(PState& st, int dist, int lc) {      // _tr_tally, deflate.ts:488-524
-    st.sym[st.lx++] = (uint32_t)lc | ((uint32_t)dist << 8);
+    const uint32_t v = (uint32_t)lc | ((uint32_t)dist << 8);
+    if (st.stg) {
+        // staged: a lane's symbols leave in 64-byte pieces (4-byte stores of 64 lanes to 64 streams
+        // wrote ~2.4x the symbol bytes to HBM: partial lines evicted before they filled)
+        st.stg[st.lx & (PS_STG - 1u)] = v;
+        if ((++st.lx & (PS_STG - 1u)) == 0) {
+            const uint2* q = (const uint2*)st.stg;
+            uint2* d = (uint2*)(uint32_t*)(st.sym + st.lx - PS_STG);   // (8-byte aligned: rp0 * 8 bytes)
+#pragma unroll
+            for (int k = 0; k < PS_STG / 2; ++k) d[k] = q[k];
+        }
+    } else {
+        st.sym[st.lx++] = v;
+    }
     st.last_lit++;
     if (dist) {
         st.matches++;
@@ -1981,6 +2002,7 @@ __device__ __forceinline__ void ps_step(PState& st, uint64_t r) {
 }
 __device__ __forceinline__ void ps_finish(PState& st, const GLB uint8_t* in, GLB FStream* F) {
     if (st.match_available) ps_tally(st, 0, in[st.strstart - 1]);
+    if (st.stg) ps_drain(st);
     ps_flush(st, 1);
     F->nblk = st.nblk;
     F->flag = st.nblk > st.nbcap ? 1u : 0u;
@@ -1995,8 +2017,10 @@ __global__ __launch_bounds__(64) void k_dfl_parse(DeflateArgs A) {
     if (in_len == 0 || A.rp0[sid] == ~0ull) { F->nblk = 0; F->flag = 1; return; }
     const GLB uint8_t* in = (const GLB uint8_t*)(A.in + A.in_off[sid]);
     const GLB uint64_t* rec = (const GLB uint64_t*)A.rec_buf + A.rp0[sid];
+    __shared__ __attribute__((aligned(16))) uint32_t stage[64 * PS_STG];
     PState st;
     ps_init(st, A, sid, (int)in_len);
+    st.stg = stage + lane * PS_STG;
     for (;;) {
         if (ps_fill(st)) break;
         uint64_t r = rec[st.strstart];                        // the step's one load (rec_word)

@@ -71,9 +71,12 @@ uint64_t inflate_dsave_bytes();  // per stream decode state
 // one-shot batches: decode with the wave decoder (k_inflate_wdec, a wave per stream) rather than the
 // lane decoder (k_inflate_decode, a lane per stream)?  SDZ_WDEC=1 / 0 forces it; by default for
 // batches of at most kWdAutoStreams streams of at most kWdAutoBytes compressed bytes each (the lane
-// decoder's time is its longest stream's serial decode, the wave decoder's the batch's total)
+// decoder's time is its longest stream's serial decode, the wave decoder's the batch's total), when
+// the longest is at least kWdAutoMinBytes (shorter ones decode in a few lane steps, and the lane
+// decoder's single decode + resolve launch keeps small calls' latency)
 constexpr uint32_t kWdAutoStreams = 8192;
 constexpr uint64_t kWdAutoBytes = 4ull << 20;
+constexpr uint64_t kWdAutoMinBytes = 16ull << 10;
 int inflate_wdec_mode();         // SDZ_WDEC: -1 unset, 0 off, 1 on
 bool inflate_wave_policy(uint32_t n, const uint64_t* host_len, const uint64_t* dev_len, void* stream);
 uint64_t inflate_rsave_bytes();  // per stream resolve state

@@ -7,4 +7,5 @@ echo "gpu suite rc=$rc: $(tail -1 gpurun_out/full_gpu.log)"
 timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" 2>&1 | tail -2 || exit 1
 [ -n "${LAT:-1}" ] && timeout -k 10 300 python3 tools/facade_prof.py 2>&1 | tail -8
 [ -n "${NODE:-1}" ] && which node > /dev/null && timeout -k 10 300 node tests/node/perf.mjs 2>&1 | tail -3
+[ -n "${C3:-}" ] && timeout -k 10 200 python3 tools/run_c2.py --mode deflate --steps 2 2>&1 | tail -2
 exit 0

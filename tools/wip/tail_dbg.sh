@@ -1,0 +1,37 @@
+#!/bin/bash
+# root-cause the LDS tail search's GPU-only mismatch.  Builds the WIP kernel
+# (tools/wip/tail_lds.patch) into a separate library with a check beside each LDS walk: the HBM walk
+# (tail_search) at the same position, and a device printf of both results, the window offset, the
+# staged range and the first link wherever they differ.  Then deflates the failing input of
+# gpurun_out/pt_dev1.log (L4, "deflate", paradiselost.txt[:100000]) and a few neighbours.
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}" && export TMPDIR=/tmp && mkdir -p gpurun_out
+D=/tmp/sdzdbg
+rm -rf $D && mkdir -p $D && cp -r sd-zlib_amd include $D/ && (cd $D && patch -s -p1 < $OLDPWD/tools/wip/tail_lds.patch) || exit 1
+python3 - $D/sd-zlib_amd/csrc/k_deflate.hip <<'PY'
+import sys
+p = sys.argv[1]; s = open(p).read()
+a = """            const uint64_t r = P <= n - MIN_MATCH ? tail_core((int)(P - off), n, P, max_chain, nice, prevw, wb) : 0ull;"""
+b = a + """
+            const uint64_t r2 = P <= n - MIN_MATCH ? tail_search(in, pv, n, P, max_chain, nice) : 0ull;
+            if (r != r2)
+                printf("TAILDBG sid %u n %lld P %lld off %lld lo %d whi %d s %d r %llx r2 %llx first %d firstg %u w0 %u %u %u\\n",
+                       sid, (long long)n, (long long)P, (long long)off, lo, whi, (int)(P - off), (unsigned long long)r,
+                       (unsigned long long)r2, prevw((int)(P - off)), (unsigned)pv[P], wb((int)(P - off)),
+                       wb((int)(P - off) + 1), wb((int)(P - off) + 2));"""
+assert s.count(a) == 1, "hook not found"
+s = s.replace(a, b)
+open(p, "w").write(s)
+PY
+(cd $D/sd-zlib_amd && rm -rf build lib && timeout -k 10 600 make -s -j16 > /dev/null 2>&1) || { echo build-failed; exit 1; }
+SDZ_LIB=$D/sd-zlib_amd/lib/libsdz.so SDZ_TAIL_LDS=1 timeout -k 10 300 python3 - <<'PY'
+import os, sys
+sys.path.insert(0, "sd-zlib_amd/python"); sys.path.insert(0, "tests"); sys.path.insert(0, "oracle")
+import sdz, oracle as O
+t = open("tests/golden/paradiselost.txt", "rb").read()
+for n in (100000, 99000, 131072, 200000, 65536 + 300):
+    for lv in (4, 6, 9):
+        g = sdz.deflate(t[:n], {"level": lv})
+        o = O.deflate(t[:n], level=lv, format="deflate")
+        d = next((i for i in range(min(len(g), len(o))) if g[i] != o[i]), None)
+        print("n %d L%d gpu %d oracle %d first diff %s" % (n, lv, len(g), len(o), d), flush=True)
+PY
