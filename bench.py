@@ -401,6 +401,37 @@ def node_facade():
     return json.loads(r.stdout.strip().splitlines()[-1])
 
 
+def small_batch_leg(sdz, L, comp, text, n, steps):
+    """A small batch (n copies of C2's stream): the wave decoder (a wave per stream, picked by
+    inflate_wave_policy for <= 8192 streams of 16 KiB - 4 MiB) against the lane decoder
+    (SDZ_WDEC=0: a lane per stream, its time the longest stream's serial decode); kernel ms."""
+    b = DeviceBatch(sdz, comp, n, len(text) + 64)
+    res = {"streams": n, "bytes_out": n * len(text)}
+    try:
+        for name, env in (("wave", None), ("lane", "0")):
+            old = os.environ.pop("SDZ_WDEC", None)
+            if env is not None:
+                os.environ["SDZ_WDEC"] = env
+            try:
+                inflate_step(sdz, b)
+                split = []
+                ms = [inflate_step(sdz, b, split) for _ in range(steps)]
+            finally:
+                os.environ.pop("SDZ_WDEC", None)
+                if old is not None:
+                    os.environ["SDZ_WDEC"] = old
+            recs = (sdz.InflateRecord * n).from_buffer_copy(b.d_rec.download(n * b.rec_size))
+            ok = all(r.success and r.out_len == len(text) for r in recs) and \
+                all(b.d_out.download(len(text), j * b.out_stride) == text for j in (0, n - 1))
+            kms = sum(ms) / len(ms)
+            res[name] = {"kernel_ms": round(kms, 3), "GBps_out": round(n * len(text) / kms / 1e6, 1),
+                         "decode_ms": round(sum(x[0] for x in split) / len(split), 3),
+                         "resolve_ms": round(sum(x[1] for x in split) / len(split), 3), "parity": bool(ok)}
+    finally:
+        b.free()
+    return res
+
+
 def facade_latency(sdz, reps=40):
     """BASELINE configs[0] (C1) through the drop-in's host path: inflate(simple.deflate) and
     deflate(simple.txt) one call at a time (staging pools, no per-call allocation); median
@@ -491,6 +522,8 @@ def main():
                     help="streams for the host-buffer (PCIe-inclusive) inflate probe, e.g. 2048; off by "
                          "default so that the rocprofv3 stats of the default command hold C2 launches only")
     ap.add_argument("--latency", type=int, default=1, help="C1-style single-call latency of the facade (0: skip)")
+    ap.add_argument("--small-streams", type=int, default=1024,
+                    help="small-batch leg: that many copies of C2's stream, wave vs lane decoder (0: skip)")
     ap.add_argument("--node", type=int, default=1,
                     help="time the reference's own perf case (test/perf.html) through the Node facade (0: skip)")
     args = ap.parse_args()
@@ -681,6 +714,9 @@ def main():
     if args.mixed_steps > 0:
         mixed = mixed_leg(sdz, L, args.mixed_steps, args.mixed_scale, barrier, allmax, world, rank)
 
+    small = None
+    if rank == 0 and args.small_streams > 0:
+        small = small_batch_leg(sdz, L, comp, text, args.small_streams, 3)
     latency = None
     if rank == 0 and args.latency > 0:
         latency = facade_latency(sdz)
@@ -735,6 +771,7 @@ def main():
         "inflate_distinct": distinct,
         "mixed": mixed,
         "facade_latency": latency,
+        "inflate_small_batch": small,
         "node_facade": nodef,
     }
     if rank == 0:

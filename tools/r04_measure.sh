@@ -28,7 +28,7 @@ cat gpurun_out/r04/r04_bench.json
 step bench kernel trace
 rm -rf gpurun_out/r04/bench_kt
 timeout -k 10 700 rocprofv3 --kernel-trace --stats -d gpurun_out/r04/bench_kt -o run --output-format csv -- \
-    python3 bench.py --node 0 --latency 0 > gpurun_out/r04/r04_bench_kt.json 2> gpurun_out/r04/r04_bench_kt.err || exit 1
+    python3 bench.py --node 0 --latency 0 --small-streams 0 > gpurun_out/r04/r04_bench_kt.json 2> gpurun_out/r04/r04_bench_kt.err || exit 1
 step configs
 timeout -k 10 300 python3 tools/run_configs.py --config c5 > gpurun_out/r04/c5.json 2> gpurun_out/r04/c5.err || exit 1
 timeout -k 10 300 python3 tools/run_configs.py --config c4 --scale 8 > gpurun_out/r04/c4.json 2> gpurun_out/r04/c4.err || exit 1
