@@ -649,3 +649,12 @@ def test_output_slot_edges():
             assert g["status"] == "OUT_OVERFLOW" and not g["success"], g["status"]
             n = g["out_len"]
             assert cap - 258 < n <= cap and g["data"][:n] == p[:n]
+
+
+@pytest.mark.parametrize("n", [65836, 100000, 200000])
+def test_deflate_tail_window_regression(paradise, n):
+    """Inputs on which an LDS-staged variant of the last positions' search (k_dfl_tail) differed from
+    the reference on the GPU only (adjacent byte reads merged into one unaligned
+    ds_read_u16): L4 / L6 / L9 bytes against the oracle."""
+    for lv in (4, 6, 9):
+        assert sdz.deflate(paradise[:n], {"level": lv}) == O.deflate(paradise[:n], level=lv, format="deflate"), lv
