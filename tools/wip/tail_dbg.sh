@@ -1,9 +1,12 @@
 #!/bin/bash
 # root-cause the LDS tail search's GPU-only mismatch.  Builds the WIP kernel
 # (tools/wip/tail_lds.patch) into a separate library with a check beside each LDS walk: the HBM walk
-# (tail_search) at the same position, and a device printf of both results, the window offset, the
-# staged range and the first link wherever they differ.  Then deflates the failing input of
-# gpurun_out/pt_dev1.log (L4, "deflate", paradiselost.txt[:100000]) and a few neighbours.
+# (tail_search) at the same position, and a device printf of both results wherever they differ
+# (TAILDBG).  Variants: TAIL_FIX=1 volatile window reads (no merged u16 reads: still differs),
+# TAIL_TRACE=1 the first links of one position, TAIL_REWALK=1 a noinline re-walk with a printf per
+# candidate on the LDS and the HBM accessors (they agree), TAIL_REC=1 the walk's candidates kept by
+# global stores (the mismatches disappear).  Cause and model: DESIGN 5, tools/wip/tail_model.py.
+# Then deflates paradiselost.txt[:100000] and a few neighbours at L4/L6/L9 against the oracle.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}" && export TMPDIR=/tmp && mkdir -p gpurun_out
 D=/tmp/sdzdbg
 rm -rf $D && mkdir -p $D && cp -r sd-zlib_amd include $D/ && (cd $D && patch -s -p1 < $OLDPWD/tools/wip/tail_lds.patch) || exit 1
@@ -40,6 +43,79 @@ if os.environ.get("TAIL_TRACE"):
                 }
             }
 """ + a3)
+if os.environ.get("TAIL_REWALK"):
+    # on a mismatch, walk again with a printf at every candidate, once on the LDS accessors and
+    # once on the HBM ones (at most 3 positions per launch): where do the two walks part?
+    walker = """template <class PrevW, class WB>
+__device__ __noinline__ void tail_log(const char* tag, long long P, int strstart, int64_t n, int chain_length, int nice,
+                                      PrevW prevw, WB wb) {
+    int cur = prevw(strstart);
+    const int lookahead = (int)(n - P);
+    if (nice > lookahead) nice = lookahead;
+    const int limit = strstart > MAX_DIST ? strstart - MAX_DIST : 0;
+    int best = MIN_MATCH - 1, k = 0;
+    uint32_t scan_end1 = wb(strstart + best - 1), scan_end = wb(strstart + best);
+    const uint32_t c0 = wb(strstart), c1 = wb(strstart + 1);
+    do {
+        const int match = cur, nx = prevw(match);
+        const uint32_t e0 = wb(match + best), e1 = wb(match + best - 1), m0 = wb(match), m1 = wb(match + 1);
+        int len = 0;
+        if ((e0 == scan_end) & (e1 == scan_end1) & (m0 == c0) & (m1 == c1)) {
+            len = 3;
+            while (len < MAX_MATCH && wb(strstart + len) == wb(match + len)) ++len;
+            if (len > best) { best = len; if (len >= nice) { printf("TAILLOG %s P %lld k %d cur %d len %d best %d break\\n", tag, P, k, cur, len, best); break; }
+                              scan_end1 = wb(strstart + best - 1); scan_end = wb(strstart + best); }
+        }
+        printf("TAILLOG %s P %lld k %d cur %d nx %d e %u %u m %u %u se %u %u len %d best %d\\n", tag, P, k, cur, nx, e0, e1, m0,
+               m1, scan_end, scan_end1, len, best);
+        ++k;
+        cur = nx;
+    } while (cur > limit && --chain_length != 0);
+}
+"""
+    a4 = "// k_dfl_tail with the window the last positions search"
+    assert s.count(a4) == 1
+    s = s.replace(a4, walker + a4)
+    a5 = """            if (r != r2)"""
+    assert s.count(a5) == 1
+    s = s.replace(a5, """            if (r != r2 && atomicAdd(&nlog, 1) < 3) {
+                tail_log("lds", (long long)P, (int)(P - off), n, max_chain, nice, prevw, wb);
+                auto prevg = [&](int i) -> int { const int64_t q = i + off; const uint32_t d = pv[q]; const int64_t rr = q - (int64_t)d;
+                                                 return d && rr > off ? (int)(rr - off) : 0; };
+                auto wbg = [&](int i) -> uint32_t { return win_byte(in, n, off, i); };
+                tail_log("hbm", (long long)P, (int)(P - off), n, max_chain, nice, prevg, wbg);
+            }
+""" + a5)
+    a6 = """    __shared__ long long psplit;"""
+    assert s.count(a6) == 1
+    s = s.replace(a6, a6 + """
+    __shared__ int nlog;
+    if (threadIdx.x == 0) nlog = 0;""")
+if os.environ.get("TAIL_REC"):
+    # the production walk itself, instrumented only by global stores: each iteration's candidate,
+    # link, chain_length and k go to g_vis[thread]; on a mismatch the record is printed
+    a7 = "template <class PrevW, class WB>\n__device__ __forceinline__ uint64_t tail_core("
+    assert s.count(a7) == 1
+    s = s.replace(a7, "__device__ int g_vis[256][4 * 40];\n__device__ int g_nv[256];\n" + a7)
+    a8 = """        if (++k == qchain) { qbest = best; qstart = bstart; }
+        cur = nx;
+    } while (cur > limit && --chain_length != 0);
+    if (qbest < 0) { qbest = best; qstart = bstart; }
+    const uint32_t full = best > MIN_MATCH - 1 ? ((uint32_t)best << 16) | (uint32_t)(strstart - bstart) : 0u;"""
+    assert s.count(a8) == 2, s.count(a8)
+    i8 = s.index(a8, s.index("__device__ __forceinline__ uint64_t tail_core("))
+    s = s[:i8] + """        if (k < 40) { int* v = g_vis[threadIdx.x] + 4 * k; v[0] = match; v[1] = nx; v[2] = chain_length; v[3] = best; }
+        g_nv[threadIdx.x] = k + 1;
+""" + s[i8:]
+    a9 = """            if (r != r2)"""
+    assert s.count(a9) == 1
+    s = s.replace(a9, """            if (r != r2 && n == 100000) {
+                const int nv = g_nv[threadIdx.x];
+                for (int q = 0; q < nv && q < 40; ++q)
+                    printf("TAILREC P %lld q %d match %d nx %d chain %d best %d\\n", (long long)P, q, g_vis[threadIdx.x][4 * q],
+                           g_vis[threadIdx.x][4 * q + 1], g_vis[threadIdx.x][4 * q + 2], g_vis[threadIdx.x][4 * q + 3]);
+            }
+""" + a9)
 if os.environ.get("TAIL_FIX"):
     # the suspected cause: two adjacent byte reads of W merged into one ds_read_u16 at an odd LDS
     # address; volatile byte reads cannot be merged
@@ -48,7 +124,7 @@ if os.environ.get("TAIL_FIX"):
     s = s.replace(a2, """        auto wb = [&](int i) -> uint32_t { return ((volatile uint8_t*)W)[i - lo]; };""")
 open(p, "w").write(s)
 PY
-grep -c "volatile uint8_t\*)W\|TAILTRACE" $D/sd-zlib_amd/csrc/k_deflate.hip | sed "s/^/hooks applied: /"
+grep -c "volatile uint8_t\*)W\|TAILTRACE\|TAILLOG %s P %lld k %d cur %d nx\|g_vis\[threadIdx.x\] + 4" $D/sd-zlib_amd/csrc/k_deflate.hip | sed "s/^/hooks applied: /"
 t0=$(date +%s); (cd $D/sd-zlib_amd && rm -rf build lib && timeout -k 10 600 make -s -j16 > /dev/null 2>&1) || { echo build-failed; exit 1; }
 echo "debug library built in $(( $(date +%s) - t0 )) s"
 SDZ_LIB=$D/sd-zlib_amd/lib/libsdz.so SDZ_TAIL_LDS=1 timeout -k 10 300 python3 - <<'PY'
