@@ -52,11 +52,22 @@ def per_kernel(path, counter):
 
 
 def load_cal(path):
-    if path and os.path.exists(path):
-        return json.load(open(path)).get("counter_bytes_over_known", {})
-    cands = sorted(glob.glob(os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "profiles",
-                                          "r[0-9][0-9]_fetch_cal.json")))
-    return json.load(open(cands[-1])).get("counter_bytes_over_known", {}) if cands else {}
+    if not (path and os.path.exists(path)):
+        cands = sorted(glob.glob(os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "profiles",
+                                              "r[0-9][0-9]_fetch_cal.json")))
+        path = cands[-1] if cands else None
+    if not path:
+        return {}, {}
+    d = json.load(open(path))
+    return d.get("counter_bytes_over_known", {}), d.get("read_GBps", {})
+
+
+def kernel_ms(root, steps):
+    """per-launch ms of each kernel from the kernel-trace pass (<root>/kt), if it is there"""
+    path = os.path.join(root, "kt", "run_kernel_stats.csv")
+    if not os.path.exists(path):
+        return {}
+    return {r["Name"].split("(")[0]: float(r["TotalDurationNs"]) / 1e6 / steps for r in csv.DictReader(open(path))}
 
 
 def main():
@@ -64,7 +75,9 @@ def main():
     root, steps, out = sys.argv[1], int(sys.argv[2]), sys.argv[3]
     if len(sys.argv) > 4 and sys.argv[4]:
         PREFIXES = tuple(sys.argv[4].split(","))
-    cal = load_cal(sys.argv[5] if len(sys.argv) > 5 else None)
+    cal, rates = load_cal(sys.argv[5] if len(sys.argv) > 5 else None)
+    kms = kernel_ms(root, steps)
+    peak = max(rates.values()) if rates else None
     fcal, wcal = cal.get("FETCH_SIZE", {}), cal.get("WRITE_SIZE", {})
     f, nf = per_kernel(os.path.join(root, "pmc_fetch", "run_counter_collection.csv"), "FETCH_SIZE")
     w, nw = per_kernel(os.path.join(root, "pmc_write", "run_counter_collection.csv"), "WRITE_SIZE")
@@ -81,10 +94,17 @@ def main():
         rows[k] = {"fetch_bytes": fb, "write_bytes": wb, "fetch_raw_bytes": fraw, "write_raw_bytes": wraw,
                    "read_class": rc if rr else "uncalibrated (raw)", "fetch_counter_over_known": rr,
                    "write_class": wc, "dispatches_per_launch": nf.get(k, 0) / steps}
+        if k in kms and kms[k] > 0:
+            # the rate the corrected bytes imply over the kernel's time, against the fastest read
+            # rate the calibration kernels reach: above it, the correction does not fit the kernel
+            rows[k]["kernel_ms"] = kms[k]
+            rows[k]["implied_GBps"] = (fb + wb) / (kms[k] * 1e6)
+            if peak:
+                rows[k]["implied_over_read_peak"] = rows[k]["implied_GBps"] / peak
         total += fb + wb
         total_raw += fraw + wraw
     res = {"hbm_bytes_per_launch": total, "hbm_raw_counter_bytes_per_launch": total_raw, "per_kernel": rows,
-           "calibration": cal,
+           "calibration": cal, "read_GBps": rates,
            "note": "KiB -> bytes; FETCH_SIZE / WRITE_SIZE divided by the counter-over-known-bytes ratio measured "
                    "for each kernel's access class (tools/ubench/fetch_cal.sh); kernels without a class are raw"}
     json.dump(res, open(out, "w"), indent=1)

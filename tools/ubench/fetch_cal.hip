@@ -11,7 +11,9 @@
 //                                                                        (bytes = 2 GiB)
 //   k_store8     8 B per lane, the same lane-per-span pattern as a store  (bytes = 2 GiB)
 // tools/ubench/fetch_cal.sh runs it under separate FETCH_SIZE / WRITE_SIZE passes and prints
-// counter KiB x 1024 / known bytes per kernel.
+// counter KiB x 1024 / known bytes per kernel.  `fetch_cal time` times each read kernel instead
+// (best of 5): the read-only rates a kernel's calibrated traffic can be checked against
+// (streaming bytes, and 128-B lines x 128 B for the scattered kernels).
 //   hipcc --offload-arch=gfx950 -O3 -o fetch_cal tools/ubench/fetch_cal.hip
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -63,13 +65,37 @@ __global__ void k_store8(uint64_t* __restrict__ a) {
     for (uint32_t k = 0; k < 65536 / 8; ++k) p[k] = lane * 31 + k;
 }
 
-int main() {
+int main(int argc, char** argv) {
     uint8_t* a = nullptr;
     uint32_t* out = nullptr;
     if (hipMalloc(&a, kBytes) != hipSuccess || hipMalloc(&out, 64) != hipSuccess) return 1;
     (void)hipMemset(a, 1, kBytes);
     (void)hipDeviceSynchronize();
     const uint32_t lanes = (uint32_t)(kBytes / 65536);   // 32 Ki spans of 64 KiB
+    if (argc > 1) {
+        hipEvent_t e0, e1;
+        (void)hipEventCreate(&e0);
+        (void)hipEventCreate(&e1);
+        const char* names[5] = {"stream16", "scatter1", "scatter8", "lane8", "lane16"};
+        for (int k = 0; k < 5; ++k) {
+            float best = 1e30f;
+            for (int r = 0; r < 5; ++r) {
+                (void)hipEventRecord(e0, 0);
+                if (k == 0) hipLaunchKernelGGL(k_stream16, dim3(4096), dim3(256), 0, 0, (const uint4*)a, out);
+                if (k == 1) hipLaunchKernelGGL(k_scatter1, dim3(4096), dim3(256), 0, 0, a, out);
+                if (k == 2) hipLaunchKernelGGL(k_scatter8, dim3(4096), dim3(256), 0, 0, (const uint64_t*)a, out);
+                if (k == 3) hipLaunchKernelGGL(k_lane8, dim3(lanes / 256), dim3(256), 0, 0, (const uint64_t*)a, out);
+                if (k == 4) hipLaunchKernelGGL(k_lane16, dim3(lanes / 256), dim3(256), 0, 0, (const uint4*)a, out);
+                (void)hipEventRecord(e1, 0);
+                if (hipEventSynchronize(e1) != hipSuccess) return 1;
+                float ms = 0;
+                (void)hipEventElapsedTime(&ms, e0, e1);
+                if (ms < best) best = ms;
+            }
+            printf("READ %s %.4f ms %.1f GB/s\n", names[k], best, (double)kBytes / (best * 1e6));
+        }
+        return 0;
+    }
     hipLaunchKernelGGL(k_stream16, dim3(4096), dim3(256), 0, 0, (const uint4*)a, out);
     hipLaunchKernelGGL(k_scatter1, dim3(4096), dim3(256), 0, 0, a, out);
     hipLaunchKernelGGL(k_scatter8, dim3(4096), dim3(256), 0, 0, (const uint64_t*)a, out);

@@ -7,6 +7,7 @@ export TMPDIR=/tmp
 mkdir -p gpurun_out/fcal
 B=tools/ubench/fetch_cal
 [ -x $B ] || hipcc --offload-arch=gfx950 -O3 -o $B tools/ubench/fetch_cal.hip || exit 1
+timeout -k 10 60 ./$B time > gpurun_out/fcal/time.txt 2>&1 || exit 1
 timeout -s KILL 60 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/fcal/f -o run --output-format csv -- ./$B > gpurun_out/fcal/f.log 2>&1 || exit 1
 timeout -s KILL 60 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/fcal/w -o run --output-format csv -- ./$B > gpurun_out/fcal/w.log 2>&1 || exit 1
 python3 - <<'PY' | tee gpurun_out/fetch_cal.txt
@@ -26,7 +27,13 @@ for c, d in (("FETCH_SIZE", "f"), ("WRITE_SIZE", "w")):
         for k, v in sorted(tot.items()):
             print("%s %-12s %.4g B  /known(lines x 128 B or bytes) = %.3f" % (c, k, v, v / known.get(k, 1)))
             res.setdefault(c, {})[k.replace("k_", "")] = v / known.get(k, 1)
-json.dump({"counter_bytes_over_known": res, "note": "FETCH_SIZE/WRITE_SIZE x 1024 over the bytes each kernel "
+rates = {}
+for l in open("gpurun_out/fcal/time.txt"):
+    f = l.split()
+    if f and f[0] == "READ":
+        rates[f[1]] = float(f[4])
+        print("read rate %-9s %.1f GB/s (known bytes / best of 5)" % (f[1], rates[f[1]]))
+json.dump({"counter_bytes_over_known": res, "read_GBps": rates, "note": "FETCH_SIZE/WRITE_SIZE x 1024 over the bytes each kernel "
            "touches once (scatter: distinct 128-B lines x 128 B); tools/ubench/fetch_cal.hip"},
           open("gpurun_out/fetch_cal.json", "w"), indent=1)
 PY
