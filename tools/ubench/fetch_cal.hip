@@ -5,6 +5,8 @@
 //   k_stream16   16 B per lane, coalesced, the whole buffer               (bytes = 2 GiB)
 //   k_scatter1   1 B per lane at a distinct 128-B line (a permutation)    (lines = 16 Mi)
 //   k_scatter8   8 B per lane at a distinct 128-B line                    (lines = 16 Mi)
+//   k_scatter2   1 B in each 64-B half of a distinct 128-B line           (lines = 16 Mi)
+//                (against k_scatter1: does a byte load fetch the line or its 64-B half?)
 //   k_lane8      8 B per lane, lane i reading line-sequentially its own 64 KiB span
 //                (k_dfl_parse's lane-per-stream record walk)            (bytes = 2 GiB)
 //   k_lane16     16 B per lane, the same per-lane spans (k_inflate_decode's input refills)
@@ -44,6 +46,12 @@ __global__ void k_scatter8(const uint64_t* __restrict__ a, uint32_t* out) {
         acc += a[perm(i) * 16 + (i & 15)];
     if (acc == 0x12345678u) out[0] = (uint32_t)acc;
 }
+__global__ void k_scatter2(const uint8_t* __restrict__ a, uint32_t* out) {
+    uint32_t acc = 0;
+    for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < kLines; i += (uint64_t)gridDim.x * 256)
+        acc += a[perm(i) * 128 + (i & 63)] + a[perm(i) * 128 + 64 + (i & 63)];
+    if (acc == 0x12345678u) out[0] = acc;
+}
 // 32 Ki lanes, each walking its own 64 KiB span 8 bytes at a time
 __global__ void k_lane8(const uint64_t* __restrict__ a, uint32_t* out) {
     const uint64_t lane = blockIdx.x * 256ull + threadIdx.x;
@@ -76,8 +84,8 @@ int main(int argc, char** argv) {
         hipEvent_t e0, e1;
         (void)hipEventCreate(&e0);
         (void)hipEventCreate(&e1);
-        const char* names[5] = {"stream16", "scatter1", "scatter8", "lane8", "lane16"};
-        for (int k = 0; k < 5; ++k) {
+        const char* names[6] = {"stream16", "scatter1", "scatter8", "lane8", "lane16", "scatter2"};
+        for (int k = 0; k < 6; ++k) {
             float best = 1e30f;
             for (int r = 0; r < 5; ++r) {
                 (void)hipEventRecord(e0, 0);
@@ -86,6 +94,7 @@ int main(int argc, char** argv) {
                 if (k == 2) hipLaunchKernelGGL(k_scatter8, dim3(4096), dim3(256), 0, 0, (const uint64_t*)a, out);
                 if (k == 3) hipLaunchKernelGGL(k_lane8, dim3(lanes / 256), dim3(256), 0, 0, (const uint64_t*)a, out);
                 if (k == 4) hipLaunchKernelGGL(k_lane16, dim3(lanes / 256), dim3(256), 0, 0, (const uint4*)a, out);
+                if (k == 5) hipLaunchKernelGGL(k_scatter2, dim3(4096), dim3(256), 0, 0, a, out);
                 (void)hipEventRecord(e1, 0);
                 if (hipEventSynchronize(e1) != hipSuccess) return 1;
                 float ms = 0;
@@ -99,6 +108,7 @@ int main(int argc, char** argv) {
     hipLaunchKernelGGL(k_stream16, dim3(4096), dim3(256), 0, 0, (const uint4*)a, out);
     hipLaunchKernelGGL(k_scatter1, dim3(4096), dim3(256), 0, 0, a, out);
     hipLaunchKernelGGL(k_scatter8, dim3(4096), dim3(256), 0, 0, (const uint64_t*)a, out);
+    hipLaunchKernelGGL(k_scatter2, dim3(4096), dim3(256), 0, 0, a, out);
     hipLaunchKernelGGL(k_lane8, dim3(lanes / 256), dim3(256), 0, 0, (const uint64_t*)a, out);
     hipLaunchKernelGGL(k_lane16, dim3(lanes / 256), dim3(256), 0, 0, (const uint4*)a, out);
     hipLaunchKernelGGL(k_store8, dim3(lanes / 256), dim3(256), 0, 0, (uint64_t*)a);

@@ -14,6 +14,7 @@ python3 - <<'PY' | tee gpurun_out/fetch_cal.txt
 import csv, glob
 import json
 known = {"k_stream16": 2 << 30, "k_scatter1": (2 << 30) // 128 * 128, "k_scatter8": (2 << 30) // 128 * 128,
+         "k_scatter2": (2 << 30) // 128 * 128,
          "k_lane8": 2 << 30, "k_lane16": 2 << 30, "k_store8": 2 << 30}
 res = {}
 for c, d in (("FETCH_SIZE", "f"), ("WRITE_SIZE", "w")):
