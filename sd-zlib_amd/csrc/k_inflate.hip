@@ -1759,8 +1759,11 @@ __device__ __noinline__ int wd_iteration(DSave* S, const uint8_t* inp, uint64_t 
 // alternates the two until no stream needs block-level work in this round.
 // first: the round's first launch (round 0: starts the streams; later rounds: resumes the streams
 // whose token ring filled).  A.flags: 2 = not live this round (finished earlier), else 0 until
-// k_inflate_wdec records the round's end.
-__global__ __launch_bounds__(IL_THREADS, 1) void k_inflate_wcold(InflateArgs A, uint32_t round, uint32_t first) {
+// k_inflate_wdec records the round's end.  lane: after kWdLaneAfter alternations (a stream of many
+// small blocks costs one launch pair per block) the lane decoder's whole loop (cold_run and
+// hot_epoch, as in k_inflate_decode) finishes the stream's round here.
+__global__ __launch_bounds__(IL_THREADS, 1) void k_inflate_wcold(InflateArgs A, uint32_t round, uint32_t first,
+                                                                  uint32_t lane) {
     uint8_t* region = lane_region();
     uint32_t* ts = lane_stage();
     const uint32_t gid = blockIdx.x * IL_STREAMS + lane_slot();
@@ -1799,7 +1802,8 @@ __global__ __launch_bounds__(IL_THREADS, 1) void k_inflate_wcold(InflateArgs A, 
         const uint32_t nt = S->ntok, b = nt & ~(IL_TSTAGE - 1u);   // the open 32-token line
         for (uint32_t q = b; q < nt; ++q) ts[q - b] = tb[q];
     }
-    cold_run<0>(S, inp, ilen, cap, tb, tcap, lens, A.format, A.dict != nullptr, did, init, G, force_slow);
+    if (lane && !init) epochs<0>(A, S, inp, ilen, cap, tb, tcap, lens, true, G);
+    else cold_run<0>(S, inp, ilen, cap, tb, tcap, lens, A.format, A.dict != nullptr, did, init, G, force_slow);
     Core H;                                              // flush the token stage
     H.tb = tb; H.ts = ts; H.ntok = S->ntok; H.litw = S->litw; H.nlit = S->nlit;
     tok_finish(H);
@@ -1932,6 +1936,8 @@ int run_inflate_rounds(const InflateArgs& a, hipStream_t s, uint32_t* host_activ
     // the wave decoder (k_inflate_wdec) for one-shot batches; the lane decoder keeps the
     // incremental mode (and the block-parallel split of long streams, off with the wave decoder)
     const bool use_wd = a.wave && a.wdprov && !a.streaming && !a.segmode && !a.split_plan;
+    uint32_t lane_after = kWdLaneAfter;                  // SDZ_WD_LANE_AFTER: development / tests
+    if (const char* e = getenv("SDZ_WD_LANE_AFTER")) lane_after = (uint32_t)strtoul(e, nullptr, 10);
     for (uint32_t round = 0;; ++round) {
         if (hipMemsetAsync(a.active, 0, sizeof(uint32_t), s) != hipSuccess) { rc = -1; break; }
         if (kernel_ms) (void)hipEventRecord(ev[0], s);
@@ -1939,12 +1945,18 @@ int run_inflate_rounds(const InflateArgs& a, hipStream_t s, uint32_t* host_activ
             // block-level work (a lane per stream) and the blocks' symbols (a wave per stream),
             // alternately, until no stream of this round needs block-level work
             for (uint32_t it = 0;; ++it) {
-                hipLaunchKernelGGL(k_inflate_wcold, g1, dim3(IL_THREADS), 0, s, a, round, it == 0 ? 1u : 0u);
+                hipLaunchKernelGGL(k_inflate_wcold, g1, dim3(IL_THREADS), 0, s, a, round, it == 0 ? 1u : 0u,
+                                   it >= lane_after ? 1u : 0u);
                 if (hipMemsetAsync(a.active, 0, 2 * sizeof(uint32_t), s) != hipSuccess) { rc = -1; break; }
                 hipLaunchKernelGGL(k_inflate_wdec, dim3(a.n), dim3(64), 0, s, a, round);
                 if (hipMemcpyAsync(host_active, a.active + 1, sizeof(uint32_t), hipMemcpyDeviceToHost, s) != hipSuccess ||
                     hipStreamSynchronize(s) != hipSuccess) { rc = -1; break; }
                 if (*host_active == 0) break;
+                // a stream of many small blocks costs a launch pair per block here: the first
+                // round starts over on the lane decoder with the block-parallel split (nothing
+                // is resolved yet); later rounds hand the rest to the lane decoder in
+                // k_inflate_wcold
+                if (round == 0 && it + 1 >= lane_after) { rc = kWdRestart; break; }
             }
             if (rc) break;
         } else {

@@ -77,6 +77,10 @@ uint64_t inflate_dsave_bytes();  // per stream decode state
 constexpr uint32_t kWdAutoStreams = 8192;
 constexpr uint64_t kWdAutoBytes = 4ull << 20;
 constexpr uint64_t kWdAutoMinBytes = 16ull << 10;
+// wave decoder: alternations of k_inflate_wcold / k_inflate_wdec per round before the lane decoder
+// finishes the round's remaining streams (one alternation per block otherwise)
+constexpr uint32_t kWdLaneAfter = 16;
+constexpr int kWdRestart = 1000;   // run_inflate_rounds: start the call over without the wave decoder
 int inflate_wdec_mode();         // SDZ_WDEC: -1 unset, 0 off, 1 on
 bool inflate_wave_policy(uint32_t n, const uint64_t* host_len, const uint64_t* dev_len, void* stream);
 uint64_t inflate_rsave_bytes();  // per stream resolve state

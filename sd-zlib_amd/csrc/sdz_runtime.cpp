@@ -660,6 +660,11 @@ int rt::inflate_batch_device(const uint8_t* in, const uint64_t* in_off, const ui
             one = host_cap[i] + 16 <= a.round_tokens && host_len[i] <= (1ull << 28);
         a.one_round = one ? 1u : 0u;
     }
+    if (a.wave) {
+        const int rw = inflate_run(a, s, false, nullptr, nullptr);
+        if (rw != kWdRestart) return rw;
+        a.wave = 0;                                       // many small blocks: lane decoder + split
+    }
     PoolUse find_use(g_find, s);
     SplitHost sh;
     if (int rc = inflate_split_start(a, s, find_use, sh)) return rc;

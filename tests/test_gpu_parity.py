@@ -272,6 +272,22 @@ def test_stored_blocks_decode_correctly():
             assert g["success"]
 
 
+def test_many_small_blocks(paradise):
+    """A stream flushed every 256 bytes (~940 dynamic and empty stored blocks): the wave decoder
+    alternates its two kernels once per block, then hands the rest of the round to the lane
+    decoder (kWdLaneAfter); ground truth = input."""
+    data = paradise[:240000]
+    for wbits in (15, -15, 31):
+        c = zlib.compressobj(6, zlib.DEFLATED, wbits)
+        comp = b"".join(c.compress(data[i:i + 256]) + c.flush(zlib.Z_SYNC_FLUSH) for i in range(0, len(data), 256))
+        comp += c.flush()
+        g = run_container([comp, comp[: len(comp) // 2]], raw=wbits < 0)
+        assert g[0]["status"] == "OK" and g[0]["data"] == data, wbits
+        if wbits > 0:
+            assert g[0]["success"]
+        assert g[1]["status"] != "OK"                         # truncated half: no success
+
+
 def test_trailing_bytes_reported():
     comp = golden("simple.deflate") + b"\x00\x01"
     g = run_container([comp])[0]
