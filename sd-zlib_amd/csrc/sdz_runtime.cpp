@@ -379,7 +379,7 @@ uint64_t split_threshold(std::vector<uint64_t> len, uint64_t split_min) {
     for (size_t k = n; k-- > 0;) {                       // split streams k .. n-1 (t = len[k])
         suffix += (double)len[k];
         if (len[k] < split_min) break;
-        if (k + 1 < n && len[k] == len[k + 1]) continue;  // (equal sizes split together)
+        if (k > 0 && len[k - 1] == len[k]) continue;      // equal sizes split together: at the run's first
         const double unsplit = k ? (double)len[k - 1] / r_lane : 0.0;
         const double t = suffix / r_find + std::max(std::max(unsplit, seg_max / r_lane), floor_t);
         if (t < best) { best = t; thr = len[k]; }

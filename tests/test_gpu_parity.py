@@ -286,6 +286,9 @@ def test_many_small_blocks(paradise):
         if wbits > 0:
             assert g[0]["success"]
         assert g[1]["status"] != "OK"                         # truncated half: no success
+    # equal streams: the block-parallel split takes all of them (lane path) or none
+    g = run_container([comp] * 16)
+    assert all(x["status"] == "OK" and x["data"] == data and x["success"] for x in g)
 
 
 def test_trailing_bytes_reported():
