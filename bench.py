@@ -403,8 +403,9 @@ def node_facade():
 
 def small_batch_leg(sdz, L, comp, text, n, steps):
     """A small batch (n copies of C2's stream): the wave decoder (a wave per stream, picked by
-    inflate_wave_policy for <= 8192 streams of 16 KiB - 4 MiB) against the lane decoder
-    (SDZ_WDEC=0: a lane per stream, its time the longest stream's serial decode); kernel ms."""
+    inflate_wave_policy for <= 8192 streams of 16 KiB - 4 MiB) against the lane path
+    (SDZ_WDEC=0: a lane per stream, its time the longest stream's serial decode, or the
+    block-parallel split of the streams where its cost model picks it); kernel ms."""
     b = DeviceBatch(sdz, comp, n, len(text) + 64)
     res = {"streams": n, "bytes_out": n * len(text)}
     try:
