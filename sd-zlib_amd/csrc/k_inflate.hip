@@ -1914,9 +1914,9 @@ bool inflate_wave_policy(uint32_t n, const uint64_t* host_len, const uint64_t* d
             return false;
         host_len = len.data();
     }
-    uint64_t mx = 0;
-    for (uint32_t i = 0; i < n; ++i) mx = host_len[i] > mx ? host_len[i] : mx;
-    return mx >= kWdAutoMinBytes && mx <= kWdAutoBytes;
+    uint64_t mx = 0, tot = 0;
+    for (uint32_t i = 0; i < n; ++i) { mx = host_len[i] > mx ? host_len[i] : mx; tot += host_len[i]; }
+    return mx >= kWdAutoMinBytes && mx <= kWdAutoBytes && tot <= kWdAutoRatio * mx;
 }
 uint64_t inflate_rsave_bytes() { return sizeof(RSave); }
 

@@ -69,12 +69,16 @@ struct InflateArgs {
 
 uint64_t inflate_dsave_bytes();  // per stream decode state
 // one-shot batches: decode with the wave decoder (k_inflate_wdec, a wave per stream) rather than the
-// lane decoder (k_inflate_decode, a lane per stream)?  SDZ_WDEC=1 / 0 forces it; by default for
-// batches of at most kWdAutoStreams streams of at most kWdAutoBytes compressed bytes each (the lane
-// decoder's time is its longest stream's serial decode, the wave decoder's the batch's total), when
-// the longest is at least kWdAutoMinBytes (shorter ones decode in a few lane steps, and the lane
-// decoder's single decode + resolve launch keeps small calls' latency)
-constexpr uint32_t kWdAutoStreams = 8192;
+// lane decoder (k_inflate_decode, a lane per stream)?  SDZ_WDEC=1 / 0 forces it.  By default when
+// the batch's compressed bytes are at most kWdAutoRatio times its longest stream's (the lane
+// decoder's time is its longest stream's serial decode, ~3.7 MB/s per lane; the wave decoder's the
+// batch's total at ~133 GB/s: equal at ~36,000 equal streams, measured crossover 32,768 on
+// paradiselost copies and on distinct 64 KiB streams, tools/wdec_sweep.sh), for at most
+// kWdAutoStreams streams of at most kWdAutoBytes each, and when the longest is at least
+// kWdAutoMinBytes (shorter ones decode in a few lane steps, and the lane decoder's single decode +
+// resolve launch keeps small calls' latency)
+constexpr uint32_t kWdAutoStreams = 65536;
+constexpr uint64_t kWdAutoRatio = 24576;
 constexpr uint64_t kWdAutoBytes = 4ull << 20;
 constexpr uint64_t kWdAutoMinBytes = 16ull << 10;
 // wave decoder: alternations of k_inflate_wcold / k_inflate_wdec per round before the lane decoder

@@ -1,7 +1,7 @@
 """The inflate parity tests of test_gpu_parity.py again, with the wave decoder forced
-(SDZ_WDEC=1).  By default it serves batches of at most 8,192 streams whose longest
-stream is 16 KiB - 4 MiB of compressed input, so most of the suite's small batches would not reach
-it: here every one-shot batch does -- errors and their messages, need-bits stalls at the end of the
+(SDZ_WDEC=1).  By default it serves batches whose total is at most 24,576 times
+their longest stream, of 16 KiB - 4 MiB of compressed input, so most of the suite's small batches
+would not reach it: here every one-shot batch does -- errors and their messages, need-bits stalls at the end of the
 input, dictionaries, stored blocks, trailing bytes, output slots at the edge, many rounds -- against
 the same oracle and ground truth."""
 import pytest
