@@ -422,13 +422,29 @@ __device__ __forceinline__ void finish_tree(Tree& T, const uint32_t (&hs)[5]) {
     T.pk[16] = ((uint32_t)(IL_BAD_IDX + 32768) << 16) | 15u;   // threshold 0: never a literal
 }
 
+// f(s, lens[s]) for s in [0, n), the lengths read 16 at a time: a lane's byte loads from its HBM
+// scratch each waited a round trip (a dynamic header's two passes over ~300 lengths: ~130 us of a
+// block's block-level work).  The scratch is 16-byte aligned and kInflateScratchPerStream (320) a
+// multiple of 16, so the aligned chunks around [lens, lens + n) stay inside the stream's scratch.
+template <class F>
+__device__ __forceinline__ void for_lens(const uint8_t* lens, int n, F f) {
+    const uintptr_t a = (uintptr_t)lens, a0 = a & ~(uintptr_t)15;
+    const int lead = (int)(a - a0);
+    for (int b = 0; b < n + lead; b += 16) {
+        const uint4 w = *(const uint4*)(a0 + (uintptr_t)b);
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            const uint32_t wj = j < 4 ? w.x : j < 8 ? w.y : j < 12 ? w.z : w.w;
+            const int s = b + j - lead;
+            if (s >= 0 && s < n) f(s, (int)((wj >> (8 * (j & 3))) & 255u));
+        }
+    }
+}
+
 // counts + Kraft remainder for n lengths read from global memory
 __device__ __forceinline__ void count_lens(Tree& T, const uint8_t* lens, int n, int root) {
     T.c[0] = T.c[1] = T.c[2] = T.c[3] = T.c[4] = 0;
-    for (int s = 0; s < n; ++s) {
-        int len = lens[s];
-        if (len) cnt_add(T.c, len, 1u);
-    }
+    for_lens(lens, n, [&](int, int len) { if (len) cnt_add(T.c, len, 1u); });
     int left = 1, kmin = 16, g = 0;
 #pragma unroll
     for (int L = 1; L <= 15; ++L) {
@@ -453,15 +469,14 @@ __device__ __forceinline__ void place_syms(const Tree& T, const uint8_t* lens, i
 #pragma unroll
     for (int L = 1; L <= 15; ++L) { cnt_add(nx, L, idx); idx += cnt_get(T.c, L); }
     int nlit = n < 256 ? n : 256;
-    for (int s = 0; s < nlit; ++s) {
-        int len = lens[s];
+    for_lens(lens, nlit, [&](int s, int len) {
         if (len) { out[cnt_get(nx, len)] = (uint8_t)s; cnt_add(nx, len, 1u); }
-    }
+    });
     hs[0] = nx[0]; hs[1] = nx[1]; hs[2] = nx[2]; hs[3] = nx[3]; hs[4] = nx[4];
-    for (int s = nlit; s < n; ++s) {
-        int len = lens[s];
-        if (len) { out[cnt_get(nx, len)] = (uint8_t)(s - 256); cnt_add(nx, len, 1u); }
-    }
+    if (n > nlit)
+        for_lens(lens + nlit, n - nlit, [&](int s, int len) {
+            if (len) { out[cnt_get(nx, len)] = (uint8_t)s; cnt_add(nx, len, 1u); }   // s = symbol - 256
+        });
 }
 
 // upper bound on the entries huft_build allocates for these counts (dummies included)
