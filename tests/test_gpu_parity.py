@@ -291,6 +291,22 @@ def test_many_small_blocks(paradise):
     assert all(x["status"] == "OK" and x["data"] == data and x["success"] for x in g)
 
 
+def test_many_small_blocks_later_rounds(monkeypatch, paradise):
+    """Big blocks first, then a block per 256 bytes, with token rounds of 8,192: the many-block part
+    falls into a later round, where the wave decoder hands the stream to the lane decoder's loop
+    (k_inflate_wcold) rather than starting over; ground truth and the oracle."""
+    monkeypatch.setenv("SDZ_ROUND_TOKENS", "8192")
+    data = paradise[:200000]
+    c = zlib.compressobj(6)
+    comp = c.compress(data[:80000])
+    comp += b"".join(c.compress(data[i:i + 256]) + c.flush(zlib.Z_SYNC_FLUSH) for i in range(80000, len(data), 256))
+    comp += c.flush()
+    g = run_container([comp, zlib.compress(paradise, 6)])
+    assert g[0]["status"] == "OK" and g[0]["data"] == data and g[0]["success"]
+    assert g[1]["status"] == "OK" and g[1]["data"] == paradise and g[1]["success"]
+    assert_same(g[0], O.inflater_run([comp]), comp)
+
+
 def test_trailing_bytes_reported():
     comp = golden("simple.deflate") + b"\x00\x01"
     g = run_container([comp])[0]

@@ -17,6 +17,7 @@ from test_gpu_parity import (  # noqa: F401  (collected here a second time, unde
     test_inflate_oracle_generated,
     test_inflate_zlib_generated,
     test_many_small_blocks,
+    test_many_small_blocks_later_rounds,
     test_output_slot_edges,
     test_raw_need_bits_at_end_of_input,
     test_repetitive_data_long_match_chains,
