@@ -1032,6 +1032,19 @@ __device__ __forceinline__ bool seg_is_cand(const SegStop& G, uint64_t bit) {
     return lo < G.ncand && G.cand[lo] == bit;
 }
 
+// n dwords src -> dst by one lane, 16 loads in flight: the lane-serial copies of a stream's symbol
+// region and open token line between HBM and LDS waited one round trip per dword (~50 us of
+// every k_inflate_wcold launch)
+__device__ __forceinline__ void copy_dw(uint32_t* dst, const uint32_t* src, uint32_t n) {
+    for (uint32_t k = 0; k < n; k += 16) {
+        uint32_t v[16];
+#pragma unroll
+        for (uint32_t j = 0; j < 16; ++j) v[j] = k + j < n ? src[k + j] : 0u;
+#pragma unroll
+        for (uint32_t j = 0; j < 16; ++j)
+            if (k + j < n) dst[k + j] = v[j];
+    }
+}
 __shared__ __attribute__((aligned(16))) uint8_t wd_region[IL_REGION];   // the wave decoder's symbol bytes
 __shared__ Tree wd_LL, wd_DD;                     // ... and trees (from the stream's state)
 // force_slow: decode the current block's symbols with the exact slow step to its end (the wave
@@ -1267,7 +1280,7 @@ __global__ __launch_bounds__(IL_THREADS, 1) void k_inflate_decode(InflateArgs A,
                              A.dict != nullptr, dict_id_of(A.dict_adler, A.dict_adler_dev), 1u, G);
         } else if (S->mode != LM_DONE && !(round > 0 && S->stall)) {
             live = true;
-            for (int k = 0; k < IL_REGION / 4; ++k) ((uint32_t*)region)[k] = ((const uint32_t*)S->region)[k];
+            copy_dw((uint32_t*)region, (const uint32_t*)S->region, IL_REGION / 4);
             S->ntok = 0; S->full = 0;
             if (round == 0) { S->pos = 0; S->stall = 0; }      // a new call: fresh output slot
         }
@@ -1297,7 +1310,7 @@ __global__ __launch_bounds__(IL_THREADS, 1) void k_inflate_decode(InflateArgs A,
     // segment: handed over or reached the trailer)
     A.flags[sid] = S->mode == LM_DONE ? 1u : S->stall ? 3u : 0u;
     if (S->mode != LM_DONE && !A.segmode)
-        for (int k = 0; k < IL_REGION / 4; ++k) ((uint32_t*)S->region)[k] = ((const uint32_t*)region)[k];
+        copy_dw((uint32_t*)S->region, (const uint32_t*)region, IL_REGION / 4);
 }
 
 // ------------------------------------------------------------------ wave decoder
@@ -1813,9 +1826,9 @@ __global__ __launch_bounds__(IL_THREADS, 1) void k_inflate_wcold(InflateArgs A, 
         force_slow = S->mode == LM_CODES ? 1 : 0;        // the wave declined the rest of this block
     }
     if (!init) {
-        for (int k = 0; k < IL_REGION / 4; ++k) ((uint32_t*)region)[k] = ((const uint32_t*)S->region)[k];
+        copy_dw((uint32_t*)region, (const uint32_t*)S->region, IL_REGION / 4);
         const uint32_t nt = S->ntok, b = nt & ~(IL_TSTAGE - 1u);   // the open 32-token line
-        for (uint32_t q = b; q < nt; ++q) ts[q - b] = tb[q];
+        copy_dw(ts, tb + b, nt - b);
     }
     if (lane && !init) epochs<0>(A, S, inp, ilen, cap, tb, tcap, lens, true, G);
     else cold_run<0>(S, inp, ilen, cap, tb, tcap, lens, A.format, A.dict != nullptr, did, init, G, force_slow);
@@ -1824,7 +1837,7 @@ __global__ __launch_bounds__(IL_THREADS, 1) void k_inflate_wcold(InflateArgs A, 
     tok_finish(H);
     S->ntok = H.ntok; S->litw = 0; S->nlit = 0;
     if (S->mode == LM_CODES)
-        for (int k = 0; k < IL_REGION / 4; ++k) ((uint32_t*)S->region)[k] = ((const uint32_t*)region)[k];
+        copy_dw((uint32_t*)S->region, (const uint32_t*)region, IL_REGION / 4);
 }
 
 // One WAVE per stream: the current block's symbols by speculative iterations, until the block
