@@ -32,5 +32,5 @@ timeout -k 10 700 rocprofv3 --kernel-trace --stats -d gpurun_out/r04/bench_kt -o
 step configs
 timeout -k 10 300 python3 tools/run_configs.py --config c5 > gpurun_out/r04/c5.json 2> gpurun_out/r04/c5.err || exit 1
 timeout -k 10 300 python3 tools/run_configs.py --config c4 --scale 8 > gpurun_out/r04/c4.json 2> gpurun_out/r04/c4.err || exit 1
-tail -3 gpurun_out/r04/c5.json gpurun_out/r04/c4.json
+tail -n 3 gpurun_out/r04/c5.json gpurun_out/r04/c4.json
 exit 0
