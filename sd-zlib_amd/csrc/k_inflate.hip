@@ -1336,7 +1336,7 @@ __global__ __launch_bounds__(IL_THREADS, 1) void k_inflate_decode(InflateArgs A,
 // Everything that is not the symbol loop of a Huffman block -- container header, block
 // headers and trees, stored blocks, trailer, the last input bits, and the exact handling of
 // errors and output room (a room overflow or an ERR hands the block to the slow step from
-// the iteration's start) -- is cold_run<0, WD> on lane 0.
+// the iteration's start) -- is cold_run<0> in k_inflate_wcold, a lane per stream.
 // Decoding uses two-level lookup tables in LDS (root 10 / 8 bits, built from the canonical
 // trees by the whole wave) instead of the lane-per-stream decoder's table-free registers: a
 // wave holds one stream, and its latency is hidden by the other waves on the SIMD.
@@ -1348,10 +1348,12 @@ __global__ __launch_bounds__(IL_THREADS, 1) void k_inflate_decode(InflateArgs A,
 #ifndef WD_CAP
 #define WD_CAP 512                // provisional tokens per lane and iteration
 #endif
+#ifndef WD_LLR
 #define WD_LLR 10                 // root bits of the literal/length table
 #define WD_DR 8                   // ... of the distance table
 #define WD_LLT 1536               // table entries (root + subtables)
 #define WD_DT 736                 // (6 waves per CU: the LDS total stays below 160 KiB / 6)
+#endif
 #ifndef WD_CMAX
 #define WD_CMAX 4096              // chunk bits
 #endif
