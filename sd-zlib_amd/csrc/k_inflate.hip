@@ -1050,7 +1050,16 @@ __shared__ Tree wd_LL, wd_DD;                     // ... and trees (from the str
 // force_slow: decode the current block's symbols with the exact slow step to its end (the wave
 // decoder's hand-back for errors, output room, tables past its LDS budget and the last input bits)
 template <int MODE>
-__device__ __noinline__ void cold_run(DSave* S, const uint8_t* inp, uint64_t ilen, uint64_t cap,
+// inlined into its callers (k_inflate_decode's epochs, k_inflate_wcold): as a call it saved and
+// restored ~180 VGPRs through scratch around every block-level step (832 B of scratch per lane);
+// inlined, C2 decode 52.2 -> 51.5 ms and the 1,024-stream wave batch 3.19 -> 3.08 ms
+// (tools/dbg/wdec_variant.sh).  IL_COLD_NOINLINE restores the call.
+#ifdef IL_COLD_NOINLINE
+#define IL_COLD_ATTR __noinline__
+#else
+#define IL_COLD_ATTR __forceinline__
+#endif
+__device__ IL_COLD_ATTR void cold_run(DSave* S, const uint8_t* inp, uint64_t ilen, uint64_t cap,
                                       uint32_t* tb, uint32_t tcap, uint8_t* lens, int32_t format, int32_t has_dict,
                                       int32_t dict_adler, uint32_t init, SegStop G, int force_slow = 0) {
     Lane L;
