@@ -37,7 +37,9 @@ namespace sdz {
 #endif
 #define IL_STREAMS 256
 #ifndef IL_STOP_SHIFT
-#define IL_STOP_SHIFT 1               // a hot epoch ends once half its lanes need block-level work
+#define IL_STOP_SHIFT 0               // a hot epoch runs until every lane needs block-level work
+                                      // (since cold_run is inlined: distinct decode 11.25 -> 11.09 ms;
+                                      // 1, half the lanes, and 2, a quarter: 11.25 / 11.41 ms; C2 equal)
                                       // (1/8: 4 % slower on distinct streams, C2 equal)
 #endif
 #define IL_THREADS (IL_STREAMS * 64 / IL_WAVE_LANES)
