@@ -1297,8 +1297,8 @@ __global__ __launch_bounds__(IL_THREADS, 1) void k_inflate_decode(InflateArgs A,
         }
     }
     // epochs: lanes that need block-level work do it together (cold_run), then
-    // every lane that can decodes symbols with register-resident state until an
-    // eighth of them has left the fast path; state is parked in DSave in between
+    // every lane that can decodes symbols with register-resident state until all of them
+    // have left the fast path (IL_STOP_SHIFT); state is parked in DSave in between
     if (A.streaming) epochs<1>(A, S, inp, ilen, cap, tb, tcap, lens, live, G);
     else if (A.segmode) epochs<2>(A, S, inp, ilen, cap, tb, tcap, lens, live, G);
     else epochs<0>(A, S, inp, ilen, cap, tb, tcap, lens, live, G);
