@@ -369,19 +369,42 @@ def cpu_threads():
     return max(1, min(avail, int(share))) if share and share.isdigit() else max(1, avail), avail
 
 
+def cgroup_cpu_limit():
+    """The CPU quota of this process's cgroup (cgroup v2 cpu.max: "quota period", or "max"), as
+    CPUs, or None when there is none: it caps what any number of threads can measure."""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        return None if q == "max" else round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        return None
+
+
 def cpu_baseline(work_one, seconds, unit_bytes_fn, sample):
-    """all-threads and one-thread runs of the same work; value in MB/s of unit_bytes_fn"""
+    """The same work on the box's CPU share for one GPU (value), on one thread (per core), and on
+    every core this process may run on (all_cores_measured_MBps: SURVEY §8(d)'s pool over all host
+    cores, measured, beside the per-core x nproc extrapolation); MB/s of unit_bytes_fn"""
     threads, avail = cpu_threads()
     cnt, nb, dt = cpu_run(work_one, seconds, threads)
     c1, nb1, d1 = cpu_run(work_one, max(0.5, seconds / 2), 1)
     per_core = unit_bytes_fn(c1, nb1) / d1 / 1e6
     nproc = os.cpu_count() or 1
+    if avail > threads:
+        ca, nba, da = cpu_run(work_one, max(1.0, seconds / 2), avail)
+        all_meas = unit_bytes_fn(ca, nba) / da / 1e6
+    else:
+        ca, da, all_meas = cnt, dt, unit_bytes_fn(cnt, nb) / dt / 1e6
+    quota = cgroup_cpu_limit()
     return {"value": round(unit_bytes_fn(cnt, nb) / dt / 1e6, 2), "unit": "MB/s", "cores": threads, "kind": "port",
             "per_core_MBps": round(per_core, 2), "nproc": nproc, "affinity_cores": avail,
+            "all_cores_measured_MBps": round(all_meas, 1), "all_cores_threads": max(avail, threads),
+            "cgroup_cpu_quota": quota,
             "all_cores_linear_MBps": round(per_core * nproc, 1),
-            "sample": "%s: %d units on %d threads in %.1f s; per core: %d in %.1f s on 1 thread; threads = the "
-                      "box's CPU share for one GPU (OMP_NUM_THREADS) of nproc %d; all_cores_linear_MBps = per-core "
-                      "x nproc, the machine-wide ceiling" % (sample, cnt, threads, dt, c1, d1, nproc)}
+            "sample": "%s: %d units on %d threads in %.1f s; per core: %d in %.1f s on 1 thread; all cores: %d in "
+                      "%.1f s on %d threads (every CPU in this process's affinity mask; cgroup quota %s CPUs); "
+                      "threads = the box's CPU share for one GPU (OMP_NUM_THREADS) of nproc %d; "
+                      "all_cores_linear_MBps = per-core x nproc, the machine-wide ceiling"
+                      % (sample, cnt, threads, dt, c1, d1, ca, da, max(avail, threads), quota, nproc)}
 
 
 def node_facade():
@@ -403,7 +426,8 @@ def node_facade():
 
 def small_batch_leg(sdz, L, comp, text, n, steps):
     """A small batch (n copies of C2's stream): the wave decoder (a wave per stream, picked by
-    inflate_wave_policy for <= 8192 streams of 16 KiB - 4 MiB) against the lane path
+    inflate_wave_policy for batches of at most 65,536 streams whose longest is 16 KiB - 4 MiB of
+    input and whose total is at most 24,576 times the longest) against the lane path
     (SDZ_WDEC=0: a lane per stream, its time the longest stream's serial decode, or the
     block-parallel split of the streams where its cost model picks it); kernel ms."""
     b = DeviceBatch(sdz, comp, n, len(text) + 64)

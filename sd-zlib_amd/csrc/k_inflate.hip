@@ -106,7 +106,24 @@ struct Hot : Core {
     g_uint4* vp;                      // next 16 input bytes to load
     g_uint4* vend;                    // first 16-byte chunk past the input
     uint32_t* ring;
+#ifdef IL_HOT_CHECK
+    // development: the readable input span and the stream, for bounds checks
+    const uint8_t* chk_lo;
+    const uint8_t* chk_hi;
+    uint32_t chk_id;
+#endif
 };
+#ifdef IL_HOT_CHECK
+// a hot-path access outside its bounds: reported once per lane, the access skipped and the
+// lane stopped (status BAD_RECORD), so the run ends without a fault
+#define HOT_CHECK(L, cond, what, a, b)                                                            \
+    (!(cond) ? (printf("IL_HOT_CHECK %s stream %u lane %u: %llx %llx lo %llx hi %llx\n", what,    \
+                       (L).chk_id, threadIdx.x, (unsigned long long)(a), (unsigned long long)(b),  \
+                       (unsigned long long)(L).chk_lo, (unsigned long long)(L).chk_hi),           \
+                (L).mode = LM_DONE, (L).status = SDZ_BAD_RECORD, (L).full = true, false) : true)
+#else
+#define HOT_CHECK(L, cond, what, a, b) true
+#endif
 // ... and the cold code: a plain reader plus the block-level state
 struct Lane : Core {
     const uint32_t* dp;               // next input dword
@@ -204,6 +221,8 @@ __device__ __forceinline__ void ring_step(Hot& L) {
     tok_flush_hot(L);
     uint32_t lvl = L.wpos - L.rpos;
     if (lvl <= 48 && L.vp < L.vend) {
+        if (!HOT_CHECK(L, (const uint8_t*)L.vp >= L.chk_lo && (const uint8_t*)(L.vp + 2) <= L.chk_hi, "ring load",
+                       (uintptr_t)L.vp, (uintptr_t)L.vend)) return;
         L.s0 = *L.vp++;
         L.ns = 1;
         if (lvl <= 32 && L.vp < L.vend) { L.s1 = *L.vp++; L.ns = 2; }
@@ -580,7 +599,8 @@ __device__ __forceinline__ void tok_flush_hot(Hot& L) {
     if (!IL_UNIFORM_FLUSH) return;
     const bool f = L.ntok - L.nfl >= 16u;
     if (__ballot(f)) {
-        if (f) {
+        if (f && HOT_CHECK(L, L.nfl + 16u <= L.tcap && L.nfl + 16u <= L.ntok && (L.nfl & 15u) == 0, "token flush",
+                           L.nfl, ((uint64_t)L.ntok << 32) | L.tcap)) {
             const uint2* st = (const uint2*)(L.ts + (L.nfl & (IL_TSTAGE - 1)));
             GLB uint4* d = (GLB uint4*)(L.tb + L.nfl);
             uint2 v[8];
@@ -1129,6 +1149,19 @@ __device__ IL_COLD_ATTR void cold_run(DSave* S, const uint8_t* inp, uint64_t ile
 
 __device__ __forceinline__ void hot_load(Hot& H, HTree& LL, HTree& DD, const DSave* S,
                                          const uint8_t* inp, uint64_t ilen, uint64_t cap) {
+#ifdef IL_HOT_CHECK
+    H.chk_lo = (const uint8_t*)((uintptr_t)inp & ~(uintptr_t)15);
+    H.chk_hi = inp + ilen + 64;                           // the batch's readable slack
+    H.chk_id = blockIdx.x * IL_STREAMS + lane_slot();
+    {
+        const uint8_t* a = (const uint8_t*)(((uintptr_t)(inp + (S->bitpos >> 3))) & ~(uintptr_t)15);
+        if (!HOT_CHECK(H, S->bitpos <= ilen * 8 && a >= H.chk_lo && a + 64 <= H.chk_hi + 16, "init load",
+                       S->bitpos, ilen)) {
+            H.mode = LM_DONE;
+            return;
+        }
+    }
+#endif
     br_init(H, inp, S->bitpos, ilen * 8, lane_ring());
     H.vend = (g_uint4*)(((uintptr_t)(inp + ilen) + 15) & ~(uintptr_t)15);
     H.pos0 = S->pos;
@@ -1165,16 +1198,37 @@ __device__ __forceinline__ bool can_hot(const DSave* S, uint64_t tbits, uint64_t
 
 // one epoch of the symbol loop: every lane with `hot` set decodes until no more
 // than `stop` lanes of the wave can continue.  Not inlined, so that its register
-// allocation is not shaped by the cold call in the caller's loop.
+// allocation is not shaped by the cold call in the caller's loop.  IL_HOT_INLINE inlines it
+// (development variant).
+#ifdef IL_HOT_INLINE
+#define IL_HOT_ATTR __forceinline__
+#else
+#define IL_HOT_ATTR __noinline__
+#endif
 template <bool STREAM>
-__device__ __noinline__ void hot_epoch(DSave* S, const uint8_t* inp, uint64_t ilen, uint64_t cap,
+__device__ IL_HOT_ATTR void hot_epoch(DSave* S, const uint8_t* inp, uint64_t ilen, uint64_t cap,
                                        uint32_t* tb, uint32_t tcap, bool hot, int stop) {
     Hot H;
     HTree LL, DD;
     const uint8_t* region = lane_region();
+    // lanes without a stream in this epoch: every field the loop body may touch is defined
+    // (mode DONE and full keep them out of the symbol steps; ring_step is not run for them)
     H.mode = LM_DONE; H.full = true; H.ntok = 0; H.nfl = 0; H.tcap = tcap; H.tb = tb; H.ts = lane_stage();
-    H.avail = 0; H.bo = 0;
+    H.avail = 0; H.bo = 0; H.avail0 = 0; H.base_bit = 0; H.room = H.room0 = 0; H.pos0 = 0;
+    H.last = 0; H.status = SDZ_OK; H.zmsg = 0; H.litw = 0; H.nlit = 0;
+    H.w0 = H.w1 = H.w2 = H.nx = 0; H.rpos = H.wpos = 0; H.ns = 0;
+    H.s0 = H.s1 = make_uint4(0u, 0u, 0u, 0u);
+    H.vp = H.vend = (g_uint4*)inp; H.ring = lane_ring();
+#ifdef IL_HOT_CHECK
+    H.chk_lo = H.chk_hi = nullptr; H.chk_id = ~0u;
+#endif
     if (hot) hot_load(H, LL, DD, S, inp, ilen, cap);
+    else {
+#pragma unroll
+        for (int k = 0; k < 16; ++k) { LL.lim[k] = DD.lim[k] = 0; }
+#pragma unroll
+        for (int k = 0; k < 17; ++k) { LL.pk[k] = DD.pk[k] = 0; }
+    }
 #if IL_BSEARCH
 #pragma unroll
     for (int k = 1; k <= 15; ++k) { LL.lim[k] -= 1u; DD.lim[k] -= 1u; }   // tsel_hot's form
@@ -1359,6 +1413,9 @@ __global__ __launch_bounds__(IL_THREADS, 1) void k_inflate_decode(InflateArgs A,
 #ifndef WD_CAP
 #define WD_CAP 512                // provisional tokens per lane and iteration
 #endif
+// the runtime sizes each stream's provisional slots (kWdProvTokens) for 64 lanes x WD_CAP tokens
+// plus one dummy slot per lane (the compaction's masked-off stores)
+static_assert(kWdProvTokens >= 64ull * WD_CAP + 64ull, "kWdProvTokens (sdz_internal.h) too small for WD_CAP");
 #ifndef WD_LLR
 #define WD_LLR 10                 // root bits of the literal/length table
 #define WD_DR 8                   // ... of the distance table
@@ -2052,6 +2109,13 @@ int run_inflate_rounds(const InflateArgs& a, hipStream_t s, uint32_t* host_activ
             kernel_ms[2] = t2;
         }
         if (hipGetLastError() != hipSuccess) rc = -1;
+    } else if (rc == kWdRestart && kernel_ms) {
+        // the wave attempt's time (the call starts over on the lane decoder) counts as decode
+        float t0 = 0.f;
+        (void)hipEventRecord(ev[1], s);
+        (void)hipEventSynchronize(ev[1]);
+        (void)hipEventElapsedTime(&t0, ev[0], ev[1]);
+        kernel_ms[0] = t0;
     }
     if (kernel_ms) for (auto& e : ev) (void)hipEventDestroy(e);
     return rc;

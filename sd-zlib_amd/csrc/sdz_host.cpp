@@ -310,7 +310,8 @@ int multi_batch(const uint8_t* const* in, const size_t* in_len, uint8_t* const* 
     std::vector<int> rcs(ndev, SDZ_API_OK);
     std::vector<std::string> errs(ndev);
     std::vector<uint8_t> gathered;                 // rank 0's all-gathered records (RCCL)
-    Barrier bar(ndev);
+    Barrier bar(ndev), bar2(ndev);
+    std::atomic<bool> coll_fail{false};            // some rank's collective failed: all stop waiting
     double t_compute = 0, t_gather0 = 0;
     std::mutex tmu;
     auto shard = [&](int k) {
@@ -343,6 +344,9 @@ int multi_batch(const uint8_t* const* in, const size_t* in_len, uint8_t* const* 
             std::lock_guard<std::mutex> lk(tmu);
             t_compute = std::max(t_compute, now_ms() - t0);
         }
+        // this rank's communicator, read while the cache entry is certainly alive (only a failed
+        // collective erases it, after the second barrier below)
+        ncclComm_t comm = rccl ? (*comms)[k] : nullptr;
         bar.wait();                                 // every shard computed (or failed) and holds its slot
         if (k == 0) t_gather0 = now_ms();
         bool any_fail = false;
@@ -350,19 +354,31 @@ int multi_batch(const uint8_t* const* in, const size_t* in_len, uint8_t* const* 
         if (any_fail || !rccl) return;              // no rank enqueues a collective
         // RCCL all-gather of the fixed-size records (max_m slots per shard), in place
         int r2 = SDZ_API_OK;
-        ncclResult_t nr = ncclAllGather(mine, g, slot_bytes, ncclUint8, (*comms)[k], nullptr);
+        // tests: SDZ_TEST_GATHER_FAIL=k makes rank k's collective fail without entering it (its
+        // peers are then inside a collective that cannot complete: the abort path)
+        const char* inj = getenv("SDZ_TEST_GATHER_FAIL");
+        ncclResult_t nr = inj && atoi(inj) == k ? ncclInternalError
+                                                : ncclAllGather(mine, g, slot_bytes, ncclUint8, comm, nullptr);
         if (nr != ncclSuccess) r2 = fail(SDZ_API_HIP_ERROR, std::string("ncclAllGather: ") + ncclGetErrorString(nr));
         if (r2 == SDZ_API_OK && k == 0) {
             gathered.resize((size_t)ndev * slot_bytes);
             if (hipMemcpyAsync(gathered.data(), g, gathered.size(), hipMemcpyDeviceToHost, nullptr) != hipSuccess)
                 r2 = fail(SDZ_API_HIP_ERROR, "records to host");
         }
-        if (r2 != SDZ_API_OK) {
-            // the other ranks are (or will be) inside the collective: abort it instead of waiting
-            comms_abort(devs);
-        } else if (hipStreamSynchronize(nullptr) != hipSuccess) {
-            r2 = fail(SDZ_API_HIP_ERROR, "gather sync");
+        if (r2 != SDZ_API_OK) coll_fail.store(true);
+        // wait for the collective, or for another rank's failure (its peers would wait forever on
+        // a collective one rank never entered): poll rather than block
+        while (r2 == SDZ_API_OK) {
+            const hipError_t q = hipStreamQuery(nullptr);
+            if (q == hipSuccess) break;
+            if (q != hipErrorNotReady) { r2 = hip_fail(q, "gather sync"); coll_fail.store(true); break; }
+            if (coll_fail.load()) { r2 = fail(SDZ_API_HIP_ERROR, "gather: another shard's collective failed"); break; }
+            std::this_thread::sleep_for(std::chrono::microseconds(20));
         }
+        // every rank has left the collective (done, failed, or given up); one of them aborts the
+        // communicators and drops them from the cache, none of the others touches them after this
+        bar2.wait();
+        if (k == 0 && coll_fail.load()) comms_abort(devs);
         if (r2) { rcs[k] = r2; errs[k] = sdz_last_error(); }
     };
     std::vector<std::thread> th;

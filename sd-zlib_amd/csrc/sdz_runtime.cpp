@@ -282,6 +282,9 @@ int inflate_scratch(InflateArgs& a, uint32_t n, bool own_state, size_t extra, hi
     size_t mem_free = 0, mem_total = 0;
     if (hipMemGetInfo(&mem_free, &mem_total) != hipSuccess) mem_free = 16ull << 30;
     uint64_t budget = std::min<uint64_t>(32ull << 30, mem_free / 4);
+    // the wave decoder's provisional slots (below) come out of the same quarter
+    const uint64_t wdp_bytes = own_state && a.wave ? (uint64_t)n * kWdProvTokens * 4 : 0;
+    budget = budget > 2 * wdp_bytes ? budget - wdp_bytes : budget / 2;
     uint64_t want = 1u << 17;
     if (const char* e = getenv("SDZ_ROUND_TOKENS")) want = strtoull(e, nullptr, 10);
     uint32_t T = (uint32_t)std::min<uint64_t>(want, std::max<uint64_t>(1024, budget / (4ull * n)));
@@ -296,7 +299,13 @@ int inflate_scratch(InflateArgs& a, uint32_t n, bool own_state, size_t extra, hi
     const size_t off_wp = (off_nt + (size_t)n * 8 + 256 + 255) & ~(size_t)255;
     const size_t off_ex = (off_wp + (wdp ? (size_t)n * kWdProvTokens * 4 : 0) + 255) & ~(size_t)255;
     void* scratch = nullptr;
-    if (int rc = use.get(off_ex + extra, &scratch)) return rc;
+    if (int rc = use.get(off_ex + extra, &scratch)) {
+        // no room for the wave decoder's slots: the lane decoder (which needs none) takes the call
+        if (!wdp || inflate_wdec_mode() == 1) return rc;
+        (void)hipGetLastError();                          // (the failed hipMalloc's error)
+        a.wave = 0;
+        return inflate_scratch(a, n, own_state, extra, s, use, extra_out);
+    }
     uint8_t* base = (uint8_t*)scratch;
     a.scratch = base;
     if (own_state) { a.dsave = base + off_ds; a.rsave = base + off_rs; }
@@ -310,6 +319,9 @@ int inflate_scratch(InflateArgs& a, uint32_t n, bool own_state, size_t extra, hi
     return SDZ_API_OK;
 }
 
+// timing_started: the call's timing events were started by an earlier attempt (the wave decoder's,
+// handed back with kWdRestart), whose decode time g_restart_ms is added to this run's breakdown
+thread_local float g_restart_ms = 0.f;
 int inflate_run(InflateArgs& a, hipStream_t s, bool timing_started = false, int (*hook)(void*) = nullptr,
                 void* hook_ctx = nullptr) {
     static thread_local uint32_t host_active = 0;
@@ -319,9 +331,18 @@ int inflate_run(InflateArgs& a, hipStream_t s, bool timing_started = false, int 
         HIPCHK(hipMalloc(&a.dbg, 64 * sizeof(unsigned long long)));
         HIPCHK(hipMemsetAsync(a.dbg, 0, 64 * sizeof(unsigned long long), s));
     }
-    if (!timing_started) timing_begin(s);
-    if (int rc = run_inflate_rounds(a, s, &host_active, g_timing ? g_breakdown : nullptr, hook, hook_ctx))
+    if (!timing_started) { timing_begin(s); g_restart_ms = 0.f; }
+    if (int rc = run_inflate_rounds(a, s, &host_active, g_timing ? g_breakdown : nullptr, hook, hook_ctx)) {
+        if (a.dbg) { (void)hipFree(a.dbg); a.dbg = nullptr; }
+        if (rc == kWdRestart) {                          // the caller starts over; timing goes on
+            g_restart_ms = g_timing ? g_breakdown[0] : 0.f;
+            return rc;
+        }
+        g_restart_ms = 0.f;
         return rc > 0 ? rc : hip_fail(hipGetLastError(), "inflate rounds");
+    }
+    if (g_timing) g_breakdown[0] += g_restart_ms;
+    g_restart_ms = 0.f;
     timing_end(s);
     if (phases) {
         unsigned long long h[64];
@@ -660,10 +681,12 @@ int rt::inflate_batch_device(const uint8_t* in, const uint64_t* in_off, const ui
             one = host_cap[i] + 16 <= a.round_tokens && host_len[i] <= (1ull << 28);
         a.one_round = one ? 1u : 0u;
     }
+    bool restarted = false;
     if (a.wave) {
         const int rw = inflate_run(a, s, false, nullptr, nullptr);
         if (rw != kWdRestart) return rw;
         a.wave = 0;                                       // many small blocks: lane decoder + split
+        restarted = true;
     }
     PoolUse find_use(g_find, s);
     SplitHost sh;
@@ -672,7 +695,7 @@ int rt::inflate_batch_device(const uint8_t* in, const uint64_t* in_off, const ui
     PoolUse split_use(g_split, sh.side ? sh.side->s : s);
     sh.seg_use = &split_use;
     if (sh.plan.nsplit) { a.split_plan = &sh.plan; a.split_state = sh.split_state; }
-    int rc = inflate_run(a, s, false, sh.plan.nsplit ? inflate_split_finish : nullptr, &sh);
+    int rc = inflate_run(a, s, restarted, sh.plan.nsplit ? inflate_split_finish : nullptr, &sh);
     if (sh.plan.nsplit) {
         // every exit: the main stream waits for the side stream's work, and the side stream
         // (where the segments' pool is released) for the main stream's rounds

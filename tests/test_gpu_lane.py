@@ -1,0 +1,73 @@
+"""The inflate parity tests of test_gpu_parity.py again, with the LANE decoder forced
+(SDZ_WDEC=0).  The default policy (`inflate_wave_policy`) sends most of the suite's
+small and mid-size batches to the wave decoder, while every 65,536-stream bench shape (C2, the
+distinct leg, the mixed leg) runs on the lane decoder: this file pins that path -- the one behind
+the headline numbers -- to the oracle and to ground truth on every inflate case (errors and their
+messages, need-bits stalls, dictionaries, stored blocks, trailing bytes, slot edges, many rounds).
+Reference: /root/reference/src/infcodes.ts:62-301 (inflate_fast), infblocks.ts:123-628 (proc)."""
+import random
+
+import pytest
+
+import oracle as O
+import sdz
+from conftest import golden
+from test_gpu_parity import (  # noqa: F401  (collected here a second time, under SDZ_WDEC=0)
+    assert_same,
+    test_c2_mini_batch_copies_of_paradiselost,
+    test_chunkwise_adler_quirk,
+    test_concurrent_streams_do_not_share_scratch,
+    test_corrupted_streams_match_reference_errors,
+    test_dictionary_stream,
+    test_fixtures_inflate_like_reference,
+    test_inflate_auto_detect_matches_inflate_function,
+    test_inflate_oracle_generated,
+    test_inflate_zlib_generated,
+    test_many_small_blocks,
+    test_many_small_blocks_later_rounds,
+    test_output_slot_edges,
+    test_raw_need_bits_at_end_of_input,
+    test_repetitive_data_long_match_chains,
+    test_small_rounds_rebuild_the_window,
+    test_stored_blocks_decode_correctly,
+    test_trailing_bytes_reported,
+)
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(autouse=True)
+def _lane_decoder(monkeypatch):
+    monkeypatch.setenv("SDZ_WDEC", "0")
+
+
+def _slices(n, size, seed):
+    """n distinct `size`-byte windows of paradiselost.txt at random offsets (the distinct leg's
+    shape: every lane of a wave decodes a different stream, so lanes diverge every step)."""
+    text = golden("paradiselost.txt")
+    rng = random.Random(seed)
+    return [text[o:o + size] for o in (rng.randrange(len(text) - size) for _ in range(n))]
+
+
+@pytest.mark.parametrize("fmt", ["deflate", "gzip", "raw"])
+def test_distinct_64k_slices_lane_decoder(fmt):
+    """256 distinct 64 KiB slices deflated by the oracle (levels 1-9) on the lane decoder: every
+    record field and byte against the oracle's Inflater (the north star's stream shape)."""
+    plain = _slices(256, 65536, 31 + len(fmt))
+    streams = [O.deflate(p, level=1 + i % 9, format=fmt, mtime=i) for i, p in enumerate(plain)]
+    raw = fmt == "raw"
+    gpu = sdz.inflate_batch(streams, [65536 + 64] * len(streams), sdz.FMT_RAW if raw else sdz.FMT_CONTAINER)
+    for g, s, p in zip(gpu, streams, plain):
+        assert_same(g, O.inflater_run([s], raw=raw), s)
+        assert g["status"] == "OK" and g["data"] == p
+
+
+def test_distinct_slices_lane_vs_wave_records(monkeypatch):
+    """The same distinct batch on both decoders gives identical records and bytes."""
+    plain = _slices(192, 40000, 77)
+    streams = [O.deflate(p, level=6) for p in plain]
+    lane = sdz.inflate_batch(streams, [40064] * len(streams), sdz.FMT_CONTAINER)
+    monkeypatch.setenv("SDZ_WDEC", "1")
+    wave = sdz.inflate_batch(streams, [40064] * len(streams), sdz.FMT_CONTAINER)
+    for a, b, p in zip(lane, wave, plain):
+        assert a == b and a["data"] == p

@@ -143,11 +143,7 @@ def test_incremental_skewed_batch():
     assert all(r["success"] and r["data"] == b"hello world " * 10 for r in res[1:])
 
 
-def test_concurrent_multi_calls_same_devices():
-    """Two host threads call inflate_batch_multi on the same device list at once (ctypes drops the
-    GIL): the library serialises multi calls, so neither waits on the other's shard at a barrier
-    (ADVICE r03: overlapping device locks held across the all-gather deadlocked), and both
-    return every record intact."""
+def _concurrent_multi(devices):
     import threading
     plain, comp = _mixed_batch(24, seed=5)
     caps = [len(p) + 64 for p in plain]
@@ -155,7 +151,7 @@ def test_concurrent_multi_calls_same_devices():
 
     def run(k):
         try:
-            res[k], _ = sdz.inflate_batch_multi(comp, [0, 0], out_caps=caps)
+            res[k], _ = sdz.inflate_batch_multi(comp, devices, out_caps=caps)
         except Exception as e:                            # reported below, not swallowed
             errs.append(e)
 
@@ -169,3 +165,36 @@ def test_concurrent_multi_calls_same_devices():
     for recs in res:
         for r, p in zip(recs, plain):
             assert r["status"] == "OK" and r["data"] == p
+
+
+@pytest.mark.skipif(sdz.device_count() < 2, reason="needs two GPUs (distinct devices: the RCCL path)")
+def test_concurrent_multi_calls_distinct_devices():
+    """As below, on two distinct devices: each call's shards hold their device locks across the
+    RCCL all-gather, the case the serialised multi calls (g_multi_mu) exist for."""
+    _concurrent_multi([0, 1])
+
+
+@pytest.mark.parametrize("devices", [[0], [0, 1]])
+def test_gather_failure_aborts_and_recovers(monkeypatch, devices):
+    """A rank whose collective fails (SDZ_TEST_GATHER_FAIL=k: rank k never enters the all-gather) ends
+    the call with an error on every rank -- its peers stop waiting instead of hanging -- the
+    communicators are aborted and dropped, and the next call builds new ones and succeeds."""
+    if max(devices) >= sdz.device_count():
+        pytest.skip("needs %d GPUs" % (max(devices) + 1))
+    plain, comp = _mixed_batch(12, seed=11)
+    caps = [len(p) + 64 for p in plain]
+    monkeypatch.setenv("SDZ_TEST_GATHER_FAIL", str(len(devices) - 1))
+    with pytest.raises(sdz.SdzError, match="ncclAllGather|collective failed"):
+        sdz.inflate_batch_multi(comp, devices, out_caps=caps)
+    monkeypatch.delenv("SDZ_TEST_GATHER_FAIL")
+    recs, st = sdz.inflate_batch_multi(comp, devices, out_caps=caps)
+    assert st["rccl"]
+    assert all(r["status"] == "OK" and r["data"] == p for r, p in zip(recs, plain))
+
+
+def test_concurrent_multi_calls_same_devices():
+    """Two host threads call inflate_batch_multi on the same device list at once (ctypes drops the
+    GIL): the library serialises multi calls, so neither waits on the other's shard at a barrier
+    (ADVICE r03: overlapping device locks held across the all-gather deadlocked), and both
+    return every record intact."""
+    _concurrent_multi([0, 0])

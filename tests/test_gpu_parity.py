@@ -688,8 +688,11 @@ def test_output_slot_edges():
 
 @pytest.mark.parametrize("n", [65836, 100000, 200000])
 def test_deflate_tail_window_regression(paradise, n):
-    """Inputs on which an LDS-staged variant of the last positions' search (k_dfl_tail) differed from
-    the reference on the GPU only (adjacent byte reads merged into one unaligned
-    ds_read_u16): L4 / L6 / L9 bytes against the oracle."""
+    """Inputs on which an LDS-staged variant of the last positions' search (k_dfl_tail,
+    tools/wip/tail_lds.patch, not shipped) differed from the reference on the GPU only. DESIGN §5
+    (round 4) traces that to a code-generation fault in the variant's walk loop: a break-edge register
+    copy (`v5 = cur`, block .LBB9_66) ran for every lane that passed the 4-byte pre-check, so each such
+    candidate was taken twice. This test guards the shipped HBM walk on those inputs: L4 / L6 / L9
+    bytes against the oracle."""
     for lv in (4, 6, 9):
         assert sdz.deflate(paradise[:n], {"level": lv}) == O.deflate(paradise[:n], level=lv, format="deflate"), lv

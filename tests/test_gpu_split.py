@@ -1,8 +1,9 @@
 """GPU parity of the block-parallel decode of long streams (k_split.hip): a batch whose
 long streams are split at their block starts and decoded as parallel segments must give
 exactly what the serial decoder gives -- bytes, records, verdicts -- including for damaged
-streams, which fall back to the serial path.  SDZ_SPLIT=0 is the serial reference here (and
-the serial decoder is itself pinned to the oracle by test_gpu_parity.py)."""
+streams, which fall back to the serial path.  SDZ_SPLIT=0 is the serial reference here.  Both
+legs force the lane decoder (SDZ_WDEC=0), so neither depends on the wave decoder's hand-off
+constant (kWdLaneAfter); the lane decoder itself is pinned to the oracle by test_gpu_lane.py."""
 import os
 import random
 import zlib
@@ -35,6 +36,11 @@ def comp(data, fmt, level=6):
         c = zlib.compressobj(level, zlib.DEFLATED, 31)
         return c.compress(data) + c.flush()
     return zlib.compress(data, level)
+
+
+@pytest.fixture(autouse=True)
+def _lane_decoder(monkeypatch):
+    monkeypatch.setenv("SDZ_WDEC", "0")
 
 
 def run(streams, caps, split):
