@@ -1197,8 +1197,11 @@ __global__ __launch_bounds__(64 * CH_WAVES) void k_dfl_chain(DeflateArgs A) {
 #ifndef PM_LAZYW4
 #define PM_LAZYW4 0                                     // measured slower: C3 543 -> 576 ms
 #endif
-#define PM_WINB (W_SIZE + PM_SEG + MAX_MATCH + 16)     // staged window bytes
-#define PM_PV (W_SIZE + PM_SEG)                         // staged links
+#ifndef PM_MORE_IF
+#define PM_MORE_IF 1                                    // long compares behind one uniform test
+#endif
+#define PM_WINB (W_SIZE + PM_SEG + PM_TAIL + MAX_MATCH + 16)   // staged window bytes (+ the last positions'
+#define PM_PV (W_SIZE + PM_SEG + PM_TAIL)                         // staged links      ... in a last segment)
 // record word of position p: the full-chain result (len << 16 | dist) in the low half, the
 // quarter-chain result in the high half, and input byte p - 1 (the literal the parse emits
 // from there) in bits 25-31 of the low half and bit 25 of the high half: the parse then
@@ -1214,6 +1217,32 @@ uint32_t deflate_match_segs(uint64_t len) {
     const uint64_t tail = len > PM_TAIL ? len - PM_TAIL : 0;
     return (uint32_t)((tail + PM_SEG - 1) / PM_SEG);
 }
+__device__ uint32_t win_byte(const GLB uint8_t* in, int64_t n, int64_t off, int64_t i);
+__device__ __forceinline__ int64_t slide_off(int64_t n, int64_t P);
+// The last PM_TAIL positions of a stream search the window the reference has there (stale bytes
+// past the input, tail_search below); a slide can fall among them, so they form one or two groups
+// of one window offset each.  k_dfl_match searches the larger group [mlo, mhi) (offset offM) in
+// its last segment's LDS window, with that group's bytes past the input staged after it;
+// k_dfl_tail the other.
+struct TailGroups {
+    int64_t mlo, mhi, offM;
+};
+__device__ __forceinline__ TailGroups tail_groups(int64_t n, int64_t tail) {
+    const int64_t offA = slide_off(n, tail), offB = slide_off(n, n - 1);
+    int64_t ps = n;                                       // first position with offB
+    if (offA != offB) {
+        int64_t lo = tail + 1, hi = n - 1;                // slide_off grows with P
+        while (lo < hi) {
+            const int64_t mid = (lo + hi) >> 1;
+            if (slide_off(n, mid) == offB) hi = mid; else lo = mid + 1;
+        }
+        ps = lo;
+    }
+    TailGroups t;
+    if (n - ps >= ps - tail) { t.mlo = ps == n ? tail : ps; t.mhi = n; t.offM = offB; }
+    else { t.mlo = tail; t.mhi = ps; t.offM = offA; }
+    return t;
+}
 __global__ __launch_bounds__(PM_THREADS) void k_dfl_match(DeflateArgs A) {
     __shared__ __attribute__((aligned(16))) uint8_t win[(PM_WINB + 15) & ~15];
     __shared__ __attribute__((aligned(16))) uint16_t pvl[PM_PV];
@@ -1228,12 +1257,18 @@ __global__ __launch_bounds__(PM_THREADS) void k_dfl_match(DeflateArgs A) {
     const int n = (int)in_len;
     const int tail = n > PM_TAIL ? n - PM_TAIL : 0;
     const int s0 = (int)(seg * PM_SEG), e0 = s0 + (A.seg_merge && seg == 0 ? 3 * PM_SEG : PM_SEG);
-    const int s1 = e0 < tail ? e0 : tail;
+    // the stream's last segment also takes the last positions (A.tail_in_match): all of them are
+    // handed out, the larger window-offset group [mlo, mhi) is searched, the rest are left to
+    // k_dfl_tail (which runs after and overwrites their records)
+    const bool tl = A.tail_in_match && e0 >= tail && tail < n;
+    const int s1 = tl ? n : e0 < tail ? e0 : tail;
     if (s0 >= s1) return;
     const int ws = s0 > W_SIZE ? s0 - W_SIZE : 0;          // staged range [ws, we) (ws even)
     const int we = s1 + MAX_MATCH + 8 < n ? s1 + MAX_MATCH + 8 : n;
     const GLB uint8_t* in = (const GLB uint8_t*)(A.in + A.in_off[sid]);
     const GLB uint16_t* pv = (const GLB uint16_t*)A.pv_buf + rp;
+    TailGroups tg = { n, n, 0 };
+    if (tl) tg = tail_groups(n, tail);
     {
         const int nw = (we - ws) >> 2;                     // whole dwords (unaligned global reads)
         uint32_t* w32 = (uint32_t*)win;
@@ -1243,6 +1278,10 @@ __global__ __launch_bounds__(PM_THREADS) void k_dfl_match(DeflateArgs A) {
             w32[i] = v;
         }
         for (int i = 4 * nw + (int)tid; i < we - ws; i += PM_THREADS) win[i] = in[ws + i];
+        // past the input: the bytes the larger group's window holds there (tail_search's wb)
+        if (tl)
+            for (int j = (int)tid; j < MAX_MATCH + 16; j += PM_THREADS)
+                win[n - ws + j] = (uint8_t)win_byte(in, n, tg.offM, (int64_t)n + j - tg.offM);
         const int np = (s1 - ws) >> 1;                     // link pairs (ws even, rp a multiple of 64)
         uint32_t* p32 = (uint32_t*)pvl;
         // links (distances) are staged as the previous position relative to ws (0 for none,
@@ -1262,7 +1301,8 @@ __global__ __launch_bounds__(PM_THREADS) void k_dfl_match(DeflateArgs A) {
     }
     __syncthreads();
     GLB uint64_t* rec = (GLB uint64_t*)A.rec_buf + rp;
-    const int max_chain = c_config[A.level][3], qchain = max_chain >> 2, nice = c_config[A.level][2];
+    const int max_chain = c_config[A.level][3], qchain = max_chain >> 2, nice0 = c_config[A.level][2];
+    int nice = nice0;                                       // (a last position: at most its lookahead)
     // Positions in chunks of PM_CHUNK: each wave starts on its own chunk and takes the next
     // free one from an LDS counter when it has handed out its last position, so waves whose
     // positions have long chains do not hold up the workgroup.
@@ -1318,7 +1358,16 @@ __global__ __launch_bounds__(PM_THREADS) void k_dfl_match(DeflateArgs A) {
 #endif
                     limit = (p > MAX_DIST ? p - MAX_DIST : 0) - ws;   // >= 0
                     s4 = pm_w4(win, (uint32_t)sp);
-                    const bool search = cur != 0 && sp - cur <= MAX_DIST;  // deflate.ts:1092
+                    bool search = cur != 0 && sp - cur <= MAX_DIST;  // deflate.ts:1092
+                    if (p >= tail) {                                  // a last position (tl only)
+                        // searched if in the larger group and lookahead >= MIN_MATCH; window index
+                        // 0 (position offM) is NIL there; nice_match at most the lookahead
+                        search = search && p <= n - MIN_MATCH && p >= tg.mlo && p < tg.mhi &&
+                                 (int64_t)(cur + ws) > tg.offM;
+                        nice = n - p < nice0 ? n - p : nice0;
+                    } else {
+                        nice = nice0;
+                    }
                     chain = search ? max_chain : 0;
                     pend = !search;                             // no search: record 0
                     nxt = pvl[search ? cur : sp];
@@ -1357,7 +1406,14 @@ __global__ __launch_bounds__(PM_THREADS) void k_dfl_match(DeflateArgs A) {
         int len1 = x1 ? (int)(__builtin_ctz(x1) >> 3) : 4;
         int len2 = x2 ? (int)(__builtin_ctz(x2) >> 3) : 4;
         bool more1 = cand1 && x1 == 0, more2 = cand2 && x2 == 0;
+#if PM_MORE_IF
+        // the long-compare loop behind one wave-uniform test: most steps have no lane with a
+        // 4-byte prefix match, and the loop's own exit test then costs nothing more
+        if (__ballot(more1 || more2)) {
+            do {
+#else
         while (__ballot(more1 || more2)) {                   // matches of more than 4 bytes
+#endif
             const uint32_t cm = more1 ? c1 : c2;
             const int lm = more1 ? len1 : len2;
             const uint32_t x = pm_w4(win, cm + (uint32_t)lm) ^ pm_w4(win, sp + (uint32_t)lm);
@@ -1367,6 +1423,9 @@ __global__ __launch_bounds__(PM_THREADS) void k_dfl_match(DeflateArgs A) {
             len2 += m2 ? d : 0;
             more1 = m1 ? x == 0 && len1 < MAX_MATCH : more1;
             more2 = m2 ? x == 0 && len2 < MAX_MATCH : more2;
+#if PM_MORE_IF
+            } while (__ballot(more1 || more2));
+#endif
         }
         len1 = len1 > MAX_MATCH ? MAX_MATCH : len1;
         len2 = len2 > MAX_MATCH ? MAX_MATCH : len2;
@@ -1862,8 +1921,13 @@ __global__ __launch_bounds__(256) void k_dfl_tail(DeflateArgs A) {
     const GLB uint16_t* pv = (const GLB uint16_t*)A.pv_buf + rp;
     GLB uint64_t* rec = (GLB uint64_t*)A.rec_buf + rp;
     const int max_chain = c_config[A.level][3], nice = c_config[A.level][2];
-    // the last MIN_MATCH - 1 positions are not searched; their records carry only the byte
+    // with A.tail_in_match, k_dfl_match searched the larger window-offset group already (a stream
+    // with match segments, tail > 0); the last MIN_MATCH - 1 positions are not searched, their
+    // records carry only the byte
+    TailGroups tg = { n, n, 0 };
+    if (A.tail_in_match && tail > 0) tg = tail_groups(n, tail);
     for (int64_t P = tail + (int64_t)threadIdx.x; P < n; P += 256) {
+        if (P >= tg.mlo && P < tg.mhi) continue;
         const uint64_t r = P <= n - MIN_MATCH ? tail_search(in, pv, n, P, max_chain, nice) : 0ull;
         rec[P] = rec_word((uint32_t)r, (uint32_t)(r >> 32), in[P > 0 ? P - 1 : 0]);
     }

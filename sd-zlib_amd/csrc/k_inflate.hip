@@ -2036,8 +2036,10 @@ int run_inflate_rounds(const InflateArgs& a, hipStream_t s, uint32_t* host_activ
     const bool use_wd = a.wave && a.wdprov && !a.streaming && !a.segmode && !a.split_plan;
     uint32_t lane_after = kWdLaneAfter;                  // SDZ_WD_LANE_AFTER: development / tests
     if (const char* e = getenv("SDZ_WD_LANE_AFTER")) lane_after = (uint32_t)strtoul(e, nullptr, 10);
+    // one round and no wave decoder: nothing reads the active counter (a launch less per call)
+    const bool count_active = !(a.one_round && !a.split_plan && !use_wd);
     for (uint32_t round = 0;; ++round) {
-        if (hipMemsetAsync(a.active, 0, sizeof(uint32_t), s) != hipSuccess) { rc = -1; break; }
+        if (count_active && hipMemsetAsync(a.active, 0, sizeof(uint32_t), s) != hipSuccess) { rc = -1; break; }
         if (kernel_ms) (void)hipEventRecord(ev[0], s);
         if (use_wd) {
             // block-level work (a lane per stream) and the blocks' symbols (a wave per stream),

@@ -858,7 +858,11 @@ void launch_inflate_finalize(const InflateArgs& a, hipStream_t s) {
     uint32_t maxc = 1;
     unsigned long long* slot = (unsigned long long*)a.tokens;
     uint32_t* parts = a.tokens + 64;
-    if (device_max_u64(a.out_cap, a.n, slot, &mx, s) == 0 && mx > chunk) {
+    // the largest output slot sizes the chunked crc32 grid: from the host when it has the slots
+    // (no device read and wait), else one device reduction
+    const bool known = a.host_cap_max != 0;
+    if (known) mx = a.host_cap_max;
+    if ((known || device_max_u64(a.out_cap, a.n, slot, &mx, s) == 0) && mx > chunk) {
         uint64_t c = (mx + chunk - 1) / chunk;
         const uint64_t lim = std::min<uint64_t>(1024, std::max<uint64_t>(1, (4ull << 20) / a.n));
         if (c > lim) { c = lim; chunk = ((mx + c - 1) / c + 7) & ~7ull; }

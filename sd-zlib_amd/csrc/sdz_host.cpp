@@ -93,12 +93,14 @@ int host_shard(const uint8_t* const* in, const size_t* in_len, uint8_t* const* o
         R.bytes_in += in_len[i];
     }
     const bool compact = m > kDirectOut;
+    // in and meta adjacent (one host-to-device copy of both), out and records adjacent (one copy
+    // back of both for small outputs): a small call is a few copies and the codec's launches
     size_t o = 0;
     const size_t o_in = o; o = al(o + ti + 128, 256);
-    const size_t o_out = o; o = al(o + to + 64, 256);
-    const size_t o_cmp = o; o = al(o + (compact ? to : 0), 256);
     const size_t o_meta = o; o = al(o + 7 * (size_t)m * 8, 256);
+    const size_t o_out = o; o = al(o + to + 64, 256);
     const size_t o_rec = o; o = al(o + (size_t)std::max(rec_cap, m) * rsz, 256);
+    const size_t o_cmp = o; o = al(o + (compact ? to : 0), 256);
     const size_t o_dict = o; o = al(o + (C.dict ? C.dict_len + 64 : 0), 256);
     void* base = nullptr;
     PoolUse use(g_host, s);
@@ -108,20 +110,21 @@ int host_shard(const uint8_t* const* in, const size_t* in_len, uint8_t* const* o
     // pinned staging: packed inputs + meta (the outputs reuse it after the records are back)
     const bool pack = ti <= kPackInMax;
     void* pin = nullptr;
-    const size_t pin_meta = pack ? al(ti, 256) : 0;
+    // packed: the staging mirrors the device's [in | meta] (one copy); else the meta alone
+    const size_t pin_meta = pack ? o_meta - o_in : 0;
     if (int rc = g_pinned.get(pin_meta + meta.size() * 8 + 64, &pin)) return rc;
     uint8_t* P = (uint8_t*)pin;
     if (pack) {
         for (uint32_t k = 0; k < m; ++k)
             if (in_len[R.order[k]]) std::memcpy(P + meta[k], in[R.order[k]], in_len[R.order[k]]);
-        if (ti) HIPCHK(hipMemcpyAsync(B + o_in, P, ti, hipMemcpyHostToDevice, s));
     } else {
         for (uint32_t k = 0; k < m; ++k)
             if (in_len[R.order[k]])
                 HIPCHK(hipMemcpyAsync(B + o_in + meta[k], in[R.order[k]], in_len[R.order[k]], hipMemcpyHostToDevice, s));
     }
     std::memcpy(P + pin_meta, meta.data(), meta.size() * 8);
-    HIPCHK(hipMemcpyAsync(d_meta, P + pin_meta, meta.size() * 8, hipMemcpyHostToDevice, s));
+    if (pack) HIPCHK(hipMemcpyAsync(B + o_in, P, pin_meta + meta.size() * 8, hipMemcpyHostToDevice, s));
+    else HIPCHK(hipMemcpyAsync(d_meta, P, meta.size() * 8, hipMemcpyHostToDevice, s));
     if (int rc = g_pinned.done(s)) return rc;       // (the next get() waits for these copies)
     uint8_t* d_dict = nullptr;
     if (C.dict) {
@@ -129,10 +132,13 @@ int host_shard(const uint8_t* const* in, const size_t* in_len, uint8_t* const* o
         if (C.dict_len) HIPCHK(hipMemcpyAsync(d_dict, C.dict, C.dict_len, hipMemcpyHostToDevice, s));
     }
     if (rec_cap > m) HIPCHK(hipMemsetAsync(B + o_rec + (size_t)m * rsz, 0, (size_t)(rec_cap - m) * rsz, s));
-    hipEvent_t e0 = nullptr, e1 = nullptr;
-    HIPCHK(hipEventCreate(&e0));
-    HIPCHK(hipEventCreate(&e1));
-    struct EvFree { hipEvent_t a, b; ~EvFree() { hipEventDestroy(a); hipEventDestroy(b); } } evf{ e0, e1 };
+    // the shard's kernel-time events: made once per thread and device
+    static thread_local hipEvent_t evs[kMaxDev][2] = {};
+    int dev = 0;
+    HIPCHK(hipGetDevice(&dev));
+    if (dev < 0 || dev >= kMaxDev) return fail(SDZ_API_BAD_ARG, "host batch: device index");
+    if (!evs[dev][0]) { HIPCHK(hipEventCreate(&evs[dev][0])); HIPCHK(hipEventCreate(&evs[dev][1])); }
+    hipEvent_t e0 = evs[dev][0], e1 = evs[dev][1];
     HIPCHK(hipEventRecord(e0, s));
     int rc = C.inflate
         ? rt::inflate_batch_device(B + o_in, d_meta, d_meta + m, B + o_out, d_meta + 2 * (size_t)m,
@@ -148,17 +154,20 @@ int host_shard(const uint8_t* const* in, const size_t* in_len, uint8_t* const* o
     std::vector<uint8_t> recs((size_t)m * rsz);
     const bool eager = !compact && to <= kEagerOut;
     uint8_t* ebuf = nullptr;
-    if (eager && to) {
+    if (eager) {                                   // outputs and records: one copy
         void* ep = nullptr;
-        if (int rc2 = g_pinned.get(al(to, 256), &ep)) return rc2;
+        const size_t nb = o_rec - o_out + recs.size();
+        if (int rc2 = g_pinned.get(al(nb, 256), &ep)) return rc2;
         ebuf = (uint8_t*)ep;
-        HIPCHK(hipMemcpyAsync(ebuf, B + o_out, to, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipMemcpyAsync(ebuf, B + o_out, nb, hipMemcpyDeviceToHost, s));
+    } else {
+        HIPCHK(hipMemcpyAsync(recs.data(), B + o_rec, recs.size(), hipMemcpyDeviceToHost, s));
     }
-    HIPCHK(hipMemcpyAsync(recs.data(), B + o_rec, recs.size(), hipMemcpyDeviceToHost, s));
     // multi-GPU: the records (rec_cap slots, padding zeroed) into the caller's gather slot, which
     // the caller keeps (its own pool use) until the all-gather is done
     if (rec_dev) HIPCHK(hipMemcpyAsync(rec_dev, B + o_rec, (size_t)rec_cap * rsz, hipMemcpyDeviceToDevice, s));
     HIPCHK(hipStreamSynchronize(s));
+    if (eager) std::memcpy(recs.data(), ebuf + (o_rec - o_out), recs.size());
     HIPCHK(hipEventElapsedTime(&R.kernel_ms, e0, e1));
     auto out_len_of = [&](uint32_t k) -> uint64_t {
         const uint8_t* r = recs.data() + (size_t)k * rsz;

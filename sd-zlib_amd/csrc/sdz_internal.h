@@ -65,6 +65,7 @@ struct InflateArgs {
     // host-side hints (host pointers / flags; kernels never read them)
     const uint64_t* host_len;    // the n input lengths, when the caller has them on the host
     uint32_t one_round;          // every stream finishes in one round: no active-count read-back
+    uint64_t host_cap_max;       // the largest out_cap when the caller has them on the host (0: unknown)
 };
 
 uint64_t inflate_dsave_bytes();  // per stream decode state
@@ -143,6 +144,8 @@ struct DeflateArgs {
     uint32_t ncunit;
     uint32_t nbmax;              // most block slots of one stream (k_dfl_trees grid)
     uint32_t wide;               // k_dfl_parse: one workgroup per stream (few, long streams)
+    uint32_t tail_in_match;      // k_dfl_match searches the last positions too (in its last segment's
+                                 // LDS window); k_dfl_tail does only those of the other window offset
     // segment-parallel lazy parse (k_lz_*, k_deflate.hip): stream k's positions cut into
     // segments of 1 << lz_shift, global segment ids [lz_sg0[k], lz_sg0[k + 1])
     uint32_t lz_shift;           // 0: the serial parse kernels instead

@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -141,6 +142,8 @@ Pool g_inflate_scratch, g_deflate_state, g_tmp, g_stage, g_split, g_find;
 // [128, 256) small results, then the file name
 constexpr size_t kTmpMax = 0, kTmpDictId = 64, kTmpFname = 256;
 constexpr uint64_t kInflaterOutCap = 4ull << 20;   // sdz_inflater: output slot per device call
+constexpr uint64_t kDeflateSmallMax = 1024;         // deflate: calls of short inputs only run serially ...
+constexpr uint32_t kDeflateSmallStreams = 16;       // ... when there are at most this many
 constexpr uint64_t kDeflaterRedo = 8;             // sdz_deflater: record mode while redone bytes <= 8 x input
 constexpr uint64_t kDeflaterRedoFloor = 64ull << 20;  //   + 64 MiB, then serial
 constexpr size_t kInflaterOnePassMin = 32u << 10;  // sdz_inflater: a first append this long tries the one-pass path
@@ -270,6 +273,25 @@ float sdz_last_kernel_ms(void) {
 
 namespace {
 
+// Free HBM of the current device, for sizing scratch: hipMemGetInfo is a driver query (tens of
+// microseconds, a visible share of a small call's latency), so its value is kept per device for
+// up to 50 ms; the pools this library grows in between are a small part of 288 GB.
+size_t free_hbm() {
+    static std::mutex mu;
+    static size_t val[kMaxDev] = {};
+    static double at[kMaxDev] = {};
+    int d = 0;
+    if (hipGetDevice(&d) != hipSuccess || d < 0 || d >= kMaxDev) d = 0;
+    const double t = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+    std::lock_guard<std::mutex> lk(mu);
+    if (val[d] == 0 || t - at[d] > 50.0) {
+        size_t f = 0, tot = 0;
+        val[d] = hipMemGetInfo(&f, &tot) == hipSuccess ? f : 16ull << 30;
+        at[d] = t;
+    }
+    return val[d];
+}
+
 // Scratch of one inflate call: per-stream code lengths, then (one-shot) decode and resolve
 // state, the token ring (round_tokens per stream; C2's streams finish in one round),
 // ntok / flags / the active counter, and `extra` bytes for the caller (incremental staging).
@@ -279,8 +301,7 @@ int inflate_scratch(InflateArgs& a, uint32_t n, bool own_state, size_t extra, hi
     const uint64_t dsb = inflate_dsave_bytes(), rsb = inflate_rsave_bytes();
     // tokens per stream per round: as many as a quarter of free HBM (at most 32 GiB) allows,
     // up to 128 Ki; SDZ_ROUND_TOKENS overrides
-    size_t mem_free = 0, mem_total = 0;
-    if (hipMemGetInfo(&mem_free, &mem_total) != hipSuccess) mem_free = 16ull << 30;
+    const size_t mem_free = free_hbm();
     uint64_t budget = std::min<uint64_t>(32ull << 30, mem_free / 4);
     // the wave decoder's provisional slots (below) come out of the same quarter
     const uint64_t wdp_bytes = own_state && a.wave ? (uint64_t)n * kWdProvTokens * 4 : 0;
@@ -675,11 +696,16 @@ int rt::inflate_batch_device(const uint8_t* in, const uint64_t* in_off, const ui
     a.split_plan = nullptr; a.split_state = nullptr; a.segmode = 0;
     a.host_len = host_len;
     a.one_round = 0;
+    a.host_cap_max = 0;
     if (host_len && host_cap) {
         bool one = true;
-        for (uint32_t i = 0; i < n && one; ++i)
-            one = host_cap[i] + 16 <= a.round_tokens && host_len[i] <= (1ull << 28);
+        uint64_t mx = 1;
+        for (uint32_t i = 0; i < n; ++i) {
+            one = one && host_cap[i] + 16 <= a.round_tokens && host_len[i] <= (1ull << 28);
+            mx = std::max<uint64_t>(mx, host_cap[i]);
+        }
         a.one_round = one ? 1u : 0u;
+        a.host_cap_max = mx;
     }
     bool restarted = false;
     if (a.wave) {
@@ -842,8 +868,7 @@ int rt::deflate_batch_device(const uint8_t* in, const uint64_t* in_off, const ui
     if (lk.rc) return lk.rc;
     // per-stream state slabs: process in sub-batches so the pool stays bounded
     const uint64_t slab = deflate_state_bytes();
-    size_t mem_free = 0, mem_total = 0;
-    if (hipMemGetInfo(&mem_free, &mem_total) != hipSuccess) mem_free = 16ull << 30;
+    const size_t mem_free = free_hbm();
     void* tmp = nullptr;
     PoolUse tmp_use(g_tmp, s);
     if (int rc = tmp_use.get(kTmpFname + fname_len + 64, &tmp)) return rc;
@@ -863,14 +888,22 @@ int rt::deflate_batch_device(const uint8_t* in, const uint64_t* in_off, const ui
     // the rounds (C3 shape at L1: 0.80 s serial, 6.8 s in rounds).
     const bool fastlv = level <= 3;
     const bool lz_on = !getenv("SDZ_SERIAL_PARSE");
-    const bool recpath = (!fastlv || lz_on) && !dict;
-    std::vector<uint64_t> len(recpath ? n : 0);
-    if (recpath && host_len) {
+    const bool recpath0 = (!fastlv || lz_on) && !dict;
+    std::vector<uint64_t> len(recpath0 ? n : 0);
+    if (recpath0 && host_len) {
         std::copy(host_len, host_len + n, len.begin());
-    } else if (recpath) {
+    } else if (recpath0) {
         HIPCHK(hipMemcpyAsync(len.data(), in_len, (size_t)n * 8, hipMemcpyDeviceToHost, s));
         HIPCHK(hipStreamSynchronize(s));
     }
+    // A call of a few short inputs (the drop-in's deflate() of a small buffer) runs the serial
+    // kernel: one launch, against the record path's ~10 launches and plan copy, which set a small
+    // call's latency.  SDZ_DEFLATE_SMALL overrides the byte limit (0: never).
+    uint64_t small_max = kDeflateSmallMax;
+    if (const char* e = getenv("SDZ_DEFLATE_SMALL")) small_max = strtoull(e, nullptr, 10);
+    bool small_call = recpath0 && !ext && !noflush && n <= kDeflateSmallStreams && small_max > 0;
+    for (uint32_t i = 0; small_call && i < n; ++i) small_call = len[i] <= small_max;
+    const bool recpath = recpath0 && !small_call;
     uint64_t tot_all = 0;
     for (uint32_t i = 0; i < (recpath ? n : 0); ++i)
         if (len[i] > 0 && len[i] <= kDeflateRecMax) tot_all += len[i];
@@ -1044,10 +1077,13 @@ int rt::deflate_batch_device(const uint8_t* in, const uint64_t* in_off, const ui
             }
             a.blk = take((size_t)blk * FB_SLOT_BYTES);
             a.cks = (int32_t*)take((size_t)m * 4);
-            uint64_t* d_rp0 = (uint64_t*)take(((size_t)m + 1) * 8);
-            uint32_t* d_tb0 = (uint32_t*)take(((size_t)m + 1) * 4);
-            uint32_t* d_units = (uint32_t*)take(units.size() * 4);
-            uint32_t* d_lzs = (uint32_t*)take(lzs.size() * 4);
+            // the plan arrays in one region, laid out as in the pinned staging (one copy, below)
+            const size_t pb = rp0.size() * 8 + tb0.size() * 4 + units.size() * 4 + lzs.size() * 4;
+            uint8_t* d_plan = take(pb);
+            uint64_t* d_rp0 = (uint64_t*)d_plan;
+            uint32_t* d_tb0 = (uint32_t*)(d_plan + rp0.size() * 8);
+            uint32_t* d_units = d_tb0 + tb0.size();
+            uint32_t* d_lzs = d_units + units.size();
             if (lz_shift) {
                 a.lz_shift = lz_shift;
                 a.nlseg = nlseg;
@@ -1077,7 +1113,6 @@ int rt::deflate_batch_device(const uint8_t* in, const uint64_t* in_off, const ui
             }
             if (o > pool_bytes) return fail(SDZ_API_OOM, "deflate: record plan exceeds its pool");
             // plan -> device through the pinned staging buffer (one copy, waited for below)
-            const size_t pb = rp0.size() * 8 + tb0.size() * 4 + units.size() * 4 + lzs.size() * 4;
             void* pin = nullptr;
             if (int rc = g_plan_pinned.get(pb + 64, &pin)) return rc;
             uint8_t* P = (uint8_t*)pin;
@@ -1087,16 +1122,16 @@ int rt::deflate_batch_device(const uint8_t* in, const uint64_t* in_off, const ui
             if (!units.empty()) std::memcpy(Pu, units.data(), units.size() * 4);
             uint8_t* Pl = Pu + units.size() * 4;
             if (!lzs.empty()) std::memcpy(Pl, lzs.data(), lzs.size() * 4);
-            HIPCHK(hipMemcpyAsync(d_rp0, P, rp0.size() * 8, hipMemcpyHostToDevice, s));
-            HIPCHK(hipMemcpyAsync(d_tb0, P + rp0.size() * 8, tb0.size() * 4, hipMemcpyHostToDevice, s));
-            if (!units.empty()) HIPCHK(hipMemcpyAsync(d_units, Pu, units.size() * 4, hipMemcpyHostToDevice, s));
-            if (!lzs.empty()) HIPCHK(hipMemcpyAsync(d_lzs, Pl, lzs.size() * 4, hipMemcpyHostToDevice, s));
+            HIPCHK(hipMemcpyAsync(d_plan, P, pb, hipMemcpyHostToDevice, s));
             a.rp0 = d_rp0; a.tb0 = d_tb0;
             a.mseg = d_units; a.nmseg = nmseg;
             a.seg_merge = seg_merge ? 1u : 0u;
             a.cunit = d_units + nmseg; a.ncunit = (uint32_t)units.size() - nmseg;
             a.nbmax = nbmax;
             a.wide = m <= 256 ? 1u : 0u;                // few streams: the LDS-staged parse
+            // the last positions' searches in k_dfl_match's LDS window (its plain walk only: a
+            // Deflater's segment list skips final segments, the 4-byte chains have their own)
+            a.tail_in_match = !ext && !match4 && !noflush && !getenv("SDZ_TAIL_HBM") ? 1u : 0u;
             if (int rc = g_plan_pinned.done(s)) return rc;   // (the next get() waits for the plan copies)
             launch_deflate(a, s, side ? side->s : nullptr, side ? side->ev : nullptr);
         } else {

@@ -696,3 +696,52 @@ def test_deflate_tail_window_regression(paradise, n):
     bytes against the oracle."""
     for lv in (4, 6, 9):
         assert sdz.deflate(paradise[:n], {"level": lv}) == O.deflate(paradise[:n], level=lv, format="deflate"), lv
+
+
+@pytest.mark.parametrize("level", [4, 6, 9])
+def test_deflate_last_positions_in_match_kernel(monkeypatch, paradise, level):
+    """The last 262 positions of a stream are searched by k_dfl_match in its last segment's LDS
+    window -- the larger window-offset group, with the bytes the reference's window holds past the
+    input (stale after a slide, zeros before) staged after it -- and the other group by k_dfl_tail
+    (DESIGN §5).  Lengths around the slides (65,274 + 32 KiB k), periodic data whose matches run past
+    the input's end into the stale bytes, and a repeat of the text 32 KiB back: bit-exact against the
+    oracle and against the all-HBM tail search (SDZ_TAIL_HBM=1)."""
+    rng = random.Random(41 + level)
+    inputs = []
+    for n in (300, 16384 + 300, 49414, 49415, 65273, 65274, 65275, 65536, 65537, 65536 + 262, 98041, 98304,
+              98305, 131072 + 5, 163840 - 262, 200000):
+        base = paradise[rng.randrange(len(paradise) - n):][:n] if n < len(paradise) else paradise[:n]
+        inputs.append(base)
+    for n in (65536, 98304, 131100):
+        unit = bytes(rng.getrandbits(8) for _ in range(rng.choice([7, 300, 1000])))
+        inputs.append((unit * (n // len(unit) + 1))[:n])                  # matches into the stale bytes
+        t = bytearray(paradise[:n])
+        t[n - 400:] = t[n - 400 - 32768:n - 32768]                        # the tail repeats 32 KiB back
+        inputs.append(bytes(t))
+    exp = [O.deflate(d, level=level) for d in inputs]
+    got = sdz.deflate_batch(inputs, level=level)
+    for i, (g, e) in enumerate(zip(got, exp)):
+        assert g["status"] == "OK" and g["data"] == e, (level, i, len(inputs[i]))
+    monkeypatch.setenv("SDZ_TAIL_HBM", "1")
+    assert [g["data"] for g in sdz.deflate_batch(inputs, level=level)] == exp
+
+
+def test_deflate_small_calls_serial_kernel(monkeypatch):
+    """A call of at most 16 inputs of at most 1 KiB runs the serial kernel (one launch; the drop-in's
+    deflate() of a small buffer): bit-exact with the oracle at every level and format, the same
+    bytes as the record path (SDZ_DEFLATE_SMALL=0), and the 1,025-byte edge takes the record path."""
+    rng = random.Random(12)
+    bufs = [golden("simple.txt")] + [text_corpus(rng, n) for n in (1, 2, 3, 4, 100, 257, 258, 259, 600, 1023, 1024, 1025)]
+    bufs.append(bytes(rng.getrandbits(8) for _ in range(700)))
+    for level in range(1, 10):
+        for fmt in ("deflate", "gzip", "raw"):
+            for b in bufs[:3] + bufs[-3:]:
+                assert sdz.deflate(b, {"level": level, "format": fmt}) == O.deflate(b, level=level, format=fmt), \
+                    (level, fmt, len(b))
+    for level in (1, 6, 9):
+        got = sdz.deflate_batch(bufs[:16], level=level)
+        exp = [O.deflate(b, level=level) for b in bufs[:16]]
+        assert [g["data"] for g in got] == exp
+        monkeypatch.setenv("SDZ_DEFLATE_SMALL", "0")
+        assert [g["data"] for g in sdz.deflate_batch(bufs[:16], level=level)] == exp
+        monkeypatch.delenv("SDZ_DEFLATE_SMALL")
