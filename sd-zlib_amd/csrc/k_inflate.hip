@@ -2095,7 +2095,7 @@ int run_inflate_rounds(const InflateArgs& a, hipStream_t s, uint32_t* host_activ
     }
     if (rc == 0) {
         if (kernel_ms) (void)hipEventRecord(ev[2], s);
-        launch_inflate_finalize(a, s);
+        if (!a.no_gzip) launch_inflate_finalize(a, s);   // (only gzip streams need it)
         if (kernel_ms) {
             (void)hipEventRecord(ev[3], s);
             (void)hipEventSynchronize(ev[3]);

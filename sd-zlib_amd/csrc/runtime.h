@@ -27,7 +27,7 @@ int ensure_device();
 int inflate_batch_device(const uint8_t* in, const uint64_t* in_off, const uint64_t* in_len, uint8_t* out,
                          const uint64_t* out_off, const uint64_t* out_cap, sdz_inflate_record* rec, uint32_t n,
                          int32_t format, const uint8_t* dict, uint32_t dict_len, void* stream, const uint64_t* host_len,
-                         const uint64_t* host_cap);
+                         const uint64_t* host_cap, bool host_no_gzip = false);
 // a Deflater's own record and link buffers (one stream, positions from 0): records below
 // rec_from and links below pv_from are final from earlier calls and not recomputed
 struct DeflateExt {

@@ -140,10 +140,16 @@ int host_shard(const uint8_t* const* in, const size_t* in_len, uint8_t* const* o
     if (!evs[dev][0]) { HIPCHK(hipEventCreate(&evs[dev][0])); HIPCHK(hipEventCreate(&evs[dev][1])); }
     hipEvent_t e0 = evs[dev][0], e1 = evs[dev][1];
     HIPCHK(hipEventRecord(e0, s));
+    // no input starts with the gzip magic (or the format is raw): the crc32 finalize is not needed
+    bool no_gzip = C.inflate;
+    for (uint32_t k = 0; no_gzip && C.format != SDZ_FMT_RAW && k < m; ++k) {
+        const uint32_t i = R.order[k];
+        no_gzip = in_len[i] < 2 || !(in[i][0] == 0x1f && in[i][1] == 0x8b);
+    }
     int rc = C.inflate
         ? rt::inflate_batch_device(B + o_in, d_meta, d_meta + m, B + o_out, d_meta + 2 * (size_t)m,
                                    d_meta + 3 * (size_t)m, (sdz_inflate_record*)(B + o_rec), m, C.format, d_dict,
-                                   (uint32_t)C.dict_len, s, meta.data() + m, meta.data() + 3 * (size_t)m)
+                                   (uint32_t)C.dict_len, s, meta.data() + m, meta.data() + 3 * (size_t)m, no_gzip)
         : rt::deflate_batch_device(B + o_in, d_meta, d_meta + m, B + o_out, d_meta + 2 * (size_t)m,
                                    d_meta + 3 * (size_t)m, (sdz_deflate_record*)(B + o_rec), m, C.level, C.format,
                                    C.fname, C.fname_len, C.mtime, d_dict, (uint32_t)C.dict_len, s, meta.data() + m);

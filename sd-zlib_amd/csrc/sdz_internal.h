@@ -66,6 +66,7 @@ struct InflateArgs {
     const uint64_t* host_len;    // the n input lengths, when the caller has them on the host
     uint32_t one_round;          // every stream finishes in one round: no active-count read-back
     uint64_t host_cap_max;       // the largest out_cap when the caller has them on the host (0: unknown)
+    uint32_t no_gzip;            // the caller saw every input: none is a gzip stream (no crc32 finalize)
 };
 
 uint64_t inflate_dsave_bytes();  // per stream decode state

@@ -142,8 +142,8 @@ Pool g_inflate_scratch, g_deflate_state, g_tmp, g_stage, g_split, g_find;
 // [128, 256) small results, then the file name
 constexpr size_t kTmpMax = 0, kTmpDictId = 64, kTmpFname = 256;
 constexpr uint64_t kInflaterOutCap = 4ull << 20;   // sdz_inflater: output slot per device call
-constexpr uint64_t kDeflateSmallMax = 1024;         // deflate: calls of short inputs only run serially ...
-constexpr uint32_t kDeflateSmallStreams = 16;       // ... when there are at most this many
+constexpr uint64_t kLzSmallMax = 1024;              // deflate L4-9: inputs up to this size take the lane parse
+constexpr uint64_t kSideMin = 4ull << 20;           // deflate: the input checksum on the side stream from this total
 constexpr uint64_t kDeflaterRedo = 8;             // sdz_deflater: record mode while redone bytes <= 8 x input
 constexpr uint64_t kDeflaterRedoFloor = 64ull << 20;  //   + 64 MiB, then serial
 constexpr size_t kInflaterOnePassMin = 32u << 10;  // sdz_inflater: a first append this long tries the one-pass path
@@ -665,7 +665,7 @@ int sdz_inflate_batch_device(const uint8_t* in, const uint64_t* in_off, const ui
 int rt::inflate_batch_device(const uint8_t* in, const uint64_t* in_off, const uint64_t* in_len, uint8_t* out,
                              const uint64_t* out_off, const uint64_t* out_cap, sdz_inflate_record* rec, uint32_t n,
                              int32_t format, const uint8_t* dict, uint32_t dict_len, void* stream,
-                             const uint64_t* host_len, const uint64_t* host_cap) {
+                             const uint64_t* host_len, const uint64_t* host_cap, bool host_no_gzip) {
     if (int rc = ensure_device()) return rc;
     if (n == 0) return SDZ_API_OK;
     if (!in || !in_off || !in_len || !out || !out_off || !out_cap || !rec)
@@ -697,6 +697,7 @@ int rt::inflate_batch_device(const uint8_t* in, const uint64_t* in_off, const ui
     a.host_len = host_len;
     a.one_round = 0;
     a.host_cap_max = 0;
+    a.no_gzip = host_no_gzip ? 1u : 0u;
     if (host_len && host_cap) {
         bool one = true;
         uint64_t mx = 1;
@@ -888,22 +889,14 @@ int rt::deflate_batch_device(const uint8_t* in, const uint64_t* in_off, const ui
     // the rounds (C3 shape at L1: 0.80 s serial, 6.8 s in rounds).
     const bool fastlv = level <= 3;
     const bool lz_on = !getenv("SDZ_SERIAL_PARSE");
-    const bool recpath0 = (!fastlv || lz_on) && !dict;
-    std::vector<uint64_t> len(recpath0 ? n : 0);
-    if (recpath0 && host_len) {
+    const bool recpath = (!fastlv || lz_on) && !dict;
+    std::vector<uint64_t> len(recpath ? n : 0);
+    if (recpath && host_len) {
         std::copy(host_len, host_len + n, len.begin());
-    } else if (recpath0) {
+    } else if (recpath) {
         HIPCHK(hipMemcpyAsync(len.data(), in_len, (size_t)n * 8, hipMemcpyDeviceToHost, s));
         HIPCHK(hipStreamSynchronize(s));
     }
-    // A call of a few short inputs (the drop-in's deflate() of a small buffer) runs the serial
-    // kernel: one launch, against the record path's ~10 launches and plan copy, which set a small
-    // call's latency.  SDZ_DEFLATE_SMALL overrides the byte limit (0: never).
-    uint64_t small_max = kDeflateSmallMax;
-    if (const char* e = getenv("SDZ_DEFLATE_SMALL")) small_max = strtoull(e, nullptr, 10);
-    bool small_call = recpath0 && !ext && !noflush && n <= kDeflateSmallStreams && small_max > 0;
-    for (uint32_t i = 0; small_call && i < n; ++i) small_call = len[i] <= small_max;
-    const bool recpath = recpath0 && !small_call;
     uint64_t tot_all = 0;
     for (uint32_t i = 0; i < (recpath ? n : 0); ++i)
         if (len[i] > 0 && len[i] <= kDeflateRecMax) tot_all += len[i];
@@ -924,6 +917,12 @@ int rt::deflate_batch_device(const uint8_t* in, const uint64_t* in_off, const ui
         while (lz_shift < 12 && (tot >> (lz_shift + 1)) >= 65536) ++lz_shift;
         if (fastlv) lz_shift = std::max(7u, lz_shift - 2);      // deflate_fast: its state is the position alone
         else if (tot >= (mx << 15) && !noflush && !ext) lz_shift = 0;
+        // a few short inputs (the drop-in's deflate() of a small buffer): one parse launch in
+        // place of the segment parse's seven, which set such a call's latency; SDZ_LZ_SMALL
+        // overrides the byte limit
+        uint64_t lz_small = kLzSmallMax;
+        if (const char* e = getenv("SDZ_LZ_SMALL")) lz_small = strtoull(e, nullptr, 10);
+        if (!fastlv && !noflush && !ext && n <= 256 && mx <= lz_small) lz_shift = 0;
         if (const char* e = getenv("SDZ_LZ_SHIFT"))            // tests: segment size 2^6 .. 2^16
             lz_shift = (uint32_t)std::min(16, std::max(6, atoi(e)));
     }
@@ -995,7 +994,9 @@ int rt::deflate_batch_device(const uint8_t* in, const uint64_t* in_off, const ui
         HIPCHK(hipMemsetAsync(dbg, 0, 64 * sizeof(unsigned long long), s));
     }
     SideStream* side = nullptr;                   // the record path's input checksum runs there
-    if (recpath && side_stream(&side) != SDZ_API_OK) side = nullptr;
+    // (a small call keeps it on its own stream: the fork's event round trips cost more than the
+    // overlap saves)
+    if (recpath && tot_all >= kSideMin && side_stream(&side) != SDZ_API_OK) side = nullptr;
     timing_begin(s);
     for (size_t j = 0; j + 1 < cb.size(); ++j) {
         const uint32_t b = cb[j], m = cb[j + 1] - cb[j];

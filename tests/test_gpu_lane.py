@@ -57,9 +57,18 @@ def test_distinct_64k_slices_lane_decoder(fmt):
     streams = [O.deflate(p, level=1 + i % 9, format=fmt, mtime=i) for i, p in enumerate(plain)]
     raw = fmt == "raw"
     gpu = sdz.inflate_batch(streams, [65536 + 64] * len(streams), sdz.FMT_RAW if raw else sdz.FMT_CONTAINER)
+    stalls = 0
     for g, s, p in zip(gpu, streams, plain):
-        assert_same(g, O.inflater_run([s], raw=raw), s)
+        o = O.inflater_run([s], raw=raw)
+        assert_same(g, o, s)
+        if raw and not o["complete"]:
+            # infcodes.ts:367-387: a raw stream whose last code ends within the table's root bits
+            # of the input's end stalls in the reference too (TRUNCATED); its bytes so far agree
+            stalls += 1
+            assert g["status"] == "TRUNCATED" and p.startswith(g["data"])
+            continue
         assert g["status"] == "OK" and g["data"] == p
+    assert stalls < len(streams) // 4
 
 
 def test_distinct_slices_lane_vs_wave_records(monkeypatch):

@@ -726,22 +726,25 @@ def test_deflate_last_positions_in_match_kernel(monkeypatch, paradise, level):
     assert [g["data"] for g in sdz.deflate_batch(inputs, level=level)] == exp
 
 
-def test_deflate_small_calls_serial_kernel(monkeypatch):
-    """A call of at most 16 inputs of at most 1 KiB runs the serial kernel (one launch; the drop-in's
-    deflate() of a small buffer): bit-exact with the oracle at every level and format, the same
-    bytes as the record path (SDZ_DEFLATE_SMALL=0), and the 1,025-byte edge takes the record path."""
+
+def test_deflate_small_inputs_lane_parse(monkeypatch):
+    """A call of inputs of at most 1 KiB (the drop-in's deflate() of a small buffer) parses with one
+    lane-per-stream launch instead of the segment-parallel parse's seven: bit-exact with the oracle at
+    every level and format, and the same bytes as the segment parse (SDZ_LZ_SMALL=0); 1,025 bytes is
+    past the limit."""
     rng = random.Random(12)
     bufs = [golden("simple.txt")] + [text_corpus(rng, n) for n in (1, 2, 3, 4, 100, 257, 258, 259, 600, 1023, 1024, 1025)]
     bufs.append(bytes(rng.getrandbits(8) for _ in range(700)))
     for level in range(1, 10):
         for fmt in ("deflate", "gzip", "raw"):
             for b in bufs[:3] + bufs[-3:]:
-                assert sdz.deflate(b, {"level": level, "format": fmt}) == O.deflate(b, level=level, format=fmt), \
+                g = sdz.deflate_batch([b], level=level, format=fmt, file_name_latin1=b"s.txt", mtime=77)[0]
+                assert g["data"] == O.deflate(b, level=level, format=fmt, file_name="s.txt", mtime=77), \
                     (level, fmt, len(b))
-    for level in (1, 6, 9):
-        got = sdz.deflate_batch(bufs[:16], level=level)
-        exp = [O.deflate(b, level=level) for b in bufs[:16]]
-        assert [g["data"] for g in got] == exp
-        monkeypatch.setenv("SDZ_DEFLATE_SMALL", "0")
-        assert [g["data"] for g in sdz.deflate_batch(bufs[:16], level=level)] == exp
-        monkeypatch.delenv("SDZ_DEFLATE_SMALL")
+    for level in (4, 6, 9):
+        exp = [O.deflate(b, level=level) for b in bufs]
+        assert [g["data"] for g in sdz.deflate_batch(bufs, level=level)] == exp
+        monkeypatch.setenv("SDZ_LZ_SMALL", "0")
+        assert [g["data"] for g in sdz.deflate_batch(bufs, level=level)] == exp
+        monkeypatch.delenv("SDZ_LZ_SMALL")
+    assert sdz.deflate(golden("simple.txt"), {"level": 6}) == golden("simple.deflate")
