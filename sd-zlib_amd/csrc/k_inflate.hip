@@ -1234,7 +1234,11 @@ __device__ IL_HOT_ATTR void hot_epoch(DSave* S, const uint8_t* inp, uint64_t ile
     for (int k = 1; k <= 15; ++k) { LL.lim[k] -= 1u; DD.lim[k] -= 1u; }   // tsel_hot's form
 #endif
     do {
-        if (hot) ring_step(H);
+        // every lane runs the ring step: an idle lane's (vp == vend, ns 0, no tokens) changes
+        // nothing.  Under `if (hot)` its reader fields were dead on the idle path, which LLVM then
+        // fed as undef into the loop's phis (seen in the IR of the hot_epoch-inlined variant that
+        // faulted in round 4); here every value the loop reads is defined for every lane
+        ring_step(H);
 #if IL_FULL_AT_RING
         // token room checked once per 4 steps: at most 2 tokens per step
         if (H.ntok + 3u + 8u > H.tcap) H.full = true;
