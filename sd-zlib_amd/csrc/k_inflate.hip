@@ -91,6 +91,12 @@ struct Core {
     uint32_t ntok, tcap;
     uint32_t litw, nlit;
     bool full;
+#ifdef IL_HOT_CHECK
+    // development (DESIGN §3.4): the readable input span and the stream, for bounds checks
+    const uint8_t* chk_lo;
+    const uint8_t* chk_hi;
+    uint32_t chk_id;
+#endif
 };
 // The symbol loop's input: w2 (next dword) is fed from a per-lane 64-byte LDS ring.
 // Once per 4 loop iterations -- a wave-uniform point -- each lane commits the 16-32
@@ -106,20 +112,18 @@ struct Hot : Core {
     g_uint4* vp;                      // next 16 input bytes to load
     g_uint4* vend;                    // first 16-byte chunk past the input
     uint32_t* ring;
-#ifdef IL_HOT_CHECK
-    // development (DESIGN §3.4): the readable input span and the stream, for bounds checks
-    const uint8_t* chk_lo;
-    const uint8_t* chk_hi;
-    uint32_t chk_id;
-#endif
 };
 #ifdef IL_HOT_CHECK
 // a hot-path access outside its bounds: reported once per lane, the access skipped and the
 // lane stopped (status BAD_RECORD), so the run ends without a fault
+// (one out-of-line report: printf expanded at every inlined check site made the build take hours)
+__device__ __noinline__ void hot_check_fail(int what, uint32_t id, unsigned long long a, unsigned long long b,
+                                            unsigned long long lo, unsigned long long hi) {
+    printf("IL_HOT_CHECK site %d stream %u lane %u: %llx %llx lo %llx hi %llx\n", what, id, threadIdx.x, a, b, lo, hi);
+}
 #define HOT_CHECK(L, cond, what, a, b)                                                            \
-    (!(cond) ? (printf("IL_HOT_CHECK %s stream %u lane %u: %llx %llx lo %llx hi %llx\n", what,    \
-                       (L).chk_id, threadIdx.x, (unsigned long long)(a), (unsigned long long)(b),  \
-                       (unsigned long long)(L).chk_lo, (unsigned long long)(L).chk_hi),           \
+    (!(cond) ? (hot_check_fail(what, (L).chk_id, (unsigned long long)(a), (unsigned long long)(b), \
+                               (unsigned long long)(L).chk_lo, (unsigned long long)(L).chk_hi),   \
                 (L).mode = LM_DONE, (L).status = SDZ_BAD_RECORD, (L).full = true, false) : true)
 #else
 #define HOT_CHECK(L, cond, what, a, b) true
@@ -154,7 +158,11 @@ __device__ __forceinline__ void br_setavail(Core& L, uint64_t bitpos, uint64_t t
 }
 
 __device__ __forceinline__ void br_refill(Lane& L) {
-    if (L.bo >= 32) { L.w0 = L.w1; L.w1 = *L.dp++; L.bo -= 32; L.avail -= 32; }
+    if (L.bo >= 32) {
+        if (!HOT_CHECK(L, (const uint8_t*)L.dp >= L.chk_lo && (const uint8_t*)(L.dp + 1) <= L.chk_hi, 4,
+                       (uintptr_t)L.dp, 0)) { L.bo = 0; L.avail = 0; return; }
+        L.w0 = L.w1; L.w1 = *L.dp++; L.bo -= 32; L.avail -= 32;
+    }
 }
 // read n <= 24 bits; returns false (stall) if the input does not hold them
 __device__ __forceinline__ bool br_get(Lane& L, int n, uint32_t& v) {
@@ -221,7 +229,7 @@ __device__ __forceinline__ void ring_step(Hot& L) {
     tok_flush_hot(L);
     uint32_t lvl = L.wpos - L.rpos;
     if (lvl <= 48 && L.vp < L.vend) {
-        if (!HOT_CHECK(L, (const uint8_t*)L.vp >= L.chk_lo && (const uint8_t*)(L.vp + 2) <= L.chk_hi, "ring load",
+        if (!HOT_CHECK(L, (const uint8_t*)L.vp >= L.chk_lo && (const uint8_t*)(L.vp + 2) <= L.chk_hi, 1,
                        (uintptr_t)L.vp, (uintptr_t)L.vend)) return;
         L.s0 = *L.vp++;
         L.ns = 1;
@@ -530,6 +538,8 @@ __device__ __forceinline__ void with_dummies(const Tree& T, uint32_t (&c)[5]) {
 // one flush per 32 tokens each), so this block runs nearly every step: all LDS reads are
 // issued before the first store (one wait, not one per 16 bytes).
 __device__ __forceinline__ void tok_flush_stage(Core& L) {
+    if (!HOT_CHECK(L, L.ntok >= IL_TSTAGE && L.ntok <= L.tcap && (L.ntok & (IL_TSTAGE - 1)) == 0, 5,
+                   L.ntok, L.tcap)) return;
     const uint2* s = (const uint2*)L.ts;
     GLB uint4* d = (GLB uint4*)(L.tb + (L.ntok - IL_TSTAGE));
     uint2 v[IL_TSTAGE / 2];
@@ -599,7 +609,7 @@ __device__ __forceinline__ void tok_flush_hot(Hot& L) {
     if (!IL_UNIFORM_FLUSH) return;
     const bool f = L.ntok - L.nfl >= 16u;
     if (__ballot(f)) {
-        if (f && HOT_CHECK(L, L.nfl + 16u <= L.tcap && L.nfl + 16u <= L.ntok && (L.nfl & 15u) == 0, "token flush",
+        if (f && HOT_CHECK(L, L.nfl + 16u <= L.tcap && L.nfl + 16u <= L.ntok && (L.nfl & 15u) == 0, 2,
                            L.nfl, ((uint64_t)L.ntok << 32) | L.tcap)) {
             const uint2* st = (const uint2*)(L.ts + (L.nfl & (IL_TSTAGE - 1)));
             GLB uint4* d = (GLB uint4*)(L.tb + L.nfl);
@@ -614,6 +624,7 @@ __device__ __forceinline__ void tok_flush_hot(Hot& L) {
 }
 __device__ __forceinline__ void tok_finish(Core& L) {
     tok_flush_lits(L);
+    if (!HOT_CHECK(L, L.ntok <= L.tcap, 6, L.ntok, L.tcap)) return;
     uint32_t k = L.ntok & (IL_TSTAGE - 1), b = L.ntok - k;
     for (uint32_t j = 0; j < k; ++j) L.tb[b + j] = L.ts[j];
 }
@@ -1089,6 +1100,11 @@ __device__ IL_COLD_ATTR void cold_run(DSave* S, const uint8_t* inp, uint64_t ile
     uint8_t* region = lane_region();
     L.ts = lane_stage();
     L.tb = tb; L.tcap = tcap; L.lens = lens;
+#ifdef IL_HOT_CHECK
+    L.chk_lo = (const uint8_t*)((uintptr_t)inp & ~(uintptr_t)15);
+    L.chk_hi = inp + ilen + 64;
+    L.chk_id = blockIdx.x * IL_STREAMS + lane_slot();
+#endif
     L.streaming = MODE == 1; L.stall = 0; L.ubit = 0;
     if (init) {
         L.mode = LM_TYPE; L.last = 0; L.status = SDZ_OK; L.zmsg = 0; L.container = SDZ_CONTAINER_RAW;
@@ -1155,7 +1171,7 @@ __device__ __forceinline__ void hot_load(Hot& H, HTree& LL, HTree& DD, const DSa
     H.chk_id = blockIdx.x * IL_STREAMS + lane_slot();
     {
         const uint8_t* a = (const uint8_t*)(((uintptr_t)(inp + (S->bitpos >> 3))) & ~(uintptr_t)15);
-        if (!HOT_CHECK(H, S->bitpos <= ilen * 8 && a >= H.chk_lo && a + 64 <= H.chk_hi + 16, "init load",
+        if (!HOT_CHECK(H, S->bitpos <= ilen * 8 && a >= H.chk_lo && a + 64 <= H.chk_hi + 16, 3,
                        S->bitpos, ilen)) {
             H.mode = LM_DONE;
             return;
@@ -1370,7 +1386,10 @@ __global__ __launch_bounds__(IL_THREADS, 1) void k_inflate_decode(InflateArgs A,
     }
     {
         Core H;                                          // flush the token stage
-        H.tb = tb; H.ts = ts; H.ntok = S->ntok; H.litw = S->litw; H.nlit = S->nlit;
+        H.tb = tb; H.ts = ts; H.ntok = S->ntok; H.litw = S->litw; H.nlit = S->nlit; H.tcap = tcap;
+#ifdef IL_HOT_CHECK
+        H.chk_lo = H.chk_hi = nullptr; H.chk_id = sid;
+#endif
         tok_finish(H);
         S->ntok = H.ntok; S->litw = 0; S->nlit = 0;
         A.ntok[sid] = H.ntok;
@@ -1907,7 +1926,10 @@ __global__ __launch_bounds__(IL_THREADS, 1) void k_inflate_wcold(InflateArgs A, 
     if (lane && !init) epochs<0>(A, S, inp, ilen, cap, tb, tcap, lens, true, G);
     else cold_run<0>(S, inp, ilen, cap, tb, tcap, lens, A.format, A.dict != nullptr, did, init, G, force_slow);
     Core H;                                              // flush the token stage
-    H.tb = tb; H.ts = ts; H.ntok = S->ntok; H.litw = S->litw; H.nlit = S->nlit;
+    H.tb = tb; H.ts = ts; H.ntok = S->ntok; H.litw = S->litw; H.nlit = S->nlit; H.tcap = tcap;
+#ifdef IL_HOT_CHECK
+    H.chk_lo = H.chk_hi = nullptr; H.chk_id = sid;
+#endif
     tok_finish(H);
     S->ntok = H.ntok; S->litw = 0; S->nlit = 0;
     if (S->mode == LM_CODES)
