@@ -176,6 +176,14 @@ __device__ __forceinline__ bool br_get(Lane& L, int n, uint32_t& v) {
 __device__ __forceinline__ void br_init(Lane& L, const uint8_t* p, uint64_t bitpos, uint64_t total_bits) {
     uintptr_t addr = (uintptr_t)(p + (bitpos >> 3));
     L.dp = (const uint32_t*)(addr & ~(uintptr_t)3);
+#ifdef IL_HOT_CHECK
+    if (!HOT_CHECK(L, bitpos <= total_bits && (const uint8_t*)L.dp >= L.chk_lo && (const uint8_t*)(L.dp + 2) <= L.chk_hi, 7,
+                   bitpos, total_bits)) {
+        L.dp = (const uint32_t*)L.chk_lo;
+        bitpos = 0;
+        addr = (uintptr_t)L.chk_lo;
+    }
+#endif
     L.w0 = L.dp[0];
     L.w1 = L.dp[1];
     L.dp += 2;
@@ -736,6 +744,7 @@ __device__ __forceinline__ bool setup_dynamic(Lane& L, Tree& LL, Tree& DD, uint8
         uint32_t c = cls[(g7 == 1 && left > 0) ? 0 : (off + (int32_t)(rc >> (7 - len)))];
         if (g7 == 1 && left > 0) len = 1;
         br_drop(L, (uint32_t)len);
+        if (!HOT_CHECK(L, idx < (int)kInflateScratchPerStream, 8, idx, total)) return false;
         if (c < 16) {
             L.lens[idx++] = (uint8_t)c;
             prev = (int)c;
