@@ -2053,6 +2053,21 @@ bool inflate_wave_policy(uint32_t n, const uint64_t* host_len, const uint64_t* d
 }
 uint64_t inflate_rsave_bytes() { return sizeof(RSave); }
 
+// SDZ_DEBUG_SYNC=1 (development): wait after every launch of the round driver and report the first
+// kernel whose run ends in an error, by name (a fault is otherwise seen at the next API call)
+static bool dbg_sync_on() {
+    static const bool on = getenv("SDZ_DEBUG_SYNC") != nullptr;
+    return on;
+}
+static int dbg_sync(hipStream_t s, const char* what, uint32_t round, uint32_t it) {
+    if (!dbg_sync_on()) return 0;
+    const hipError_t e = hipStreamSynchronize(s);
+    if (e == hipSuccess) return 0;
+    fprintf(stderr, "sdz debug sync: %s (round %u, step %u): %s\n", what, round, it, hipGetErrorString(e));
+    return -1;
+}
+#define DBG_SYNC(s, what, round, it) do { if (dbg_sync((s), (what), (round), (it))) { rc = -1; break; } } while (0)
+
 // host driver: rounds of (decode, resolve) until no stream needs another round.
 // kernel_ms (optional, 3 entries) accumulates decode / resolve / finalize times.
 int run_inflate_rounds(const InflateArgs& a, hipStream_t s, uint32_t* host_active, float* kernel_ms,
@@ -2082,8 +2097,10 @@ int run_inflate_rounds(const InflateArgs& a, hipStream_t s, uint32_t* host_activ
             for (uint32_t it = 0;; ++it) {
                 hipLaunchKernelGGL(k_inflate_wcold, g1, dim3(IL_THREADS), 0, s, a, round, it == 0 ? 1u : 0u,
                                    it >= lane_after ? 1u : 0u);
+                DBG_SYNC(s, "k_inflate_wcold", round, it);
                 if (hipMemsetAsync(a.active, 0, 2 * sizeof(uint32_t), s) != hipSuccess) { rc = -1; break; }
                 hipLaunchKernelGGL(k_inflate_wdec, dim3(a.n), dim3(64), 0, s, a, round);
+                DBG_SYNC(s, "k_inflate_wdec", round, it);
                 if (hipMemcpyAsync(host_active, a.active + 1, sizeof(uint32_t), hipMemcpyDeviceToHost, s) != hipSuccess ||
                     hipStreamSynchronize(s) != hipSuccess) { rc = -1; break; }
                 if (*host_active == 0) break;
@@ -2096,6 +2113,7 @@ int run_inflate_rounds(const InflateArgs& a, hipStream_t s, uint32_t* host_activ
             if (rc) break;
         } else {
             hipLaunchKernelGGL(k_inflate_decode, g1, dim3(IL_THREADS), 0, s, a, round);
+            DBG_SYNC(s, "k_inflate_decode", round, 0);
         }
         if (round == 0 && hook) {
             if (int hr = hook(hook_ctx)) { rc = hr; break; }
@@ -2106,15 +2124,28 @@ int run_inflate_rounds(const InflateArgs& a, hipStream_t s, uint32_t* host_activ
                 // streams whose chain broke, serially from their start
                 const SplitPlan& P = *a.split_plan;
                 if (hipStreamWaitEvent(s, (hipEvent_t)P.ready, 0) != hipSuccess) { rc = -1; break; }
+                if (dbg_sync_on()) {                              // the side stream's finder and segments
+                    const hipError_t e = hipEventSynchronize((hipEvent_t)P.ready);
+                    if (e != hipSuccess) {
+                        fprintf(stderr, "sdz debug sync: side stream (split finder, segment decode): %s\n",
+                                hipGetErrorString(e));
+                        rc = -1;
+                        break;
+                    }
+                }
                 launch_seg_chain(a, P.sp, P.nsplit, P.seg, P.cand, P.segD, P.chain, P.chain_tok, a.split_state, s);
+                DBG_SYNC(s, "k_seg_chain", round, 0);
                 InflateArgs f = a;
                 f.fallback_pass = 1;
                 hipLaunchKernelGGL(k_inflate_decode, g1, dim3(IL_THREADS), 0, s, f, 0u);
+                DBG_SYNC(s, "k_inflate_decode (fallback pass)", round, 0);
             }
             launch_seg_feed(a, round, s);
+            DBG_SYNC(s, "k_seg_feed", round, 0);
         }
         if (kernel_ms) (void)hipEventRecord(ev[1], s);
         hipLaunchKernelGGL(k_inflate_resolve, g2, dim3(resolve_block_threads()), 0, s, a, round);
+        DBG_SYNC(s, "k_inflate_resolve", round, 0);
         if (kernel_ms) (void)hipEventRecord(ev[2], s);
         if (a.one_round && !a.split_plan) break;         // (times read after finalize)
         if (hipMemcpyAsync(host_active, a.active, sizeof(uint32_t), hipMemcpyDeviceToHost, s) != hipSuccess) { rc = -1; break; }

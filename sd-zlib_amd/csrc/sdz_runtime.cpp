@@ -519,6 +519,8 @@ int inflate_split_start(const InflateArgs& a, hipStream_t s, PoolUse& find_use, 
     // (every candidate was a survivor: the survivor list's room holds the packed candidates)
     launch_split_pack(H.d_sp1, ns, H.d_cand1, H.d_surv, H.d_npacked, H.side->s);
     HIPCHK(hipGetLastError());
+    if (getenv("SDZ_DEBUG_SYNC") && hipStreamSynchronize(H.side->s) != hipSuccess)   // (development)
+        return fail(SDZ_API_HIP_ERROR, "debug sync: split finder");
     H.plan.nsplit = ns;
     return SDZ_API_OK;
 }
@@ -624,6 +626,8 @@ int inflate_split_finish(void* ctx) {
     g.segtok = H.plan.segtok;
     launch_seg_decode(g, ss);
     HIPCHK(hipGetLastError());
+    if (getenv("SDZ_DEBUG_SYNC") && hipStreamSynchronize(ss) != hipSuccess)            // (development)
+        return fail(SDZ_API_HIP_ERROR, "debug sync: segment decode");
     HIPCHK(hipEventRecord(H.side->ev, ss));
     H.plan.segD = g.dsave;
     H.plan.ready = (void*)H.side->ev;
