@@ -2097,10 +2097,22 @@ __global__ __launch_bounds__(64) void k_dfl_parse(DeflateArgs A) {
 // stage the records in LDS chunks ahead of lane 0, which parses from LDS (a lone lane waits
 // on every dependent HBM load otherwise)
 #define PW_THREADS 256
+#ifndef PW_UNIFORM
+#define PW_UNIFORM 1
+#endif
 #define PW_CHUNK 4096                                    // records per LDS chunk (>= MAX_MATCH)
+#ifdef DT_PROF
+#define PW_T(k) do { if (blockIdx.x == 0 && tid == 0) tw[k] = wall_clock64(); } while (0)
+#else
+#define PW_T(k) do { } while (0)
+#endif
 __global__ __launch_bounds__(PW_THREADS) void k_dfl_parse_wide(DeflateArgs A) {
     __shared__ uint64_t buf[2][PW_CHUNK];
     const uint32_t sid = blockIdx.x, tid = threadIdx.x;
+#ifdef DT_PROF
+    uint64_t tw[6] = {};
+#endif
+    PW_T(0);
     if (sid >= A.n) return;
     GLB DSlab* S = (GLB DSlab*)(A.state + (uint64_t)sid * SLAB_BYTES);
     GLB FStream* F = (GLB FStream*)S->window;
@@ -2112,30 +2124,54 @@ __global__ __launch_bounds__(PW_THREADS) void k_dfl_parse_wide(DeflateArgs A) {
     const int nch = (n + PW_CHUNK - 1) / PW_CHUNK;
     for (int i = (int)tid; i < PW_CHUNK && i < n; i += PW_THREADS) buf[0][i] = rec[i];
     __syncthreads();
+    PW_T(1);
     PState st;
     bool done = false;
-    if (tid == 0) ps_init(st, A, sid, n);
+#if PW_UNIFORM
+    // wave 0 runs the parse with every lane on the same values: the state is wave-uniform
+    // (scalar registers, scalar branches) instead of lane 0's masked vector code; the
+    // symbol and block stores are made by all 64 lanes to one address
+    const bool parser = __builtin_amdgcn_readfirstlane(tid) < 64;
+#else
+    const bool parser = tid == 0;
+#endif
+    if (parser) ps_init(st, A, sid, n);
+    PW_T(2);
     for (int c = 0; c < nch; ++c) {
         const int c1 = c + 1;
         if (tid >= 64 && c1 < nch) {                    // stage the next chunk
             const int b0 = c1 * PW_CHUNK, m = n - b0 < PW_CHUNK ? n - b0 : PW_CHUNK;
             for (int i = (int)tid - 64; i < m; i += PW_THREADS - 64) buf[c1 & 1][i] = rec[b0 + i];
         }
-        if (tid == 0 && !done) {
+        if (parser && !done) {
             const int end = (c + 1) * PW_CHUNK, b0 = c * PW_CHUNK;
             const uint64_t* cb = buf[c & 1];
             for (;;) {
                 if (st.strstart >= end) break;             // the next chunk (a step moves <= MAX_MATCH)
                 if (ps_fill(st)) { done = true; break; }
-                ps_step(st, cb[st.strstart - b0]);
+                const uint64_t rv = cb[st.strstart - b0];
+#if PW_UNIFORM
+                const uint64_t r = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)rv) |
+                                   ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(rv >> 32)) << 32);
+#else
+                const uint64_t r = rv;
+#endif
+                ps_step(st, r);
             }
         }
         __syncthreads();
     }
-    if (tid == 0) {
+    PW_T(3);
+    if (parser) {
         // (the records past the last chunk: none -- a stream's positions end at n)
         ps_finish(st, in, F);
     }
+    PW_T(4);
+#ifdef DT_PROF
+    if (sid == 0 && tid == 0)
+        printf("PW_PROF n %d | stage %lu init %lu loop %lu finish %lu [x10ns]\n", n, tw[1] - tw[0], tw[2] - tw[1],
+               tw[3] - tw[2], tw[4] - tw[3]);
+#endif
 }
 
 // ------------------------------------------------------------------ segment-parallel lazy parse
@@ -2843,6 +2879,622 @@ struct LTreeCtx {
     }
 };
 
+#ifndef DT_WAVE
+#define DT_WAVE 1                         // wave-cooperative k_dfl_trees (round 5; 0: lane 0 alone)
+#endif
+#if DT_WAVE
+// k_dfl_trees, wave-cooperative: the same trees and header as _tr_flush_block
+// (deftree.ts:190-267 build_tree, 60-132 gen_bitlen, 155-182 gen_codes, deflate.ts:267-429
+// scan_tree / send_tree), with only the heap (pqdownheap and the merge loop, whose tie
+// order decides the code lengths) left to one lane.  A lone lane pays the full LDS or HBM
+// latency on every dependent access, so everything that is not the heap is spread over the
+// wave or kept in registers:
+// - the heap holds packed keys freq << 16 | depth << 10 | node, so smaller() (deftree.ts /
+//   deflate.ts:233-238: freq, then depth, ties taken as "smaller") is one compare of key >> 10
+//   with no indirection through tree[] and depth[], and both children come in one 8-byte load;
+// - gen_bitlen: every node's depth below the root by chasing its parent links, all lanes at
+//   once; Len = min(depth, max_length) and overflow = #nodes deeper than max_length are what
+//   the reference's top-down loop computes (Len[dad] is already clamped there); the overflow
+//   repair (rare) is the reference's loop on lane 0;
+// - gen_codes: next_code[len] plus the symbol's rank among the same-length symbols below it
+//   (ballots), as the reference's in-order next_code[len]++;
+// - scan_tree / send_tree: the code lengths read 64 at a time into a register and taken
+//   lane by lane (readlane), the bit-length counts in a lane-indexed register, the header
+//   bits in a register accumulator stored a word at a time;
+// - the static trees and extra-bit tables are staged in LDS (global loads of a lone lane
+//   were most of this kernel's time on a one-block call: 149 us on simple.txt).
+#define DT_NODE_BITS 10                   // node ids < 573
+#ifdef DT_PROF                            // development: phase clocks of the first (stream, block), printf
+#define DT_T(a, k) do { if (a) (a)[k] = wall_clock64(); } while (0)
+#else
+#define DT_T(a, k) do { } while (0)
+#endif
+#define DT_KEY(f, d, n) (((uint32_t)(f) << 16) | ((uint32_t)(d) << DT_NODE_BITS) | (uint32_t)(n))
+struct WTree {
+    uint16_t* order;                      // the reference's heap[heap_max..HEAP_SIZE-1]: node order
+    uint32_t* hk;                         // heap of packed keys, [1..heap_len] (8-byte aligned)
+    uint32_t* blc;                        // bl_count[0..15]
+    int* xch;                             // lane 0 -> wave
+    int opt_len, static_len;              // wave-uniform
+};
+__device__ __forceinline__ int dt_rdl(uint32_t v, int i) { return __builtin_amdgcn_readlane((int)v, i); }
+__device__ __forceinline__ int dt_sum(int v) {
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+}
+__device__ __forceinline__ void dt_down(uint32_t* hk, int len, int k) {   // pqdownheap, deflate.ts:241-263
+    const uint32_t v = hk[k];
+    int j = k << 1;
+    while (j <= len) {
+        const uint2 ab = *(const uint2*)(hk + j);                  // j even: both children
+        uint32_t c = ab.x;
+        if (j < len && (ab.y >> DT_NODE_BITS) <= (ab.x >> DT_NODE_BITS)) { c = ab.y; j++; }
+        if ((v >> DT_NODE_BITS) <= (c >> DT_NODE_BITS)) break;
+        hk[k] = c;
+        k = j;
+        j <<= 1;
+    }
+    hk[k] = v;
+}
+#ifndef DT_RHEAP
+#define DT_RHEAP 1                        // heaps of <= 62 entries in one register (0: all in LDS)
+#endif
+// A heap of at most 62 entries in one register: entry i at lane i, read with readlane at a
+// wave-uniform index and written with a lane compare and select; the compares run on scalars.
+// In LDS each level of a pqdownheap is a dependent load (23 us of a one-block call's ~25-leaf
+// heap, DT_PROF); a 5-register heap for all sizes (the index's register picked by a switch)
+// measured twice as slow as LDS: its branches cost more than the loads.
+__device__ __forceinline__ void dt_down_1(int& H, int len, int k) {   // pqdownheap, deflate.ts:241-263
+    const int me = (int)threadIdx.x;
+    const uint32_t v = (uint32_t)__builtin_amdgcn_readlane(H, k);
+    int j = k << 1;
+    while (j <= len) {
+        uint32_t c = (uint32_t)__builtin_amdgcn_readlane(H, j);
+        if (j < len) {
+            const uint32_t c1 = (uint32_t)__builtin_amdgcn_readlane(H, j + 1);
+            if ((c1 >> DT_NODE_BITS) <= (c >> DT_NODE_BITS)) { c = c1; j++; }
+        }
+        if ((v >> DT_NODE_BITS) <= (c >> DT_NODE_BITS)) break;
+        H = me == k ? (int)c : H;
+        k = j;
+        j <<= 1;
+    }
+    H = me == k ? (int)v : H;
+}
+// build_tree (deftree.ts:190-267) with gen_bitlen and gen_codes; returns max_code.  tree:
+// LDS, tsize entries; stree: the static tree (LDS) or null; called by the whole wave.
+__device__ int dt_build(WTree& W, uint16_t* tree, const uint16_t* stree, const uint8_t* extra, int base,
+                        int elems, int max_length, uint64_t* tp = nullptr) {
+    const uint32_t lane = threadIdx.x;
+    const uint64_t below = (1ull << lane) - 1ull;
+    int heap_len = 0, max_code = -1;
+    for (int cb = 0; cb < elems; cb += 64) {                      // the leaves in symbol order
+        const int n = cb + (int)lane;
+        const uint32_t f = n < elems ? tree[n * 2] : 0u;
+        const uint64_t m = __ballot(f != 0);
+        if (f) W.hk[heap_len + 1 + (int)__popcll(m & below)] = DT_KEY(f, 0, n);
+        else if (n < elems) tree[n * 2 + 1] = 0;
+        heap_len += (int)__popcll(m);
+        if (m) max_code = cb + 63 - (int)__clzll(m);
+    }
+    while (heap_len < 2) {                                        // at least two codes
+        const int node = max_code < 2 ? ++max_code : 0;
+        ++heap_len;
+        if (lane == 0) { W.hk[heap_len] = DT_KEY(1, 0, node); tree[node * 2] = 1; }
+        W.opt_len--;
+        if (stree) W.static_len -= stree[node * 2 + 1];
+    }
+    const int nodes = 2 * heap_len - 1, hmax = HEAP_SIZE - nodes;
+    __syncthreads();
+    DT_T(tp, 0);
+#if DT_RHEAP
+    if (heap_len <= 62) {
+        int H = (int)W.hk[lane];
+        int len = heap_len, node = elems, hm = HEAP_SIZE;
+        for (int k = len / 2; k >= 1; --k) dt_down_1(H, len, k);
+        do {
+            const uint32_t a = (uint32_t)__builtin_amdgcn_readlane(H, 1);
+            const int tl = __builtin_amdgcn_readlane(H, len--);
+            H = lane == 1 ? tl : H;
+            dt_down_1(H, len, 1);
+            const uint32_t b = (uint32_t)__builtin_amdgcn_readlane(H, 1);
+            const uint32_t na = a & 1023u, nb = b & 1023u;
+            hm -= 2;
+            const uint32_t da = (a >> DT_NODE_BITS) & 63u, db = (b >> DT_NODE_BITS) & 63u;
+            const uint32_t f = (a >> 16) + (b >> 16);
+            if (lane == 0) {
+                W.order[hm + 1] = (uint16_t)na;
+                W.order[hm] = (uint16_t)nb;
+                tree[node * 2] = (uint16_t)f;
+                tree[na * 2 + 1] = tree[nb * 2 + 1] = (uint16_t)node;   // Dad
+            }
+            H = lane == 1 ? (int)DT_KEY(f, (da > db ? da : db) + 1u, node) : H;
+            node++;
+            dt_down_1(H, len, 1);
+        } while (len >= 2);
+        if (lane == 0) W.order[hm - 1] = (uint16_t)((uint32_t)__builtin_amdgcn_readlane(H, 1) & 1023u);
+    } else
+#endif
+    if (lane == 0) {
+        int len = heap_len, node = elems, hm = HEAP_SIZE;
+        for (int k = len / 2; k >= 1; --k) dt_down(W.hk, len, k);
+        do {
+            const uint32_t a = W.hk[1];
+            W.hk[1] = W.hk[len--];
+            dt_down(W.hk, len, 1);
+            const uint32_t b = W.hk[1];
+            const uint32_t na = a & 1023u, nb = b & 1023u;
+            W.order[--hm] = (uint16_t)na;
+            W.order[--hm] = (uint16_t)nb;
+            const uint32_t da = (a >> DT_NODE_BITS) & 63u, db = (b >> DT_NODE_BITS) & 63u;
+            const uint32_t f = (a >> 16) + (b >> 16);
+            tree[node * 2] = (uint16_t)f;
+            tree[na * 2 + 1] = tree[nb * 2 + 1] = (uint16_t)node;       // Dad
+            W.hk[1] = DT_KEY(f, (da > db ? da : db) + 1u, node);
+            node++;
+            dt_down(W.hk, len, 1);
+        } while (len >= 2);
+        W.order[--hm] = (uint16_t)(W.hk[1] & 1023u);
+    }
+    __syncthreads();
+    DT_T(tp, 1);
+    // gen_bitlen: depths below the root, then Len, bl_count, opt_len, static_len
+    const int root = W.order[hmax];
+    if (lane < 16) W.blc[lane] = 0;
+    constexpr int NC = (HEAP_SIZE + 63) / 64;
+    int nd[NC], dp[NC];
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+        const int h = hmax + 1 + c * 64 + (int)lane;
+        nd[c] = h < HEAP_SIZE ? W.order[h] : root;
+        dp[c] = 0;
+    }
+    {
+        int x[NC];
+#pragma unroll
+        for (int c = 0; c < NC; ++c) x[c] = nd[c];
+        for (;;) {
+            bool live = false;
+#pragma unroll
+            for (int c = 0; c < NC; ++c)
+                if (x[c] != root) { x[c] = tree[x[c] * 2 + 1]; dp[c]++; live = true; }
+            if (!__ballot(live)) break;
+        }
+    }
+    __syncthreads();                                              // every chase done before Len
+    DT_T(tp, 2);
+    int ovf = 0, opt = 0, stl = 0;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+        const int h = hmax + 1 + c * 64 + (int)lane;
+        if (h < HEAP_SIZE) {
+            const int n = nd[c], bits = dp[c] > max_length ? max_length : dp[c];
+            ovf += dp[c] > max_length;
+            tree[n * 2 + 1] = (uint16_t)bits;
+            if (n <= max_code) {
+                atomicAdd(&W.blc[bits], 1u);
+                const int xb = n >= base ? extra[n - base] : 0, f = tree[n * 2];
+                opt += f * (bits + xb);
+                if (stree) stl += f * (stree[n * 2 + 1] + xb);
+            }
+        }
+    }
+    if (lane == 0) tree[root * 2 + 1] = 0;
+    const int overflow = dt_sum(ovf);
+    W.opt_len += dt_sum(opt);
+    W.static_len += dt_sum(stl);
+    __syncthreads();
+    if (overflow) {                                               // deftree.ts:98-131, as written
+        if (lane == 0) {
+            int ov = overflow, bits, d = 0;
+            do {
+                bits = max_length - 1;
+                while (W.blc[bits] == 0) bits--;
+                W.blc[bits]--;
+                W.blc[bits + 1] += 2;
+                W.blc[max_length]--;
+                ov -= 2;
+            } while (ov > 0);
+            int h = HEAP_SIZE;
+            for (bits = max_length; bits != 0; bits--) {
+                int k = (int)W.blc[bits];
+                while (k != 0) {
+                    const int m = W.order[--h];
+                    if (m > max_code) continue;
+                    const int t = tree[m * 2 + 1];
+                    if (t != bits) { d += (bits - t) * (int)tree[m * 2]; tree[m * 2 + 1] = (uint16_t)bits; }
+                    k--;
+                }
+            }
+            *W.xch = d;
+        }
+        __syncthreads();
+        W.opt_len += *W.xch;
+        __syncthreads();
+    }
+    DT_T(tp, 3);
+    // gen_codes: lane L holds next_code[L]
+    const uint32_t blc = lane < 16 ? W.blc[lane] : 0u;
+    uint32_t ncv = 0, code = 0;
+    for (int b = 1; b <= max_length; ++b) {
+        code = (code + (uint32_t)dt_rdl(blc, b - 1)) << 1;
+        if ((int)lane == b) ncv = code;
+    }
+    for (int cb = 0; cb <= max_code; cb += 64) {
+        const int n = cb + (int)lane;
+        const int len = n <= max_code ? tree[n * 2 + 1] : 0;
+        uint32_t cd = 0;
+        for (int L = 1; L <= max_length; ++L) {
+            const uint64_t m = __ballot(len == L);
+            if (!m) continue;
+            const uint32_t b0 = (uint32_t)dt_rdl(ncv, L);
+            if (len == L) cd = b0 + (uint32_t)__popcll(m & below);
+            if ((int)lane == L) ncv += (uint32_t)__popcll(m);
+        }
+        if (len) tree[n * 2] = (uint16_t)bitrev_n(cd, len);
+    }
+    __syncthreads();
+    DT_T(tp, 4);
+    return max_code;
+}
+// the code lengths tree[0..max_code + 1] (with the guard), 64 at a time: lenat(i), i ascending
+struct DtLens {
+    const uint16_t* tree;
+    int tsize, c = -1;
+    uint32_t v = 0;
+    __device__ int at(int i) {
+        const int k = i >> 6;
+        if (k != c) {
+            c = k;
+            const int j = (k * 64 + (int)threadIdx.x) * 2 + 1;
+            v = j < tsize ? tree[j] : 0u;
+        }
+        return dt_rdl(v, i & 63);
+    }
+};
+// scan_tree (deflate.ts:267-312): the bit-length counts into blv (lane j: code j)
+__device__ void dt_scan(uint16_t* tree, int tsize, int max_code, uint32_t& blv) {
+    const uint32_t lane = threadIdx.x;
+    if (lane == 0) tree[(max_code + 1) * 2 + 1] = 0xffff;
+    __syncthreads();
+    DtLens L{tree, tsize};
+    int prevlen = -1, curlen, nextlen = L.at(0), count = 0, max_count = 7, min_count = 4;
+    if (nextlen == 0) { max_count = 138; min_count = 3; }
+    for (int n = 0; n <= max_code; n++) {
+        curlen = nextlen;
+        nextlen = L.at(n + 1);
+        if (++count < max_count && curlen == nextlen) continue;
+        else if (count < min_count) blv += (int)lane == curlen ? (uint32_t)count : 0u;
+        else if (curlen != 0) { if (curlen != prevlen) blv += (int)lane == curlen; blv += lane == 16; }
+        else if (count <= 10) blv += lane == 17;
+        else blv += lane == 18;
+        count = 0;
+        prevlen = curlen;
+        if (nextlen == 0) { max_count = 138; min_count = 3; }
+        else if (curlen == nextlen) { max_count = 6; min_count = 3; }
+        else { max_count = 7; min_count = 4; }
+    }
+}
+// the block header's bits: a register accumulator, stored a 32-bit word at a time (lane 0)
+struct DtBits {
+    uint32_t* hdr;
+    uint64_t acc = 0;
+    uint32_t n = 0, nb = 0, w = 0;
+    __device__ void bits(uint32_t v, int len) {
+        acc |= (uint64_t)v << n;
+        n += (uint32_t)len;
+        nb += (uint32_t)len;
+        if (n >= 32) {
+            if (threadIdx.x == 0) hdr[w] = (uint32_t)acc;
+            ++w;
+            acc >>= 32;
+            n -= 32;
+        }
+    }
+    __device__ void flush() { if (n && threadIdx.x == 0) hdr[w] = (uint32_t)acc; }
+    // bits up to bit position p were OR-ed into hdr (zero past them): go on from p
+    __device__ void resume(uint32_t p) {
+        nb = p;
+        w = p >> 5;
+        n = p & 31u;
+        acc = n ? (uint64_t)hdr[w] : 0ull;
+    }
+};
+#ifndef DT_PAR
+#define DT_PAR 1                          // scan_tree / send_tree over the wave (0: one lane's loop)
+#endif
+// scan_tree and send_tree cut each run of equal code lengths into the same pieces: a run of
+// zeros into pieces of up to 138; any other run into a first piece of up to 7, then pieces of
+// up to 6 (the max_count / min_count they set after each piece: 138 / 3 when the next length
+// is 0, 6 / 3 when the run goes on, 7 / 4 when a new nonzero run starts).  So a length at
+// offset t of its run starts a piece iff t % 138 == 0 (zeros), or t == 0 or (t - 7) % 6 == 0,
+// and the piece's size is min(138 | 7 | 6, the rest of the run).  dt_pieces finds every
+// position's run (start and end from per-chunk ballots of "differs from the previous length",
+// with the guard at max_code + 1 ending the last run) and hands f, chunk by chunk with the
+// whole wave: (piece start?, length, piece size, first piece of its run?).
+template <class F>
+__device__ __forceinline__ void dt_pieces(const uint16_t* tree, int max_code, F f) {
+    const int lane = (int)threadIdx.x;
+    const int nch = (max_code + 2 + 63) >> 6;                     // positions 0 .. max_code + 1
+    uint32_t lv[5];
+    uint64_t S[5];
+    int fsa[5];
+#pragma unroll
+    for (int c = 0; c < 5; ++c) {
+        const int i = c * 64 + lane;
+        lv[c] = c < nch && i <= max_code ? (uint32_t)tree[i * 2 + 1] : 0xffffu;
+    }
+#pragma unroll
+    for (int c = 0; c < 5; ++c) {
+        uint32_t prev = (uint32_t)__shfl_up((int)lv[c], 1);
+        if (lane == 0) prev = c ? (uint32_t)dt_rdl(lv[c ? c - 1 : 0], 63) : 0xfffeu;
+        S[c] = c < nch ? __ballot(lv[c] != prev) : 0ull;
+    }
+    int nxt = 0;
+#pragma unroll
+    for (int c = 4; c >= 0; --c) {
+        fsa[c] = nxt;
+        if (S[c]) nxt = c * 64 + (int)__builtin_ctzll(S[c]);
+    }
+    int ls = 0;
+#pragma unroll
+    for (int c = 0; c < 5; ++c) {
+        if (c < nch) {
+            const int n = c * 64 + lane;
+            const uint64_t le = (2ull << lane) - 1ull;               // positions <= n (lane 63: all)
+            const uint64_t mb = S[c] & le, ma = S[c] & ~le;
+            const int st = mb ? c * 64 + 63 - (int)__clzll(mb) : ls;
+            const int en = ma ? c * 64 + (int)__builtin_ctzll(ma) : fsa[c];
+            const int v = (int)lv[c], t = n - st;
+            const bool first = t == 0;
+            const bool pc = n <= max_code && (v == 0 ? t % 138 == 0 : (first || (t >= 7 && (t - 7) % 6 == 0)));
+            const int P = v == 0 ? 138 : first ? 7 : 6;
+            f(pc, v & 31, min(P, en - n), first);
+            if (S[c]) ls = c * 64 + 63 - (int)__clzll(S[c]);
+        }
+    }
+}
+// scan_tree (deflate.ts:267-312): each piece's bit-length codes counted into blacc (LDS)
+__device__ void dt_scan_par(uint16_t* tree, int max_code, uint32_t* blacc) {
+    if (threadIdx.x == 0) tree[(max_code + 1) * 2 + 1] = 0xffff;   // the reference's guard (kept as it leaves it)
+    dt_pieces(tree, max_code, [&](bool pc, int v, int q, bool first) {
+        if (!pc) return;
+        if (v == 0) {
+            if (q < 3) atomicAdd(&blacc[0], (uint32_t)q);
+            else atomicAdd(&blacc[q <= 10 ? 17 : 18], 1u);
+        } else if (q < (first ? 4 : 3)) atomicAdd(&blacc[v], (uint32_t)q);
+        else {
+            if (first) atomicAdd(&blacc[v], 1u);
+            atomicAdd(&blacc[16], 1u);
+        }
+    });
+    __syncthreads();
+}
+// send_tree (deflate.ts:378-429): each piece's bits (<= 21) at its prefix-summed offset from
+// bit o.nb, OR-ed into the zeroed header words; blc: lane j holds bl code j as code | len << 16
+__device__ void dt_send_par(DtBits& o, const uint16_t* tree, int max_code, uint32_t blc) {
+    const int lane = (int)threadIdx.x;
+    o.flush();
+    __syncthreads();
+    const uint32_t e16 = (uint32_t)dt_rdl(blc, 16), e17 = (uint32_t)dt_rdl(blc, 17), e18 = (uint32_t)dt_rdl(blc, 18);
+    uint32_t base = o.nb;
+    dt_pieces(tree, max_code, [&](bool pc, int v, int q, bool first) {
+        const uint32_t ev = (uint32_t)__shfl((int)blc, v);
+        uint32_t b = 0, nbits = 0;
+        if (pc) {
+            const uint32_t cv = ev & 0xffffu, lv = ev >> 16;
+            if (q < (v == 0 || !first ? 3 : 4)) {
+                for (int i = 0; i < q; ++i) b |= cv << (i * lv);
+                nbits = (uint32_t)q * lv;
+            } else if (v != 0) {
+                const uint32_t c16 = e16 & 0xffffu, l16 = e16 >> 16;
+                if (first) { b = cv | (c16 << lv) | ((uint32_t)(q - 4) << (lv + l16)); nbits = lv + l16 + 2; }
+                else { b = c16 | ((uint32_t)(q - 3) << l16); nbits = l16 + 2; }
+            } else if (q <= 10) { b = (e17 & 0xffffu) | ((uint32_t)(q - 3) << (e17 >> 16)); nbits = (e17 >> 16) + 3; }
+            else { b = (e18 & 0xffffu) | ((uint32_t)(q - 11) << (e18 >> 16)); nbits = (e18 >> 16) + 7; }
+        }
+        uint32_t x = nbits;                                       // inclusive scan over the wave
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t y = (uint32_t)__shfl_up((int)x, d);
+            if (lane >= d) x += y;
+        }
+        if (nbits) {
+            const uint32_t off = base + x - nbits, w = off >> 5, sh = off & 31u;
+            atomicOr(&o.hdr[w], b << sh);
+            if (sh + nbits > 32) atomicOr(&o.hdr[w + 1], b >> (32 - sh));
+        }
+        base += (uint32_t)dt_rdl(x, 63);
+    });
+    __syncthreads();
+    o.resume(base);
+}
+// send_tree (deflate.ts:378-429); blc: lane j holds bl code j as code | len << 16
+__device__ void dt_send(DtBits& o, const uint16_t* tree, int tsize, int max_code, uint32_t blc) {
+    DtLens L{tree, tsize};
+    auto put = [&](int c) { const uint32_t e = (uint32_t)dt_rdl(blc, c); o.bits(e & 0xffffu, (int)(e >> 16)); };
+    int prevlen = -1, curlen, nextlen = L.at(0), count = 0, max_count = 7, min_count = 4;
+    if (nextlen == 0) { max_count = 138; min_count = 3; }
+    for (int n = 0; n <= max_code; n++) {
+        curlen = nextlen;
+        nextlen = L.at(n + 1);
+        if (++count < max_count && curlen == nextlen) continue;
+        else if (count < min_count) { do { put(curlen); } while (--count != 0); }
+        else if (curlen != 0) {
+            if (curlen != prevlen) { put(curlen); count--; }
+            put(16);
+            o.bits((uint32_t)(count - 3), 2);
+        } else if (count <= 10) { put(17); o.bits((uint32_t)(count - 3), 3); }
+        else { put(18); o.bits((uint32_t)(count - 11), 7); }
+        count = 0;
+        prevlen = curlen;
+        if (nextlen == 0) { max_count = 138; min_count = 3; }
+        else if (curlen == nextlen) { max_count = 6; min_count = 3; }
+        else { max_count = 7; min_count = 4; }
+    }
+}
+// k_dfl_trees: one wave per (stream, block), blocks y, y + ny, ...  Frequencies from the
+// symbols (LDS atomics), the trees and the block type choice of _tr_flush_block
+// (deftree.ts:1044-1108), the code table (code | len << 16) and the header bits out.
+__global__ __launch_bounds__(64) void k_dfl_trees(DeflateArgs A) {
+    __shared__ uint16_t ltree[HEAP_SIZE * 2], dtree[(2 * D_CODES + 1) * 2], bltree[(2 * BL_CODES + 1) * 2];
+    __shared__ uint16_t order[HEAP_SIZE];
+    __shared__ __attribute__((aligned(8))) uint32_t hk[L_CODES + 2];
+    __shared__ uint32_t blcnt[16], blacc[32], hist[L_CODES + D_CODES], hdr[FB_HDR_WORDS];
+    __shared__ int xch;
+    __shared__ uint16_t s_sl[288 * 2], s_sd[30 * 2];
+    __shared__ uint8_t s_xl[32], s_xd[32], s_xbl[32], lcode_t[256], dcode_t[512];
+    const uint32_t sid = blockIdx.x, lane = threadIdx.x;
+#ifdef DT_PROF
+    uint64_t tk[16] = {}, tb[5] = {};
+    uint64_t* const tpk = sid == 0 && blockIdx.y == 0 ? tk : nullptr;
+    uint64_t* const tpb = sid == 0 && blockIdx.y == 0 ? tb : nullptr;
+#else
+    uint64_t* const tpk = nullptr;
+    uint64_t* const tpb = nullptr;
+    (void)tpk;
+#endif
+    DT_T(tpk, 0);
+    if (sid >= A.n) return;
+    GLB DSlab* S = (GLB DSlab*)(A.state + (uint64_t)sid * SLAB_BYTES);
+    GLB FStream* F = (GLB FStream*)S->window;
+    // the stream's words and the tables in one round trip (a lone wave waits for each)
+    const uint32_t flag = F->flag, nblk = F->nblk;
+    const uint64_t rp0 = A.rp0[sid], tb0 = A.tb0[sid];
+    const GLB DTables* T = (const GLB DTables*)&g_dt;
+    for (int i = (int)lane; i < 256; i += 64) lcode_t[i] = T->length_code[i];
+    for (int i = (int)lane; i < 512; i += 64) dcode_t[i] = T->dist_code[i];
+    for (int i = (int)lane; i < 288 * 2; i += 64) s_sl[i] = T->static_ltree[i];
+    if (lane < 60) s_sd[lane] = T->static_dtree[lane];
+    if (lane < 29) s_xl[lane] = T->extra_lbits[lane];
+    if (lane < 30) s_xd[lane] = T->extra_dbits[lane];
+    if (lane < 19) s_xbl[lane] = T->extra_blbits[lane];
+    if (flag) return;
+    const GLB uint32_t* sym = (const GLB uint32_t*)A.sym_buf + 2 * rp0;
+    for (uint32_t b = blockIdx.y; b < nblk; b += gridDim.y) {
+        GLB FBlock* Bk = (GLB FBlock*)(A.blk + (tb0 + b) * FB_SLOT);
+        const uint32_t sym0 = Bk->sym0, nsym = Bk->nsym, eof = Bk->eof;
+        const int block_start = Bk->block_start, strstart = Bk->strstart;
+        for (int i = (int)lane; i < L_CODES + D_CODES; i += 64) hist[i] = 0;
+        for (int i = (int)lane; i < HEAP_SIZE * 2; i += 64) ltree[i] = 0;
+        for (int i = (int)lane; i < (2 * D_CODES + 1) * 2; i += 64) dtree[i] = 0;
+        for (int i = (int)lane; i < (2 * BL_CODES + 1) * 2; i += 64) bltree[i] = 0;
+        for (int i = (int)lane; i < FB_HDR_WORDS; i += 64) hdr[i] = 0;
+        if (lane < 32) blacc[lane] = 0;
+        __syncthreads();
+        for (uint32_t i = lane; i < nsym; i += 64) {
+            const uint32_t s = sym[sym0 + i], lc = s & 255u, dist = s >> 8;
+            if (dist == 0) atomicAdd(&hist[lc], 1u);
+            else {
+                const uint32_t d = dist - 1;
+                atomicAdd(&hist[257 + lcode_t[lc]], 1u);
+                atomicAdd(&hist[L_CODES + (d < 256 ? dcode_t[d] : dcode_t[256 + (d >> 7)])], 1u);
+            }
+        }
+        __syncthreads();
+        if (lane == 0) hist[END_BLOCK] += 1;                 // init_block's END_BLOCK count
+        __syncthreads();
+        for (int i = (int)lane; i < L_CODES; i += 64) ltree[i * 2] = (uint16_t)hist[i];
+        for (int i = (int)lane; i < D_CODES; i += 64) dtree[i * 2] = (uint16_t)hist[L_CODES + i];
+        __syncthreads();
+        WTree W{order, hk, blcnt, &xch, 0, 0};
+        DT_T(tpk, 1);
+        const int l_max = dt_build(W, ltree, s_sl, s_xl, 257, L_CODES, 15, tpb);
+        DT_T(tpk, 2);
+        const int d_max = dt_build(W, dtree, s_sd, s_xd, 0, D_CODES, 15);
+        DT_T(tpk, 3);
+#if DT_PAR
+        dt_scan_par(ltree, l_max, blacc);
+        dt_scan_par(dtree, d_max, blacc);
+        if (lane < BL_CODES) bltree[lane * 2] = (uint16_t)blacc[lane];
+#else
+        uint32_t blv = 0;
+        dt_scan(ltree, HEAP_SIZE * 2, l_max, blv);
+        dt_scan(dtree, (2 * D_CODES + 1) * 2, d_max, blv);
+        if (lane < BL_CODES) bltree[lane * 2] = (uint16_t)blv;
+#endif
+        __syncthreads();
+        DT_T(tpk, 4);
+        dt_build(W, bltree, (const uint16_t*)nullptr, s_xbl, 0, BL_CODES, 7);
+        DT_T(tpk, 5);
+        const uint32_t blc = lane < BL_CODES ? (uint32_t)bltree[lane * 2] | ((uint32_t)bltree[lane * 2 + 1] << 16) : 0u;
+        int max_blindex;
+        for (max_blindex = BL_CODES - 1; max_blindex >= 3; max_blindex--)
+            if (dt_rdl(blc, c_bl_order[max_blindex]) >> 16) break;
+        const int opt_len = W.opt_len + 3 * (max_blindex + 1) + 5 + 5 + 4;
+        uint32_t opt_lenb = (uint32_t)(opt_len + 3 + 7) >> 3;
+        const uint32_t static_lenb = (uint32_t)(W.static_len + 3 + 7) >> 3;
+        if (static_lenb <= opt_lenb) opt_lenb = static_lenb;
+        const int stored_len = strstart - block_start;
+        DtBits o{hdr};
+        uint32_t type;
+        if ((uint32_t)(stored_len + 4) <= opt_lenb && block_start >= 0) {
+            type = 0;
+            o.bits(eof, 3);
+        } else {
+            type = static_lenb == opt_lenb ? 1 : 2;
+            if (type == 1) o.bits(2u + eof, 3);
+            else {
+                o.bits(4u + eof, 3);
+                const int lcodes = l_max + 1, dcodes = d_max + 1, blcodes = max_blindex + 1;
+                o.bits((uint32_t)(lcodes - 257), 5);
+                o.bits((uint32_t)(dcodes - 1), 5);
+                o.bits((uint32_t)(blcodes - 4), 4);
+                for (int rank = 0; rank < blcodes; rank++) o.bits((uint32_t)dt_rdl(blc, c_bl_order[rank]) >> 16, 3);
+#if DT_PAR
+                dt_send_par(o, ltree, lcodes - 1, blc);
+                dt_send_par(o, dtree, dcodes - 1, blc);
+#else
+                dt_send(o, ltree, HEAP_SIZE * 2, lcodes - 1, blc);
+                dt_send(o, dtree, (2 * D_CODES + 1) * 2, dcodes - 1, blc);
+#endif
+            }
+        }
+        o.flush();
+        DT_T(tpk, 6);
+        // the data bits of the block (codes and extra bits; compress_block's length)
+        uint32_t db = 0;
+        if (type != 0) {
+            const bool st = type == 1;
+            for (int i = (int)lane; i < L_CODES; i += 64) {
+                const uint32_t h = hist[i];
+                if (h) db += h * (uint32_t)(st ? s_sl[i * 2 + 1] : ltree[i * 2 + 1]);
+                if (i >= 257) db += h * s_xl[i - 257];
+            }
+            if (lane < D_CODES) {
+                const uint32_t h = hist[L_CODES + lane];
+                if (h) db += h * ((uint32_t)(st ? 5 : dtree[lane * 2 + 1]) + s_xd[lane]);
+            }
+        }
+        const uint32_t dbits = (uint32_t)dt_sum((int)db), hbits = o.nb;
+        GLB uint32_t* tab = (GLB uint32_t*)((GLB uint8_t*)Bk + 64);
+        if (type != 0)
+            for (int i = (int)lane; i < L_CODES + D_CODES; i += 64) {
+                uint32_t e;
+                if (i < L_CODES) e = type == 2 ? (uint32_t)ltree[i * 2] | ((uint32_t)ltree[i * 2 + 1] << 16)
+                                               : (uint32_t)s_sl[i * 2] | ((uint32_t)s_sl[i * 2 + 1] << 16);
+                else {
+                    const int d = i - L_CODES;
+                    e = type == 2 ? (uint32_t)dtree[d * 2] | ((uint32_t)dtree[d * 2 + 1] << 16)
+                                  : (uint32_t)s_sd[d * 2] | ((uint32_t)s_sd[d * 2 + 1] << 16);
+                }
+                tab[i] = e;
+            }
+        __syncthreads();                                      // the header words (lane 0) stored
+        for (uint32_t i = lane; i < (hbits + 31) / 32; i += 64) tab[FB_HDR_OFF / 4 + i] = hdr[i];
+        if (lane == 0) {
+            Bk->type = type; Bk->hbits = hbits; Bk->dbits = dbits; Bk->stored_len = (uint32_t)stored_len;
+        }
+        __syncthreads();
+        DT_T(tpk, 7);
+#ifdef DT_PROF
+        if (tpk && lane == 0)
+            printf("DT_PROF lmax %d type %u | setup %lu ltree %lu (leaves %lu heap %lu chase %lu len %lu codes %lu) dtree %lu scan %lu bltree %lu hdr %lu out %lu [x10ns]\n",
+                   l_max, type, tk[1] - tk[0], tk[2] - tk[1], tb[0] - tk[1], tb[1] - tb[0], tb[2] - tb[1], tb[3] - tb[2],
+                   tb[4] - tb[3], tk[3] - tk[2], tk[4] - tk[3], tk[5] - tk[4], tk[6] - tk[5], tk[7] - tk[6]);
+#endif
+    }
+}
+#else
 // k_dfl_trees: one wave per stream, its blocks in turn.  Frequencies from the symbols (LDS
 // atomics), then lane 0 runs build_tree / scan_tree / build_bl_tree and the block type choice
 // exactly as _tr_flush_block does, and the wave exports the code table (code | len << 16)
@@ -2954,6 +3606,7 @@ __global__ __launch_bounds__(64) void k_dfl_trees(DeflateArgs A) {   // grid (n,
         __syncthreads();
     }
 }
+#endif
 
 // k_dfl_encode: one workgroup per stream.  Thread 0 lays the blocks out (bit offsets; the
 // 16-bit pending units behind the overlay check; stored blocks' byte alignment), the group

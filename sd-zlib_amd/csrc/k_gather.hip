@@ -68,4 +68,37 @@ void launch_gather(uint8_t* dst, const uint64_t* dst_off, const uint8_t* src, co
     hipLaunchKernelGGL(k_gather, dim3(n, GA_SLICES), dim3(GA_THREADS), 0, s, dst, dst_off, src, src_off, len, n);
 }
 
+// The host path's copy back of a small call: the [outputs | records] region of the device pool
+// into the same layout in pinned host memory, only the bytes each stream wrote (its record's
+// out_len, at len_off) and the m records.  Block k < m: stream k's output; block m: the records.
+// A copy engine's copy of the whole region started ~20 us after the last kernel on a one-stream
+// inflate (rocprofv3 trace, profiles/r05/lat); this kernel follows the codec's last launch.
+// dst is device-mapped pinned memory; out_off are 8-byte aligned, rec_off 256-byte aligned.
+__global__ __launch_bounds__(GA_THREADS) void k_copy_back(uint8_t* dst, const uint8_t* src, const uint64_t* out_off,
+                                                          const uint64_t* out_cap, uint64_t rec_off, uint32_t rsz,
+                                                          uint32_t len_off, uint32_t m) {
+    const uint32_t k = blockIdx.x;
+    uint64_t o, L;
+    if (k == m) {
+        o = rec_off;
+        L = (uint64_t)m * rsz;
+    } else {
+        o = out_off[k];
+        const uint64_t ol = *(const uint64_t*)(src + rec_off + (uint64_t)k * rsz + len_off);
+        L = ol < out_cap[k] ? ol : out_cap[k];
+    }
+    const uint64_t nq = L >> 3;
+    const uint64_t* s8 = (const uint64_t*)(src + o);
+    uint64_t* d8 = (uint64_t*)(dst + o);
+    for (uint64_t q = threadIdx.x; q < nq; q += GA_THREADS) d8[q] = s8[q];
+    const uint64_t t = nq << 3;
+    if (threadIdx.x < L - t) dst[o + t + threadIdx.x] = src[o + t + threadIdx.x];
+}
+
+void launch_copy_back(uint8_t* dst, const uint8_t* src, const uint64_t* out_off, const uint64_t* out_cap,
+                      uint64_t rec_off, uint32_t rsz, uint32_t len_off, uint32_t m, hipStream_t s) {
+    hipLaunchKernelGGL(k_copy_back, dim3(m + 1), dim3(GA_THREADS), 0, s, dst, src, out_off, out_cap, rec_off, rsz,
+                       len_off, m);
+}
+
 }  // namespace sdz

@@ -165,7 +165,19 @@ int host_shard(const uint8_t* const* in, const size_t* in_len, uint8_t* const* o
         const size_t nb = o_rec - o_out + recs.size();
         if (int rc2 = g_pinned.get(al(nb, 256), &ep)) return rc2;
         ebuf = (uint8_t*)ep;
-        HIPCHK(hipMemcpyAsync(ebuf, B + o_out, nb, hipMemcpyDeviceToHost, s));
+        // the bytes written and the records, by a kernel into the mapped staging (a copy engine
+        // started ~20 us late on small calls); SDZ_COPY_BACK=0: the whole region by hipMemcpyAsync
+        static const bool kb = !getenv("SDZ_COPY_BACK") || atoi(getenv("SDZ_COPY_BACK")) != 0;
+        void* dp = nullptr;
+        if (kb && hipHostGetDevicePointer(&dp, ep, 0) == hipSuccess && dp) {
+            const uint32_t len_off = C.inflate ? (uint32_t)offsetof(sdz_inflate_record, out_len)
+                                               : (uint32_t)offsetof(sdz_deflate_record, out_len);
+            launch_copy_back((uint8_t*)dp, B + o_out, d_meta + 2 * (size_t)m, d_meta + 3 * (size_t)m, o_rec - o_out,
+                             (uint32_t)rsz, len_off, m, s);
+            HIPCHK(hipGetLastError());
+        } else {
+            HIPCHK(hipMemcpyAsync(ebuf, B + o_out, nb, hipMemcpyDeviceToHost, s));
+        }
     } else {
         HIPCHK(hipMemcpyAsync(recs.data(), B + o_rec, recs.size(), hipMemcpyDeviceToHost, s));
     }

@@ -216,6 +216,9 @@ void launch_checksum_one(const uint8_t* in, uint64_t len, int kind, int32_t seed
 // batched span copy (k_gather.hip)
 void launch_gather(uint8_t* dst, const uint64_t* dst_off, const uint8_t* src, const uint64_t* src_off,
                    const uint64_t* len, uint32_t n, hipStream_t s);
+// a small host call's [outputs | records] region back into mapped pinned memory (k_gather.hip)
+void launch_copy_back(uint8_t* dst, const uint8_t* src, const uint64_t* out_off, const uint64_t* out_cap,
+                      uint64_t rec_off, uint32_t rsz, uint32_t len_off, uint32_t m, hipStream_t s);
 // the DICTID a kernel compares / writes
 __device__ __forceinline__ int32_t dict_id_of(int32_t v, const int32_t* dev) { return dev ? *dev : v; }
 
