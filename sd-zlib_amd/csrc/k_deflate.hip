@@ -2146,15 +2146,29 @@ __global__ __launch_bounds__(PW_THREADS) void k_dfl_parse_wide(DeflateArgs A) {
         if (parser && !done) {
             const int end = (c + 1) * PW_CHUNK, b0 = c * PW_CHUNK;
             const uint64_t* cb = buf[c & 1];
+#if PW_UNIFORM
+            // the records of positions rb .. rb + 63 in lane order (one LDS read per 64
+            // positions); a step takes its record with readlane instead of waiting on LDS
+            int rb = -(1 << 30);
+            uint32_t rlo = 0, rhi = 0;
+#endif
             for (;;) {
                 if (st.strstart >= end) break;             // the next chunk (a step moves <= MAX_MATCH)
                 if (ps_fill(st)) { done = true; break; }
-                const uint64_t rv = cb[st.strstart - b0];
 #if PW_UNIFORM
-                const uint64_t r = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)rv) |
-                                   ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(rv >> 32)) << 32);
+                int o = st.strstart - rb;
+                if ((uint32_t)o >= 64u) {
+                    rb = st.strstart;
+                    o = 0;
+                    const int i = rb - b0 + (int)tid;
+                    const uint64_t v = i < PW_CHUNK ? cb[i] : 0ull;
+                    rlo = (uint32_t)v;
+                    rhi = (uint32_t)(v >> 32);
+                }
+                const uint64_t r = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)rlo, o) |
+                                   ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)rhi, o) << 32);
 #else
-                const uint64_t r = rv;
+                const uint64_t r = cb[st.strstart - b0];
 #endif
                 ps_step(st, r);
             }

@@ -75,6 +75,20 @@ struct Pool {
     int get(size_t bytes, hipStream_t s, void** out, Slot** slot);
     static int done(Slot* S, hipStream_t s);
 };
+// Deferred done events.  Each hipEventRecord is a marker in the stream, and a marker between two
+// launches delayed the second by ~5 us on small calls (rocprofv3 trace, profiles/r05/lat).  While a
+// DeferScope is alive on this thread, Pool::done / Pinned::done on its stream queue their event
+// instead of recording it; a get() of a slot whose event is queued records it first; the scope's
+// flush() (after the call's last launch) and its destructor record the rest.  A later event only
+// makes the next user wait longer.
+// If the scope's owner synchronises the stream after its last launch (synced()), the queued
+// events are dropped instead and their slots marked idle: the work they would mark is done.
+struct DeferScope {
+    explicit DeferScope(hipStream_t s);
+    ~DeferScope();
+    static void flush();
+    static void synced();
+};
 // records the pool's event on every exit path once get() succeeded
 struct PoolUse {
     Pool& pool;
@@ -96,7 +110,9 @@ struct Pinned {
     size_t cap[kMaxDev] = {};
     hipEvent_t ev[kMaxDev] = {};
     bool pending[kMaxDev] = {};
-    int get(size_t bytes, void** out);
+    // wait = false: the caller does not write the buffer from the host (only stream-ordered
+    // device work does), so the pending copies are not waited for unless it must grow
+    int get(size_t bytes, void** out, bool wait = true);
     int done(hipStream_t s);
 };
 extern Pinned g_pinned;

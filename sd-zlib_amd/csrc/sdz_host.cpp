@@ -61,6 +61,7 @@ struct Codec {
 struct ShardOut {
     std::vector<uint32_t> order;               // caller index of device record k
     void* d_rec = nullptr;                     // device records, rec_cap slots (padding zeroed)
+    bool timed = false;                        // kernel_ms wanted (events around the codec's launches)
     float kernel_ms = 0.f;
     uint64_t bytes_in = 0, bytes_out = 0;
 };
@@ -78,6 +79,7 @@ int host_shard(const uint8_t* const* in, const size_t* in_len, uint8_t* const* o
     const uint32_t m = (uint32_t)ids.size();
     const size_t rsz = C.rec_size();
     hipStream_t s = nullptr;
+    DeferScope defer(s);                           // the call's done events after its copy back
     R.order = ids;
     if (C.inflate)                                 // longest streams first: a wave decodes similar lengths
         std::stable_sort(R.order.begin(), R.order.end(), [&](uint32_t a, uint32_t b) { return in_len[a] > in_len[b]; });
@@ -123,23 +125,31 @@ int host_shard(const uint8_t* const* in, const size_t* in_len, uint8_t* const* o
                 HIPCHK(hipMemcpyAsync(B + o_in + meta[k], in[R.order[k]], in_len[R.order[k]], hipMemcpyHostToDevice, s));
     }
     std::memcpy(P + pin_meta, meta.data(), meta.size() * 8);
+    // the staging's done event goes in after the copy back (a marker between the input copy and
+    // the first kernel delays that kernel); an error return before it waits for the copies here
+    struct SyncOnExit {
+        hipStream_t s;
+        bool armed = true;
+        ~SyncOnExit() { if (armed) (void)hipStreamSynchronize(s); }
+    } staged{s};
     if (pack) HIPCHK(hipMemcpyAsync(B + o_in, P, pin_meta + meta.size() * 8, hipMemcpyHostToDevice, s));
     else HIPCHK(hipMemcpyAsync(d_meta, P, meta.size() * 8, hipMemcpyHostToDevice, s));
-    if (int rc = g_pinned.done(s)) return rc;       // (the next get() waits for these copies)
     uint8_t* d_dict = nullptr;
     if (C.dict) {
         d_dict = B + o_dict;
         if (C.dict_len) HIPCHK(hipMemcpyAsync(d_dict, C.dict, C.dict_len, hipMemcpyHostToDevice, s));
     }
     if (rec_cap > m) HIPCHK(hipMemsetAsync(B + o_rec + (size_t)m * rsz, 0, (size_t)(rec_cap - m) * rsz, s));
-    // the shard's kernel-time events: made once per thread and device
+    // the shard's kernel-time events (multi-GPU stats only: each is a marker in the stream, and
+    // a marker between two launches delayed the second by ~5 us on small calls): made once per
+    // thread and device
     static thread_local hipEvent_t evs[kMaxDev][2] = {};
     int dev = 0;
     HIPCHK(hipGetDevice(&dev));
     if (dev < 0 || dev >= kMaxDev) return fail(SDZ_API_BAD_ARG, "host batch: device index");
-    if (!evs[dev][0]) { HIPCHK(hipEventCreate(&evs[dev][0])); HIPCHK(hipEventCreate(&evs[dev][1])); }
+    if (R.timed && !evs[dev][0]) { HIPCHK(hipEventCreate(&evs[dev][0])); HIPCHK(hipEventCreate(&evs[dev][1])); }
     hipEvent_t e0 = evs[dev][0], e1 = evs[dev][1];
-    HIPCHK(hipEventRecord(e0, s));
+    if (R.timed) HIPCHK(hipEventRecord(e0, s));
     // no input starts with the gzip magic (or the format is raw): the crc32 finalize is not needed
     bool no_gzip = C.inflate;
     for (uint32_t k = 0; no_gzip && C.format != SDZ_FMT_RAW && k < m; ++k) {
@@ -154,7 +164,7 @@ int host_shard(const uint8_t* const* in, const size_t* in_len, uint8_t* const* o
                                    d_meta + 3 * (size_t)m, (sdz_deflate_record*)(B + o_rec), m, C.level, C.format,
                                    C.fname, C.fname_len, C.mtime, d_dict, (uint32_t)C.dict_len, s, meta.data() + m);
     if (rc) return rc;
-    HIPCHK(hipEventRecord(e1, s));
+    if (R.timed) HIPCHK(hipEventRecord(e1, s));
     // records back (one copy), then the outputs; small output slots come back with the
     // records, under the same wait (the drop-in's one-buffer calls)
     std::vector<uint8_t> recs((size_t)m * rsz);
@@ -163,7 +173,8 @@ int host_shard(const uint8_t* const* in, const size_t* in_len, uint8_t* const* o
     if (eager) {                                   // outputs and records: one copy
         void* ep = nullptr;
         const size_t nb = o_rec - o_out + recs.size();
-        if (int rc2 = g_pinned.get(al(nb, 256), &ep)) return rc2;
+        // (written by stream-ordered device work only: no wait for the input copy)
+        if (int rc2 = g_pinned.get(al(nb, 256), &ep, false)) return rc2;
         ebuf = (uint8_t*)ep;
         // the bytes written and the records, by a kernel into the mapped staging (a copy engine
         // started ~20 us late on small calls); SDZ_COPY_BACK=0: the whole region by hipMemcpyAsync
@@ -184,9 +195,11 @@ int host_shard(const uint8_t* const* in, const size_t* in_len, uint8_t* const* o
     // multi-GPU: the records (rec_cap slots, padding zeroed) into the caller's gather slot, which
     // the caller keeps (its own pool use) until the all-gather is done
     if (rec_dev) HIPCHK(hipMemcpyAsync(rec_dev, B + o_rec, (size_t)rec_cap * rsz, hipMemcpyDeviceToDevice, s));
+    if (int rc2 = g_pinned.done(s)) return rc2;     // (the next get() waits for the copies above)
+    staged.armed = false;
     HIPCHK(hipStreamSynchronize(s));
     if (eager) std::memcpy(recs.data(), ebuf + (o_rec - o_out), recs.size());
-    HIPCHK(hipEventElapsedTime(&R.kernel_ms, e0, e1));
+    if (R.timed) HIPCHK(hipEventElapsedTime(&R.kernel_ms, e0, e1));
     auto out_len_of = [&](uint32_t k) -> uint64_t {
         const uint8_t* r = recs.data() + (size_t)k * rsz;
         const uint64_t len = C.inflate ? ((const sdz_inflate_record*)r)->out_len : ((const sdz_deflate_record*)r)->out_len;
@@ -232,6 +245,7 @@ int host_shard(const uint8_t* const* in, const size_t* in_len, uint8_t* const* o
         for (uint32_t k = 0; k < m; ++k)
             std::memcpy((uint8_t*)rec_host + (size_t)R.order[k] * rsz, recs.data() + (size_t)k * rsz, rsz);
     R.d_rec = rec_dev ? rec_dev : B + o_rec;
+    DeferScope::synced();                          // (nothing enqueued after the last wait above)
     return SDZ_API_OK;
 }
 
@@ -357,6 +371,7 @@ int multi_batch(const uint8_t* const* in, const size_t* in_len, uint8_t* const* 
             g = (uint8_t*)gp;
         }
         uint8_t* mine = g ? g + (size_t)k * slot_bytes : nullptr;
+        R[k].timed = true;
         if (rc == SDZ_API_OK && !ids[k].empty())
             rc = host_shard(in, in_len, out, out_cap, ids[k], max_m, C, loopback ? rec : nullptr, R[k], mine);
         else if (rc == SDZ_API_OK && rccl) {

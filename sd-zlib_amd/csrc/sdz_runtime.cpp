@@ -52,11 +52,60 @@ int cur_device(int* d) {
     return SDZ_API_OK;
 }
 
+namespace {
+struct DeferredEv {
+    hipEvent_t ev;
+    hipStream_t s;
+    bool* pending;
+};
+thread_local int t_defer_depth = 0;
+thread_local bool t_defer_synced = false;
+thread_local hipStream_t t_defer_s = nullptr;
+thread_local std::vector<DeferredEv> t_deferred;
+// record a queued event now (a get() of its slot)
+void defer_take(hipEvent_t ev) {
+    for (size_t i = 0; i < t_deferred.size(); ++i)
+        if (t_deferred[i].ev == ev) {
+            (void)hipEventRecord(ev, t_deferred[i].s);
+            t_deferred.erase(t_deferred.begin() + (long)i);
+            return;
+        }
+}
+bool defer_put(hipEvent_t ev, hipStream_t s, bool* pending) {
+    if (!t_defer_depth || s != t_defer_s) return false;
+    defer_take(ev);                                   // (one entry per event: the later use wins)
+    t_deferred.push_back({ev, s, pending});
+    return true;
+}
+}  // namespace
+
+DeferScope::DeferScope(hipStream_t s) {
+    if (t_defer_depth++ == 0) {
+        t_defer_s = s;
+        t_defer_synced = false;
+    }
+}
+DeferScope::~DeferScope() {
+    if (--t_defer_depth) return;
+    if (t_defer_synced) {
+        for (const DeferredEv& d : t_deferred) *d.pending = false;
+        t_deferred.clear();
+    } else {
+        flush();
+    }
+}
+void DeferScope::flush() {
+    for (const DeferredEv& d : t_deferred) (void)hipEventRecord(d.ev, d.s);
+    t_deferred.clear();
+}
+void DeferScope::synced() { t_defer_synced = true; }
+
 int Pool::get(size_t bytes, hipStream_t s, void** out, Slot** slot) {
     int d = 0;
     if (int rc = cur_device(&d)) return rc;
     Slot& S = slots[d];
     if (!S.ev) HIPCHK(hipEventCreateWithFlags(&S.ev, hipEventDisableTiming));
+    if (S.pending) defer_take(S.ev);
     if (S.p && S.cap < bytes) {
         if (S.pending) HIPCHK(hipEventSynchronize(S.ev));
         HIPCHK(hipFree(S.p));
@@ -77,15 +126,17 @@ int Pool::get(size_t bytes, hipStream_t s, void** out, Slot** slot) {
 }
 
 int Pool::done(Slot* S, hipStream_t s) {
-    HIPCHK(hipEventRecord(S->ev, s));
     S->pending = true;
+    if (defer_put(S->ev, s, &S->pending)) return SDZ_API_OK;
+    HIPCHK(hipEventRecord(S->ev, s));
     return SDZ_API_OK;
 }
 
-int Pinned::get(size_t bytes, void** out) {
+int Pinned::get(size_t bytes, void** out, bool wait) {
     int d = 0;
     if (int rc = cur_device(&d)) return rc;
-    if (pending[d]) {
+    if (pending[d] && (wait || cap[d] < bytes)) {
+        defer_take(ev[d]);
         HIPCHK(hipEventSynchronize(ev[d]));
         pending[d] = false;
     }
@@ -122,8 +173,9 @@ int Pinned::done(hipStream_t s) {
     int d = 0;
     if (int rc = cur_device(&d)) return rc;
     if (!ev[d]) HIPCHK(hipEventCreateWithFlags(&ev[d], hipEventDisableTiming));
-    HIPCHK(hipEventRecord(ev[d], s));
     pending[d] = true;
+    if (defer_put(ev[d], s, &pending[d])) return SDZ_API_OK;
+    HIPCHK(hipEventRecord(ev[d], s));
     return SDZ_API_OK;
 }
 
