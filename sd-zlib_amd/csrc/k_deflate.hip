@@ -1200,6 +1200,9 @@ __global__ __launch_bounds__(64 * CH_WAVES) void k_dfl_chain(DeflateArgs A) {
 #ifndef PM_MORE_IF
 #define PM_MORE_IF 1                                    // long compares behind one uniform test
 #endif
+#ifndef PM_WBSKIP
+#define PM_WBSKIP 0                                     // the byte-at-best filter only where best >= 4
+#endif
 #define PM_WINB (W_SIZE + PM_SEG + PM_TAIL + MAX_MATCH + 16)   // staged window bytes (+ the last positions'
 #define PM_PV (W_SIZE + PM_SEG + PM_TAIL)                         // staged links      ... in a last segment)
 // record word of position p: the full-chain result (len << 16 | dist) in the low half, the
@@ -1396,6 +1399,20 @@ __global__ __launch_bounds__(PM_THREADS) void k_dfl_match(DeflateArgs A) {
         uint32_t x1 = 0, x2 = 0;
         if (cand1) x1 = pm_w4(win, c1) ^ s4;
         if (cand2) x2 = pm_w4(win, c2) ^ s4;
+#elif PM_WBSKIP
+        // the byte at best only filters (a candidate that differs there cannot beat best); while
+        // best < 4 the 4-byte compare decides that exactly, so only lanes with best >= 4 read it
+        // (fewer lanes in the random LDS reads, fewer bank conflicts)
+        uint32_t x1 = pm_w4(win, c1) ^ s4, x2 = pm_w4(win, c2) ^ s4;
+        const bool go2 = c3 > limit && chain > 2;            // ... and after c2
+        const int c4 = pvl[l2 && go2 ? c3 : sp];
+        bool f1 = true, f2 = true;
+        if (best >= 4) {
+            const uint32_t sb = win[sp + best];
+            f1 = win[c1 + best] == sb;
+            f2 = win[c2 + best] == sb;
+        }
+        const bool cand1 = live && f1, cand2 = l2 && f2;
 #else
         const uint32_t sb = win[sp + best], wb1 = win[c1 + best], wb2 = win[c2 + best];
         uint32_t x1 = pm_w4(win, c1) ^ s4, x2 = pm_w4(win, c2) ^ s4;
