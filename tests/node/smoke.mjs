@@ -121,6 +121,26 @@ check("deflate L6 == reference fixture", eq(deflate(text, { level: 6 }), golden(
 	check("deflateBatch devices [0,0]", eq(dz[0].data, golden("paradiselost.deflate")) &&
 		eq(dz[1].data, golden("simple.deflate")));
 }
+{
+	// inflate()'s errors (one-shot path) are the ones an Inflater append + finish gives
+	const s = golden("simple.deflate");
+	const viaInflater = data => {
+		const inf = new Inflater();
+		try { inf.append(data); } catch (e) { return e.message; }
+		const r = inf.finish();
+		return r.success ? "" : !r.complete ? "Unexpected EOF during decompression" :
+			r.checksum === "mismatch" ? "Data integrity check failed" : "Decompression error";
+	};
+	const bad = s.slice();
+	bad[bad.length - 1] ^= 1;
+	const junk = s.slice();
+	junk[2] = 0xff;
+	for (const [name, data] of [["truncated", s.subarray(0, s.length - 6)], ["bad adler32", bad], ["bad block", junk]]) {
+		let m = "";
+		try { inflate(data); } catch (e) { m = e.message; }
+		check("inflate " + name + ": " + m, m !== "" && m === viaInflater(data));
+	}
+}
 check("adler32 KAT", adler32(golden("simple.txt")) === -1612443532);
 check("crc32 KAT", crc32(golden("simple.txt")) === 1488305224);
 let threw = "";
