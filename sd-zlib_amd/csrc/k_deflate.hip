@@ -3660,12 +3660,51 @@ __device__ __forceinline__ uint32_t en_scan(uint32_t v, uint32_t* wsum, uint32_t
     total = all;
     return base + x - v;
 }
+#ifndef EN_V2
+#define EN_V2 1                           // encode rows: DPP scan, double-buffered stage and sums (2 barriers per row, not 4)
+#endif
+#if EN_V2
+template <int CTRL, int ROWS>
+__device__ __forceinline__ uint32_t en_dpp_add(uint32_t x) {
+    return x + (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, ROWS, 0xf, false);
+}
+// the row's exclusive prefix of v over the workgroup and its total: an inclusive wave scan
+// with DPP row shifts / broadcasts, the wave sums through wsum (this row's half of a double
+// buffer: the next row writes the other half, so one barrier per row suffices)
+__device__ __forceinline__ uint32_t en_scan2(uint32_t v, uint32_t* wsum, uint32_t& total) {
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
+    uint32_t x = v;
+    x = en_dpp_add<0x111, 0xf>(x);                        // row_shr:1
+    x = en_dpp_add<0x112, 0xf>(x);                        // row_shr:2
+    x = en_dpp_add<0x114, 0xf>(x);                        // row_shr:4
+    x = en_dpp_add<0x118, 0xf>(x);                        // row_shr:8
+    x = en_dpp_add<0x142, 0xa>(x);                        // row_bcast:15 -> rows 1, 3
+    x = en_dpp_add<0x143, 0xc>(x);                        // row_bcast:31 -> rows 2, 3
+    if (lane == 63) wsum[wv] = x;
+    __syncthreads();
+    uint32_t base = 0, all = 0;
+#pragma unroll
+    for (uint32_t w = 0; w < EN_THREADS / 64; ++w) {
+        const uint32_t t = wsum[w];
+        base += w < wv ? t : 0u;
+        all += t;
+    }
+    total = all;
+    return base + x - v;
+}
+#endif
 __global__ __launch_bounds__(EN_THREADS) void k_dfl_encode(DeflateArgs A) {
     __shared__ uint32_t codes[L_CODES + D_CODES];
     __shared__ uint8_t lcode_t[256], dcode_t[512];
     __shared__ uint16_t lbase[29], dbase[30];
+#if EN_V2
+    __shared__ uint8_t xl_t[32], xd_t[32];
+    __shared__ uint32_t wsum2[2][EN_THREADS / 64];
+    __shared__ uint32_t stg2[2][EN_STG_WORDS];
+#else
     __shared__ uint32_t wsum[EN_THREADS / 64];
     __shared__ uint32_t stg[EN_STG_WORDS];
+#endif
     __shared__ uint64_t sh_end, sh_al;
     __shared__ uint32_t sh_bad;
     const uint32_t sid = blockIdx.x, tid = threadIdx.x;
@@ -3678,6 +3717,17 @@ __global__ __launch_bounds__(EN_THREADS) void k_dfl_encode(DeflateArgs A) {
     for (uint32_t i = tid; i < 512; i += EN_THREADS) dcode_t[i] = T->dist_code[i];
     if (tid < 29) lbase[tid] = T->base_length[tid];
     if (tid < 30) dbase[tid] = T->base_dist[tid];
+#if EN_V2
+    if (tid < 29) xl_t[tid] = T->extra_lbits[tid];
+    if (tid < 30) xd_t[tid] = T->extra_dbits[tid];
+    for (uint32_t i = tid; i < 2 * EN_STG_WORDS; i += EN_THREADS) (&stg2[0][0])[i] = 0;
+    uint32_t rowpar = 0;                                     // which half of the double buffers
+#define EN_XL(c) xl_t[c]
+#define EN_XD(c) xd_t[c]
+#else
+#define EN_XL(c) c_extra_lbits[c]
+#define EN_XD(c) c_extra_dbits[c]
+#endif
     const uint32_t nblk = F->nblk;
     const bool gzip = A.format == SDZ_DEFLATE_GZIP;
     const uint32_t hdr_bytes = A.format == SDZ_DEFLATE_ZLIB ? 2 : gzip ? 10 + (A.fname_len ? A.fname_len + 1 : 0) : 0;
@@ -3770,13 +3820,13 @@ __global__ __launch_bounds__(EN_THREADS) void k_dfl_encode(DeflateArgs A) {
             if (j == nsym) { const uint32_t c = codes[END_BLOCK]; lo = c & 0xffffu; nlo = c >> 16; nhi = 0; hi = 0; return; }
             const uint32_t s = sym[sym0 + j], lc = s & 255u, dist = s >> 8;
             if (dist == 0) { const uint32_t c = codes[lc]; lo = c & 0xffffu; nlo = c >> 16; nhi = 0; hi = 0; return; }
-            const uint32_t lcode = lcode_t[lc], c = codes[257 + lcode], cl = c >> 16, xl = c_extra_lbits[lcode];
+            const uint32_t lcode = lcode_t[lc], c = codes[257 + lcode], cl = c >> 16, xl = EN_XL(lcode);
             lo = (c & 0xffffu) | (xl ? (lc - lbase[lcode]) << cl : 0u);   // code 28 (258): no extra bits
             nlo = cl + xl;
             const uint32_t d = dist - 1, dc = d < 256 ? dcode_t[d] : dcode_t[256 + (d >> 7)];
             const uint32_t e = codes[L_CODES + dc], el = e >> 16;
             hi = (e & 0xffffu) | ((d - dbase[dc]) << el);
-            nhi = el + c_extra_dbits[dc];
+            nhi = el + EN_XD(dc);
         };
         // rows of EN_THREADS symbols (coalesced reads): scan the bit counts, OR each symbol's
         // bits into an LDS image of the row, write the image out (edge words OR-ed)
@@ -3787,14 +3837,23 @@ __global__ __launch_bounds__(EN_THREADS) void k_dfl_encode(DeflateArgs A) {
             uint32_t lo = 0, nlo = 0, hi = 0, nhi = 0;
             if (j < items) sym_bits(j, lo, nlo, hi, nhi);
             uint32_t tot;
+#if EN_V2
+            // stg2[rowpar] is all zero here: the row that used it last zeroed what it wrote
+            uint32_t* stg = stg2[rowpar];
+            const uint32_t excl = en_scan2(nlo + nhi, wsum2[rowpar], tot);
+            rowpar ^= 1u;
+#else
             const uint32_t excl = en_scan(nlo + nhi, wsum, tot);
+#endif
             // pending_buf bytes written before symbol j is read (SURVEY A7 overlay)
             const uint64_t pend = 2 * ((carry + (rowbit + excl - b0)) >> 4);
             if (j < nsym && pend > (uint64_t)D_BUF + 2 * j) bad = 1;
             const uint64_t a0 = rowbit + bias, wbase = a0 >> 5;
             const uint32_t nw = (uint32_t)(((a0 + tot + 31) >> 5) - wbase);
+#if !EN_V2
             for (uint32_t i = tid; i < nw; i += EN_THREADS) stg[i] = 0;
             __syncthreads();
+#endif
             const uint32_t at = (uint32_t)(a0 - wbase * 32) + excl;
             if (nlo) {
                 const uint32_t w = at >> 5, sh = at & 31;
@@ -3809,11 +3868,16 @@ __global__ __launch_bounds__(EN_THREADS) void k_dfl_encode(DeflateArgs A) {
             __syncthreads();
             for (uint32_t i = tid; i < nw; i += EN_THREADS) {
                 const uint32_t v = stg[i];
+#if EN_V2
+                stg[i] = 0;                                  // (for the row after next)
+#endif
                 const bool edge = (i == 0 && (a0 & 31)) || (i == nw - 1 && ((a0 + tot) & 31));
                 if (!edge) ow[wbase + i] = v;
                 else if (v) atomicOr((uint32_t*)&ow[wbase + i], v);
             }
+#if !EN_V2
             __syncthreads();
+#endif
             rowbit += tot;
         }
     }
