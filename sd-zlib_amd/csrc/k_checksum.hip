@@ -12,13 +12,21 @@
 
 namespace sdz {
 
-#define CK_THREADS 64
+#define CK_THREADS 256
+#define CK_BLK 256                        // adler32 NMAX blocks per pass (LDS partials)
 
-// block sid = blockIdx.x of a batch (in_off / in_len / seed / result indexed by it)
+// block sid = blockIdx.x of a batch (in_off / in_len / seed / result indexed by it).
+// adler32: the stream's 5552-byte blocks go to the workgroup's waves (16-byte loads, byte sums
+// and index-weighted sums by v_dot4), their partials T = sum b_i and W = sum (blen - i) b_i into
+// LDS, and one thread chains them exactly as adler32.ts does (a one-wave serial walk over the
+// blocks with byte loads took 0.88 ms for a 481 KB buffer; one-buffer deflate() waits for it).
+// crc32: wave 0 (crc32_wave).
 __device__ __forceinline__ void k_checksum_body(const uint8_t* in, const uint64_t* in_off, const uint64_t* in_len,
                                                 const int32_t* seed, int32_t* result, int kind) {
     __shared__ CrcTables ct;
-    uint32_t lane = threadIdx.x;
+    __shared__ uint32_t ck_T[CK_BLK];
+    __shared__ uint64_t ck_W[CK_BLK];
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
     if (kind != 0) crc_tables_init(ct);
     __syncthreads();
     uint32_t sid = blockIdx.x;
@@ -28,28 +36,54 @@ __device__ __forceinline__ void k_checksum_body(const uint8_t* in, const uint64_
 
     if (kind == 0) {                                     // adler32
         uint64_t s1 = sd & 0xffffu, s2 = (sd >> 16) & 0xffffu;
-        uint64_t nblk = len / 5552, rem = len % 5552;
-        for (uint64_t b = 0; b <= nblk; ++b) {
-            uint32_t blen = b < nblk ? 5552u : (uint32_t)rem;
-            if (blen == 0) break;
-            const uint8_t* q = p + b * 5552;
-            uint64_t T = 0, W = 0;
-            for (uint32_t i = lane; i < blen; i += CK_THREADS) {
-                uint32_t v = q[i];
-                T += v;
-                W += (uint64_t)(blen - i) * v;
+        const uint64_t nblk = len / 5552, rem = len % 5552, nall = nblk + (rem ? 1u : 0u);
+        for (uint64_t c0 = 0; c0 < nall; c0 += CK_BLK) {
+            const uint32_t nc = (uint32_t)(nall - c0 < CK_BLK ? nall - c0 : CK_BLK);
+            for (uint32_t k = wv; k < nc; k += CK_THREADS / 64) {
+                const uint64_t b = c0 + k;
+                const uint32_t blen = b < nblk ? 5552u : (uint32_t)rem;
+                const uint8_t* q = p + b * 5552;
+                // 16-byte aligned pieces covering [q, q + blen): each holds a byte of the block,
+                // so no load leaves the pages the buffer lies in; bytes outside are masked off
+                const uintptr_t a0 = (uintptr_t)q & ~(uintptr_t)15;
+                const uint32_t lead = (uint32_t)((uintptr_t)q - a0), npc = (lead + blen + 15u) >> 4;
+                uint32_t T = 0;
+                int64_t I = 0;                                // sum i b_i (block index i)
+                for (uint32_t c = lane; c < npc; c += 64) {
+                    const uint4 v4 = *(const uint4*)(a0 + 16u * (uintptr_t)c);
+                    const uint32_t wd[4] = { v4.x, v4.y, v4.z, v4.w };
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        const int32_t ib = (int32_t)(16u * c + 4u * (uint32_t)j) - (int32_t)lead;   // index of byte 0
+                        const int32_t lo = ib < 0 ? -ib : 0, hi = (int32_t)blen - ib;               // valid bytes [lo, hi)
+                        const uint32_t mlo = lo >= 4 ? 0u : ~0u << (8 * lo);
+                        const uint32_t mhi = hi >= 4 ? ~0u : hi <= 0 ? 0u : (1u << (8 * hi)) - 1u;
+                        const uint32_t x = wd[j] & mlo & mhi;
+                        const uint32_t sb = __builtin_amdgcn_udot4(x, 0x01010101u, 0u, false);
+                        T += sb;
+                        I += (int64_t)ib * sb + __builtin_amdgcn_udot4(x, 0x03020100u, 0u, false);
+                    }
+                }
+                for (int o = 32; o > 0; o >>= 1) {
+                    T += __shfl_xor(T, o);
+                    I += __shfl_xor(I, o);
+                }
+                if (lane == 0) { ck_T[k] = T; ck_W[k] = (uint64_t)blen * T - (uint64_t)I; }
             }
-            for (int o = 32; o > 0; o >>= 1) {
-                T += __shfl_xor(T, o);
-                W += __shfl_xor(W, o);
-            }
-            s2 += (uint64_t)blen * s1 + W;
-            s1 += T;
-            if (b < nblk) { s1 %= 65521u; s2 += 65521u; }
-            else { s1 %= 65521u; s2 %= 65521u; }
+            __syncthreads();
+            if (tid == 0)
+                for (uint32_t k = 0; k < nc; ++k) {               // adler32.ts:45-67, block by block
+                    const uint64_t b = c0 + k;
+                    const uint32_t blen = b < nblk ? 5552u : (uint32_t)rem;
+                    s2 += (uint64_t)blen * s1 + ck_W[k];
+                    s1 += ck_T[k];
+                    if (b < nblk) { s1 %= 65521u; s2 += 65521u; }
+                    else { s1 %= 65521u; s2 %= 65521u; }
+                }
+            __syncthreads();
         }
-        if (lane == 0) result[sid] = (int32_t)((uint32_t)s1 | ((uint32_t)s2 << 16));
-    } else {                                             // crc32
+        if (tid == 0) result[sid] = (int32_t)((uint32_t)s1 | ((uint32_t)s2 << 16));
+    } else if (wv == 0) {                                // crc32
         const uint32_t crc = crc32_wave(p, len, ct);
         if (lane == 0) result[sid] = (int32_t)(gf2_mulmod(gf2_xbytes(len, ct.x2n), sd) ^ crc);
     }

@@ -2867,6 +2867,7 @@ __global__ __launch_bounds__(64) void k_fz_fix(DeflateArgs A) {
 // whose I changed anywhere goes another round
 __global__ __launch_bounds__(LZ_THREADS) void k_fz_merge(DeflateArgs A) {
     const uint32_t seg = blockIdx.x * LZ_THREADS + threadIdx.x;
+    if (seg == 0) *A.lz_nact = 0;                          // k_fz_roll counts into it next (no memset launch)
     if (seg >= A.nlseg) return;
     const LzSeg q = lz_seg(A, seg);
     if (!(A.lz_act[q.k] & 1u)) return;
@@ -3989,10 +3990,12 @@ void launch_deflate(const DeflateArgs& a, hipStream_t st, hipStream_t side, hipE
                         hipLaunchKernelGGL(k_fz_join, gseg, dim3(LZ_THREADS), 0, st, r);
                         hipLaunchKernelGGL(k_fz_fix, dim3(a.n), dim3(64), 0, st, r);
                         hipLaunchKernelGGL(k_fz_merge, gseg, dim3(LZ_THREADS), 0, st, r);
-                        (void)hipMemsetAsync(a.lz_nact, 0, 4, st);
                         hipLaunchKernelGGL(k_fz_roll, dim3((a.n + 255) / 256), dim3(256), 0, st, r);
                     }
-                    uint32_t moving = 0;
+                    uint32_t moving_pageable = 0;
+                    uint32_t* const pw = rt_pinned_words();
+                    uint32_t& moving = pw ? pw[1] : moving_pageable;
+                    moving = 0;
                     if (hipMemcpyAsync(&moving, a.lz_nact, 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
                         hipStreamSynchronize(st) != hipSuccess || moving == 0)
                         break;

@@ -1897,6 +1897,9 @@ __global__ __launch_bounds__(IL_THREADS, 1) void k_inflate_wcold(InflateArgs A, 
     uint8_t* region = lane_region();
     uint32_t* ts = lane_stage();
     const uint32_t gid = blockIdx.x * IL_STREAMS + lane_slot();
+    // the counters k_inflate_wdec fills next (no memset launch between the pair; this kernel
+    // does not read them)
+    if (blockIdx.x == 0 && threadIdx.x == 0) { A.active[0] = 0; A.active[1] = 0; }
     if (gid >= A.n || (threadIdx.x & 63u) >= IL_WAVE_LANES) return;
     const uint32_t sid = gid;
     DSave* S = (DSave*)A.dsave + sid;
@@ -2098,7 +2101,6 @@ int run_inflate_rounds(const InflateArgs& a, hipStream_t s, uint32_t* host_activ
                 hipLaunchKernelGGL(k_inflate_wcold, g1, dim3(IL_THREADS), 0, s, a, round, it == 0 ? 1u : 0u,
                                    it >= lane_after ? 1u : 0u);
                 DBG_SYNC(s, "k_inflate_wcold", round, it);
-                if (hipMemsetAsync(a.active, 0, 2 * sizeof(uint32_t), s) != hipSuccess) { rc = -1; break; }
                 hipLaunchKernelGGL(k_inflate_wdec, dim3(a.n), dim3(64), 0, s, a, round);
                 DBG_SYNC(s, "k_inflate_wdec", round, it);
                 if (hipMemcpyAsync(host_active, a.active + 1, sizeof(uint32_t), hipMemcpyDeviceToHost, s) != hipSuccess ||

@@ -115,6 +115,9 @@ struct Pinned {
     int get(size_t bytes, void** out, bool wait = true);
     int done(hipStream_t s);
 };
+// a few pinned host words of this thread for the round drivers' counter read-backs (a copy into
+// pageable memory goes through a staging buffer; null if the allocation failed)
+uint32_t* pinned_words();
 extern Pinned g_pinned;
 extern Pinned g_plan_pinned;                      // the deflate plan's staging (beside a host batch's)
 

@@ -216,6 +216,8 @@ void launch_checksum_one(const uint8_t* in, uint64_t len, int kind, int32_t seed
 // batched span copy (k_gather.hip)
 void launch_gather(uint8_t* dst, const uint64_t* dst_off, const uint8_t* src, const uint64_t* src_off,
                    const uint64_t* len, uint32_t n, hipStream_t s);
+// a few pinned host words of this thread (sdz_runtime.cpp) for a round driver's counter read-back
+uint32_t* rt_pinned_words();
 // a small host call's [outputs | records] region back into mapped pinned memory (k_gather.hip)
 void launch_copy_back(uint8_t* dst, const uint8_t* src, const uint64_t* out_off, const uint64_t* out_cap,
                       uint64_t rec_off, uint32_t rsz, uint32_t len_off, uint32_t m, hipStream_t s);

@@ -169,6 +169,16 @@ void timing_end(hipStream_t s) {
     g_ev_pending = true;
 }
 
+uint32_t* pinned_words() {
+    struct W {
+        uint32_t* p = nullptr;
+        ~W() { if (p) (void)hipHostFree(p); }
+    };
+    static thread_local W w;
+    if (!w.p && hipHostMalloc((void**)&w.p, 64, hipHostMallocDefault) != hipSuccess) w.p = nullptr;
+    return w.p;
+}
+
 int Pinned::done(hipStream_t s) {
     int d = 0;
     if (int rc = cur_device(&d)) return rc;
@@ -180,6 +190,7 @@ int Pinned::done(hipStream_t s) {
 }
 
 }  // namespace rt
+uint32_t* rt_pinned_words() { return rt::pinned_words(); }
 }  // namespace sdz
 
 using namespace sdz::rt;
@@ -397,7 +408,9 @@ int inflate_scratch(InflateArgs& a, uint32_t n, bool own_state, size_t extra, hi
 thread_local float g_restart_ms = 0.f;
 int inflate_run(InflateArgs& a, hipStream_t s, bool timing_started = false, int (*hook)(void*) = nullptr,
                 void* hook_ctx = nullptr) {
-    static thread_local uint32_t host_active = 0;
+    static thread_local uint32_t host_active_pageable = 0;
+    uint32_t* const pw = pinned_words();
+    uint32_t& host_active = pw ? pw[0] : host_active_pageable;
     a.dbg = nullptr;
     const bool phases = getenv("SDZ_PHASE_TIMING") != nullptr;   // development aid
     if (phases) {
