@@ -1216,9 +1216,9 @@ __device__ __forceinline__ uint32_t pm_w4(const uint8_t* w, uint32_t x) {   // 4
     const uint32_t* w32 = (const uint32_t*)w;
     return __builtin_amdgcn_alignbyte(w32[(x >> 2) + 1], w32[x >> 2], x & 3u);
 }
-uint32_t deflate_match_segs(uint64_t len) {
+uint32_t deflate_match_segs(uint64_t len, uint32_t seg) {
     const uint64_t tail = len > PM_TAIL ? len - PM_TAIL : 0;
-    return (uint32_t)((tail + PM_SEG - 1) / PM_SEG);
+    return (uint32_t)((tail + seg - 1) / seg);
 }
 __device__ uint32_t win_byte(const GLB uint8_t* in, int64_t n, int64_t off, int64_t i);
 __device__ __forceinline__ int64_t slide_off(int64_t n, int64_t P);
@@ -1259,7 +1259,10 @@ __global__ __launch_bounds__(PM_THREADS) void k_dfl_match(DeflateArgs A) {
     if (rp == ~0ull) return;
     const int n = (int)in_len;
     const int tail = n > PM_TAIL ? n - PM_TAIL : 0;
-    const int s0 = (int)(seg * PM_SEG), e0 = s0 + (A.seg_merge && seg == 0 ? 3 * PM_SEG : PM_SEG);
+    // (segments of pm_seg <= PM_SEG positions: few streams spread over more workgroups; the LDS
+    // window is sized for PM_SEG, and every segment stages its own 32 KiB of history)
+    const int pseg = A.pm_seg ? (int)A.pm_seg : PM_SEG;
+    const int s0 = (int)seg * pseg, e0 = s0 + (A.seg_merge && seg == 0 ? 3 * pseg : pseg);
     // the stream's last segment also takes the last positions (A.tail_in_match): all of them are
     // handed out, the larger window-offset group [mlo, mhi) is searched, the rest are left to
     // k_dfl_tail (which runs after and overwrites their records)
@@ -2419,20 +2422,48 @@ __global__ __launch_bounds__(LZ_THREADS) void k_lz_count(DeflateArgs A) {
     if (seg + 1 == A.lz_sg0[q.k + 1]) cnt += A.lz_fin[q.k] & 1u;
     A.lz_cnt[seg] = cnt;
 }
-__global__ __launch_bounds__(LZ_THREADS) void k_lz_scan(DeflateArgs A) {
-    const uint32_t k = blockIdx.x * LZ_THREADS + threadIdx.x;
-    if (k >= A.n || A.rp0[k] == ~0ull) return;
+// one workgroup per stream: the exclusive scan of its segments' symbol counts, 256 at a time
+// (a lane walking a long stream's ~1,000 segments serially took 0.3 ms of a one-buffer deflate)
+#define LS_THREADS 256
+template <int CTRL, int ROWS>
+__device__ __forceinline__ uint32_t ls_dpp_add(uint32_t x) {
+    return x + (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, ROWS, 0xf, false);
+}
+__global__ __launch_bounds__(LS_THREADS) void k_lz_scan(DeflateArgs A) {
+    __shared__ uint32_t wsum[LS_THREADS / 64];
+    const uint32_t k = blockIdx.x, tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
+    if (k >= A.n || A.rp0[k] == ~0ull) return;              // (block-uniform)
+    const uint32_t s0 = A.lz_sg0[k], s1 = A.lz_sg0[k + 1];
     uint32_t o = 0;
-    for (uint32_t s = A.lz_sg0[k]; s < A.lz_sg0[k + 1]; ++s) {
-        const uint32_t c = A.lz_cnt[s];
-        A.lz_cnt[s] = o;
-        o += c;
+    for (uint32_t b = s0; b < s1; b += LS_THREADS) {
+        const uint32_t s = b + tid;
+        const uint32_t c = s < s1 ? A.lz_cnt[s] : 0u;
+        uint32_t x = c;                                     // inclusive wave scan (DPP)
+        x = ls_dpp_add<0x111, 0xf>(x);
+        x = ls_dpp_add<0x112, 0xf>(x);
+        x = ls_dpp_add<0x114, 0xf>(x);
+        x = ls_dpp_add<0x118, 0xf>(x);
+        x = ls_dpp_add<0x142, 0xa>(x);
+        x = ls_dpp_add<0x143, 0xc>(x);
+        if (lane == 63) wsum[wv] = x;
+        __syncthreads();
+        uint32_t base = 0, all = 0;
+#pragma unroll
+        for (uint32_t w = 0; w < LS_THREADS / 64; ++w) {
+            const uint32_t t = wsum[w];
+            base += w < wv ? t : 0u;
+            all += t;
+        }
+        if (s < s1) A.lz_cnt[s] = o + base + x - c;
+        o += all;
+        __syncthreads();                                    // (wsum is rewritten next)
     }
-    // (no segment: NO_FLUSH before MIN_LOOKAHEAD bytes, nothing parsed)
-    const uint32_t fin = A.lz_sg0[k + 1] > A.lz_sg0[k] ? (A.lz_fin[k] & 1u) : 0u;
-    if (A.lz_sg0[k + 1] == A.lz_sg0[k])
-        ((GLB FStream*)((GLB DSlab*)(A.state + (uint64_t)k * SLAB_BYTES))->window)->pad[0] = 0u;
-    A.lz_fin[k] = fin | (o << 1);
+    if (tid == 0) {
+        // (no segment: NO_FLUSH before MIN_LOOKAHEAD bytes, nothing parsed)
+        const uint32_t fin = s1 > s0 ? (A.lz_fin[k] & 1u) : 0u;
+        if (s1 == s0) ((GLB FStream*)((GLB DSlab*)(A.state + (uint64_t)k * SLAB_BYTES))->window)->pad[0] = 0u;
+        A.lz_fin[k] = fin | (o << 1);
+    }
 }
 // symbols to the front of the stream's record buffer (no record is read any more)
 __global__ __launch_bounds__(LZ_THREADS) void k_lz_emit(DeflateArgs A) {
@@ -3644,8 +3675,9 @@ __global__ __launch_bounds__(64) void k_dfl_trees(DeflateArgs A) {   // grid (n,
 // 16-bit pending units behind the overlay check; stored blocks' byte alignment), the group
 // zeroes the output slot, then for each block every thread packs a run of symbols at its
 // prefix-summed bit offset: whole words are stored, the partial words at run edges OR-ed.
-#define EN_THREADS 256
-#define EN_STG_WORDS (EN_THREADS * 48 / 32 + 2)        // one row's bits (<= 48 per symbol)
+#define EN_THREADS 256                                // (batches; few streams: 1024, k_dfl_encode_t<1024>)
+#define EN_STG_WORDS_T(NT) ((NT) * 48 / 32 + 2)       // one row's bits (<= 48 per symbol)
+template <int NT>
 __device__ __forceinline__ uint32_t en_scan(uint32_t v, uint32_t* wsum, uint32_t& total) {
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
     uint32_t x = v;
@@ -3656,7 +3688,7 @@ __device__ __forceinline__ uint32_t en_scan(uint32_t v, uint32_t* wsum, uint32_t
     if (lane == 63) wsum[wv] = x;
     __syncthreads();
     uint32_t base = 0, all = 0;
-    for (uint32_t w = 0; w < EN_THREADS / 64; ++w) { base += w < wv ? wsum[w] : 0u; all += wsum[w]; }
+    for (uint32_t w = 0; w < NT / 64; ++w) { base += w < wv ? wsum[w] : 0u; all += wsum[w]; }
     __syncthreads();
     total = all;
     return base + x - v;
@@ -3672,6 +3704,7 @@ __device__ __forceinline__ uint32_t en_dpp_add(uint32_t x) {
 // the row's exclusive prefix of v over the workgroup and its total: an inclusive wave scan
 // with DPP row shifts / broadcasts, the wave sums through wsum (this row's half of a double
 // buffer: the next row writes the other half, so one barrier per row suffices)
+template <int NT>
 __device__ __forceinline__ uint32_t en_scan2(uint32_t v, uint32_t* wsum, uint32_t& total) {
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
     uint32_t x = v;
@@ -3685,7 +3718,7 @@ __device__ __forceinline__ uint32_t en_scan2(uint32_t v, uint32_t* wsum, uint32_
     __syncthreads();
     uint32_t base = 0, all = 0;
 #pragma unroll
-    for (uint32_t w = 0; w < EN_THREADS / 64; ++w) {
+    for (uint32_t w = 0; w < NT / 64; ++w) {
         const uint32_t t = wsum[w];
         base += w < wv ? t : 0u;
         all += t;
@@ -3694,17 +3727,18 @@ __device__ __forceinline__ uint32_t en_scan2(uint32_t v, uint32_t* wsum, uint32_
     return base + x - v;
 }
 #endif
-__global__ __launch_bounds__(EN_THREADS) void k_dfl_encode(DeflateArgs A) {
+template <int NT>
+__global__ __launch_bounds__(NT) void k_dfl_encode_t(DeflateArgs A) {
     __shared__ uint32_t codes[L_CODES + D_CODES];
     __shared__ uint8_t lcode_t[256], dcode_t[512];
     __shared__ uint16_t lbase[29], dbase[30];
 #if EN_V2
     __shared__ uint8_t xl_t[32], xd_t[32];
-    __shared__ uint32_t wsum2[2][EN_THREADS / 64];
-    __shared__ uint32_t stg2[2][EN_STG_WORDS];
+    __shared__ uint32_t wsum2[2][NT / 64];
+    __shared__ uint32_t stg2[2][EN_STG_WORDS_T(NT)];
 #else
-    __shared__ uint32_t wsum[EN_THREADS / 64];
-    __shared__ uint32_t stg[EN_STG_WORDS];
+    __shared__ uint32_t wsum[NT / 64];
+    __shared__ uint32_t stg[EN_STG_WORDS_T(NT)];
 #endif
     __shared__ uint64_t sh_end, sh_al;
     __shared__ uint32_t sh_bad;
@@ -3714,14 +3748,14 @@ __global__ __launch_bounds__(EN_THREADS) void k_dfl_encode(DeflateArgs A) {
     GLB FStream* F = (GLB FStream*)S->window;
     if (F->flag) return;
     const GLB DTables* T = (const GLB DTables*)&g_dt;
-    for (uint32_t i = tid; i < 256; i += EN_THREADS) lcode_t[i] = T->length_code[i];
-    for (uint32_t i = tid; i < 512; i += EN_THREADS) dcode_t[i] = T->dist_code[i];
+    for (uint32_t i = tid; i < 256; i += NT) lcode_t[i] = T->length_code[i];
+    for (uint32_t i = tid; i < 512; i += NT) dcode_t[i] = T->dist_code[i];
     if (tid < 29) lbase[tid] = T->base_length[tid];
     if (tid < 30) dbase[tid] = T->base_dist[tid];
 #if EN_V2
     if (tid < 29) xl_t[tid] = T->extra_lbits[tid];
     if (tid < 30) xd_t[tid] = T->extra_dbits[tid];
-    for (uint32_t i = tid; i < 2 * EN_STG_WORDS; i += EN_THREADS) (&stg2[0][0])[i] = 0;
+    for (uint32_t i = tid; i < 2 * EN_STG_WORDS_T(NT); i += NT) (&stg2[0][0])[i] = 0;
     uint32_t rowpar = 0;                                     // which half of the double buffers
 #define EN_XL(c) xl_t[c]
 #define EN_XD(c) xd_t[c]
@@ -3770,8 +3804,8 @@ __global__ __launch_bounds__(EN_THREADS) void k_dfl_encode(DeflateArgs A) {
         if (tid < head) out[tid] = 0;
         const uint64_t nw = (total - head) / 4;
         GLB uint32_t* w = (GLB uint32_t*)(out + head);
-        for (uint64_t i = tid; i < nw; i += EN_THREADS) w[i] = 0;
-        for (uint64_t i = head + 4 * nw + tid; i < total; i += EN_THREADS) out[i] = 0;
+        for (uint64_t i = tid; i < nw; i += NT) w[i] = 0;
+        for (uint64_t i = head + 4 * nw + tid; i < total; i += NT) out[i] = 0;
     }
     __threadfence();
     __syncthreads();
@@ -3800,12 +3834,12 @@ __global__ __launch_bounds__(EN_THREADS) void k_dfl_encode(DeflateArgs A) {
         const uint32_t type = Bk->type, hbits = Bk->hbits;
         const GLB uint32_t* tab = (const GLB uint32_t*)((const GLB uint8_t*)Bk + 64);
         const uint64_t b0 = Bk->bstart;
-        for (uint32_t i = tid; i < (hbits + 31) / 32; i += EN_THREADS) orbits(b0 + 32 * i, tab[FB_HDR_OFF / 4 + i]);
+        for (uint32_t i = tid; i < (hbits + 31) / 32; i += NT) orbits(b0 + 32 * i, tab[FB_HDR_OFF / 4 + i]);
         if (type == 0) {                                     // _tr_stored_block: aligned LEN NLEN bytes
             const uint32_t len = Bk->stored_len;
             const uint64_t pay = ((b0 + 3 + 7) & ~7ull) / 8;
             const GLB uint8_t* src = (const GLB uint8_t*)(A.in + A.in_off[sid]) + Bk->off + Bk->block_start;
-            for (uint32_t i = tid; i < 4 + len; i += EN_THREADS) {
+            for (uint32_t i = tid; i < 4 + len; i += NT) {
                 uint8_t v;
                 if (i < 4) v = (uint8_t)((i < 2 ? len : ~len) >> (8 * (i & 1)));
                 else v = src[i - 4];
@@ -3814,7 +3848,7 @@ __global__ __launch_bounds__(EN_THREADS) void k_dfl_encode(DeflateArgs A) {
             __syncthreads();
             continue;
         }
-        for (uint32_t i = tid; i < L_CODES + D_CODES; i += EN_THREADS) codes[i] = tab[i];
+        for (uint32_t i = tid; i < L_CODES + D_CODES; i += NT) codes[i] = tab[i];
         __syncthreads();
         const uint32_t sym0 = Bk->sym0, nsym = Bk->nsym, items = nsym + 1;   // + END_BLOCK
         auto sym_bits = [&](uint32_t j, uint32_t& lo, uint32_t& nlo, uint32_t& hi, uint32_t& nhi) {
@@ -3829,11 +3863,11 @@ __global__ __launch_bounds__(EN_THREADS) void k_dfl_encode(DeflateArgs A) {
             hi = (e & 0xffffu) | ((d - dbase[dc]) << el);
             nhi = el + EN_XD(dc);
         };
-        // rows of EN_THREADS symbols (coalesced reads): scan the bit counts, OR each symbol's
+        // rows of NT symbols (coalesced reads): scan the bit counts, OR each symbol's
         // bits into an LDS image of the row, write the image out (edge words OR-ed)
         const uint32_t carry = Bk->carry;
         uint64_t rowbit = b0 + hbits;                        // slot-relative bit of the row's start
-        for (uint32_t r0 = 0; r0 < items; r0 += EN_THREADS) {
+        for (uint32_t r0 = 0; r0 < items; r0 += NT) {
             const uint32_t j = r0 + tid;
             uint32_t lo = 0, nlo = 0, hi = 0, nhi = 0;
             if (j < items) sym_bits(j, lo, nlo, hi, nhi);
@@ -3841,10 +3875,10 @@ __global__ __launch_bounds__(EN_THREADS) void k_dfl_encode(DeflateArgs A) {
 #if EN_V2
             // stg2[rowpar] is all zero here: the row that used it last zeroed what it wrote
             uint32_t* stg = stg2[rowpar];
-            const uint32_t excl = en_scan2(nlo + nhi, wsum2[rowpar], tot);
+            const uint32_t excl = en_scan2<NT>(nlo + nhi, wsum2[rowpar], tot);
             rowpar ^= 1u;
 #else
-            const uint32_t excl = en_scan(nlo + nhi, wsum, tot);
+            const uint32_t excl = en_scan<NT>(nlo + nhi, wsum, tot);
 #endif
             // pending_buf bytes written before symbol j is read (SURVEY A7 overlay)
             const uint64_t pend = 2 * ((carry + (rowbit + excl - b0)) >> 4);
@@ -3852,7 +3886,7 @@ __global__ __launch_bounds__(EN_THREADS) void k_dfl_encode(DeflateArgs A) {
             const uint64_t a0 = rowbit + bias, wbase = a0 >> 5;
             const uint32_t nw = (uint32_t)(((a0 + tot + 31) >> 5) - wbase);
 #if !EN_V2
-            for (uint32_t i = tid; i < nw; i += EN_THREADS) stg[i] = 0;
+            for (uint32_t i = tid; i < nw; i += NT) stg[i] = 0;
             __syncthreads();
 #endif
             const uint32_t at = (uint32_t)(a0 - wbase * 32) + excl;
@@ -3867,7 +3901,7 @@ __global__ __launch_bounds__(EN_THREADS) void k_dfl_encode(DeflateArgs A) {
                 if (sh + nhi > 32) atomicOr(&stg[w + 1], hi >> (32 - sh));
             }
             __syncthreads();
-            for (uint32_t i = tid; i < nw; i += EN_THREADS) {
+            for (uint32_t i = tid; i < nw; i += NT) {
                 const uint32_t v = stg[i];
 #if EN_V2
                 stg[i] = 0;                                  // (for the row after next)
@@ -4006,7 +4040,7 @@ void launch_deflate(const DeflateArgs& a, hipStream_t st, hipStream_t side, hipE
                 hipLaunchKernelGGL(k_lz_fix, dim3(a.n), dim3(64), 0, st, a);
             }
             if (a.nlseg) hipLaunchKernelGGL(k_lz_count, gseg, dim3(LZ_THREADS), 0, st, a);
-            hipLaunchKernelGGL(k_lz_scan, gstr, dim3(LZ_THREADS), 0, st, a);
+            hipLaunchKernelGGL(k_lz_scan, dim3(a.n), dim3(LS_THREADS), 0, st, a);
             if (a.nlseg) hipLaunchKernelGGL(k_lz_emit, gseg, dim3(LZ_THREADS), 0, st, a);
             hipLaunchKernelGGL(k_lz_blocks, dim3(a.n), dim3(LB_THREADS), 0, st, a);
         } else if (a.wide) hipLaunchKernelGGL(k_dfl_parse_wide, dim3(a.n), dim3(PW_THREADS), 0, st, a);
@@ -4014,7 +4048,10 @@ void launch_deflate(const DeflateArgs& a, hipStream_t st, hipStream_t side, hipE
         hipLaunchKernelGGL(k_dfl_trees, dim3(a.n, a.nbmax < 32 ? (a.nbmax ? a.nbmax : 1) : 32), dim3(64), 0, st, a);
         if (fork) (void)hipStreamWaitEvent(st, ev, 0);
         else launch_checksum(a.in, a.in_off, a.in_len, nullptr, a.cks, a.n, ck_kind, st);
-        hipLaunchKernelGGL(k_dfl_encode, dim3(a.n), dim3(EN_THREADS), 0, st, a);
+        // few streams (one-buffer calls): 1,024 threads, a quarter of the rows (each row's fixed
+        // scan and barriers were most of a 481 KB stream's 0.46 ms on 256 threads)
+        if (a.n <= 16) hipLaunchKernelGGL(k_dfl_encode_t<1024>, dim3(a.n), dim3(1024), 0, st, a);
+        else hipLaunchKernelGGL(k_dfl_encode_t<EN_THREADS>, dim3(a.n), dim3(EN_THREADS), 0, st, a);
         if (a.noflush) return;                               // (the caller redoes a flagged stream)
         DeflateArgs f = a;
         f.fast = 1;                                          // streams the record path handed back

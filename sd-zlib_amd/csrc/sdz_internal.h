@@ -141,6 +141,7 @@ struct DeflateArgs {
     const uint32_t* mseg;        // match segments (PM_SEG positions each)
     uint32_t nmseg;
     uint32_t seg_merge;          // match kernels: a stream's segment 0 also covers segments 1-2
+    uint32_t pm_seg;             // k_dfl_match: positions per segment (0: PM_SEG; smaller for few streams)
     const uint32_t* cunit;       // chain units (k_dfl_chain)
     uint32_t ncunit;
     uint32_t nbmax;              // most block slots of one stream (k_dfl_trees grid)
@@ -204,7 +205,7 @@ constexpr uint64_t kDeflateRecMax = 1ull << 30;    // longest input on the recor
 constexpr uint32_t kRecUnitShift = 16;              // work units: k << 16 | unit (k, unit < 65536)
 uint64_t deflate_rec_blocks(uint64_t len);          // block slots a record-path stream needs
 uint32_t deflate_chain_units(uint64_t len);         // its k_dfl_chain units
-uint32_t deflate_match_segs(uint64_t len);          // its k_dfl_match segments
+uint32_t deflate_match_segs(uint64_t len, uint32_t seg = 16384);   // its k_dfl_match segments of `seg` positions
 // max of n device-resident u64 values (blocking; for scratch sizing); d_slot: 8 device bytes
 int device_max_u64(const uint64_t* v, uint32_t n, unsigned long long* d_slot, uint64_t* out, hipStream_t s);
 int device_sum_u64(const uint64_t* v, uint32_t n, unsigned long long* d_slot, uint64_t* out, hipStream_t s);

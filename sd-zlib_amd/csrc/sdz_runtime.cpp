@@ -1009,6 +1009,18 @@ int rt::deflate_batch_device(const uint8_t* in, const uint64_t* in_off, const ui
     // the segments final from earlier calls); SDZ_SEG_MERGE=0 turns it off
     const char* sme = getenv("SDZ_SEG_MERGE");
     const bool seg_merge = recpath && !ext && !(sme && sme[0] == '0');
+    // k_dfl_match segment size: 16 Ki positions, or for a call whose segments would not fill the
+    // chip (one buffer of a few hundred KB: ~30 workgroups on 256 CUs) the power of two >= 2 Ki
+    // that gives ~256 of them (each stages its own 32 KiB of history); SDZ_PM_SEG=N forces it
+    uint32_t pm_seg = 16384;
+    if (recpath && !ext && !match4) {
+        const uint64_t want = tot_all / 256;
+        while (pm_seg > 2048 && pm_seg / 2 >= want) pm_seg /= 2;
+        if (const char* e = getenv("SDZ_PM_SEG")) {
+            const uint32_t v = (uint32_t)atoi(e);
+            if (v >= 1024 && v <= 16384 && (v & (v - 1)) == 0) pm_seg = v;
+        }
+    }
     // per position: record 8, link 2, parse words 8 + 4 + 3 bitmaps, 4-byte link 4; per segment 28
     const uint64_t kPosBytes = (lz_shift ? 8 + 2 + 8 + 4 + 1 : 8 + 2) + (match4 ? 4 : 0);
     auto rec_cost = [&](uint32_t i) -> uint64_t {
@@ -1039,7 +1051,7 @@ int rt::deflate_batch_device(const uint8_t* in, const uint64_t* in_off, const ui
             if (on_path(i)) {
                 pos += (len[i] + 63) & ~63ull;
                 blk += deflate_rec_blocks(len[i]);
-                units += deflate_chain_units(len[i]) + deflate_match_segs(len[i]);
+                units += deflate_chain_units(len[i]) + deflate_match_segs(len[i], pm_seg);
                 segs += lz_segs(len[i]);
             }
         }
@@ -1094,7 +1106,7 @@ int rt::deflate_batch_device(const uint8_t* in, const uint64_t* in_off, const ui
                 const uint32_t nb = (uint32_t)deflate_rec_blocks(len[i]);
                 blk += nb;
                 nbmax = std::max(nbmax, nb);
-                const uint32_t ms = deflate_match_segs(len[i]);
+                const uint32_t ms = deflate_match_segs(len[i], pm_seg);
                 for (uint32_t u = 0; u < ms; ++u) {
                     if (ext && (uint64_t)(u + 1) * 16384 <= ext->rec_from) continue;   // final from earlier calls
                     if (seg_merge && u > 0) continue;    // (second pass below)
@@ -1105,7 +1117,7 @@ int rt::deflate_batch_device(const uint8_t* in, const uint64_t* in_off, const ui
             // seg_merge: every stream's segment 0 (covering segments 0-2) first, then segments 3..
             for (uint32_t k = 0; seg_merge && k < m; ++k) {
                 if (rp0[k] == ~0ull) continue;
-                const uint32_t ms = deflate_match_segs(len[b + k]);
+                const uint32_t ms = deflate_match_segs(len[b + k], pm_seg);
                 for (uint32_t u = 3; u < ms; ++u) { units.push_back(k << kRecUnitShift | u); ++nm; }
             }
             rp0[m] = pos;
@@ -1196,6 +1208,7 @@ int rt::deflate_batch_device(const uint8_t* in, const uint64_t* in_off, const ui
             a.rp0 = d_rp0; a.tb0 = d_tb0;
             a.mseg = d_units; a.nmseg = nmseg;
             a.seg_merge = seg_merge ? 1u : 0u;
+            a.pm_seg = pm_seg;
             a.cunit = d_units + nmseg; a.ncunit = (uint32_t)units.size() - nmseg;
             a.nbmax = nbmax;
             a.wide = m <= 256 ? 1u : 0u;                // few streams: the LDS-staged parse
