@@ -2493,22 +2493,14 @@ __global__ __launch_bounds__(LZ_THREADS) void k_lz_emit(DeflateArgs A) {
 // so (level > 2), and at last_lit == LIT_BUFSIZE - 1; the final literal's verdict is ignored
 // (deflate.ts:1172-1176).  At a cut, strstart - block_start is the block's bytes, less the
 // cutting match's length - 1 (its tally precedes strstart += prev_length - 1).
-#define LB_THREADS 256
+#define LB_THREADS 256                                // (batches; few streams: 1024, k_lz_blocks_t<1024>)
 struct LzSums { uint32_t mat, dxb, cov, last; };
-__device__ __forceinline__ uint32_t lb_sum(uint32_t v, uint32_t* red) {
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-    const uint32_t wv = threadIdx.x >> 6;
-    __syncthreads();
-    if ((threadIdx.x & 63) == 0) red[wv] = v;
-    __syncthreads();
-    uint32_t t = 0;
-    for (uint32_t i = 0; i < LB_THREADS / 64; ++i) t += red[i];
-    return t;
-}
-// sums over symbols [a, b): matches, extra-bit estimate, bytes covered by [a, b - 1), and by b - 1
-__device__ LzSums lb_sums(const GLB uint32_t* sym, uint32_t a, uint32_t b, uint32_t* red) {
+// sums over symbols [a, b): matches, extra-bit estimate, bytes covered by [a, b - 1), and by b - 1;
+// the four reduced together (one pair of barriers)
+template <int NT>
+__device__ LzSums lb_sums(const GLB uint32_t* sym, uint32_t a, uint32_t b, uint4* red) {
     uint32_t mat = 0, dxb = 0, cov = 0, last = 0;
-    for (uint32_t i = a + threadIdx.x; i < b; i += LB_THREADS) {
+    for (uint32_t i = a + threadIdx.x; i < b; i += NT) {
         const uint32_t v = sym[i], dist = v >> 8;
         const uint32_t len = dist ? (v & 255u) + MIN_MATCH : 1u;
         if (dist) {
@@ -2519,15 +2511,27 @@ __device__ LzSums lb_sums(const GLB uint32_t* sym, uint32_t a, uint32_t b, uint3
         if (i + 1 < b) cov += len;
         else last = len;
     }
-    LzSums r;
-    r.mat = lb_sum(mat, red);
-    r.dxb = lb_sum(dxb, red);
-    r.cov = lb_sum(cov, red);
-    r.last = lb_sum(last, red);
+    for (int o = 32; o > 0; o >>= 1) {
+        mat += __shfl_xor(mat, o);
+        dxb += __shfl_xor(dxb, o);
+        cov += __shfl_xor(cov, o);
+        last += __shfl_xor(last, o);
+    }
+    const uint32_t wv = threadIdx.x >> 6;
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) red[wv] = make_uint4(mat, dxb, cov, last);
+    __syncthreads();
+    LzSums r{0, 0, 0, 0};
+#pragma unroll
+    for (uint32_t i = 0; i < NT / 64; ++i) {
+        const uint4 t = red[i];
+        r.mat += t.x; r.dxb += t.y; r.cov += t.z; r.last += t.w;
+    }
     return r;
 }
-__global__ __launch_bounds__(LB_THREADS) void k_lz_blocks(DeflateArgs A) {
-    __shared__ uint32_t red[LB_THREADS / 64];
+template <int NT>
+__global__ __launch_bounds__(NT) void k_lz_blocks_t(DeflateArgs A) {
+    __shared__ uint4 red[NT / 64];
     const uint32_t sid = blockIdx.x;
     if (sid >= A.n) return;
     GLB DSlab* S = (GLB DSlab*)(A.state + (uint64_t)sid * SLAB_BYTES);
@@ -2556,7 +2560,7 @@ __global__ __launch_bounds__(LB_THREADS) void k_lz_blocks(DeflateArgs A) {
         uint32_t cnt = 0, eof = 0;
         int64_t step = n, strstart = n;                        // the cutting step's position; strstart after it
         if (b0 + 8192 <= nchk) {
-            const LzSums a = lb_sums(sym, b0, b0 + 8192, red);
+            const LzSums a = lb_sums<NT>(sym, b0, b0 + 8192, red);
             const int64_t in_length = a.cov + plus;
             const uint32_t out_length = (8192u * 8u + a.dxb) >> 3;
             if (trunc && a.mat < 4096 && (int64_t)out_length < in_length / 2) {
@@ -2564,7 +2568,7 @@ __global__ __launch_bounds__(LB_THREADS) void k_lz_blocks(DeflateArgs A) {
                 step = block_start + in_length;
                 strstart = block_start + a.cov + a.last;
             } else if (b0 + LIT_BUFSIZE - 1 <= nchk) {
-                const LzSums b = lb_sums(sym, b0 + 8192, b0 + LIT_BUFSIZE - 1, red);
+                const LzSums b = lb_sums<NT>(sym, b0 + 8192, b0 + LIT_BUFSIZE - 1, red);
                 cnt = LIT_BUFSIZE - 1;
                 const int64_t before = (int64_t)a.cov + a.last + b.cov;   // symbols [b0, b0 + 16382)
                 step = block_start + before + plus;
@@ -4042,7 +4046,8 @@ void launch_deflate(const DeflateArgs& a, hipStream_t st, hipStream_t side, hipE
             if (a.nlseg) hipLaunchKernelGGL(k_lz_count, gseg, dim3(LZ_THREADS), 0, st, a);
             hipLaunchKernelGGL(k_lz_scan, dim3(a.n), dim3(LS_THREADS), 0, st, a);
             if (a.nlseg) hipLaunchKernelGGL(k_lz_emit, gseg, dim3(LZ_THREADS), 0, st, a);
-            hipLaunchKernelGGL(k_lz_blocks, dim3(a.n), dim3(LB_THREADS), 0, st, a);
+            if (a.n <= 16) hipLaunchKernelGGL(k_lz_blocks_t<1024>, dim3(a.n), dim3(1024), 0, st, a);
+            else hipLaunchKernelGGL(k_lz_blocks_t<LB_THREADS>, dim3(a.n), dim3(LB_THREADS), 0, st, a);
         } else if (a.wide) hipLaunchKernelGGL(k_dfl_parse_wide, dim3(a.n), dim3(PW_THREADS), 0, st, a);
         else hipLaunchKernelGGL(k_dfl_parse, grid, dim3(64), 0, st, a);
         hipLaunchKernelGGL(k_dfl_trees, dim3(a.n, a.nbmax < 32 ? (a.nbmax ? a.nbmax : 1) : 32), dim3(64), 0, st, a);

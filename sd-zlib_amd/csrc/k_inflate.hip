@@ -1894,9 +1894,16 @@ __device__ __noinline__ int wd_iteration(DSave* S, const uint8_t* inp, uint64_t 
 // hot_epoch, as in k_inflate_decode) finishes the stream's round here.
 __global__ __launch_bounds__(IL_THREADS, 1) void k_inflate_wcold(InflateArgs A, uint32_t round, uint32_t first,
                                                                   uint32_t lane) {
+#ifdef IL_PROF                                           // development: phase clocks of stream 0, printf
+    uint64_t tq[8] = {};
+#define WC_T(k) do { if (gid == 0) tq[k] = wall_clock64(); } while (0)
+#else
+#define WC_T(k) do { } while (0)
+#endif
     uint8_t* region = lane_region();
     uint32_t* ts = lane_stage();
     const uint32_t gid = blockIdx.x * IL_STREAMS + lane_slot();
+    WC_T(0);
     // the counters k_inflate_wdec fills next (no memset launch between the pair; this kernel
     // does not read them)
     if (blockIdx.x == 0 && threadIdx.x == 0) { A.active[0] = 0; A.active[1] = 0; }
@@ -1930,13 +1937,16 @@ __global__ __launch_bounds__(IL_THREADS, 1) void k_inflate_wcold(InflateArgs A, 
         if (A.flags[sid] == 2 || S->mode == LM_DONE || S->full) return;
         force_slow = S->mode == LM_CODES ? 1 : 0;        // the wave declined the rest of this block
     }
+    WC_T(1);
     if (!init) {
         copy_dw((uint32_t*)region, (const uint32_t*)S->region, IL_REGION / 4);
         const uint32_t nt = S->ntok, b = nt & ~(IL_TSTAGE - 1u);   // the open 32-token line
         copy_dw(ts, tb + b, nt - b);
     }
+    WC_T(2);
     if (lane && !init) epochs<0>(A, S, inp, ilen, cap, tb, tcap, lens, true, G);
     else cold_run<0>(S, inp, ilen, cap, tb, tcap, lens, A.format, A.dict != nullptr, did, init, G, force_slow);
+    WC_T(3);
     Core H;                                              // flush the token stage
     H.tb = tb; H.ts = ts; H.ntok = S->ntok; H.litw = S->litw; H.nlit = S->nlit; H.tcap = tcap;
 #ifdef IL_HOT_CHECK
@@ -1946,6 +1956,12 @@ __global__ __launch_bounds__(IL_THREADS, 1) void k_inflate_wcold(InflateArgs A, 
     S->ntok = H.ntok; S->litw = 0; S->nlit = 0;
     if (S->mode == LM_CODES)
         copy_dw((uint32_t*)S->region, (const uint32_t*)region, IL_REGION / 4);
+    WC_T(4);
+#ifdef IL_PROF
+    if (gid == 0)
+        printf("WC_PROF round %u first %u init %u mode %d | entry %lu region+stage %lu cold %lu flush+save %lu [x10ns]\n",
+               round, first, init, (int)S->mode, tq[1] - tq[0], tq[2] - tq[1], tq[3] - tq[2], tq[4] - tq[3]);
+#endif
 }
 
 // One WAVE per stream: the current block's symbols by speculative iterations, until the block
