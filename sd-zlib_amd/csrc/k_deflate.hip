@@ -1192,7 +1192,7 @@ __global__ __launch_bounds__(64 * CH_WAVES) void k_dfl_chain(DeflateArgs A) {
 #define PM_CHUNK 128                                    // positions a wave takes at a time
 #endif
 #ifndef PM_REFILL
-#define PM_REFILL 8                                     // idle lanes that trigger a refill
+#define PM_REFILL 12                                    // idle lanes that trigger a refill (8: 1 % slower)
 #endif
 #ifndef PM_LAZYW4
 #define PM_LAZYW4 0                                     // measured slower: C3 543 -> 576 ms
@@ -1200,8 +1200,17 @@ __global__ __launch_bounds__(64 * CH_WAVES) void k_dfl_chain(DeflateArgs A) {
 #ifndef PM_MORE_IF
 #define PM_MORE_IF 1                                    // long compares behind one uniform test
 #endif
+#ifndef PM_COUNT
+#define PM_COUNT 0                                      // development: long-compare counters in A.dbg[16..19]
+#endif
 #ifndef PM_WBSKIP
 #define PM_WBSKIP 0                                     // the byte-at-best filter only where best >= 4
+#endif
+#ifndef PM_W8
+#define PM_W8 (!PM_LAZYW4 && !PM_WBSKIP)                // first compare over 8 bytes (default form only)
+#endif
+#ifndef PM_WBLATE
+#define PM_WBLATE 0                                     // the filter read after the 8-byte compare (measured slower: C3 344.5 -> 353.4 ms)
 #endif
 #define PM_WINB (W_SIZE + PM_SEG + PM_TAIL + MAX_MATCH + 16)   // staged window bytes (+ the last positions'
 #define PM_PV (W_SIZE + PM_SEG + PM_TAIL)                         // staged links      ... in a last segment)
@@ -1215,6 +1224,13 @@ __device__ __forceinline__ uint64_t rec_word(uint32_t full, uint32_t quarter, ui
 __device__ __forceinline__ uint32_t pm_w4(const uint8_t* w, uint32_t x) {   // 4 bytes at x, aligned reads
     const uint32_t* w32 = (const uint32_t*)w;
     return __builtin_amdgcn_alignbyte(w32[(x >> 2) + 1], w32[x >> 2], x & 3u);
+}
+// 8 bytes at x as two words (lo: bytes x..x+3, hi: x+4..x+7) from three aligned dword reads
+__device__ __forceinline__ void pm_w8(const uint8_t* w, uint32_t x, uint32_t& lo, uint32_t& hi) {
+    const uint32_t* w32 = (const uint32_t*)w + (x >> 2);
+    const uint32_t d0 = w32[0], d1 = w32[1], d2 = w32[2];
+    lo = __builtin_amdgcn_alignbyte(d1, d0, x & 3u);
+    hi = __builtin_amdgcn_alignbyte(d2, d1, x & 3u);
 }
 uint32_t deflate_match_segs(uint64_t len, uint32_t seg) {
     const uint64_t tail = len > PM_TAIL ? len - PM_TAIL : 0;
@@ -1324,9 +1340,13 @@ __global__ __launch_bounds__(PM_THREADS) void k_dfl_match(DeflateArgs A) {
     // link of a step does not wait on the previous one).  cur, nxt, bpos, qpos, limit and sp
     // (the position itself) are relative to ws; p is absolute.
     int p = s0, sp = 0, cur = 0, nxt = 0, best = 0, bpos = 0, qbest = 0, qpos = 0, chain = 0, limit = 0;
-    uint32_t s4 = 0, sbv = 0;
+    uint32_t s4 = 0, s4b = 0, sbv = 0;
+    (void)s4b;
     (void)sbv;
     unsigned long long n_live = 0, n_step = 0, n_fill = 0;   // SDZ_PHASE_TIMING counters
+#if PM_COUNT
+    unsigned long long n_it = 0, n_itl = 0, n_lst = 0, n_upd = 0;   // long-compare iterations, their lanes, steps with one
+#endif
     for (;;) {
         // Idle lanes store their records and take the next positions once PM_REFILL lanes
         // are idle (or all are): the refill and the record store then run once per several
@@ -1364,6 +1384,10 @@ __global__ __launch_bounds__(PM_THREADS) void k_dfl_match(DeflateArgs A) {
 #endif
                     limit = (p > MAX_DIST ? p - MAX_DIST : 0) - ws;   // >= 0
                     s4 = pm_w4(win, (uint32_t)sp);
+#if PM_W8
+                    s4b = pm_w4(win, (uint32_t)sp + 4u);
+#endif
+
                     bool search = cur != 0 && sp - cur <= MAX_DIST;  // deflate.ts:1092
                     if (p >= tail) {                                  // a last position (tl only)
                         // searched if in the larger group and lookahead >= MIN_MATCH; window index
@@ -1416,20 +1440,58 @@ __global__ __launch_bounds__(PM_THREADS) void k_dfl_match(DeflateArgs A) {
             f2 = win[c2 + best] == sb;
         }
         const bool cand1 = live && f1, cand2 = l2 && f2;
+#elif PM_W8 && PM_WBLATE
+        // The byte-at-best filter only decides which candidates enter the long compare: a
+        // candidate that beats best agrees at best anyway.  While best < 8 the 8-byte compare
+        // decides that exactly too, so the filter bytes are read only for lanes with best >= 8
+        // and an 8-byte prefix match, after the compare, and only when some lane has one.
+        uint32_t x1, x2, y1, y2;
+        pm_w8(win, c1, x1, y1);
+        pm_w8(win, c2, x2, y2);
+        x1 ^= s4; x2 ^= s4; y1 ^= s4b; y2 ^= s4b;
+        const bool go2 = c3 > limit && chain > 2;            // ... and after c2
+        const int c4 = pvl[l2 && go2 ? c3 : sp];
+        const bool chk1 = live && best >= 8 && (x1 | y1) == 0, chk2 = l2 && best >= 8 && (x2 | y2) == 0;
+        bool cand1 = live, cand2 = l2;
+        if (__ballot(chk1 || chk2)) {
+            if (chk1 || chk2) {
+                const uint32_t sb = win[sp + best], wb1 = win[(chk1 ? c1 : sp) + best], wb2 = win[(chk2 ? c2 : sp) + best];
+                cand1 = live && wb1 == sb;
+                cand2 = l2 && wb2 == sb;
+            }
+        }
 #else
         const uint32_t sb = win[sp + best], wb1 = win[c1 + best], wb2 = win[c2 + best];
+#if PM_W8
+        uint32_t x1, x2, y1, y2;
+        pm_w8(win, c1, x1, y1);
+        pm_w8(win, c2, x2, y2);
+        x1 ^= s4; x2 ^= s4; y1 ^= s4b; y2 ^= s4b;
+#else
         uint32_t x1 = pm_w4(win, c1) ^ s4, x2 = pm_w4(win, c2) ^ s4;
+#endif
         const bool go2 = c3 > limit && chain > 2;            // ... and after c2
         const int c4 = pvl[l2 && go2 ? c3 : sp];
         const bool cand1 = live && wb1 == sb, cand2 = l2 && wb2 == sb;
 #endif
+#if PM_W8
+        // bytes 4-7 in the same round trip (a third aligned dword): matches of 4-7 bytes, most of
+        // those that pass the filter, then need no long-compare iteration
+        int len1 = x1 ? (int)(__builtin_ctz(x1) >> 3) : y1 ? 4 + (int)(__builtin_ctz(y1) >> 3) : 8;
+        int len2 = x2 ? (int)(__builtin_ctz(x2) >> 3) : y2 ? 4 + (int)(__builtin_ctz(y2) >> 3) : 8;
+        bool more1 = cand1 && (x1 | y1) == 0, more2 = cand2 && (x2 | y2) == 0;
+#else
         int len1 = x1 ? (int)(__builtin_ctz(x1) >> 3) : 4;
         int len2 = x2 ? (int)(__builtin_ctz(x2) >> 3) : 4;
         bool more1 = cand1 && x1 == 0, more2 = cand2 && x2 == 0;
+#endif
 #if PM_MORE_IF
         // the long-compare loop behind one wave-uniform test: most steps have no lane with a
         // 4-byte prefix match, and the loop's own exit test then costs nothing more
         if (__ballot(more1 || more2)) {
+#if PM_COUNT
+            if (A.dbg) ++n_lst;
+#endif
             do {
 #else
         while (__ballot(more1 || more2)) {                   // matches of more than 4 bytes
@@ -1439,6 +1501,9 @@ __global__ __launch_bounds__(PM_THREADS) void k_dfl_match(DeflateArgs A) {
             const uint32_t x = pm_w4(win, cm + (uint32_t)lm) ^ pm_w4(win, sp + (uint32_t)lm);
             const int d = x ? (int)(__builtin_ctz(x) >> 3) : 4;
             const bool m1 = more1, m2 = !more1 && more2;
+#if PM_COUNT
+            if (A.dbg) { ++n_it; n_itl += __popcll(__ballot(more1 || more2)); }
+#endif
             len1 += m1 ? d : 0;
             len2 += m2 ? d : 0;
             more1 = m1 ? x == 0 && len1 < MAX_MATCH : more1;
@@ -1465,6 +1530,9 @@ __global__ __launch_bounds__(PM_THREADS) void k_dfl_match(DeflateArgs A) {
         qbest = cap2 ? best : qbest;
         qpos = cap2 ? bpos : qpos;
         const bool fin = live && (!w2 || (upd2 && len2 >= nice) || !go2);
+#if PM_COUNT
+        if (A.dbg) n_upd += __popcll(__ballot(upd1 || upd2));
+#endif
 #if PM_LAZYW4
         if (upd1 || upd2) sbv = win[sp + best];
 #endif
@@ -1474,6 +1542,9 @@ __global__ __launch_bounds__(PM_THREADS) void k_dfl_match(DeflateArgs A) {
         chain = fin ? 0 : chain - 2;
     }
     if (A.dbg && lane == 0) { atomicAdd(&A.dbg[13], n_live); atomicAdd(&A.dbg[14], n_step); atomicAdd(&A.dbg[15], n_fill); }
+#if PM_COUNT
+    if (A.dbg && lane == 0) { atomicAdd(&A.dbg[16], n_it); atomicAdd(&A.dbg[17], n_itl); atomicAdd(&A.dbg[18], n_lst); atomicAdd(&A.dbg[19], n_upd); }
+#endif
 }
 
 // ------------------------------------------------------------------ levels 4-9: search over 4-byte chains
