@@ -1209,6 +1209,9 @@ __global__ __launch_bounds__(64 * CH_WAVES) void k_dfl_chain(DeflateArgs A) {
 #ifndef PM_W8
 #define PM_W8 (!PM_LAZYW4 && !PM_WBSKIP)                // first compare over 8 bytes (default form only)
 #endif
+#ifndef PM_ISSUE
+#define PM_ISSUE 1                                      // every read of a step issued before the first use
+#endif
 #ifndef PM_WBLATE
 #define PM_WBLATE 0                                     // the filter read after the 8-byte compare (measured slower: C3 344.5 -> 353.4 ms)
 #endif
@@ -1343,7 +1346,8 @@ __global__ __launch_bounds__(PM_THREADS) void k_dfl_match(DeflateArgs A) {
     uint32_t s4 = 0, s4b = 0, sbv = 0;
     (void)s4b;
     (void)sbv;
-    unsigned long long n_live = 0, n_step = 0, n_fill = 0;   // SDZ_PHASE_TIMING counters
+    unsigned long long n_live = 0, n_step = 0, n_fill = 0;   // SDZ_PHASE_TIMING counters (PM_COUNT builds)
+    (void)n_live; (void)n_step; (void)n_fill;
 #if PM_COUNT
     unsigned long long n_it = 0, n_itl = 0, n_lst = 0, n_upd = 0;   // long-compare iterations, their lanes, steps with one
 #endif
@@ -1369,7 +1373,9 @@ __global__ __launch_bounds__(PM_THREADS) void k_dfl_match(DeflateArgs A) {
                 }
             }
             if (next >= q1 && nidle == 64) break;
+#if PM_COUNT
             ++n_fill;
+#endif
             if (next < q1) {
                 const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(im >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)im, 0u));
                 const int pn = next + (int)rank;
@@ -1410,7 +1416,9 @@ __global__ __launch_bounds__(PM_THREADS) void k_dfl_match(DeflateArgs A) {
         // a candidate that passes gets its exact length.  The links after c2 (c3, then c4)
         // are read in turn, so the next step starts with two candidates again.
         const bool live = chain > 0;
+#if PM_COUNT
         if (A.dbg) { ++n_step; n_live += __popcll(__ballot(live)); }
+#endif
         const bool go1 = nxt > limit && chain > 1;           // the walk continues after c1
         const bool l2 = live && go1;                          // c2 is walked (unless nice at c1)
         const uint32_t c1 = (uint32_t)(live ? cur : sp), c2 = (uint32_t)(l2 ? nxt : sp);
@@ -1462,7 +1470,21 @@ __global__ __launch_bounds__(PM_THREADS) void k_dfl_match(DeflateArgs A) {
         }
 #else
         const uint32_t sb = win[sp + best], wb1 = win[c1 + best], wb2 = win[c2 + best];
-#if PM_W8
+#if PM_W8 && PM_ISSUE
+        // both candidates' dwords issued with the link and filter reads, before any use (the
+        // scheduler otherwise waited for c1's bytes before issuing c2's reads: a round trip)
+        const uint32_t* w32 = (const uint32_t*)win;
+        const uint32_t a1 = c1 >> 2, a2 = c2 >> 2;
+        const uint32_t d10 = w32[a1], d11 = w32[a1 + 1], d12 = w32[a1 + 2];
+        const uint32_t d20 = w32[a2], d21 = w32[a2 + 1], d22 = w32[a2 + 2];
+        // then the next link (c4, on the walk's critical path) as soon as c3 is in, then the rest
+        __builtin_amdgcn_sched_barrier(0);
+        const bool go2 = c3 > limit && chain > 2;            // ... and after c2
+        const int c4 = pvl[l2 && go2 ? c3 : sp];
+        __builtin_amdgcn_sched_barrier(0);
+        uint32_t x1 = __builtin_amdgcn_alignbyte(d11, d10, c1 & 3u) ^ s4, y1 = __builtin_amdgcn_alignbyte(d12, d11, c1 & 3u) ^ s4b;
+        uint32_t x2 = __builtin_amdgcn_alignbyte(d21, d20, c2 & 3u) ^ s4, y2 = __builtin_amdgcn_alignbyte(d22, d21, c2 & 3u) ^ s4b;
+#elif PM_W8
         uint32_t x1, x2, y1, y2;
         pm_w8(win, c1, x1, y1);
         pm_w8(win, c2, x2, y2);
@@ -1470,16 +1492,20 @@ __global__ __launch_bounds__(PM_THREADS) void k_dfl_match(DeflateArgs A) {
 #else
         uint32_t x1 = pm_w4(win, c1) ^ s4, x2 = pm_w4(win, c2) ^ s4;
 #endif
+#if !(PM_W8 && PM_ISSUE)
         const bool go2 = c3 > limit && chain > 2;            // ... and after c2
         const int c4 = pvl[l2 && go2 ? c3 : sp];
+#endif
         const bool cand1 = live && wb1 == sb, cand2 = l2 && wb2 == sb;
 #endif
 #if PM_W8
         // bytes 4-7 in the same round trip (a third aligned dword): matches of 4-7 bytes, most of
         // those that pass the filter, then need no long-compare iteration
-        int len1 = x1 ? (int)(__builtin_ctz(x1) >> 3) : y1 ? 4 + (int)(__builtin_ctz(y1) >> 3) : 8;
-        int len2 = x2 ? (int)(__builtin_ctz(x2) >> 3) : y2 ? 4 + (int)(__builtin_ctz(y2) >> 3) : 8;
-        bool more1 = cand1 && (x1 | y1) == 0, more2 = cand2 && (x2 | y2) == 0;
+        // (as one 64-bit count: no branch)
+        const uint64_t v1 = ((uint64_t)y1 << 32) | x1, v2 = ((uint64_t)y2 << 32) | x2;
+        int len1 = (int)((v1 ? (uint32_t)__builtin_ctzll(v1) : 64u) >> 3);
+        int len2 = (int)((v2 ? (uint32_t)__builtin_ctzll(v2) : 64u) >> 3);
+        bool more1 = cand1 && v1 == 0, more2 = cand2 && v2 == 0;
 #else
         int len1 = x1 ? (int)(__builtin_ctz(x1) >> 3) : 4;
         int len2 = x2 ? (int)(__builtin_ctz(x2) >> 3) : 4;
@@ -1541,8 +1567,8 @@ __global__ __launch_bounds__(PM_THREADS) void k_dfl_match(DeflateArgs A) {
         pend = pend || fin;                                   // stored at the next refill
         chain = fin ? 0 : chain - 2;
     }
-    if (A.dbg && lane == 0) { atomicAdd(&A.dbg[13], n_live); atomicAdd(&A.dbg[14], n_step); atomicAdd(&A.dbg[15], n_fill); }
 #if PM_COUNT
+    if (A.dbg && lane == 0) { atomicAdd(&A.dbg[13], n_live); atomicAdd(&A.dbg[14], n_step); atomicAdd(&A.dbg[15], n_fill); }
     if (A.dbg && lane == 0) { atomicAdd(&A.dbg[16], n_it); atomicAdd(&A.dbg[17], n_itl); atomicAdd(&A.dbg[18], n_lst); atomicAdd(&A.dbg[19], n_upd); }
 #endif
 }
