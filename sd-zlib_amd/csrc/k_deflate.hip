@@ -1212,6 +1212,9 @@ __global__ __launch_bounds__(64 * CH_WAVES) void k_dfl_chain(DeflateArgs A) {
 #ifndef PM_ISSUE
 #define PM_ISSUE 1                                      // every read of a step issued before the first use
 #endif
+#ifndef PM_UNIFORM
+#define PM_UNIFORM 1                                    // the wave's queue head in SGPRs (uniform loop exit)
+#endif
 #ifndef PM_WBLATE
 #define PM_WBLATE 0                                     // the filter read after the 8-byte compare (measured slower: C3 344.5 -> 353.4 ms)
 #endif
@@ -1331,7 +1334,13 @@ __global__ __launch_bounds__(PM_THREADS) void k_dfl_match(DeflateArgs A) {
     // Positions in chunks of PM_CHUNK: each wave starts on its own chunk and takes the next
     // free one from an LDS counter when it has handed out its last position, so waves whose
     // positions have long chains do not hold up the workgroup.
+    // (the wave's queue head and end held wave-uniform -- SGPRs -- so that the loop's exit is a
+    // uniform branch: no per-lane exit masks and copies of the loop state at every step)
+#if PM_UNIFORM
+    const int c0 = s0 + (int)__builtin_amdgcn_readfirstlane(wv) * PM_CHUNK;
+#else
     const int c0 = s0 + (int)wv * PM_CHUNK;
+#endif
     int next = c0 < s1 ? c0 : s1;                           // wave-uniform queue head
     int q1 = c0 + PM_CHUNK < s1 ? c0 + PM_CHUNK : s1;
     // A lane walks while chain > 0 (chain counts the candidates left); a finished lane keeps
