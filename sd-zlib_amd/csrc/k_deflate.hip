@@ -1215,6 +1215,9 @@ __global__ __launch_bounds__(64 * CH_WAVES) void k_dfl_chain(DeflateArgs A) {
 #ifndef PM_UNIFORM
 #define PM_UNIFORM 1                                    // the wave's queue head in SGPRs (uniform loop exit)
 #endif
+#ifndef PM_SBREG
+#define PM_SBREG 0                                      // the position's byte at best in a register (measured slower: C3 312.3 -> 323.2 ms)
+#endif
 #ifndef PM_WBLATE
 #define PM_WBLATE 0                                     // the filter read after the 8-byte compare (measured slower: C3 344.5 -> 353.4 ms)
 #endif
@@ -1268,9 +1271,21 @@ __device__ __forceinline__ TailGroups tail_groups(int64_t n, int64_t tail) {
     else { t.mlo = tail; t.mhi = ps; t.offM = offA; }
     return t;
 }
+#ifndef PM_LDS0
+#define PM_LDS0 1                                       // window bytes at LDS address 0
+#endif
 __global__ __launch_bounds__(PM_THREADS) void k_dfl_match(DeflateArgs A) {
+#if PM_LDS0
+    // one LDS object: the window at address 0 and the links right after it, so every window
+    // address is the index itself and every link address folds its base into the instruction's
+    // 16-bit offset (separate arrays put the larger link array first, the window at 96.5 KiB)
+    __shared__ __attribute__((aligned(16))) struct { uint8_t win[(PM_WINB + 15) & ~15]; uint16_t pvl[PM_PV]; } pm_lds;
+    uint8_t* const win = pm_lds.win;
+    uint16_t* const pvl = pm_lds.pvl;
+#else
     __shared__ __attribute__((aligned(16))) uint8_t win[(PM_WINB + 15) & ~15];
     __shared__ __attribute__((aligned(16))) uint16_t pvl[PM_PV];
+#endif
     __shared__ int pm_next;                                 // first position not yet handed to a wave
     const uint32_t tid = threadIdx.x;
     const uint32_t lane = tid & 63u, wv = tid >> 6;
@@ -1402,6 +1417,9 @@ __global__ __launch_bounds__(PM_THREADS) void k_dfl_match(DeflateArgs A) {
 #if PM_W8
                     s4b = pm_w4(win, (uint32_t)sp + 4u);
 #endif
+#if PM_SBREG
+                    sbv = (s4 >> 16) & 255u;                    // the position's byte at best = 2
+#endif
 
                     bool search = cur != 0 && sp - cur <= MAX_DIST;  // deflate.ts:1092
                     if (p >= tail) {                                  // a last position (tl only)
@@ -1478,7 +1496,11 @@ __global__ __launch_bounds__(PM_THREADS) void k_dfl_match(DeflateArgs A) {
             }
         }
 #else
+#if PM_SBREG
+        const uint32_t sb = sbv, wb1 = win[c1 + best], wb2 = win[c2 + best];
+#else
         const uint32_t sb = win[sp + best], wb1 = win[c1 + best], wb2 = win[c2 + best];
+#endif
 #if PM_W8 && PM_ISSUE
         // both candidates' dwords issued with the link and filter reads, before any use (the
         // scheduler otherwise waited for c1's bytes before issuing c2's reads: a round trip)
@@ -1520,6 +1542,9 @@ __global__ __launch_bounds__(PM_THREADS) void k_dfl_match(DeflateArgs A) {
         int len2 = x2 ? (int)(__builtin_ctz(x2) >> 3) : 4;
         bool more1 = cand1 && x1 == 0, more2 = cand2 && x2 == 0;
 #endif
+#if PM_SBREG
+        uint32_t lb1 = 0, lb2 = 0;                            // the position's byte where a long compare ended
+#endif
 #if PM_MORE_IF
         // the long-compare loop behind one wave-uniform test: most steps have no lane with a
         // 4-byte prefix match, and the loop's own exit test then costs nothing more
@@ -1533,9 +1558,19 @@ __global__ __launch_bounds__(PM_THREADS) void k_dfl_match(DeflateArgs A) {
 #endif
             const uint32_t cm = more1 ? c1 : c2;
             const int lm = more1 ? len1 : len2;
+#if PM_SBREG
+            const uint32_t wsp = pm_w4(win, sp + (uint32_t)lm);
+            const uint32_t x = pm_w4(win, cm + (uint32_t)lm) ^ wsp;
+#else
             const uint32_t x = pm_w4(win, cm + (uint32_t)lm) ^ pm_w4(win, sp + (uint32_t)lm);
+#endif
             const int d = x ? (int)(__builtin_ctz(x) >> 3) : 4;
             const bool m1 = more1, m2 = !more1 && more2;
+#if PM_SBREG
+            const uint32_t xb = (wsp >> (8 * (d & 3))) & 255u;
+            lb1 = m1 ? xb : lb1;
+            lb2 = m2 ? xb : lb2;
+#endif
 #if PM_COUNT
             if (A.dbg) { ++n_it; n_itl += __popcll(__ballot(more1 || more2)); }
 #endif
@@ -1570,6 +1605,11 @@ __global__ __launch_bounds__(PM_THREADS) void k_dfl_match(DeflateArgs A) {
 #endif
 #if PM_LAZYW4
         if (upd1 || upd2) sbv = win[sp + best];
+#endif
+#if PM_SBREG
+        // the position's byte at the new best: in the first 8 bytes (registers), else where the
+        // long compare that set it ended (a best of MAX_MATCH ends the walk: nice <= MAX_MATCH)
+        sbv = best < 8 ? __builtin_amdgcn_perm(s4b, s4, 0x0c0c0c00u | (uint32_t)best) : upd2 ? lb2 : upd1 ? lb1 : sbv;
 #endif
         cur = c3;
         nxt = c4;
