@@ -1218,6 +1218,9 @@ __global__ __launch_bounds__(64 * CH_WAVES) void k_dfl_chain(DeflateArgs A) {
 #ifndef PM_SBREG
 #define PM_SBREG 0                                      // the position's byte at best in a register (measured slower: C3 312.3 -> 323.2 ms)
 #endif
+#ifndef PM_SELFILL
+#define PM_SELFILL 0                                    // refill without a divergent region (measured slower: C3 309.4 -> 312.7 ms)
+#endif
 #ifndef PM_WBLATE
 #define PM_WBLATE 0                                     // the filter read after the 8-byte compare (measured slower: C3 344.5 -> 353.4 ms)
 #endif
@@ -1404,6 +1407,35 @@ __global__ __launch_bounds__(PM_THREADS) void k_dfl_match(DeflateArgs A) {
                 const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(im >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)im, 0u));
                 const int pn = next + (int)rank;
                 next += nidle;
+#if PM_SELFILL && PM_W8 && !PM_LAZYW4 && !PM_SBREG
+                // every lane reads (a lane that takes no position reads at its own position) and
+                // the taken lanes' new state is selected in place: no divergent region, so the
+                // walk state keeps its registers and the steps without a refill copy nothing
+                const bool take = chain <= 0 && pn < q1;
+                const int spn = take ? pn - ws : sp;
+                const int h = pvl[spn];                         // hash_head
+                const uint32_t w0 = pm_w4(win, (uint32_t)spn), w1 = pm_w4(win, (uint32_t)spn + 4u);
+                const bool last = pn >= tail;                   // a last position (tl only): searched
+                // if in the larger group and lookahead >= MIN_MATCH; window index 0 (position offM)
+                // is NIL there; nice_match at most the lookahead
+                const bool search = h != 0 && spn - h <= MAX_DIST &&   // deflate.ts:1092
+                                    (!last || (pn <= n - MIN_MATCH && pn >= tg.mlo && pn < tg.mhi &&
+                                               (int64_t)(h + ws) > tg.offM));
+                const int nx = pvl[search ? h : spn];
+                p = take ? pn : p;
+                sp = spn;
+                cur = take ? h : cur;
+                best = take ? MIN_MATCH - 1 : best;
+                bpos = take ? 0 : bpos;
+                qbest = take ? -1 : qbest;
+                limit = take ? (pn > MAX_DIST ? pn - MAX_DIST : 0) - ws : limit;   // >= 0
+                s4 = take ? w0 : s4;
+                s4b = take ? w1 : s4b;
+                nice = take ? (last && n - pn < nice0 ? n - pn : nice0) : nice;
+                chain = take ? (search ? max_chain : 0) : chain;
+                pend = take ? !search : pend;                   // no search: record 0
+                nxt = take ? nx : nxt;
+#else
                 if (chain <= 0 && pn < q1) {
                     p = pn;
                     sp = p - ws;
@@ -1435,6 +1467,7 @@ __global__ __launch_bounds__(PM_THREADS) void k_dfl_match(DeflateArgs A) {
                     pend = !search;                             // no search: record 0
                     nxt = pvl[search ? cur : sp];
                 }
+#endif
             }
         }
         // two candidates per walking lane and step: cur (c1) and nxt (c2).  Both pass the
