@@ -428,6 +428,41 @@ def test_deflate_4byte_chain_search(monkeypatch, paradise, level):
     assert [g["data"] for g in old] == exp
 
 
+def _length_ladder(rng, n):
+    """Copies of earlier bytes cut after 3..20 bytes, then a byte that differs from the source's
+    next one: matches that end just before, at and after the 4- and 8-byte marks of
+    k_dfl_match's first compare, some at distances of a few bytes (overlapping the position)."""
+    out = bytearray(rng.getrandbits(8) for _ in range(64))
+    while len(out) < n:
+        ln = rng.choice([3, 4, 5, 7, 8, 9, 11, 12, 13, 16, 17, 20])
+        if rng.random() < 0.7:
+            src = rng.randrange(0, len(out) - ln - 1)
+        else:
+            src = len(out) - rng.choice([1, 2, 3, 7, 8, 9]) - ln
+        out += out[src:src + ln] + bytes([out[src + ln] ^ 0x5A])
+        if rng.random() < 0.3:
+            out += bytes(rng.getrandbits(8) for _ in range(rng.randrange(1, 6)))
+    return bytes(out[:n])
+
+
+@pytest.mark.parametrize("level", [4, 6, 9])
+def test_deflate_match_lengths_around_compare_width(monkeypatch, level):
+    """k_dfl_match compares a candidate's first 8 bytes in one round trip and longer matches 4
+    bytes at a time from there (the match step): lengths ending just before, at and
+    after bytes 4 and 8, bit-exact with the oracle, with the call's own segment size and with
+    16 Ki / 1 Ki segments forced (SDZ_PM_SEG: segment starts among the matches)."""
+    rng = random.Random(808 + level)
+    inputs = [_length_ladder(rng, k) for k in (300, 5000, 65536, 100000)]
+    inputs.append(inputs[2][:40000] * 2)
+    exp = [O.deflate(d, level=level) for d in inputs]
+    for seg in (None, "16384", "1024"):
+        if seg:
+            monkeypatch.setenv("SDZ_PM_SEG", seg)
+        g = sdz.deflate_batch(inputs, level=level)
+        for i, (x, e) in enumerate(zip(g, exp)):
+            assert x["status"] == "OK" and x["data"] == e, (level, seg, i)
+
+
 def test_deflate_record_path_long_inputs(paradise):
     """Inputs past 64 KiB on the record path: window slides every 32 KiB (deflate.ts:708-737)
     -- chain units with 32 KiB of history, matches across segments, the last positions
