@@ -2043,7 +2043,7 @@ void launch_seg_decode(const InflateArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(k_inflate_decode, dim3((a.n + IL_STREAMS - 1) / IL_STREAMS), dim3(IL_THREADS), 0, s, a, 0u);
 }
 
-__global__ void k_inflate_resolve(InflateArgs A, uint32_t round);
+void launch_inflate_resolve(const InflateArgs& a, uint32_t round, dim3 grid, hipStream_t s);
 uint32_t resolve_block_threads();
 uint32_t resolve_streams_per_block();
 void launch_inflate_finalize(const InflateArgs& a, hipStream_t s);
@@ -2169,7 +2169,7 @@ int run_inflate_rounds(const InflateArgs& a, hipStream_t s, uint32_t* host_activ
             DBG_SYNC(s, "k_seg_feed", round, 0);
         }
         if (kernel_ms) (void)hipEventRecord(ev[1], s);
-        hipLaunchKernelGGL(k_inflate_resolve, g2, dim3(resolve_block_threads()), 0, s, a, round);
+        launch_inflate_resolve(a, round, g2, s);
         DBG_SYNC(s, "k_inflate_resolve", round, 0);
         if (kernel_ms) (void)hipEventRecord(ev[2], s);
         if (a.one_round && !a.split_plan) break;         // (times read after finalize)

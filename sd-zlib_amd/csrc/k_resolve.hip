@@ -48,11 +48,13 @@ namespace sdz {
 #define RS_BM 4096                    // finality map bytes (>= RS_SLACK; lap = position >> 12)
 #define RS_SPIN_LIMIT (1u << 22)      // watchdog: polls per wait (~0.4 s)
 
-__device__ __forceinline__ uint32_t ridx(int32_t x) {            // x in (-R, 2R)
-    x += x < 0 ? RS_R : 0;
-    x -= x >= RS_R ? RS_R : 0;
+template <uint32_t RR>
+__device__ __forceinline__ uint32_t ridx_t(int32_t x) {          // x in (-R, 2R)
+    x += x < 0 ? (int32_t)RR : 0;
+    x -= x >= (int32_t)RR ? (int32_t)RR : 0;
     return (uint32_t)x;
 }
+__device__ __forceinline__ uint32_t ridx(int32_t x) { return ridx_t<RS_R>(x); }
 
 // inclusive wave scan with DPP row shifts and row broadcasts (gfx9)
 template <int CTRL, int ROWS>
@@ -67,6 +69,27 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) {
     x = dpp_add<0x142, 0xa>(x);                           // row_bcast:15 -> rows 1, 3
     x = dpp_add<0x143, 0xc>(x);                           // row_bcast:31 -> rows 2, 3
     return x;
+}
+// lane & 7, recomputed where it is used (volatile: not hoisted out of a loop and kept live, which made
+// the register allocator spill the LDS addresses built from it to scratch)
+__device__ __forceinline__ uint32_t lane_lo8() {
+    uint32_t r;
+    asm volatile("v_and_b32 %0, 7, %1" : "=v"(r) : "v"(threadIdx.x));
+    return r;
+}
+__device__ __forceinline__ uint32_t tid_fresh() {
+    uint32_t r;
+    asm volatile("v_mov_b32 %0, %1" : "=v"(r) : "v"(threadIdx.x));
+    return r;
+}
+// inclusive prefix max over lanes 0..7 (row 0): lane 7 holds the max of lanes 0..7
+__device__ __forceinline__ uint32_t dpp_max8(uint32_t x) {
+    uint32_t y = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, false);   // row_shr:1
+    x = x > y ? x : y;
+    y = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, false);            // row_shr:2
+    x = x > y ? x : y;
+    y = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, false);            // row_shr:4
+    return x > y ? x : y;
 }
 __device__ __forceinline__ uint32_t uni(uint32_t x) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)x); }
 __device__ __forceinline__ uint32_t lane_at(uint32_t x, uint32_t l) {
@@ -97,25 +120,27 @@ __device__ __forceinline__ void lds_put(uint32_t* p, uint32_t v) {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
+template <uint32_t RR>
 __device__ __forceinline__ uint32_t ridx64(int64_t p) {         // ring index of a (call-relative) position
-    int64_t x = p % RS_R;
-    return (uint32_t)(x < 0 ? x + RS_R : x);
+    int64_t x = p % (int64_t)RR;
+    return (uint32_t)(x < 0 ? x + RR : x);
 }
 
 // adler32.ts:34-105 over the r ring bytes from position p0, seeded with the chunk-start
 // state (NMAX quirk: sum2 += BASE instead of a reduction after each 5552-byte block)
+template <uint32_t RR>
 __device__ int32_t adler_quirk_ring(const uint8_t* ring, int64_t p0, uint32_t r, uint32_t s1, uint32_t s2in) {
     uint64_t a = s1, s2 = s2in;
     int64_t off = p0;
     uint32_t len = r;
     while (len >= 5552) {
         len -= 5552;
-        for (int i = 0; i < 5552; ++i) { a += ring[ridx64(off++)]; s2 += a; }
+        for (int i = 0; i < 5552; ++i) { a += ring[ridx64<RR>(off++)]; s2 += a; }
         a %= 65521u;
         s2 += 65521u;
     }
     if (len) {
-        while (len--) { a += ring[ridx64(off++)]; s2 += a; }
+        while (len--) { a += ring[ridx64<RR>(off++)]; s2 += a; }
         a %= 65521u;
         s2 %= 65521u;
     }
@@ -135,7 +160,7 @@ __device__ int32_t adler_quirk_ring(const uint8_t* ring, int64_t p0, uint32_t r,
 // exact without divergent branches.  Tokens that cross the ring's (or the map's) end
 // go byte-serial.  Ring bytes are stored before their map bytes (LDS operations of a
 // wave complete in order), so a reader that sees the map byte sees the data.
-#define RS_DUMMY (RS_R + 4u * (threadIdx.x & 63u))
+#define RS_DUMMY (RR + 4u * (threadIdx.x & 63u))
 #define RS_CBAR() asm volatile("" ::: "memory")
 __device__ __forceinline__ uint32_t lap_next(uint32_t lb) { return (lb & 127u) + 1u; }
 // the 4 bytes of a period-`dist` (1..3) pattern P starting at phase ph: byte j = P[(ph + j) mod dist]
@@ -149,15 +174,16 @@ __device__ __forceinline__ uint32_t rep4(uint32_t P, uint32_t dist, uint32_t ph)
 __device__ __forceinline__ uint32_t src_word(const uint32_t* ring32, uint32_t x) {
     return __builtin_amdgcn_alignbyte(ring32[(x >> 2) + 1], ring32[x >> 2], x & 3u);
 }
-__device__ __noinline__ void emit_tokens(uint8_t* ring, uint8_t* fmap, bool act, uint32_t t, uint32_t d,
-                                            uint32_t s, uint32_t len, uint32_t dist, uint32_t mp, uint32_t lb) {
+template <uint32_t RR, bool MAP>
+__device__ __forceinline__ void emit_tokens_body(uint8_t* ring, uint8_t* fmap, bool act, uint32_t t, uint32_t d,
+                                                 uint32_t s, uint32_t len, uint32_t dist, uint32_t mp, uint32_t lb) {
     uint32_t* ring32 = (uint32_t*)ring;
     uint32_t* fmap32 = (uint32_t*)fmap;
     uint8_t* dum8 = ring + RS_DUMMY;
     uint16_t* dum16 = (uint16_t*)(ring + RS_DUMMY);
     uint32_t* dum32 = ring32 + RS_DUMMY / 4;
     const bool lit = (t >> 31) == 0;
-    const bool slow = act && (d + len > RS_R || (!lit && (s + len > RS_R || s < 4u)) || mp + len > RS_BM);
+    const bool slow = act && (d + len > RR || (!lit && (s + len > RR || s < 4u)) || (MAP && mp + len > RS_BM));
     const bool fast = act && !slow;
     const bool per = fast && !lit && dist < 4;
     const bool cp = fast && !lit && dist >= 4;
@@ -182,13 +208,17 @@ __device__ __noinline__ void emit_tokens(uint8_t* ring, uint8_t* fmap, bool act,
         *(w8 ? ring + d : dum8) = (uint8_t)Vh;
         *(w16 ? (uint16_t*)(ring + p16) : dum16) = (uint16_t)v16;
         RS_CBAR();
-        *(w8 ? fmap + mp : dum8) = (uint8_t)lb;
-        *(w16 ? (uint16_t*)(fmap + (mp + (p16 - d))) : dum16) = (uint16_t)lw;
+        if constexpr (MAP) {
+            *(w8 ? fmap + mp : dum8) = (uint8_t)lb;
+            *(w16 ? (uint16_t*)(fmap + (mp + (p16 - d))) : dum16) = (uint16_t)lw;
+        }
         const bool w8b = kd == 1 && h == 2;
         if (__ballot(w8b)) {
             *(w8b ? ring + d + 1 : dum8) = (uint8_t)(Vh >> 8);
             RS_CBAR();
-            *(w8b ? fmap + mp + 1 : dum8) = (uint8_t)lb;
+            if constexpr (MAP) {
+                *(w8b ? fmap + mp + 1 : dum8) = (uint8_t)lb;
+            }
         }
     }
     // body: whole aligned dwords
@@ -208,15 +238,19 @@ __device__ __noinline__ void emit_tokens(uint8_t* ring, uint8_t* fmap, bool act,
             *(q + j < na ? ring32 + db + q + j : dum32) = v;
         }
         RS_CBAR();
+        if constexpr (MAP) {
 #pragma unroll
-        for (int j = 0; j < 2; ++j) *(q + j < na ? fmap32 + mb + q + j : dum32) = lw;
+            for (int j = 0; j < 2; ++j) *(q + j < na ? fmap32 + mb + q + j : dum32) = lw;
+        }
     }
     for (uint32_t q = 0; __ballot(q < nb); ++q) {
         const bool a = q < nb;
         const uint32_t x0 = ring32[a ? sa + q : 0u], x1 = ring32[a ? sa + q + 1 : 0u];
         *(a ? ring32 + db + q : dum32) = __builtin_amdgcn_alignbyte(x1, x0, k);
         RS_CBAR();
-        *(a ? fmap32 + mb + q : dum32) = lw;
+        if constexpr (MAP) {
+            *(a ? fmap32 + mb + q : dum32) = lw;
+        }
     }
     // tail: bytes [e, e + r) -- b16 at e, b8 at e + r - 1 for odd r
     if (__ballot(r != 0)) {
@@ -228,19 +262,29 @@ __device__ __noinline__ void emit_tokens(uint8_t* ring, uint8_t* fmap, bool act,
         *(w16 ? (uint16_t*)(ring + e) : dum16) = (uint16_t)Vt;
         *(w8 ? ring + e + r - 1 : dum8) = (uint8_t)(Vt >> (8 * (r - 1)));
         RS_CBAR();
-        *(w16 ? (uint16_t*)(fmap + (mp + (e - d))) : dum16) = (uint16_t)lw;
-        *(w8 ? fmap + (mp + (e - d) + r - 1) : dum8) = (uint8_t)lb;
+        if constexpr (MAP) {
+            *(w16 ? (uint16_t*)(fmap + (mp + (e - d))) : dum16) = (uint16_t)lw;
+            *(w8 ? fmap + (mp + (e - d) + r - 1) : dum8) = (uint8_t)lb;
+        }
     }
     if (__ballot(slow)) {                                 // across the ring's / map's end: byte-serial
         for (uint32_t i = 0; __ballot(slow && i < len); ++i) {
             const bool a = slow && i < len;
-            const uint32_t b = lit ? (t >> (8 * (i & 3u))) & 255u : ring[a && !lit ? ridx((int32_t)(s + i)) : 0u];
-            ring[a ? ridx((int32_t)(d + i)) : RS_DUMMY] = (uint8_t)b;
+            const uint32_t b = lit ? (t >> (8 * (i & 3u))) & 255u : ring[a && !lit ? ridx_t<RR>((int32_t)(s + i)) : 0u];
+            ring[a ? ridx_t<RR>((int32_t)(d + i)) : RS_DUMMY] = (uint8_t)b;
             RS_CBAR();
             const uint32_t m = mp + i;
-            *(a ? fmap + (m & (RS_BM - 1)) : ring + RS_DUMMY) = (uint8_t)(m >= RS_BM ? lap_next(lb) : lb);
+            if constexpr (MAP) {
+                *(a ? fmap + (m & (RS_BM - 1)) : ring + RS_DUMMY) = (uint8_t)(m >= RS_BM ? lap_next(lb) : lb);
+            }
         }
     }
+}
+
+template <uint32_t RR, bool MAP>
+__device__ __noinline__ void emit_tokens(uint8_t* ring, uint8_t* fmap, bool act, uint32_t t, uint32_t d,
+                                            uint32_t s, uint32_t len, uint32_t dist, uint32_t mp, uint32_t lb) {
+    emit_tokens_body<RR, MAP>(ring, fmap, act, t, d, s, len, dist, mp, lb);
 }
 
 template <int J, int N, typename F>
@@ -271,16 +315,24 @@ __device__ __forceinline__ void lds_mskor_at(uint32_t* base32, uint32_t i, uint3
 #ifndef RS_MW
 #define RS_MW 2
 #endif
+// GEN: 0 -- no lane needs the general path (the caller routed them elsewhere); 1 -- through the
+// out-of-line emit_tokens; 2 -- emit_tokens inlined (one call site per kernel: no callee-saved
+// registers forced around a call)
+template <uint32_t RR, bool MAP, int MW, int GEN = 1>
 __device__ __forceinline__ void emit_msk(uint8_t* ring, uint8_t* fmap, bool act, uint32_t t, uint32_t d,
                                          uint32_t s, uint32_t len, uint32_t dist, uint32_t mp, uint32_t lb) {
     uint32_t* ring32 = (uint32_t*)ring;
     uint32_t* fmap32 = (uint32_t*)fmap;
-    const uint32_t dumi = RS_R / 4 + (threadIdx.x & 31u);   // reads run RS_MW dwords on
+    const uint32_t dumi = RR / 4 + (threadIdx.x & 31u);     // reads run MW dwords on
     const bool lit = (t >> 31) == 0;
     // (a token across the map's end stays here: its map dwords wrap, with the next lap's byte)
-    const bool slow = act && (d + len > RS_R || (!lit && (s + len > RS_R || s < 4u)));
+    const bool slow = act && (d + len > RR || (!lit && (s + len > RR || s < 4u)));
     const bool gen = act && (slow || (!lit && dist < len));  // periods and self-overlapping copies too
-    if (__ballot(gen)) emit_tokens(ring, fmap, gen, t, d, s, len, dist, mp, lb);
+    if constexpr (GEN == 1) {
+        if (__ballot(gen)) emit_tokens<RR, MAP>(ring, fmap, gen, t, d, s, len, dist, mp, lb);
+    } else if constexpr (GEN == 2) {
+        if (__ballot(gen)) emit_tokens_body<RR, MAP>(ring, fmap, gen, t, d, s, len, dist, mp, lb);
+    }
     const bool one = act && !gen;
     const uint32_t kd = d & 3u, D0 = d >> 2, M0 = mp >> 2;
     const uint32_t sx = s - kd, k = sx & 3u;
@@ -289,36 +341,40 @@ __device__ __forceinline__ void emit_msk(uint8_t* ring, uint8_t* fmap, bool act,
     const uint32_t lw = lb * 0x01010101u;
     // a literal: x0 = t (kd = 0), or x0 = 0, x1 = t with shift 4 - kd
     const uint32_t kk = lit ? (4u - kd) & 3u : k;
-    uint32_t x[RS_MW + 1];
+    uint32_t x[MW + 1];
 #pragma unroll
-    for (int j = 0; j <= RS_MW; ++j) {
+    for (int j = 0; j <= MW; ++j) {
         const uint32_t r = ring32[xa + (uint32_t)j];
         x[j] = !lit ? r : j == 0 ? (kd ? 0u : t) : j == 1 ? (kd ? t : 0u) : 0u;
     }
     const uint32_t lom = 0xffffffffu << (8 * kd);
-    static_for<0, RS_MW>([&](auto jc) {                   // each dword's data, then its finality
+    static_for<0, MW>([&](auto jc) {                   // each dword's data, then its finality
         constexpr int j = decltype(jc)::value;
         const int32_t hb = (int32_t)e - 4 * j;            // bytes of the token in dword j: up to hb
         const uint32_t h = hb >= 4 ? 0xffffffffu : hb <= 0 ? 0u : (1u << (8 * hb)) - 1u;
         const uint32_t mk = j == 0 ? h & lom : h;
         lds_mskor_at<j>(ring32, D0, mk, __builtin_amdgcn_alignbyte(x[j + 1], x[j], kk));
-        const uint32_t mi = M0 + (uint32_t)j;                // map dword, wrapped (dword-aligned end)
-        const bool wr = mi >= RS_BM / 4u;
-        lds_mskor_at<0>(fmap32, wr ? mi - RS_BM / 4u : mi, mk, wr ? lap_next(lb) * 0x01010101u : lw);
+        if constexpr (MAP) {
+            const uint32_t mi = M0 + (uint32_t)j;            // map dword, wrapped (dword-aligned end)
+            const bool wr = mi >= RS_BM / 4u;
+            lds_mskor_at<0>(fmap32, wr ? mi - RS_BM / 4u : mi, mk, wr ? lap_next(lb) * 0x01010101u : lw);
+        }
     });
     // later steps of copies longer than 4 RS_MW - 3 bytes
-    for (uint32_t w0 = RS_MW; __ballot(e > 4u * w0); w0 += RS_MW) {
+    for (uint32_t w0 = MW; __ballot(e > 4u * w0); w0 += MW) {
         const bool on = e > 4u * w0;
 #pragma unroll
-        for (int j = 0; j <= RS_MW; ++j) x[j] = ring32[on ? xa + w0 + (uint32_t)j : dumi + (uint32_t)j];
+        for (int j = 0; j <= MW; ++j) x[j] = ring32[on ? xa + w0 + (uint32_t)j : dumi + (uint32_t)j];
 #pragma unroll
-        for (int j = 0; j < RS_MW; ++j) {
+        for (int j = 0; j < MW; ++j) {
             const int32_t hb = (int32_t)e - 4 * (int32_t)(w0 + j);
             const uint32_t mw = !on || hb <= 0 ? 0u : hb >= 4 ? 0xffffffffu : (1u << (8 * hb)) - 1u;
             lds_mskor_at<0>(ring32, D0 + w0 + (uint32_t)j, mw, __builtin_amdgcn_alignbyte(x[j + 1], x[j], k));
-            const uint32_t mi = M0 + w0 + (uint32_t)j;
-            const bool wr = mi >= RS_BM / 4u;
-            lds_mskor_at<0>(fmap32, wr ? mi - RS_BM / 4u : mi, mw, wr ? lap_next(lb) * 0x01010101u : lw);
+            if constexpr (MAP) {
+                const uint32_t mi = M0 + w0 + (uint32_t)j;
+                const bool wr = mi >= RS_BM / 4u;
+                lds_mskor_at<0>(fmap32, wr ? mi - RS_BM / 4u : mi, mw, wr ? lap_next(lb) * 0x01010101u : lw);
+            }
         }
     }
 }
@@ -373,6 +429,205 @@ __device__ __forceinline__ void publish_wf(uint32_t* wf, uint32_t v1) {
     rs_wake();
 }
 
+// The ring's window at the start of a round (all threads; a barrier must follow): output bytes
+// [pos0 - 32 KiB, pos0); before position 0 of this call, the window saved by the previous call
+// (incremental mode), else the dictionary / zeros.  Position p sits at ring index p mod RR.
+template <uint32_t RR, uint32_t NT>
+__device__ __forceinline__ void ring_window_init(uint8_t* ring, const InflateArgs& A, uint32_t sid, uint32_t round,
+                                                 uint64_t pos0, const uint8_t* out, int64_t dl, const uint8_t* dict) {
+    // the window: output bytes [pos0 - 32 KiB, pos0); before position 0 of this call, the
+    // window saved by the previous call (incremental mode), else the dictionary / zeros
+    const uint32_t tid = threadIdx.x;
+    const uint32_t rp0 = (uint32_t)(pos0 % RR);
+    RSave* R = (RSave*)A.rsave + sid;
+    const uint8_t* hist = A.streaming && R->hist ? A.window + (uint64_t)sid * IS_WIN : nullptr;
+    static_assert((RR - RS_WIN) % 16 == 0 && IS_WIN == RS_WIN, "ring window start must be 16-aligned");
+    if (pos0 == 0 && hist) {
+        // ring bytes [RR - RS_WIN, RR) hold positions [-32 KiB, 0)
+        for (uint32_t k = tid; k < RS_WIN / 16; k += NT)
+            ((uint4*)(ring + (RR - RS_WIN)))[k] = ((const uint4*)hist)[k];
+    } else if (pos0 == 0 && dl == 0) {
+        // a stream's first round without a dictionary: zeros
+        for (uint32_t k = tid; k < RS_WIN / 16; k += NT)
+            ((uint4*)(ring + (RR - RS_WIN)))[k] = make_uint4(0, 0, 0, 0);
+    } else if (round && pos0 >= RS_WIN) {
+        // a later round: the 32 KiB before pos0 from the output, 4 loads in flight per thread
+        for (uint32_t k = 4 * tid; k < RS_WIN; k += 4 * NT) {
+            const uint8_t* q = out + pos0 - RS_WIN + k;
+            const uint32_t b0 = q[0], b1 = q[1], b2 = q[2], b3 = q[3];
+            const int32_t r = (int32_t)rp0 - RS_WIN + (int32_t)k;
+            ring[ridx_t<RR>(r)] = (uint8_t)b0; ring[ridx_t<RR>(r + 1)] = (uint8_t)b1;
+            ring[ridx_t<RR>(r + 2)] = (uint8_t)b2; ring[ridx_t<RR>(r + 3)] = (uint8_t)b3;
+        }
+    } else {
+        for (uint32_t k = tid; k < RS_WIN; k += NT) {
+            const int64_t p = (int64_t)pos0 - RS_WIN + k;
+            uint32_t b = 0;
+            if (p >= 0) b = round ? out[p] : 0u;
+            else if (hist) b = hist[RS_WIN + p];
+            else if (p >= -dl) b = dict[dl + p];
+            ring[ridx_t<RR>((int32_t)rp0 - RS_WIN + (int32_t)k)] = (uint8_t)b;
+        }
+    }
+}
+
+// The end of a round, shared by the resolve kernels (all threads of the workgroup): the adler32
+// partials combined, RSave updated, and on the stream's last round of the call the record and the
+// Inflater verdicts (sd-inflate.ts:134-179), plus the incremental mode's window and carry.
+// pos: output bytes of this call resolved so far (or, with chainp, pos0 + the low word of *chainp,
+// read after the barrier); failp: the watchdog word (0 = none).
+template <uint32_t RR, int NW>
+__device__ __forceinline__ void resolve_finish(const InflateArgs& A, uint32_t round, uint32_t sid, uint32_t flag, bool fin0,
+                                               bool gz, uint64_t pos0, uint64_t pos, const uint64_t* chainp,
+                                               const uint32_t* failp, const uint8_t* ring, uint32_t accS, uint64_t accT,
+                                               uint64_t* red) {
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, w = tid >> 6;
+    RSave* R = (RSave*)A.rsave + sid;
+    DSave* S = (DSave*)A.dsave + sid;
+    // combine the adler partials of this round
+    __syncthreads();
+    const uint32_t fail = *(const volatile uint32_t*)failp;
+    if (chainp) pos = pos0 + (uint64_t)(uint32_t)*(const volatile uint64_t*)chainp;   // end of the last group
+    const bool failed = fail != 0 || (round && R->ck != 0);   // sticky across rounds
+    uint32_t S_all = 0, T_all = 0;
+    if (!gz) {
+        uint64_t a = accS, b = accT;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) { a += __shfl_xor(a, o); b += __shfl_xor(b, o); }
+        if (lane == 0) { red[2 * w] = a; red[2 * w + 1] = b; }
+        __syncthreads();
+        uint64_t tS = round ? R->s1 : 0, tT = round ? R->s2 : 0;
+#pragma unroll
+        for (int q = 0; q < NW; ++q) { tS += mod65521(red[2 * q]); tT += mod65521(red[2 * q + 1]); }
+        S_all = mod65521(tS);
+        T_all = mod65521(tT);
+    }
+    __syncthreads();                                     // R->s1 / s2 were read above
+    if (tid == 0) { R->pos = pos; R->s1 = S_all; R->s2 = T_all; R->ck = failed ? 1 : 0; }
+    const bool fin = flag == 1 || flag == 3 || fin0;    // the stream's last round of this call
+    if (!fin) return;
+    const uint64_t bitpos = S->bitpos;
+    const uint64_t ilen = A.in_len[sid];
+    uint32_t carry_n = 0;
+    uint64_t keep_end = 0;
+    bool carry_over = false;
+    if (A.streaming && flag == 3) {
+        // stalled: keep the window (the 32 KiB before the next call's output) and the input
+        // from the unit in progress on (the bits the reference holds in its bit buffer)
+        uint8_t* win = A.window + (uint64_t)sid * IS_WIN;
+        const uint32_t wb = (uint32_t)((pos % RR + RR - RS_WIN) % RR);   // ring index of pos - 32 KiB
+        for (uint32_t k = tid; k < RS_WIN; k += 64 * NW) win[k] = ring[(wb + k) % RR];
+        // out of input: all of it from the unit's first byte; out of room: only the carried
+        // bytes -- the caller passes its own unconsumed bytes again (from in_used on)
+        const uint64_t cb = bitpos >> 3;
+        const uint64_t nc = R->carry_len;
+        keep_end = S->stall == 2 ? (cb > nc ? cb : nc) : ilen;
+        carry_n = (uint32_t)(keep_end - cb);
+        carry_over = keep_end - cb > SDZ_INFLATE_CARRY;
+        if (!carry_over) {
+            const uint8_t* src = A.in + A.in_off[sid] + cb;
+            uint8_t* dst = A.carry + (uint64_t)sid * SDZ_INFLATE_CARRY;
+            for (uint32_t k = tid; k < carry_n; k += 64 * NW) dst[k] = src[k];
+        }
+    }
+    // Inflater.checksum (sd-inflate.ts:136-146): adler32 over 16 KiB output chunks counted
+    // from the start of each append()'s output (abase), with the NMAX quirk (adler32.ts:67):
+    // a final chunk of 5552 or 11104 bytes leaves sum2 unreduced.  Every other chunk ends
+    // reduced, so the value is the plain adler32 state except after such a chunk, which is
+    // replayed from the state at its start -- recovered from the plain state at its end and
+    // its bytes (the last <= 11104 output bytes are in the ring).
+    const bool cont_next = A.streaming && flag == 3 && S->stall == 2;   // this append continues
+    const uint64_t T0 = A.streaming ? R->total : 0, T1 = T0 + pos;
+    const uint64_t abase = A.streaming ? R->abase : 0;
+    const uint32_t rr = (uint32_t)((T1 - abase) & 16383u);
+    const bool quirk = !gz && !failed && !cont_next && (rr == 5552u || rr == 11104u);
+    uint64_t qa = 0, qb = 0;                              // sum b_j, sum (rr - j) b_j of that chunk
+    if (quirk) {
+        for (uint32_t k = tid; k < rr; k += 64 * NW) {
+            const uint32_t v = ring[ridx64<RR>((int64_t)pos - rr + k)];
+            qa += v;
+            qb += (uint64_t)(rr - k) * v;
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) { qa += __shfl_xor(qa, o); qb += __shfl_xor(qb, o); }
+        if (lane == 0) { red[2 * w] = qa; red[2 * w + 1] = qb; }
+        __syncthreads();
+        qa = 0; qb = 0;
+#pragma unroll
+        for (int q = 0; q < NW; ++q) { qa += red[2 * q]; qb += red[2 * q + 1]; }
+    }
+    __syncthreads();                                      // window / carry copies done
+    if (tid != 0) return;
+    if (carry_over) { S->mode = LM_DONE; S->status = SDZ_CARRY_OVERFLOW; S->zmsg = 0; }
+    // final: record + verdicts (sd-inflate.ts:134-179); gzip's crc32 comes from k_inflate_finalize
+    sdz_inflate_record Rc;
+    Rc.status = failed ? SDZ_INTERNAL : S->status;
+    Rc.zmsg = failed ? (int32_t)fail : S->zmsg;      // watchdog: site | position << 4
+    Rc.out_len = pos;
+    uint64_t used = (bitpos + 7) >> 3;
+    if (used > ilen) used = ilen;
+    // incremental: the stream offset up to which input is consumed or held by the device
+    Rc.in_used = A.streaming ? R->in_base + (flag == 3 && !carry_over ? keep_end : used) : used;
+    Rc.stored_checksum = S->stored_ck;
+    const uint64_t total = T1;
+    bool have = total > 0;                                // Inflater.checksum stays undefined otherwise
+    int32_t running = 0;
+    uint32_t a1 = A.streaming ? R->a1 : 1u, a2 = A.streaming ? R->a2 : 0u;   // state at T0 (exact)
+    if (!gz) {
+        if (pos) {                                        // no output keeps the exact (quirky) state
+            const uint32_t nm = mod65521(pos);
+            const uint32_t b1 = (uint32_t)(((uint64_t)a1 + S_all) % 65521u);
+            const uint32_t b2 = (uint32_t)(((uint64_t)a2 + (uint64_t)nm * a1 + (uint64_t)nm * S_all +
+                                            65521ull * 65521ull - T_all) % 65521u);
+            a1 = b1;
+            a2 = b2;
+        }
+        if (quirk) {
+            uint32_t s1s, s2s;                            // state at the final chunk's start
+            if (T1 - rr == abase) {
+                s1s = A.streaming ? R->a1s : 1u;
+                s2s = A.streaming ? R->a2s : 0u;
+            } else {
+                s1s = (uint32_t)((a1 + 65521u - mod65521(qa)) % 65521u);
+                s2s = (uint32_t)(((uint64_t)a2 + 65521ull * 65521ull - (uint64_t)rr * s1s - mod65521(qb)) % 65521u);
+            }
+            running = adler_quirk_ring<RR>(ring, (int64_t)pos - rr, rr, s1s, s2s);
+        } else {
+            running = (int32_t)(a1 | (a2 << 16));
+        }
+    }
+    Rc.running_checksum = have ? running : 0;
+    Rc.stored_size = S->stored_size;
+    Rc.mtime = S->mtime;
+    Rc.name_off = S->name_off;
+    Rc.name_len = S->name_len;
+    Rc.container = (uint8_t)S->container;
+    bool complete = !failed && S->mode == LM_DONE && (S->status == SDZ_OK || S->status == SDZ_TRAILING);
+    Rc.complete = complete ? 1 : 0;
+    uint8_t cv = S->stored_ck == 0 ? SDZ_UNCHECKED : ((have && S->stored_ck == running) ? SDZ_MATCH : SDZ_MISMATCH);
+    uint8_t sv = S->stored_size == 0 ? SDZ_UNCHECKED
+               : ((int64_t)S->stored_size == (int64_t)total ? SDZ_MATCH : SDZ_MISMATCH);
+    Rc.checksum_verdict = cv;
+    Rc.size_verdict = sv;
+    Rc.success = (complete && cv != SDZ_MISMATCH && sv != SDZ_MISMATCH) ? 1 : 0;
+    Rc.out_full = S->mode != LM_DONE && S->stall == 2 ? 1 : 0;
+    if (!complete && Rc.status == SDZ_OK) Rc.status = SDZ_TRUNCATED;   // incremental: needs more input
+    for (int k = 0; k < 10; ++k) Rc.reserved[k] = 0;
+    A.rec[sid] = Rc;
+    if (A.streaming) {                                    // state for the next call
+        R->total = total;
+        if (!gz && have) { R->a1 = (uint32_t)running & 0xffffu; R->a2 = (uint32_t)running >> 16; }
+        if (flag == 3 && !carry_over) {
+            R->in_base += bitpos >> 3;
+            R->carry_len = carry_n;
+            R->hist = 1;
+            S->bitpos = bitpos & 7;
+        } else {
+            R->carry_len = 0;
+        }
+    }
+}
+
 __global__ __launch_bounds__(RS_THREADS) __attribute__((amdgpu_waves_per_eu(RS_WPE, RS_WPE))) void k_inflate_resolve(InflateArgs A, uint32_t round) {
     __shared__ __attribute__((aligned(16))) uint8_t ring[RS_R + 256];   // + per-lane dummies
     __shared__ uint64_t chain;                           // (tag of the last started group) << 32 | its end
@@ -397,39 +652,9 @@ __global__ __launch_bounds__(RS_THREADS) __attribute__((amdgpu_waves_per_eu(RS_W
     const int64_t dl = S->dict_used && A.dict ? (A.dict_len > 32767 ? 32767 : A.dict_len) : 0;
     const uint8_t* dict = dl ? A.dict + (A.dict_len - dl) : nullptr;
 
-    // the window: output bytes [pos0 - 32 KiB, pos0); before position 0 of this call, the
-    // window saved by the previous call (incremental mode), else the dictionary / zeros
     const uint32_t rp0 = (uint32_t)(pos0 % RS_R);
     const uint32_t pm0 = (uint32_t)(pos0 % 65521u);
-    const uint8_t* hist = A.streaming && R->hist ? A.window + (uint64_t)sid * IS_WIN : nullptr;
-    static_assert((RS_R - RS_WIN) % 16 == 0 && IS_WIN == RS_WIN, "ring window start must be 16-aligned");
-    if (pos0 == 0 && hist) {
-        // ring bytes [RS_R - RS_WIN, RS_R) hold positions [-32 KiB, 0)
-        for (uint32_t k = tid; k < RS_WIN / 16; k += RS_THREADS)
-            ((uint4*)(ring + (RS_R - RS_WIN)))[k] = ((const uint4*)hist)[k];
-    } else if (pos0 == 0 && dl == 0) {
-        // a stream's first round without a dictionary: zeros
-        for (uint32_t k = tid; k < RS_WIN / 16; k += RS_THREADS)
-            ((uint4*)(ring + (RS_R - RS_WIN)))[k] = make_uint4(0, 0, 0, 0);
-    } else if (round && pos0 >= RS_WIN) {
-        // a later round: the 32 KiB before pos0 from the output, 4 loads in flight per thread
-        for (uint32_t k = 4 * tid; k < RS_WIN; k += 4 * RS_THREADS) {
-            const uint8_t* q = out + pos0 - RS_WIN + k;
-            const uint32_t b0 = q[0], b1 = q[1], b2 = q[2], b3 = q[3];
-            const int32_t r = (int32_t)rp0 - RS_WIN + (int32_t)k;
-            ring[ridx(r)] = (uint8_t)b0; ring[ridx(r + 1)] = (uint8_t)b1;
-            ring[ridx(r + 2)] = (uint8_t)b2; ring[ridx(r + 3)] = (uint8_t)b3;
-        }
-    } else {
-        for (uint32_t k = tid; k < RS_WIN; k += RS_THREADS) {
-            const int64_t p = (int64_t)pos0 - RS_WIN + k;
-            uint32_t b = 0;
-            if (p >= 0) b = round ? out[p] : 0u;
-            else if (hist) b = hist[RS_WIN + p];
-            else if (p >= -dl) b = dict[dl + p];
-            ring[ridx((int32_t)rp0 - RS_WIN + (int32_t)k)] = (uint8_t)b;
-        }
-    }
+    ring_window_init<RS_R, RS_THREADS>(ring, A, sid, round, pos0, out, dl, dict);
     if (tid == 0) { chain = 0xffffffff00000000ull; wf = 0; wwb = 0; fail = 0; edone = 0; }
     for (uint32_t k = tid; k < RS_BM / 4; k += RS_THREADS) ((uint32_t*)fmap)[k] = 0;
     __syncthreads();
@@ -518,7 +743,7 @@ __global__ __launch_bounds__(RS_THREADS) __attribute__((amdgpu_waves_per_eu(RS_W
             const uint64_t rm = __ballot(rdy);
             if (rm) {
                 RS_CBAR();
-                emit_msk(ring, fmap, rdy, t, d, s, len, dist, mp, lb);
+                emit_msk<RS_R, true, RS_MW>(ring, fmap, rdy, t, d, s, len, dist, mp, lb);
 #ifdef RS_XSALU
                 {   // experiment: extra SALU per emit round
                     uint32_t z = uni(len);
@@ -634,147 +859,430 @@ __global__ __launch_bounds__(RS_THREADS) __attribute__((amdgpu_waves_per_eu(RS_W
     }
     if (timed) for (int k = 0; k < 8; ++k) atomicAdd(&A.dbg[k], tacc[k]);
 
-    // combine the adler partials of this round
-    __syncthreads();
-    const bool failed = fail != 0 || (round && R->ck != 0);   // sticky across rounds
-    const uint64_t pos = pos0 + (uint64_t)(uint32_t)chain;   // end of the last group (all published)
-    uint32_t S_all = 0, T_all = 0;
-    if (!gz) {
-        uint64_t a = accS, b = accT;
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) { a += __shfl_xor(a, o); b += __shfl_xor(b, o); }
-        if (lane == 0) { red[w][0] = a; red[w][1] = b; }
-        __syncthreads();
-        uint64_t tS = round ? R->s1 : 0, tT = round ? R->s2 : 0;
-#pragma unroll
-        for (int q = 0; q < RS_WAVES; ++q) { tS += mod65521(red[q][0]); tT += mod65521(red[q][1]); }
-        S_all = mod65521(tS);
-        T_all = mod65521(tT);
-    }
-    __syncthreads();                                     // R->s1 / s2 were read above
-    if (tid == 0) { R->pos = pos; R->s1 = S_all; R->s2 = T_all; R->ck = failed ? 1 : 0; }
-    const bool fin = flag == 1 || flag == 3 || fin0;    // the stream's last round of this call
-    if (!fin) return;
-    const uint64_t bitpos = S->bitpos;
-    const uint64_t ilen = A.in_len[sid];
-    uint32_t carry_n = 0;
-    uint64_t keep_end = 0;
-    bool carry_over = false;
-    if (A.streaming && flag == 3) {
-        // stalled: keep the window (the 32 KiB before the next call's output) and the input
-        // from the unit in progress on (the bits the reference holds in its bit buffer)
-        uint8_t* win = A.window + (uint64_t)sid * IS_WIN;
-        const uint32_t wb = (uint32_t)((pos % RS_R + RS_R - RS_WIN) % RS_R);   // ring index of pos - 32 KiB
-        for (uint32_t k = tid; k < RS_WIN; k += RS_THREADS) win[k] = ring[(wb + k) % RS_R];
-        // out of input: all of it from the unit's first byte; out of room: only the carried
-        // bytes -- the caller passes its own unconsumed bytes again (from in_used on)
-        const uint64_t cb = bitpos >> 3;
-        const uint64_t nc = R->carry_len;
-        keep_end = S->stall == 2 ? (cb > nc ? cb : nc) : ilen;
-        carry_n = (uint32_t)(keep_end - cb);
-        carry_over = keep_end - cb > SDZ_INFLATE_CARRY;
-        if (!carry_over) {
-            const uint8_t* src = A.in + A.in_off[sid] + cb;
-            uint8_t* dst = A.carry + (uint64_t)sid * SDZ_INFLATE_CARRY;
-            for (uint32_t k = tid; k < carry_n; k += RS_THREADS) dst[k] = src[k];
+    resolve_finish<RS_R, RS_WAVES>(A, round, sid, flag, fin0, gz, pos0, 0, &chain, &fail, ring, accS, accT, &red[0][0]);
+}
+
+// ------------------------------------------------------------------ block-synchronous resolve
+//
+// k_inflate_resolve_b: the same job as k_inflate_resolve without the group pipeline.  The
+// workgroup takes the round's tokens in BATCHES of RB_THREADS (one per thread):
+//   1. a block scan of the token lengths gives every token its output offset; a batch is cut
+//      where its bytes would pass RB_CAP (the ring's room beyond the 32 KiB window);
+//   2. a copy whose source bytes end before the batch starts reads only final bytes (earlier
+//      batches): it and every literal are written at once (masked dword writes, emit_msk);
+//      the other copies -- DEPENDENTS, whose sources lie in this batch -- mark their
+//      destination bytes in a pending bitmap first;
+//   3. after a barrier, each wave writes its dependents as their source bytes' pending bits
+//      clear, clearing their own after the bytes (one wave's LDS operations complete in order,
+//      so a wave that sees a bit clear reads the bytes);
+//   4. during the next batch, the workgroup copies the batch's complete dwords to HBM and
+//      folds them into adler32.
+// Against the pipeline of groups (k_inflate_resolve) this drops the finality map (a masked map
+// write per data write, a map read per source), the per-group frontier chain and the rounds of
+// retries that emitted a group to its longest token: a literal or a copy from before the batch
+// is written once, and only the dependents (on text ~1 in 6 copies) wait.
+#define RB_WAVES 8
+#define RB_THREADS (64 * RB_WAVES)
+#define RB_TW (RB_WAVES - 1)          // token waves; the last wave writes the dependents
+#define RB_BATCH (64 * RB_TW)         // tokens per batch at most
+#define RB_CAP 2432                   // output bytes of one batch at most
+#define RB_R (RS_WIN + 2 * RB_CAP + 16)   // ring: the 32 KiB window + two batches in flight
+#define RB_BMW (RB_CAP / 32)          // pending bitmap words per batch
+#define RB_DLW 22                     // dependents list entries per token wave and batch
+#ifndef RB_MW
+#define RB_MW 3                       // destination dwords per masked-write step
+#endif
+#define RB_SPIN_LIMIT (1u << 22)
+#ifndef RB_ABL
+#define RB_ABL 0                      // development: a phase left out, for its cost (output wrong)
+#endif
+static_assert(2 * RB_CAP + 8 <= RB_R - RS_WIN, "two batches must not overwrite the window they read");
+static_assert(RB_CAP % 32 == 0 && RB_R % 16 == 0, "");
+
+// bits [lo, lo + n) of the pending bitmap set (or cleared), for the lanes with act (n >= 1)
+__device__ __forceinline__ void rb_bits(uint32_t* bm, bool act, uint32_t lo, uint32_t n, bool set) {
+    const uint32_t hi = lo + n - 1u;                      // inclusive
+    const uint32_t k0 = lo >> 5, nw = act ? (hi >> 5) - k0 + 1u : 0u;
+    for (uint32_t i = 0; __ballot(i < nw); ++i) {
+        const uint32_t k = k0 + i;
+        const uint32_t a = i == 0 ? lo & 31u : 0u, b = k == (hi >> 5) ? (hi & 31u) : 31u;
+        const uint32_t m = (0xffffffffu >> (31u - b)) & (0xffffffffu << a);
+        if (i < nw) {
+            if (set) __hip_atomic_fetch_or(bm + k, m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            else __hip_atomic_fetch_and(bm + k, ~m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
     }
-    // Inflater.checksum (sd-inflate.ts:136-146): adler32 over 16 KiB output chunks counted
-    // from the start of each append()'s output (abase), with the NMAX quirk (adler32.ts:67):
-    // a final chunk of 5552 or 11104 bytes leaves sum2 unreduced.  Every other chunk ends
-    // reduced, so the value is the plain adler32 state except after such a chunk, which is
-    // replayed from the state at its start -- recovered from the plain state at its end and
-    // its bytes (the last <= 11104 output bytes are in the ring).
-    const bool cont_next = A.streaming && flag == 3 && S->stall == 2;   // this append continues
-    const uint64_t T0 = A.streaming ? R->total : 0, T1 = T0 + pos;
-    const uint64_t abase = A.streaming ? R->abase : 0;
-    const uint32_t rr = (uint32_t)((T1 - abase) & 16383u);
-    const bool quirk = !gz && !failed && !cont_next && (rr == 5552u || rr == 11104u);
-    uint64_t qa = 0, qb = 0;                              // sum b_j, sum (rr - j) b_j of that chunk
-    if (quirk) {
-        for (uint32_t k = tid; k < rr; k += RS_THREADS) {
-            const uint32_t v = ring[ridx64((int64_t)pos - rr + k)];
-            qa += v;
-            qb += (uint64_t)(rr - k) * v;
-        }
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) { qa += __shfl_xor(qa, o); qb += __shfl_xor(qb, o); }
-        if (lane == 0) { red[w][0] = qa; red[w][1] = qb; }
-        __syncthreads();
-        qa = 0; qb = 0;
-#pragma unroll
-        for (int q = 0; q < RS_WAVES; ++q) { qa += red[q][0]; qb += red[q][1]; }
+}
+// are bits [lo, hi) of the pending bitmap all clear?  (lanes without act: true)
+__device__ __forceinline__ bool rb_clear(uint32_t* bm, bool act, uint32_t lo, uint32_t hi) {
+    const bool any = act && hi > lo;
+    const uint32_t k0 = lo >> 5, nw = any ? ((hi - 1u) >> 5) - k0 + 1u : 0u;
+    uint32_t miss = 0;
+    for (uint32_t i = 0; __ballot(i < nw); ++i) {
+        const uint32_t k = k0 + i;
+        const uint32_t a = i == 0 ? lo & 31u : 0u, b = k == ((hi - 1u) >> 5) ? ((hi - 1u) & 31u) : 31u;
+        const uint32_t m = (0xffffffffu >> (31u - b)) & (0xffffffffu << a);
+        const uint32_t v = __hip_atomic_load(bm + (i < nw ? k : 0u), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        miss |= i < nw ? v & m : 0u;
     }
-    __syncthreads();                                      // window / carry copies done
-    if (tid != 0) return;
-    if (carry_over) { S->mode = LM_DONE; S->status = SDZ_CARRY_OVERFLOW; S->zmsg = 0; }
-    // final: record + verdicts (sd-inflate.ts:134-179); gzip's crc32 comes from k_inflate_finalize
-    sdz_inflate_record Rc;
-    Rc.status = failed ? SDZ_INTERNAL : S->status;
-    Rc.zmsg = failed ? (int32_t)fail : S->zmsg;      // watchdog: site | position << 4
-    Rc.out_len = pos;
-    uint64_t used = (bitpos + 7) >> 3;
-    if (used > ilen) used = ilen;
-    // incremental: the stream offset up to which input is consumed or held by the device
-    Rc.in_used = A.streaming ? R->in_base + (flag == 3 && !carry_over ? keep_end : used) : used;
-    Rc.stored_checksum = S->stored_ck;
-    const uint64_t total = T1;
-    bool have = total > 0;                                // Inflater.checksum stays undefined otherwise
-    int32_t running = 0;
-    uint32_t a1 = A.streaming ? R->a1 : 1u, a2 = A.streaming ? R->a2 : 0u;   // state at T0 (exact)
-    if (!gz) {
-        if (pos) {                                        // no output keeps the exact (quirky) state
-            const uint32_t nm = mod65521(pos);
-            const uint32_t b1 = (uint32_t)(((uint64_t)a1 + S_all) % 65521u);
-            const uint32_t b2 = (uint32_t)(((uint64_t)a2 + (uint64_t)nm * a1 + (uint64_t)nm * S_all +
-                                            65521ull * 65521ull - T_all) % 65521u);
-            a1 = b1;
-            a2 = b2;
+    return miss == 0;
+}
+
+// write-back by the whole workgroup: output bytes [pos0 + WB, pos0 + ae) from the ring to HBM (all
+// four bytes of the dwords inside, the edge dwords byte by byte), folded into each thread's adler32
+// partials.  Every thread's ring reads are issued before its stores.
+template <uint32_t NT>
+__device__ __forceinline__ void rb_write_back(uint8_t* out, const uint32_t* ring32, uint64_t pos0, uint64_t ae, bool gz,
+                                              uint32_t& WB, uint32_t& rW, uint32_t& gm, uint32_t& accS, uint64_t& accT) {
+    const uint32_t tid = threadIdx.x;
+    const uint64_t ab = pos0 + WB;
+    if (ae <= ab) return;
+    const uint32_t h = (uint32_t)(ab & 3u);
+    const uint32_t nq = (uint32_t)(((ae + 3u) >> 2) - (ab >> 2));
+    const uint32_t tl = (uint32_t)(ae & 3u);
+    uint32_t* dstw = (uint32_t*)(out + (ab - h));
+    const int32_t rb0 = (int32_t)rW - (int32_t)h;      // ring index of the first dword (4-aligned)
+    const uint32_t gi0 = gm + 65521u - h;              // index of its byte 0, mod 65521 (+ 65521)
+    for (uint32_t q0 = 0; q0 < nq; q0 += 2 * NT) {
+        uint32_t v[2];
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const uint32_t q = q0 + tid + u * NT;
+            v[u] = ring32[q < nq ? ridx_t<RB_R>(rb0 + 4 * (int32_t)q) >> 2 : 0u];
         }
-        if (quirk) {
-            uint32_t s1s, s2s;                            // state at the final chunk's start
-            if (T1 - rr == abase) {
-                s1s = A.streaming ? R->a1s : 1u;
-                s2s = A.streaming ? R->a2s : 0u;
-            } else {
-                s1s = (uint32_t)((a1 + 65521u - mod65521(qa)) % 65521u);
-                s2s = (uint32_t)(((uint64_t)a2 + 65521ull * 65521ull - (uint64_t)rr * s1s - mod65521(qb)) % 65521u);
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const uint32_t q = q0 + tid + u * NT;
+            if (q >= nq) break;
+            const uint32_t blo = q == 0 ? h : 0u;
+            const uint32_t bhi = q + 1 < nq || tl == 0 ? 4u : tl;
+            if (blo == 0 && bhi == 4) dstw[q] = v[u];
+            else for (uint32_t bb = blo; bb < bhi; ++bb) ((uint8_t*)(dstw + q))[bb] = (uint8_t)(v[u] >> (8 * bb));
+            if (!gz) {
+                const uint32_t mk = (bhi == 4u ? ~0u : (1u << (8 * bhi)) - 1u) & (~0u << (8 * blo));
+                const uint32_t vm = v[u] & mk;
+                const uint32_t s4 = __builtin_amdgcn_udot4(vm, 0x01010101u, 0u, false);
+                accS += s4;
+                accT += (uint64_t)(gi0 + 4 * q) * s4 + __builtin_amdgcn_udot4(vm, 0x03020100u, 0u, false);
             }
-            running = adler_quirk_ring(ring, (int64_t)pos - rr, rr, s1s, s2s);
-        } else {
-            running = (int32_t)(a1 | (a2 << 16));
         }
     }
-    Rc.running_checksum = have ? running : 0;
-    Rc.stored_size = S->stored_size;
-    Rc.mtime = S->mtime;
-    Rc.name_off = S->name_off;
-    Rc.name_len = S->name_len;
-    Rc.container = (uint8_t)S->container;
-    bool complete = !failed && S->mode == LM_DONE && (S->status == SDZ_OK || S->status == SDZ_TRAILING);
-    Rc.complete = complete ? 1 : 0;
-    uint8_t cv = S->stored_ck == 0 ? SDZ_UNCHECKED : ((have && S->stored_ck == running) ? SDZ_MATCH : SDZ_MISMATCH);
-    uint8_t sv = S->stored_size == 0 ? SDZ_UNCHECKED
-               : ((int64_t)S->stored_size == (int64_t)total ? SDZ_MATCH : SDZ_MISMATCH);
-    Rc.checksum_verdict = cv;
-    Rc.size_verdict = sv;
-    Rc.success = (complete && cv != SDZ_MISMATCH && sv != SDZ_MISMATCH) ? 1 : 0;
-    Rc.out_full = S->mode != LM_DONE && S->stall == 2 ? 1 : 0;
-    if (!complete && Rc.status == SDZ_OK) Rc.status = SDZ_TRUNCATED;   // incremental: needs more input
-    for (int k = 0; k < 10; ++k) Rc.reserved[k] = 0;
-    A.rec[sid] = Rc;
-    if (A.streaming) {                                    // state for the next call
-        R->total = total;
-        if (!gz && have) { R->a1 = (uint32_t)running & 0xffffu; R->a2 = (uint32_t)running >> 16; }
-        if (flag == 3 && !carry_over) {
-            R->in_base += bitpos >> 3;
-            R->carry_len = carry_n;
-            R->hist = 1;
-            S->bitpos = bitpos & 7;
+    const uint32_t m = (uint32_t)(ae - ab);
+    WB += m;
+    rW += m;
+    rW -= rW >= RB_R ? RB_R : 0u;
+    gm = (uint32_t)((gm + (uint64_t)m) % 65521u);
+}
+
+// RB_PROF (development build): phase clocks of the first 8 workgroups, summed into A.dbg[16..]
+// (SDZ_PHASE_TIMING=1 prints them).  Token waves: [16] wait for the dependents wave, [17] offsets
+// and cut, [18] classify and immediate writes, [19] scan and write-back, [20] barrier, [21] an
+// overflowed list; dependents wave: [22] waiting, [23] writing; [24] batches, [25] overflows, [26] cuts
+#ifdef RB_PROF
+#define RB_T0() unsigned long long rb_t = clock64()
+#define RB_TICK(k) do { if (prof) { unsigned long long tn = clock64(); pacc[k] += tn - rb_t; rb_t = tn; } } while (0)
+#else
+#define RB_T0() do {} while (0)
+#define RB_TICK(k) do {} while (0)
+#endif
+
+// the batch's token lengths and their wave scan; the waves' totals go to wsum
+// (the length is recomputed where it is used: one register less across the batch)
+struct RbTok {
+    uint32_t t, incl;
+};
+__device__ __forceinline__ uint32_t rb_len(uint32_t t) {
+    return (int32_t)t < 0 ? ((t >> 16) & 255u) + 3u : ((t >> 24) & 3u) + 1u;
+}
+__device__ __forceinline__ RbTok rb_scan(uint32_t t, bool valid, uint32_t* wsum, uint32_t wu) {
+    RbTok r;
+    r.t = valid ? t : 0u;                                // (an invalid lane: a 1-byte literal, length 0 here)
+    r.incl = wave_incl_scan(valid ? rb_len(t) : 0u);
+    if ((threadIdx.x & 63u) == 63u) wsum[wu] = r.incl;
+    return r;
+}
+
+// a token of the batch, placed: its ring destination d and source s, and the batch-relative
+// source bytes [sb, se) it reads (sb < 0: before the batch)
+struct RbPlace {
+    uint32_t len, dist, d, s;
+    int32_t sb, se;
+    bool ism, gen;
+};
+__device__ __forceinline__ RbPlace rb_place(uint32_t t, uint32_t dp, uint32_t rP) {
+    RbPlace q;
+    q.ism = (int32_t)t < 0;
+    q.len = q.ism ? ((t >> 16) & 255u) + 3u : ((t >> 24) & 3u) + 1u;
+    q.dist = q.ism ? (t & 0x7fffu) + 1u : 0u;
+    uint32_t d = rP + dp;
+    d -= d >= RB_R ? RB_R : 0u;
+    q.d = d;
+    const int32_t sr = (int32_t)d - (int32_t)q.dist;
+    q.s = sr < 0 ? (uint32_t)(sr + RB_R) : (uint32_t)sr;
+    q.sb = (int32_t)dp - (int32_t)q.dist;
+    q.se = q.ism ? q.sb + (int32_t)(q.len < q.dist ? q.len : q.dist) : q.sb;
+    // copies that overlap themselves or cross the ring's end take the general path, which runs
+    // with the dependents (inlined at one site)
+    q.gen = d + q.len > RB_R || (q.ism && (q.dist < q.len || q.s + q.len > RB_R || q.s < 4u));
+    return q;
+}
+
+// The dependents of one batch, written as their sources allow (whole wave; lanes with pend):
+// a dependent is ready once the pending bits of its source bytes inside the batch are clear; it
+// writes its bytes, then clears its own bits.  false: the watchdog tripped.
+__device__ __forceinline__ bool rb_dependents(uint8_t* ring, uint32_t* bmh, bool pend, uint32_t t, uint32_t dp,
+                                              const RbPlace& r, uint32_t* fail, uint32_t site) {
+    const uint32_t lo = r.sb > 0 ? (uint32_t)r.sb : 0u;
+    const uint32_t hi = r.se > 0 ? (uint32_t)r.se : 0u;
+    for (uint32_t n = 1; __ballot(pend); ++n) {
+        const bool rdy = pend && rb_clear(bmh, pend, lo, hi);
+        RS_CBAR();
+        if (__ballot(rdy)) {
+            emit_msk<RB_R, false, RB_MW, 2>(ring, nullptr, rdy, t, r.d, r.s, r.len, r.dist, 0, 0);
+            RS_CBAR();
+            rb_bits(bmh, rdy, dp, r.len, false);
+            pend = pend && !rdy;
+            n = 0;
         } else {
-            R->carry_len = 0;
+            if ((n & 63u) == 0 && (n > RB_SPIN_LIMIT || lds_get(fail))) {
+                if (!lds_get(fail)) lds_put(fail, site);
+                return false;
+            }
+            __builtin_amdgcn_s_sleep(1);
         }
     }
+    return true;
+}
+
+// a bounded wait until *p >= v (false: the watchdog tripped or another wave's did)
+__device__ __forceinline__ bool rb_wait(uint32_t* p, uint32_t v, uint32_t* fail, uint32_t site) {
+    for (uint32_t n = 1;; ++n) {
+        if (lds_get(p) >= v) { lds_acquire(); return true; }
+        if ((n & 15u) == 0 && (n > RB_SPIN_LIMIT || lds_get(fail))) {
+            if (!lds_get(fail)) lds_put(fail, site);
+            return false;
+        }
+        __builtin_amdgcn_s_sleep(1);
+    }
+}
+// a barrier of the token waves (the dependents wave runs on): a counter in LDS
+__device__ __forceinline__ bool rb_bar(uint32_t* cnt, uint32_t& gen, uint32_t* fail) {
+    lds_release();
+    if ((threadIdx.x & 63u) == 0) __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    gen += RB_TW;
+    return rb_wait(cnt, gen, fail, 6u);
+}
+
+// k_inflate_resolve_b, the pipeline: the token waves take batch b's tokens (one per lane), write
+// its literals and its copies whose sources are final, and list the rest (the DEPENDENTS: sources
+// in batch b, or on bytes of batch b - 1 still pending) with their destination bytes marked in the
+// batch's pending bitmap; the dependents wave meanwhile writes batch b - 1's list.  Two batches are
+// in flight, so the ring holds the window and two batches, and the token waves wait only when the
+// dependents wave is two batches behind.  A batch whose list overflows is finished by the token
+// waves themselves (each lane its own dependent) once the dependents wave has caught up.
+__global__ __launch_bounds__(RB_THREADS) __attribute__((amdgpu_waves_per_eu(RB_WAVES, RB_WAVES)))
+void k_inflate_resolve_b(InflateArgs A, uint32_t round) {
+    __shared__ __attribute__((aligned(16))) uint8_t ring[RB_R + 256];   // + per-lane dummies
+    __shared__ uint32_t bm[2][RB_BMW];                   // pending bytes of each batch in flight
+    __shared__ uint32_t tl[2][RB_TW * RB_DLW];           // dependents lists: token ...
+    __shared__ uint16_t dpl[2][RB_TW * RB_DLW];          // ... and batch-relative offset
+    __shared__ uint32_t wsum[2][RB_WAVES], wcnt[RB_WAVES], wend[RB_WAVES], dcnt[2][RB_WAVES];
+    __shared__ uint32_t bP[2], brP[2], ovf[2];           // per batch in flight: start, its ring index, list overflow
+    __shared__ uint32_t bar, listed, done, tfin, fail;   // token-wave barrier; batches listed / done; batch count
+    __shared__ uint32_t Pend;                            // the round's output bytes (for all waves at the end)
+    __shared__ uint64_t red[RB_WAVES][2];
+
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, w = tid >> 6;
+    const uint32_t sid = blockIdx.x;
+    if (sid >= A.n) return;
+    const uint32_t flag = A.flags[sid];
+    const bool fin0 = A.streaming && round == 0 && flag == 2;   // (as in k_inflate_resolve)
+    if (flag == 2 && !fin0) return;
+    RSave* R = (RSave*)A.rsave + sid;
+    DSave* S = (DSave*)A.dsave + sid;
+    const bool gz = S->container == SDZ_CONTAINER_GZIP;
+    const uint64_t pos0 = round == 0 ? 0 : R->pos;
+    uint8_t* out = A.out + A.out_off[sid];
+    const uint32_t* tk = A.tokens + (uint64_t)sid * A.round_tokens;
+    const uint32_t ntok = A.ntok[sid];
+    const int64_t dl = S->dict_used && A.dict ? (A.dict_len > 32767 ? 32767 : A.dict_len) : 0;
+    const uint8_t* dict = dl ? A.dict + (A.dict_len - dl) : nullptr;
+    const uint32_t rp0 = (uint32_t)(pos0 % RB_R);
+    ring_window_init<RB_R, RB_THREADS>(ring, A, sid, round, pos0, out, dl, dict);
+    for (uint32_t k = tid; k < 2 * RB_BMW; k += RB_THREADS) (&bm[0][0])[k] = 0;
+    if (tid == 0) { fail = 0; bar = 0; listed = 0; done = 0; tfin = 0xffffffffu; ovf[0] = 0; ovf[1] = 0; }
+
+    const uint32_t wu = uni(w);
+    uint32_t accS = 0;
+    uint64_t accT = 0;
+    const uint32_t* ring32 = (const uint32_t*)ring;
+    uint32_t P = 0;                                       // end of the batches listed so far (round-relative)
+    RbTok K;
+    uint32_t tnext = 0;                                   // token waves: batch b + 1's tokens, loaded a batch
+    if (wu < RB_TW) {                                     // early assuming batch b is not cut
+        K = rb_scan(tk[tid < ntok ? tid : 0u], tid < ntok, wsum[0], wu);
+        tnext = tk[RB_BATCH + tid < ntok ? RB_BATCH + tid : 0u];
+    }
+    __syncthreads();
+#ifdef RB_PROF
+    const bool prof = A.dbg && sid < 8 && lane == 0;
+    unsigned long long pacc[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+#endif
+    RB_T0();
+    if (wu < RB_TW) {
+        // ---- token waves
+        uint32_t rP = rp0, WB = 0, rW = rp0, gm = (uint32_t)(pos0 % 65521u);
+        uint32_t tb = 0, b = 0, Tprev = 0, gen = 0;
+        while (tb < ntok) {
+            const uint32_t pb = b & 1u;
+            // batch b - 2 complete: its bitmap half and list are free, its bytes final
+            if (b >= 2 && !rb_wait(&done, b - 1u, &fail, 7u)) break;
+            RB_TICK(0);
+            // 1. offsets and the cut (the scan ran before the last barrier)
+            const uint32_t t = K.t, len = tb + tid < ntok ? rb_len(t) : 0u;
+            const uint32_t xs = wave_incl_scan(lane < RB_TW ? wsum[pb][lane_lo8()] : 0u);
+            const uint32_t pre = wu ? lane_at(xs, wu - 1u) : 0u, tot = lane_at(xs, RB_TW - 1);
+            const uint32_t dp = pre + K.incl - len;      // batch-relative offset of the token's first byte
+            const uint32_t rest = ntok - tb;
+            uint32_t Tb = tot, nb = rest < RB_BATCH ? rest : RB_BATCH;
+            bool in = tb + tid < ntok;
+            if (tot > RB_CAP) {                          // cut: the tokens that end within RB_CAP (a prefix)
+                in = in && dp + len <= RB_CAP;
+                const uint64_t bk = __ballot(in);
+                const uint32_t last = bk ? 63u - (uint32_t)__builtin_clzll(bk) : 0u;
+                const uint32_t e = lane_at(dp + len, last);
+                if (lane == 0) { wcnt[wu] = (uint32_t)__builtin_popcountll(bk); wend[wu] = bk ? e : 0u; }
+                if (!rb_bar(&bar, gen, &fail)) break;
+                const uint32_t xc = wave_incl_scan(lane < RB_TW ? wcnt[lane_lo8()] : 0u);
+                nb = lane_at(xc, RB_TW - 1);
+                Tb = lane_at(dpp_max8(lane < RB_TW ? wend[lane_lo8()] : 0u), RB_TW - 1);
+            }
+#ifdef RB_PROF
+            if (prof) { pacc[10] += tot > RB_CAP ? 1 : 0; pacc[8]++; }
+#endif
+            RB_TICK(1);
+            // the next batch's tokens (scanned below): prefetched unless this batch was cut, then the
+            // one after it
+            const uint32_t tb1 = tb + nb;
+            const uint32_t i1 = tb1 + tid_fresh();
+            uint32_t t1 = tnext;
+            if (nb != RB_BATCH) t1 = tk[i1 < ntok ? i1 : 0u];
+            {
+                const uint32_t j = tb1 + RB_BATCH + tid_fresh();
+                tnext = tk[j < ntok ? j : 0u];
+            }
+            // 2. classify: a dependent reads bytes of this batch, or pending bytes of the last
+            const RbPlace q = rb_place(t, dp, rP);
+            bool dep = RB_ABL < 5 && in && ((q.ism && q.se > 0) || q.gen);
+            {
+                const int32_t plo = q.sb > -(int32_t)Tprev ? q.sb : -(int32_t)Tprev, phi = q.se < 0 ? q.se : 0;
+                const bool chk = RB_ABL != 4 && RB_ABL < 5 && in && !dep && q.ism && phi > plo;
+                if (__ballot(chk))
+                    dep = dep || (chk && !rb_clear(bm[pb ^ 1u], chk, (uint32_t)(plo + (int32_t)Tprev),
+                                                   (uint32_t)(phi + (int32_t)Tprev)));
+            }
+            const bool now = in && !dep;
+            const uint64_t dk = __ballot(dep);
+            if (dk) {
+                rb_bits(bm[pb], dep, dp, len, true);
+                const uint32_t k = (uint32_t)__builtin_popcountll(dk & ((1ull << lane) - 1ull));
+                if (dep && k < RB_DLW) { tl[pb][wu * RB_DLW + k] = t; dpl[pb][wu * RB_DLW + k] = (uint16_t)dp; }
+                if (lane == 0 && __builtin_popcountll(dk) > RB_DLW) ovf[pb] = b + 1u;   // (no reset needed)
+            }
+            if (lane == 0) dcnt[pb][wu] = (uint32_t)__builtin_popcountll(dk);
+            if (tid == 0) { bP[pb] = P; brP[pb] = rP; }
+#if RB_ABL != 2 && RB_ABL < 6
+            if (__ballot(now)) emit_msk<RB_R, false, RB_MW, 0>(ring, nullptr, now, t, q.d, q.s, len, q.dist, 0, 0);
+#endif
+            RB_TICK(2);
+            // 3. the next batch's scan, then the complete dwords of batches up to b - 2 to HBM
+            // (the stores come after the wait for the tokens)
+            if (tb1 < ntok) K = rb_scan(t1, i1 < ntok, wsum[pb ^ 1u], wu);
+#if RB_ABL != 1 && RB_ABL < 7
+            rb_write_back<64 * RB_TW>(out, ring32, pos0, (pos0 + (P - Tprev)) & ~3ull, gz, WB, rW, gm, accS, accT);
+#endif
+            RB_TICK(3);
+            if (!rb_bar(&bar, gen, &fail)) break;
+            if (tid == 0) lds_put(&listed, b + 1u);
+            RB_TICK(4);
+            // 4. an overflowed list: this batch's dependents by their own lanes, after the
+            // dependents wave has finished the batch before
+            if (uni(ovf[pb]) == b + 1u) {
+                if (!rb_wait(&done, b, &fail, 8u)) break;
+                if (!rb_dependents(ring, bm[pb], dep, t, dp, q, &fail, 9u)) break;
+                if (!rb_bar(&bar, gen, &fail)) break;
+#ifdef RB_PROF
+                if (prof) pacc[9]++;
+#endif
+            }
+            RB_TICK(5);
+            Tprev = Tb;
+            P += Tb;
+            rP += Tb;
+            rP -= rP >= RB_R ? RB_R : 0u;
+            tb = tb1;
+            ++b;
+        }
+        if (tid == 0) { Pend = P; lds_put(&tfin, b); }
+        // the last batches: the rest once the dependents wave is done
+        if (rb_wait(&done, b, &fail, 10u))
+            rb_write_back<64 * RB_TW>(out, ring32, pos0, pos0 + P, gz, WB, rW, gm, accS, accT);
+    } else {
+        // ---- the dependents wave: batch b's list once it is listed, in order of position (the
+        // list is in token order per wave, waves in order), 64 entries at a time: an entry
+        // depends only on earlier ones
+        for (uint32_t b = 0;; ++b) {
+            bool go = false;
+            for (uint32_t n = 1;; ++n) {
+                if (lds_get(&listed) > b) { go = true; break; }
+                if (lds_get(&tfin) <= b || lds_get(&fail)) break;
+                if ((n & 15u) == 0 && n > RB_SPIN_LIMIT) { lds_put(&fail, 11u); break; }
+                __builtin_amdgcn_s_sleep(1);
+            }
+            if (!go) break;
+            RB_TICK(6);
+            lds_acquire();
+            const uint32_t pb = b & 1u;
+            if (uni(ovf[pb]) != b + 1u) {
+                const uint32_t rPb = uni(brP[pb]);
+                const uint32_t cw = lane < RB_TW ? dcnt[pb][lane_lo8()] : 0u;
+                const uint32_t cs = wave_incl_scan(cw);  // inclusive per-wave prefix of the counts
+                const uint32_t nd = lane_at(cs, RB_TW - 1);
+                bool ok = true;
+                for (uint32_t c = 0; c < nd && ok; c += 64) {
+                    const uint32_t e = c + lane;
+                    const bool act = e < nd;
+                    uint32_t wq = 0, base = 0;           // the wave whose entry e is, and its prefix
+#pragma unroll
+                    for (int v = 0; v < RB_TW - 1; ++v) {
+                        const uint32_t pv = lane_at(cs, (uint32_t)v);
+                        const bool past = e >= pv;
+                        wq += past ? 1u : 0u;
+                        base = past ? pv : base;
+                    }
+                    const uint32_t idx = act ? wq * RB_DLW + (e - base) : 0u;
+                    const uint32_t t = tl[pb][idx], dp = dpl[pb][idx];
+                    const RbPlace r = rb_place(t, dp, rPb);
+#if RB_ABL == 3
+                    rb_bits(bm[pb], act, dp, r.len, false);
+#else
+                    ok = rb_dependents(ring, bm[pb], act, t, dp, r, &fail, 12u);
+#endif
+                }
+                if (!ok) break;
+            }
+            lds_release();
+            if (lane == 0) lds_put(&done, b + 1u);
+            RB_TICK(7);
+        }
+    }
+#ifdef RB_PROF
+    if (prof) for (int k = 0; k < 12; ++k) atomicAdd(&A.dbg[16 + k], pacc[k]);
+#endif
+    if (tid == 0 && ntok == 0) Pend = 0;
+    __syncthreads();
+    resolve_finish<RB_R, RB_WAVES>(A, round, sid, flag, fin0, gz, pos0, pos0 + (uint64_t)uni(Pend), nullptr, &fail, ring,
+                                   accS, accT, &red[0][0]);
 }
 
 // ------------------------------------------------------------------ gzip: crc32 + verdicts
@@ -848,6 +1356,18 @@ __global__ __launch_bounds__(64) void k_inflate_finalize(InflateArgs A, uint64_t
 }
 
 uint32_t resolve_block_threads() { return RS_THREADS; }
+static_assert(RS_THREADS == RB_THREADS, "both resolve kernels run one workgroup of the same size per stream");
+// SDZ_RESOLVE=1 (read at each launch, so tests can switch it): the batch pipeline
+// (k_inflate_resolve_b); default: the group pipeline (k_inflate_resolve), faster on
+// every bench shape measured
+static bool resolve_batches() {
+    const char* e = getenv("SDZ_RESOLVE");
+    return e && *e == '1';
+}
+void launch_inflate_resolve(const InflateArgs& a, uint32_t round, dim3 grid, hipStream_t s) {
+    if (resolve_batches()) hipLaunchKernelGGL(k_inflate_resolve_b, grid, dim3(RB_THREADS), 0, s, a, round);
+    else hipLaunchKernelGGL(k_inflate_resolve, grid, dim3(RS_THREADS), 0, s, a, round);
+}
 uint32_t resolve_streams_per_block() { return 1; }
 // parts: scratch for the chunk crcs (a.tokens: the token rings are free once the rounds are
 // done; >= 1024 entries per stream); chunks of >= 256 KiB, <= 1024 per stream and <= 4 Mi
