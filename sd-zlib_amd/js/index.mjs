@@ -192,31 +192,31 @@ export function inflate(data, dictionary) {
 	// Inflater(...).append(input) + finish() on one buffer is one one-shot decode: the batched
 	// engine's records carry the same verdicts, and its path has no incremental-stream state
 	// to create, carry and destroy per call (C1: ~0.22 -> ~0.1 ms through this facade)
-	let cap = Math.max(65536, 4 * input.length);
-	let r;
-	for (;;) {
-		r = addon.inflateBatch([input], ident ? FMT_CONTAINER : FMT_RAW, [cap], inflater.dict || null, null)[0];
-		if (r.status !== "OUT_OVERFLOW") {
-			break;
-		}
-		cap *= 4;
-	}
-	if (r.status !== "TRUNCATED") {
+	// A stream that expands by more than 4x does not fit that one slot: it takes the reference's
+	// own path (Inflater.append + finish, output in pieces) instead of growing the slot and
+	// decoding again, so no input is decoded more than twice and no slot outgrows its output.
+	const cap = Math.max(65536, 4 * input.length);
+	const r = addon.inflateBatch([input], ident ? FMT_CONTAINER : FMT_RAW, [cap], inflater.dict || null, null)[0];
+	let buffers = null, result = r;
+	if (r.status === "OUT_OVERFLOW") {
+		buffers = inflater.append(input);
+		result = inflater.finish();
+	} else if (r.status !== "TRUNCATED") {
 		throwFor(r);
 	}
-	if (!r.success) {
-		if (!r.complete) {
+	if (!result.success) {
+		if (!result.complete) {
 			throw new Error("Unexpected EOF during decompression");
 		}
-		if (r.checksum === "mismatch") {
+		if (result.checksum === "mismatch") {
 			throw new Error("Data integrity check failed");
 		}
-		if (r.fileSize === "mismatch") {
+		if (result.fileSize === "mismatch") {
 			throw new Error("Data size check failed");
 		}
 		throw new Error("Decompression error");
 	}
-	return r.data.slice();                       // (a buffer of its own length, as mergeBuffers returns)
+	return buffers ? mergeBuffers(buffers) : r.data.slice();   // (a buffer of its own length, as mergeBuffers returns)
 }
 
 // sd-deflate.ts:51-254

@@ -140,6 +140,16 @@ check("deflate L6 == reference fixture", eq(deflate(text, { level: 6 }), golden(
 		try { inflate(data); } catch (e) { m = e.message; }
 		check("inflate " + name + ": " + m, m !== "" && m === viaInflater(data));
 	}
+	// a stream that expands ~1000x overflows the one-shot slot: inflate() takes the Inflater path, with
+	// the same bytes, and the same error for a corrupted copy
+	const zeros = new Uint8Array(1 << 20);
+	const zc = deflate(zeros, { level: 9 });
+	check("inflate 1 MiB of zeros (" + zc.length + " B in)", eq(inflate(zc), zeros));
+	const zbad = zc.slice();
+	zbad[zbad.length - 1] ^= 1;
+	let zm = "";
+	try { inflate(zbad); } catch (e) { zm = e.message; }
+	check("inflate zeros, bad adler32: " + zm, zm !== "" && zm === viaInflater(zbad));
 }
 check("adler32 KAT", adler32(golden("simple.txt")) === -1612443532);
 check("crc32 KAT", crc32(golden("simple.txt")) === 1488305224);
