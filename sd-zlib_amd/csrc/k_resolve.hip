@@ -37,7 +37,12 @@ namespace sdz {
 #define RS_EW (RS_WAVES - 1)           // emitter waves; the last wave writes back
 #define RS_THREADS (64 * RS_WAVES)
 #define RS_WIN 32768
+#ifndef RS_DB
+#define RS_DB 0                       // 1: two groups per emitter wave, one token per lane and pass (measured slower)
+#endif
+#ifndef RS_R
 #define RS_R 36352                    // ring bytes: 32 KiB window + bytes in flight
+#endif
 #define RS_SLACK (RS_R - RS_WIN)
 #ifndef RS_WPE
 #define RS_WPE RS_WAVES               // waves per SIMD the register budget is sized for
@@ -45,7 +50,9 @@ namespace sdz {
 #ifndef RS_NAP
 #define RS_NAP 8                      // s_sleep units (64 clocks) between polls
 #endif
-#define RS_BM 4096                    // finality map bytes (>= RS_SLACK; lap = position >> 12)
+#ifndef RS_BM
+#define RS_BM 4096                    // finality map bytes (a power of 2 >= RS_SLACK; lap = position / RS_BM)
+#endif
 #define RS_SPIN_LIMIT (1u << 22)      // watchdog: polls per wait (~0.4 s)
 
 template <uint32_t RR>
@@ -394,12 +401,12 @@ __device__ __forceinline__ bool wait_ge(uint32_t* p, uint32_t v, uint32_t* fail)
 }
 
 // Finality map over the bytes in flight: map byte (g mod RS_BM) holds the lap byte
-// ((g >> 12) & 127) + 1 of global position g once byte g is in the ring.  A stale value
+// ((g / RS_BM) & 127) + 1 of global position g once byte g is in the ring.  A stale value
 // is a different lap, so nothing is ever cleared; a map byte overwritten by a later lap
 // belongs to a byte already below Wf (RS_SLACK <= RS_BM), where the check is skipped.
 // Wave-uniform loop over the aligned map dwords of [lo, hi) (low 32 bits of global
 // positions) of each active lane.
-__device__ __forceinline__ uint32_t lap_of(uint32_t g) { return ((g >> 12) & 127u) + 1u; }
+__device__ __forceinline__ uint32_t lap_of(uint32_t g) { return ((g / RS_BM) & 127u) + 1u; }
 __device__ __forceinline__ bool map_all(const uint8_t* fmap, bool act, uint32_t lo, uint32_t hi) {
     const uint32_t* fmap32 = (const uint32_t*)fmap;
     uint32_t miss = 0;                                    // VGPR accumulation: no lane-mask (SALU) ops
@@ -426,6 +433,35 @@ __device__ __forceinline__ void rs_wake() {
 __device__ __forceinline__ void publish_wf(uint32_t* wf, uint32_t v1) {
     lds_release();
     if ((threadIdx.x & 63u) == 0) lds_put(wf, v1);
+    rs_wake();
+}
+#ifndef RS_MINF
+#define RS_MINF 0                     // 1: the frontier as a minimum over the emitter waves (0: published in group order)
+#endif
+// The frontier of final bytes without an in-order publication (RS_MINF): every emitter wave keeps
+// the first byte it has still to write in low[w] (~0: nothing pending), and a byte is final once it
+// lies below the end of the groups started so far (the chain's end, read first: a group started
+// later lowers its wave's low before it extends the chain) and below every wave's low.
+__device__ __forceinline__ uint32_t min_dpp8(uint32_t x) {    // lane 7: the minimum of lanes 0..7
+    uint32_t y = (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)x, 0x111, 0xf, 0xf, false);   // row_shr:1
+    x = x < y ? x : y;
+    y = (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)x, 0x112, 0xf, 0xf, false);            // row_shr:2
+    x = x < y ? x : y;
+    y = (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)x, 0x114, 0xf, 0xf, false);            // row_shr:4
+    return x < y ? x : y;
+}
+__device__ __forceinline__ uint32_t rs_frontier(uint64_t* chain, uint32_t* low) {
+    const uint32_t ce = uni((uint32_t)lds_get64(chain));
+    lds_acquire();
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t v = __hip_atomic_load(&low[lane < RS_EW ? lane : 0u], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    const uint32_t m = lane_at(min_dpp8(lane < RS_EW ? v : ~0u), 7);
+    lds_acquire();
+    return ce < m ? ce : m;
+}
+__device__ __forceinline__ void rs_publish_low(uint32_t* low, uint32_t wu, uint32_t v) {
+    lds_release();
+    if ((threadIdx.x & 63u) == 0) lds_put(&low[wu], v);
     rs_wake();
 }
 
@@ -628,12 +664,55 @@ __device__ __forceinline__ void resolve_finish(const InflateArgs& A, uint32_t ro
     }
 }
 
+// One write-back chunk of the writer (or finisher) wave: output bytes [ab, ab + m) from ring index Wr
+// to HBM as coalesced dwords (an output-aligned KiB as 4 full dwords per lane), folded into the
+// lane's adler32 sums; gm = ab mod 65521.
+__device__ __forceinline__ void rs_write_chunk(uint8_t* out, const uint32_t* ring32, bool gz, uint64_t ab, uint32_t m,
+                                               uint32_t Wr, uint32_t gm, uint32_t& accS, uint64_t& accT) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t h = (uint32_t)(ab & 3u);
+    const uint32_t gi0 = gm + 65521u - h;                // index of byte 0 of dword 0, mod 65521 (+ 65521)
+    if (m == 1024u) {
+        uint32_t* dstw = (uint32_t*)(out + ab);
+#pragma unroll
+        for (uint32_t k = 0; k < 4; ++k) {
+            const uint32_t q = lane + 64u * k;
+            const uint32_t v = ring32[ridx((int32_t)Wr + 4 * (int32_t)q) >> 2];
+            dstw[q] = v;
+            if (!gz) {
+                const uint32_t s4 = __builtin_amdgcn_udot4(v, 0x01010101u, 0u, false);
+                accS += s4;
+                accT += (uint64_t)(gi0 + 4 * q) * s4 + __builtin_amdgcn_udot4(v, 0x03020100u, 0u, false);
+            }
+        }
+    } else {
+        const uint32_t nq = (uint32_t)(((ab + m + 3u) >> 2) - (ab >> 2));
+        uint32_t* dstw = (uint32_t*)(out + (ab - h));
+        const int32_t rb0 = (int32_t)Wr - (int32_t)h;    // ring index of the first dword (4-aligned)
+        const uint32_t tl = (uint32_t)((ab + m) & 3u);
+        for (uint32_t q = lane; q < nq; q += 64) {
+            const uint32_t v = ring32[ridx(rb0 + 4 * (int32_t)q) >> 2];
+            const uint32_t blo = q == 0 ? h : 0u;
+            const uint32_t bhi = q + 1 < nq || tl == 0 ? 4u : tl;
+            if (blo == 0 && bhi == 4) dstw[q] = v;
+            else for (uint32_t bb = blo; bb < bhi; ++bb) ((uint8_t*)(dstw + q))[bb] = (uint8_t)(v >> (8 * bb));
+            if (!gz) {
+                const uint32_t mk = (bhi == 4u ? ~0u : (1u << (8 * bhi)) - 1u) & (~0u << (8 * blo));
+                const uint32_t vm = v & mk;
+                const uint32_t s4 = __builtin_amdgcn_udot4(vm, 0x01010101u, 0u, false);
+                accS += s4;
+                accT += (uint64_t)(gi0 + 4 * q) * s4 + __builtin_amdgcn_udot4(vm, 0x03020100u, 0u, false);
+            }
+        }
+    }
+}
+
 __global__ __launch_bounds__(RS_THREADS) __attribute__((amdgpu_waves_per_eu(RS_WPE, RS_WPE))) void k_inflate_resolve(InflateArgs A, uint32_t round) {
     __shared__ __attribute__((aligned(16))) uint8_t ring[RS_R + 256];   // + per-lane dummies
     __shared__ uint64_t chain;                           // (tag of the last started group) << 32 | its end
     __shared__ uint32_t wf, wwb, fail, edone;            // frontiers: final bytes, written-back bytes; emitters done
     __shared__ __attribute__((aligned(16))) uint8_t fmap[RS_BM];   // finality map of the bytes in flight
-    __shared__ uint64_t red[RS_WAVES][2];
+    __shared__ uint32_t low[RS_EW];                      // RS_MINF: each emitter wave's first byte still to write
 
     const uint32_t tid = threadIdx.x, lane = tid & 63u, w = tid >> 6;
     const uint32_t sid = blockIdx.x;
@@ -656,8 +735,15 @@ __global__ __launch_bounds__(RS_THREADS) __attribute__((amdgpu_waves_per_eu(RS_W
     const uint32_t pm0 = (uint32_t)(pos0 % 65521u);
     ring_window_init<RS_R, RS_THREADS>(ring, A, sid, round, pos0, out, dl, dict);
     if (tid == 0) { chain = 0xffffffff00000000ull; wf = 0; wwb = 0; fail = 0; edone = 0; }
+    if (tid < RS_EW) low[tid] = ~0u;
     for (uint32_t k = tid; k < RS_BM / 4; k += RS_THREADS) ((uint32_t*)fmap)[k] = 0;
     __syncthreads();
+#if RS_MINF
+#define RS_WF() rs_frontier(&chain, low)
+#else
+#define RS_WF() lds_get(&wf)
+#endif
+    uint32_t lowpub = ~0u;                                // RS_MINF: this wave's low as published
 
     // adler32 as sums over the whole output: s1 = 1 + S, s2 = n + n S - T (mod 65521),
     // S = sum b_i, T = sum i b_i -- per-lane partials, combined once per round
@@ -678,10 +764,148 @@ __global__ __launch_bounds__(RS_THREADS) __attribute__((amdgpu_waves_per_eu(RS_W
     // costs ~3 SIMD cycles, measured), so divergent ifs and their exec-mask juggling
     // are avoided on the hot path.  `fail` is polled once per 64 waits only.
     const uint32_t wu = uni(w);
+    const uint32_t g32 = (uint32_t)pos0;
     // emitter waves: no global stores, so the token prefetch is their only vector-memory
     // traffic and its wait does not cover write-back stores
     uint32_t tnext = tk[wu * 64u + lane < ntok ? wu * 64u + lane : 0u];
     bool bad = false;                                     // this wave's watchdog tripped
+#if RS_DB
+    if (wu < RS_EW) {
+        // An emitter wave holds two groups: O, the older (not yet final), and N, the next of its
+        // groups.  Each pass gives every lane one token -- its O token while that one is pending,
+        // else its N token -- so a token its group's first pass could not write (its sources were not
+        // final yet) goes out alongside the next group's first pass instead of in a round of its own.
+        // O is published (wf) once it is complete and the frontier has reached it; a head O publishes
+        // its finished prefix, so a group larger than the ring's slack never waits on itself.
+        uint32_t tA = 0, dA = 0, rA = 0, tB = 0, dB = 0, rB = 0;   // token, round-relative start, ring index
+        uint64_t pA = 0, pB = 0;                                   // pending lanes of O and N
+        uint32_t SO = 0, TO = 0, SN = 0, TN = 0;
+        bool haveO = false, haveN = false, scanned = false;
+        uint32_t gn = wu;                                          // the next group to take
+        for (uint32_t n = 1;; ++n) {
+            bool prog = false;
+            // 1. the next group into N: its tokens and offsets, then its start from its predecessor
+            if (!haveN && gn < ngroups) {
+                if (!scanned) {
+                    const uint32_t ti = gn * 64u + lane;
+                    const bool valid = ti < ntok;
+                    const uint32_t t = tnext;
+                    tnext = tk[ti + 64u * RS_EW < ntok ? ti + 64u * RS_EW : 0u];
+                    const uint32_t len = !valid ? 0u : (int32_t)t < 0 ? ((t >> 16) & 255u) + 3u : ((t >> 24) & 3u) + 1u;
+                    const uint32_t incl = wave_incl_scan(len);
+                    tB = t;
+                    dB = incl - len;                               // (group-relative until the start is known)
+                    TN = lane_at(incl, 63);
+                    pB = __ballot(len != 0);
+                    scanned = true;
+                }
+                const uint64_t c = lds_get64(&chain);
+                if (uni((uint32_t)(c >> 32)) == gn - 1u) {
+                    SN = uni((uint32_t)c);
+#if RS_MINF
+                    if (SN < lowpub) { rs_publish_low(low, wu, SN); lowpub = SN; lds_release(); }
+#endif
+                    if (lane == 0) __hip_atomic_store(&chain, ((uint64_t)gn << 32) | (SN + TN), __ATOMIC_RELAXED,
+                                                      __HIP_MEMORY_SCOPE_WORKGROUP);
+                    const uint32_t sr = uni((rp0 + SN) % RS_R);    // ring index of byte SN (u32: SN < 2^26)
+                    rB = ridx((int32_t)(sr + dB));
+                    dB += SN;
+                    haveN = true;
+                    scanned = false;
+                    gn += RS_EW;
+                    prog = true;
+                    if (!haveO) {                                  // (the wave's first group)
+                        tA = tB; dA = dB; rA = rB; pA = pB; SO = SN; TO = TN;
+                        haveO = true;
+                        haveN = false;
+                        continue;
+                    }
+                }
+            }
+            if (!haveO && gn >= ngroups) break;                    // every group of this wave is final
+            RS_TICK(1);
+            // 2. a pass: each lane's O token while pending, else its N token
+            const uint64_t pBv = haveN ? pB : 0u;                  // (a group scanned but not started: not yet)
+            const bool useA = (pA >> lane) & 1u;
+            const bool act = useA || ((pBv >> lane) & 1u);
+            if (__ballot(act)) {
+                const uint32_t t = useA ? tA : tB, dst = useA ? dA : dB, d = useA ? rA : rB;
+                const bool ism = (int32_t)t < 0;
+                const uint32_t len = !act ? 0u : ism ? ((t >> 16) & 255u) + 3u : ((t >> 24) & 3u) + 1u;
+                const uint32_t dist = ism ? (t & 0x7fffu) + 1u : 0u;
+                const uint32_t dend = dst + len;
+                const int32_t src = (int32_t)dst - (int32_t)dist;  // round-relative (may be < 0)
+                const int32_t need = ism ? src + (int32_t)(len < dist ? len : dist) : INT32_MIN;
+                const uint32_t s = ridx((int32_t)d - (int32_t)dist);
+                const uint32_t gd = g32 + dst;                     // low bits of the global position
+                const uint32_t cwf = RS_WF();
+                const uint32_t cwb = lds_get(&wwb);
+                const bool room = act && dend <= cwf + RS_SLACK && dend <= cwb + RS_R;
+                const bool inwin = need <= (int32_t)cwf;
+                const uint32_t blo = src > (int32_t)cwf ? (uint32_t)src : cwf;
+                const bool chk = room && !inwin;
+                bool ok = true;
+                if (__ballot(chk)) ok = map_all(fmap, chk, g32 + blo, g32 + (uint32_t)need);
+                const bool rdy = room && (inwin || ok);
+                const uint64_t rm = __ballot(rdy);
+                if (rm) {
+                    RS_CBAR();
+                    emit_msk<RS_R, true, RS_MW>(ring, fmap, rdy, t, d, s, len, dist, gd & (RS_BM - 1), lap_of(gd));
+                    const uint64_t ma = __ballot(useA);
+                    pA &= ~(rm & ma);
+                    pB &= ~(rm & ~ma);
+                    prog = true;
+                    if (timed) tacc[6]++;
+                }
+            }
+            RS_TICK(2);
+            // 3. O final: complete and reached by the frontier (a head O publishes its finished prefix)
+#if RS_MINF
+            if (haveO && pA == 0) {                                // O complete: N becomes O
+                tA = tB; dA = dB; rA = rB; pA = haveN ? pB : 0u; SO = SN; TO = TN;
+                haveO = haveN;
+                haveN = false;
+                prog = true;
+            }
+            {
+                const uint64_t pBv2 = haveN ? pB : 0u;
+                const uint32_t lv = pA ? lane_at(dA, (uint32_t)__builtin_ctzll(pA))
+                                  : pBv2 ? lane_at(dB, (uint32_t)__builtin_ctzll(pBv2)) : ~0u;
+                if (lv != lowpub) { rs_publish_low(low, wu, lv); lowpub = lv; }
+            }
+#else
+            if (haveO) {
+                const uint32_t cwf = lds_get(&wf);
+                if (cwf >= SO) {
+                    lds_acquire();
+                    if (pA == 0) {
+                        publish_wf(&wf, SO + TO);
+                        tA = tB; dA = dB; rA = rB; pA = haveN ? pB : 0u; SO = SN; TO = TN;
+                        haveO = haveN;
+                        haveN = false;
+                        prog = true;
+                    } else {
+                        const uint32_t pre = lane_at(dA, (uint32_t)__builtin_ctzll(pA));   // the first pending byte
+                        if (cwf < pre) { publish_wf(&wf, pre); prog = true; }
+                    }
+                }
+            }
+#endif
+            RS_TICK(4);
+            if (prog) {
+                n = 0;
+            } else {
+                if (timed) tacc[7]++;
+                if ((n & 63u) == 0 && (n > RS_SPIN_LIMIT || lds_get(&fail))) {
+                    if (!lds_get(&fail)) lds_put(&fail, 3u | (SO << 4));
+                    bad = true;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(RS_NAP);
+            }
+        }
+    }
+#else
     for (uint32_t g = wu; wu < RS_EW && g < ngroups; g += RS_EW) {
         const uint32_t ti = g * 64u + lane;
         const bool valid = ti < ntok;
@@ -708,6 +932,9 @@ __global__ __launch_bounds__(RS_THREADS) __attribute__((amdgpu_waves_per_eu(RS_W
             __builtin_amdgcn_s_sleep(RS_NAP);
         }
         if (bad) break;
+#if RS_MINF
+        if (Sg < lowpub) { rs_publish_low(low, wu, Sg); lowpub = Sg; lds_release(); }
+#endif
         if (lane == 0) __hip_atomic_store(&chain, ((uint64_t)g << 32) | (Sg + T), __ATOMIC_RELAXED,
                                           __HIP_MEMORY_SCOPE_WORKGROUP);
         rs_wake();
@@ -722,10 +949,13 @@ __global__ __launch_bounds__(RS_THREADS) __attribute__((amdgpu_waves_per_eu(RS_W
         const uint32_t s = ridx((int32_t)(sr + off) - (int32_t)dist);
         const uint32_t gd = (uint32_t)pos0 + dst;                       // low bits of the global position
         const uint32_t mp = gd & (RS_BM - 1), lb = lap_of(gd);
-        const uint32_t g32 = (uint32_t)pos0;
         bool done = len == 0;
         uint64_t nd = __ballot(!done);
         for (uint32_t n = 1; nd; ++n) {
+#if RS_MINF
+            const uint32_t cwf = RS_WF();
+            const uint32_t cwb = lds_get(&wwb);
+#else
             const uint32_t pre = lane_at(off, (uint32_t)__builtin_ctzll(nd));   // finished prefix
             uint32_t cwf = lds_get(&wf);
             const uint32_t cwb = lds_get(&wwb);
@@ -733,29 +963,30 @@ __global__ __launch_bounds__(RS_THREADS) __attribute__((amdgpu_waves_per_eu(RS_W
                 publish_wf(&wf, Sg + pre);
                 cwf = Sg + pre;
             }
+#endif
             const bool room = !done && dend <= cwf + RS_SLACK && dend <= cwb + RS_R;
             const bool inwin = need <= (int32_t)cwf;
             const uint32_t blo = src > (int32_t)cwf ? (uint32_t)src : cwf;
             const bool chk = room && !inwin;
             bool ok = true;
             if (__ballot(chk)) ok = map_all(fmap, chk, g32 + blo, g32 + (uint32_t)need);
+#ifdef RS_ABL_ONE
+            const bool rdy = room;                        // development: sources never waited for (output wrong)
+#else
             const bool rdy = room && (inwin || ok);
+#endif
             const uint64_t rm = __ballot(rdy);
             if (rm) {
                 RS_CBAR();
                 emit_msk<RS_R, true, RS_MW>(ring, fmap, rdy, t, d, s, len, dist, mp, lb);
-#ifdef RS_XSALU
-                {   // experiment: extra SALU per emit round
-                    uint32_t z = uni(len);
-#pragma unroll
-                    for (int q = 0; q < RS_XSALU; ++q) asm volatile("s_add_u32 %0, %0, 1" : "+s"(z));
-                    if (z == 0xdeadbeef) tacc[5]++;
-                }
-#endif
                 done = done || rdy;
                 nd &= ~rm;
                 n = 0;
                 if (timed) tacc[6]++;
+#if RS_MINF
+                const uint32_t lv = nd ? Sg + lane_at(off, (uint32_t)__builtin_ctzll(nd)) : ~0u;   // our first pending byte
+                if (lv != lowpub) { rs_publish_low(low, wu, lv); lowpub = lv; }
+#endif
             } else {
                 if (timed) tacc[7]++;
                 if ((n & 63u) == 0 && (n > RS_SPIN_LIMIT || lds_get(&fail))) {
@@ -768,6 +999,9 @@ __global__ __launch_bounds__(RS_THREADS) __attribute__((amdgpu_waves_per_eu(RS_W
         }
         if (bad) break;
         RS_TICK(2);
+#if RS_MINF
+        continue;                                         // (final once every wave's low is past it)
+#endif
         // 3. finality, in group order: publish now if we are the head (no one else can
         // move wf past Sg), else once the frontier reaches us
         for (uint32_t n = 1;; ++n) {
@@ -783,6 +1017,8 @@ __global__ __launch_bounds__(RS_THREADS) __attribute__((amdgpu_waves_per_eu(RS_W
         publish_wf(&wf, Sg + T);
         RS_TICK(4);
     }
+#endif
+    const uint32_t* ring32 = (const uint32_t*)ring;
     if (wu < RS_EW) {
         lds_release();
         if (lane == 0) __hip_atomic_fetch_add(&edone, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -790,11 +1026,10 @@ __global__ __launch_bounds__(RS_THREADS) __attribute__((amdgpu_waves_per_eu(RS_W
         // the writer wave: final bytes -> HBM in output-aligned 1 KiB chunks, folded into the
         // adler32 sums; publishes wwb, which frees ring slots
         uint32_t WB = 0, Wr = rp0, gm = pm0;              // written back (round-relative), its ring index, (pos0 + WB) mod 65521
-        const uint32_t* ring32 = (const uint32_t*)ring;
         for (uint32_t n = 1;; ++n) {
             const bool fi = lds_get(&edone) == RS_EW;     // every group published: wf is the round's end
             lds_acquire();
-            const uint32_t Fv = lds_get(&wf);
+            const uint32_t Fv = RS_WF();
             const uint64_t ab = pos0 + WB;
             const uint32_t nk = 1024u - (uint32_t)(ab & 1023u);
             uint32_t m;
@@ -811,42 +1046,7 @@ __global__ __launch_bounds__(RS_THREADS) __attribute__((amdgpu_waves_per_eu(RS_W
                 continue;
             }
             n = 0;
-            const uint32_t h = (uint32_t)(ab & 3u);
-            const uint32_t gi0 = gm + 65521u - h;          // index of byte 0 of dword 0, mod 65521 (+ 65521)
-            if (m == 1024u) {
-                // a whole aligned KiB: 4 full dwords per lane, no edge bytes
-                uint32_t* dstw = (uint32_t*)(out + ab);
-#pragma unroll
-                for (uint32_t k = 0; k < 4; ++k) {
-                    const uint32_t q = lane + 64u * k;
-                    const uint32_t v = ring32[ridx((int32_t)Wr + 4 * (int32_t)q) >> 2];
-                    dstw[q] = v;
-                    if (!gz) {
-                        const uint32_t s4 = __builtin_amdgcn_udot4(v, 0x01010101u, 0u, false);
-                        accS += s4;
-                        accT += (uint64_t)(gi0 + 4 * q) * s4 + __builtin_amdgcn_udot4(v, 0x03020100u, 0u, false);
-                    }
-                }
-            } else {
-                const uint32_t nq = (uint32_t)(((ab + m + 3u) >> 2) - (ab >> 2));
-                uint32_t* dstw = (uint32_t*)(out + (ab - h));
-                const int32_t rb0 = (int32_t)Wr - (int32_t)h;  // ring index of the first dword (4-aligned)
-                const uint32_t tl = (uint32_t)((ab + m) & 3u);
-                for (uint32_t q = lane; q < nq; q += 64) {
-                    const uint32_t v = ring32[ridx(rb0 + 4 * (int32_t)q) >> 2];
-                    const uint32_t blo = q == 0 ? h : 0u;
-                    const uint32_t bhi = q + 1 < nq || tl == 0 ? 4u : tl;
-                    if (blo == 0 && bhi == 4) dstw[q] = v;
-                    else for (uint32_t bb = blo; bb < bhi; ++bb) ((uint8_t*)(dstw + q))[bb] = (uint8_t)(v >> (8 * bb));
-                    if (!gz) {
-                        const uint32_t mk = (bhi == 4u ? ~0u : (1u << (8 * bhi)) - 1u) & (~0u << (8 * blo));
-                        const uint32_t vm = v & mk;
-                        const uint32_t s4 = __builtin_amdgcn_udot4(vm, 0x01010101u, 0u, false);
-                        accS += s4;
-                        accT += (uint64_t)(gi0 + 4 * q) * s4 + __builtin_amdgcn_udot4(vm, 0x03020100u, 0u, false);
-                    }
-                }
-            }
+            rs_write_chunk(out, ring32, gz, ab, m, Wr, gm, accS, accT);
             WB += m;
             Wr += m;
             Wr -= Wr >= RS_R ? RS_R : 0u;
@@ -859,7 +1059,8 @@ __global__ __launch_bounds__(RS_THREADS) __attribute__((amdgpu_waves_per_eu(RS_W
     }
     if (timed) for (int k = 0; k < 8; ++k) atomicAdd(&A.dbg[k], tacc[k]);
 
-    resolve_finish<RS_R, RS_WAVES>(A, round, sid, flag, fin0, gz, pos0, 0, &chain, &fail, ring, accS, accT, &red[0][0]);
+    // (the adler partials' reduction reuses the finality map, which no one reads any more)
+    resolve_finish<RS_R, RS_WAVES>(A, round, sid, flag, fin0, gz, pos0, 0, &chain, &fail, ring, accS, accT, (uint64_t*)fmap);
 }
 
 // ------------------------------------------------------------------ block-synchronous resolve
@@ -1356,7 +1557,7 @@ __global__ __launch_bounds__(64) void k_inflate_finalize(InflateArgs A, uint64_t
 }
 
 uint32_t resolve_block_threads() { return RS_THREADS; }
-static_assert(RS_THREADS == RB_THREADS, "both resolve kernels run one workgroup of the same size per stream");
+uint32_t resolve_streams_per_block() { return 1; }
 // SDZ_RESOLVE=1 (read at each launch, so tests can switch it): the batch pipeline
 // (k_inflate_resolve_b); default: the group pipeline (k_inflate_resolve), faster on
 // every bench shape measured
@@ -1368,7 +1569,6 @@ void launch_inflate_resolve(const InflateArgs& a, uint32_t round, dim3 grid, hip
     if (resolve_batches()) hipLaunchKernelGGL(k_inflate_resolve_b, grid, dim3(RB_THREADS), 0, s, a, round);
     else hipLaunchKernelGGL(k_inflate_resolve, grid, dim3(RS_THREADS), 0, s, a, round);
 }
-uint32_t resolve_streams_per_block() { return 1; }
 // parts: scratch for the chunk crcs (a.tokens: the token rings are free once the rounds are
 // done; >= 1024 entries per stream); chunks of >= 256 KiB, <= 1024 per stream and <= 4 Mi
 // blocks in all
