@@ -1226,13 +1226,23 @@ __global__ __launch_bounds__(64 * CH_WAVES) void k_dfl_chain(DeflateArgs A) {
 #endif
 #define PM_WINB (W_SIZE + PM_SEG + PM_TAIL + MAX_MATCH + 16)   // staged window bytes (+ the last positions'
 #define PM_PV (W_SIZE + PM_SEG + PM_TAIL)                         // staged links      ... in a last segment)
-// record word of position p: the full-chain result (len << 16 | dist) in the low half, the
-// quarter-chain result in the high half, and input byte p - 1 (the literal the parse emits
-// from there) in bits 25-31 of the low half and bit 25 of the high half: the parse then
-// needs one load per step
-__device__ __forceinline__ uint64_t rec_word(uint32_t full, uint32_t quarter, uint32_t lb) {
-    return ((uint64_t)(quarter | ((lb >> 7) << 25)) << 32) | (full | ((lb & 127u) << 25));
+// Match records: one u32 per position p, at u32 index rp0 + p of the record buffer (8 bytes per
+// position are allocated): the full-chain result -- distance in bits 0-14 (0: no match), length - 3
+// in bits 15-22 --, bit 23 set when the quarter-chain result (deflate.ts:836-838, prev_length >=
+// good_match) differs, and input byte p - 1 (the literal the parse emits from there) in bits
+// 24-31.  A differing quarter result is the u32 at qoff + rp0 + p (same low 23 bits; qoff: the
+// batch's positions, or a Deflater's record capacity).  The parse reads one word per step, and the
+// quarter word only on the steps that use it and where it differs (4 bytes per position each way
+// instead of 8).  The symbols later go to u32 rp0 + k, over records already read.
+__device__ __forceinline__ uint32_t rc_res(uint32_t len, uint32_t dist) {    // a search's result (len >= 3)
+    return dist | ((len - MIN_MATCH) << 15);
 }
+__device__ __forceinline__ uint32_t rc_len(uint32_t e) { return (e & 0x7fffu) ? ((e >> 15) & 255u) + MIN_MATCH : 0u; }
+__device__ __forceinline__ uint32_t rc_word(uint32_t full, uint32_t quarter, uint32_t lb) {
+    return full | (quarter != full ? 1u << 23 : 0u) | (lb << 24);
+}
+// (len << 16 | dist, 0: none -- the search functions' form) as a result word
+__device__ __forceinline__ uint32_t rc_from16(uint32_t w) { return (w >> 16) >= MIN_MATCH ? rc_res(w >> 16, w & 0xffffu) : 0u; }
 __device__ __forceinline__ uint32_t pm_w4(const uint8_t* w, uint32_t x) {   // 4 bytes at x, aligned reads
     const uint32_t* w32 = (const uint32_t*)w;
     return __builtin_amdgcn_alignbyte(w32[(x >> 2) + 1], w32[x >> 2], x & 3u);
@@ -1346,7 +1356,8 @@ __global__ __launch_bounds__(PM_THREADS) void k_dfl_match(DeflateArgs A) {
         if (tid == 0) pm_next = s0 + (PM_THREADS / 64) * PM_CHUNK;
     }
     __syncthreads();
-    GLB uint64_t* rec = (GLB uint64_t*)A.rec_buf + rp;
+    GLB uint32_t* rec = (GLB uint32_t*)A.rec_buf + rp;
+    GLB uint32_t* qrec = (GLB uint32_t*)A.rec_buf + A.qoff + rp;   // the differing quarter results
     const int max_chain = c_config[A.level][3], qchain = max_chain >> 2, nice0 = c_config[A.level][2];
     int nice = nice0;                                       // (a last position: at most its lookahead)
     // Positions in chunks of PM_CHUNK: each wave starts on its own chunk and takes the next
@@ -1387,9 +1398,10 @@ __global__ __launch_bounds__(PM_THREADS) void k_dfl_match(DeflateArgs A) {
         if (nidle >= PM_REFILL || nidle == 64) {
             if (pend) {
                 if (qbest < 0) { qbest = best; qpos = bpos; }
-                const uint32_t full = best > MIN_MATCH - 1 ? ((uint32_t)best << 16) | (uint32_t)(sp - bpos) : 0u;
-                const uint32_t quarter = qbest > MIN_MATCH - 1 ? ((uint32_t)qbest << 16) | (uint32_t)(sp - qpos) : 0u;
-                rec[p] = rec_word(full, quarter, win[p > 0 ? sp - 1 : 0]);
+                const uint32_t full = best > MIN_MATCH - 1 ? rc_res((uint32_t)best, (uint32_t)(sp - bpos)) : 0u;
+                const uint32_t quarter = qbest > MIN_MATCH - 1 ? rc_res((uint32_t)qbest, (uint32_t)(sp - qpos)) : 0u;
+                rec[p] = rc_word(full, quarter, win[p > 0 ? sp - 1 : 0]);
+                if (quarter != full) qrec[p] = quarter;
                 pend = false;
             }
             if (next >= q1) {                               // chunk handed out: take another
@@ -1675,10 +1687,12 @@ __global__ __launch_bounds__(PM_THREADS) void k_dfl_match(DeflateArgs A) {
 //                (with their gaps) in LDS.
 // Both chain lengths come from one walk as in k_dfl_match (the quarter window is ranks <= K/4).
 // Link word: (gap - 1) << 16 | distance, 0 if none (k_dfl_match4 stages it packed, m4_pack).
-// the record (k_dfl_match's word) of a search whose best is the 3-byte entry f3 (k_dfl_link4)
-__device__ __forceinline__ uint64_t m4_rec3(uint32_t f3, uint32_t lb) {
-    const uint32_t d = f3 & 0x7fffu, w = d ? (3u << 16) | d : 0u;
-    return rec_word(w, (f3 & 0x8000u) ? w : 0u, lb);
+// the record (k_dfl_match's word) of a search whose best is the 3-byte entry f3 (k_dfl_link4); the
+// quarter word is written for every position here (k_dfl_match4 reads it back)
+__device__ __forceinline__ void m4_rec3(GLB uint32_t* rec, GLB uint32_t* qrec, int p, uint32_t f3, uint32_t lb) {
+    const uint32_t d = f3 & 0x7fffu, w = d ? rc_res(3u, d) : 0u, q = (f3 & 0x8000u) ? w : 0u;
+    rec[p] = rc_word(w, q, lb);
+    qrec[p] = q;
 }
 __global__ __launch_bounds__(PM_THREADS) void k_dfl_link4(DeflateArgs A) {
     __shared__ __attribute__((aligned(16))) uint8_t win[(PM_WINB + 15) & ~15];
@@ -1726,7 +1740,8 @@ __global__ __launch_bounds__(PM_THREADS) void k_dfl_link4(DeflateArgs A) {
     }
     __syncthreads();
     GLB uint32_t* l4 = (GLB uint32_t*)A.l4_buf + rp;
-    GLB uint64_t* rec = (GLB uint64_t*)A.rec_buf + rp;
+    GLB uint32_t* rec = (GLB uint32_t*)A.rec_buf + rp;
+    GLB uint32_t* qrec = (GLB uint32_t*)A.rec_buf + A.qoff + rp;
     const int K = c_config[A.level][3], Kq = K >> 2;
     // Each lane walks one position at a time and takes the next from an LDS counter itself,
     // one step ahead: its first link and 4 bytes are read in the step after the take, beside
@@ -1761,7 +1776,7 @@ __global__ __launch_bounds__(PM_THREADS) void k_dfl_link4(DeflateArgs A) {
             ++r;
             if (fin) {
                 l4[sp + ws] = res;
-                rec[sp + ws] = m4_rec3(f3, win[sp + ws > 0 ? sp - 1 : 0]);
+                m4_rec3(rec, qrec, sp + ws, f3, win[sp + ws > 0 ? sp - 1 : 0]);
                 busy = false;
             }
         }
@@ -1773,7 +1788,7 @@ __global__ __launch_bounds__(PM_THREADS) void k_dfl_link4(DeflateArgs A) {
             res = 0; f3 = 0; r = 1;
             limit = (np > MAX_DIST ? np - MAX_DIST : 0) - ws;
             busy = cur != 0 && sp - cur <= MAX_DIST;      // the first entry (deflate.ts:1092)
-            if (!busy) { l4[np] = 0u; rec[np] = m4_rec3(0u, win[np > 0 ? sp - 1 : 0]); }
+            if (!busy) { l4[np] = 0u; m4_rec3(rec, qrec, np, 0u, win[np > 0 ? sp - 1 : 0]); }
             stg = 0;
         }
         if (stg == 0) {
@@ -1828,7 +1843,7 @@ __device__ __forceinline__ int m4_lcp16(uint32_t x0, uint32_t x1, uint32_t x2, u
 // k_dfl_match4's walks (kHbm: the escape table overflowed, some link words stay in HBM)
 template <bool kHbm>
 __device__ __forceinline__ void m4_walks(const uint8_t* win, const uint16_t* lk, const uint32_t* esc,
-                                         const GLB uint32_t* l4g, GLB uint64_t* rec, int* pm_next, int ws, int s1,
+                                         const GLB uint32_t* l4g, GLB uint32_t* rec, GLB uint32_t* qrec, int* pm_next, int ws, int s1,
                                          int K, int Kq, int nice, unsigned long long* dbg, uint32_t lane) {
     // Each lane runs M4_WALKERS walks side by side (their LDS round trips overlap) and takes
     // the next position from an LDS counter itself, one step ahead (as k_dfl_link4): the taken
@@ -1913,11 +1928,16 @@ __device__ __forceinline__ void m4_walks(const uint8_t* win, const uint16_t* lk,
 #pragma unroll
         for (int k = 0; k < W; ++k) {
             if (!busy[k] && sp[k] >= 0) {                    // a walk ended: the halves it improves
-                // (k_dfl_link4 wrote the record of the 3-byte entry; rec_word's layout)
-                const uint32_t lb = win[sp[k] + ws > 0 ? sp[k] - 1 : 0];
-                GLB uint32_t* r32 = (GLB uint32_t*)(rec + sp[k] + ws);
-                if (best[k] >= 4) r32[0] = ((uint32_t)best[k] << 16 | (uint32_t)(sp[k] - bpos[k])) | ((lb & 127u) << 25);
-                if (qbest[k] >= 4) r32[1] = ((uint32_t)qbest[k] << 16 | (uint32_t)(sp[k] - qpos[k])) | ((lb >> 7) << 25);
+                // (k_dfl_link4 wrote the record of the 3-byte entry, and its quarter word)
+                if (best[k] >= 4 || qbest[k] >= 4) {
+                    const int pp = sp[k] + ws;
+                    const uint32_t lb = win[pp > 0 ? sp[k] - 1 : 0];
+                    const uint32_t o = rec[pp], oq = qrec[pp];
+                    const uint32_t full = best[k] >= 4 ? rc_res((uint32_t)best[k], (uint32_t)(sp[k] - bpos[k])) : o & 0x7fffffu;
+                    const uint32_t quarter = qbest[k] >= 4 ? rc_res((uint32_t)qbest[k], (uint32_t)(sp[k] - qpos[k])) : oq;
+                    rec[pp] = rc_word(full, quarter, lb);
+                    qrec[pp] = quarter;
+                }
                 sp[k] = -1;
             }
             if (sp[k] < 0 && stg == 2) {                     // start the taken position
@@ -1992,10 +2012,11 @@ __global__ __launch_bounds__(PM_THREADS) void k_dfl_match4(DeflateArgs A) {
         if (tid == 0) pm_next = s0;
     }
     __syncthreads();
-    GLB uint64_t* rec = (GLB uint64_t*)A.rec_buf + rp;
+    GLB uint32_t* rec = (GLB uint32_t*)A.rec_buf + rp;
+    GLB uint32_t* qrec = (GLB uint32_t*)A.rec_buf + A.qoff + rp;
     const int K = c_config[A.level][3], Kq = K >> 2, nice = c_config[A.level][2];
-    if (esc_n > M4_ESC) m4_walks<true>(win, lk, esc, l4g, rec, &pm_next, ws, s1, K, Kq, nice, A.dbg, lane);
-    else m4_walks<false>(win, lk, esc, l4g, rec, &pm_next, ws, s1, K, Kq, nice, A.dbg, lane);
+    if (esc_n > M4_ESC) m4_walks<true>(win, lk, esc, l4g, rec, qrec, &pm_next, ws, s1, K, Kq, nice, A.dbg, lane);
+    else m4_walks<false>(win, lk, esc, l4g, rec, qrec, &pm_next, ws, s1, K, Kq, nice, A.dbg, lane);
 }
 
 // ------------------------------------------------------------------ record path: tail, parse, trees, encode
@@ -2118,7 +2139,8 @@ __global__ __launch_bounds__(256) void k_dfl_tail(DeflateArgs A) {
     const int64_t n = (int64_t)A.in_len[sid], tail = n > PM_TAIL ? n - PM_TAIL : 0;
     const GLB uint8_t* in = (const GLB uint8_t*)(A.in + A.in_off[sid]);
     const GLB uint16_t* pv = (const GLB uint16_t*)A.pv_buf + rp;
-    GLB uint64_t* rec = (GLB uint64_t*)A.rec_buf + rp;
+    GLB uint32_t* rec = (GLB uint32_t*)A.rec_buf + rp;
+    GLB uint32_t* qrec = (GLB uint32_t*)A.rec_buf + A.qoff + rp;
     const int max_chain = c_config[A.level][3], nice = c_config[A.level][2];
     // with A.tail_in_match, k_dfl_match searched the larger window-offset group already (a stream
     // with match segments, tail > 0); the last MIN_MATCH - 1 positions are not searched, their
@@ -2128,7 +2150,9 @@ __global__ __launch_bounds__(256) void k_dfl_tail(DeflateArgs A) {
     for (int64_t P = tail + (int64_t)threadIdx.x; P < n; P += 256) {
         if (P >= tg.mlo && P < tg.mhi) continue;
         const uint64_t r = P <= n - MIN_MATCH ? tail_search(in, pv, n, P, max_chain, nice) : 0ull;
-        rec[P] = rec_word((uint32_t)r, (uint32_t)(r >> 32), in[P > 0 ? P - 1 : 0]);
+        const uint32_t full = rc_from16((uint32_t)r), quarter = rc_from16((uint32_t)(r >> 32));
+        rec[P] = rc_word(full, quarter, in[P > 0 ? P - 1 : 0]);
+        if (quarter != full) qrec[P] = quarter;
     }
 }
 
@@ -2166,7 +2190,7 @@ __device__ __forceinline__ void ps_init(PState& st, const DeflateArgs& A, uint32
     st.strstart = 0; st.match_length = MIN_MATCH - 1; st.match_start = 0; st.match_available = 0;
     st.block_start = 0; st.off = 0;
     st.last_lit = 0; st.matches = 0; st.lx = 0; st.nblk = 0; st.sym0 = 0; st.dxb = 0;
-    st.sym = (GLB uint32_t*)A.sym_buf + 2 * A.rp0[sid];
+    st.sym = (GLB uint32_t*)A.sym_buf + A.rp0[sid];
     st.stg = nullptr;
     st.blk = A.blk + (uint64_t)A.tb0[sid] * FB_SLOT;
     st.nbcap = A.tb0[sid + 1] - A.tb0[sid];
@@ -2184,7 +2208,7 @@ __device__ __forceinline__ bool ps_tally(PState& st, int dist, int lc) {      //
         st.stg[st.lx & (PS_STG - 1u)] = v;
         if ((++st.lx & (PS_STG - 1u)) == 0) {
             const uint2* q = (const uint2*)st.stg;
-            uint2* d = (uint2*)(uint32_t*)(st.sym + st.lx - PS_STG);   // (8-byte aligned: rp0 * 8 bytes)
+            uint2* d = (uint2*)(uint32_t*)(st.sym + st.lx - PS_STG);   // (8-byte aligned: rp0 is a multiple of 64)
 #pragma unroll
             for (int k = 0; k < PS_STG / 2; ++k) d[k] = q[k];
         }
@@ -2225,9 +2249,13 @@ __device__ __forceinline__ bool ps_fill(PState& st) {
     }
     return false;
 }
-// one step at position strstart with its record r (rec_word) and the literal byte lb
-__device__ __forceinline__ void ps_step(PState& st, uint64_t r) {
-    const uint32_t lb = ((uint32_t)r >> 25) | (((uint32_t)(r >> 32) >> 18) & 128u);
+// one step at position strstart with its record r (rc_word) and, when prev_length >= good_match,
+// the quarter word q there (ps_qload: loaded beside the record, not after it)
+__device__ __forceinline__ uint32_t ps_qload(const PState& st, const GLB uint32_t* qrec) {
+    return st.match_length >= st.good ? qrec[st.strstart] : 0u;
+}
+__device__ __forceinline__ void ps_step(PState& st, uint32_t r, uint32_t q) {
+    const uint32_t lb = r >> 24;
     const int lookahead = st.n - st.strstart;
     const int prev_length = st.match_length, prev_match = st.match_start;
     st.match_length = MIN_MATCH - 1;
@@ -2237,10 +2265,10 @@ __device__ __forceinline__ void ps_step(PState& st, uint64_t r) {
     // ends <= prev_length, so with prev_length >= MIN_MATCH the previous match is emitted
     // either way, and otherwise it stays MIN_MATCH - 1.  So the link load is not needed.
     if (lookahead >= MIN_MATCH && prev_length < st.max_lazy) {
-        const uint32_t e = prev_length >= st.good ? (uint32_t)(r >> 32) : (uint32_t)r;
-        const int len = (int)((e >> 16) & 511u);
+        const uint32_t e = prev_length >= st.good && (r & (1u << 23)) ? q : r;
+        const int len = (int)rc_len(e);
         int ml = prev_length;
-        if (len > prev_length) { ml = len; st.match_start = st.strstart - (int)(e & 0xffffu); }
+        if (len > prev_length) { ml = len; st.match_start = st.strstart - (int)(e & 0x7fffu); }
         st.match_length = ml < lookahead ? ml : lookahead;
         if (st.match_length <= 5 && st.match_length == MIN_MATCH && st.strstart - st.match_start > 4096)
             st.match_length = MIN_MATCH - 1;
@@ -2279,16 +2307,18 @@ __global__ __launch_bounds__(64) void k_dfl_parse(DeflateArgs A) {
     const uint64_t in_len = A.in_len[sid];
     if (in_len == 0 || A.rp0[sid] == ~0ull) { F->nblk = 0; F->flag = 1; return; }
     const GLB uint8_t* in = (const GLB uint8_t*)(A.in + A.in_off[sid]);
-    const GLB uint64_t* rec = (const GLB uint64_t*)A.rec_buf + A.rp0[sid];
+    const GLB uint32_t* rec = (const GLB uint32_t*)A.rec_buf + A.rp0[sid];
+    const GLB uint32_t* qrec = (const GLB uint32_t*)A.rec_buf + A.qoff + A.rp0[sid];
     __shared__ __attribute__((aligned(16))) uint32_t stage[64 * PS_STG];
     PState st;
     ps_init(st, A, sid, (int)in_len);
     st.stg = stage + lane * PS_STG;
     for (;;) {
         if (ps_fill(st)) break;
-        uint64_t r = rec[st.strstart];                        // the step's one load (rec_word)
-        asm volatile("" : "+v"(r));                           // here, not sunk into the branches
-        ps_step(st, r);
+        uint32_t r = rec[st.strstart];                        // the step's one load (rc_word) ...
+        uint32_t q = ps_qload(st, qrec);                      // ... and beside it the quarter word it may use
+        asm volatile("" : "+v"(r), "+v"(q));                  // here, not sunk into the branches
+        ps_step(st, r, q);
     }
     ps_finish(st, in, F);
 }
@@ -2306,7 +2336,7 @@ __global__ __launch_bounds__(64) void k_dfl_parse(DeflateArgs A) {
 #define PW_T(k) do { } while (0)
 #endif
 __global__ __launch_bounds__(PW_THREADS) void k_dfl_parse_wide(DeflateArgs A) {
-    __shared__ uint64_t buf[2][PW_CHUNK];
+    __shared__ uint32_t buf[2][PW_CHUNK];
     const uint32_t sid = blockIdx.x, tid = threadIdx.x;
 #ifdef DT_PROF
     uint64_t tw[6] = {};
@@ -2319,7 +2349,8 @@ __global__ __launch_bounds__(PW_THREADS) void k_dfl_parse_wide(DeflateArgs A) {
     if (in_len == 0 || A.rp0[sid] == ~0ull) { if (tid == 0) { F->nblk = 0; F->flag = 1; } return; }
     const int n = (int)in_len;
     const GLB uint8_t* in = (const GLB uint8_t*)(A.in + A.in_off[sid]);
-    const GLB uint64_t* rec = (const GLB uint64_t*)A.rec_buf + A.rp0[sid];
+    const GLB uint32_t* rec = (const GLB uint32_t*)A.rec_buf + A.rp0[sid];
+    const GLB uint32_t* qrec = (const GLB uint32_t*)A.rec_buf + A.qoff + A.rp0[sid];
     const int nch = (n + PW_CHUNK - 1) / PW_CHUNK;
     for (int i = (int)tid; i < PW_CHUNK && i < n; i += PW_THREADS) buf[0][i] = rec[i];
     __syncthreads();
@@ -2344,12 +2375,12 @@ __global__ __launch_bounds__(PW_THREADS) void k_dfl_parse_wide(DeflateArgs A) {
         }
         if (parser && !done) {
             const int end = (c + 1) * PW_CHUNK, b0 = c * PW_CHUNK;
-            const uint64_t* cb = buf[c & 1];
+            const uint32_t* cb = buf[c & 1];
 #if PW_UNIFORM
             // the records of positions rb .. rb + 63 in lane order (one LDS read per 64
             // positions); a step takes its record with readlane instead of waiting on LDS
             int rb = -(1 << 30);
-            uint32_t rlo = 0, rhi = 0;
+            uint32_t rlo = 0;
 #endif
             for (;;) {
                 if (st.strstart >= end) break;             // the next chunk (a step moves <= MAX_MATCH)
@@ -2360,16 +2391,13 @@ __global__ __launch_bounds__(PW_THREADS) void k_dfl_parse_wide(DeflateArgs A) {
                     rb = st.strstart;
                     o = 0;
                     const int i = rb - b0 + (int)tid;
-                    const uint64_t v = i < PW_CHUNK ? cb[i] : 0ull;
-                    rlo = (uint32_t)v;
-                    rhi = (uint32_t)(v >> 32);
+                    rlo = i < PW_CHUNK ? cb[i] : 0u;
                 }
-                const uint64_t r = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)rlo, o) |
-                                   ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)rhi, o) << 32);
+                const uint32_t r = (uint32_t)__builtin_amdgcn_readlane((int)rlo, o);
 #else
-                const uint64_t r = cb[st.strstart - b0];
+                const uint32_t r = cb[st.strstart - b0];
 #endif
-                ps_step(st, r);
+                ps_step(st, r, ps_qload(st, qrec));
             }
         }
         __syncthreads();
@@ -2430,15 +2458,15 @@ __device__ __forceinline__ LzSt lz_load(uint64_t v) {
 }
 // one step of deflate_slow at t.s with the record r there (as ps_step); returns the symbol
 // it emits (LZ_SYM set) or 0
-__device__ __forceinline__ uint32_t lz_step(LzSt& t, uint64_t r, int n, int good, int max_lazy) {
+__device__ __forceinline__ uint32_t lz_step(LzSt& t, uint32_t r, const GLB uint32_t* qrec, int n, int good, int max_lazy) {
     const int lookahead = n - t.s;
     const int prev_length = t.ml, prev_match = t.ms;
     int ml = MIN_MATCH - 1, ms = t.ms;
     if (lookahead >= MIN_MATCH && prev_length < max_lazy) {
-        const uint32_t e = prev_length >= good ? (uint32_t)(r >> 32) : (uint32_t)r;
-        const int len = (int)((e >> 16) & 511u);
+        const uint32_t e = prev_length >= good && (r & (1u << 23)) ? qrec[t.s] : r;
+        const int len = (int)rc_len(e);
         ml = prev_length;
-        if (len > prev_length) { ml = len; ms = t.s - (int)(e & 0xffffu); }
+        if (len > prev_length) { ml = len; ms = t.s - (int)(e & 0x7fffu); }
         ml = ml < lookahead ? ml : lookahead;
         if (ml == MIN_MATCH && t.s - ms > 4096) ml = MIN_MATCH - 1;           // TOO_FAR
     }
@@ -2448,7 +2476,7 @@ __device__ __forceinline__ uint32_t lz_step(LzSt& t, uint64_t r, int n, int good
         t.avail = 0; t.ml = MIN_MATCH - 1; t.ms = 0;
         return sym;
     }
-    const uint32_t lb = ((uint32_t)r >> 25) | (((uint32_t)(r >> 32) >> 18) & 128u);
+    const uint32_t lb = r >> 24;
     const uint32_t sym = t.avail ? (lb | LZ_SYM) : 0u;
     t.avail = 1; t.ml = ml; t.ms = ms;
     t.s += 1;
@@ -2476,17 +2504,18 @@ __global__ __launch_bounds__(LZ_THREADS) void k_lz_spec(DeflateArgs A) {
     if (seg >= A.nlseg) return;
     const LzSeg q = lz_seg(A, seg);
     const int good = c_config[A.level][0], max_lazy = c_config[A.level][1];
-    const GLB uint64_t* rec = (const GLB uint64_t*)A.rec_buf + q.rp;
+    const GLB uint32_t* rec = (const GLB uint32_t*)A.rec_buf + q.rp;
+    const GLB uint32_t* qrec = (const GLB uint32_t*)A.rec_buf + A.qoff + q.rp;
     GLB uint64_t* w = (GLB uint64_t*)A.lz_w + q.rp;
     GLB uint64_t* v1 = (GLB uint64_t*)A.lz_v1 + (q.rp >> 6);
     GLB uint64_t* e1 = (GLB uint64_t*)A.lz_e1 + (q.rp >> 6);
     LzSt t{q.g, MIN_MATCH - 1, 0, 0};
     uint64_t va = 0, ea = 0;
     int wc = q.g >> 6;
-    auto one = [&](int s, uint64_t r) {
+    auto one = [&](int s, uint32_t r) {
         for (; (s >> 6) != wc; ++wc) { v1[wc] = va; e1[wc] = ea; va = 0; ea = 0; }
         const uint32_t st = lz_pack(t);
-        const uint32_t sym = lz_step(t, r, q.n, good, max_lazy);
+        const uint32_t sym = lz_step(t, r, qrec, q.n, good, max_lazy);
         va |= 1ull << (s & 63);
         if (sym) ea |= 1ull << (s & 63);
         w[s] = (uint64_t)st | ((uint64_t)sym << 32);
@@ -2494,7 +2523,7 @@ __global__ __launch_bounds__(LZ_THREADS) void k_lz_spec(DeflateArgs A) {
     while (t.s < q.h) {
         // two records per round trip: a step moves on by one position except after a match
         const int s = t.s;
-        const uint64_t r0 = rec[s], r1 = rec[s + 1 < q.n ? s + 1 : s];
+        const uint32_t r0 = rec[s], r1 = rec[s + 1 < q.n ? s + 1 : s];
         one(s, r0);
         if (t.s == s + 1 && t.s < q.h) one(s + 1, r1);
     }
@@ -2506,7 +2535,8 @@ __global__ __launch_bounds__(LZ_THREADS) void k_lz_spec(DeflateArgs A) {
 // position, same state); returns that position, or q.h (t then is the state leaving the
 // segment).  Writes the symbols of its steps (lz_s2, lz_e2 words [g, returned position)).
 __device__ int lz_join_run(const DeflateArgs& A, const LzSeg& q, LzSt& t, int good, int max_lazy) {
-    const GLB uint64_t* rec = (const GLB uint64_t*)A.rec_buf + q.rp;
+    const GLB uint32_t* rec = (const GLB uint32_t*)A.rec_buf + q.rp;
+    const GLB uint32_t* qrec = (const GLB uint32_t*)A.rec_buf + A.qoff + q.rp;
     const GLB uint64_t* w = (const GLB uint64_t*)A.lz_w + q.rp;
     const GLB uint64_t* v1 = (const GLB uint64_t*)A.lz_v1 + (q.rp >> 6);
     GLB uint32_t* s2 = (GLB uint32_t*)A.lz_s2 + q.rp;
@@ -2521,9 +2551,9 @@ __device__ int lz_join_run(const DeflateArgs& A, const LzSeg& q, LzSt& t, int go
             for (; (s >> 6) != wc; ++wc) { e2[wc] = ea; ea = 0; }
             vw = v1[wc];
         }
-        const uint64_t r = rec[s];
+        const uint32_t r = rec[s];
         if (((vw >> (s & 63)) & 1ull) && (uint32_t)w[s] == lz_pack(t)) { c = s; break; }
-        const uint32_t sym = lz_step(t, r, q.n, good, max_lazy);
+        const uint32_t sym = lz_step(t, r, qrec, q.n, good, max_lazy);
         if (sym) { ea |= 1ull << (s & 63); s2[s] = sym; }
     }
     if (c > q.g)
@@ -2654,7 +2684,7 @@ __global__ __launch_bounds__(LZ_THREADS) void k_lz_emit(DeflateArgs A) {
     const GLB uint32_t* s2 = (const GLB uint32_t*)A.lz_s2 + q.rp;
     const GLB uint64_t* e1 = (const GLB uint64_t*)A.lz_e1 + (q.rp >> 6);
     const GLB uint64_t* e2 = (const GLB uint64_t*)A.lz_e2 + (q.rp >> 6);
-    GLB uint32_t* sym = (GLB uint32_t*)A.sym_buf + 2 * q.rp;
+    GLB uint32_t* sym = (GLB uint32_t*)A.sym_buf + q.rp;
     uint32_t o = A.lz_cnt[seg];
     for (int wi = q.g >> 6; wi <= ((q.h - 1) >> 6); ++wi) {
         const uint64_t m2 = lz_range(wi, q.g, c), m1 = lz_range(wi, c, q.h);
@@ -2730,7 +2760,7 @@ __global__ __launch_bounds__(NT) void k_lz_blocks_t(DeflateArgs A) {
     const int64_t plus = A.level >= 4 ? 1 : 0;
     const bool trunc = A.level > 2;
     const uint32_t fin = A.lz_fin[sid], nsym = fin >> 1, nchk = nsym - (fin & 1u);
-    const GLB uint32_t* sym = (const GLB uint32_t*)A.sym_buf + 2 * A.rp0[sid];
+    const GLB uint32_t* sym = (const GLB uint32_t*)A.sym_buf + A.rp0[sid];
     GLB uint8_t* slots = (GLB uint8_t*)(A.blk + (uint64_t)A.tb0[sid] * FB_SLOT);
     const uint32_t nbcap = A.tb0[sid + 1] - A.tb0[sid];
     uint32_t nb = 0, b0 = 0;
@@ -2922,7 +2952,7 @@ __global__ __launch_bounds__(256) void k_fz_match(DeflateArgs A) {
     const GLB uint8_t* in = (const GLB uint8_t*)(A.in + A.in_off[q.k]);
     const GLB uint16_t* pv = (const GLB uint16_t*)A.pv_buf + q.rp;
     const GLB uint64_t* I = (const GLB uint64_t*)A.lz_i + (q.rp >> 6);
-    GLB uint64_t* rec = (GLB uint64_t*)A.rec_buf + q.rp;
+    GLB uint32_t* rec = (GLB uint32_t*)A.rec_buf + q.rp;       // (the slow levels' layout: u32 at rp0 + p)
     const int nice = c_config[A.level][2], chain = c_config[A.level][3];
     for (int p = q.g + (int)threadIdx.x; p < q.h; p += (int)blockDim.x) {
         uint32_t r = 0;
@@ -2955,7 +2985,7 @@ __global__ __launch_bounds__(LZ_THREADS) void k_fz_spec(DeflateArgs A) {
     const LzSeg q = lz_seg(A, seg);
     if (!(A.lz_act[q.k] & 1u) || A.fz_rc[seg] != A.lz_round) return;
     const GLB uint8_t* in = (const GLB uint8_t*)(A.in + A.in_off[q.k]);
-    const GLB uint64_t* rec = (const GLB uint64_t*)A.rec_buf + q.rp;
+    const GLB uint32_t* rec = (const GLB uint32_t*)A.rec_buf + q.rp;
     GLB uint64_t* w = (GLB uint64_t*)A.lz_w + q.rp;
     const int max_ins = c_config[A.level][1];
     BitW V{(GLB uint64_t*)A.lz_v1 + (q.rp >> 6), q.g >> 6, 0};
@@ -2970,10 +3000,10 @@ __global__ __launch_bounds__(LZ_THREADS) void k_fz_spec(DeflateArgs A) {
         if (p - wb0 >= 4) {
             wb0 = p;
             const int last = q.n - 1;
-            r0 = (uint32_t)rec[p];
-            r1 = (uint32_t)rec[p + 1 < last ? p + 1 : last];
-            r2 = (uint32_t)rec[p + 2 < last ? p + 2 : last];
-            r3 = (uint32_t)rec[p + 3 < last ? p + 3 : last];
+            r0 = rec[p];
+            r1 = rec[p + 1 < last ? p + 1 : last];
+            r2 = rec[p + 2 < last ? p + 2 : last];
+            r3 = rec[p + 3 < last ? p + 3 : last];
             if (p + 4 <= q.n) __builtin_memcpy(&lw, (const uint8_t*)(in + p), 4);
             else {
                 lw = 0;
@@ -2998,7 +3028,7 @@ __global__ __launch_bounds__(LZ_THREADS) void k_fz_spec(DeflateArgs A) {
 // match crossing in (inserted iff cin).  Returns the meeting position or q.h.
 __device__ int fz_join_run(const DeflateArgs& A, const LzSeg& q, int& s, bool& cin, int max_ins) {
     const GLB uint8_t* in = (const GLB uint8_t*)(A.in + A.in_off[q.k]);
-    const GLB uint64_t* rec = (const GLB uint64_t*)A.rec_buf + q.rp;
+    const GLB uint32_t* rec = (const GLB uint32_t*)A.rec_buf + q.rp;
     const GLB uint64_t* v1 = (const GLB uint64_t*)A.lz_v1 + (q.rp >> 6);
     GLB uint32_t* s2 = (GLB uint32_t*)A.lz_s2 + q.rp;
     BitW E{(GLB uint64_t*)A.lz_e2 + (q.rp >> 6), q.g >> 6, 0};
@@ -3011,7 +3041,7 @@ __device__ int fz_join_run(const DeflateArgs& A, const LzSeg& q, int& s, bool& c
         if ((s >> 6) != vwc) { vwc = s >> 6; vw = v1[vwc]; }
         if ((vw >> (s & 63)) & 1ull) { c = s; break; }
         const int p = s;
-        const uint32_t r = (uint32_t)rec[p];
+        const uint32_t r = rec[p];
         E.set(p);
         s2[p] = fz_step(s, r, in[p], q.n, max_ins, I, cin);
     }
@@ -3615,7 +3645,7 @@ __global__ __launch_bounds__(64) void k_dfl_trees(DeflateArgs A) {
     if (lane < 30) s_xd[lane] = T->extra_dbits[lane];
     if (lane < 19) s_xbl[lane] = T->extra_blbits[lane];
     if (flag) return;
-    const GLB uint32_t* sym = (const GLB uint32_t*)A.sym_buf + 2 * rp0;
+    const GLB uint32_t* sym = (const GLB uint32_t*)A.sym_buf + rp0;
     for (uint32_t b = blockIdx.y; b < nblk; b += gridDim.y) {
         GLB FBlock* Bk = (GLB FBlock*)(A.blk + (tb0 + b) * FB_SLOT);
         const uint32_t sym0 = Bk->sym0, nsym = Bk->nsym, eof = Bk->eof;
@@ -3760,7 +3790,7 @@ __global__ __launch_bounds__(64) void k_dfl_trees(DeflateArgs A) {   // grid (n,
     const GLB DTables* T = (const GLB DTables*)&g_dt;
     for (int i = (int)lane; i < 256; i += 64) lcode_t[i] = T->length_code[i];
     for (int i = (int)lane; i < 512; i += 64) dcode_t[i] = T->dist_code[i];
-    const GLB uint32_t* sym = (const GLB uint32_t*)A.sym_buf + 2 * A.rp0[sid];
+    const GLB uint32_t* sym = (const GLB uint32_t*)A.sym_buf + A.rp0[sid];
     const uint32_t nblk = F->nblk;
     for (uint32_t b = blockIdx.y; b < nblk; b += gridDim.y) {
         GLB FBlock* Bk = (GLB FBlock*)(A.blk + ((uint64_t)A.tb0[sid] + b) * FB_SLOT);
@@ -4010,7 +4040,7 @@ __global__ __launch_bounds__(NT) void k_dfl_encode_t(DeflateArgs A) {
             for (uint32_t i = 0; i < A.fname_len; i++) orbits(80 + 8 * i, A.fname[i]);
         }
     }
-    const GLB uint32_t* sym = (const GLB uint32_t*)A.sym_buf + 2 * A.rp0[sid];
+    const GLB uint32_t* sym = (const GLB uint32_t*)A.sym_buf + A.rp0[sid];
     uint32_t bad = 0;
     for (uint32_t b = 0; b < nblk; ++b) {
         const GLB FBlock* Bk = blk_at(b);

@@ -34,6 +34,7 @@ struct DeflateExt {
     uint64_t* rec;
     uint16_t* pv;
     uint64_t rec_from, pv_from;
+    uint64_t rec_cap;                 // positions the record buffer holds (its quarter words start there)
 };
 // sdz_deflate_batch_device with the input lengths optionally known on the host
 int deflate_batch_device(const uint8_t* in, const uint64_t* in_off, const uint64_t* in_len, uint8_t* out,

@@ -129,11 +129,12 @@ struct DeflateArgs {
     // owns positions [rp0[k], rp0[k] + in_len) of the record and link buffers (rp0[k] = ~0: not
     // on the record path) and block slots [tb0[k], tb0[k + 1]); the match and chain kernels
     // run over work-unit lists (k << kRecUnitShift | unit)
-    uint64_t* rec_buf;           // match records, one per position (null: classic path only)
+    uint64_t* rec_buf;           // match records, a u32 per position at rp0[k] + p (null: classic path only)
+    uint64_t qoff;               // ... and the differing quarter-chain results at qoff + rp0[k] + p (u32 units)
     uint16_t* pv_buf;            // hash chain links: distance to the previous same-hash position
     uint32_t* l4_buf;            // levels 4-9 (null: k_dfl_match): per position the 4-byte chain link
                                  // and its rank in the hash chain (k_dfl_link4)
-    uint32_t* sym_buf;           // the parse's symbols, u32 index 2 rp0[k] (normally rec_buf itself:
+    uint32_t* sym_buf;           // the parse's symbols, u32 index rp0[k] (normally rec_buf itself:
                                  // records are dead once parsed; a Deflater keeps its records)
     const uint64_t* rp0;         // n + 1 entries
     const uint32_t* tb0;         // n + 1 entries

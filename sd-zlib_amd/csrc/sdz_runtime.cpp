@@ -120,6 +120,10 @@ int Pool::get(size_t bytes, hipStream_t s, void** out, Slot** slot) {
         S.cap = want;
     }
     if (S.pending) HIPCHK(hipStreamWaitEvent(s, S.ev, 0));
+    // SDZ_POISON=1 (development aid): every get() hands out its bytes as 0xA5, so a kernel that reads
+    // pool memory it has not written in this call reads the same wrong value from the first call on
+    static const bool poison = getenv("SDZ_POISON") && *getenv("SDZ_POISON") == '1';
+    if (poison) HIPCHK(hipMemsetAsync(S.p, 0xA5, bytes, s));
     *slot = &S;
     *out = S.p;
     return SDZ_API_OK;
@@ -391,6 +395,16 @@ int inflate_scratch(InflateArgs& a, uint32_t n, bool own_state, size_t extra, hi
         return inflate_scratch(a, n, own_state, extra, s, use, extra_out);
     }
     uint8_t* base = (uint8_t*)scratch;
+    // SDZ_POISON_SCRATCH=<bits> (development aid): parts of the layout handed out as 0xA5 bytes --
+    // 1 code-length scratch, 2 DSave, 4 RSave, 8 token rings, 16 ntok / flags / active, 32 wave slots
+    if (const char* e = getenv("SDZ_POISON_SCRATCH")) {
+        const unsigned bits = (unsigned)strtoul(e, nullptr, 0);
+        const size_t part[6][2] = { { 0, off_ds }, { off_ds, own_state ? (size_t)n * dsb : 0 },
+                                    { off_rs, own_state ? (size_t)n * rsb : 0 }, { off_tk, (size_t)n * T * 4 },
+                                    { off_nt, (size_t)n * 8 + 256 }, { off_wp, wdp ? (size_t)n * kWdProvTokens * 4 : 0 } };
+        for (int k = 0; k < 6; ++k)
+            if ((bits >> k) & 1u && part[k][1]) HIPCHK(hipMemsetAsync(base + part[k][0], 0xA5, part[k][1], s));
+    }
     a.scratch = base;
     if (own_state) { a.dsave = base + off_ds; a.rsave = base + off_rs; }
     a.tokens = (uint32_t*)(base + off_tk);
@@ -1153,10 +1167,12 @@ int rt::deflate_batch_device(const uint8_t* in, const uint64_t* in_off, const ui
             auto take = [&](size_t bytes) { uint8_t* p = B + o; o += (bytes + 255) & ~(size_t)255; return p; };
             if (ext) {                                    // a Deflater's own records and links
                 a.rec_buf = ext->rec;
+                a.qoff = ext->rec_cap;                    // (its quarter words sit past its capacity)
                 a.pv_buf = ext->pv;
                 a.sym_buf = (uint32_t*)take((size_t)pos * 8);
             } else {
                 a.rec_buf = (uint64_t*)take((size_t)pos * 8);
+                a.qoff = pos;                             // records [0, pos), quarter words [pos, 2 pos) (u32)
                 a.pv_buf = (uint16_t*)take((size_t)pos * 2);
                 a.sym_buf = (uint32_t*)a.rec_buf;
                 if (match4) a.l4_buf = (uint32_t*)take((size_t)pos * 4);
@@ -1701,8 +1717,10 @@ int deflater_record_call(sdz_deflater* z, const uint8_t* data, size_t len, int32
         uint16_t* l = nullptr;
         HIPCHK(hipMalloc(&r, c * 8));
         HIPCHK(hipMalloc(&l, c * 2 + 256));
-        if (z->recs_cap) {
-            HIPCHK(hipMemcpy(r, z->d_recs, z->recs_cap * 8, hipMemcpyDeviceToDevice));
+        if (z->recs_cap) {                            // records at [0, cap), quarter words at [cap, 2 cap) (u32)
+            HIPCHK(hipMemcpy(r, z->d_recs, z->recs_cap * 4, hipMemcpyDeviceToDevice));
+            HIPCHK(hipMemcpy((uint32_t*)r + c, (const uint32_t*)z->d_recs + z->recs_cap, z->recs_cap * 4,
+                             hipMemcpyDeviceToDevice));
             HIPCHK(hipMemcpy(l, z->d_links, z->recs_cap * 2, hipMemcpyDeviceToDevice));
         }
         if (z->d_recs) hipFree(z->d_recs);
@@ -1710,7 +1728,7 @@ int deflater_record_call(sdz_deflater* z, const uint8_t* data, size_t len, int32
         z->d_recs = r; z->d_links = l; z->recs_cap = c;
     }
     const uint64_t old = z->total;
-    rt::DeflateExt ext{ z->d_recs, z->d_links, old >= 262 ? old - 262 : 0, old >= 2 ? old - 2 : 0 };
+    rt::DeflateExt ext{ z->d_recs, z->d_links, old >= 262 ? old - 262 : 0, old >= 2 ? old - 2 : 0, z->recs_cap };
     int rc = rt::deflate_batch_device(z->d_all, z->d_meta, z->d_meta + 1, z->d_out, z->d_meta + 2, z->d_meta + 3,
                                       z->d_rec, 1, z->level, z->format, z->fname.empty() ? nullptr : z->fname.data(),
                                       (uint32_t)z->fname.size(), z->mtime, nullptr, 0, nullptr, &total,
