@@ -257,15 +257,22 @@ def mixed_leg(sdz, L, steps, scale, barrier, allmax, world, rank):
     caps = [len(plain[j]) + 64 for j in pick]
     slots = rc.Slots(pool, pick, caps)
 
+    split = []
+
     def step():
         a, b, c, d = slots.ptrs()
         if L.sdz_inflate_batch_device(slots.d_in.ptr, a, b, slots.d_out.ptr, c, d, slots.d_rec.ptr, slots.n,
                                       sdz.FMT_AUTO, None, 0, None):
             raise RuntimeError(L.sdz_last_error().decode())
-        return L.sdz_last_kernel_ms()
+        ms = L.sdz_last_kernel_ms()
+        f3 = (ctypes.c_float * 3)()                       # decode (incl. the split rounds) / resolve / finalize
+        L.sdz_last_kernel_breakdown(f3)
+        split.append(list(f3))
+        return ms
     step()
     L.sdz_sync(None)
     barrier()
+    split.clear()
     t0 = time.perf_counter()
     ks = [step() for _ in range(steps)]
     L.sdz_sync(None)
@@ -285,10 +292,27 @@ def mixed_leg(sdz, L, steps, scale, barrier, allmax, world, rank):
     total_out = sum(len(plain[j]) for pk in picks for j in pk)
     total_in = sum(len(pool[j]) for pk in picks for j in pk)
     kms = sum(ks) / len(ks)
+    kp = [sum(x[k] for x in split) / len(split) for k in range(3)]
+    alg = in_bytes + sum(len(plain[j]) for j in pick)      # one rank's launch: compressed in + plain out
+    mtraffic = None                                        # rocprofv3 PMC pass of this leg (tools/run_c2.py --mode mixed)
+    mp = sorted(glob.glob(os.path.join(ROOT, "profiles", "r[0-9][0-9]_mixed_pmc.json")))
+    if mp and world == 1 and scale == 8:
+        try:
+            mtraffic = json.load(open(mp[-1])).get("hbm_bytes_per_launch")
+        except Exception:
+            mtraffic = None
+    achieved = alg / kms / 1e6
     return {"value": round(total_out / wall / 1e6, 2), "unit": "MB/s", "ms_per_step": round(1000 * wall, 3),
             "kernel_ms": round(kms, 3),
-            "roofline": {"bound": "hbm", "achieved": round((in_bytes + sum(len(plain[j]) for j in pick)) / kms / 1e6, 2),
-                         "peak": 8000.0, "unit": "GB/s"},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": mtraffic,
+                         "algorithmic_bytes_per_launch": alg,
+                         "kernels_ms": {"k_inflate_decode": round(kp[0], 3), "k_inflate_resolve": round(kp[1], 3),
+                                        "k_inflate_finalize": round(kp[2], 3),
+                                        "other": round(max(0.0, kms - sum(kp)), 3)},
+                         "launch": "one sdz_inflate_batch_device call: the lane / wave decoder and the block-split "
+                                   "decoder rounds (k_split) in 'k_inflate_decode', resolve rounds, gzip crc32; "
+                                   "'other': the rest of the launch (staging, copies)"},
             "config": {"workload": "C4 shape: 262,144 streams of 4 KiB-16 MiB (raw/zlib/gzip) LPT-sharded over 8 "
                                    "GPUs; each rank decodes every %dth stream of its shard" % scale,
                        "streams_per_gpu": len(pick), "bytes_out_all_ranks": total_out, "bytes_in_all_ranks": total_in,

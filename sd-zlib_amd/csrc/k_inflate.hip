@@ -1329,6 +1329,14 @@ __device__ __forceinline__ void epochs(const InflateArgs& A, DSave* S, const uin
 __global__ __launch_bounds__(IL_THREADS, 1) void k_inflate_decode(InflateArgs A, uint32_t round) {
     uint8_t* region = lane_region();
     uint32_t* ts = lane_stage();
+#ifdef IL_LDS_POISON
+    {   // development: this lane's LDS (symbol region, token stage, input ring) starts as 0xA5 bytes, so a
+        // read before a write sees the same value whatever ran on the CU before
+        for (uint32_t k = 0; k < IL_REGION / 4; ++k) ((uint32_t*)region)[k] = 0xA5A5A5A5u;
+        for (uint32_t k = 0; k < IL_TSTRIDE / 4; ++k) ts[k] = 0xA5A5A5A5u;
+        for (uint32_t k = 0; k < 18; ++k) lane_ring()[k] = 0xA5A5A5A5u;
+    }
+#endif
     uint32_t gid = blockIdx.x * IL_STREAMS + lane_slot();
     bool valid = gid < A.n && (threadIdx.x & 63u) < IL_WAVE_LANES;
     uint32_t sid = valid ? gid : 0u;

@@ -6,11 +6,13 @@
 #   suite               the whole -m gpu suite
 #   c2[:ENV=V,...]      tools/run_c2.py --mode inflate (C2), with the given environment
 #   dist[:ENV=V,...]    tools/run_c2.py --mode distinct (64 Ki distinct 64 KiB streams)
+#   mixed[:ENV=V,...]   tools/run_c2.py --mode mixed (the bench's C4-shaped leg, one rank)
 #   c3[:ENV=V,...]      tools/run_c2.py --mode deflate (C3)
 #   bench[:ARGS]        bench.py with the given arguments (commas become spaces)
-#   kt:<mode>           rocprofv3 kernel trace + stats of run_c2.py --mode <mode>
+#   kt:<mode>[:ENV=V,...]  rocprofv3 kernel trace + stats of run_c2.py --mode <mode> (into kt_<mode>_<step>)
 #   pmc:<mode>:<set>    rocprofv3 --pmc pass <set> (sq1 sq2 sq3 fetch write) of run_c2.py --mode <mode>
 #   configs             tools/run_configs.py (C4 / C5)
+#   node                tests/node/smoke.mjs (the drop-in facade)
 # Outputs under gpurun_out/$OUT/.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -42,9 +44,13 @@ for st in "$@"; do
     c2) envrun "$arg" timeout -k 10 300 python3 tools/run_c2.py --mode inflate --steps 3 > $log 2>&1 ;;
     dist) envrun "$arg" timeout -k 10 300 python3 tools/run_c2.py --mode distinct --steps 3 > $log 2>&1 ;;
     c3) envrun "$arg" timeout -k 10 300 python3 tools/run_c2.py --mode deflate --steps 3 > $log 2>&1 ;;
+    mixed) envrun "$arg" timeout -k 10 300 python3 tools/run_c2.py --mode mixed --steps 2 > $log 2>&1 ;;
+    node) timeout -k 10 300 node tests/node/smoke.mjs > $log 2>&1 ;;
     bench) timeout -k 10 600 python3 bench.py ${arg//,/ } > $log 2> $log.err ;;
-    kt) rm -rf $O/kt_$arg; timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/kt_$arg -o run --output-format csv -- \
-            python3 tools/run_c2.py --mode $arg --steps 2 > $log 2>&1 ;;
+    kt) mode=${arg%%:*}; e=""; [[ "$arg" == *:* ]] && e=${arg#*:}
+        d=$O/kt_${mode}_$n; rm -rf $d
+        envrun "$e" timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $d -o run --output-format csv -- \
+            python3 tools/run_c2.py --mode $mode --steps 2 > $log 2>&1 ;;
     pmc) mode=${arg%%:*}; set_=${arg#*:}
          rm -rf $O/pmc_${mode}_$set_
          timeout -s KILL 240 rocprofv3 --pmc ${PMC[$set_]} -d $O/pmc_${mode}_$set_ -o run --output-format csv -- \

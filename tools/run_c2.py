@@ -17,7 +17,7 @@ from bench import DeviceBatch, inflate_step, deflate_step, slice_offsets, fill_s
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--mode", default="inflate", choices=["inflate", "deflate", "distinct", "fast"])
+    ap.add_argument("--mode", default="inflate", choices=["inflate", "deflate", "distinct", "fast", "mixed"])
     ap.add_argument("--same", action="store_true", help="deflate: one slice in every stream")
     ap.add_argument("--steps", type=int, default=2)
     ap.add_argument("--streams", type=int, default=65536)
@@ -50,6 +50,13 @@ def main():
         print("distinct inflate: kernel %.3f ms %s, %.1f GB/s out, parity %s"
               % (r["roofline"]["kernel_ms"], r["roofline"]["kernels_ms"],
                  r["config"]["bytes_out_per_gpu"] / r["roofline"]["kernel_ms"] / 1e6, r["parity"]), flush=True)
+    elif args.mode == "mixed":
+        # the bench's C4-shaped leg (one rank, every 8th stream of its LPT shard)
+        from bench import mixed_leg
+        r = mixed_leg(sdz, L, args.steps, 8, lambda: None, lambda x: x, 1, 0)
+        print("mixed inflate: kernel %.3f ms %s, %.1f GB/s in+out, parity %s"
+              % (r["kernel_ms"], r["roofline"]["kernels_ms"], r["roofline"]["achieved"], r["parity"]), flush=True)
+        return
     elif args.mode == "fast":
         # the opt-in fast compressor on the C3 layout; validity checked with Python's zlib
         import ctypes
