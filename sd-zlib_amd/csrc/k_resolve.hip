@@ -37,9 +37,6 @@ namespace sdz {
 #define RS_EW (RS_WAVES - 1)           // emitter waves; the last wave writes back
 #define RS_THREADS (64 * RS_WAVES)
 #define RS_WIN 32768
-#ifndef RS_DB
-#define RS_DB 0                       // 1: two groups per emitter wave, one token per lane and pass (measured slower)
-#endif
 #ifndef RS_R
 #define RS_R 36352                    // ring bytes: 32 KiB window + bytes in flight
 #endif
@@ -435,35 +432,6 @@ __device__ __forceinline__ void publish_wf(uint32_t* wf, uint32_t v1) {
     if ((threadIdx.x & 63u) == 0) lds_put(wf, v1);
     rs_wake();
 }
-#ifndef RS_MINF
-#define RS_MINF 0                     // 1: the frontier as a minimum over the emitter waves (0: published in group order)
-#endif
-// The frontier of final bytes without an in-order publication (RS_MINF): every emitter wave keeps
-// the first byte it has still to write in low[w] (~0: nothing pending), and a byte is final once it
-// lies below the end of the groups started so far (the chain's end, read first: a group started
-// later lowers its wave's low before it extends the chain) and below every wave's low.
-__device__ __forceinline__ uint32_t min_dpp8(uint32_t x) {    // lane 7: the minimum of lanes 0..7
-    uint32_t y = (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)x, 0x111, 0xf, 0xf, false);   // row_shr:1
-    x = x < y ? x : y;
-    y = (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)x, 0x112, 0xf, 0xf, false);            // row_shr:2
-    x = x < y ? x : y;
-    y = (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)x, 0x114, 0xf, 0xf, false);            // row_shr:4
-    return x < y ? x : y;
-}
-__device__ __forceinline__ uint32_t rs_frontier(uint64_t* chain, uint32_t* low) {
-    const uint32_t ce = uni((uint32_t)lds_get64(chain));
-    lds_acquire();
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t v = __hip_atomic_load(&low[lane < RS_EW ? lane : 0u], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    const uint32_t m = lane_at(min_dpp8(lane < RS_EW ? v : ~0u), 7);
-    lds_acquire();
-    return ce < m ? ce : m;
-}
-__device__ __forceinline__ void rs_publish_low(uint32_t* low, uint32_t wu, uint32_t v) {
-    lds_release();
-    if ((threadIdx.x & 63u) == 0) lds_put(&low[wu], v);
-    rs_wake();
-}
 
 // The ring's window at the start of a round (all threads; a barrier must follow): output bytes
 // [pos0 - 32 KiB, pos0); before position 0 of this call, the window saved by the previous call
@@ -712,7 +680,6 @@ __global__ __launch_bounds__(RS_THREADS) __attribute__((amdgpu_waves_per_eu(RS_W
     __shared__ uint64_t chain;                           // (tag of the last started group) << 32 | its end
     __shared__ uint32_t wf, wwb, fail, edone;            // frontiers: final bytes, written-back bytes; emitters done
     __shared__ __attribute__((aligned(16))) uint8_t fmap[RS_BM];   // finality map of the bytes in flight
-    __shared__ uint32_t low[RS_EW];                      // RS_MINF: each emitter wave's first byte still to write
 
     const uint32_t tid = threadIdx.x, lane = tid & 63u, w = tid >> 6;
     const uint32_t sid = blockIdx.x;
@@ -735,15 +702,8 @@ __global__ __launch_bounds__(RS_THREADS) __attribute__((amdgpu_waves_per_eu(RS_W
     const uint32_t pm0 = (uint32_t)(pos0 % 65521u);
     ring_window_init<RS_R, RS_THREADS>(ring, A, sid, round, pos0, out, dl, dict);
     if (tid == 0) { chain = 0xffffffff00000000ull; wf = 0; wwb = 0; fail = 0; edone = 0; }
-    if (tid < RS_EW) low[tid] = ~0u;
     for (uint32_t k = tid; k < RS_BM / 4; k += RS_THREADS) ((uint32_t*)fmap)[k] = 0;
     __syncthreads();
-#if RS_MINF
-#define RS_WF() rs_frontier(&chain, low)
-#else
-#define RS_WF() lds_get(&wf)
-#endif
-    uint32_t lowpub = ~0u;                                // RS_MINF: this wave's low as published
 
     // adler32 as sums over the whole output: s1 = 1 + S, s2 = n + n S - T (mod 65521),
     // S = sum b_i, T = sum i b_i -- per-lane partials, combined once per round
@@ -769,143 +729,6 @@ __global__ __launch_bounds__(RS_THREADS) __attribute__((amdgpu_waves_per_eu(RS_W
     // traffic and its wait does not cover write-back stores
     uint32_t tnext = tk[wu * 64u + lane < ntok ? wu * 64u + lane : 0u];
     bool bad = false;                                     // this wave's watchdog tripped
-#if RS_DB
-    if (wu < RS_EW) {
-        // An emitter wave holds two groups: O, the older (not yet final), and N, the next of its
-        // groups.  Each pass gives every lane one token -- its O token while that one is pending,
-        // else its N token -- so a token its group's first pass could not write (its sources were not
-        // final yet) goes out alongside the next group's first pass instead of in a round of its own.
-        // O is published (wf) once it is complete and the frontier has reached it; a head O publishes
-        // its finished prefix, so a group larger than the ring's slack never waits on itself.
-        uint32_t tA = 0, dA = 0, rA = 0, tB = 0, dB = 0, rB = 0;   // token, round-relative start, ring index
-        uint64_t pA = 0, pB = 0;                                   // pending lanes of O and N
-        uint32_t SO = 0, TO = 0, SN = 0, TN = 0;
-        bool haveO = false, haveN = false, scanned = false;
-        uint32_t gn = wu;                                          // the next group to take
-        for (uint32_t n = 1;; ++n) {
-            bool prog = false;
-            // 1. the next group into N: its tokens and offsets, then its start from its predecessor
-            if (!haveN && gn < ngroups) {
-                if (!scanned) {
-                    const uint32_t ti = gn * 64u + lane;
-                    const bool valid = ti < ntok;
-                    const uint32_t t = tnext;
-                    tnext = tk[ti + 64u * RS_EW < ntok ? ti + 64u * RS_EW : 0u];
-                    const uint32_t len = !valid ? 0u : (int32_t)t < 0 ? ((t >> 16) & 255u) + 3u : ((t >> 24) & 3u) + 1u;
-                    const uint32_t incl = wave_incl_scan(len);
-                    tB = t;
-                    dB = incl - len;                               // (group-relative until the start is known)
-                    TN = lane_at(incl, 63);
-                    pB = __ballot(len != 0);
-                    scanned = true;
-                }
-                const uint64_t c = lds_get64(&chain);
-                if (uni((uint32_t)(c >> 32)) == gn - 1u) {
-                    SN = uni((uint32_t)c);
-#if RS_MINF
-                    if (SN < lowpub) { rs_publish_low(low, wu, SN); lowpub = SN; lds_release(); }
-#endif
-                    if (lane == 0) __hip_atomic_store(&chain, ((uint64_t)gn << 32) | (SN + TN), __ATOMIC_RELAXED,
-                                                      __HIP_MEMORY_SCOPE_WORKGROUP);
-                    const uint32_t sr = uni((rp0 + SN) % RS_R);    // ring index of byte SN (u32: SN < 2^26)
-                    rB = ridx((int32_t)(sr + dB));
-                    dB += SN;
-                    haveN = true;
-                    scanned = false;
-                    gn += RS_EW;
-                    prog = true;
-                    if (!haveO) {                                  // (the wave's first group)
-                        tA = tB; dA = dB; rA = rB; pA = pB; SO = SN; TO = TN;
-                        haveO = true;
-                        haveN = false;
-                        continue;
-                    }
-                }
-            }
-            if (!haveO && gn >= ngroups) break;                    // every group of this wave is final
-            RS_TICK(1);
-            // 2. a pass: each lane's O token while pending, else its N token
-            const uint64_t pBv = haveN ? pB : 0u;                  // (a group scanned but not started: not yet)
-            const bool useA = (pA >> lane) & 1u;
-            const bool act = useA || ((pBv >> lane) & 1u);
-            if (__ballot(act)) {
-                const uint32_t t = useA ? tA : tB, dst = useA ? dA : dB, d = useA ? rA : rB;
-                const bool ism = (int32_t)t < 0;
-                const uint32_t len = !act ? 0u : ism ? ((t >> 16) & 255u) + 3u : ((t >> 24) & 3u) + 1u;
-                const uint32_t dist = ism ? (t & 0x7fffu) + 1u : 0u;
-                const uint32_t dend = dst + len;
-                const int32_t src = (int32_t)dst - (int32_t)dist;  // round-relative (may be < 0)
-                const int32_t need = ism ? src + (int32_t)(len < dist ? len : dist) : INT32_MIN;
-                const uint32_t s = ridx((int32_t)d - (int32_t)dist);
-                const uint32_t gd = g32 + dst;                     // low bits of the global position
-                const uint32_t cwf = RS_WF();
-                const uint32_t cwb = lds_get(&wwb);
-                const bool room = act && dend <= cwf + RS_SLACK && dend <= cwb + RS_R;
-                const bool inwin = need <= (int32_t)cwf;
-                const uint32_t blo = src > (int32_t)cwf ? (uint32_t)src : cwf;
-                const bool chk = room && !inwin;
-                bool ok = true;
-                if (__ballot(chk)) ok = map_all(fmap, chk, g32 + blo, g32 + (uint32_t)need);
-                const bool rdy = room && (inwin || ok);
-                const uint64_t rm = __ballot(rdy);
-                if (rm) {
-                    RS_CBAR();
-                    emit_msk<RS_R, true, RS_MW>(ring, fmap, rdy, t, d, s, len, dist, gd & (RS_BM - 1), lap_of(gd));
-                    const uint64_t ma = __ballot(useA);
-                    pA &= ~(rm & ma);
-                    pB &= ~(rm & ~ma);
-                    prog = true;
-                    if (timed) tacc[6]++;
-                }
-            }
-            RS_TICK(2);
-            // 3. O final: complete and reached by the frontier (a head O publishes its finished prefix)
-#if RS_MINF
-            if (haveO && pA == 0) {                                // O complete: N becomes O
-                tA = tB; dA = dB; rA = rB; pA = haveN ? pB : 0u; SO = SN; TO = TN;
-                haveO = haveN;
-                haveN = false;
-                prog = true;
-            }
-            {
-                const uint64_t pBv2 = haveN ? pB : 0u;
-                const uint32_t lv = pA ? lane_at(dA, (uint32_t)__builtin_ctzll(pA))
-                                  : pBv2 ? lane_at(dB, (uint32_t)__builtin_ctzll(pBv2)) : ~0u;
-                if (lv != lowpub) { rs_publish_low(low, wu, lv); lowpub = lv; }
-            }
-#else
-            if (haveO) {
-                const uint32_t cwf = lds_get(&wf);
-                if (cwf >= SO) {
-                    lds_acquire();
-                    if (pA == 0) {
-                        publish_wf(&wf, SO + TO);
-                        tA = tB; dA = dB; rA = rB; pA = haveN ? pB : 0u; SO = SN; TO = TN;
-                        haveO = haveN;
-                        haveN = false;
-                        prog = true;
-                    } else {
-                        const uint32_t pre = lane_at(dA, (uint32_t)__builtin_ctzll(pA));   // the first pending byte
-                        if (cwf < pre) { publish_wf(&wf, pre); prog = true; }
-                    }
-                }
-            }
-#endif
-            RS_TICK(4);
-            if (prog) {
-                n = 0;
-            } else {
-                if (timed) tacc[7]++;
-                if ((n & 63u) == 0 && (n > RS_SPIN_LIMIT || lds_get(&fail))) {
-                    if (!lds_get(&fail)) lds_put(&fail, 3u | (SO << 4));
-                    bad = true;
-                    break;
-                }
-                __builtin_amdgcn_s_sleep(RS_NAP);
-            }
-        }
-    }
-#else
     for (uint32_t g = wu; wu < RS_EW && g < ngroups; g += RS_EW) {
         const uint32_t ti = g * 64u + lane;
         const bool valid = ti < ntok;
@@ -932,9 +755,6 @@ __global__ __launch_bounds__(RS_THREADS) __attribute__((amdgpu_waves_per_eu(RS_W
             __builtin_amdgcn_s_sleep(RS_NAP);
         }
         if (bad) break;
-#if RS_MINF
-        if (Sg < lowpub) { rs_publish_low(low, wu, Sg); lowpub = Sg; lds_release(); }
-#endif
         if (lane == 0) __hip_atomic_store(&chain, ((uint64_t)g << 32) | (Sg + T), __ATOMIC_RELAXED,
                                           __HIP_MEMORY_SCOPE_WORKGROUP);
         rs_wake();
@@ -952,10 +772,6 @@ __global__ __launch_bounds__(RS_THREADS) __attribute__((amdgpu_waves_per_eu(RS_W
         bool done = len == 0;
         uint64_t nd = __ballot(!done);
         for (uint32_t n = 1; nd; ++n) {
-#if RS_MINF
-            const uint32_t cwf = RS_WF();
-            const uint32_t cwb = lds_get(&wwb);
-#else
             const uint32_t pre = lane_at(off, (uint32_t)__builtin_ctzll(nd));   // finished prefix
             uint32_t cwf = lds_get(&wf);
             const uint32_t cwb = lds_get(&wwb);
@@ -963,7 +779,6 @@ __global__ __launch_bounds__(RS_THREADS) __attribute__((amdgpu_waves_per_eu(RS_W
                 publish_wf(&wf, Sg + pre);
                 cwf = Sg + pre;
             }
-#endif
             const bool room = !done && dend <= cwf + RS_SLACK && dend <= cwb + RS_R;
             const bool inwin = need <= (int32_t)cwf;
             const uint32_t blo = src > (int32_t)cwf ? (uint32_t)src : cwf;
@@ -983,10 +798,6 @@ __global__ __launch_bounds__(RS_THREADS) __attribute__((amdgpu_waves_per_eu(RS_W
                 nd &= ~rm;
                 n = 0;
                 if (timed) tacc[6]++;
-#if RS_MINF
-                const uint32_t lv = nd ? Sg + lane_at(off, (uint32_t)__builtin_ctzll(nd)) : ~0u;   // our first pending byte
-                if (lv != lowpub) { rs_publish_low(low, wu, lv); lowpub = lv; }
-#endif
             } else {
                 if (timed) tacc[7]++;
                 if ((n & 63u) == 0 && (n > RS_SPIN_LIMIT || lds_get(&fail))) {
@@ -999,9 +810,6 @@ __global__ __launch_bounds__(RS_THREADS) __attribute__((amdgpu_waves_per_eu(RS_W
         }
         if (bad) break;
         RS_TICK(2);
-#if RS_MINF
-        continue;                                         // (final once every wave's low is past it)
-#endif
         // 3. finality, in group order: publish now if we are the head (no one else can
         // move wf past Sg), else once the frontier reaches us
         for (uint32_t n = 1;; ++n) {
@@ -1017,7 +825,6 @@ __global__ __launch_bounds__(RS_THREADS) __attribute__((amdgpu_waves_per_eu(RS_W
         publish_wf(&wf, Sg + T);
         RS_TICK(4);
     }
-#endif
     const uint32_t* ring32 = (const uint32_t*)ring;
     if (wu < RS_EW) {
         lds_release();
@@ -1029,7 +836,7 @@ __global__ __launch_bounds__(RS_THREADS) __attribute__((amdgpu_waves_per_eu(RS_W
         for (uint32_t n = 1;; ++n) {
             const bool fi = lds_get(&edone) == RS_EW;     // every group published: wf is the round's end
             lds_acquire();
-            const uint32_t Fv = RS_WF();
+            const uint32_t Fv = lds_get(&wf);
             const uint64_t ab = pos0 + WB;
             const uint32_t nk = 1024u - (uint32_t)(ab & 1023u);
             uint32_t m;
@@ -1061,429 +868,6 @@ __global__ __launch_bounds__(RS_THREADS) __attribute__((amdgpu_waves_per_eu(RS_W
 
     // (the adler partials' reduction reuses the finality map, which no one reads any more)
     resolve_finish<RS_R, RS_WAVES>(A, round, sid, flag, fin0, gz, pos0, 0, &chain, &fail, ring, accS, accT, (uint64_t*)fmap);
-}
-
-// ------------------------------------------------------------------ block-synchronous resolve
-//
-// k_inflate_resolve_b: the same job as k_inflate_resolve without the group pipeline.  The
-// workgroup takes the round's tokens in BATCHES of RB_THREADS (one per thread):
-//   1. a block scan of the token lengths gives every token its output offset; a batch is cut
-//      where its bytes would pass RB_CAP (the ring's room beyond the 32 KiB window);
-//   2. a copy whose source bytes end before the batch starts reads only final bytes (earlier
-//      batches): it and every literal are written at once (masked dword writes, emit_msk);
-//      the other copies -- DEPENDENTS, whose sources lie in this batch -- mark their
-//      destination bytes in a pending bitmap first;
-//   3. after a barrier, each wave writes its dependents as their source bytes' pending bits
-//      clear, clearing their own after the bytes (one wave's LDS operations complete in order,
-//      so a wave that sees a bit clear reads the bytes);
-//   4. during the next batch, the workgroup copies the batch's complete dwords to HBM and
-//      folds them into adler32.
-// Against the pipeline of groups (k_inflate_resolve) this drops the finality map (a masked map
-// write per data write, a map read per source), the per-group frontier chain and the rounds of
-// retries that emitted a group to its longest token: a literal or a copy from before the batch
-// is written once, and only the dependents (on text ~1 in 6 copies) wait.
-#define RB_WAVES 8
-#define RB_THREADS (64 * RB_WAVES)
-#define RB_TW (RB_WAVES - 1)          // token waves; the last wave writes the dependents
-#define RB_BATCH (64 * RB_TW)         // tokens per batch at most
-#define RB_CAP 2432                   // output bytes of one batch at most
-#define RB_R (RS_WIN + 2 * RB_CAP + 16)   // ring: the 32 KiB window + two batches in flight
-#define RB_BMW (RB_CAP / 32)          // pending bitmap words per batch
-#define RB_DLW 22                     // dependents list entries per token wave and batch
-#ifndef RB_MW
-#define RB_MW 3                       // destination dwords per masked-write step
-#endif
-#define RB_SPIN_LIMIT (1u << 22)
-#ifndef RB_ABL
-#define RB_ABL 0                      // development: a phase left out, for its cost (output wrong)
-#endif
-static_assert(2 * RB_CAP + 8 <= RB_R - RS_WIN, "two batches must not overwrite the window they read");
-static_assert(RB_CAP % 32 == 0 && RB_R % 16 == 0, "");
-
-// bits [lo, lo + n) of the pending bitmap set (or cleared), for the lanes with act (n >= 1)
-__device__ __forceinline__ void rb_bits(uint32_t* bm, bool act, uint32_t lo, uint32_t n, bool set) {
-    const uint32_t hi = lo + n - 1u;                      // inclusive
-    const uint32_t k0 = lo >> 5, nw = act ? (hi >> 5) - k0 + 1u : 0u;
-    for (uint32_t i = 0; __ballot(i < nw); ++i) {
-        const uint32_t k = k0 + i;
-        const uint32_t a = i == 0 ? lo & 31u : 0u, b = k == (hi >> 5) ? (hi & 31u) : 31u;
-        const uint32_t m = (0xffffffffu >> (31u - b)) & (0xffffffffu << a);
-        if (i < nw) {
-            if (set) __hip_atomic_fetch_or(bm + k, m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            else __hip_atomic_fetch_and(bm + k, ~m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        }
-    }
-}
-// are bits [lo, hi) of the pending bitmap all clear?  (lanes without act: true)
-__device__ __forceinline__ bool rb_clear(uint32_t* bm, bool act, uint32_t lo, uint32_t hi) {
-    const bool any = act && hi > lo;
-    const uint32_t k0 = lo >> 5, nw = any ? ((hi - 1u) >> 5) - k0 + 1u : 0u;
-    uint32_t miss = 0;
-    for (uint32_t i = 0; __ballot(i < nw); ++i) {
-        const uint32_t k = k0 + i;
-        const uint32_t a = i == 0 ? lo & 31u : 0u, b = k == ((hi - 1u) >> 5) ? ((hi - 1u) & 31u) : 31u;
-        const uint32_t m = (0xffffffffu >> (31u - b)) & (0xffffffffu << a);
-        const uint32_t v = __hip_atomic_load(bm + (i < nw ? k : 0u), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        miss |= i < nw ? v & m : 0u;
-    }
-    return miss == 0;
-}
-
-// write-back by the whole workgroup: output bytes [pos0 + WB, pos0 + ae) from the ring to HBM (all
-// four bytes of the dwords inside, the edge dwords byte by byte), folded into each thread's adler32
-// partials.  Every thread's ring reads are issued before its stores.
-template <uint32_t NT>
-__device__ __forceinline__ void rb_write_back(uint8_t* out, const uint32_t* ring32, uint64_t pos0, uint64_t ae, bool gz,
-                                              uint32_t& WB, uint32_t& rW, uint32_t& gm, uint32_t& accS, uint64_t& accT) {
-    const uint32_t tid = threadIdx.x;
-    const uint64_t ab = pos0 + WB;
-    if (ae <= ab) return;
-    const uint32_t h = (uint32_t)(ab & 3u);
-    const uint32_t nq = (uint32_t)(((ae + 3u) >> 2) - (ab >> 2));
-    const uint32_t tl = (uint32_t)(ae & 3u);
-    uint32_t* dstw = (uint32_t*)(out + (ab - h));
-    const int32_t rb0 = (int32_t)rW - (int32_t)h;      // ring index of the first dword (4-aligned)
-    const uint32_t gi0 = gm + 65521u - h;              // index of its byte 0, mod 65521 (+ 65521)
-    for (uint32_t q0 = 0; q0 < nq; q0 += 2 * NT) {
-        uint32_t v[2];
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {
-            const uint32_t q = q0 + tid + u * NT;
-            v[u] = ring32[q < nq ? ridx_t<RB_R>(rb0 + 4 * (int32_t)q) >> 2 : 0u];
-        }
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {
-            const uint32_t q = q0 + tid + u * NT;
-            if (q >= nq) break;
-            const uint32_t blo = q == 0 ? h : 0u;
-            const uint32_t bhi = q + 1 < nq || tl == 0 ? 4u : tl;
-            if (blo == 0 && bhi == 4) dstw[q] = v[u];
-            else for (uint32_t bb = blo; bb < bhi; ++bb) ((uint8_t*)(dstw + q))[bb] = (uint8_t)(v[u] >> (8 * bb));
-            if (!gz) {
-                const uint32_t mk = (bhi == 4u ? ~0u : (1u << (8 * bhi)) - 1u) & (~0u << (8 * blo));
-                const uint32_t vm = v[u] & mk;
-                const uint32_t s4 = __builtin_amdgcn_udot4(vm, 0x01010101u, 0u, false);
-                accS += s4;
-                accT += (uint64_t)(gi0 + 4 * q) * s4 + __builtin_amdgcn_udot4(vm, 0x03020100u, 0u, false);
-            }
-        }
-    }
-    const uint32_t m = (uint32_t)(ae - ab);
-    WB += m;
-    rW += m;
-    rW -= rW >= RB_R ? RB_R : 0u;
-    gm = (uint32_t)((gm + (uint64_t)m) % 65521u);
-}
-
-// RB_PROF (development build): phase clocks of the first 8 workgroups, summed into A.dbg[16..]
-// (SDZ_PHASE_TIMING=1 prints them).  Token waves: [16] wait for the dependents wave, [17] offsets
-// and cut, [18] classify and immediate writes, [19] scan and write-back, [20] barrier, [21] an
-// overflowed list; dependents wave: [22] waiting, [23] writing; [24] batches, [25] overflows, [26] cuts
-#ifdef RB_PROF
-#define RB_T0() unsigned long long rb_t = clock64()
-#define RB_TICK(k) do { if (prof) { unsigned long long tn = clock64(); pacc[k] += tn - rb_t; rb_t = tn; } } while (0)
-#else
-#define RB_T0() do {} while (0)
-#define RB_TICK(k) do {} while (0)
-#endif
-
-// the batch's token lengths and their wave scan; the waves' totals go to wsum
-// (the length is recomputed where it is used: one register less across the batch)
-struct RbTok {
-    uint32_t t, incl;
-};
-__device__ __forceinline__ uint32_t rb_len(uint32_t t) {
-    return (int32_t)t < 0 ? ((t >> 16) & 255u) + 3u : ((t >> 24) & 3u) + 1u;
-}
-__device__ __forceinline__ RbTok rb_scan(uint32_t t, bool valid, uint32_t* wsum, uint32_t wu) {
-    RbTok r;
-    r.t = valid ? t : 0u;                                // (an invalid lane: a 1-byte literal, length 0 here)
-    r.incl = wave_incl_scan(valid ? rb_len(t) : 0u);
-    if ((threadIdx.x & 63u) == 63u) wsum[wu] = r.incl;
-    return r;
-}
-
-// a token of the batch, placed: its ring destination d and source s, and the batch-relative
-// source bytes [sb, se) it reads (sb < 0: before the batch)
-struct RbPlace {
-    uint32_t len, dist, d, s;
-    int32_t sb, se;
-    bool ism, gen;
-};
-__device__ __forceinline__ RbPlace rb_place(uint32_t t, uint32_t dp, uint32_t rP) {
-    RbPlace q;
-    q.ism = (int32_t)t < 0;
-    q.len = q.ism ? ((t >> 16) & 255u) + 3u : ((t >> 24) & 3u) + 1u;
-    q.dist = q.ism ? (t & 0x7fffu) + 1u : 0u;
-    uint32_t d = rP + dp;
-    d -= d >= RB_R ? RB_R : 0u;
-    q.d = d;
-    const int32_t sr = (int32_t)d - (int32_t)q.dist;
-    q.s = sr < 0 ? (uint32_t)(sr + RB_R) : (uint32_t)sr;
-    q.sb = (int32_t)dp - (int32_t)q.dist;
-    q.se = q.ism ? q.sb + (int32_t)(q.len < q.dist ? q.len : q.dist) : q.sb;
-    // copies that overlap themselves or cross the ring's end take the general path, which runs
-    // with the dependents (inlined at one site)
-    q.gen = d + q.len > RB_R || (q.ism && (q.dist < q.len || q.s + q.len > RB_R || q.s < 4u));
-    return q;
-}
-
-// The dependents of one batch, written as their sources allow (whole wave; lanes with pend):
-// a dependent is ready once the pending bits of its source bytes inside the batch are clear; it
-// writes its bytes, then clears its own bits.  false: the watchdog tripped.
-__device__ __forceinline__ bool rb_dependents(uint8_t* ring, uint32_t* bmh, bool pend, uint32_t t, uint32_t dp,
-                                              const RbPlace& r, uint32_t* fail, uint32_t site) {
-    const uint32_t lo = r.sb > 0 ? (uint32_t)r.sb : 0u;
-    const uint32_t hi = r.se > 0 ? (uint32_t)r.se : 0u;
-    for (uint32_t n = 1; __ballot(pend); ++n) {
-        const bool rdy = pend && rb_clear(bmh, pend, lo, hi);
-        RS_CBAR();
-        if (__ballot(rdy)) {
-            emit_msk<RB_R, false, RB_MW, 2>(ring, nullptr, rdy, t, r.d, r.s, r.len, r.dist, 0, 0);
-            RS_CBAR();
-            rb_bits(bmh, rdy, dp, r.len, false);
-            pend = pend && !rdy;
-            n = 0;
-        } else {
-            if ((n & 63u) == 0 && (n > RB_SPIN_LIMIT || lds_get(fail))) {
-                if (!lds_get(fail)) lds_put(fail, site);
-                return false;
-            }
-            __builtin_amdgcn_s_sleep(1);
-        }
-    }
-    return true;
-}
-
-// a bounded wait until *p >= v (false: the watchdog tripped or another wave's did)
-__device__ __forceinline__ bool rb_wait(uint32_t* p, uint32_t v, uint32_t* fail, uint32_t site) {
-    for (uint32_t n = 1;; ++n) {
-        if (lds_get(p) >= v) { lds_acquire(); return true; }
-        if ((n & 15u) == 0 && (n > RB_SPIN_LIMIT || lds_get(fail))) {
-            if (!lds_get(fail)) lds_put(fail, site);
-            return false;
-        }
-        __builtin_amdgcn_s_sleep(1);
-    }
-}
-// a barrier of the token waves (the dependents wave runs on): a counter in LDS
-__device__ __forceinline__ bool rb_bar(uint32_t* cnt, uint32_t& gen, uint32_t* fail) {
-    lds_release();
-    if ((threadIdx.x & 63u) == 0) __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    gen += RB_TW;
-    return rb_wait(cnt, gen, fail, 6u);
-}
-
-// k_inflate_resolve_b, the pipeline: the token waves take batch b's tokens (one per lane), write
-// its literals and its copies whose sources are final, and list the rest (the DEPENDENTS: sources
-// in batch b, or on bytes of batch b - 1 still pending) with their destination bytes marked in the
-// batch's pending bitmap; the dependents wave meanwhile writes batch b - 1's list.  Two batches are
-// in flight, so the ring holds the window and two batches, and the token waves wait only when the
-// dependents wave is two batches behind.  A batch whose list overflows is finished by the token
-// waves themselves (each lane its own dependent) once the dependents wave has caught up.
-__global__ __launch_bounds__(RB_THREADS) __attribute__((amdgpu_waves_per_eu(RB_WAVES, RB_WAVES)))
-void k_inflate_resolve_b(InflateArgs A, uint32_t round) {
-    __shared__ __attribute__((aligned(16))) uint8_t ring[RB_R + 256];   // + per-lane dummies
-    __shared__ uint32_t bm[2][RB_BMW];                   // pending bytes of each batch in flight
-    __shared__ uint32_t tl[2][RB_TW * RB_DLW];           // dependents lists: token ...
-    __shared__ uint16_t dpl[2][RB_TW * RB_DLW];          // ... and batch-relative offset
-    __shared__ uint32_t wsum[2][RB_WAVES], wcnt[RB_WAVES], wend[RB_WAVES], dcnt[2][RB_WAVES];
-    __shared__ uint32_t bP[2], brP[2], ovf[2];           // per batch in flight: start, its ring index, list overflow
-    __shared__ uint32_t bar, listed, done, tfin, fail;   // token-wave barrier; batches listed / done; batch count
-    __shared__ uint32_t Pend;                            // the round's output bytes (for all waves at the end)
-    __shared__ uint64_t red[RB_WAVES][2];
-
-    const uint32_t tid = threadIdx.x, lane = tid & 63u, w = tid >> 6;
-    const uint32_t sid = blockIdx.x;
-    if (sid >= A.n) return;
-    const uint32_t flag = A.flags[sid];
-    const bool fin0 = A.streaming && round == 0 && flag == 2;   // (as in k_inflate_resolve)
-    if (flag == 2 && !fin0) return;
-    RSave* R = (RSave*)A.rsave + sid;
-    DSave* S = (DSave*)A.dsave + sid;
-    const bool gz = S->container == SDZ_CONTAINER_GZIP;
-    const uint64_t pos0 = round == 0 ? 0 : R->pos;
-    uint8_t* out = A.out + A.out_off[sid];
-    const uint32_t* tk = A.tokens + (uint64_t)sid * A.round_tokens;
-    const uint32_t ntok = A.ntok[sid];
-    const int64_t dl = S->dict_used && A.dict ? (A.dict_len > 32767 ? 32767 : A.dict_len) : 0;
-    const uint8_t* dict = dl ? A.dict + (A.dict_len - dl) : nullptr;
-    const uint32_t rp0 = (uint32_t)(pos0 % RB_R);
-    ring_window_init<RB_R, RB_THREADS>(ring, A, sid, round, pos0, out, dl, dict);
-    for (uint32_t k = tid; k < 2 * RB_BMW; k += RB_THREADS) (&bm[0][0])[k] = 0;
-    if (tid == 0) { fail = 0; bar = 0; listed = 0; done = 0; tfin = 0xffffffffu; ovf[0] = 0; ovf[1] = 0; }
-
-    const uint32_t wu = uni(w);
-    uint32_t accS = 0;
-    uint64_t accT = 0;
-    const uint32_t* ring32 = (const uint32_t*)ring;
-    uint32_t P = 0;                                       // end of the batches listed so far (round-relative)
-    RbTok K;
-    uint32_t tnext = 0;                                   // token waves: batch b + 1's tokens, loaded a batch
-    if (wu < RB_TW) {                                     // early assuming batch b is not cut
-        K = rb_scan(tk[tid < ntok ? tid : 0u], tid < ntok, wsum[0], wu);
-        tnext = tk[RB_BATCH + tid < ntok ? RB_BATCH + tid : 0u];
-    }
-    __syncthreads();
-#ifdef RB_PROF
-    const bool prof = A.dbg && sid < 8 && lane == 0;
-    unsigned long long pacc[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-#endif
-    RB_T0();
-    if (wu < RB_TW) {
-        // ---- token waves
-        uint32_t rP = rp0, WB = 0, rW = rp0, gm = (uint32_t)(pos0 % 65521u);
-        uint32_t tb = 0, b = 0, Tprev = 0, gen = 0;
-        while (tb < ntok) {
-            const uint32_t pb = b & 1u;
-            // batch b - 2 complete: its bitmap half and list are free, its bytes final
-            if (b >= 2 && !rb_wait(&done, b - 1u, &fail, 7u)) break;
-            RB_TICK(0);
-            // 1. offsets and the cut (the scan ran before the last barrier)
-            const uint32_t t = K.t, len = tb + tid < ntok ? rb_len(t) : 0u;
-            const uint32_t xs = wave_incl_scan(lane < RB_TW ? wsum[pb][lane_lo8()] : 0u);
-            const uint32_t pre = wu ? lane_at(xs, wu - 1u) : 0u, tot = lane_at(xs, RB_TW - 1);
-            const uint32_t dp = pre + K.incl - len;      // batch-relative offset of the token's first byte
-            const uint32_t rest = ntok - tb;
-            uint32_t Tb = tot, nb = rest < RB_BATCH ? rest : RB_BATCH;
-            bool in = tb + tid < ntok;
-            if (tot > RB_CAP) {                          // cut: the tokens that end within RB_CAP (a prefix)
-                in = in && dp + len <= RB_CAP;
-                const uint64_t bk = __ballot(in);
-                const uint32_t last = bk ? 63u - (uint32_t)__builtin_clzll(bk) : 0u;
-                const uint32_t e = lane_at(dp + len, last);
-                if (lane == 0) { wcnt[wu] = (uint32_t)__builtin_popcountll(bk); wend[wu] = bk ? e : 0u; }
-                if (!rb_bar(&bar, gen, &fail)) break;
-                const uint32_t xc = wave_incl_scan(lane < RB_TW ? wcnt[lane_lo8()] : 0u);
-                nb = lane_at(xc, RB_TW - 1);
-                Tb = lane_at(dpp_max8(lane < RB_TW ? wend[lane_lo8()] : 0u), RB_TW - 1);
-            }
-#ifdef RB_PROF
-            if (prof) { pacc[10] += tot > RB_CAP ? 1 : 0; pacc[8]++; }
-#endif
-            RB_TICK(1);
-            // the next batch's tokens (scanned below): prefetched unless this batch was cut, then the
-            // one after it
-            const uint32_t tb1 = tb + nb;
-            const uint32_t i1 = tb1 + tid_fresh();
-            uint32_t t1 = tnext;
-            if (nb != RB_BATCH) t1 = tk[i1 < ntok ? i1 : 0u];
-            {
-                const uint32_t j = tb1 + RB_BATCH + tid_fresh();
-                tnext = tk[j < ntok ? j : 0u];
-            }
-            // 2. classify: a dependent reads bytes of this batch, or pending bytes of the last
-            const RbPlace q = rb_place(t, dp, rP);
-            bool dep = RB_ABL < 5 && in && ((q.ism && q.se > 0) || q.gen);
-            {
-                const int32_t plo = q.sb > -(int32_t)Tprev ? q.sb : -(int32_t)Tprev, phi = q.se < 0 ? q.se : 0;
-                const bool chk = RB_ABL != 4 && RB_ABL < 5 && in && !dep && q.ism && phi > plo;
-                if (__ballot(chk))
-                    dep = dep || (chk && !rb_clear(bm[pb ^ 1u], chk, (uint32_t)(plo + (int32_t)Tprev),
-                                                   (uint32_t)(phi + (int32_t)Tprev)));
-            }
-            const bool now = in && !dep;
-            const uint64_t dk = __ballot(dep);
-            if (dk) {
-                rb_bits(bm[pb], dep, dp, len, true);
-                const uint32_t k = (uint32_t)__builtin_popcountll(dk & ((1ull << lane) - 1ull));
-                if (dep && k < RB_DLW) { tl[pb][wu * RB_DLW + k] = t; dpl[pb][wu * RB_DLW + k] = (uint16_t)dp; }
-                if (lane == 0 && __builtin_popcountll(dk) > RB_DLW) ovf[pb] = b + 1u;   // (no reset needed)
-            }
-            if (lane == 0) dcnt[pb][wu] = (uint32_t)__builtin_popcountll(dk);
-            if (tid == 0) { bP[pb] = P; brP[pb] = rP; }
-#if RB_ABL != 2 && RB_ABL < 6
-            if (__ballot(now)) emit_msk<RB_R, false, RB_MW, 0>(ring, nullptr, now, t, q.d, q.s, len, q.dist, 0, 0);
-#endif
-            RB_TICK(2);
-            // 3. the next batch's scan, then the complete dwords of batches up to b - 2 to HBM
-            // (the stores come after the wait for the tokens)
-            if (tb1 < ntok) K = rb_scan(t1, i1 < ntok, wsum[pb ^ 1u], wu);
-#if RB_ABL != 1 && RB_ABL < 7
-            rb_write_back<64 * RB_TW>(out, ring32, pos0, (pos0 + (P - Tprev)) & ~3ull, gz, WB, rW, gm, accS, accT);
-#endif
-            RB_TICK(3);
-            if (!rb_bar(&bar, gen, &fail)) break;
-            if (tid == 0) lds_put(&listed, b + 1u);
-            RB_TICK(4);
-            // 4. an overflowed list: this batch's dependents by their own lanes, after the
-            // dependents wave has finished the batch before
-            if (uni(ovf[pb]) == b + 1u) {
-                if (!rb_wait(&done, b, &fail, 8u)) break;
-                if (!rb_dependents(ring, bm[pb], dep, t, dp, q, &fail, 9u)) break;
-                if (!rb_bar(&bar, gen, &fail)) break;
-#ifdef RB_PROF
-                if (prof) pacc[9]++;
-#endif
-            }
-            RB_TICK(5);
-            Tprev = Tb;
-            P += Tb;
-            rP += Tb;
-            rP -= rP >= RB_R ? RB_R : 0u;
-            tb = tb1;
-            ++b;
-        }
-        if (tid == 0) { Pend = P; lds_put(&tfin, b); }
-        // the last batches: the rest once the dependents wave is done
-        if (rb_wait(&done, b, &fail, 10u))
-            rb_write_back<64 * RB_TW>(out, ring32, pos0, pos0 + P, gz, WB, rW, gm, accS, accT);
-    } else {
-        // ---- the dependents wave: batch b's list once it is listed, in order of position (the
-        // list is in token order per wave, waves in order), 64 entries at a time: an entry
-        // depends only on earlier ones
-        for (uint32_t b = 0;; ++b) {
-            bool go = false;
-            for (uint32_t n = 1;; ++n) {
-                if (lds_get(&listed) > b) { go = true; break; }
-                if (lds_get(&tfin) <= b || lds_get(&fail)) break;
-                if ((n & 15u) == 0 && n > RB_SPIN_LIMIT) { lds_put(&fail, 11u); break; }
-                __builtin_amdgcn_s_sleep(1);
-            }
-            if (!go) break;
-            RB_TICK(6);
-            lds_acquire();
-            const uint32_t pb = b & 1u;
-            if (uni(ovf[pb]) != b + 1u) {
-                const uint32_t rPb = uni(brP[pb]);
-                const uint32_t cw = lane < RB_TW ? dcnt[pb][lane_lo8()] : 0u;
-                const uint32_t cs = wave_incl_scan(cw);  // inclusive per-wave prefix of the counts
-                const uint32_t nd = lane_at(cs, RB_TW - 1);
-                bool ok = true;
-                for (uint32_t c = 0; c < nd && ok; c += 64) {
-                    const uint32_t e = c + lane;
-                    const bool act = e < nd;
-                    uint32_t wq = 0, base = 0;           // the wave whose entry e is, and its prefix
-#pragma unroll
-                    for (int v = 0; v < RB_TW - 1; ++v) {
-                        const uint32_t pv = lane_at(cs, (uint32_t)v);
-                        const bool past = e >= pv;
-                        wq += past ? 1u : 0u;
-                        base = past ? pv : base;
-                    }
-                    const uint32_t idx = act ? wq * RB_DLW + (e - base) : 0u;
-                    const uint32_t t = tl[pb][idx], dp = dpl[pb][idx];
-                    const RbPlace r = rb_place(t, dp, rPb);
-#if RB_ABL == 3
-                    rb_bits(bm[pb], act, dp, r.len, false);
-#else
-                    ok = rb_dependents(ring, bm[pb], act, t, dp, r, &fail, 12u);
-#endif
-                }
-                if (!ok) break;
-            }
-            lds_release();
-            if (lane == 0) lds_put(&done, b + 1u);
-            RB_TICK(7);
-        }
-    }
-#ifdef RB_PROF
-    if (prof) for (int k = 0; k < 12; ++k) atomicAdd(&A.dbg[16 + k], pacc[k]);
-#endif
-    if (tid == 0 && ntok == 0) Pend = 0;
-    __syncthreads();
-    resolve_finish<RB_R, RB_WAVES>(A, round, sid, flag, fin0, gz, pos0, pos0 + (uint64_t)uni(Pend), nullptr, &fail, ring,
-                                   accS, accT, &red[0][0]);
 }
 
 // ------------------------------------------------------------------ gzip: crc32 + verdicts
@@ -1558,16 +942,8 @@ __global__ __launch_bounds__(64) void k_inflate_finalize(InflateArgs A, uint64_t
 
 uint32_t resolve_block_threads() { return RS_THREADS; }
 uint32_t resolve_streams_per_block() { return 1; }
-// SDZ_RESOLVE=1 (read at each launch, so tests can switch it): the batch pipeline
-// (k_inflate_resolve_b); default: the group pipeline (k_inflate_resolve), faster on
-// every bench shape measured
-static bool resolve_batches() {
-    const char* e = getenv("SDZ_RESOLVE");
-    return e && *e == '1';
-}
 void launch_inflate_resolve(const InflateArgs& a, uint32_t round, dim3 grid, hipStream_t s) {
-    if (resolve_batches()) hipLaunchKernelGGL(k_inflate_resolve_b, grid, dim3(RB_THREADS), 0, s, a, round);
-    else hipLaunchKernelGGL(k_inflate_resolve, grid, dim3(RS_THREADS), 0, s, a, round);
+    hipLaunchKernelGGL(k_inflate_resolve, grid, dim3(RS_THREADS), 0, s, a, round);
 }
 // parts: scratch for the chunk crcs (a.tokens: the token rings are free once the rounds are
 // done; >= 1024 entries per stream); chunks of >= 256 KiB, <= 1024 per stream and <= 4 Mi
