@@ -2128,6 +2128,9 @@ int run_inflate_rounds(const InflateArgs& a, hipStream_t s, uint32_t* host_activ
             // the end finds nothing to do: ~10 us, against a ~25 us host round trip per read)
             for (uint32_t it = 0;;) {
                 for (uint32_t b = 0; b < WD_PAIRS; ++b, ++it) {
+                    // (round 0 starts over on the lane decoder after lane_after pairs: no pair of that
+                    // round runs with the lane flag, whose work the restart would throw away)
+                    if (round == 0 && it >= lane_after) break;
                     hipLaunchKernelGGL(k_inflate_wcold, g1, dim3(IL_THREADS), 0, s, a, round, it == 0 ? 1u : 0u,
                                        it >= lane_after ? 1u : 0u);
                     DBG_SYNC(s, "k_inflate_wcold", round, it);

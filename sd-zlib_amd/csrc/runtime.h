@@ -113,7 +113,9 @@ struct Pinned {
     bool pending[kMaxDev] = {};
     // wait = false: the caller does not write the buffer from the host (only stream-ordered
     // device work does), so the pending copies are not waited for unless it must grow
-    int get(size_t bytes, void** out, bool wait = true);
+    // busy: a stream on which this caller's copies from the buffer may still run (a growing get()
+    // waits for it before the old buffer is freed)
+    int get(size_t bytes, void** out, bool wait = true, hipStream_t busy = nullptr);
     int done(hipStream_t s);
 };
 // a few pinned host words of this thread for the round drivers' counter read-backs (a copy into

@@ -174,7 +174,8 @@ int host_shard(const uint8_t* const* in, const size_t* in_len, uint8_t* const* o
         void* ep = nullptr;
         const size_t nb = o_rec - o_out + recs.size();
         // (written by stream-ordered device work only: no wait for the input copy)
-        if (int rc2 = g_pinned.get(al(nb, 256), &ep, false)) return rc2;
+        // (a growing get() first waits for this call's input copy from the staging it replaces)
+        if (int rc2 = g_pinned.get(al(nb, 256), &ep, false, s)) return rc2;
         ebuf = (uint8_t*)ep;
         // the bytes written and the records, by a kernel into the mapped staging (a copy engine
         // started ~20 us late on small calls); SDZ_COPY_BACK=0: the whole region by hipMemcpyAsync
@@ -409,12 +410,21 @@ int multi_batch(const uint8_t* const* in, const size_t* in_len, uint8_t* const* 
         }
         if (r2 != SDZ_API_OK) coll_fail.store(true);
         // wait for the collective, or for another rank's failure (its peers would wait forever on
-        // a collective one rank never entered): poll rather than block
+        // a collective one rank never entered): poll rather than block, and give up after
+        // SDZ_GATHER_TIMEOUT_MS (default 120 s: a collective that hangs without any rank failing
+        // ends the call with an error instead of spinning every thread forever)
+        static const long long limit_ms = getenv("SDZ_GATHER_TIMEOUT_MS") ? atoll(getenv("SDZ_GATHER_TIMEOUT_MS")) : 120000;
+        const auto t0 = std::chrono::steady_clock::now();
         while (r2 == SDZ_API_OK) {
             const hipError_t q = hipStreamQuery(nullptr);
             if (q == hipSuccess) break;
             if (q != hipErrorNotReady) { r2 = hip_fail(q, "gather sync"); coll_fail.store(true); break; }
             if (coll_fail.load()) { r2 = fail(SDZ_API_HIP_ERROR, "gather: another shard's collective failed"); break; }
+            if (limit_ms > 0 && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(limit_ms)) {
+                r2 = fail(SDZ_API_HIP_ERROR, "gather: the collective did not complete within SDZ_GATHER_TIMEOUT_MS");
+                coll_fail.store(true);
+                break;
+            }
             std::this_thread::sleep_for(std::chrono::microseconds(20));
         }
         // every rank has left the collective (done, failed, or given up); one of them aborts the

@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -24,6 +25,8 @@ namespace sdz {
 namespace rt {
 
 thread_local std::string g_err;
+// bumped by every device allocation or free of the pools: free_hbm()'s cached value is stale then
+static std::atomic<unsigned> g_hbm_epoch{0};
 std::recursive_mutex g_dev_mu[kMaxDev];
 Pool g_host;
 Pinned g_pinned;
@@ -112,9 +115,11 @@ int Pool::get(size_t bytes, hipStream_t s, void** out, Slot** slot) {
         S.p = nullptr;
         S.cap = 0;
         S.pending = false;
+        g_hbm_epoch.fetch_add(1);
     }
     if (!S.p) {
         size_t want = std::max(bytes, (size_t)1 << 20);
+        g_hbm_epoch.fetch_add(1);
         hipError_t e = hipMalloc(&S.p, want);
         if (e != hipSuccess) { S.p = nullptr; return hip_fail(e, "hipMalloc(scratch)"); }
         S.cap = want;
@@ -136,7 +141,7 @@ int Pool::done(Slot* S, hipStream_t s) {
     return SDZ_API_OK;
 }
 
-int Pinned::get(size_t bytes, void** out, bool wait) {
+int Pinned::get(size_t bytes, void** out, bool wait, hipStream_t busy) {
     int d = 0;
     if (int rc = cur_device(&d)) return rc;
     if (pending[d] && (wait || cap[d] < bytes)) {
@@ -145,6 +150,9 @@ int Pinned::get(size_t bytes, void** out, bool wait) {
         pending[d] = false;
     }
     if (cap[d] < bytes) {
+        // (busy: the caller's own copies from the old buffer may still be in flight on that stream,
+        // not yet covered by a done() event)
+        if (p[d] && busy) HIPCHK(hipStreamSynchronize(busy));
         if (p[d]) HIPCHK(hipHostFree(p[d]));
         p[d] = nullptr;
         cap[d] = 0;
@@ -347,14 +355,19 @@ size_t free_hbm() {
     static std::mutex mu;
     static size_t val[kMaxDev] = {};
     static double at[kMaxDev] = {};
+    static unsigned ep[kMaxDev] = {};
     int d = 0;
     if (hipGetDevice(&d) != hipSuccess || d < 0 || d >= kMaxDev) d = 0;
     const double t = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+    const unsigned e = g_hbm_epoch.load();
     std::lock_guard<std::mutex> lk(mu);
-    if (val[d] == 0 || t - at[d] > 50.0) {
+    // re-read after 50 ms, or once a pool of this process allocated or freed since (another
+    // process's allocations are seen within the 50 ms)
+    if (val[d] == 0 || t - at[d] > 50.0 || ep[d] != e) {
         size_t f = 0, tot = 0;
         val[d] = hipMemGetInfo(&f, &tot) == hipSuccess ? f : 16ull << 30;
         at[d] = t;
+        ep[d] = e;
     }
     return val[d];
 }

@@ -6,6 +6,7 @@ the headline numbers -- to the oracle and to ground truth on every inflate case 
 messages, need-bits stalls, dictionaries, stored blocks, trailing bytes, slot edges, many rounds).
 Reference: /root/reference/src/infcodes.ts:62-301 (inflate_fast), infblocks.ts:123-628 (proc)."""
 import random
+import zlib
 
 import pytest
 
@@ -80,3 +81,29 @@ def test_distinct_slices_lane_vs_wave_records(monkeypatch):
     wave = sdz.inflate_batch(streams, [40064] * len(streams), sdz.FMT_CONTAINER)
     for a, b, p in zip(lane, wave, plain):
         assert a == b and a["data"] == p
+
+
+@pytest.mark.parametrize("lane_after", [3, 7])
+def test_wave_decoder_restart_odd_lane_after(monkeypatch, lane_after):
+    """Streams of many small blocks make the wave decoder start round 0 over on the lane decoder
+    after SDZ_WD_LANE_AFTER launch pairs; with an odd count (pairs are queued two at a time) the
+    restart still happens before any pair runs with the lane flag, and the records and bytes equal
+    the lane decoder's (k_inflate.hip run_inflate_rounds)."""
+    paradise = golden("paradiselost.txt")
+    streams, plain = [], []
+    for k, wbits in enumerate((15, -15, 31, 15)):
+        data = paradise[k * 9000:k * 9000 + 60000]
+        c = zlib.compressobj(6, zlib.DEFLATED, wbits)
+        comp = b"".join(c.compress(data[i:i + 300]) + c.flush(zlib.Z_SYNC_FLUSH) for i in range(0, len(data), 300))
+        streams.append(comp + c.flush())
+        plain.append(data)
+    streams.append(zlib.compress(paradise[:20000], 6))            # one ordinary stream beside them
+    plain.append(paradise[:20000])
+    caps = [len(p) + 64 for p in plain]
+    lane = sdz.inflate_batch(streams, caps, sdz.FMT_AUTO)
+    monkeypatch.setenv("SDZ_WDEC", "1")
+    monkeypatch.setenv("SDZ_WD_LANE_AFTER", str(lane_after))
+    wave = sdz.inflate_batch(streams, caps, sdz.FMT_AUTO)
+    for a, b, p in zip(lane, wave, plain):
+        assert a["status"] == "OK" and a["data"] == p
+        assert a == b
