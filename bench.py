@@ -783,7 +783,7 @@ def main():
                            "paradiselost.deflate inflated by the oracle C restatement, uncompressed MB/s")
 
     traffic = None
-    # the latest round's PMC traffic summary (tools/round_measure.sh writes profiles/rNN_inflate_pmc.json)
+    # the latest round's PMC traffic summary (tools/pmc_traffic.py over tools/profile_inflate.sh passes: profiles/rNN_inflate_pmc.json)
     pmcs = sorted(glob.glob(os.path.join(ROOT, "profiles", "r[0-9][0-9]_inflate_pmc.json")))
     pmc = pmcs[-1] if pmcs else ""
     if pmc and os.path.exists(pmc) and n == 65536:
