@@ -61,9 +61,18 @@ __device__ __forceinline__ uint32_t lane_slot() {   // this lane's stream slot i
 __shared__ __attribute__((aligned(16))) uint8_t g_region[IL_STREAMS * IL_REGION];
 __shared__ __attribute__((aligned(16))) uint32_t g_stage[IL_STREAMS * (IL_TSTRIDE / 4)];
 __device__ __forceinline__ uint8_t* lane_region() { return g_region + lane_slot() * IL_REGION; }
-__shared__ __attribute__((aligned(16))) uint32_t g_ring[IL_STREAMS * 18];   // 64 B + 8 B pad per lane
+#ifndef IL_REFILL2
+#define IL_REFILL2 1                  // symbol loop: one refill of up to 2 dwords per step (br_refill2)
+#endif
+#if IL_REFILL2
+#define IL_RING_DW 32                 // input ring dwords per lane (128 B + 8 B pad)
+#else
+#define IL_RING_DW 16                 // (64 B + 8 B pad)
+#endif
+#define IL_RING_STRIDE (IL_RING_DW + 2)
+__shared__ __attribute__((aligned(16))) uint32_t g_ring[IL_STREAMS * IL_RING_STRIDE];
 __device__ __forceinline__ uint32_t* lane_stage() { return g_stage + lane_slot() * (IL_TSTRIDE / 4); }
-__device__ __forceinline__ uint32_t* lane_ring() { return g_ring + lane_slot() * 18; }
+__device__ __forceinline__ uint32_t* lane_ring() { return g_ring + lane_slot() * IL_RING_STRIDE; }
 
 __constant__ uint8_t c_border[19] = { 16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15 };
 
@@ -105,6 +114,8 @@ struct Core {
 // registers every lane reads, and the wave would wait on it at each refill.
 struct Hot : Core {
     uint32_t w2, nx;                  // next dword, and the ring dword after it (read ahead)
+    uint32_t nx2;                     // (IL_REFILL2) and the one after that
+    uint32_t arp;                     // (IL_REFILL2) avail + 8 * rpos: the loop keeps avail implicit
     uint32_t rpos, wpos;              // ring bytes consumed / committed (mod 2^32)
     uint4 s0, s1;                     // loads in flight, committed at the next group
     uint32_t ns;
@@ -234,7 +245,9 @@ __device__ __forceinline__ void ring_step(Hot& L) {
         }
         L.ns = 0;
     }
+#if !IL_FLUSH_LATE
     tok_flush_hot(L);
+#endif
     uint32_t lvl = L.wpos - L.rpos;
     if (lvl <= 48 && L.vp < L.vend) {
         if (!HOT_CHECK(L, (const uint8_t*)L.vp >= L.chk_lo && (const uint8_t*)(L.vp + 2) <= L.chk_hi, 1,
@@ -243,6 +256,9 @@ __device__ __forceinline__ void ring_step(Hot& L) {
         L.ns = 1;
         if (lvl <= 32 && L.vp < L.vend) { L.s1 = *L.vp++; L.ns = 2; }
     }
+#if IL_FLUSH_LATE
+    tok_flush_hot(L);
+#endif
 }
 // the same ring step for the wave decoder (k_inflate_wdec), whose tokens have their own stage
 __device__ __forceinline__ void ring_step_wd(Hot& L) {
@@ -289,6 +305,84 @@ __device__ __forceinline__ void br_init(Hot& L, const uint8_t* p, uint64_t bitpo
     L.bo = (uint32_t)(8 * (addr & 3) + (bitpos & 7));
     br_setavail(L, bitpos, total_bits);
 }
+
+#if IL_REFILL2
+// The lane decoder's reader (IL_REFILL2): a step refills once, by 0, 1 or 2 dwords, and takes a
+// 64-bit peek, so that a length code's distance code is read from the same peek instead of after
+// a second refill.  The ring (32 dwords) holds two read-ahead dwords (nx, nx2).  Invariant: at a
+// ring step, after its commit, lvl = wpos - rpos >= 32 bytes, so every read-ahead of the next 4
+// steps (at most 6 dwords of advance, + nx2) reads committed bytes: with loads of 32 B at lvl <= 64
+// and 16 B at lvl <= 96, committed one ring step later, lvl drops by at most 24 B per 4 steps.
+__device__ __forceinline__ void br_init2(Hot& L, const uint8_t* p, uint64_t bitpos, uint64_t total_bits,
+                                         uint32_t* ring) {
+    uintptr_t addr = (uintptr_t)(p + (bitpos >> 3));
+    g_uint4* vp = (g_uint4*)(addr & ~(uintptr_t)15);
+    uint4 c0 = vp[0], c1 = vp[1], c2 = vp[2], c3 = vp[3];
+    L.ring = ring;
+    *(uint2*)(ring + 0) = make_uint2(c0.x, c0.y); *(uint2*)(ring + 2) = make_uint2(c0.z, c0.w);
+    *(uint2*)(ring + 4) = make_uint2(c1.x, c1.y); *(uint2*)(ring + 6) = make_uint2(c1.z, c1.w);
+    *(uint2*)(ring + 8) = make_uint2(c2.x, c2.y); *(uint2*)(ring + 10) = make_uint2(c2.z, c2.w);
+    *(uint2*)(ring + 12) = make_uint2(c3.x, c3.y); *(uint2*)(ring + 14) = make_uint2(c3.z, c3.w);
+    ring[IL_RING_DW] = c0.x;                          // the mirror of dword 0 (see br_refill2)
+    L.vp = vp + 4;
+    L.wpos = 64;
+    uint32_t k = (uint32_t)((addr >> 2) & 3);
+    L.w0 = ring[k];
+    L.w1 = ring[k + 1];
+    L.w2 = ring[k + 2];
+    L.nx = ring[k + 3];
+    L.nx2 = ring[k + 4];
+    L.rpos = 4 * (k + 3);                             // lvl = 64 - rpos >= 40
+    L.ns = 0;
+    L.bo = (uint32_t)(8 * (addr & 3) + (bitpos & 7));
+    br_setavail(L, bitpos, total_bits);
+    L.arp = (uint32_t)L.avail + 8u * L.rpos;
+}
+// input bits from the current position, and the explicit avail the cold code and br_consumed use
+__device__ __forceinline__ int32_t br_avail2(const Hot& L) { return (int32_t)(L.arp - 8u * L.rpos) - (int32_t)L.bo; }
+__device__ __forceinline__ void br_sync2(Hot& L) { L.avail = (int32_t)(L.arp - 8u * L.rpos); }
+// bo < 96 (a step leaves it below 32 + 48)
+__device__ __forceinline__ void br_refill2(Hot& L) {
+    const uint32_t bo = L.bo;
+    const bool c1 = bo >= 32, c2 = bo >= 64;
+    const uint32_t w0 = L.w0, w1 = L.w1, w2 = L.w2, nx = L.nx, nx2 = L.nx2;
+    L.w0 = c2 ? w2 : (c1 ? w1 : w0);
+    L.w1 = c2 ? nx : (c1 ? w2 : w1);
+    L.w2 = c2 ? nx2 : (c1 ? nx : w2);
+    L.rpos += (bo >> 3) & ~3u;                        // 4 bytes per dword moved in
+    L.bo = bo & 31u;
+    // nx and nx2 in one ds_read2_b32: dword IL_RING_DW mirrors dword 0
+    const uint32_t* q = (const uint32_t*)((const uint8_t*)L.ring + (L.rpos & (4u * IL_RING_DW - 4u)));
+    L.nx = q[0];
+    L.nx2 = q[1];
+}
+__device__ __forceinline__ void ring_step2(Hot& L) {
+    if (L.ns) {
+        uint32_t k = (L.wpos >> 2) & (IL_RING_DW - 1);
+        *(uint2*)(L.ring + k) = make_uint2(L.s0.x, L.s0.y);
+        *(uint2*)(L.ring + k + 2) = make_uint2(L.s0.z, L.s0.w);
+        L.ring[k == 0 ? IL_RING_DW : IL_RING_DW + 1] = L.s0.x;   // mirror of dword 0 (else the pad)
+        L.wpos += 16;
+        if (L.ns == 2) {
+            k = (L.wpos >> 2) & (IL_RING_DW - 1);
+            *(uint2*)(L.ring + k) = make_uint2(L.s1.x, L.s1.y);
+            *(uint2*)(L.ring + k + 2) = make_uint2(L.s1.z, L.s1.w);
+            L.ring[k == 0 ? IL_RING_DW : IL_RING_DW + 1] = L.s1.x;
+            L.wpos += 16;
+        }
+        L.ns = 0;
+    }
+    tok_flush_hot(L);
+    uint32_t lvl = L.wpos - L.rpos;
+    if (lvl <= 96 && L.vp < L.vend) {
+        if (!HOT_CHECK(L, (const uint8_t*)L.vp >= L.chk_lo && (const uint8_t*)(L.vp + 2) <= L.chk_hi, 1,
+                       (uintptr_t)L.vp, (uintptr_t)L.vend)) return;
+        L.s0 = *L.vp++;
+        L.ns = 1;
+        if (lvl <= 64 && L.vp < L.vend) { L.s1 = *L.vp++; L.ns = 2; }
+    }
+}
+#endif
 
 // ------------------------------------------------------------------ canonical trees
 
@@ -366,8 +460,66 @@ __device__ __forceinline__ uint32_t tsel_bs(const HTree& T, uint32_t rc) {
     const uint32_t m4 = ge(bfi(m3, k3, k1));
     return bfi(m4, r2, r1);
 }
+#ifndef IL_TSEL_ASM
+#define IL_TSEL_ASM 1
+#endif
+#if IL_TSEL_ASM
+// tsel_bs<true> as one asm block: as separate statements the compiler put an s_nop between an asm
+// statement and the next one reading its result (it cannot see inside them), 7 per distance decode
+__device__ __forceinline__ uint32_t tsel_hot_asm(const HTree& T, uint32_t rc) {
+    uint32_t r, m, lx, p1, p2, p3, p4, p5, p6, p7, p8, a1, a2, a3, a5, a6, a7;
+    asm("v_sub_u32 %[m], %[L8], %[rc]\n\t"
+        "v_ashrrev_i32 %[m], 31, %[m]\n\t"
+        "v_bfi_b32 %[lx], %[m], %[L12], %[L4]\n\t"
+        "v_bfi_b32 %[p1], %[m], %[P9], %[P1]\n\t"
+        "v_bfi_b32 %[p2], %[m], %[P10], %[P2]\n\t"
+        "v_bfi_b32 %[p3], %[m], %[P11], %[P3]\n\t"
+        "v_bfi_b32 %[p4], %[m], %[P12], %[P4]\n\t"
+        "v_bfi_b32 %[p5], %[m], %[P13], %[P5]\n\t"
+        "v_bfi_b32 %[p6], %[m], %[P14], %[P6]\n\t"
+        "v_bfi_b32 %[p7], %[m], %[P15], %[P7]\n\t"
+        "v_bfi_b32 %[p8], %[m], %[P16], %[P8]\n\t"
+        "v_bfi_b32 %[a1], %[m], %[L9], %[L1]\n\t"
+        "v_bfi_b32 %[a2], %[m], %[L10], %[L2]\n\t"
+        "v_bfi_b32 %[a3], %[m], %[L11], %[L3]\n\t"
+        "v_bfi_b32 %[a5], %[m], %[L13], %[L5]\n\t"
+        "v_bfi_b32 %[a6], %[m], %[L14], %[L6]\n\t"
+        "v_bfi_b32 %[a7], %[m], %[L15], %[L7]\n\t"
+        "v_sub_u32 %[m], %[lx], %[rc]\n\t"          // level 2
+        "v_ashrrev_i32 %[m], 31, %[m]\n\t"
+        "v_bfi_b32 %[p1], %[m], %[p5], %[p1]\n\t"
+        "v_bfi_b32 %[p2], %[m], %[p6], %[p2]\n\t"
+        "v_bfi_b32 %[p3], %[m], %[p7], %[p3]\n\t"
+        "v_bfi_b32 %[p4], %[m], %[p8], %[p4]\n\t"
+        "v_bfi_b32 %[lx], %[m], %[a6], %[a2]\n\t"
+        "v_bfi_b32 %[a1], %[m], %[a5], %[a1]\n\t"
+        "v_bfi_b32 %[a3], %[m], %[a7], %[a3]\n\t"
+        "v_sub_u32 %[m], %[lx], %[rc]\n\t"          // level 3
+        "v_ashrrev_i32 %[m], 31, %[m]\n\t"
+        "v_bfi_b32 %[lx], %[m], %[a3], %[a1]\n\t"
+        "v_bfi_b32 %[p1], %[m], %[p3], %[p1]\n\t"
+        "v_bfi_b32 %[p2], %[m], %[p4], %[p2]\n\t"
+        "v_sub_u32 %[m], %[lx], %[rc]\n\t"          // level 4
+        "v_ashrrev_i32 %[m], 31, %[m]\n\t"
+        "v_bfi_b32 %[r], %[m], %[p2], %[p1]"
+        : [r] "=&v"(r), [m] "=&v"(m), [lx] "=&v"(lx), [p1] "=&v"(p1), [p2] "=&v"(p2), [p3] "=&v"(p3),
+          [p4] "=&v"(p4), [p5] "=&v"(p5), [p6] "=&v"(p6), [p7] "=&v"(p7), [p8] "=&v"(p8), [a1] "=&v"(a1),
+          [a2] "=&v"(a2), [a3] "=&v"(a3), [a5] "=&v"(a5), [a6] "=&v"(a6), [a7] "=&v"(a7)
+        : [rc] "v"(rc), [L1] "v"(T.lim[1]), [L2] "v"(T.lim[2]), [L3] "v"(T.lim[3]), [L4] "v"(T.lim[4]),
+          [L5] "v"(T.lim[5]), [L6] "v"(T.lim[6]), [L7] "v"(T.lim[7]), [L8] "v"(T.lim[8]), [L9] "v"(T.lim[9]),
+          [L10] "v"(T.lim[10]), [L11] "v"(T.lim[11]), [L12] "v"(T.lim[12]), [L13] "v"(T.lim[13]),
+          [L14] "v"(T.lim[14]), [L15] "v"(T.lim[15]), [P1] "v"(T.pk[1]), [P2] "v"(T.pk[2]), [P3] "v"(T.pk[3]),
+          [P4] "v"(T.pk[4]), [P5] "v"(T.pk[5]), [P6] "v"(T.pk[6]), [P7] "v"(T.pk[7]), [P8] "v"(T.pk[8]),
+          [P9] "v"(T.pk[9]), [P10] "v"(T.pk[10]), [P11] "v"(T.pk[11]), [P12] "v"(T.pk[12]),
+          [P13] "v"(T.pk[13]), [P14] "v"(T.pk[14]), [P15] "v"(T.pk[15]), [P16] "v"(T.pk[16]));
+    return r;
+}
+#define tsel tsel_bs<false>
+#define tsel_hot tsel_hot_asm
+#else
 #define tsel tsel_bs<false>
 #define tsel_hot tsel_bs<true>
+#endif
 #else
 #define tsel_hot tsel
 #endif
@@ -579,13 +731,27 @@ __device__ __forceinline__ void tok_flush_lits(C& L) {
 #ifndef IL_FULL_AT_RING
 #define IL_FULL_AT_RING 1                 // token room checked at the ring step (C2 decode -2 %, distinct -3 %)
 #endif
+#ifndef IL_UNCHECKED_RUN
+#define IL_UNCHECKED_RUN 1                // 4 steps without bit / room checks when the ring step allows
+#endif
 #ifndef IL_BF_TOKENS
 #define IL_BF_TOKENS 1
+#endif
+#ifndef IL_OPEN_SLOT
+#define IL_OPEN_SLOT 1                    // symbol loop: the open literal token kept in its stage slot
 #endif
 template <class C>
 __device__ __forceinline__ void tok_lit(C& L, uint32_t b) {
     L.litw |= b << (8 * L.nlit);
-    if constexpr (IL_BF_TOKENS && IL_UNIFORM_FLUSH && std::is_same<C, Hot>::value) {
+    if constexpr (IL_OPEN_SLOT && IL_UNIFORM_FLUSH && std::is_same<C, Hot>::value) {
+        // the token of the pending literals is stored in slot ntok & 31 as it grows (not yet
+        // counted, so no flush takes it); the third literal counts it, and a match only counts it
+        L.ts[L.ntok & (IL_TSTAGE - 1)] = (L.nlit << 24) | L.litw;
+        const bool full = ++L.nlit == 3;
+        L.ntok += full ? 1u : 0u;
+        L.litw = full ? 0u : L.litw;
+        L.nlit = full ? 0u : L.nlit;
+    } else if constexpr (IL_BF_TOKENS && IL_UNIFORM_FLUSH && std::is_same<C, Hot>::value) {
         // symbol loop: no branch -- a store that does not push goes to the stage's spare slot
         const bool full = ++L.nlit == 3;
         L.ts[full ? (L.ntok & (IL_TSTAGE - 1)) : IL_TSTAGE] = (2u << 24) | L.litw;
@@ -598,7 +764,13 @@ __device__ __forceinline__ void tok_lit(C& L, uint32_t b) {
 }
 template <class C>
 __device__ __forceinline__ void tok_match(C& L, uint32_t len, uint32_t dist) {
-    if constexpr (IL_BF_TOKENS && IL_UNIFORM_FLUSH && std::is_same<C, Hot>::value) {
+    if constexpr (IL_OPEN_SLOT && IL_UNIFORM_FLUSH && std::is_same<C, Hot>::value) {
+        L.ntok += L.nlit != 0 ? 1u : 0u;                  // (its token is in its slot: tok_lit)
+        L.ts[L.ntok & (IL_TSTAGE - 1)] = 0x80000000u | ((len - 3u) << 16) | (dist - 1u);
+        L.ntok++;
+        L.nlit = 0;
+        L.litw = 0;
+    } else if constexpr (IL_BF_TOKENS && IL_UNIFORM_FLUSH && std::is_same<C, Hot>::value) {
         const bool hl = L.nlit != 0;
         L.ts[hl ? (L.ntok & (IL_TSTAGE - 1)) : IL_TSTAGE] = ((L.nlit - 1u) << 24) | L.litw;
         L.ntok += hl ? 1u : 0u;
@@ -893,6 +1065,9 @@ __device__ __forceinline__ uint32_t dist_base(uint32_t ds, uint32_t& e) {
 
 // decode one literal/length symbol (+ its distance): the fast path, taken while at
 // least 64 input bits remain (one step reads at most 48)
+// CHK = false: the caller has checked for the next 4 steps what the room checks test (room for 4
+// matches), so a step has none (IL_UNCHECKED_RUN)
+template <bool CHK = true>
 __device__ __forceinline__ void fast_step(Hot& L, const HTree& LL, const HTree& DD, const uint8_t* region) {
     uint32_t pw = br_refill_peek(L);
     uint32_t rc = __builtin_bitreverse32(pw) >> 17;
@@ -902,7 +1077,7 @@ __device__ __forceinline__ void fast_step(Hot& L, const HTree& LL, const HTree& 
     uint32_t b = region[idx];
     L.bo += len;
     if (idx < (int32_t)((v >> 5) & 511u)) {               // literal
-        if (L.room == 0) { lane_fail(L, SDZ_OUT_OVERFLOW, 0); return; }
+        if (CHK && L.room == 0) { lane_fail(L, SDZ_OUT_OVERFLOW, 0); return; }
         L.room--;
         tok_lit(L, b);
         return;
@@ -926,10 +1101,73 @@ __device__ __forceinline__ void fast_step(Hot& L, const HTree& LL, const HTree& 
     uint32_t dist = dist_base(ds, e);
     dist += (pw >> len) & ((1u << e) - 1u);
     L.bo += len + e;
-    if (L.room < mlen) { lane_fail(L, SDZ_OUT_OVERFLOW, 0); return; }
+    if (CHK && L.room < mlen) { lane_fail(L, SDZ_OUT_OVERFLOW, 0); return; }
     L.room -= mlen;
     tok_match(L, mlen, dist);
 }
+#if IL_REFILL2
+// fast_step on the IL_REFILL2 reader: one refill, a 64-bit peek (lo, hi) at the symbol's first
+// bit; the length's extra bits (<= 15 + 5 bits in) and the distance code with its extra bits
+// (<= 15 + 13 bits from its start) come from it
+// A failure in the symbol loop sets the mode and the message only (zm 0: output overflow); the
+// status follows from them when the epoch ends (hot_fix_status): one value less to merge per step.
+__device__ __forceinline__ void hot_fail(Hot& L, int zm) { L.mode = LM_DONE; L.zmsg = zm; }
+__device__ __forceinline__ void hot_fix_status(Hot& L) {
+    if (L.mode == LM_DONE && L.status == SDZ_OK) L.status = L.zmsg ? SDZ_DATA_ERROR : SDZ_OUT_OVERFLOW;
+}
+template <bool CHK = true>
+__device__ __forceinline__ void fast_step2(Hot& L, const HTree& LL, const HTree& DD, const uint8_t* region) {
+    br_refill2(L);
+    const uint32_t lo = __builtin_amdgcn_alignbit(L.w1, L.w0, L.bo);
+    const uint32_t hi = __builtin_amdgcn_alignbit(L.w2, L.w1, L.bo);
+    uint32_t rc = __builtin_bitreverse32(lo) >> 17;
+    uint32_t v = tsel_hot(LL, rc);
+    const int32_t idx = pk_rank(v, rc);
+    const uint32_t len = 15u - (v & 15u);
+    const uint32_t b = region[idx];
+    if (idx < (int32_t)((v >> 5) & 511u)) {               // literal
+        L.bo += len;
+        if (CHK && L.room == 0) { hot_fail(L, 0); return; }
+        L.room--;
+        tok_lit(L, b);
+        return;
+    }
+    // a length code -- or the end of block or an invalid code, tested once with the distance
+    // code's validity below (the distance decode of those is discarded)
+    uint32_t e;
+    uint32_t mlen = len_base(b, e);
+    mlen += (lo >> len) & ((1u << e) - 1u);
+    const uint32_t s = len + e;                           // <= 20
+    const uint32_t pd = __builtin_amdgcn_alignbit(hi, lo, s);
+    rc = __builtin_bitreverse32(pd) >> 17;
+    v = tsel_hot(DD, rc);
+    const int32_t dx = pk_rank(v, rc);
+    const uint32_t dlen = 15u - (v & 15u);
+    const uint32_t ds = region[IL_DSYM + dx];
+    uint32_t de;
+    uint32_t dist = dist_base(ds, de);
+    dist += (pd >> dlen) & ((1u << de) - 1u);
+    const bool badl = b - 1u >= 29u || idx >= 288;
+    if (badl || dx >= (int32_t)((v >> 5) & 511u)) {
+        if (!badl) { L.bo += s; hot_fail(L, ZM_INVALID_DIST); return; }
+        L.bo += len;
+        if (b == 0 && idx < 288) L.mode = L.last ? LM_TRAILER : LM_TYPE;
+        else hot_fail(L, ZM_INVALID_LITLEN);
+        return;
+    }
+    L.bo += s + dlen + de;
+    if (CHK && L.room < mlen) { hot_fail(L, 0); return; }
+    L.room -= mlen;
+    tok_match(L, mlen, dist);
+}
+#define IL_FAST_STEP fast_step2
+#define IL_RING_STEP ring_step2
+#define IL_BR_INIT br_init2
+#else
+#define IL_FAST_STEP fast_step
+#define IL_RING_STEP ring_step
+#define IL_BR_INIT br_init
+#endif
 
 // the same with the reference's end-of-input behaviour: every read checks the
 // bits available, and a code is only resolved once the reference's table walk
@@ -1187,7 +1425,7 @@ __device__ __forceinline__ void hot_load(Hot& H, HTree& LL, HTree& DD, const DSa
         }
     }
 #endif
-    br_init(H, inp, S->bitpos, ilen * 8, lane_ring());
+    IL_BR_INIT(H, inp, S->bitpos, ilen * 8, lane_ring());
     H.vend = (g_uint4*)(((uintptr_t)(inp + ilen) + 15) & ~(uintptr_t)15);
     H.pos0 = S->pos;
     uint64_t r = cap - H.pos0;
@@ -1211,9 +1449,14 @@ __device__ __forceinline__ void hot_save(const Hot& H, DSave* S) {
 // OUT_OVERFLOW.  (Leaving those symbols to the cold code too, so that the loop needs no room
 // checks, was measured: the extra cold epoch at every stream's end cost 3 ms of the
 // distinct streams' 14.)
+#if IL_REFILL2
+#define IL_HOT_AVAIL br_avail2
+#else
+#define IL_HOT_AVAIL br_avail
+#endif
 template <bool STREAM>
 __device__ __forceinline__ bool hot_ready(const Hot& H) {
-    return H.mode == LM_CODES && !H.full && br_avail(H) >= 64 && (!STREAM || H.room >= 258);
+    return H.mode == LM_CODES && !H.full && IL_HOT_AVAIL(H) >= 64 && (!STREAM || H.room >= 258);
 }
 template <int MODE>
 __device__ __forceinline__ bool can_hot(const DSave* S, uint64_t tbits, uint64_t cap) {
@@ -1230,9 +1473,16 @@ __device__ __forceinline__ bool can_hot(const DSave* S, uint64_t tbits, uint64_t
 #else
 #define IL_HOT_ATTR __noinline__
 #endif
+#ifdef SDZ_TIMING
+#define IL_DBG_PARAM , unsigned long long* dbg
+#define IL_DBG_ARG , (timed ? A.dbg : nullptr)
+#else
+#define IL_DBG_PARAM
+#define IL_DBG_ARG
+#endif
 template <bool STREAM>
 __device__ IL_HOT_ATTR void hot_epoch(DSave* S, const uint8_t* inp, uint64_t ilen, uint64_t cap,
-                                       uint32_t* tb, uint32_t tcap, bool hot, int stop) {
+                                       uint32_t* tb, uint32_t tcap, bool hot, int stop IL_DBG_PARAM) {
     Hot H;
     HTree LL, DD;
     const uint8_t* region = lane_region();
@@ -1241,14 +1491,19 @@ __device__ IL_HOT_ATTR void hot_epoch(DSave* S, const uint8_t* inp, uint64_t ile
     H.mode = LM_DONE; H.full = true; H.ntok = 0; H.nfl = 0; H.tcap = tcap; H.tb = tb; H.ts = lane_stage();
     H.avail = 0; H.bo = 0; H.avail0 = 0; H.base_bit = 0; H.room = H.room0 = 0; H.pos0 = 0;
     H.last = 0; H.status = SDZ_OK; H.zmsg = 0; H.litw = 0; H.nlit = 0;
-    H.w0 = H.w1 = H.w2 = H.nx = 0; H.rpos = H.wpos = 0; H.ns = 0;
+    H.w0 = H.w1 = H.w2 = H.nx = H.nx2 = 0; H.rpos = H.wpos = 0; H.ns = 0; H.arp = 0;
     H.s0 = H.s1 = make_uint4(0u, 0u, 0u, 0u);
     H.vp = H.vend = (g_uint4*)inp; H.ring = lane_ring();
 #ifdef IL_HOT_CHECK
     H.chk_lo = H.chk_hi = nullptr; H.chk_id = ~0u;
 #endif
-    if (hot) hot_load(H, LL, DD, S, inp, ilen, cap);
-    else {
+    if (hot) {
+        hot_load(H, LL, DD, S, inp, ilen, cap);
+#if IL_OPEN_SLOT && IL_UNIFORM_FLUSH
+        // literals left pending by the cold code: their token into its slot (see tok_lit)
+        if (H.nlit) H.ts[H.ntok & (IL_TSTAGE - 1)] = ((H.nlit - 1u) << 24) | H.litw;
+#endif
+    } else {
 #pragma unroll
         for (int k = 0; k < 16; ++k) { LL.lim[k] = DD.lim[k] = 0; }
 #pragma unroll
@@ -1258,12 +1513,21 @@ __device__ IL_HOT_ATTR void hot_epoch(DSave* S, const uint8_t* inp, uint64_t ile
 #pragma unroll
     for (int k = 1; k <= 15; ++k) { LL.lim[k] -= 1u; DD.lim[k] -= 1u; }   // tsel_hot's form
 #endif
+#ifdef SDZ_TIMING
+    unsigned long long t_ring = 0, n_ring = 0;   // development: wave clocks spent in the ring step
+#endif
     do {
         // every lane runs the ring step: an idle lane's (vp == vend, ns 0, no tokens) changes
         // nothing.  Under `if (hot)` its reader fields were dead on the idle path, which LLVM then
         // fed as undef into the loop's phis (seen in the IR of the hot_epoch-inlined variant that
         // faulted in round 4); here every value the loop reads is defined for every lane
-        ring_step(H);
+#ifdef SDZ_TIMING
+        const unsigned long long t_a = dbg ? clock64() : 0;
+#endif
+        IL_RING_STEP(H);
+#ifdef SDZ_TIMING
+        if (dbg) { t_ring += clock64() - t_a; ++n_ring; }
+#endif
 #if IL_FULL_AT_RING
         // token room checked once per 4 steps: at most 2 tokens per step
         if (H.ntok + 3u + 8u > H.tcap) H.full = true;
@@ -1271,20 +1535,41 @@ __device__ IL_HOT_ATTR void hot_epoch(DSave* S, const uint8_t* inp, uint64_t ile
 #ifndef IL_REP_UNROLL
 #define IL_REP_UNROLL 4                   // the 4 steps between ring steps, unrolled (C2 decode -3 %)
 #endif
+#if IL_UNCHECKED_RUN && IL_FULL_AT_RING
+        // when every lane that can step has the input bits and the output room for 4 steps of up
+        // to 48 bits and 258 bytes each, the 4 steps run without their bit and room checks; a
+        // step then only tests that its lane is still in the block (an end of block or an error
+        // in an earlier step ends it)
+        const bool rdy = hot_ready<STREAM>(H);
+        if (!__ballot(rdy && !(IL_HOT_AVAIL(H) >= 64 + 3 * 48 && H.room >= 4u * 258u))) {
+#pragma unroll
+            for (int rep = 0; rep < 4; ++rep)
+                if (rdy && H.mode == LM_CODES) IL_FAST_STEP<false>(H, LL, DD, region);
+        } else
+#endif
+        {
 #pragma unroll IL_REP_UNROLL
         for (int rep = 0; rep < 4; ++rep) {
             if (hot_ready<STREAM>(H)) {
-                fast_step(H, LL, DD, region);
+                IL_FAST_STEP(H, LL, DD, region);
 #if !IL_FULL_AT_RING
                 if (H.ntok + 3 > H.tcap) H.full = true;
 #endif
             }
         }
+        }
     } while (__popcll(__ballot(hot_ready<STREAM>(H))) > stop);
     // back to the cold code's invariant: everything below the open 32-token line in HBM
     // (nfl >= ntok - 15 after this, and a multiple of 16)
     tok_flush_hot(H);
+#if IL_REFILL2
+    br_sync2(H);
+    hot_fix_status(H);
+#endif
     if (hot) hot_save(H, S);
+#ifdef SDZ_TIMING
+    if (dbg) { atomicAdd(&dbg[12], t_ring); atomicAdd(&dbg[13], n_ring); }
+#endif
 }
 
 template <int MODE>
@@ -1313,7 +1598,7 @@ __device__ __forceinline__ void epochs(const InflateArgs& A, DSave* S, const uin
         uint64_t hm = __ballot(hot);
         if (hm == 0) break;
         int nhot = __popcll(hm);
-        hot_epoch<MODE == 1>(S, inp, ilen, cap, tb, tcap, hot, nhot - (nhot >= 16 ? nhot >> IL_STOP_SHIFT : 1));
+        hot_epoch<MODE == 1>(S, inp, ilen, cap, tb, tcap, hot, nhot - (nhot >= 16 ? nhot >> IL_STOP_SHIFT : 1) IL_DBG_ARG);
 #ifdef SDZ_TIMING
         if (timed) { const unsigned long long t = clock64(); th += t - t0; t0 = t; ++nh; }
 #endif
@@ -1334,7 +1619,7 @@ __global__ __launch_bounds__(IL_THREADS, 1) void k_inflate_decode(InflateArgs A,
         // read before a write sees the same value whatever ran on the CU before
         for (uint32_t k = 0; k < IL_REGION / 4; ++k) ((uint32_t*)region)[k] = 0xA5A5A5A5u;
         for (uint32_t k = 0; k < IL_TSTRIDE / 4; ++k) ts[k] = 0xA5A5A5A5u;
-        for (uint32_t k = 0; k < 18; ++k) lane_ring()[k] = 0xA5A5A5A5u;
+        for (uint32_t k = 0; k < IL_RING_STRIDE; ++k) lane_ring()[k] = 0xA5A5A5A5u;
     }
 #endif
     uint32_t gid = blockIdx.x * IL_STREAMS + lane_slot();
