@@ -731,6 +731,9 @@ __device__ __forceinline__ void tok_flush_lits(C& L) {
 #ifndef IL_FULL_AT_RING
 #define IL_FULL_AT_RING 1                 // token room checked at the ring step (C2 decode -2 %, distinct -3 %)
 #endif
+#ifndef IL_TWO_LOOPS
+#define IL_TWO_LOOPS 1                    // the unchecked 4-step loop, then the checked one (hot_epoch)
+#endif
 #ifndef IL_UNCHECKED_RUN
 #define IL_UNCHECKED_RUN 1                // 4 steps without bit / room checks when the ring step allows
 #endif
@@ -1473,16 +1476,9 @@ __device__ __forceinline__ bool can_hot(const DSave* S, uint64_t tbits, uint64_t
 #else
 #define IL_HOT_ATTR __noinline__
 #endif
-#ifdef SDZ_TIMING
-#define IL_DBG_PARAM , unsigned long long* dbg
-#define IL_DBG_ARG , (timed ? A.dbg : nullptr)
-#else
-#define IL_DBG_PARAM
-#define IL_DBG_ARG
-#endif
 template <bool STREAM>
 __device__ IL_HOT_ATTR void hot_epoch(DSave* S, const uint8_t* inp, uint64_t ilen, uint64_t cap,
-                                       uint32_t* tb, uint32_t tcap, bool hot, int stop IL_DBG_PARAM) {
+                                       uint32_t* tb, uint32_t tcap, bool hot, int stop) {
     Hot H;
     HTree LL, DD;
     const uint8_t* region = lane_region();
@@ -1513,27 +1509,44 @@ __device__ IL_HOT_ATTR void hot_epoch(DSave* S, const uint8_t* inp, uint64_t ile
 #pragma unroll
     for (int k = 1; k <= 15; ++k) { LL.lim[k] -= 1u; DD.lim[k] -= 1u; }   // tsel_hot's form
 #endif
-#ifdef SDZ_TIMING
-    unsigned long long t_ring = 0, n_ring = 0;   // development: wave clocks spent in the ring step
+#ifndef IL_REP_UNROLL
+#define IL_REP_UNROLL 4                   // the 4 steps between ring steps, unrolled (C2 decode -3 %)
 #endif
-    do {
-        // every lane runs the ring step: an idle lane's (vp == vend, ns 0, no tokens) changes
-        // nothing.  Under `if (hot)` its reader fields were dead on the idle path, which LLVM then
-        // fed as undef into the loop's phis (seen in the IR of the hot_epoch-inlined variant that
-        // faulted in round 4); here every value the loop reads is defined for every lane
-#ifdef SDZ_TIMING
-        const unsigned long long t_a = dbg ? clock64() : 0;
-#endif
+    // every lane runs the ring step: an idle lane's (vp == vend, ns 0, no tokens) changes
+    // nothing.  Under `if (hot)` its reader fields were dead on the idle path, which LLVM then
+    // fed as undef into the loop's phis (seen in the IR of the hot_epoch-inlined variant that
+    // faulted in round 4); here every value the loop reads is defined for every lane
+#if IL_UNCHECKED_RUN && IL_FULL_AT_RING && IL_TWO_LOOPS
+    // Two loops in sequence: the first runs 4 steps without their bit and room checks as long as
+    // every lane that can step has the input bits and the output room for 4 steps of up to 48 bits
+    // and 258 bytes each (a step then only tests that its lane is still in the block); once some lane
+    // has not, the rest of the epoch runs checked steps.  (One loop with both bodies merged their
+    // values at its back edge: ~20 register copies per 4 steps.)
+    bool more = true;
+    for (;;) {
         IL_RING_STEP(H);
-#ifdef SDZ_TIMING
-        if (dbg) { t_ring += clock64() - t_a; ++n_ring; }
-#endif
+        if (H.ntok + 3u + 8u > H.tcap) H.full = true;     // token room, once per 4 steps: <= 2 tokens per step
+        const bool rdy = hot_ready<STREAM>(H);
+        if (__ballot(rdy && !(IL_HOT_AVAIL(H) >= 64 + 3 * 48 && H.room >= 4u * 258u))) break;
+#pragma unroll
+        for (int rep = 0; rep < 4; ++rep)
+            if (rdy && H.mode == LM_CODES) IL_FAST_STEP<false>(H, LL, DD, region);
+        if (__popcll(__ballot(hot_ready<STREAM>(H))) <= stop) { more = false; break; }
+    }
+    while (more) {
+#pragma unroll IL_REP_UNROLL
+        for (int rep = 0; rep < 4; ++rep)
+            if (hot_ready<STREAM>(H)) IL_FAST_STEP(H, LL, DD, region);
+        if (__popcll(__ballot(hot_ready<STREAM>(H))) <= stop) break;
+        IL_RING_STEP(H);
+        if (H.ntok + 3u + 8u > H.tcap) H.full = true;
+    }
+#else
+    do {
+        IL_RING_STEP(H);
 #if IL_FULL_AT_RING
         // token room checked once per 4 steps: at most 2 tokens per step
         if (H.ntok + 3u + 8u > H.tcap) H.full = true;
-#endif
-#ifndef IL_REP_UNROLL
-#define IL_REP_UNROLL 4                   // the 4 steps between ring steps, unrolled (C2 decode -3 %)
 #endif
 #if IL_UNCHECKED_RUN && IL_FULL_AT_RING
         // when every lane that can step has the input bits and the output room for 4 steps of up
@@ -1559,6 +1572,7 @@ __device__ IL_HOT_ATTR void hot_epoch(DSave* S, const uint8_t* inp, uint64_t ile
         }
         }
     } while (__popcll(__ballot(hot_ready<STREAM>(H))) > stop);
+#endif
     // back to the cold code's invariant: everything below the open 32-token line in HBM
     // (nfl >= ntok - 15 after this, and a multiple of 16)
     tok_flush_hot(H);
@@ -1567,9 +1581,6 @@ __device__ IL_HOT_ATTR void hot_epoch(DSave* S, const uint8_t* inp, uint64_t ile
     hot_fix_status(H);
 #endif
     if (hot) hot_save(H, S);
-#ifdef SDZ_TIMING
-    if (dbg) { atomicAdd(&dbg[12], t_ring); atomicAdd(&dbg[13], n_ring); }
-#endif
 }
 
 template <int MODE>
@@ -1598,7 +1609,7 @@ __device__ __forceinline__ void epochs(const InflateArgs& A, DSave* S, const uin
         uint64_t hm = __ballot(hot);
         if (hm == 0) break;
         int nhot = __popcll(hm);
-        hot_epoch<MODE == 1>(S, inp, ilen, cap, tb, tcap, hot, nhot - (nhot >= 16 ? nhot >> IL_STOP_SHIFT : 1) IL_DBG_ARG);
+        hot_epoch<MODE == 1>(S, inp, ilen, cap, tb, tcap, hot, nhot - (nhot >= 16 ? nhot >> IL_STOP_SHIFT : 1));
 #ifdef SDZ_TIMING
         if (timed) { const unsigned long long t = clock64(); th += t - t0; t0 = t; ++nh; }
 #endif
