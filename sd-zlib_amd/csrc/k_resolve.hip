@@ -319,6 +319,9 @@ __device__ __forceinline__ void lds_mskor_at(uint32_t* base32, uint32_t i, uint3
 #ifndef RS_MW
 #define RS_MW 2
 #endif
+#ifndef RS_READ_ALL
+#define RS_READ_ALL 1
+#endif
 // GEN: 0 -- no lane needs the general path (the caller routed them elsewhere); 1 -- through the
 // out-of-line emit_tokens; 2 -- emit_tokens inlined (one call site per kernel: no callee-saved
 // registers forced around a call)
@@ -345,12 +348,17 @@ __device__ __forceinline__ void emit_msk(uint8_t* ring, uint8_t* fmap, bool act,
     const uint32_t lw = lb * 0x01010101u;
     // a literal: x0 = t (kd = 0), or x0 = 0, x1 = t with shift 4 - kd
     const uint32_t kk = lit ? (4u - kd) & 3u : k;
-    uint32_t x[MW + 1];
+    uint32_t x[MW + 1], r[MW + 1];
 #pragma unroll
-    for (int j = 0; j <= MW; ++j) {
-        const uint32_t r = ring32[xa + (uint32_t)j];
-        x[j] = !lit ? r : j == 0 ? (kd ? 0u : t) : j == 1 ? (kd ? t : 0u) : 0u;
-    }
+    for (int j = 0; j <= MW; ++j) r[j] = ring32[xa + (uint32_t)j];
+#if RS_READ_ALL
+    // every lane reads (a literal lane its dummy dwords): without this the compiler sank the
+    // reads under `if (!lit)`, an exec-mask save / branch / restore around each of them
+    if constexpr (MW == 2) asm volatile("" : "+v"(r[0]), "+v"(r[1]), "+v"(r[2]));
+#endif
+#pragma unroll
+    for (int j = 0; j <= MW; ++j)
+        x[j] = !lit ? r[j] : j == 0 ? (kd ? 0u : t) : j == 1 ? (kd ? t : 0u) : 0u;
     const uint32_t lom = 0xffffffffu << (8 * kd);
     static_for<0, MW>([&](auto jc) {                   // each dword's data, then its finality
         constexpr int j = decltype(jc)::value;
@@ -410,6 +418,21 @@ __device__ __forceinline__ bool map_all(const uint8_t* fmap, bool act, uint32_t 
     const uint32_t n = act ? hi - lo : 0u;               // modulo 2^32: positions are low bits
     const uint32_t m0 = lo >> 2, nw = n ? ((lo & 3u) + n + 3u) >> 2 : 0u;
     const uint32_t bt = ((lo + n - 1u) & 3u) + 1u;       // bytes used of the last dword
+#if RS_READ_ALL
+    // byte masks without selects or branches: lanes past their last dword read map dword 0 and
+    // mask it out (the compiler had turned the selects around the read into an exec-mask branch)
+    const uint32_t lm = ~0u << (8 * (lo & 3u));          // the first dword's bytes
+    const uint32_t hm = bt == 4u ? ~0u : (1u << (8 * bt)) - 1u;   // the last dword's
+    for (uint32_t i = 0; __ballot(i < nw); ++i) {
+        const uint32_t m = m0 + i;
+        const uint32_t in = (uint32_t)((int32_t)(i - nw) >> 31);        // i < nw
+        const uint32_t more = (uint32_t)((int32_t)(i + 1u - nw) >> 31); // i + 1 < nw
+        const uint32_t mask = in & (more | hm) & (i == 0 ? lm : ~0u);
+        uint32_t v = fmap32[m & (RS_BM / 4 - 1) & in];
+        asm volatile("" : "+v"(v));
+        miss |= (v ^ (lap_of(4 * m) * 0x01010101u)) & mask;
+    }
+#else
     for (uint32_t i = 0; __ballot(i < nw); ++i) {
         const uint32_t m = m0 + i;
         const uint32_t bl = i == 0 ? lo & 3u : 0u, bh = i + 1 == nw ? bt : 4u;
@@ -417,6 +440,7 @@ __device__ __forceinline__ bool map_all(const uint8_t* fmap, bool act, uint32_t 
         const uint32_t v = fmap32[i < nw ? m & (RS_BM / 4 - 1) : 0u];
         miss |= (v ^ (lap_of(4 * m) * 0x01010101u)) & mask;
     }
+#endif
     return miss == 0;
 }
 #ifndef RS_WAKE
