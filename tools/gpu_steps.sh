@@ -11,6 +11,8 @@
 #   bench[:ARGS]        bench.py with the given arguments (commas become spaces)
 #   kt:<mode>[:ENV=V,...]  rocprofv3 kernel trace + stats of run_c2.py --mode <mode> (into kt_<mode>_<step>)
 #   pmc:<mode>:<set>    rocprofv3 --pmc pass <set> (sq1 sq2 sq3 fetch write) of run_c2.py --mode <mode>
+#   ktbench[:ARGS]      rocprofv3 kernel trace + stats of bench.py with the given arguments (into kt_bench_<step>)
+#   smoke               __graft_entry__.smoke()
 #   configs             tools/run_configs.py (C4 / C5)
 #   node                tests/node/smoke.mjs (the drop-in facade)
 # Outputs under gpurun_out/$OUT/.
@@ -55,6 +57,10 @@ for st in "$@"; do
          rm -rf $O/pmc_${mode}_$set_
          timeout -s KILL 240 rocprofv3 --pmc ${PMC[$set_]} -d $O/pmc_${mode}_$set_ -o run --output-format csv -- \
             python3 tools/run_c2.py --mode $mode --steps 1 > $log 2>&1 ;;
+    ktbench) d=$O/kt_bench_$n; rm -rf $d
+        timeout -k 10 900 rocprofv3 --kernel-trace --stats -d $d -o run --output-format csv -- \
+            python3 bench.py ${arg//,/ } > $log 2> $log.err ;;
+    smoke) timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke(); print('smoke OK')" > $log 2>&1 ;;
     configs) timeout -k 10 600 python3 tools/run_configs.py $arg > $log 2>&1 ;;
     *) echo "unknown step $st"; exit 2 ;;
   esac
