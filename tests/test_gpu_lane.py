@@ -107,3 +107,37 @@ def test_wave_decoder_restart_odd_lane_after(monkeypatch, lane_after):
     for a, b, p in zip(lane, wave, plain):
         assert a["status"] == "OK" and a["data"] == p
         assert a == b
+
+
+def test_unchecked_runs_meet_stream_ends():
+    """The symbol loop's 4-step runs without bit and room checks hand over
+    to the checked loop once some lane of the wave is within 64 + 3 x 48 bits of its input's end or
+    4 x 258 bytes of its output slot's end.  One wave of lanes whose ends fall at every distance
+    from those bounds -- output slots from exact to 2,100 bytes short, inputs cut 0 to 40 bytes
+    early -- beside lanes far from theirs: records and bytes against the oracle's Inflater (cut
+    inputs) and the slot-edge rule (short slots)."""
+    text = golden("paradiselost.txt")
+    rng = random.Random(5)
+    plain = [text[o:o + 30000] for o in (rng.randrange(len(text) - 30000) for _ in range(8))]
+    comp = [zlib.compress(p, 6) for p in plain]
+    streams, caps, kinds = [], [], []
+    for i in range(64):                                   # short output slots
+        p, c = plain[i % 8], comp[i % 8]
+        k = (i * 33) % 2101
+        streams.append(c); caps.append(len(p) - k); kinds.append(("slot", i % 8, k))
+    for i in range(41):                                   # cut inputs
+        c = comp[i % 8]
+        streams.append(c[:len(c) - i]); caps.append(len(plain[i % 8]) + 64); kinds.append(("cut", i % 8, i))
+    for i in range(23):                                   # lanes far from their ends
+        streams.append(comp[i % 8]); caps.append(len(plain[i % 8]) + 64); kinds.append(("whole", i % 8, 0))
+    gpu = sdz.inflate_batch(streams, caps, sdz.FMT_CONTAINER)
+    for g, s, cap, (kind, j, k) in zip(gpu, streams, caps, kinds):
+        p = plain[j]
+        if kind == "slot" and k:
+            assert g["status"] == "OUT_OVERFLOW" and not g["success"], (k, g["status"])
+            n = g["out_len"]
+            assert cap - 258 < n <= cap and g["data"][:n] == p[:n]
+        elif kind == "cut" and k:
+            assert_same(g, O.inflater_run([s]), s)
+        else:
+            assert g["success"] and g["data"] == p
