@@ -322,6 +322,9 @@ __device__ __forceinline__ void lds_mskor_at(uint32_t* base32, uint32_t i, uint3
 #ifndef RS_READ_ALL
 #define RS_READ_ALL 1
 #endif
+#ifndef RS_MAP2
+#define RS_MAP2 1                     // finality-map check: two map dwords per loop pass
+#endif
 // GEN: 0 -- no lane needs the general path (the caller routed them elsewhere); 1 -- through the
 // out-of-line emit_tokens; 2 -- emit_tokens inlined (one call site per kernel: no callee-saved
 // registers forced around a call)
@@ -423,6 +426,20 @@ __device__ __forceinline__ bool map_all(const uint8_t* fmap, bool act, uint32_t 
     // mask it out (the compiler had turned the selects around the read into an exec-mask branch)
     const uint32_t lm = ~0u << (8 * (lo & 3u));          // the first dword's bytes
     const uint32_t hm = bt == 4u ? ~0u : (1u << (8 * bt)) - 1u;   // the last dword's
+#if RS_MAP2
+    // two dwords per pass (the loop's test, ballot and counters once per pair)
+    for (uint32_t i = 0; __ballot(i < nw); i += 2) {
+        const uint32_t m = m0 + i, m1 = m + 1u;
+        const uint32_t in = (uint32_t)((int32_t)(i - nw) >> 31);        // i < nw
+        const uint32_t in1 = (uint32_t)((int32_t)(i + 1u - nw) >> 31);  // i + 1 < nw
+        const uint32_t in2 = (uint32_t)((int32_t)(i + 2u - nw) >> 31);  // i + 2 < nw
+        const uint32_t mask = in & (in1 | hm) & (i == 0 ? lm : ~0u);
+        const uint32_t mask1 = in1 & (in2 | hm);
+        uint32_t v = fmap32[m & (RS_BM / 4 - 1) & in], v1 = fmap32[m1 & (RS_BM / 4 - 1) & in1];
+        asm volatile("" : "+v"(v), "+v"(v1));
+        miss |= ((v ^ (lap_of(4 * m) * 0x01010101u)) & mask) | ((v1 ^ (lap_of(4 * m1) * 0x01010101u)) & mask1);
+    }
+#else
     for (uint32_t i = 0; __ballot(i < nw); ++i) {
         const uint32_t m = m0 + i;
         const uint32_t in = (uint32_t)((int32_t)(i - nw) >> 31);        // i < nw
@@ -432,6 +449,7 @@ __device__ __forceinline__ bool map_all(const uint8_t* fmap, bool act, uint32_t 
         asm volatile("" : "+v"(v));
         miss |= (v ^ (lap_of(4 * m) * 0x01010101u)) & mask;
     }
+#endif
 #else
     for (uint32_t i = 0; __ballot(i < nw); ++i) {
         const uint32_t m = m0 + i;
