@@ -2,7 +2,7 @@
 # One GPU call as a list of named steps (run through gpurun), e.g.
 #   gpurun -- 'bash tools/gpu_steps.sh OUT=r06a "t:tests/test_gpu_lane.py" c2 "c2:SDZ_RESOLVE=0" dist'
 # Steps (each under its own time limit; the first failure ends the call):
-#   t:<pytest args>     pytest -m gpu on the given files / -k expression
+#   t:[ENV=V,...|]<pytest args>  pytest -m gpu on the given files / -k expression (with that environment)
 #   suite               the whole -m gpu suite
 #   c2[:ENV=V,...]      tools/run_c2.py --mode inflate (C2), with the given environment
 #   dist[:ENV=V,...]    tools/run_c2.py --mode distinct (64 Ki distinct 64 KiB streams)
@@ -41,7 +41,8 @@ for st in "$@"; do
   log=$O/$(printf %02d $n)_$name.log
   echo "== step $n: $st" | tee -a $O/steps.txt
   case $name in
-    t) timeout -k 10 900 python3 -u -m pytest -m gpu -x -v --timeout 240 --timeout-method thread $arg > $log 2>&1 ;;
+    t) e=""; a=$arg; [[ "$arg" == *"|"* ]] && { e=${arg%%|*}; a=${arg#*|}; }
+       envrun "$e" timeout -k 10 900 python3 -u -m pytest -m gpu -x -v --timeout 240 --timeout-method thread $a > $log 2>&1 ;;
     suite) timeout -k 10 1000 python3 -u -m pytest tests -m gpu -x -q --timeout 240 --timeout-method thread > $log 2>&1 ;;
     c2) envrun "$arg" timeout -k 10 300 python3 tools/run_c2.py --mode inflate --steps 3 > $log 2>&1 ;;
     dist) envrun "$arg" timeout -k 10 300 python3 tools/run_c2.py --mode distinct --steps 3 > $log 2>&1 ;;
