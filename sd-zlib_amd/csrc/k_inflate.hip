@@ -1522,24 +1522,30 @@ __device__ IL_HOT_ATTR void hot_epoch(DSave* S, const uint8_t* inp, uint64_t ile
     // and 258 bytes each (a step then only tests that its lane is still in the block); once some lane
     // has not, the rest of the epoch runs checked steps.  (One loop with both bodies merged their
     // values at its back edge: ~20 register copies per 4 steps.)
+    // the exit test's count against a scalar (`stop` arrives in a VGPR: the loop's exit was a
+    // divergent-looking test with exec-mask bookkeeping), and the readiness it computes is the next
+    // run's (the ring step changes none of its inputs; the token-room check moves before it)
+    const int stop_s = __builtin_amdgcn_readfirstlane(stop);
     bool more = true;
+    if (H.ntok + 3u + 8u > H.tcap) H.full = true;         // token room, once per 4 steps: <= 2 tokens per step
+    bool rdy = hot_ready<STREAM>(H);
     for (;;) {
         IL_RING_STEP(H);
-        if (H.ntok + 3u + 8u > H.tcap) H.full = true;     // token room, once per 4 steps: <= 2 tokens per step
-        const bool rdy = hot_ready<STREAM>(H);
         if (__ballot(rdy && !(IL_HOT_AVAIL(H) >= 64 + 3 * 48 && H.room >= 4u * 258u))) break;
 #pragma unroll
         for (int rep = 0; rep < 4; ++rep)
             if (rdy && H.mode == LM_CODES) IL_FAST_STEP<false>(H, LL, DD, region);
-        if (__popcll(__ballot(hot_ready<STREAM>(H))) <= stop) { more = false; break; }
+        if (H.ntok + 3u + 8u > H.tcap) H.full = true;
+        rdy = hot_ready<STREAM>(H);
+        if ((int)__popcll(__ballot(rdy)) <= stop_s) { more = false; break; }
     }
     while (more) {
 #pragma unroll IL_REP_UNROLL
         for (int rep = 0; rep < 4; ++rep)
             if (hot_ready<STREAM>(H)) IL_FAST_STEP(H, LL, DD, region);
-        if (__popcll(__ballot(hot_ready<STREAM>(H))) <= stop) break;
-        IL_RING_STEP(H);
         if (H.ntok + 3u + 8u > H.tcap) H.full = true;
+        if ((int)__popcll(__ballot(hot_ready<STREAM>(H))) <= stop_s) break;
+        IL_RING_STEP(H);
     }
 #else
     do {
