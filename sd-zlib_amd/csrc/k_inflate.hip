@@ -64,6 +64,9 @@ __device__ __forceinline__ uint8_t* lane_region() { return g_region + lane_slot(
 #ifndef IL_REFILL2
 #define IL_REFILL2 1                  // symbol loop: one refill of up to 2 dwords per step (br_refill2)
 #endif
+#ifndef IL_RING32
+#define IL_RING32 1                   // ... its ring step loads 32 B at a time (ring_step2)
+#endif
 #if IL_REFILL2
 #define IL_RING_DW 32                 // input ring dwords per lane (128 B + 8 B pad)
 #else
@@ -357,6 +360,31 @@ __device__ __forceinline__ void br_refill2(Hot& L) {
     L.nx2 = q[1];
 }
 __device__ __forceinline__ void ring_step2(Hot& L) {
+#if IL_RING32
+    // loads of 32 B only, at lvl <= 80 (committed one ring step later: lvl stays >= 32 and below
+    // 112 + 16); wpos stays a multiple of 32, so only a load's first 16 B can land on dword 0.  The
+    // second chunk may lie past the input's last 16-B chunk: inside the 64 readable bytes the C-ABI
+    // asks for after a stream (include/sdz.h), and never consumed (the bit count ends before it)
+    if (L.ns) {
+        const uint32_t k = (L.wpos >> 2) & (IL_RING_DW - 1);
+        *(uint2*)(L.ring + k) = make_uint2(L.s0.x, L.s0.y);
+        *(uint2*)(L.ring + k + 2) = make_uint2(L.s0.z, L.s0.w);
+        *(uint2*)(L.ring + k + 4) = make_uint2(L.s1.x, L.s1.y);
+        *(uint2*)(L.ring + k + 6) = make_uint2(L.s1.z, L.s1.w);
+        L.ring[k == 0 ? IL_RING_DW : IL_RING_DW + 1] = L.s0.x;   // mirror of dword 0 (else the pad)
+        L.wpos += 32;
+        L.ns = 0;
+    }
+    tok_flush_hot(L);
+    if (L.wpos - L.rpos <= 80 && L.vp < L.vend) {
+        if (!HOT_CHECK(L, (const uint8_t*)L.vp >= L.chk_lo && (const uint8_t*)(L.vp + 2) <= L.chk_hi, 1,
+                       (uintptr_t)L.vp, (uintptr_t)L.vend)) return;
+        L.s0 = L.vp[0];
+        L.s1 = L.vp[1];
+        L.vp += 2;
+        L.ns = 2;
+    }
+#else
     if (L.ns) {
         uint32_t k = (L.wpos >> 2) & (IL_RING_DW - 1);
         *(uint2*)(L.ring + k) = make_uint2(L.s0.x, L.s0.y);
@@ -381,6 +409,7 @@ __device__ __forceinline__ void ring_step2(Hot& L) {
         L.ns = 1;
         if (lvl <= 64 && L.vp < L.vend) { L.s1 = *L.vp++; L.ns = 2; }
     }
+#endif
 }
 #endif
 
