@@ -152,13 +152,20 @@ def inflate_distinct(sdz, L, bd, drec, text, offs, slice_len, steps, barrier, al
     kernel_ms = sum(kms) / len(kms)
     bin_, bout = sum(in_len), n * slice_len
     achieved = (bin_ + bout) / (kernel_ms / 1000.0) / 1e9
+    dtraffic = None                                       # rocprofv3 PMC pass of this leg (tools/run_c2.py --mode distinct)
+    dps = sorted(glob.glob(os.path.join(ROOT, "profiles", "r[0-9][0-9]_distinct_pmc.json")))
+    if dps and n == 65536 and slice_len == 65536:
+        try:
+            dtraffic = json.load(open(dps[-1])).get("hbm_bytes_per_launch")
+        except Exception:
+            dtraffic = None
     return {
         "value": round(world * bout / wall / 1e6, 2), "unit": "MB/s", "ms_per_step": round(1000 * wall, 3),
         "config": {"workload": "64 Ki distinct 64 KiB dynamic-Huffman zlib streams (the deflate leg's "
                                "outputs; north-star target)", "streams_per_gpu": n,
                    "bytes_in_per_gpu": bin_, "bytes_out_per_gpu": bout},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBS, 5), "kernel_ms": round(kernel_ms, 3),
+                     "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": dtraffic, "kernel_ms": round(kernel_ms, 3),
                      "kernels_ms": {"k_inflate_decode": round(sum(x[0] for x in split) / len(split), 3),
                                     "k_inflate_resolve": round(sum(x[1] for x in split) / len(split), 3),
                                     "k_inflate_finalize": round(sum(x[2] for x in split) / len(split), 3)}},
