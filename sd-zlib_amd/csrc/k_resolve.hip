@@ -45,7 +45,7 @@ namespace sdz {
 #define RS_WPE RS_WAVES               // waves per SIMD the register budget is sized for
 #endif
 #ifndef RS_NAP
-#define RS_NAP 8                      // s_sleep units (64 clocks) between polls
+#define RS_NAP 12                     // s_sleep units (64 clocks) between polls (8: C2 resolve +0.5 ms, distinct +0.2 ms)
 #endif
 #ifndef RS_BM
 #define RS_BM 4096                    // finality map bytes (a power of 2 >= RS_SLACK; lap = position / RS_BM)
